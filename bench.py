@@ -1,0 +1,211 @@
+#!/usr/bin/env python3
+"""bench.py — M points/s through the PointNet++ SetAbstraction stack on 65 536-point frames.
+
+BASELINE.json metric: "M points/sec through SetAbstraction, 65k-pt frames; 1->8 GPU
+scaling".  Workload (configs[2] / configs[3]): the 3-level SSG encoder
+(SA1 N/16 r=0.2 ns=32 [64,64,128]; SA2 N/64 r=0.4 ns=64 [128,128,256]; group_all
+[256,512,1024]) in fp32 on 65 536-point frames; per GPU a batch of 32 frames — the
+per-GPU share of configs[3] (256 frames over 8 GPUs) — so N GPUs process 32*N frames
+per step (weak scaling, per-frame data parallel, no collective on the data path).
+
+A step = FPS + ball query + fused group/MLP/max-pool for SA1 and SA2, then group_all
+(three MFMA dense layers with a fused max-pool) over the batch, inputs resident in HBM.
+Synthetic data: uniform [-1, 1]^3 float32 frames (seeded per rank), random-init weights.
+
+Run:  python bench.py [--gpus N --steps K --warmup W]  (N>1 via torch.distributed.run)
+"""
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+# per-frame algorithmic work of each kernel of the SSG stack at N points
+FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: fp32 matrix (= vector) peak
+HBM_PEAK_GBS = 8000.0
+
+
+def mlp_flops(rows, widths_in):
+    return 2 * rows * sum(a * b for a, b in zip(widths_in[:-1], widths_in[1:]))
+
+
+def ssg_kernel_work(n):
+    m1, m2 = n // 16, n // 64
+    return {
+        "sa1_group_mlp": ("mfma", mlp_flops(m1 * 32, [3, 64, 64, 128])),
+        "sa2_group_mlp": ("mfma", mlp_flops(m2 * 64, [131, 128, 128, 256])),
+        "sa3_dense1": ("mfma", mlp_flops(m2, [259, 256])),
+        "sa3_dense2": ("mfma", mlp_flops(m2, [256, 512])),
+        "sa3_dense3_pool": ("mfma", mlp_flops(m2, [512, 1024])),
+        # compulsory bytes: read xyz, write idx + new_xyz
+        "sa1_fps": ("hbm", 12 * n + 16 * m1),
+        "sa2_fps": ("hbm", 12 * m1 + 16 * m2),
+        "sa1_ball_query": ("hbm", 12 * (n + m1) + 4 * m1 * 32),
+        "sa2_ball_query": ("hbm", 12 * (m1 + m2) + 4 * m2 * 64),
+    }
+
+
+def cpu_baseline(n, budget_s=20.0):
+    """The oracle SA stack (C FPS / ball query + numpy MLP, BLAS pinned to 1 thread) on
+    one frame of the same workload, on this host.  kind = "port" (the reference has no
+    SetAbstraction code to time)."""
+    from threadpoolctl import threadpool_limits
+    from oracle import tier_n
+    from lidar_ai_recommendation_software_amd import pointnet2 as pn
+    from lidar_ai_recommendation_software_amd.synthetic import unit_frames
+    cfg = pn.SSG
+    w = pn.init_weights(cfg, 0)
+    frames, t0 = 0, time.perf_counter()
+    with threadpool_limits(limits=1):
+        while True:
+            x = unit_frames(1, n, 1000 + frames)[0]
+            tier_n.sa_stack(x, {"levels": pn.resolve(cfg, n)}, w)
+            frames += 1
+            if time.perf_counter() - t0 > budget_s or frames >= 8:
+                break
+    dt = time.perf_counter() - t0
+    cpu = platform.processor() or platform.machine()
+    try:
+        with open("/proc/cpuinfo") as f:
+            cpu = next(l.split(":", 1)[1].strip() for l in f if l.startswith("model name"))
+    except Exception:
+        pass
+    return {"value": frames * n / dt / 1e6, "unit": "M points/s", "cores": 1, "kind": "port",
+            "sample": f"{frames} x {n}-point SSG frame(s) through oracle/tier_n.sa_stack "
+                      f"(C FPS + C ball query + numpy fp32 MLP, 1 thread) in {dt:.1f} s on {cpu}; "
+                      f"host has {os.cpu_count()} logical CPUs"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=32, help="frames per GPU per step")
+    ap.add_argument("--points", type=int, default=65536)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=20.0)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    from lidar_ai_recommendation_software_amd import pointnet2 as pn
+    from lidar_ai_recommendation_software_amd.synthetic import unit_frames
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    B, N = args.batch, args.points
+    bb = pn.PointNet2Backbone(pn.SSG, device=dev, seed=0)
+    x = torch.from_numpy(unit_frames(B, N, seed=rank)).to(dev)
+
+    # instrument every launch of a step with events on the launch stream
+    stream = torch.cuda.current_stream(dev)
+    timers = {}
+
+    def timed(name, fn, *a, **k):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        out = fn(*a, **k)
+        e1.record(stream)
+        timers.setdefault(name, []).append((e0, e1))
+        return out
+
+    def step(instrument):
+        t = timed if instrument else (lambda name, fn, *a, **k: fn(*a, **k))
+        lv = bb.levels
+        xyz, feats = x, None
+        for li, lvl in enumerate(lv[:2]):
+            M = N // lvl["div"]
+            idx, nxyz = t(f"sa{li+1}_fps", pn.farthest_point_sample, xyz, M, return_xyz=True)
+            br = lvl["branches"][0]
+            stride = lv[li + 1]["k"] if lv[li + 1].get("group_all") else br["widths"][-1]
+            out = torch.empty((B, M, stride), dtype=torch.float32, device=dev)
+            gidx = t(f"sa{li+1}_ball_query", pn.ball_query, br["r"], br["ns"], xyz, nxyz)
+            t(f"sa{li+1}_group_mlp", pn.group_mlp, xyz, feats, nxyz, gidx, br["packed"], br["widths"],
+              out=out, out_offset=0)
+            xyz, feats = nxyz, out
+        g = lv[2]
+        M = xyz.shape[1]
+        pn.nat.call("lidar_concat_xyz_pad_f32", pn.nat.handle(dev.index), pn.nat.ptr(xyz), B * M,
+                    pn.nat.ptr(feats), g["k"], g["cfeat"], pn.nat.stream_ptr())
+        h1 = t("sa3_dense1", pn.dense_relu, feats.view(B * M, g["k"]), g["w"][0], g["b"][0])
+        h2 = t("sa3_dense2", pn.dense_relu, h1, g["w"][1], g["b"][1])
+        return t("sa3_dense3_pool", pn.dense_relu, h2, g["w"][2], g["b"][2], pool_rows=M)
+
+    # correctness of the instrumented step == the library forward
+    for _ in range(args.warmup):
+        step(False)
+    ref, _ = bb.forward(x)
+    got = step(False)
+    torch.cuda.synchronize(dev)
+    assert torch.equal(ref, got), "bench step diverged from PointNet2Backbone.forward"
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    kern = {k: float(np.mean([a.elapsed_time(b) for a, b in v])) for k, v in timers.items()}
+    work = ssg_kernel_work(N)
+    dom = max(kern, key=lambda k: kern[k])
+    bound, per_frame = work[dom]
+    per_launch = per_frame * B
+    avg_s = kern[dom] / 1e3
+    if bound == "mfma":
+        achieved, peak, unit = per_launch / avg_s / 1e12, FP32_MFMA_PEAK_TFLOPS, "TFLOP/s"
+    else:
+        achieved, peak, unit = per_launch / avg_s / 1e9, HBM_PEAK_GBS, "GB/s"
+
+    value = world * B * N * args.steps / elapsed / 1e6
+    if rank == 0:
+        rec = {
+            "metric": "M points/sec through SetAbstraction, 65k-pt frames; 1->8 GPU scaling",
+            "value": value, "unit": "M points/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic: uniform [-1,1]^3 float32 frames (seeded per rank), random-init SSG weights",
+            "config": {"workload": "PointNet++ SSG encoder (SA1 N/16 r0.2 ns32 [64,64,128]; "
+                                   "SA2 N/64 r0.4 ns64 [128,128,256]; group_all [256,512,1024]) fp32",
+                       "points_per_frame": N, "frames_per_gpu": B, "global_batch_frames": B * world,
+                       "parallelism": f"per-frame data parallel x{world} (no collectives)"},
+            "roofline": {"kernel": dom, "bound": bound, "achieved": achieved, "peak": peak,
+                         "unit": unit, "frac": achieved / peak, "traffic": None,
+                         "work_per_launch": per_launch,
+                         "avg_launch_ms": kern[dom]},
+            "kernel_ms": kern,
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            rec["cpu_baseline"] = cpu_baseline(N, args.cpu_budget)
+            rec["speedup_vs_cpu"] = value / rec["cpu_baseline"]["value"]
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

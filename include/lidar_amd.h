@@ -1,0 +1,153 @@
+/*
+ * lidar_amd.h — C-ABI of the MI355X (gfx950) LiDAR hot-path library, liblidar_amd.so.
+ *
+ * This is the drop-in boundary.  The reference (FortuneMU2025/LIDAR_AI_Recommendation_Software)
+ * is pure Python; its hot path is the operator set in utils/data_processing.py and
+ * models/crowd_density_model.py.  Each entry point below names the reference
+ * interface it replaces (file:line in /root/reference).  The Python host layer
+ * (lidar_ai_recommendation_software_amd/) binds these with ctypes, mirroring the
+ * reference's Python signatures; INTEGRATION.md shows the binding.
+ *
+ * Conventions
+ *  - Plain pointers and sizes only.  Every array pointer is a DEVICE pointer
+ *    (hipMalloc / torch CUDA tensor storage) unless the name ends in `_host`.
+ *  - The caller owns every input/output buffer.  The library owns only the scratch
+ *    workspace inside a handle (grown on demand; lidar_reserve() pre-sizes it so a
+ *    later call can be captured into a hipGraph).
+ *  - Calls are asynchronous on `stream` (a hipStream_t; NULL = legacy default stream).
+ *  - Return 0 on success, a negative LIDAR_E* code on failure; nothing throws across
+ *    the ABI.  lidar_last_error() returns a thread-local message for the last failure.
+ *  - A handle is bound to one device.  Use one handle per (thread, stream): calls on
+ *    one handle must not run concurrently (the scratch workspace is shared).
+ *  - Frames are batched: `batch` frames of `n` points, (batch, n, 3) row-major, unless a
+ *    CSR `offsets` array is given (Tier R, ragged frames).
+ */
+#ifndef LIDAR_AMD_H
+#define LIDAR_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LIDAR_OK 0
+#define LIDAR_EINVAL -1   /* bad argument (shape, size, null pointer) */
+#define LIDAR_EHIP -2     /* a HIP runtime call failed */
+#define LIDAR_ENOMEM -3   /* workspace allocation failed */
+#define LIDAR_EDEVICE -4  /* device is not gfx950 */
+
+typedef struct lidar_handle lidar_handle;
+
+/* ------------------------------------------------------------------ handle */
+int lidar_create(int device, lidar_handle **out);
+int lidar_destroy(lidar_handle *h);
+/* grow the scratch workspace to at least `bytes` now (not inside graph capture) */
+int lidar_reserve(lidar_handle *h, uint64_t bytes);
+const char *lidar_last_error(void);
+int lidar_version(void);
+
+/* ============================================================ Tier N (SA stack)
+ * North_star operators.  The reference has no PointNet++ code; these
+ * are exposed beside utils/data_processing.py:231 (downsample_point_cloud) and drive
+ * CrowdDensityModel's optional PointNet++ backbone (models/crowd_density_model.py:14).
+ */
+
+/* farthest-point sampling: idx (batch, npoint) int32; optionally new_xyz (batch, npoint, 3)
+ * = xyz[idx] (pass NULL to skip).  Start index 0, fp32 no-FMA distances, lowest index on
+ * ties.  Replaces: downsample_point_cloud's random subset (utils/data_processing.py:231-249)
+ * where a spatially uniform subset is wanted. */
+int lidar_fps_f32(lidar_handle *h, const float *xyz, int64_t batch, int64_t n, int64_t npoint,
+                  int32_t *idx, float *new_xyz, void *stream);
+
+/* ball query: idx (batch, m, nsample) int32 — the first `nsample` point indices (ascending)
+ * with d < radius^2, padded with the first hit, 0 when there is none.  Replaces the eps-ball
+ * query the reference runs through sklearn (utils/data_processing.py:197,
+ * models/crowd_flow_model.py:216,228 query_radius) with a bounded-nsample form. */
+int lidar_ball_query_f32(lidar_handle *h, const float *xyz, const float *centres, int64_t batch,
+                         int64_t n, int64_t m, float radius, int32_t nsample, int32_t *idx,
+                         void *stream);
+
+/* grouped shared MLP (3 layers, BN folded, ReLU) + max-pool over nsample for one SA
+ * branch, fused with the grouping gather:
+ *   row (b, c, s) = [xyz[b, idx[b,c,s]] - centres[b,c], feats[b, idx[b,c,s], 0:cfeat]]
+ *   out[b, c, out_offset + j] = max_s relu(...relu(row W1 + b1)... W3 + b3)[j]
+ * `packed` is the weight image from lidar_mlp_pack_f32 (device copy).  widths: c1, c2, c3
+ * multiples of 32; cfeat 0 or a multiple of 8; nsample 16, 32, 64 or 128.
+ * out row stride is `out_stride` floats.  feats row stride is `feat_stride` floats. */
+int lidar_sa_group_mlp_f32(lidar_handle *h, const float *xyz, const float *feats,
+                           int64_t feat_stride, const float *centres, const int32_t *idx,
+                           int64_t batch, int64_t n, int64_t m, int32_t nsample, int32_t cfeat,
+                           int32_t c1, int32_t c2, int32_t c3, const float *packed,
+                           float *out, int64_t out_stride, int64_t out_offset, void *stream);
+
+/* size (floats) and host-side construction of the packed weight image for
+ * lidar_sa_group_mlp_f32.  W_l are (cin_l, cout_l) row-major host arrays, canonical
+ * PointNet++ channel order [dx, dy, dz, feat...] for layer 1. */
+int64_t lidar_mlp_packed_size(int32_t cfeat, int32_t c1, int32_t c2, int32_t c3);
+int lidar_mlp_pack_f32(int32_t cfeat, int32_t c1, int32_t c2, int32_t c3, const float *w1_host,
+                       const float *b1_host, const float *w2_host, const float *b2_host,
+                       const float *w3_host, const float *b3_host, float *packed_host);
+
+/* dense layer on MFMA: y (rows, cout) = relu(x (rows, k) W (k, cout) + b), fp32.
+ * If pool_rows > 0: y is (rows / pool_rows, cout) = max over each run of pool_rows rows
+ * (group_all's max-pool, fused); y must then be zeroed by the caller first.
+ * k a multiple of 16, cout a multiple of 128, rows a multiple of 128
+ * (pool_rows a multiple of 128 when used). */
+int lidar_dense_relu_f32(lidar_handle *h, const float *x, int64_t rows, int32_t k,
+                         const float *w, const float *bias, int32_t cout, int32_t pool_rows,
+                         float *y, void *stream);
+
+/* y (batch*m, ldy) columns [col0, col0+3) = xyz rows; columns [col0+3, ldy) zeroed —
+ * builds group_all's input [feats, xyz, 0-pad] next to features already in y. */
+int lidar_concat_xyz_pad_f32(lidar_handle *h, const float *xyz, int64_t rows, float *y,
+                             int64_t ldy, int64_t col0, void *stream);
+
+/* voxel downsample: per-point voxel id (rank of its voxel key, ascending), centroids
+ * (sequential fp32 sums in point order / count), counts; *nvox_host receives V
+ * (synchronises `stream`).  centroids/counts must hold n entries. */
+int lidar_voxel_downsample_f32(lidar_handle *h, const float *xyz, int64_t n, float voxel,
+                               int32_t *voxel_id, float *centroids, int32_t *counts,
+                               int64_t *nvox_host, void *stream);
+
+/* ======================================================= Tier R (density path)
+ * Bit-exact replacements for the reference's CPU path. */
+
+/* eps-ball neighbour count over scaled points (self included, fp64,
+ * ((dx*dx+dy*dy)+dz*dz) <= eps*eps) and DBSCAN labels (min_samples).  Replaces
+ * sklearn DBSCAN(eps, min_samples).fit(x).labels_ at utils/data_processing.py:197. */
+int lidar_dbscan_f64(lidar_handle *h, const double *x, int64_t n, double eps, int32_t min_samples,
+                     int64_t *labels, int32_t *counts, void *stream);
+
+/* Whole preprocess_lidar_data (utils/data_processing.py:127-229) on one frame already in
+ * device memory.  Outputs (device): mask (n) u8 inlier flag, colors (n,3) f64 for all
+ * points, labels (n) int64 (inlier-compacted order, first n_in valid), and `scalars`
+ * (host-visible layout, device memory, 32 doubles):
+ *   [0] n_in  [1] n_ground  [2] n_nonground  [3] z_threshold  [4] eps  [5..10] x/y/z min,max
+ *   [11..14] ground plane a,b,-1,c (or the fallbacks)  [15] status (0 ok, 1 = no inliers)
+ *   [16..18] 3-sigma mean  [19..21] std  [22..24] scaler mean  [25..27] scaler scale
+ * compact_xyz (n,3) f64 receives the inlier points in order. */
+int lidar_preprocess_f64(lidar_handle *h, const double *xyz, int64_t n, uint8_t *mask,
+                         double *colors, double *compact_xyz, int64_t *labels, double *scalars,
+                         void *stream);
+
+/* people positions (extract_people_positions, utils/data_processing.py:251-280):
+ * centroid (x, y) of every label >= 0, sequential index-order sums;
+ * people (n,2) f64, *k_host receives K (synchronises). */
+int lidar_people_f64(lidar_handle *h, const double *xyz, const int64_t *labels, int64_t n,
+                     double *people, int64_t *k_host, void *stream);
+
+/* grid density (calculate_grid_density, utils/data_processing.py:282-328): np.arange
+ * edges a + i*((a+g)-a), histogram2d binning (searchsorted right, last edge closed).
+ * nx = len(x_edges) - 1 etc. are computed on the host by lidar_grid_dims. */
+int lidar_grid_dims(double xmin, double xmax, double ymin, double ymax, double grid,
+                    int64_t *nx, int64_t *ny);
+int lidar_density_grid_f64(lidar_handle *h, const double *people, int64_t k, double xmin,
+                           double xmax, double ymin, double ymax, double grid, int64_t nx,
+                           int64_t ny, double *grid_x, double *grid_y, double *density,
+                           void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,131 @@
+"""ctypes binding of liblidar_amd.so (the C-ABI declared in include/lidar_amd.h).
+
+The shared library is built in-tree (``csrc/Makefile`` -> ``liblidar_amd.so`` next to
+this file) by ``__graft_entry__.build()``.  There is NO fallback: if the library is
+missing or cannot create a handle on the current GPU, every operator raises
+``NativeUnavailable`` — the HIP path is the only compute path.
+
+Handles are per (thread, device): the library's scratch workspace is shared by the
+calls on one handle, so two threads never share one.
+"""
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "liblidar_amd.so")
+
+LIDAR_ERRORS = {-1: "invalid argument", -2: "HIP runtime error", -3: "out of memory",
+                -4: "unsupported device"}
+
+
+class NativeUnavailable(RuntimeError):
+    """liblidar_amd.so is missing, failed to load, or found no gfx950 device."""
+
+
+class LidarError(RuntimeError):
+    """A liblidar_amd call returned a negative status."""
+
+
+_lib = None
+_lib_lock = threading.Lock()
+_tls = threading.local()
+
+P = ctypes.c_void_p
+I64, I32, F32, F64 = ctypes.c_int64, ctypes.c_int32, ctypes.c_float, ctypes.c_double
+
+# name -> argtypes (restype int unless listed in _RESTYPES)
+SIGNATURES = {
+    "lidar_create": [ctypes.c_int, ctypes.POINTER(P)],
+    "lidar_destroy": [P],
+    "lidar_reserve": [P, ctypes.c_uint64],
+    "lidar_last_error": [],
+    "lidar_version": [],
+    "lidar_fps_f32": [P, P, I64, I64, I64, P, P, P],
+    "lidar_ball_query_f32": [P, P, P, I64, I64, I64, F32, I32, P, P],
+    "lidar_sa_group_mlp_f32": [P, P, P, I64, P, P, I64, I64, I64, I32, I32, I32, I32, I32, P, P,
+                               I64, I64, P],
+    "lidar_mlp_packed_size": [I32, I32, I32, I32],
+    "lidar_mlp_pack_f32": [I32, I32, I32, I32, P, P, P, P, P, P, P],
+    "lidar_dense_relu_f32": [P, P, I64, I32, P, P, I32, I32, P, P],
+    "lidar_concat_xyz_pad_f32": [P, P, I64, P, I64, I64, P],
+    "lidar_voxel_downsample_f32": [P, P, I64, F32, P, P, P, P, P],
+    "lidar_dbscan_f64": [P, P, I64, F64, I32, P, P, P],
+    "lidar_preprocess_f64": [P, P, I64, P, P, P, P, P, P],
+    "lidar_people_f64": [P, P, P, I64, P, P, P],
+    "lidar_grid_dims": [F64, F64, F64, F64, F64, P, P],
+    "lidar_density_grid_f64": [P, P, I64, F64, F64, F64, F64, F64, I64, I64, P, P, P, P],
+}
+_RESTYPES = {"lidar_last_error": ctypes.c_char_p, "lidar_mlp_packed_size": I64}
+
+
+def load_library(path=LIB_PATH):
+    """Load and type the library (no GPU needed).  Raises NativeUnavailable."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise NativeUnavailable(
+                f"{path} not built — run __graft_entry__.build() (make -C csrc); "
+                "there is no CPU fallback")
+        try:
+            lib = ctypes.CDLL(path)
+        except OSError as e:  # pragma: no cover - depends on the box
+            raise NativeUnavailable(f"cannot load {path}: {e}") from e
+        for name, argtypes in SIGNATURES.items():
+            fn = getattr(lib, name, None)
+            if fn is None:
+                continue  # reported by missing_symbols(); calling it raises AttributeError
+            fn.argtypes = argtypes
+            fn.restype = _RESTYPES.get(name, ctypes.c_int)
+        _lib = lib
+        return lib
+
+
+def missing_symbols():
+    lib = load_library()
+    return [n for n in SIGNATURES if getattr(lib, n, None) is None]
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = load_library().lidar_last_error().decode(errors="replace")
+        raise LidarError(f"{what} failed ({rc}: {LIDAR_ERRORS.get(rc, '?')}): {msg}")
+
+
+def handle(device=None):
+    """The calling thread's handle for `device` (default: torch's current device)."""
+    import torch
+    if not torch.cuda.is_available():
+        raise NativeUnavailable("no GPU visible: the liblidar_amd HIP path needs a gfx950 device")
+    if device is None:
+        device = torch.cuda.current_device()
+    hs = getattr(_tls, "handles", None)
+    if hs is None:
+        hs = _tls.handles = {}
+    h = hs.get(device)
+    if h is None:
+        lib = load_library()
+        hp = P()
+        check(lib.lidar_create(int(device), ctypes.byref(hp)), "lidar_create")
+        h = hs[device] = hp
+    return h
+
+
+def stream_ptr(stream=None):
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return P(s.cuda_stream)
+
+
+def ptr(t):
+    """Device pointer of a contiguous torch tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return P(t.data_ptr())
+
+
+def call(name, *args):
+    lib = load_library()
+    check(getattr(lib, name)(*args), name)

@@ -1,0 +1,235 @@
+"""PointNet++ SetAbstraction operators and backbones on liblidar_amd (gfx950 HIP).
+
+These are the north_star operators that the reference does not have (SURVEY.md §0,
+§8a N2-N6).  They sit beside the reference's operator set
+(``utils/data_processing.py:231`` ``downsample_point_cloud`` and the density model,
+``models/crowd_density_model.py:14``), and every one runs on the HIP kernels behind
+``include/lidar_amd.h``.  Torch only holds device memory and the stream.
+
+Spec (frozen in DESIGN.md §3, restated by ``oracle/tier_n.py``): fp32 coordinates,
+distances ``(dx*dx + dy*dy) + dz*dz`` with one rounding per operation;
+FPS starts at index 0 and breaks ties to the lowest index; ball query keeps the first
+``nsample`` hits in index order; grouping is ``[xyz - centre, features]`` (use_xyz);
+each SA branch is a 3-layer shared MLP (conv1x1 + folded BN + ReLU) max-pooled over
+its neighbourhood; the last level is group_all.
+
+Layouts: xyz (B, N, 3) float32; features channels-last (B, N, C) float32.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _native as nat
+
+# ------------------------------------------------------------------ configs
+# BASELINE.json configs: C2 = one SA1 layer, C3 = 3-level SSG, C5 = 3-level MSG.
+SSG = {
+    "name": "ssg",
+    "levels": [
+        {"npoint_div": 16, "radii": [0.2], "nsamples": [32], "mlps": [[64, 64, 128]]},
+        {"npoint_div": 64, "radii": [0.4], "nsamples": [64], "mlps": [[128, 128, 256]]},
+        {"group_all": True, "mlps": [[256, 512, 1024]]},
+    ],
+}
+MSG = {
+    "name": "msg",
+    "levels": [
+        {"npoint_div": 16, "radii": [0.1, 0.2, 0.4], "nsamples": [16, 32, 128],
+         "mlps": [[32, 32, 64], [64, 64, 128], [64, 96, 128]]},
+        {"npoint_div": 64, "radii": [0.2, 0.4, 0.8], "nsamples": [32, 64, 128],
+         "mlps": [[64, 64, 128], [128, 128, 256], [128, 128, 256]]},
+        {"group_all": True, "mlps": [[256, 512, 1024]]},
+    ],
+}
+SA1_ONLY = {  # C2: 16 384 points -> 1 024 centroids, r = 0.2, nsample 32
+    "name": "sa1",
+    "levels": [{"npoint_div": 16, "radii": [0.2], "nsamples": [32], "mlps": [[64, 64, 128]]}],
+}
+CONFIGS = {"ssg": SSG, "msg": MSG, "sa1": SA1_ONLY}
+
+
+def resolve(cfg, n):
+    """Per-level dicts with concrete npoint for an n-point frame (oracle format)."""
+    out = []
+    for lvl in cfg["levels"]:
+        d = dict(lvl)
+        if not lvl.get("group_all"):
+            d["npoint"] = max(1, n // lvl["npoint_div"])
+        out.append(d)
+    return out
+
+
+def init_weights(cfg, seed=0):
+    """Deterministic random init (conv1x1 default: U(-1/sqrt(cin), 1/sqrt(cin)), BN folded
+    at its fresh-init identity).  Returns [level][branch][layer] = (W (cin, cout), b)."""
+    rng = np.random.default_rng(seed)
+    weights, cin_feat = [], 0
+    for lvl in cfg["levels"]:
+        branches, cout_total = [], 0
+        for widths in lvl["mlps"]:
+            layers, cin = [], 3 + cin_feat
+            for cout in widths:
+                bound = 1.0 / np.sqrt(cin)
+                W = rng.uniform(-bound, bound, (cin, cout)).astype(np.float32)
+                b = rng.uniform(-bound, bound, cout).astype(np.float32)
+                layers.append((W, b))
+                cin = cout
+            branches.append(layers)
+            cout_total += widths[-1]
+        weights.append(branches)
+        cin_feat = cout_total
+    return weights
+
+
+# --------------------------------------------------------------- functional ops
+def _dev_check(*ts):
+    for t in ts:
+        if t is not None and (not t.is_cuda or not t.is_contiguous()):
+            raise ValueError("liblidar_amd operators take contiguous CUDA tensors")
+
+
+def farthest_point_sample(xyz, npoint, return_xyz=False):
+    """xyz (B, N, 3) float32 CUDA -> idx (B, npoint) int32 [, new_xyz (B, npoint, 3)]."""
+    _dev_check(xyz)
+    if xyz.dtype != torch.float32 or xyz.dim() != 3 or xyz.shape[2] != 3:
+        raise ValueError("xyz must be (B, N, 3) float32")
+    B, N, _ = xyz.shape
+    idx = torch.empty((B, npoint), dtype=torch.int32, device=xyz.device)
+    new_xyz = torch.empty((B, npoint, 3), dtype=torch.float32, device=xyz.device) if return_xyz else None
+    nat.call("lidar_fps_f32", nat.handle(xyz.device.index), nat.ptr(xyz), B, N, npoint,
+             nat.ptr(idx), nat.ptr(new_xyz), nat.stream_ptr())
+    return (idx, new_xyz) if return_xyz else idx
+
+
+def ball_query(radius, nsample, xyz, new_xyz):
+    """-> idx (B, M, nsample) int32 (pointnet2 argument order)."""
+    _dev_check(xyz, new_xyz)
+    B, N, _ = xyz.shape
+    M = new_xyz.shape[1]
+    idx = torch.empty((B, M, nsample), dtype=torch.int32, device=xyz.device)
+    nat.call("lidar_ball_query_f32", nat.handle(xyz.device.index), nat.ptr(xyz), nat.ptr(new_xyz),
+             B, N, M, float(radius), int(nsample), nat.ptr(idx), nat.stream_ptr())
+    return idx
+
+
+def pack_branch(layers, cfeat):
+    """Host-side packed weight image for lidar_sa_group_mlp_f32 (3-layer branch)."""
+    (w1, b1), (w2, b2), (w3, b3) = layers
+    c1, c2, c3 = w1.shape[1], w2.shape[1], w3.shape[1]
+    lib = nat.load_library()
+    size = lib.lidar_mlp_packed_size(cfeat, c1, c2, c3)
+    out = np.zeros(size, dtype=np.float32)
+    arrs = [np.ascontiguousarray(a, dtype=np.float32) for a in (w1, b1, w2, b2, w3, b3)]
+    nat.check(lib.lidar_mlp_pack_f32(cfeat, c1, c2, c3, *[a.ctypes.data_as(ctypes.c_void_p) for a in arrs],
+                                     out.ctypes.data_as(ctypes.c_void_p)), "lidar_mlp_pack_f32")
+    return out
+
+
+def group_mlp(xyz, feats, new_xyz, idx, packed, widths, out=None, out_offset=0):
+    """Fused grouping + 3-layer MLP + max over nsample -> (B, M, c3) (or into `out`)."""
+    B, N, _ = xyz.shape
+    M, ns = idx.shape[1], idx.shape[2]
+    cfeat = 0 if feats is None else feats.shape[2]
+    c1, c2, c3 = widths
+    if out is None:
+        out = torch.empty((B, M, c3), dtype=torch.float32, device=xyz.device)
+    _dev_check(xyz, feats, new_xyz, idx, packed, out)
+    nat.call("lidar_sa_group_mlp_f32", nat.handle(xyz.device.index), nat.ptr(xyz), nat.ptr(feats),
+             cfeat, nat.ptr(new_xyz), nat.ptr(idx), B, N, M, ns, cfeat, c1, c2, c3,
+             nat.ptr(packed), nat.ptr(out), out.shape[-1], out_offset, nat.stream_ptr())
+    return out
+
+
+def dense_relu(x, w, b, pool_rows=0, out=None):
+    rows, k = x.shape
+    cout = w.shape[1]
+    if out is None:
+        shape = (rows // pool_rows, cout) if pool_rows else (rows, cout)
+        out = (torch.zeros if pool_rows else torch.empty)(shape, dtype=torch.float32, device=x.device)
+    _dev_check(x, w, b, out)
+    nat.call("lidar_dense_relu_f32", nat.handle(x.device.index), nat.ptr(x), rows, k, nat.ptr(w),
+             nat.ptr(b), cout, pool_rows, nat.ptr(out), nat.stream_ptr())
+    return out
+
+
+# ----------------------------------------------------------------------- backbone
+class PointNet2Backbone:
+    """SSG / MSG PointNet++ encoder on liblidar_amd.  ``forward(xyz)`` -> global feature
+    (B, C_last) plus the per-level (new_xyz, features, fps_idx)."""
+
+    def __init__(self, cfg=SSG, weights=None, device="cuda", seed=0):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.weights = weights if weights is not None else init_weights(cfg, seed)
+        self.levels = []
+        cfeat = 0
+        for lvl, wl in zip(cfg["levels"], self.weights):
+            if lvl.get("group_all"):
+                (w1, b1), (w2, b2), (w3, b3) = wl[0]
+                kp = (cfeat + 3 + 15) // 16 * 16
+                # canonical rows [x, y, z, f...] -> physical input [f..., x, y, z, 0-pad]
+                w1p = np.zeros((kp, w1.shape[1]), np.float32)
+                w1p[:cfeat] = w1[3:]
+                w1p[cfeat:cfeat + 3] = w1[:3]
+                t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(self.device)
+                self.levels.append({"group_all": True, "k": kp, "cfeat": cfeat,
+                                    "w": [t(w1p), t(w2), t(w3)], "b": [t(b1), t(b2), t(b3)]})
+                cfeat = w3.shape[1]
+            else:
+                branches = []
+                for (r, ns, widths, layers) in zip(lvl["radii"], lvl["nsamples"], lvl["mlps"], wl):
+                    packed = torch.from_numpy(pack_branch(layers, cfeat)).to(self.device)
+                    branches.append({"r": r, "ns": ns, "widths": widths, "packed": packed})
+                self.levels.append({"div": lvl["npoint_div"], "branches": branches, "cfeat": cfeat})
+                cfeat = sum(w[-1] for w in lvl["mlps"])
+        self.out_channels = cfeat
+
+    def forward(self, xyz, keep_levels=False):
+        B, N, _ = xyz.shape
+        N0 = N  # npoint_div is relative to the input frame (N/16, N/64)
+        feats = None
+        out_levels = []
+        for li, lvl in enumerate(self.levels):
+            if lvl.get("group_all"):
+                return self._group_all(xyz, feats, lvl), out_levels
+            M = max(1, N0 // lvl["div"])
+            idx, new_xyz = farthest_point_sample(xyz, M, return_xyz=True)
+            ctot = sum(br["widths"][-1] for br in lvl["branches"])
+            nxt = self.levels[li + 1] if li + 1 < len(self.levels) else None
+            # the level feeding group_all writes straight into its padded input rows
+            stride = nxt["k"] if nxt is not None and nxt.get("group_all") else ctot
+            out = torch.empty((B, M, stride), dtype=torch.float32, device=xyz.device)
+            off = 0
+            for br in lvl["branches"]:
+                gidx = ball_query(br["r"], br["ns"], xyz, new_xyz)
+                group_mlp(xyz, feats, new_xyz, gidx, br["packed"], br["widths"], out=out, out_offset=off)
+                off += br["widths"][-1]
+            if keep_levels:
+                out_levels.append((new_xyz, out[..., :ctot], idx))
+            xyz, feats = new_xyz, out
+        return feats, out_levels
+
+    def _group_all(self, xyz, feats, lvl):
+        B, M, _ = xyz.shape
+        kp, cfeat = lvl["k"], lvl["cfeat"]
+        x = feats if feats is not None and feats.shape[-1] == kp else None
+        if x is None:  # previous level did not pre-pad (only when group_all is level 0)
+            x = torch.empty((B, M, kp), dtype=torch.float32, device=xyz.device)
+        nat.call("lidar_concat_xyz_pad_f32", nat.handle(xyz.device.index), nat.ptr(xyz), B * M,
+                 nat.ptr(x), kp, cfeat, nat.stream_ptr())
+        rows = B * M
+        x2 = x.view(rows, kp)
+        if M % 128:
+            # the MFMA tiles want 128-row runs: pad each frame with copies of its first row
+            # (the max-pool is invariant to duplicated rows)
+            mp = (M + 127) // 128 * 128
+            sel = torch.cat([torch.arange(M, device=x.device),
+                             torch.zeros(mp - M, dtype=torch.long, device=x.device)])
+            x2 = x.view(B, M, kp)[:, sel].reshape(B * mp, kp).contiguous()
+            M, rows = mp, B * mp
+        h1 = dense_relu(x2, lvl["w"][0], lvl["b"][0])
+        h2 = dense_relu(h1, lvl["w"][1], lvl["b"][1])
+        return dense_relu(h2, lvl["w"][2], lvl["b"][2], pool_rows=M)
+
+    __call__ = forward

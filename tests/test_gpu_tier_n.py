@@ -1,0 +1,122 @@
+"""Tier N parity on the GPU: HIP path (through the C-ABI) vs the CPU oracle.
+
+FPS / ball-query indices must be bit-exact; MLP features within the fp32 tolerance
+RTOL = 1e-4 relative with an absolute floor of 1e-4 x the RMS of the reference
+(the MFMA accumulates in a different order than BLAS; near-zero outputs have no
+meaningful relative error).  Parity unpinned by the reference (it has no PointNet++).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import tier_n
+from lidar_ai_recommendation_software_amd import pointnet2 as pn
+from lidar_ai_recommendation_software_amd.synthetic import unit_frames
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-4
+
+
+def feat_close(got, want, what=""):
+    got = np.asarray(got, dtype=np.float64)
+    want = np.asarray(want, dtype=np.float64)
+    scale = np.sqrt(np.mean(want ** 2)) + 1e-30
+    err = np.abs(got - want)
+    bad = err > RTOL * np.abs(want) + RTOL * scale
+    assert not bad.any(), f"{what}: {bad.sum()} / {bad.size} outside tol, max err {err.max():.3e} (rms {scale:.3e})"
+
+
+def frames_for(kind, b, n, seed):
+    x = unit_frames(b, n, seed)
+    if kind == "clumped":  # most points in a tiny ball, a few far away: skewed buckets
+        x[:, : n - 16] *= np.float32(0.01)
+    elif kind == "dups":  # exact duplicates: distance ties, zero distances
+        x[:, n // 2:] = x[:, : n - n // 2]
+    elif kind == "grid":  # lattice: many exactly equal distances (argmax ties)
+        g = np.stack(np.meshgrid(*[np.arange(16)] * 3, indexing="ij"), -1).reshape(-1, 3)
+        x = np.tile((g[:n] / 8.0 - 1.0).astype(np.float32)[None], (b, 1, 1))
+    return np.ascontiguousarray(x)
+
+
+@pytest.mark.parametrize("kind,b,n,m", [
+    ("uniform", 3, 1000, 100), ("uniform", 2, 4096, 1024), ("uniform", 1, 16384, 1024),
+    ("uniform", 1, 65536, 4096), ("uniform", 1, 131072, 512), ("uniform", 1, 150000, 64),
+    ("clumped", 2, 5000, 300), ("dups", 2, 3000, 2000), ("grid", 1, 4096, 600),
+    ("uniform", 2, 1, 4), ("uniform", 1, 37, 60), ("uniform", 1, 64, 64),
+])
+def test_fps_bit_exact(cuda, kind, b, n, m):
+    x = frames_for(kind, b, n, 11)
+    idx, nx = pn.farthest_point_sample(torch.from_numpy(x).to(cuda), m, return_xyz=True)
+    want = tier_n.fps(x, m)
+    got = idx.cpu().numpy()
+    assert np.array_equal(got, want), f"{(got != want).sum()} indices differ, first {np.argwhere(got != want)[:3]}"
+    assert np.array_equal(nx.cpu().numpy(), np.take_along_axis(x, want[..., None].astype(np.int64), 1))
+
+
+def test_fps_matches_numpy_restatement():
+    # the C oracle against the pure-numpy loop (oracle self-check, no GPU needed)
+    x = frames_for("dups", 1, 2000, 3)[0]
+    assert np.array_equal(tier_n.fps(x, 500), tier_n.fps_numpy(x, 500))
+
+
+@pytest.mark.parametrize("n,m,r,ns", [(16384, 1024, 0.2, 32), (4096, 1024, 0.4, 64), (8192, 512, 0.1, 16),
+                                      (8192, 512, 0.8, 128), (1000, 50, 0.05, 8), (70, 33, 0.3, 200)])
+def test_ball_query_bit_exact(cuda, n, m, r, ns):
+    x = unit_frames(2, n, 5)
+    c = x[:, :m].copy()
+    c[:, :3] += 3.0  # centres with no neighbour at all -> all-zero rows
+    idx = pn.ball_query(r, ns, torch.from_numpy(x).to(cuda), torch.from_numpy(c).to(cuda))
+    want = tier_n.ball_query(x, c, r, ns)
+    got = idx.cpu().numpy()
+    assert np.array_equal(got, want), f"{(got != want).sum()} differ"
+
+
+@pytest.mark.parametrize("cfg_name,level,branch", [("ssg", 0, 0), ("ssg", 1, 0), ("msg", 0, 0), ("msg", 0, 1),
+                                                   ("msg", 0, 2), ("msg", 1, 0), ("msg", 1, 1), ("msg", 1, 2)])
+def test_group_mlp(cuda, cfg_name, level, branch):
+    cfg = pn.CONFIGS[cfg_name]
+    w = pn.init_weights(cfg, seed=3)
+    lvl = cfg["levels"][level]
+    layers = w[level][branch]
+    cfeat = layers[0][0].shape[0] - 3
+    r, ns, widths = lvl["radii"][branch], lvl["nsamples"][branch], lvl["mlps"][branch]
+    B, N, M = 2, 2048, 128
+    rng = np.random.default_rng(7)
+    x = unit_frames(B, N, 9)
+    f = rng.standard_normal((B, N, cfeat)).astype(np.float32) if cfeat else None
+    c = x[:, :M].copy()
+    gi = tier_n.ball_query(x, c, r, ns)
+    packed = torch.from_numpy(pn.pack_branch(layers, cfeat)).to(cuda)
+    T = lambda a: None if a is None else torch.from_numpy(np.ascontiguousarray(a)).to(cuda)
+    got = pn.group_mlp(T(x), T(f), T(c), T(gi), packed, widths).cpu().numpy()
+    for bi in range(B):
+        want = tier_n.mlp_maxpool(tier_n.group(x[bi], None if f is None else f[bi], c[bi], gi[bi]), layers, ns)
+        feat_close(got[bi], want, f"{cfg_name} L{level} br{branch} frame {bi}")
+
+
+def test_dense_relu_and_pool(cuda):
+    rng = np.random.default_rng(1)
+    x = rng.standard_normal((512, 272)).astype(np.float32)
+    w = (rng.standard_normal((272, 256)) / 16).astype(np.float32)
+    b = rng.standard_normal(256).astype(np.float32)
+    T = lambda a: torch.from_numpy(a).to(cuda)
+    got = pn.dense_relu(T(x), T(w), T(b)).cpu().numpy()
+    want = np.maximum(x @ w + b, 0)
+    feat_close(got, want, "dense")
+    pooled = pn.dense_relu(T(x), T(w), T(b), pool_rows=256).cpu().numpy()
+    feat_close(pooled, want.reshape(2, 256, 256).max(axis=1), "dense pooled")
+
+
+@pytest.mark.parametrize("cfg_name,n", [("ssg", 16384), ("ssg", 65536), ("sa1", 16384), ("msg", 16384)])
+def test_backbone_vs_oracle(cuda, cfg_name, n):
+    cfg = pn.CONFIGS[cfg_name]
+    bb = pn.PointNet2Backbone(cfg, device=cuda, seed=0)
+    x = unit_frames(1, n, 21)
+    g, levels = bb.forward(torch.from_numpy(x).to(cuda), keep_levels=True)
+    torch.cuda.synchronize()
+    want, wl = tier_n.sa_stack(x[0], {"levels": pn.resolve(cfg, n)}, bb.weights)
+    for li, ((nx, nf, ni), (ox, of, oi)) in enumerate(zip(levels, wl)):
+        assert np.array_equal(ni.cpu().numpy()[0], oi), f"level {li} FPS indices differ"
+        assert np.array_equal(nx.cpu().numpy()[0], ox)
+        feat_close(nf.cpu().numpy()[0], of, f"level {li} features")
+    feat_close(g.cpu().numpy()[0], want, "global feature")

@@ -120,16 +120,18 @@ int lidar_dbscan_f64(lidar_handle *h, const double *x, int64_t n, double eps, in
                      int64_t *labels, int32_t *counts, void *stream);
 
 /* Whole preprocess_lidar_data (utils/data_processing.py:127-229) on one frame already in
- * device memory.  Outputs (device): mask (n) u8 inlier flag, colors (n,3) f64 for all
- * points, labels (n) int64 (inlier-compacted order, first n_in valid), and `scalars`
- * (host-visible layout, device memory, 32 doubles):
+ * device memory (n >= 1 points, (n,3) f64).  Outputs (device, caller-allocated with n rows):
+ *   mask (n) u8 inlier flag; colors, normals, compact_xyz (n,3) f64 of the inliers in input
+ *   order (first n_in rows valid); labels (n) int64 over the inliers (ground -1);
+ *   scalars (64 f64):
  *   [0] n_in  [1] n_ground  [2] n_nonground  [3] z_threshold  [4] eps  [5..10] x/y/z min,max
- *   [11..14] ground plane a,b,-1,c (or the fallbacks)  [15] status (0 ok, 1 = no inliers)
+ *   [11..14] ground plane  [15] status (0 ok, 1 = no inliers -> reference IndexError)
  *   [16..18] 3-sigma mean  [19..21] std  [22..24] scaler mean  [25..27] scaler scale
- * compact_xyz (n,3) f64 receives the inlier points in order. */
+ *   [28..33] scaled bbox  [39] n_clusters  [40] plane kind (0 lstsq, 1 min-z fallback,
+ *   2 rank-deficient ground).  Asynchronous on `stream`. */
 int lidar_preprocess_f64(lidar_handle *h, const double *xyz, int64_t n, uint8_t *mask,
-                         double *colors, double *compact_xyz, int64_t *labels, double *scalars,
-                         void *stream);
+                         double *colors, double *normals, double *compact_xyz, int64_t *labels,
+                         double *scalars, void *stream);
 
 /* people positions (extract_people_positions, utils/data_processing.py:251-280):
  * centroid (x, y) of every label >= 0, sequential index-order sums;
@@ -137,9 +139,14 @@ int lidar_preprocess_f64(lidar_handle *h, const double *xyz, int64_t n, uint8_t 
 int lidar_people_f64(lidar_handle *h, const double *xyz, const int64_t *labels, int64_t n,
                      double *people, int64_t *k_host, void *stream);
 
-/* grid density (calculate_grid_density, utils/data_processing.py:282-328): np.arange
- * edges a + i*((a+g)-a), histogram2d binning (searchsorted right, last edge closed).
- * nx = len(x_edges) - 1 etc. are computed on the host by lidar_grid_dims. */
+/* grid density (calculate_grid_density, utils/data_processing.py:282-328, and the statistics
+ * of CrowdDensityModel.analyze, models/crowd_density_model.py:56-82): np.arange edges
+ * a + i*((a+g)-a), histogram2d binning (searchsorted right, last edge closed), /g^2.
+ * lidar_grid_dims gives nx, ny (host arithmetic of np.arange's length).  Outputs: grid_x (nx),
+ * grid_y (ny); `density` must hold 3*nx*ny + 13 doubles laid out as
+ *   density (nx*ny) | flat_x (nx*ny) | flat_y (nx*ny) | stats (8) | hotspot index (5, int64)
+ * stats = [max, avg of occupied cells (numpy pairwise mean), threshold, n_hotspots,
+ * n_occupied, k].  Synchronises `stream`. */
 int lidar_grid_dims(double xmin, double xmax, double ymin, double ymax, double grid,
                     int64_t *nx, int64_t *ny);
 int lidar_density_grid_f64(lidar_handle *h, const double *people, int64_t k, double xmin,

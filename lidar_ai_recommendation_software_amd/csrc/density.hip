@@ -1,0 +1,1215 @@
+// density.hip — the reference density path (Tier R) on gfx950, bit-exact with the CPU path.
+//
+// Replaces, kernel for kernel:
+//   preprocess_kernel  utils/data_processing.py:143-195 — height colours, 3-sigma filter
+//                      (numpy sequential axis-0 sums), 30th-percentile ground split
+//                      (radix select + numpy's _lerp), ground plane (normal equations;
+//                      LAPACK gelsd is not bit-reproducible, parity 1e-9 rel), StandardScaler
+//                      (sklearn's corrected two-pass variance, near-constant mask), eps heuristic.
+//   dbscan_*           data_processing.py:197 sklearn DBSCAN(eps, min_samples=5):
+//                      counting-sort voxel hash (cells > eps, 27-cell stencil), fp64
+//                      ((dx*dx+dy*dy)+dz*dz) <= eps*eps counts, union-find over core-core
+//                      edges (root = min index), rank by min core index, border = min
+//                      adjacent label.  Order-independent: identical to dbscan_inner's DFS.
+//   people_kernel      data_processing.py:251-280 per-cluster mean, sequential index-order sums
+//   density_kernel     data_processing.py:282-328 + crowd_density_model.py:56-82: np.arange
+//                      edges, histogram2d binning, /g^2, cell centres, max, numpy pairwise
+//                      mean of the occupied cells, hotspot threshold, stable top-5.
+// Sequential sums are one lane each (numpy's axis-0 order is sequential: reproducing it
+// bit for bit leaves no freedom); everything else is wave/workgroup parallel.
+#include <cmath>
+
+#include "common.hpp"
+
+namespace {
+
+constexpr int kT = 1024;  // threads of the one-workgroup-per-frame kernels
+constexpr int kW = kT / 64;
+
+// ------------------------------------------------------------------ scalars layout
+enum : int {
+    S_NIN = 0, S_NGROUND = 1, S_NNG = 2, S_ZT = 3, S_EPS = 4, S_DIMS = 5,   // 5..10
+    S_PLANE = 11,                                                            // 11..14
+    S_STATUS = 15, S_MEAN = 16, S_STD = 19, S_SMEAN = 22, S_SSCALE = 25,
+    S_SLO = 28, S_SHI = 31, S_CELL = 34, S_CDIM = 35, S_NCELL = 38, S_NCLUST = 39,
+    S_PLANE_KIND = 40, S_N = 41, S_MINPTS = 42, S_COUNT = 64
+};
+
+__device__ __forceinline__ double dadd(double a, double b) { return __dadd_rn(a, b); }
+__device__ __forceinline__ double dsub(double a, double b) { return __dsub_rn(a, b); }
+__device__ __forceinline__ double dmul(double a, double b) { return __dmul_rn(a, b); }
+__device__ __forceinline__ double ddiv(double a, double b) { return __ddiv_rn(a, b); }
+
+// ---- workgroup helpers (1024 threads)
+struct BlockScratch {
+    double d[6][kW];
+    int i[kW + 1];
+    unsigned hist[2][256];
+    double bc[16];  // broadcast
+};
+
+__device__ double block_min(BlockScratch &s, double v)
+{
+    for (int m = 32; m >= 1; m >>= 1) v = fmin(v, __shfl_xor(v, m, 64));
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) s.d[0][threadIdx.x >> 6] = v;
+    __syncthreads();
+    double r = s.d[0][0];
+    for (int w = 1; w < kW; ++w) r = fmin(r, s.d[0][w]);
+    return r;
+}
+__device__ double block_max(BlockScratch &s, double v)
+{
+    for (int m = 32; m >= 1; m >>= 1) v = fmax(v, __shfl_xor(v, m, 64));
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) s.d[1][threadIdx.x >> 6] = v;
+    __syncthreads();
+    double r = s.d[1][0];
+    for (int w = 1; w < kW; ++w) r = fmax(r, s.d[1][w]);
+    return r;
+}
+// deterministic (fixed tree) block sum — used only where the reference itself is not
+// bit-reproducible (the gelsd plane fit)
+__device__ double block_sum(BlockScratch &s, double v, int slot)
+{
+    for (int m = 32; m >= 1; m >>= 1) v = dadd(v, __shfl_xor(v, m, 64));
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) s.d[2 + slot][threadIdx.x >> 6] = v;
+    __syncthreads();
+    double r = s.d[2 + slot][0];
+    for (int w = 1; w < kW; ++w) r = dadd(r, s.d[2 + slot][w]);
+    return r;
+}
+// exclusive scan of a 0/1 flag over the workgroup; returns the position, *total set
+__device__ int block_flag_scan(BlockScratch &s, bool f, int *total)
+{
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t m = __ballot(f);
+    const int inwave = __popcll(m & ((1ull << lane) - 1));
+    __syncthreads();
+    if (lane == 0) s.i[wave] = __popcll(m);
+    __syncthreads();
+    int base = 0, tot = 0;
+    for (int w = 0; w < kW; ++w) {
+        int c = s.i[w];
+        base += w < wave ? c : 0;
+        tot += c;
+    }
+    *total = tot;
+    return base + inwave;
+}
+
+__device__ __forceinline__ uint64_t ordkey(double v)
+{
+    uint64_t u = (uint64_t)__double_as_longlong(v);
+    return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
+}
+__device__ __forceinline__ double unordkey(uint64_t k)
+{
+    uint64_t u = (k >> 63) ? (k & 0x7fffffffffffffffull) : ~k;
+    return __longlong_as_double((long long)u);
+}
+
+// sequential (numpy axis-0) sum of column c of an (n, 3) array: lane-serial, unrolled loads
+__device__ double seq_sum_col(const double *x, int64_t n, int c)
+{
+    double s = 0.0;
+    int64_t i = 0;
+    for (; i + 8 <= n; i += 8) {
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = x[3 * (i + u) + c];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s = dadd(s, v[u]);
+    }
+    for (; i < n; ++i) s = dadd(s, x[3 * i + c]);
+    return s;
+}
+// sequential sum of (x - m)^2
+__device__ double seq_sqdev_col(const double *x, int64_t n, int c, double m)
+{
+    double s = 0.0;
+    int64_t i = 0;
+    for (; i + 8 <= n; i += 8) {
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = x[3 * (i + u) + c];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const double d = dsub(v[u], m);
+            s = dadd(s, dmul(d, d));
+        }
+    }
+    for (; i < n; ++i) {
+        const double d = dsub(x[3 * i + c], m);
+        s = dadd(s, dmul(d, d));
+    }
+    return s;
+}
+
+// ------------------------------------------------------------------ preprocess
+__global__ __launch_bounds__(kT) void preprocess_kernel(const double *__restrict__ xyz, int64_t n,
+                                                        uint8_t *__restrict__ mask,
+                                                        double *__restrict__ colors,
+                                                        double *__restrict__ normals,
+                                                        double *__restrict__ comp,
+                                                        double *__restrict__ sc,
+                                                        int32_t *__restrict__ ng_pos,
+                                                        double *__restrict__ S)
+{
+    __shared__ BlockScratch s;
+    const int tid = threadIdx.x;
+
+    // ---- A: colours over ALL points (data_processing.py:143-147)
+    double lo = INFINITY, hi = -INFINITY;
+    for (int64_t i = tid; i < n; i += kT) {
+        const double z = xyz[3 * i + 2];
+        lo = fmin(lo, z);
+        hi = fmax(hi, z);
+    }
+    const double zmin = block_min(s, lo), zmax = block_max(s, hi);
+    const double denom = dadd(dsub(zmax, zmin), 1e-10);
+
+    // ---- B: mean / std with numpy's sequential axis-0 sums (:151-152)
+    if (tid < 3) {
+        const double mean = ddiv(seq_sum_col(xyz, n, tid), (double)n);
+        const double var = ddiv(seq_sqdev_col(xyz, n, tid, mean), (double)n);
+        s.bc[tid] = mean;
+        s.bc[3 + tid] = __dsqrt_rn(var);
+    }
+    __syncthreads();
+    double mean[3], thr[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        mean[c] = s.bc[c];
+        thr[c] = dmul(3.0, s.bc[3 + c]);
+    }
+    if (tid < 3) {
+        S[S_MEAN + tid] = mean[tid];
+        S[S_STD + tid] = s.bc[3 + tid];
+    }
+
+    // ---- C: strict 3-sigma mask, order-preserving compaction (:155-157)
+    int64_t nin = 0;
+    for (int64_t b0 = 0; b0 < n; b0 += kT) {
+        const int64_t i = b0 + tid;
+        bool f = false;
+        double p[3] = {0, 0, 0};
+        if (i < n) {
+            f = true;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                p[c] = xyz[3 * i + c];
+                f = f && (fabs(dsub(p[c], mean[c])) < thr[c]);
+            }
+            mask[i] = f ? 1 : 0;
+        }
+        int tot;
+        const int pos = block_flag_scan(s, f, &tot);
+        if (f) {
+            const int64_t o = nin + pos;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) comp[3 * o + c] = p[c];
+            // colours of the inliers (:143-147, masked at :157), normals (:160-161)
+            const double nh = ddiv(dsub(p[2], zmin), denom);
+            colors[3 * o] = nh;
+            colors[3 * o + 1] = dmul(0.5, dsub(1.0, nh));
+            colors[3 * o + 2] = 0.5;
+            normals[3 * o] = 0.0;
+            normals[3 * o + 1] = 0.0;
+            normals[3 * o + 2] = 1.0;
+        }
+        nin += tot;
+    }
+    if (tid == 0) {
+        S[S_NIN] = (double)nin;
+        S[S_STATUS] = nin == 0 ? 1.0 : 0.0;
+        S[S_N] = (double)n;
+    }
+    if (nin == 0) return;  // reference: IndexError from np.percentile on an empty array
+    __threadfence_block();
+    __syncthreads();
+
+    // ---- D: z threshold = np.percentile(z, 30) 'linear' (:164)
+    const double q = ddiv(30.0, 100.0);
+    const double v = dmul((double)(nin - 1), q);
+    const double prev = floor(v);
+    int64_t klo, khi;
+    if (v >= (double)(nin - 1)) {
+        klo = khi = nin - 1;
+    } else {
+        klo = (int64_t)prev;
+        khi = klo + 1;
+    }
+    double za, zb;
+    {
+        // z column of the compacted points, strided view
+        // (select reads comp[3*i+2] through a small lambda-free loop)
+        uint64_t pre[2] = {0, 0};
+        int64_t kk[2] = {klo, khi};
+        for (int pass = 0; pass < 8; ++pass) {
+            const int shift = 56 - 8 * pass;
+            for (int i = tid; i < 512; i += kT) (&s.hist[0][0])[i] = 0;
+            __syncthreads();
+            for (int64_t i = tid; i < nin; i += kT) {
+                const uint64_t key = ordkey(comp[3 * i + 2]);
+                const uint64_t hk = pass == 0 ? 0 : key >> (shift + 8);
+                const unsigned dig = (unsigned)(key >> shift) & 255u;
+                if (hk == pre[0]) atomicAdd(&s.hist[0][dig], 1u);
+                if (hk == pre[1]) atomicAdd(&s.hist[1][dig], 1u);
+            }
+            __syncthreads();
+            if (tid < 2) {
+                int64_t cum = 0;
+                int d = 0;
+                for (; d < 256; ++d) {
+                    if (cum + s.hist[tid][d] > kk[tid]) break;
+                    cum += s.hist[tid][d];
+                }
+                s.d[4 + tid][0] = __longlong_as_double((long long)((pre[tid] << 8) | (uint64_t)d));
+                s.d[4 + tid][1] = __longlong_as_double((long long)(kk[tid] - cum));
+            }
+            __syncthreads();
+            for (int r = 0; r < 2; ++r) {
+                pre[r] = (uint64_t)__double_as_longlong(s.d[4 + r][0]);
+                kk[r] = (int64_t)__double_as_longlong(s.d[4 + r][1]);
+            }
+            __syncthreads();
+        }
+        za = unordkey(pre[0]);
+        zb = unordkey(pre[1]);
+    }
+    const double t = dsub(v, prev);
+    const double diff = dsub(zb, za);
+    double zt = dadd(za, dmul(diff, t));
+    if (t >= 0.5) zt = dsub(zb, dmul(diff, dsub(1.0, t)));
+
+    // ---- E: ground count and plane (:165-183)
+    double cnt = 0, sx = 0, sy = 0, sz = 0, imin[3] = {INFINITY, INFINITY, INFINITY},
+           imax[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int64_t i = tid; i < nin; i += kT) {
+        const double px = comp[3 * i], py = comp[3 * i + 1], pz = comp[3 * i + 2];
+        imin[0] = fmin(imin[0], px);
+        imin[1] = fmin(imin[1], py);
+        imin[2] = fmin(imin[2], pz);
+        imax[0] = fmax(imax[0], px);
+        imax[1] = fmax(imax[1], py);
+        imax[2] = fmax(imax[2], pz);
+        if (pz <= zt) {
+            cnt += 1.0;
+            sx = dadd(sx, px);
+            sy = dadd(sy, py);
+            sz = dadd(sz, pz);
+        }
+    }
+    double dmin[3], dmax[3];
+    for (int c = 0; c < 3; ++c) {
+        dmin[c] = block_min(s, imin[c]);
+        dmax[c] = block_max(s, imax[c]);
+    }
+    const double ng = block_sum(s, cnt, 0);
+    const int64_t nground = (int64_t)ng;
+    double plane[4] = {0.0, 0.0, 1.0, -dmin[2]};
+    double pkind = 1.0;
+    if (nground > 10) {
+        const double mx = block_sum(s, sx, 1) / ng, my = block_sum(s, sy, 2) / ng,
+                     mz = block_sum(s, sz, 3) / ng;
+        double axx = 0, axy = 0, ayy = 0, axz = 0, ayz = 0;
+        for (int64_t i = tid; i < nin; i += kT) {
+            const double pz = comp[3 * i + 2];
+            if (pz <= zt) {
+                const double dx = comp[3 * i] - mx, dy = comp[3 * i + 1] - my, dz = pz - mz;
+                axx += dx * dx;
+                axy += dx * dy;
+                ayy += dy * dy;
+                axz += dx * dz;
+                ayz += dy * dz;
+            }
+        }
+        axx = block_sum(s, axx, 0);
+        axy = block_sum(s, axy, 1);
+        ayy = block_sum(s, ayy, 2);
+        axz = block_sum(s, axz, 3);
+        ayz = block_sum(s, ayz, 0);
+        const double det = axx * ayy - axy * axy;
+        if (det != 0.0) {
+            const double a = (axz * ayy - ayz * axy) / det, b = (axx * ayz - axy * axz) / det;
+            plane[0] = a;
+            plane[1] = b;
+            plane[2] = -1.0;
+            plane[3] = mz - a * mx - b * my;
+            pkind = 0.0;
+        } else {
+            // rank-deficient (collinear) ground: pseudo-inverse of the centred 2x2 normal
+            // system — gelsd's minimum-norm answer is reproduced only approximately here
+            const double tr = axx + ayy;
+            double a = 0.0, b = 0.0;
+            if (tr > 0.0) {
+                const double k = (axz * axx + ayz * axy) / (tr * tr);
+                a = k * axx;
+                b = k * axy;
+                if (axx == 0.0) {
+                    const double k2 = ayz / ayy;
+                    a = 0.0;
+                    b = k2;
+                }
+            }
+            plane[0] = a;
+            plane[1] = b;
+            plane[2] = -1.0;
+            plane[3] = mz - a * mx - b * my;
+            pkind = 2.0;
+        }
+    }
+    if (tid == 0) {
+        S[S_ZT] = zt;
+        S[S_NGROUND] = ng;
+        for (int c = 0; c < 3; ++c) {
+            S[S_DIMS + 2 * c] = dmin[c];
+            S[S_DIMS + 2 * c + 1] = dmax[c];
+        }
+        for (int c = 0; c < 4; ++c) S[S_PLANE + c] = plane[c];
+        S[S_PLANE_KIND] = pkind;
+    }
+
+    // ---- F: non-ground compaction (:186)
+    int64_t nng = 0;
+    for (int64_t b0 = 0; b0 < nin; b0 += kT) {
+        const int64_t i = b0 + tid;
+        const bool f = i < nin && !(comp[3 * i + 2] <= zt);
+        int tot;
+        const int pos = block_flag_scan(s, f, &tot);
+        if (f) {
+            for (int c = 0; c < 3; ++c) sc[3 * (nng + pos) + c] = comp[3 * i + c];
+            ng_pos[nng + pos] = (int32_t)i;
+        }
+        nng += tot;
+    }
+    if (tid == 0) S[S_NNG] = (double)nng;
+    if (nng <= 10) return;  // reference: all non-ground labelled 0, no DBSCAN (:199-200)
+    __threadfence_block();
+    __syncthreads();
+
+    // ---- G: StandardScaler fit (sklearn _incremental_mean_and_var, zero prior) (:190-191)
+    if (tid < 3) {
+        const double nn = (double)nng;
+        const double sum = seq_sum_col(sc, nng, tid);
+        const double T = ddiv(sum, nn);
+        double corr = 0.0, un = 0.0;
+        for (int64_t i = 0; i < nng; ++i) {
+            const double d = dsub(sc[3 * i + tid], T);
+            corr = dadd(corr, d);
+            un = dadd(un, dmul(d, d));
+        }
+        un = dsub(un, ddiv(dmul(corr, corr), nn));
+        const double var = ddiv(un, nn);
+        const double e = 2.220446049250313e-16;
+        const double ub = dadd(dmul(dmul(nn, e), var), dmul(dmul(dmul(nn, T), e), dmul(dmul(nn, T), e)));
+        const double scale = var <= ub ? 1.0 : __dsqrt_rn(var);
+        s.bc[6 + tid] = T;
+        s.bc[9 + tid] = scale;
+    }
+    __syncthreads();
+    double smean[3], sscale[3];
+    for (int c = 0; c < 3; ++c) {
+        smean[c] = s.bc[6 + c];
+        sscale[c] = s.bc[9 + c];
+    }
+    if (tid < 3) {
+        S[S_SMEAN + tid] = smean[tid];
+        S[S_SSCALE + tid] = sscale[tid];
+    }
+    // ---- H: transform (X -= mean_; X /= scale_) and bbox of the scaled cloud
+    double slo[3] = {INFINITY, INFINITY, INFINITY}, shi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int64_t i = tid; i < nng; i += kT)
+        for (int c = 0; c < 3; ++c) {
+            const double y = ddiv(dsub(sc[3 * i + c], smean[c]), sscale[c]);
+            sc[3 * i + c] = y;
+            slo[c] = fmin(slo[c], y);
+            shi[c] = fmax(shi[c], y);
+        }
+    double blo[3], bhi[3];
+    for (int c = 0; c < 3; ++c) {
+        blo[c] = block_min(s, slo[c]);
+        bhi[c] = block_max(s, shi[c]);
+    }
+    __threadfence_block();
+    __syncthreads();
+    // ---- I: eps = max(0.2, min(0.5, mean(std(scaled, axis=0)) * 0.5)) (:194-195)
+    if (tid < 3) {
+        const double nn = (double)nng;
+        const double m = ddiv(seq_sum_col(sc, nng, tid), nn);
+        s.bc[12 + tid] = __dsqrt_rn(ddiv(seq_sqdev_col(sc, nng, tid, m), nn));
+    }
+    __syncthreads();
+    if (tid == 0) {
+        const double avg = dmul(ddiv(dadd(dadd(dadd(0.0, s.bc[12]), s.bc[13]), s.bc[14]), 3.0), 0.5);
+        const double mn = avg < 0.5 ? avg : 0.5;
+        const double eps = 0.2 >= mn ? 0.2 : mn;
+        S[S_EPS] = eps;
+        for (int c = 0; c < 3; ++c) {
+            S[S_SLO + c] = blo[c];
+            S[S_SHI + c] = bhi[c];
+        }
+    }
+}
+
+// ------------------------------------------------------------------ DBSCAN
+// params (double) P: [0] n, [1] eps, [2..4] lo, [5..7] hi, [8] cell, [9..11] dims,
+// [12] ncell, [13] clusters, [14] active (n > 10 for the preprocess path)
+enum : int { P_N = 0, P_EPS = 1, P_LO = 2, P_HI = 5, P_CELL = 8, P_DIM = 9, P_NCELL = 12,
+             P_NCLUST = 13, P_ACTIVE = 14, P_COUNT = 16 };
+
+__global__ void dbscan_params_from_preprocess(const double *S, double *P, int64_t max_cells)
+{
+    if (threadIdx.x) return;
+    const double nng = S[S_NNG];
+    P[P_N] = nng;
+    P[P_EPS] = S[S_EPS];
+    P[P_ACTIVE] = (S[S_STATUS] == 0.0 && nng > 10.0) ? 1.0 : 0.0;
+    for (int c = 0; c < 3; ++c) {
+        P[P_LO + c] = S[S_SLO + c];
+        P[P_HI + c] = S[S_SHI + c];
+    }
+}
+
+__global__ __launch_bounds__(kT) void dbscan_bbox_kernel(const double *x, double *P)
+{
+    __shared__ BlockScratch s;
+    const int64_t n = (int64_t)P[P_N];
+    double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int64_t i = threadIdx.x; i < n; i += kT)
+        for (int c = 0; c < 3; ++c) {
+            lo[c] = fmin(lo[c], x[3 * i + c]);
+            hi[c] = fmax(hi[c], x[3 * i + c]);
+        }
+    for (int c = 0; c < 3; ++c) {
+        const double a = block_min(s, lo[c]), b = block_max(s, hi[c]);
+        if (threadIdx.x == 0) {
+            P[P_LO + c] = a;
+            P[P_HI + c] = b;
+        }
+    }
+}
+
+__global__ void dbscan_setup_kernel(double *P, int64_t max_cells)
+{
+    if (threadIdx.x) return;
+    const double n = P[P_N];
+    double dims[3] = {1.0, 1.0, 1.0}, tot = 1.0;
+    // cells strictly larger than eps: a 27-cell stencil sees every pair the fp64 test accepts
+    double cell = P[P_EPS] * (1.0 + 1.0 / 1048576.0);
+    if (P[P_ACTIVE] == 0.0 || !(cell > 0.0) || !(cell < INFINITY)) {
+        P[P_ACTIVE] = 0.0;
+        cell = 1.0;
+    } else {
+        const double cap = fmin(4.0 * n + 64.0, (double)max_cells);
+        bool fit = false;
+        for (int it = 0; it < 256 && !fit; ++it) {  // bounded: 1.5^256 covers any finite box
+            tot = 1.0;
+            for (int c = 0; c < 3; ++c) {
+                dims[c] = floor((P[P_HI + c] - P[P_LO + c]) / cell) + 1.0;
+                tot *= dims[c];
+            }
+            fit = tot <= cap;
+            if (!fit) cell *= 1.5;
+        }
+        if (!fit) {  // non-finite box: one cell (still exact, only slower)
+            dims[0] = dims[1] = dims[2] = 1.0;
+            tot = 1.0;
+            cell = INFINITY;
+        }
+    }
+    P[P_CELL] = cell;
+    for (int c = 0; c < 3; ++c) P[P_DIM + c] = dims[c];
+    P[P_NCELL] = tot;
+}
+
+__device__ __forceinline__ int64_t cell_coord(double v, double lo, double cell, int64_t dim)
+{
+    int64_t c = (int64_t)floor((v - lo) / cell);
+    return c < 0 ? 0 : (c >= dim ? dim - 1 : c);
+}
+
+struct Grid {
+    double lo[3], cell, eps2;
+    int64_t dim[3], n;
+    __device__ void load(const double *P)
+    {
+        for (int c = 0; c < 3; ++c) {
+            lo[c] = P[P_LO + c];
+            dim[c] = (int64_t)P[P_DIM + c];
+        }
+        cell = P[P_CELL];
+        eps2 = dmul(P[P_EPS], P[P_EPS]);
+        n = (int64_t)P[P_N];
+    }
+    __device__ int64_t cid(const double *p) const
+    {
+        return (cell_coord(p[0], lo[0], cell, dim[0]) * dim[1] + cell_coord(p[1], lo[1], cell, dim[1])) * dim[2] +
+               cell_coord(p[2], lo[2], cell, dim[2]);
+    }
+};
+
+__global__ void zero_u32_kernel(uint32_t *a, const double *P, int idx, int64_t extra)
+{
+    const int64_t n = (int64_t)P[idx] + extra;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        a[i] = 0;
+}
+
+__global__ void dbscan_cells_kernel(const double *x, const double *P, uint32_t *cid, uint32_t *cellcnt,
+                                    int32_t *parent)
+{
+    if (P[P_ACTIVE] == 0.0) return;
+    Grid g;
+    g.load(P);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < g.n; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t c = (uint32_t)g.cid(x + 3 * i);
+        cid[i] = c;
+        parent[i] = (int32_t)i;
+        atomicAdd(&cellcnt[c], 1u);
+    }
+}
+
+// --- exclusive scan of u32 over count = P[idx] (+extra) entries; out[count] = total
+constexpr int kScanPer = 4 * kT;
+__global__ __launch_bounds__(kT) void scan_partial_kernel(const uint32_t *in, const double *P, int idx,
+                                                          int64_t extra, uint32_t *partial)
+{
+    const int64_t n = (int64_t)P[idx] + extra;
+    const int64_t b0 = (int64_t)blockIdx.x * kScanPer;
+    uint32_t v = 0;
+    for (int u = 0; u < 4; ++u) {
+        const int64_t i = b0 + threadIdx.x * 4 + u;
+        v += i < n ? in[i] : 0;
+    }
+    for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+    __shared__ uint32_t ws[kW];
+    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (int w = 0; w < kW; ++w) t += ws[w];
+        partial[blockIdx.x] = t;
+    }
+}
+__global__ __launch_bounds__(kT) void scan_top_kernel(uint32_t *partial, int64_t nblk)
+{
+    // nblk <= 4 * kT
+    __shared__ uint32_t ws[kW];
+    uint32_t v[4], s = 0;
+    for (int u = 0; u < 4; ++u) {
+        const int64_t i = threadIdx.x * 4 + u;
+        v[u] = i < nblk ? partial[i] : 0;
+        s += v[u];
+    }
+    uint32_t incl = s;
+    const int lane = threadIdx.x & 63;
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t t = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += t;
+    }
+    if (lane == 63) ws[threadIdx.x >> 6] = incl;
+    __syncthreads();
+    uint32_t base = 0;
+    for (int w = 0; w < (int)(threadIdx.x >> 6); ++w) base += ws[w];
+    uint32_t e = base + incl - s;
+    for (int u = 0; u < 4; ++u) {
+        const int64_t i = threadIdx.x * 4 + u;
+        if (i < nblk) partial[i] = e;
+        e += v[u];
+    }
+}
+__global__ __launch_bounds__(kT) void scan_final_kernel(const uint32_t *in, uint32_t *out, const double *P,
+                                                        int idx, int64_t extra, const uint32_t *partial)
+{
+    const int64_t n = (int64_t)P[idx] + extra;
+    const int64_t b0 = (int64_t)blockIdx.x * kScanPer;
+    if (b0 > n) return;
+    __shared__ uint32_t ws[kW];
+    uint32_t v[4], s = 0;
+    for (int u = 0; u < 4; ++u) {
+        const int64_t i = b0 + threadIdx.x * 4 + u;
+        v[u] = i < n ? in[i] : 0;
+        s += v[u];
+    }
+    uint32_t incl = s;
+    const int lane = threadIdx.x & 63;
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t t = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += t;
+    }
+    if (lane == 63) ws[threadIdx.x >> 6] = incl;
+    __syncthreads();
+    uint32_t base = partial[blockIdx.x];
+    for (int w = 0; w < (int)(threadIdx.x >> 6); ++w) base += ws[w];
+    uint32_t e = base + incl - s;
+    for (int u = 0; u < 4; ++u) {
+        const int64_t i = b0 + threadIdx.x * 4 + u;
+        if (i <= n) out[i] = e;  // out[n] = total
+        e += v[u];
+    }
+}
+
+__global__ void dbscan_scatter_kernel(const double *x, const double *P, const uint32_t *cid,
+                                      uint32_t *fill, uint32_t *order, double *sxyz)
+{
+    if (P[P_ACTIVE] == 0.0) return;
+    const int64_t n = (int64_t)P[P_N];
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t pos = atomicAdd(&fill[cid[i]], 1u);
+        order[pos] = (uint32_t)i;
+        sxyz[3 * pos] = x[3 * i];
+        sxyz[3 * pos + 1] = x[3 * i + 1];
+        sxyz[3 * pos + 2] = x[3 * i + 2];
+    }
+}
+
+// visit every sorted slot u whose point is within eps of point (px,py,pz) in cell c
+template <class F>
+__device__ __forceinline__ void for_neighbours(const Grid &g, const uint32_t *start, const double *sxyz,
+                                               double px, double py, double pz, uint32_t c, F &&f)
+{
+    const int64_t cz = c % g.dim[2], cy = (c / g.dim[2]) % g.dim[1], cx = c / (g.dim[2] * g.dim[1]);
+    for (int64_t X = cx - 1; X <= cx + 1; ++X) {
+        if (X < 0 || X >= g.dim[0]) continue;
+        for (int64_t Y = cy - 1; Y <= cy + 1; ++Y) {
+            if (Y < 0 || Y >= g.dim[1]) continue;
+            const int64_t z0 = cz > 0 ? cz - 1 : 0, z1 = cz + 1 < g.dim[2] ? cz + 1 : g.dim[2] - 1;
+            // cells (X, Y, z0..z1) are contiguous in the sorted order
+            const int64_t cc0 = (X * g.dim[1] + Y) * g.dim[2] + z0, cc1 = (X * g.dim[1] + Y) * g.dim[2] + z1;
+            const uint32_t u0 = start[cc0], u1 = start[cc1 + 1];
+            for (uint32_t u = u0; u < u1; ++u) {
+                const double d = lidar::dist2d(px, py, pz, sxyz[3 * u], sxyz[3 * u + 1], sxyz[3 * u + 2]);
+                if (d <= g.eps2) f(u);
+            }
+        }
+    }
+}
+
+__global__ void dbscan_count_kernel(const double *P, const uint32_t *cid, const uint32_t *start,
+                                    const uint32_t *order, const double *sxyz, int32_t *cnt)
+{
+    if (P[P_ACTIVE] == 0.0) return;
+    Grid g;
+    g.load(P);
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < g.n; t += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t i = order[t];
+        int32_t k = 0;
+        for_neighbours(g, start, sxyz, sxyz[3 * t], sxyz[3 * t + 1], sxyz[3 * t + 2], cid[i],
+                       [&](uint32_t) { ++k; });
+        cnt[i] = k;
+    }
+}
+
+__device__ __forceinline__ int32_t ld(const int32_t *p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ int32_t uf_find(int32_t *parent, int32_t x)
+{
+    int32_t p = ld(parent + x);
+    while (p != x) {
+        x = p;
+        p = ld(parent + x);
+    }
+    return x;
+}
+__device__ void uf_unite(int32_t *parent, int32_t a, int32_t b)
+{
+    for (;;) {
+        a = uf_find(parent, a);
+        b = uf_find(parent, b);
+        if (a == b) return;
+        if (a < b) {
+            const int32_t t = a;
+            a = b;
+            b = t;
+        }
+        // hook the larger root under the smaller: the final root is the component minimum
+        const int32_t old = atomicCAS(parent + a, a, b);
+        if (old == a) return;
+        a = old;
+    }
+}
+
+__global__ void dbscan_union_kernel(const double *P, const uint32_t *cid, const uint32_t *start,
+                                    const uint32_t *order, const double *sxyz, const int32_t *cnt,
+                                    int32_t min_samples, int32_t *parent)
+{
+    if (P[P_ACTIVE] == 0.0) return;
+    Grid g;
+    g.load(P);
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < g.n; t += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t i = (int32_t)order[t];
+        if (cnt[i] < min_samples) continue;
+        for_neighbours(g, start, sxyz, sxyz[3 * t], sxyz[3 * t + 1], sxyz[3 * t + 2], cid[i], [&](uint32_t u) {
+            const int32_t j = (int32_t)order[u];
+            if (j < i && cnt[j] >= min_samples) uf_unite(parent, i, j);
+        });
+    }
+}
+
+__global__ void dbscan_roots_kernel(const double *P, const int32_t *cnt, int32_t min_samples,
+                                    int32_t *parent, uint32_t *flag)
+{
+    const int64_t n = (int64_t)P[P_N];
+    const bool active = P[P_ACTIVE] != 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        uint32_t f = 0;
+        if (active && cnt[i] >= min_samples) {
+            const int32_t r = uf_find(parent, (int32_t)i);
+            parent[i] = r;
+            f = r == (int32_t)i ? 1u : 0u;
+        }
+        flag[i] = f;
+    }
+}
+
+__global__ void dbscan_labels_kernel(double *P, const uint32_t *cid, const uint32_t *start,
+                                     const uint32_t *order, const double *sxyz, const int32_t *cnt,
+                                     int32_t min_samples, const int32_t *parent, const uint32_t *rank,
+                                     int64_t *labels)
+{
+    if (P[P_ACTIVE] == 0.0) return;
+    Grid g;
+    g.load(P);
+    if (blockIdx.x == 0 && threadIdx.x == 0) P[P_NCLUST] = (double)rank[g.n];
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < g.n; t += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t i = (int32_t)order[t];
+        int64_t lab;
+        if (cnt[i] >= min_samples) {
+            lab = rank[parent[i]];
+        } else {
+            int64_t best = -1;
+            for_neighbours(g, start, sxyz, sxyz[3 * t], sxyz[3 * t + 1], sxyz[3 * t + 2], cid[i], [&](uint32_t u) {
+                const int32_t j = (int32_t)order[u];
+                if (cnt[j] >= min_samples) {
+                    const int64_t l = rank[parent[j]];
+                    if (best < 0 || l < best) best = l;
+                }
+            });
+            lab = best;
+        }
+        labels[i] = lab;
+    }
+}
+
+// full labels over the inliers: ground -1, non-ground = DBSCAN label (or 0 when <= 10)
+__global__ void scatter_labels_kernel(const double *S, const int64_t *ng_labels, const int32_t *ng_pos,
+                                      int64_t *full)
+{
+    if (S[S_STATUS] != 0.0) return;
+    const int64_t nin = (int64_t)S[S_NIN];
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nin; i += stride) full[i] = -1;
+    __syncthreads();
+}
+__global__ void scatter_labels2_kernel(const double *S, const int64_t *ng_labels, const int32_t *ng_pos,
+                                       int64_t *full)
+{
+    if (S[S_STATUS] != 0.0) return;
+    const int64_t nng = (int64_t)S[S_NNG];
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nng; i += stride)
+        full[ng_pos[i]] = nng > 10 ? ng_labels[i] : 0;
+}
+
+// ------------------------------------------------------------------ people
+// one wavefront per cluster scans the frame in index order: ballot the members of each
+// 64-point chunk, then add them lane by lane — numpy's sequential axis-0 order
+__global__ __launch_bounds__(256) void people_kernel(const double *xyz, const int64_t *labels, int64_t n,
+                                                     const int64_t *kdev, double *out)
+{
+    const int lane = threadIdx.x & 63;
+    const int64_t K = *kdev;
+    const int64_t nw = (int64_t)gridDim.x * 4;
+    for (int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); c < K; c += nw) {
+        double sx = 0.0, sy = 0.0;
+        int64_t cnt = 0;
+        for (int64_t b0 = 0; b0 < n; b0 += 64) {
+            const int64_t i = b0 + lane;
+            const bool hit = i < n && labels[i] == c;
+            double x = 0.0, y = 0.0;
+            if (hit) {
+                x = xyz[3 * i];
+                y = xyz[3 * i + 1];
+            }
+            uint64_t m = __ballot(hit);
+            while (m) {
+                const int b = __ffsll((unsigned long long)m) - 1;
+                m &= m - 1;
+                const double vx = __shfl(x, b, 64), vy = __shfl(y, b, 64);
+                if (cnt == 0) {
+                    sx = vx;
+                    sy = vy;
+                } else {
+                    sx = dadd(sx, vx);
+                    sy = dadd(sy, vy);
+                }
+                ++cnt;
+            }
+        }
+        if (lane == 0) {
+            out[2 * c] = ddiv(sx, (double)cnt);
+            out[2 * c + 1] = ddiv(sy, (double)cnt);
+        }
+    }
+}
+
+__global__ void max_label_kernel(const int64_t *labels, int64_t n, int64_t *kout)
+{
+    // K = number of distinct labels >= 0 = max + 1 (labels are dense ranks)
+    int64_t m = -1;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        m = labels[i] > m ? labels[i] : m;
+    for (int o = 32; o >= 1; o >>= 1) {
+        const int64_t t = __shfl_xor(m, o, 64);
+        m = t > m ? t : m;
+    }
+    if ((threadIdx.x & 63) == 0) atomicMax((unsigned long long *)kout, (unsigned long long)(m + 1));
+}
+
+// ------------------------------------------------------------------ density grid
+// numpy float64 add.reduce of a contiguous 1-D array: 8192-element buffer chunks,
+// each summed by pairwise_sum (8-way unrolled leaves of <= 128), chunks added in order
+__device__ double np_pairwise(const double *a, int64_t n)
+{
+    if (n < 8) {
+        double r = 0.0;
+        for (int64_t i = 0; i < n; ++i) r = dadd(r, a[i]);
+        return r;
+    }
+    if (n <= 128) {
+        double r[8];
+        for (int j = 0; j < 8; ++j) r[j] = a[j];
+        int64_t i = 8;
+        for (; i < n - (n % 8); i += 8)
+            for (int j = 0; j < 8; ++j) r[j] = dadd(r[j], a[i + j]);
+        double res = dadd(dadd(dadd(r[0], r[1]), dadd(r[2], r[3])), dadd(dadd(r[4], r[5]), dadd(r[6], r[7])));
+        for (; i < n; ++i) res = dadd(res, a[i]);
+        return res;
+    }
+    int64_t n2 = n / 2;
+    n2 -= n2 % 8;
+    return dadd(np_pairwise(a, n2), np_pairwise(a + n2, n - n2));
+}
+__device__ double np_sum(const double *a, int64_t n)
+{
+    double out = 0.0;
+    for (int64_t i = 0; i < n; i += 8192) out = dadd(out, np_pairwise(a + i, n - i < 8192 ? n - i : 8192));
+    return out;
+}
+
+__device__ int64_t searchsorted_right(const double *e, int64_t len, double v)
+{
+    int64_t lo = 0, hi = len;  // first index with e[idx] > v
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (e[mid] <= v) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(kT) void density_kernel(const double *people, const int64_t *kdev,
+                                                     double xa, double ya, double g, int64_t nx, int64_t ny,
+                                                     double *xe, double *ye, uint32_t *count,
+                                                     double *grid_x, double *grid_y, double *density,
+                                                     double *flat_x, double *flat_y, double *pos_scratch,
+                                                     double *stats, int64_t *hot)
+{
+    const int64_t K = *kdev;
+    const int tid = threadIdx.x;
+    // np.arange: e[0] = a, e[1] = a + g, e[i] = a + i * (e[1] - e[0])
+    const double dx = dsub(dadd(xa, g), xa), dy = dsub(dadd(ya, g), ya);
+    for (int64_t i = tid; i <= nx; i += kT) xe[i] = i == 0 ? xa : (i == 1 ? dadd(xa, g) : dadd(xa, dmul((double)i, dx)));
+    for (int64_t i = tid; i <= ny; i += kT) ye[i] = i == 0 ? ya : (i == 1 ? dadd(ya, g) : dadd(ya, dmul((double)i, dy)));
+    for (int64_t i = tid; i < nx * ny; i += kT) count[i] = 0;
+    __threadfence_block();
+    __syncthreads();
+    for (int64_t k = tid; k < K; k += kT) {
+        const double px = people[2 * k], py = people[2 * k + 1];
+        int64_t bx = searchsorted_right(xe, nx + 1, px), by = searchsorted_right(ye, ny + 1, py);
+        if (px == xe[nx]) --bx;
+        if (py == ye[ny]) --by;
+        if (bx >= 1 && bx <= nx && by >= 1 && by <= ny) atomicAdd(&count[(bx - 1) * ny + (by - 1)], 1u);
+    }
+    __threadfence_block();
+    __syncthreads();
+    const double g2 = dmul(g, g);
+    for (int64_t i = tid; i < nx; i += kT) grid_x[i] = ddiv(dadd(xe[i], xe[i + 1]), 2.0);
+    for (int64_t i = tid; i < ny; i += kT) grid_y[i] = ddiv(dadd(ye[i], ye[i + 1]), 2.0);
+    for (int64_t i = tid; i < nx * ny; i += kT) {
+        density[i] = ddiv((double)count[i], g2);
+        flat_x[i] = ddiv(dadd(xe[i / ny], xe[i / ny + 1]), 2.0);
+        flat_y[i] = ddiv(dadd(ye[i % ny], ye[i % ny + 1]), 2.0);
+    }
+    __threadfence_block();
+    __syncthreads();
+    if (tid == 0) {
+        // max, occupied cells in flat order, numpy mean, threshold, stable top-5
+        double mx = -INFINITY;
+        int64_t np_ = 0;
+        for (int64_t i = 0; i < nx * ny; ++i) {
+            const double d = density[i];
+            mx = d > mx ? d : mx;
+            if (d > 0.0) pos_scratch[np_++] = d;
+        }
+        const double avg = np_ > 0 ? ddiv(np_sum(pos_scratch, np_), (double)np_) : 0.0;
+        const double a15 = dmul(avg, 1.5);
+        const double thr = 0.5 >= a15 ? 0.5 : a15;
+        int64_t nh = 0;
+        double last = INFINITY;
+        int64_t last_i = -1;
+        for (; nh < 5; ++nh) {
+            // next hotspot: highest density below (last, last_i) in (desc density, asc index) order
+            int64_t best = -1;
+            double bd = -INFINITY;
+            for (int64_t i = 0; i < nx * ny; ++i) {
+                const double d = density[i];
+                if (!(d >= thr)) continue;
+                const bool after = d < last || (d == last && i > last_i);
+                if (!after) continue;
+                if (best < 0 || d > bd) {
+                    best = i;
+                    bd = d;
+                }
+            }
+            if (best < 0) break;
+            hot[nh] = best;
+            last = bd;
+            last_i = best;
+        }
+        stats[0] = mx;
+        stats[1] = avg;
+        stats[2] = thr;
+        stats[3] = (double)nh;
+        stats[4] = (double)np_;
+        stats[5] = (double)K;
+    }
+}
+
+// ------------------------------------------------------------------ workspace plan
+struct DbscanWs {
+    double *P;
+    uint32_t *cid, *cellcnt, *cellstart, *fill, *order, *flag, *rank, *partial;
+    double *sxyz;
+    int32_t *cnt, *parent;
+    int64_t max_cells, nblk_cells, nblk_pts;
+};
+
+int64_t max_cells_for(int64_t n) { return std::min<int64_t>(4 * n + 64, 1 << 22); }
+
+void plan_dbscan(lidar::Carver &cv, int64_t n, uint64_t *off)
+{
+    const int64_t mc = max_cells_for(n);
+    off[0] = cv.take<double>(P_COUNT);
+    off[1] = cv.take<uint32_t>(n);           // cid
+    off[2] = cv.take<uint32_t>(mc + 1);      // cellcnt
+    off[3] = cv.take<uint32_t>(mc + 1);      // cellstart
+    off[4] = cv.take<uint32_t>(mc + 1);      // fill
+    off[5] = cv.take<uint32_t>(n + 1);       // order
+    off[6] = cv.take<uint32_t>(n + 1);       // flag
+    off[7] = cv.take<uint32_t>(n + 1);       // rank
+    off[8] = cv.take<uint32_t>(4 * kT);      // partial
+    off[9] = cv.take<double>(3 * n);         // sxyz
+    off[10] = cv.take<int32_t>(n);           // cnt
+    off[11] = cv.take<int32_t>(n);           // parent
+}
+
+DbscanWs bind_dbscan(char *base, const uint64_t *off, int64_t n)
+{
+    DbscanWs w;
+    w.P = reinterpret_cast<double *>(base + off[0]);
+    w.cid = reinterpret_cast<uint32_t *>(base + off[1]);
+    w.cellcnt = reinterpret_cast<uint32_t *>(base + off[2]);
+    w.cellstart = reinterpret_cast<uint32_t *>(base + off[3]);
+    w.fill = reinterpret_cast<uint32_t *>(base + off[4]);
+    w.order = reinterpret_cast<uint32_t *>(base + off[5]);
+    w.flag = reinterpret_cast<uint32_t *>(base + off[6]);
+    w.rank = reinterpret_cast<uint32_t *>(base + off[7]);
+    w.partial = reinterpret_cast<uint32_t *>(base + off[8]);
+    w.sxyz = reinterpret_cast<double *>(base + off[9]);
+    w.cnt = reinterpret_cast<int32_t *>(base + off[10]);
+    w.parent = reinterpret_cast<int32_t *>(base + off[11]);
+    w.max_cells = max_cells_for(n);
+    w.nblk_cells = (w.max_cells + 1 + kScanPer - 1) / kScanPer;
+    w.nblk_pts = (n + 1 + kScanPer - 1) / kScanPer;
+    return w;
+}
+
+int run_scan(const uint32_t *in, uint32_t *out, const double *P, int idx, int64_t extra, uint32_t *partial,
+             int64_t nblk, hipStream_t s)
+{
+    hipLaunchKernelGGL(scan_partial_kernel, dim3((unsigned)nblk), dim3(kT), 0, s, in, P, idx, extra, partial);
+    hipLaunchKernelGGL(scan_top_kernel, dim3(1), dim3(kT), 0, s, partial, nblk);
+    hipLaunchKernelGGL(scan_final_kernel, dim3((unsigned)nblk), dim3(kT), 0, s, in, out, P, idx, extra, partial);
+    LAUNCH_CHECK();
+    return LIDAR_OK;
+}
+
+// the DBSCAN pipeline on x (P[P_N] points, eps P[P_EPS], bbox in P) -> labels
+int run_dbscan(const double *x, int64_t nmax, int32_t min_samples, DbscanWs &w, int64_t *labels, hipStream_t s)
+{
+    const unsigned gp = (unsigned)std::max<int64_t>(1, std::min<int64_t>((nmax + 255) / 256, 4096));
+    hipLaunchKernelGGL(dbscan_setup_kernel, dim3(1), dim3(64), 0, s, w.P, w.max_cells);
+    hipLaunchKernelGGL(zero_u32_kernel, dim3(512), dim3(256), 0, s, w.cellcnt, w.P, P_NCELL, 1);
+    hipLaunchKernelGGL(dbscan_cells_kernel, dim3(gp), dim3(256), 0, s, x, w.P, w.cid, w.cellcnt, w.parent);
+    int rc = run_scan(w.cellcnt, w.cellstart, w.P, P_NCELL, 0, w.partial, w.nblk_cells, s);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(w.fill, w.cellstart, sizeof(uint32_t) * (w.max_cells + 1), hipMemcpyDeviceToDevice, s));
+    hipLaunchKernelGGL(dbscan_scatter_kernel, dim3(gp), dim3(256), 0, s, x, w.P, w.cid, w.fill, w.order, w.sxyz);
+    hipLaunchKernelGGL(dbscan_count_kernel, dim3(gp), dim3(256), 0, s, w.P, w.cid, w.cellstart, w.order, w.sxyz, w.cnt);
+    hipLaunchKernelGGL(dbscan_union_kernel, dim3(gp), dim3(256), 0, s, w.P, w.cid, w.cellstart, w.order, w.sxyz,
+                       w.cnt, min_samples, w.parent);
+    hipLaunchKernelGGL(dbscan_roots_kernel, dim3(gp), dim3(256), 0, s, w.P, w.cnt, min_samples, w.parent, w.flag);
+    rc = run_scan(w.flag, w.rank, w.P, P_N, 0, w.partial, w.nblk_pts, s);
+    if (rc) return rc;
+    hipLaunchKernelGGL(dbscan_labels_kernel, dim3(gp), dim3(256), 0, s, w.P, w.cid, w.cellstart, w.order, w.sxyz,
+                       w.cnt, min_samples, w.parent, w.rank, labels);
+    LAUNCH_CHECK();
+    return LIDAR_OK;
+}
+
+}  // namespace
+
+// ====================================================================== C-ABI
+LIDAR_EXPORT int lidar_dbscan_f64(lidar_handle *h, const double *x, int64_t n, double eps,
+                                  int32_t min_samples, int64_t *labels, int32_t *counts, void *stream)
+{
+    REQUIRE(h && x && labels, "lidar_dbscan_f64: null pointer");
+    REQUIRE(n >= 0 && n < 0x7fffffff, "lidar_dbscan_f64: n out of range");
+    REQUIRE(eps > 0.0, "lidar_dbscan_f64: eps must be > 0");
+    REQUIRE(min_samples >= 1, "lidar_dbscan_f64: min_samples must be >= 1");
+    if (n == 0) return LIDAR_OK;
+    HIP_TRY(hipSetDevice(h->device));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    lidar::Carver cv;
+    uint64_t off[12];
+    plan_dbscan(cv, n, off);
+    char *base = static_cast<char *>(lidar::workspace(h, cv.off));
+    if (!base) return LIDAR_ENOMEM;
+    DbscanWs w = bind_dbscan(base, off, n);
+    double hp[P_COUNT] = {};
+    hp[P_N] = (double)n;
+    hp[P_EPS] = eps;
+    hp[P_ACTIVE] = 1.0;
+    HIP_TRY(hipMemcpyAsync(w.P, hp, sizeof hp, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(dbscan_bbox_kernel, dim3(1), dim3(kT), 0, s, x, w.P);
+    int rc = run_dbscan(x, n, min_samples, w, labels, s);
+    if (rc) return rc;
+    if (counts) HIP_TRY(hipMemcpyAsync(counts, w.cnt, sizeof(int32_t) * n, hipMemcpyDeviceToDevice, s));
+    // hp is a stack buffer: make sure the H2D copy has consumed it
+    HIP_TRY(hipStreamSynchronize(s));
+    return LIDAR_OK;
+}
+
+LIDAR_EXPORT int lidar_preprocess_f64(lidar_handle *h, const double *xyz, int64_t n, uint8_t *mask,
+                                      double *colors, double *normals, double *compact_xyz,
+                                      int64_t *labels, double *scalars, void *stream)
+{
+    REQUIRE(h && xyz && mask && colors && normals && compact_xyz && labels && scalars,
+            "lidar_preprocess_f64: null pointer");
+    REQUIRE(n >= 1 && n < 0x7fffffff, "lidar_preprocess_f64: need 1 <= n < 2^31");
+    HIP_TRY(hipSetDevice(h->device));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    lidar::Carver cv;
+    const uint64_t o_sc = cv.take<double>(3 * n);
+    const uint64_t o_pos = cv.take<int32_t>(n);
+    const uint64_t o_lab = cv.take<int64_t>(n);
+    uint64_t off[12];
+    plan_dbscan(cv, n, off);
+    char *base = static_cast<char *>(lidar::workspace(h, cv.off));
+    if (!base) return LIDAR_ENOMEM;
+    double *sc = reinterpret_cast<double *>(base + o_sc);
+    int32_t *ng_pos = reinterpret_cast<int32_t *>(base + o_pos);
+    int64_t *ng_lab = reinterpret_cast<int64_t *>(base + o_lab);
+    DbscanWs w = bind_dbscan(base, off, n);
+    HIP_TRY(hipMemsetAsync(scalars, 0, sizeof(double) * S_COUNT, s));
+    hipLaunchKernelGGL(preprocess_kernel, dim3(1), dim3(kT), 0, s, xyz, n, mask, colors, normals, compact_xyz,
+                       sc, ng_pos, scalars);
+    hipLaunchKernelGGL(dbscan_params_from_preprocess, dim3(1), dim3(64), 0, s, scalars, w.P, w.max_cells);
+    int rc = run_dbscan(sc, n, 5, w, ng_lab, s);
+    if (rc) return rc;
+    const unsigned gp = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 4096));
+    hipLaunchKernelGGL(scatter_labels_kernel, dim3(gp), dim3(256), 0, s, scalars, ng_lab, ng_pos, labels);
+    hipLaunchKernelGGL(scatter_labels2_kernel, dim3(gp), dim3(256), 0, s, scalars, ng_lab, ng_pos, labels);
+    HIP_TRY(hipMemcpyAsync(scalars + S_NCLUST, w.P + P_NCLUST, sizeof(double), hipMemcpyDeviceToDevice, s));
+    LAUNCH_CHECK();
+    return LIDAR_OK;
+}
+
+LIDAR_EXPORT int lidar_people_f64(lidar_handle *h, const double *xyz, const int64_t *labels, int64_t n,
+                                  double *people, int64_t *k_host, void *stream)
+{
+    REQUIRE(h && xyz && labels && people && k_host, "lidar_people_f64: null pointer");
+    REQUIRE(n >= 0, "lidar_people_f64: n < 0");
+    *k_host = 0;
+    if (n == 0) return LIDAR_OK;
+    HIP_TRY(hipSetDevice(h->device));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    int64_t *kd = static_cast<int64_t *>(lidar::workspace(h, 256));
+    if (!kd) return LIDAR_ENOMEM;
+    HIP_TRY(hipMemsetAsync(kd, 0, sizeof(int64_t), s));
+    const unsigned gp = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 1024));
+    hipLaunchKernelGGL(max_label_kernel, dim3(gp), dim3(256), 0, s, labels, n, kd);
+    hipLaunchKernelGGL(people_kernel, dim3(1024), dim3(256), 0, s, xyz, labels, n, kd, people);
+    LAUNCH_CHECK();
+    int64_t *hk = static_cast<int64_t *>(h->host_pinned);
+    HIP_TRY(hipMemcpyAsync(hk, kd, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    *k_host = *hk;
+    return LIDAR_OK;
+}
+
+LIDAR_EXPORT int lidar_grid_dims(double xmin, double xmax, double ymin, double ymax, double grid,
+                                 int64_t *nx, int64_t *ny)
+{
+    REQUIRE(nx && ny && grid > 0.0, "lidar_grid_dims: bad arguments");
+    // data_processing.py:305-313: margin 2g, np.arange(min - 2g, max + 2g + g, g)
+    const double m = grid * 2.0;
+    const double x0 = xmin - m, x1 = (xmax + m) + grid;
+    const double y0 = ymin - m, y1 = (ymax + m) + grid;
+    const double lx = std::ceil((x1 - x0) / grid), ly = std::ceil((y1 - y0) / grid);
+    REQUIRE(lx >= 2 && ly >= 2 && lx < 1e8 && ly < 1e8, "lidar_grid_dims: degenerate grid");
+    *nx = (int64_t)lx - 1;
+    *ny = (int64_t)ly - 1;
+    return LIDAR_OK;
+}
+
+// people (k, 2) -> grid_x (nx), grid_y (ny), density (nx*ny), flat_x, flat_y (nx*ny),
+// stats [max, avg, thr, n_hot, n_occupied, k], hot (5) int64.  `out` layout (doubles):
+// grid_x | grid_y | density | flat_x | flat_y | stats(8) | hot(5, int64)
+LIDAR_EXPORT int lidar_density_grid_f64(lidar_handle *h, const double *people, int64_t k, double xmin,
+                                        double xmax, double ymin, double ymax, double grid, int64_t nx,
+                                        int64_t ny, double *grid_x, double *grid_y, double *density,
+                                        void *stream)
+{
+    REQUIRE(h && people && grid_x && grid_y && density, "lidar_density_grid_f64: null pointer");
+    REQUIRE(nx >= 1 && ny >= 1 && k >= 0, "lidar_density_grid_f64: bad sizes");
+    HIP_TRY(hipSetDevice(h->device));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    lidar::Carver cv;
+    const uint64_t o_xe = cv.take<double>(nx + 1), o_ye = cv.take<double>(ny + 1);
+    const uint64_t o_cnt = cv.take<uint32_t>(nx * ny), o_pos = cv.take<double>(nx * ny);
+    const uint64_t o_k = cv.take<int64_t>(1);
+    char *base = static_cast<char *>(lidar::workspace(h, cv.off));
+    if (!base) return LIDAR_ENOMEM;
+    int64_t *kd = reinterpret_cast<int64_t *>(base + o_k);
+    int64_t *hk = static_cast<int64_t *>(h->host_pinned);
+    *hk = k;
+    HIP_TRY(hipMemcpyAsync(kd, hk, sizeof(int64_t), hipMemcpyHostToDevice, s));
+    const double m = grid * 2.0;
+    // density points at: density (nx*ny) | flat_x | flat_y | stats (8) | hot (5)
+    double *flat_x = density + nx * ny, *flat_y = flat_x + nx * ny, *stats = flat_y + nx * ny;
+    int64_t *hot = reinterpret_cast<int64_t *>(stats + 8);
+    hipLaunchKernelGGL(density_kernel, dim3(1), dim3(kT), 0, s, people, kd, xmin - m, ymin - m, grid, nx, ny,
+                       reinterpret_cast<double *>(base + o_xe), reinterpret_cast<double *>(base + o_ye),
+                       reinterpret_cast<uint32_t *>(base + o_cnt), grid_x, grid_y, density, flat_x, flat_y,
+                       reinterpret_cast<double *>(base + o_pos), stats, hot);
+    LAUNCH_CHECK();
+    HIP_TRY(hipStreamSynchronize(s));  // hk is reused by the next call
+    return LIDAR_OK;
+}

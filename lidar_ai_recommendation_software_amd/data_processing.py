@@ -1,0 +1,270 @@
+"""Drop-in for the reference's ``utils/data_processing.py`` on MI355X.
+
+Same function names, positional arguments, defaults, return types and exceptions as
+the reference (FortuneMU2025/LIDAR_AI_Recommendation_Software ``utils/data_processing.py``);
+the arithmetic runs in the gfx950 kernels of ``liblidar_amd.so`` and is bit-identical
+to the reference's NumPy / scikit-learn CPU path (see DESIGN.md §2 and
+``tests/test_gpu_tier_r.py``).  Inputs and outputs are NumPy, as the reference's
+callers expect (``app.py:81``, ``visualization.py``); device copies of the last
+results are cached so that ``extract_people_positions`` / ``CrowdDensityModel.analyze``
+on a ``preprocess_lidar_data`` result do not re-upload the frame.
+
+Extensions beyond the reference (north_star operators):
+``voxel_downsample`` and ``farthest_point_sample``.
+"""
+import os
+import re
+import weakref
+
+import numpy as np
+
+from . import _native as nat
+
+# ----------------------------------------------------------------- device cache
+_cache = {}
+
+
+def _remember(arr, tensor):
+    key = id(arr)
+    _cache[key] = (weakref.ref(arr, lambda _r, k=key: _cache.pop(k, None)), tensor)
+
+
+def _on_device(arr, dtype):
+    import torch
+    hit = _cache.get(id(arr))
+    if hit is not None and hit[0]() is arr and hit[1].dtype == dtype:
+        return hit[1]
+    npd = {torch.float64: np.float64, torch.int64: np.int64, torch.float32: np.float32}[dtype]
+    return torch.from_numpy(np.ascontiguousarray(arr, dtype=npd)).cuda()
+
+
+def _handle():
+    import torch
+    return nat.handle(torch.cuda.current_device())
+
+
+# ----------------------------------------------------------------------- I/O (L1)
+def load_lidar_data(file_path):
+    """Load an (n, 3) point array from CSV / XYZ / TXT / PCD (ascii) / PLY (ascii) / NPY.
+
+    Mirrors ``utils/data_processing.py:8-125`` (the "next" input boundary of SURVEY §8f;
+    host-side parsing, not accelerated): same formats and column rules, and every
+    failure is re-raised as ``Exception("Failed to load point cloud file: ...")``.
+    """
+    try:
+        ext = file_path.lower().split(".")[-1]
+        if ext == "csv":
+            import pandas as pd
+            df = pd.read_csv(file_path)
+            cols = [c for c in df.columns if c.lower() in ("x", "y", "z")]
+            pts = df[cols[:3]].values if len(cols) >= 3 else df.iloc[:, :3].values
+        elif ext in ("xyz", "txt"):
+            pts = np.loadtxt(file_path, delimiter=None)[:, :3]
+        elif ext == "npy":
+            pts = np.load(file_path)[:, :3]
+        elif ext == "pcd":
+            pts = _read_ascii_body(file_path, _pcd_body_start)
+        elif ext == "ply":
+            pts = _read_ascii_body(file_path, _ply_body)
+        else:
+            raise ValueError(f"Unsupported file format: {ext}")
+        if len(pts) == 0:
+            raise ValueError("The loaded point cloud contains no points")
+        return pts
+    except Exception as e:
+        raise Exception(f"Failed to load point cloud file: {str(e)}")
+
+
+_PCD_HEADER = re.compile(r"([A-Z_]+)\s+([\w\s\.]+)")
+
+
+def _pcd_body_start(lines):
+    # header lines are "KEY value"; the first line that is neither a comment, blank,
+    # nor such a header starts the data
+    for i, ln in enumerate(lines):
+        s = ln.strip()
+        if ln.startswith("#") or not s or _PCD_HEADER.match(s):
+            continue
+        return i, len(lines)
+    return 0, len(lines)
+
+
+def _ply_body(lines):
+    nvert = None
+    for i, ln in enumerate(lines):
+        if ln.strip() == "end_header":
+            start = i + 1
+            return start, start + (nvert if nvert is not None else len(lines))
+        if "element vertex" in ln:
+            nvert = int(ln.split()[-1])
+    return 0, (nvert if nvert is not None else len(lines))
+
+
+def _read_ascii_body(path, locate):
+    with open(path, "r") as f:
+        lines = f.readlines()
+    a, b = locate(lines)
+    rows = []
+    for ln in lines[a:min(b, len(lines))]:
+        vals = ln.strip().split()
+        if len(vals) >= 3:
+            rows.append([float(v) for v in vals[:3]])
+    return np.array(rows)
+
+
+# ---------------------------------------------------------------- preprocess (L2)
+def preprocess_lidar_data(points):
+    """Replaces ``utils/data_processing.py:127-229`` — one frame on the GPU.
+
+    Returns the reference's dict {points, colors, normals, clusters, ground_plane,
+    dimensions} with the same dtypes; raises the reference's exceptions (ValueError
+    on an empty frame, IndexError when no point survives the 3-sigma filter).
+    """
+    import torch
+    pts = np.asarray(points)
+    if pts.ndim != 2 or pts.shape[1] < 3:
+        raise IndexError("too many indices for array")
+    n = len(pts)
+    if n == 0:
+        raise ValueError("zero-size array to reduction operation minimum which has no identity")
+    is_int = pts.dtype.kind in "iub"
+    x = torch.from_numpy(np.ascontiguousarray(pts[:, :3], dtype=np.float64)).cuda()
+    dev = x.device
+    mask = torch.empty(n, dtype=torch.uint8, device=dev)
+    colors = torch.empty((n, 3), dtype=torch.float64, device=dev)
+    normals = torch.empty((n, 3), dtype=torch.float64, device=dev)
+    comp = torch.empty((n, 3), dtype=torch.float64, device=dev)
+    labels = torch.empty(n, dtype=torch.int64, device=dev)
+    scal = torch.empty(64, dtype=torch.float64, device=dev)
+    nat.call("lidar_preprocess_f64", _handle(), nat.ptr(x), n, nat.ptr(mask), nat.ptr(colors),
+             nat.ptr(normals), nat.ptr(comp), nat.ptr(labels), nat.ptr(scal), nat.stream_ptr())
+    S = scal.cpu().numpy()
+    if S[15] != 0:
+        raise IndexError("index -1 is out of bounds for axis 0 with size 0")
+    nin = int(S[0])
+    comp_d, lab_d = comp[:nin], labels[:nin]
+    inl = comp_d.cpu().numpy()
+    if is_int:
+        inl = inl.astype(pts.dtype)
+    cols = colors[:nin].cpu().numpy()
+    nrm = normals[:nin].cpu().numpy()
+    if is_int:
+        nrm = nrm.astype(pts.dtype)
+    clusters = lab_d.cpu().numpy()
+    kind = S[40]
+    if kind == 1.0 and is_int:
+        plane = np.array([0, 0, 1, -int(S[9])])
+    elif kind == 1.0:
+        plane = np.array([0.0, 0.0, 1.0, S[14]])
+    else:
+        plane = np.array([S[11], S[12], -1, S[14]], dtype=np.float64)
+    mins, maxs = S[[5, 7, 9]], S[[6, 8, 10]]
+    if is_int:
+        mins, maxs = mins.astype(pts.dtype), maxs.astype(pts.dtype)
+    (x_min, y_min, z_min), (x_max, y_max, z_max) = mins, maxs
+    dims = {"x_range": (x_min, x_max), "y_range": (y_min, y_max), "z_range": (z_min, z_max),
+            "width": x_max - x_min, "length": y_max - y_min, "height": z_max - z_min}
+    out = {"points": inl, "colors": cols, "normals": nrm, "clusters": clusters,
+           "ground_plane": plane, "dimensions": dims}
+    _remember(inl, comp_d)
+    _remember(clusters, lab_d)
+    return out
+
+
+def downsample_point_cloud(points, factor=0.1):
+    """Replaces ``utils/data_processing.py:231-249``: identity for factor >= 1, else
+    ``points[np.random.choice(n, max(1, int(n*factor)), replace=False)]`` drawn from the
+    GLOBAL legacy NumPy RNG exactly as the reference does (the draw is host RNG state, not
+    arithmetic; the gather is a host index)."""
+    if factor >= 1.0:
+        return points
+    num = len(points)
+    keep = max(1, int(num * factor))
+    idx = np.random.choice(num, keep, replace=False)
+    return points[idx]
+
+
+# ------------------------------------------------------------- people / density (L2)
+def extract_people_positions(processed_data):
+    """Replaces ``utils/data_processing.py:251-280``: (K, 2) per-cluster centroids
+    (x, y) in ascending label order, ``np.array([])`` when there is no cluster."""
+    import torch
+    pts, lab = processed_data["points"], processed_data["clusters"]
+    n = len(pts)
+    if n == 0:
+        return np.array([])
+    x = _on_device(pts, torch.float64)
+    lbl = _on_device(lab, torch.int64)
+    people = torch.empty((n, 2), dtype=torch.float64, device=x.device)
+    k = nat.I64(0)
+    import ctypes
+    nat.call("lidar_people_f64", _handle(), nat.ptr(x), nat.ptr(lbl), n, nat.ptr(people), ctypes.byref(k),
+             nat.stream_ptr())
+    k = k.value
+    if k == 0:
+        return np.array([])
+    out = people[:k].cpu().numpy()
+    _remember(out, people[:k])
+    return out
+
+
+def _grid(people_positions, x_range, y_range, grid_size):
+    import ctypes
+    import torch
+    x_min, x_max = x_range
+    y_min, y_max = y_range
+    nx, ny = nat.I64(0), nat.I64(0)
+    nat.call("lidar_grid_dims", float(x_min), float(x_max), float(y_min), float(y_max), float(grid_size),
+             ctypes.byref(nx), ctypes.byref(ny))
+    nx, ny = nx.value, ny.value
+    p = _on_device(np.asarray(people_positions, dtype=np.float64).reshape(-1, 2), torch.float64)
+    dev = p.device
+    gx = torch.empty(nx, dtype=torch.float64, device=dev)
+    gy = torch.empty(ny, dtype=torch.float64, device=dev)
+    buf = torch.empty(3 * nx * ny + 13, dtype=torch.float64, device=dev)
+    nat.call("lidar_density_grid_f64", _handle(), nat.ptr(p), len(p), float(x_min), float(x_max),
+             float(y_min), float(y_max), float(grid_size), nx, ny, nat.ptr(gx), nat.ptr(gy), nat.ptr(buf),
+             nat.stream_ptr())
+    b = buf.cpu().numpy()
+    m = nx * ny
+    dens = b[:m].reshape(nx, ny)
+    stats = b[3 * m:3 * m + 8]
+    hot = b[3 * m + 8:3 * m + 13].view(np.int64)[: int(stats[3])]
+    return gx.cpu().numpy(), gy.cpu().numpy(), dens, b[m:2 * m], b[2 * m:3 * m], stats, hot
+
+
+def calculate_grid_density(people_positions, x_range, y_range, grid_size=1.0):
+    """Replaces ``utils/data_processing.py:282-328``: (grid_x, grid_y, density (nx, ny))
+    in people per square metre; ``(None, None, None)`` when there are no positions."""
+    if len(people_positions) == 0:
+        return None, None, None
+    gx, gy, dens, *_ = _grid(people_positions, x_range, y_range, grid_size)
+    return gx, gy, dens
+
+
+# ------------------------------------------------------------- north_star extensions
+def voxel_downsample(points, voxel_size):
+    """One point per occupied voxel (mean of its points, voxels in ascending key order)
+    plus the voxel id of every input point.  Returns (centroids (V, 3) float32,
+    voxel_id (N,) int32, counts (V,) int32).  SURVEY §8a N1 (no reference counterpart)."""
+    import ctypes
+    import torch
+    x = _on_device(np.asarray(points, dtype=np.float32).reshape(-1, 3), torch.float32)
+    n = len(x)
+    vid = torch.empty(n, dtype=torch.int32, device=x.device)
+    cent = torch.empty((max(n, 1), 3), dtype=torch.float32, device=x.device)
+    cnt = torch.empty(max(n, 1), dtype=torch.int32, device=x.device)
+    v = nat.I64(0)
+    nat.call("lidar_voxel_downsample_f32", _handle(), nat.ptr(x), n, float(voxel_size), nat.ptr(vid),
+             nat.ptr(cent), nat.ptr(cnt), ctypes.byref(v), nat.stream_ptr())
+    v = v.value
+    return cent[:v].cpu().numpy(), vid.cpu().numpy(), cnt[:v].cpu().numpy()
+
+
+def farthest_point_sample(points, npoint):
+    """Indices (npoint,) int32 of the farthest-point subset of an (N, 3) frame (start at
+    index 0, ties to the lowest index).  SURVEY §8a N2 (no reference counterpart)."""
+    import torch
+    from .pointnet2 import farthest_point_sample as fps
+    x = _on_device(np.asarray(points, dtype=np.float32).reshape(-1, 3), torch.float32)
+    return fps(x[None], int(npoint))[0].cpu().numpy()

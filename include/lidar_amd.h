@@ -55,10 +55,15 @@ int lidar_version(void);
 
 /* farthest-point sampling: idx (batch, npoint) int32; optionally new_xyz (batch, npoint, 3)
  * = xyz[idx] (pass NULL to skip).  Start index 0, fp32 no-FMA distances, lowest index on
- * ties.  Replaces: downsample_point_cloud's random subset (utils/data_processing.py:231-249)
- * where a spatially uniform subset is wanted. */
+ * ties.  Optional first_zero (batch) receives the first step whose winning distance was 0
+ * (npoint if none).  Optional prefix_ok (batch): when xyz are the first points of a parent
+ * FPS ordering, pass the parent's first_zero — frames with npoint <= prefix_ok[b] get the
+ * exact identity result without running (nested SA levels).  Replaces:
+ * downsample_point_cloud's random subset (utils/data_processing.py:231-249) where a
+ * spatially uniform subset is wanted. */
 int lidar_fps_f32(lidar_handle *h, const float *xyz, int64_t batch, int64_t n, int64_t npoint,
-                  int32_t *idx, float *new_xyz, void *stream);
+                  int32_t *idx, float *new_xyz, int32_t *first_zero, const int32_t *prefix_ok,
+                  void *stream);
 
 /* ball query: idx (batch, m, nsample) int32 — the first `nsample` point indices (ascending)
  * with d < radius^2, padded with the first hit, 0 when there is none.  Replaces the eps-ball

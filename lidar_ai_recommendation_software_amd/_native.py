@@ -41,7 +41,7 @@ SIGNATURES = {
     "lidar_reserve": [P, ctypes.c_uint64],
     "lidar_last_error": [],
     "lidar_version": [],
-    "lidar_fps_f32": [P, P, I64, I64, I64, P, P, P],
+    "lidar_fps_f32": [P, P, I64, I64, I64, P, P, P, P, P],
     "lidar_ball_query_f32": [P, P, P, I64, I64, I64, F32, I32, P, P],
     "lidar_sa_group_mlp_f32": [P, P, P, I64, P, P, I64, I64, I64, I32, I32, I32, I32, I32, P, P,
                                I64, I64, P],
@@ -94,8 +94,11 @@ def check(rc, what):
         raise LidarError(f"{what} failed ({rc}: {LIDAR_ERRORS.get(rc, '?')}): {msg}")
 
 
-def handle(device=None):
-    """The calling thread's handle for `device` (default: torch's current device)."""
+def handle(device=None, slot=0):
+    """The calling thread's handle for `device` (default: torch's current device).
+
+    `slot` selects an independent handle (own scratch workspace) for work that runs
+    concurrently on another stream — calls on one handle must not overlap."""
     import torch
     if not torch.cuda.is_available():
         raise NativeUnavailable("no GPU visible: the liblidar_amd HIP path needs a gfx950 device")
@@ -104,12 +107,13 @@ def handle(device=None):
     hs = getattr(_tls, "handles", None)
     if hs is None:
         hs = _tls.handles = {}
-    h = hs.get(device)
+    key = (device, slot)
+    h = hs.get(key)
     if h is None:
         lib = load_library()
         hp = P()
         check(lib.lidar_create(int(device), ctypes.byref(hp)), "lidar_create")
-        h = hs[device] = hp
+        h = hs[key] = hp
     return h
 
 

@@ -4,42 +4,75 @@
 // point indices in ascending order with d < r*r (fp32, d = (dx*dx+dy*dy)+dz*dz, one
 // rounding per op), unused slots repeat the first hit, no hit -> 0.
 //
-// One wavefront per centre scans the frame in index order, 64 points per step
-// (coalesced loads of consecutive points, L2/L1 resident across the centres of a
-// frame), __ballot collects the hits, popcount ranks them, and the scan stops as soon
-// as nsample hits are in — for uniform frames at r = 0.2 that is ~12 % of the frame.
+// One wavefront serves 8 centres of a frame: it scans the frame in index order, 64
+// points per step (one coalesced load), tests the chunk against all 8 centres (the
+// load is shared 8 ways), __ballot collects each centre's hits, popcount ranks them,
+// and the scan stops once every centre has nsample hits — for uniform frames at
+// r = 0.2 that is ~12 % of the frame.
 #include "common.hpp"
 
 namespace {
 
+constexpr int kC = 8;  // centres per wavefront: every loaded 64-point chunk is tested against all
+
 __global__ __launch_bounds__(256) void ball_query_kernel(const float *__restrict__ xyz,
                                                          const float *__restrict__ centres,
-                                                         int n, int m, int64_t total, float r2,
-                                                         int ns, int32_t *__restrict__ out)
+                                                         int n, int m, int64_t groups_per_frame,
+                                                         int64_t total_groups, float r2, int ns,
+                                                         int32_t *__restrict__ out)
 {
     const int lane = threadIdx.x & 63;
-    const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (c >= total) return;  // wave-uniform
-    const int64_t b = c / m;
+    const int64_t gw = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (gw >= total_groups) return;  // wave-uniform
+    const int64_t b = gw / groups_per_frame;
+    const int c0 = (int)(gw % groups_per_frame) * kC;
+    const int nc = min(kC, m - c0);
     const float *p = xyz + b * (int64_t)n * 3;
-    const float cx = centres[3 * c], cy = centres[3 * c + 1], cz = centres[3 * c + 2];
-    int32_t *o = out + c * ns;
+    float cx[kC], cy[kC], cz[kC];
+    int cnt[kC], first[kC];
+#pragma unroll
+    for (int j = 0; j < kC; ++j) {
+        const int64_t c = b * m + c0 + (j < nc ? j : 0);
+        cx[j] = centres[3 * c];
+        cy[j] = centres[3 * c + 1];
+        cz[j] = centres[3 * c + 2];
+        cnt[j] = j < nc ? 0 : ns;  // padding centres start "done"
+        first[j] = -1;
+    }
     const uint64_t below = (1ull << lane) - 1;
-    int cnt = 0, first = -1;
-    for (int base = 0; base < n && cnt < ns; base += 64) {
+    for (int base = 0; base < n; base += 64) {
+        bool open = false;
+#pragma unroll
+        for (int j = 0; j < kC; ++j) open |= cnt[j] < ns;
+        if (!open) break;  // wave-uniform
         const int k = base + lane;
-        bool hit = false;
-        if (k < n) hit = lidar::dist2f(p[3 * k], p[3 * k + 1], p[3 * k + 2], cx, cy, cz) < r2;
-        const uint64_t mask = __ballot(hit);
-        if (mask) {
-            if (first < 0) first = base + __ffsll((unsigned long long)mask) - 1;
-            const int rank = cnt + __popcll(mask & below);
-            if (hit && rank < ns) o[rank] = k;
-            cnt += __popcll(mask);
+        float px = 0.f, py = 0.f, pz = 0.f;
+        if (k < n) {
+            px = p[3 * k];
+            py = p[3 * k + 1];
+            pz = p[3 * k + 2];
+        }
+#pragma unroll
+        for (int j = 0; j < kC; ++j) {
+            if (cnt[j] >= ns) continue;  // wave-uniform
+            const bool hit = k < n && lidar::dist2f(px, py, pz, cx[j], cy[j], cz[j]) < r2;
+            const uint64_t mask = __ballot(hit);
+            if (mask) {
+                int32_t *o = out + (b * m + c0 + j) * (int64_t)ns;
+                if (first[j] < 0) first[j] = base + __ffsll((unsigned long long)mask) - 1;
+                const int rank = cnt[j] + __popcll(mask & below);
+                if (hit && rank < ns) o[rank] = k;
+                cnt[j] += __popcll(mask);
+            }
         }
     }
-    const int fill = first < 0 ? 0 : first;
-    for (int s = min(cnt, ns) + lane; s < ns; s += 64) o[s] = fill;
+#pragma unroll
+    for (int j = 0; j < kC; ++j) {
+        if (j >= nc) break;
+        int32_t *o = out + (b * m + c0 + j) * (int64_t)ns;
+        const int fill = first[j] < 0 ? 0 : first[j];
+        for (int s2 = min(cnt[j], ns) + lane; s2 < ns; s2 += 64) o[s2] = fill;
+    }
 }
 
 }  // namespace
@@ -56,10 +89,11 @@ LIDAR_EXPORT int lidar_ball_query_f32(lidar_handle *h, const float *xyz, const f
     if (total == 0) return LIDAR_OK;
     HIP_TRY(hipSetDevice(h->device));
     const float r2 = radius * radius;
-    const int64_t blocks = (total + 3) / 4;
+    const int64_t gpf = (m + kC - 1) / kC, groups = batch * gpf;
+    const int64_t blocks = (groups + 3) / 4;
     REQUIRE(blocks <= 0x7fffffff, "lidar_ball_query_f32: too many centres");
     hipLaunchKernelGGL(ball_query_kernel, dim3((unsigned)blocks), dim3(256), 0,
-                       static_cast<hipStream_t>(stream), xyz, centres, (int)n, (int)m, total, r2,
+                       static_cast<hipStream_t>(stream), xyz, centres, (int)n, (int)m, gpf, groups, r2,
                        (int)nsample, idx);
     LAUNCH_CHECK();
     return LIDAR_OK;

@@ -113,3 +113,48 @@ __device__ __forceinline__ float wave_min_f(float v)
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
 }  // namespace lidar
+
+// ----------------------------------------------------------------- DPP wave reductions
+// gfx9 DPP controls: quad_perm [1,0,3,2] = 0xB1, [2,3,0,1] = 0x4E, row_half_mirror 0x141,
+// row_mirror 0x140.  Four DPP steps reduce each 16-lane row; 4 readlanes finish the wave.
+// Far cheaper than __shfl_xor (ds_bpermute, ~50+ cycles per hop).
+namespace lidar {
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v)
+{
+    return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, true);
+}
+__device__ __forceinline__ float wave_max_dpp(float v)
+{
+    v = fmaxf(v, __int_as_float(dpp_i<0xB1>(__float_as_int(v))));
+    v = fmaxf(v, __int_as_float(dpp_i<0x4E>(__float_as_int(v))));
+    v = fmaxf(v, __int_as_float(dpp_i<0x141>(__float_as_int(v))));
+    v = fmaxf(v, __int_as_float(dpp_i<0x140>(__float_as_int(v))));
+    const float a = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+    const float b = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+    const float c = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+    const float d = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+    return fmaxf(fmaxf(a, b), fmaxf(c, d));
+}
+__device__ __forceinline__ uint32_t wave_min_u32_dpp(uint32_t v)
+{
+    v = min(v, (uint32_t)dpp_i<0xB1>((int)v));
+    v = min(v, (uint32_t)dpp_i<0x4E>((int)v));
+    v = min(v, (uint32_t)dpp_i<0x141>((int)v));
+    v = min(v, (uint32_t)dpp_i<0x140>((int)v));
+    const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)v, 0), b = (uint32_t)__builtin_amdgcn_readlane((int)v, 16);
+    const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)v, 32), d = (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
+    return min(min(a, b), min(c, d));
+}
+// lane holding the wave argmax of (d, -idx): max d, lowest idx among equal d.
+// Inactive lanes pass d = -1.  Returns the lane; *dmax = the max.
+__device__ __forceinline__ int wave_argmax_lane(float d, uint32_t idx, float *dmax)
+{
+    const float m = wave_max_dpp(d);
+    const uint64_t c = __ballot(d == m);
+    *dmax = m;
+    if (__popcll(c) == 1) return __ffsll((unsigned long long)c) - 1;
+    const uint32_t mi = wave_min_u32_dpp(d == m ? idx : 0xffffffffu);
+    return __ffsll((unsigned long long)__ballot(d == m && idx == mi)) - 1;
+}
+}  // namespace lidar

@@ -14,14 +14,22 @@
 // its current dist.  lb = dist-from-bbox(q) computed with the SAME rounded operations
 // as d is a lower bound of every member's d (fl() is monotone), so `lb >= bucket max`
 // proves no member changes and the bucket is skipped — an exact pruning, not an
-// approximation.  Active buckets are streamed (64 lanes = 64 points, coalesced SoA
-// loads, L2-resident), updated, and re-reduced; the frame argmax is a wave
-// __shfl_xor max over 64-bit keys (dist bits << 32 | ~index) and a 16-way LDS merge.
+// approximation.  Active buckets are streamed (64 lanes = 64 points, one coalesced float4
+// (x, y, z, dist) load each, up to 4 buckets' loads in flight together), updated, and
+// re-reduced with DPP argmax reductions (max dist, lowest index on ties); the frame argmax
+// is a DPP wave argmax of the per-lane bucket maxima and a 16-way LDS merge of
+// (dist bits << 32 | ~index) keys.
+//
+// Nested FPS (SA2 samples SA1's centroids): FPS over the first m points of an FPS ordering
+// is the identity 0..m-1 while the parent's winning distance stayed > 0 — the parent
+// run records the first step whose winning distance was 0 (`first_zero`), the child run
+// takes it as `prefix_ok` and copies the prefix when m <= prefix_ok.
 #include "common.hpp"
 
 namespace {
 
-constexpr int kThreads = 1024;
+constexpr int kThreads = 1024;  // 16 waves: active-bucket updates and their reductions run in
+                                // parallel across waves; the merge runs on wave 0 alone
 constexpr int kWaves = kThreads / 64;
 constexpr int kGrid = 16;  // Morton cells per axis for the bucket ordering
 constexpr int kCells = kGrid * kGrid * kGrid;
@@ -35,8 +43,8 @@ __device__ __forceinline__ uint32_t spread3(uint32_t v)  // 4 bits -> every thir
 }
 
 struct FrameWs {
-    float *x, *y, *z, *d;
-    uint32_t *idx;
+    float4 *p;      // sorted (x, y, z, dist)
+    uint32_t *idx;  // original index of each sorted point
 };
 
 __device__ __forceinline__ float gap(float q, float lo, float hi)
@@ -44,27 +52,125 @@ __device__ __forceinline__ float gap(float q, float lo, float hi)
     return q < lo ? __fsub_rn(lo, q) : (q > hi ? __fsub_rn(q, hi) : 0.0f);
 }
 
-template <int BPL>
+constexpr int kBatch = 4;  // active buckets whose loads are issued together
+constexpr int kLoopWaves = kThreads / 64;
+
+// Update K active buckets of one owner slot (their loads issued together, their DPP
+// reductions interleaved): new distances against q, bucket max + its lowest-index argmax
+// point into the owner lane's registers.
+template <int K>
+__device__ __forceinline__ void update_batch(uint64_t &mask, const FrameWs &W, int n, int wave, int q, int lane,
+                                             float qx, float qy, float qz, float &bd, uint32_t &bi, float *bx)
+{
+    int bbs[K], pos[K];
+    float4 P[K];
+    uint32_t I[K];
+#pragma unroll
+    for (int u = 0; u < K; ++u) {
+        bbs[u] = __ffsll((unsigned long long)mask) - 1;
+        mask &= mask - 1;
+        pos[u] = (wave + kLoopWaves * (q * 64 + bbs[u])) * 64 + lane;
+    }
+#pragma unroll
+    for (int u = 0; u < K; ++u) {
+        P[u] = make_float4(0.f, 0.f, 0.f, -1.0f);  // lanes past the end never win
+        I[u] = 0xffffffffu;
+        if (pos[u] < n) {
+            P[u] = W.p[pos[u]];
+            I[u] = W.idx[pos[u]];
+        }
+    }
+    float od[K], dm[K];
+#pragma unroll
+    for (int u = 0; u < K; ++u) {
+        od[u] = P[u].w;
+        if (pos[u] < n) {
+            const float d = lidar::dist2f(P[u].x, P[u].y, P[u].z, qx, qy, qz);
+            if (d < od[u]) {
+                W.p[pos[u]].w = d;
+                od[u] = d;
+            }
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < K; ++u) dm[u] = lidar::wave_max_dpp(od[u]);
+#pragma unroll
+    for (int u = 0; u < K; ++u) {
+        const uint64_t c = __ballot(od[u] == dm[u]);
+        int wl;
+        if (__popcll(c) == 1) {
+            wl = __ffsll((unsigned long long)c) - 1;
+        } else {
+            const uint32_t mi = lidar::wave_min_u32_dpp(od[u] == dm[u] ? I[u] : 0xffffffffu);
+            wl = __ffsll((unsigned long long)__ballot(od[u] == dm[u] && I[u] == mi)) - 1;
+        }
+        const uint32_t wi = (uint32_t)__builtin_amdgcn_readlane((int)I[u], wl);
+        const float wx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(P[u].x), wl));
+        const float wy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(P[u].y), wl));
+        const float wz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(P[u].z), wl));
+        if (lane == bbs[u]) {
+            bd = dm[u];
+            bi = wi;
+            bx[0] = wx;
+            bx[1] = wy;
+            bx[2] = wz;
+        }
+    }
+}
+
+__device__ __forceinline__ uint64_t stamp()
+{
+    uint64_t t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    return t;
+}
+
+// DIAG builds (lidar_diag_fps_phases only) accumulate per-phase shader cycles per wave:
+// [0] bucket tests + active-bucket updates, [1] wave argmax + LDS publish, [2] barrier
+// wait, [3] 16-way merge, [4] active-bucket batches processed, [5] steps
+template <int BPL, bool DIAG = false>
 __global__ __launch_bounds__(kThreads) void fps_bucket_kernel(const float *__restrict__ xyz,
                                                               int n, int npoint,
                                                               int32_t *__restrict__ out_idx,
                                                               float *__restrict__ out_xyz,
-                                                              float *__restrict__ ws, int64_t ws_stride)
+                                                              int32_t *__restrict__ first_zero,
+                                                              const int32_t *__restrict__ prefix_ok,
+                                                              float *__restrict__ ws, int64_t ws_stride,
+                                                              uint64_t *__restrict__ diag = nullptr)
 {
+    uint64_t dacc[6] = {0, 0, 0, 0, 0, 0};
+    uint64_t t0 = 0, t1 = 0;
     const int b = blockIdx.x;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
     const float *p = xyz + (int64_t)b * n * 3;
+
+    // nested FPS shortcut: FPS over the first m points of an FPS ordering returns 0..m-1
+    // as long as the parent's winning distance stayed > 0 — exact.
+    if (prefix_ok != nullptr && prefix_ok[b] >= npoint) {
+        for (int i = tid; i < npoint; i += kThreads) {
+            out_idx[(int64_t)b * npoint + i] = i;
+            if (out_xyz) {
+                float *o = out_xyz + ((int64_t)b * npoint + i) * 3;
+                o[0] = p[3 * i];
+                o[1] = p[3 * i + 1];
+                o[2] = p[3 * i + 2];
+            }
+        }
+        if (first_zero && tid == 0) first_zero[b] = prefix_ok[b];
+        return;
+    }
+
     float *wsb = ws + (int64_t)b * ws_stride;
-    FrameWs W{wsb, wsb + n, wsb + 2 * (int64_t)n, wsb + 3 * (int64_t)n,
-              reinterpret_cast<uint32_t *>(wsb + 4 * (int64_t)n)};
+    FrameWs W{reinterpret_cast<float4 *>(wsb), reinterpret_cast<uint32_t *>(wsb + 4 * (int64_t)n)};
 
     __shared__ uint32_t hist[kCells];
     __shared__ float red[6][kWaves];
     __shared__ uint32_t wsum[kWaves];
-    __shared__ uint64_t skey[2][kWaves];
-    __shared__ float sxyz[2][kWaves][3];
+    __shared__ float sd[kWaves], sx[kWaves], sy[kWaves], sz[kWaves];
+    __shared__ uint32_t si[kWaves];
+    __shared__ float qbuf[4];
 
     // ---- frame bounding box
     float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
@@ -115,9 +221,15 @@ __global__ __launch_bounds__(kThreads) void fps_bucket_kernel(const float *__res
     };
     for (int i = tid; i < n; i += kThreads) atomicAdd(&hist[cell_of(i)], 1u);
     __syncthreads();
-    {  // exclusive scan of 4096 counts, 4 per thread
-        uint32_t v0 = hist[4 * tid], v1 = hist[4 * tid + 1], v2 = hist[4 * tid + 2], v3 = hist[4 * tid + 3];
-        uint32_t s = v0 + v1 + v2 + v3, incl = s;
+    {  // exclusive scan of the cell counts, kCells / kThreads consecutive cells per thread
+        constexpr int per = kCells / kThreads;
+        uint32_t v[per], s = 0;
+#pragma unroll
+        for (int j = 0; j < per; ++j) {
+            v[j] = hist[per * tid + j];
+            s += v[j];
+        }
+        uint32_t incl = s;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
             uint32_t t = __shfl_up(incl, o, 64);
@@ -125,63 +237,66 @@ __global__ __launch_bounds__(kThreads) void fps_bucket_kernel(const float *__res
         }
         if (lane == 63) wsum[wave] = incl;
         __syncthreads();
-        uint32_t base = 0;
-        for (int w = 0; w < wave; ++w) base += wsum[w];
-        uint32_t e = base + incl - s;
-        hist[4 * tid] = e;
-        hist[4 * tid + 1] = e + v0;
-        hist[4 * tid + 2] = e + v0 + v1;
-        hist[4 * tid + 3] = e + v0 + v1 + v2;
+        uint32_t e = incl - s;
+        for (int w = 0; w < wave; ++w) e += wsum[w];
+#pragma unroll
+        for (int j = 0; j < per; ++j) {
+            hist[per * tid + j] = e;
+            e += v[j];
+        }
     }
     __syncthreads();
     for (int i = tid; i < n; i += kThreads) {
         uint32_t pos = atomicAdd(&hist[cell_of(i)], 1u);
-        W.x[pos] = p[3 * i];
-        W.y[pos] = p[3 * i + 1];
-        W.z[pos] = p[3 * i + 2];
-        W.d[pos] = INFINITY;
+        W.p[pos] = make_float4(p[3 * i], p[3 * i + 1], p[3 * i + 2], INFINITY);
         W.idx[pos] = (uint32_t)i;
     }
     __threadfence_block();
     __syncthreads();
 
-    // ---- per-bucket state in the owner lane: bucket = wave + 16 * (q * 64 + lane)
+    // ---- bucket bounding boxes: every wave reduces 64-point buckets into an LDS table
     const int nb = (n + 63) / 64;
-    float bmin[BPL][3], bmax[BPL][3], bx[BPL][3];
-    uint64_t bkey[BPL];
-#pragma unroll
-    for (int q = 0; q < BPL; ++q) {
+    extern __shared__ float bbox_tab[];  // [nb][6]
+    for (int bucket = wave; bucket < nb; bucket += kWaves) {
+        const int pos = bucket * 64 + lane;
+        float v[3] = {INFINITY, INFINITY, INFINITY}, u[3] = {-INFINITY, -INFINITY, -INFINITY};
+        if (pos < n) {
+            const float4 P = W.p[pos];
+            v[0] = u[0] = P.x;
+            v[1] = u[1] = P.y;
+            v[2] = u[2] = P.z;
+        }
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
-            bmin[q][a] = INFINITY;
-            bmax[q][a] = -INFINITY;
-            bx[q][a] = 0.0f;
+            v[a] = lidar::wave_min_f(v[a]);
+            u[a] = lidar::wave_max_f(u[a]);
         }
-        bkey[q] = 0;  // dist 0: never active, never the argmax
-        for (int bb = 0; bb < 64; ++bb) {
-            int bucket = wave + kWaves * (q * 64 + bb);
-            if (bucket >= nb) break;  // wave-uniform
-            int pos = bucket * 64 + lane;
-            float v[3] = {INFINITY, INFINITY, INFINITY}, u[3] = {-INFINITY, -INFINITY, -INFINITY};
-            if (pos < n) {
-                v[0] = u[0] = W.x[pos];
-                v[1] = u[1] = W.y[pos];
-                v[2] = u[2] = W.z[pos];
-            }
+        if (lane == 0) {
 #pragma unroll
             for (int a = 0; a < 3; ++a) {
-                v[a] = lidar::wave_min_f(v[a]);
-                u[a] = lidar::wave_max_f(u[a]);
-            }
-            if (lane == bb) {
-#pragma unroll
-                for (int a = 0; a < 3; ++a) {
-                    bmin[q][a] = v[a];
-                    bmax[q][a] = u[a];
-                }
-                bkey[q] = lidar::make_key(INFINITY, 0u);
+                bbox_tab[bucket * 6 + a] = v[a];
+                bbox_tab[bucket * 6 + 3 + a] = u[a];
             }
         }
+    }
+    __syncthreads();
+    static_assert(kWaves == kLoopWaves, "every wave runs the step loop");
+
+    // ---- per-bucket state in the owner lane: bucket = wave + 4 * (q * 64 + lane)
+    float bmin[BPL][3], bmax[BPL][3], bx[BPL][3], bd[BPL];
+    uint32_t bi[BPL];
+#pragma unroll
+    for (int q = 0; q < BPL; ++q) {
+        const int bucket = wave + kLoopWaves * (q * 64 + lane);
+        const bool have = bucket < nb;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            bmin[q][a] = have ? bbox_tab[bucket * 6 + a] : INFINITY;
+            bmax[q][a] = have ? bbox_tab[bucket * 6 + 3 + a] : -INFINITY;
+            bx[q][a] = 0.0f;
+        }
+        bd[q] = have ? INFINITY : 0.0f;  // empty slot: never active, never the argmax
+        bi[q] = have ? 0u : 0xffffffffu;
     }
 
     // ---- sample 0 is index 0
@@ -195,97 +310,136 @@ __global__ __launch_bounds__(kThreads) void fps_bucket_kernel(const float *__res
             o[2] = qz;
         }
     }
+    int zero_at = npoint;  // first step whose winning distance is 0
 
+    float w_d = 0.0f, w_x = 0.0f, w_y = 0.0f, w_z = 0.0f;  // this wave's current argmax
+    uint32_t w_i = 0xffffffffu;
     for (int it = 1; it < npoint; ++it) {
+        bool wave_dirty = it == 1;
+        if constexpr (DIAG) {
+            __builtin_amdgcn_sched_barrier(0);
+            t0 = stamp();
+            __builtin_amdgcn_sched_barrier(0);
+        }
 #pragma unroll
         for (int q = 0; q < BPL; ++q) {
-            float gx = gap(qx, bmin[q][0], bmax[q][0]);
-            float gy = gap(qy, bmin[q][1], bmax[q][1]);
-            float gz = gap(qz, bmin[q][2], bmax[q][2]);
-            float lb = __fadd_rn(__fadd_rn(__fmul_rn(gx, gx), __fmul_rn(gy, gy)), __fmul_rn(gz, gz));
-            bool active = lb < lidar::key_dist(bkey[q]);
-            uint64_t mask = __ballot(active);
-            while (mask) {
-                int bb = __ffsll((unsigned long long)mask) - 1;
-                mask &= mask - 1;
-                int bucket = wave + kWaves * (q * 64 + bb);
-                int pos = bucket * 64 + lane;
-                uint64_t key = 0;
-                float px = 0.f, py = 0.f, pz = 0.f;
-                if (pos < n) {
-                    px = W.x[pos];
-                    py = W.y[pos];
-                    pz = W.z[pos];
-                    float od = W.d[pos];
-                    float d = lidar::dist2f(px, py, pz, qx, qy, qz);
-                    if (d < od) {
-                        W.d[pos] = d;
-                        od = d;
-                    }
-                    key = lidar::make_key(od, W.idx[pos]);
-                }
-                uint64_t km = lidar::wave_max_u64(key);
-                int wl = __ffsll((unsigned long long)__ballot(key == km)) - 1;
-                float wx = __shfl(px, wl, 64), wy = __shfl(py, wl, 64), wz = __shfl(pz, wl, 64);
-                if (lane == bb) {
-                    bkey[q] = km;
-                    bx[q][0] = wx;
-                    bx[q][1] = wy;
-                    bx[q][2] = wz;
-                }
+            const float gx = gap(qx, bmin[q][0], bmax[q][0]);
+            const float gy = gap(qy, bmin[q][1], bmax[q][1]);
+            const float gz = gap(qz, bmin[q][2], bmax[q][2]);
+            const float lb = __fadd_rn(__fadd_rn(__fmul_rn(gx, gx), __fmul_rn(gy, gy)), __fmul_rn(gz, gz));
+            uint64_t mask = __ballot(lb < bd[q]);
+            wave_dirty = wave_dirty || mask != 0;
+            while (mask) {  // wave-uniform
+                if constexpr (DIAG) dacc[4]++;
+                const int cnt = __popcll(mask);
+                if (cnt >= 4)
+                    update_batch<4>(mask, W, n, wave, q, lane, qx, qy, qz, bd[q], bi[q], bx[q]);
+                else if (cnt >= 2)
+                    update_batch<2>(mask, W, n, wave, q, lane, qx, qy, qz, bd[q], bi[q], bx[q]);
+                else
+                    update_batch<1>(mask, W, n, wave, q, lane, qx, qy, qz, bd[q], bi[q], bx[q]);
             }
         }
-        // frame argmax over bucket keys
-        uint64_t best = bkey[0];
-        float cx = bx[0][0], cy = bx[0][1], cz = bx[0][2];
+        if constexpr (DIAG) {
+            __builtin_amdgcn_sched_barrier(0);
+            t1 = stamp();
+            dacc[0] += t1 - t0;
+            t0 = t1;
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        // frame argmax: lane best over its buckets -> wave argmax (DPP, only when one of the
+        // wave's buckets changed) -> LDS slots -> wave 0 merges -> q broadcast through LDS
+        if (wave_dirty) {
+            float best = bd[0];
+            uint32_t besti = bi[0];
+            float cx = bx[0][0], cy = bx[0][1], cz = bx[0][2];
 #pragma unroll
-        for (int q = 1; q < BPL; ++q) {
-            if (bkey[q] > best) {
-                best = bkey[q];
-                cx = bx[q][0];
-                cy = bx[q][1];
-                cz = bx[q][2];
+            for (int q = 1; q < BPL; ++q) {
+                if (bd[q] > best || (bd[q] == best && bi[q] < besti)) {
+                    best = bd[q];
+                    besti = bi[q];
+                    cx = bx[q][0];
+                    cy = bx[q][1];
+                    cz = bx[q][2];
+                }
+            }
+            const int wl = lidar::wave_argmax_lane(best, besti, &w_d);
+            w_i = (uint32_t)__builtin_amdgcn_readlane((int)besti, wl);
+            w_x = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cx), wl));
+            w_y = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cy), wl));
+            w_z = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cz), wl));
+            if (lane == 0) {
+                sd[wave] = w_d;
+                si[wave] = w_i;
+                sx[wave] = w_x;
+                sy[wave] = w_y;
+                sz[wave] = w_z;
             }
         }
-        uint64_t wm = lidar::wave_max_u64(best);
-        const int par = it & 1;
-        const int first = __ffsll((unsigned long long)__ballot(best == wm)) - 1;
-        if (lane == first) {
-            skey[par][wave] = wm;
-            sxyz[par][wave][0] = cx;
-            sxyz[par][wave][1] = cy;
-            sxyz[par][wave][2] = cz;
+        if constexpr (DIAG) {
+            __builtin_amdgcn_sched_barrier(0);
+            t1 = stamp();
+            dacc[1] += t1 - t0;
+            t0 = t1;
+            __builtin_amdgcn_sched_barrier(0);
         }
         __syncthreads();
-        uint64_t g = skey[par][0];
-        int gw = 0;
-#pragma unroll
-        for (int w = 1; w < kWaves; ++w) {
-            uint64_t k = skey[par][w];
-            if (k > g) {
-                g = k;
-                gw = w;
-            }
+        if constexpr (DIAG) {
+            __builtin_amdgcn_sched_barrier(0);
+            t1 = stamp();
+            dacc[2] += t1 - t0;
+            t0 = t1;
+            __builtin_amdgcn_sched_barrier(0);
         }
-        qx = sxyz[par][gw][0];
-        qy = sxyz[par][gw][1];
-        qz = sxyz[par][gw][2];
-        if (tid == 0) {
-            out_idx[(int64_t)b * npoint + it] = (int32_t)lidar::key_index(g);
-            if (out_xyz) {
-                float *o = out_xyz + ((int64_t)b * npoint + it) * 3;
-                o[0] = qx;
-                o[1] = qy;
-                o[2] = qz;
+        if (wave == 0) {
+            const bool slot = lane < kWaves;
+            const float md = slot ? sd[lane] : -1.0f;
+            const uint32_t mi = slot ? si[lane] : 0xffffffffu;
+            const float mx = slot ? sx[lane] : 0.0f, my = slot ? sy[lane] : 0.0f, mz = slot ? sz[lane] : 0.0f;
+            float gdist;
+            const int gl = lidar::wave_argmax_lane(md, mi, &gdist);
+            const uint32_t gidx = (uint32_t)__builtin_amdgcn_readlane((int)mi, gl);
+            const float gx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mx), gl));
+            const float gy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my), gl));
+            const float gz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mz), gl));
+            if (lane == 0) {
+                qbuf[0] = gx;
+                qbuf[1] = gy;
+                qbuf[2] = gz;
+                out_idx[(int64_t)b * npoint + it] = (int32_t)gidx;
+                if (out_xyz) {
+                    float *o = out_xyz + ((int64_t)b * npoint + it) * 3;
+                    o[0] = gx;
+                    o[1] = gy;
+                    o[2] = gz;
+                }
             }
+            if (zero_at == npoint && gdist == 0.0f) zero_at = it;
         }
+        __syncthreads();
+        qx = qbuf[0];
+        qy = qbuf[1];
+        qz = qbuf[2];
+        if constexpr (DIAG) {
+            __builtin_amdgcn_sched_barrier(0);
+            t1 = stamp();
+            dacc[3] += t1 - t0;
+            dacc[5]++;
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    if (first_zero && tid == 0) first_zero[b] = zero_at;
+    if constexpr (DIAG) {
+        if (lane == 0)
+            for (int k = 0; k < 6; ++k) diag[((int64_t)b * kWaves + wave) * 6 + k] = dacc[k];
     }
 }
 
 }  // namespace
 
 LIDAR_EXPORT int lidar_fps_f32(lidar_handle *h, const float *xyz, int64_t batch, int64_t n,
-                               int64_t npoint, int32_t *idx, float *new_xyz, void *stream)
+                               int64_t npoint, int32_t *idx, float *new_xyz, int32_t *first_zero,
+                               const int32_t *prefix_ok, void *stream)
 {
     REQUIRE(h && xyz && idx, "lidar_fps_f32: null pointer");
     REQUIRE(batch >= 0 && n >= 1 && npoint >= 1, "lidar_fps_f32: need n >= 1 and npoint >= 1");
@@ -293,21 +447,47 @@ LIDAR_EXPORT int lidar_fps_f32(lidar_handle *h, const float *xyz, int64_t batch,
     REQUIRE(batch <= 0x7fffffff, "lidar_fps_f32: batch too large");
     if (batch == 0) return LIDAR_OK;
     HIP_TRY(hipSetDevice(h->device));
+    REQUIRE(prefix_ok == nullptr || npoint <= n, "lidar_fps_f32: prefix_ok needs npoint <= n");
     int64_t stride = lidar::align_up(5 * n, 64);
     float *ws = static_cast<float *>(lidar::workspace(h, (uint64_t)(batch * stride) * 4));
     if (!ws) return LIDAR_ENOMEM;
     hipStream_t s = static_cast<hipStream_t>(stream);
     dim3 grid((unsigned)batch), block(kThreads);
-    int nb = (int)((n + 63) / 64);
-    if (nb <= 1024)
-        hipLaunchKernelGGL(fps_bucket_kernel<1>, grid, block, 0, s, xyz, (int)n, (int)npoint, idx,
-                           new_xyz, ws, stride);
-    else if (nb <= 2048)
-        hipLaunchKernelGGL(fps_bucket_kernel<2>, grid, block, 0, s, xyz, (int)n, (int)npoint, idx,
-                           new_xyz, ws, stride);
-    else
-        hipLaunchKernelGGL(fps_bucket_kernel<4>, grid, block, 0, s, xyz, (int)n, (int)npoint, idx,
-                           new_xyz, ws, stride);
+    const int nb = (int)((n + 63) / 64);
+    const size_t lds = (size_t)nb * 6 * sizeof(float);
+    const int lanes = kLoopWaves * 64;
+    auto go = [&](auto kern) -> int {
+        HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        hipLaunchKernelGGL(kern, grid, block, lds, s, xyz, (int)n, (int)npoint, idx, new_xyz, first_zero,
+                           prefix_ok, ws, stride, nullptr);
+        return LIDAR_OK;
+    };
+    int rc;
+    if (nb <= lanes) rc = go(fps_bucket_kernel<1>);
+    else if (nb <= 2 * lanes) rc = go(fps_bucket_kernel<2>);
+    else rc = go(fps_bucket_kernel<4>);  // n <= 262144 is checked above
+    if (rc) return rc;
+    LAUNCH_CHECK();
+    return LIDAR_OK;
+}
+
+// diagnostic build (not part of the product ABI): per-wave phase cycle totals of one FPS run
+LIDAR_EXPORT int lidar_diag_fps_phases(lidar_handle *h, const float *xyz, int64_t batch, int64_t n,
+                                       int64_t npoint, int32_t *idx, uint64_t *diag, void *stream)
+{
+    REQUIRE(h && xyz && idx && diag && n <= 65536 && n >= 1 && npoint >= 1, "lidar_diag_fps_phases: bad args");
+    HIP_TRY(hipSetDevice(h->device));
+    int64_t stride = lidar::align_up(5 * n, 64);
+    float *ws = static_cast<float *>(lidar::workspace(h, (uint64_t)(batch * stride) * 4));
+    if (!ws) return LIDAR_ENOMEM;
+    const size_t lds = (size_t)((n + 63) / 64) * 6 * sizeof(float);
+    REQUIRE((n + 63) / 64 <= kLoopWaves * 64, "lidar_diag_fps_phases: n too large for BPL=1");
+    HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(fps_bucket_kernel<1, true>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL((fps_bucket_kernel<1, true>), dim3((unsigned)batch), dim3(kThreads), lds,
+                       static_cast<hipStream_t>(stream), xyz, (int)n, (int)npoint, idx, nullptr, nullptr,
+                       nullptr, ws, stride, diag);
     LAUNCH_CHECK();
     return LIDAR_OK;
 }

@@ -89,26 +89,34 @@ def _dev_check(*ts):
             raise ValueError("liblidar_amd operators take contiguous CUDA tensors")
 
 
-def farthest_point_sample(xyz, npoint, return_xyz=False):
-    """xyz (B, N, 3) float32 CUDA -> idx (B, npoint) int32 [, new_xyz (B, npoint, 3)]."""
-    _dev_check(xyz)
+def farthest_point_sample(xyz, npoint, return_xyz=False, first_zero=None, prefix_ok=None, slot=0,
+                          out_idx=None, out_xyz=None):
+    """xyz (B, N, 3) float32 CUDA -> idx (B, npoint) int32 [, new_xyz (B, npoint, 3)].
+
+    first_zero: optional (B,) int32 output — first step whose winning distance was 0.
+    prefix_ok: optional (B,) int32 — the parent run's first_zero when xyz is the parent's
+    FPS-ordered sample set (nested SA levels): the exact identity result is copied."""
+    _dev_check(xyz, first_zero, prefix_ok)
     if xyz.dtype != torch.float32 or xyz.dim() != 3 or xyz.shape[2] != 3:
         raise ValueError("xyz must be (B, N, 3) float32")
     B, N, _ = xyz.shape
-    idx = torch.empty((B, npoint), dtype=torch.int32, device=xyz.device)
-    new_xyz = torch.empty((B, npoint, 3), dtype=torch.float32, device=xyz.device) if return_xyz else None
-    nat.call("lidar_fps_f32", nat.handle(xyz.device.index), nat.ptr(xyz), B, N, npoint,
-             nat.ptr(idx), nat.ptr(new_xyz), nat.stream_ptr())
+    idx = out_idx if out_idx is not None else torch.empty((B, npoint), dtype=torch.int32, device=xyz.device)
+    new_xyz = None
+    if return_xyz:
+        new_xyz = out_xyz if out_xyz is not None else torch.empty((B, npoint, 3), dtype=torch.float32,
+                                                                  device=xyz.device)
+    nat.call("lidar_fps_f32", nat.handle(xyz.device.index, slot), nat.ptr(xyz), B, N, npoint,
+             nat.ptr(idx), nat.ptr(new_xyz), nat.ptr(first_zero), nat.ptr(prefix_ok), nat.stream_ptr())
     return (idx, new_xyz) if return_xyz else idx
 
 
-def ball_query(radius, nsample, xyz, new_xyz):
+def ball_query(radius, nsample, xyz, new_xyz, out=None, slot=0):
     """-> idx (B, M, nsample) int32 (pointnet2 argument order)."""
-    _dev_check(xyz, new_xyz)
+    _dev_check(xyz, new_xyz, out)
     B, N, _ = xyz.shape
     M = new_xyz.shape[1]
-    idx = torch.empty((B, M, nsample), dtype=torch.int32, device=xyz.device)
-    nat.call("lidar_ball_query_f32", nat.handle(xyz.device.index), nat.ptr(xyz), nat.ptr(new_xyz),
+    idx = out if out is not None else torch.empty((B, M, nsample), dtype=torch.int32, device=xyz.device)
+    nat.call("lidar_ball_query_f32", nat.handle(xyz.device.index, slot), nat.ptr(xyz), nat.ptr(new_xyz),
              B, N, M, float(radius), int(nsample), nat.ptr(idx), nat.stream_ptr())
     return idx
 
@@ -154,6 +162,29 @@ def dense_relu(x, w, b, pool_rows=0, out=None):
 
 
 # ----------------------------------------------------------------------- backbone
+class _Timers:
+    """Optional per-launch HIP-event timing on the launching stream (bench.py)."""
+
+    def __init__(self):
+        self.ev = {}
+
+    def __call__(self, name, fn, *a, **k):
+        s = torch.cuda.current_stream()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        out = fn(*a, **k)
+        e1.record(s)
+        self.ev.setdefault(name, []).append((e0, e1))
+        return out
+
+    def mean_ms(self):
+        return {k: sum(a.elapsed_time(b) for a, b in v) / len(v) for k, v in self.ev.items()}
+
+
+def _call(timers, name, fn, *a, **k):
+    return timers(name, fn, *a, **k) if timers is not None else fn(*a, **k)
+
+
 class PointNet2Backbone:
     """SSG / MSG PointNet++ encoder on liblidar_amd.  ``forward(xyz)`` -> global feature
     (B, C_last) plus the per-level (new_xyz, features, fps_idx)."""
@@ -184,26 +215,43 @@ class PointNet2Backbone:
                 self.levels.append({"div": lvl["npoint_div"], "branches": branches, "cfeat": cfeat})
                 cfeat = sum(w[-1] for w in lvl["mlps"])
         self.out_channels = cfeat
+        self.timers = None  # set to a _Timers() to time every launch
 
-    def forward(self, xyz, keep_levels=False):
+    def forward_from_sa1_fps(self, xyz, idx1, new_xyz1, fz1, gidx1=None):
+        """forward() with level 0's FPS (and ball queries) already computed (StreamingSSG)."""
+        return self.forward(xyz, pre_fps=(idx1, new_xyz1, fz1), pre_bq=gidx1)[0]
+
+    def forward(self, xyz, keep_levels=False, pre_fps=None, pre_bq=None):
         B, N, _ = xyz.shape
         N0 = N  # npoint_div is relative to the input frame (N/16, N/64)
         feats = None
         out_levels = []
+        fz = None  # previous level's FPS first_zero (nested-FPS shortcut)
         for li, lvl in enumerate(self.levels):
             if lvl.get("group_all"):
                 return self._group_all(xyz, feats, lvl), out_levels
             M = max(1, N0 // lvl["div"])
-            idx, new_xyz = farthest_point_sample(xyz, M, return_xyz=True)
+            if li == 0 and pre_fps is not None:
+                idx, new_xyz, nfz = pre_fps
+            else:
+                nfz = torch.empty(B, dtype=torch.int32, device=xyz.device)
+                idx, new_xyz = _call(self.timers, f"sa{li + 1}_fps", farthest_point_sample, xyz, M,
+                                     return_xyz=True, first_zero=nfz, prefix_ok=fz)
+            fz = nfz
             ctot = sum(br["widths"][-1] for br in lvl["branches"])
             nxt = self.levels[li + 1] if li + 1 < len(self.levels) else None
             # the level feeding group_all writes straight into its padded input rows
             stride = nxt["k"] if nxt is not None and nxt.get("group_all") else ctot
             out = torch.empty((B, M, stride), dtype=torch.float32, device=xyz.device)
             off = 0
-            for br in lvl["branches"]:
-                gidx = ball_query(br["r"], br["ns"], xyz, new_xyz)
-                group_mlp(xyz, feats, new_xyz, gidx, br["packed"], br["widths"], out=out, out_offset=off)
+            for bi_, br in enumerate(lvl["branches"]):
+                tag = f"sa{li + 1}" + (f"_b{bi_}" if len(lvl["branches"]) > 1 else "")
+                if li == 0 and pre_bq is not None:
+                    gidx = pre_bq[bi_]
+                else:
+                    gidx = _call(self.timers, f"{tag}_ball_query", ball_query, br["r"], br["ns"], xyz, new_xyz)
+                _call(self.timers, f"{tag}_group_mlp", group_mlp, xyz, feats, new_xyz, gidx, br["packed"],
+                      br["widths"], out=out, out_offset=off)
                 off += br["widths"][-1]
             if keep_levels:
                 out_levels.append((new_xyz, out[..., :ctot], idx))
@@ -228,8 +276,80 @@ class PointNet2Backbone:
                              torch.zeros(mp - M, dtype=torch.long, device=x.device)])
             x2 = x.view(B, M, kp)[:, sel].reshape(B * mp, kp).contiguous()
             M, rows = mp, B * mp
-        h1 = dense_relu(x2, lvl["w"][0], lvl["b"][0])
-        h2 = dense_relu(h1, lvl["w"][1], lvl["b"][1])
-        return dense_relu(h2, lvl["w"][2], lvl["b"][2], pool_rows=M)
+        t = self.timers
+        h1 = _call(t, "sa3_dense1", dense_relu, x2, lvl["w"][0], lvl["b"][0])
+        h2 = _call(t, "sa3_dense2", dense_relu, h1, lvl["w"][1], lvl["b"][1])
+        out = torch.zeros((rows // M, lvl["w"][2].shape[1]), dtype=torch.float32, device=x.device)
+        return _call(t, "sa3_dense3_pool", dense_relu, h2, lvl["w"][2], lvl["b"][2], pool_rows=M, out=out)
 
     __call__ = forward
+
+
+# ------------------------------------------------------------------ streaming executor
+class StreamingSSG:
+    """Frame-batch pipeline for a continuous feed (SSG/MSG backbone).
+
+    SA1's farthest-point sampling is a serial chain of N/16 argmax steps per frame
+    (latency-bound, one workgroup per frame), while everything after it (ball queries,
+    fused MFMA MLPs, SA2's nested FPS, group_all) fills the whole GPU.  `run` therefore
+    issues batch k+1's SA1 FPS on its own stream (own library handle / workspace) while
+    batch k's remaining levels run on the main stream; events order the hand-off and a
+    ring of `depth + 1` FPS output slots bounds memory.  Results are identical to
+    ``PointNet2Backbone.forward`` (same kernels, same inputs).
+    """
+
+    def __init__(self, backbone, batch, n, depth=1):
+        self.bb = backbone
+        self.B, self.N, self.depth = batch, n, depth
+        dev = backbone.device
+        lvl0 = backbone.levels[0]
+        self.M1 = max(1, n // lvl0["div"])
+        self.fps_streams = [torch.cuda.Stream(device=dev) for _ in range(depth)]
+        nslot = depth + 1
+        self.idx = [torch.empty((batch, self.M1), dtype=torch.int32, device=dev) for _ in range(nslot)]
+        self.cxyz = [torch.empty((batch, self.M1, 3), dtype=torch.float32, device=dev) for _ in range(nslot)]
+        self.fz = [torch.empty(batch, dtype=torch.int32, device=dev) for _ in range(nslot)]
+        # level-0 ball queries of every branch ride on the FPS stream too
+        self.gidx = [[torch.empty((batch, self.M1, br["ns"]), dtype=torch.int32, device=dev)
+                      for br in lvl0["branches"]] for _ in range(nslot)]
+        self.fps_done = [torch.cuda.Event() for _ in range(nslot)]
+        self.slot_free = [torch.cuda.Event() for _ in range(nslot)]
+        for e in self.slot_free:
+            e.record(torch.cuda.current_stream(dev))
+
+    def _fps(self, k, x):
+        slot = k % (self.depth + 1)
+        fs = self.fps_streams[k % self.depth]
+        fs.wait_event(self.slot_free[slot])
+        with torch.cuda.stream(fs):
+            _call(self.bb.timers, "sa1_fps", farthest_point_sample, x, self.M1, return_xyz=True,
+                  first_zero=self.fz[slot], slot=1 + k % self.depth, out_idx=self.idx[slot],
+                  out_xyz=self.cxyz[slot])
+            lvl0 = self.bb.levels[0]
+            for bi_, br in enumerate(lvl0["branches"]):
+                tag = "sa1" + (f"_b{bi_}" if len(lvl0["branches"]) > 1 else "")
+                _call(self.bb.timers, f"{tag}_ball_query", ball_query, br["r"], br["ns"], x, self.cxyz[slot],
+                      out=self.gidx[slot][bi_], slot=1 + k % self.depth)
+            self.fps_done[slot].record(fs)
+        return slot
+
+    def _rest(self, slot, x, main):
+        main.wait_event(self.fps_done[slot])
+        out = self.bb.forward_from_sa1_fps(x, self.idx[slot], self.cxyz[slot], self.fz[slot], self.gidx[slot])
+        self.slot_free[slot].record(main)
+        return out
+
+    def run(self, inputs):
+        """inputs: list of (B, N, 3) CUDA tensors -> list of global features (B, C)."""
+        main = torch.cuda.current_stream(self.bb.device)
+        outs = []
+        pending = []
+        for k, x in enumerate(inputs):
+            pending.append((self._fps(k, x), x))
+            if len(pending) > self.depth:
+                slot, px = pending.pop(0)
+                outs.append(self._rest(slot, px, main))
+        while pending:
+            slot, px = pending.pop(0)
+            outs.append(self._rest(slot, px, main))
+        return outs

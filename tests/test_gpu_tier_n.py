@@ -120,3 +120,37 @@ def test_backbone_vs_oracle(cuda, cfg_name, n):
         assert np.array_equal(nx.cpu().numpy()[0], ox)
         feat_close(nf.cpu().numpy()[0], of, f"level {li} features")
     feat_close(g.cpu().numpy()[0], want, "global feature")
+
+
+@pytest.mark.parametrize("kind", ["uniform", "dups", "grid"])
+def test_nested_fps_prefix_shortcut(cuda, kind):
+    # SA2 samples SA1's FPS-ordered centroids: the child run may copy the prefix only
+    # while the parent's winning distance stayed > 0; otherwise it must run for real
+    n, m1, m2 = 4096, 1024, 256
+    x = frames_for(kind, 2, n, 3)
+    if kind == "dups":
+        x[:, 64:] = x[:, :64].repeat(n // 64 - 1, axis=1)[:, : n - 64]  # only 64 distinct points
+    xt = torch.from_numpy(x).to(cuda)
+    fz = torch.empty(2, dtype=torch.int32, device=cuda)
+    i1, c1 = pn.farthest_point_sample(xt, m1, return_xyz=True, first_zero=fz)
+    i2, c2 = pn.farthest_point_sample(c1, m2, return_xyz=True, prefix_ok=fz)
+    for b in range(2):
+        w1 = tier_n.fps(x[b], m1)
+        assert np.array_equal(i1.cpu().numpy()[b], w1)
+        cx = x[b][w1]
+        w2 = tier_n.fps(cx, m2)
+        assert np.array_equal(i2.cpu().numpy()[b], w2), kind
+        assert np.array_equal(c2.cpu().numpy()[b], cx[w2])
+    if kind == "dups":
+        assert (fz.cpu().numpy() == 64).all()
+
+
+@pytest.mark.parametrize("depth", [1, 2])
+def test_streaming_executor_matches_forward(cuda, depth):
+    bb = pn.PointNet2Backbone(pn.SSG, device=cuda, seed=1)
+    xs = [torch.from_numpy(unit_frames(3, 8192, s)).to(cuda) for s in range(4)]
+    want = [bb.forward(x)[0] for x in xs]
+    got = pn.StreamingSSG(bb, 3, 8192, depth=depth).run(xs)
+    torch.cuda.synchronize()
+    for a, b in zip(got, want):
+        assert torch.equal(a, b)

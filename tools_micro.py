@@ -1,0 +1,100 @@
+"""Micro-benchmarks of single kernels (GPU box): python tools_micro.py [fps|mlp|bq]."""
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, ".")
+from lidar_ai_recommendation_software_amd import pointnet2 as pn  # noqa: E402
+from lidar_ai_recommendation_software_amd.synthetic import unit_frames  # noqa: E402
+
+
+def timeit(fn, reps=5):
+    fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        fn()
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    return float(np.median(ts))
+
+
+def main():
+    what = sys.argv[1:] or ["fps", "mlp", "bq"]
+    dev = torch.device("cuda:0")
+    for B, N in ((32, 65536), (1, 65536), (256, 65536)):
+        x = torch.from_numpy(unit_frames(B, N, 0)).to(dev)
+        if "fps" in what:
+            M = N // 16
+            ms = timeit(lambda: pn.farthest_point_sample(x, M, return_xyz=True))
+            print(f"fps B={B} N={N} M={M}: {ms:.3f} ms  ({ms * 1e3 / M:.2f} us/step)", flush=True)
+            if B == 32:
+                c = pn.farthest_point_sample(x, M, return_xyz=True)[1]
+                ms2 = timeit(lambda: pn.farthest_point_sample(c, N // 64, return_xyz=True))
+                print(f"fps2 (no shortcut) B={B} N={M} M={N // 64}: {ms2:.3f} ms", flush=True)
+        if "bq" in what and B == 32:
+            c = x[:, : N // 16].contiguous()
+            ms = timeit(lambda: pn.ball_query(0.2, 32, x, c))
+            print(f"ball_query B={B} N={N} M={N // 16} r0.2 ns32: {ms:.3f} ms", flush=True)
+
+
+if __name__ == "__main__" and not ({"phases", "mlp"} & set(sys.argv)):
+    main()
+
+
+def fps_phases():
+    import ctypes
+    from lidar_ai_recommendation_software_amd import _native as nat
+    lib = nat.load_library()
+    lib.lidar_diag_fps_phases.argtypes = [nat.P, nat.P, nat.I64, nat.I64, nat.I64, nat.P, nat.P, nat.P]
+    dev = torch.device("cuda:0")
+    for B in (1, 32):
+        N, M = 65536, 4096
+        x = torch.from_numpy(unit_frames(B, N, 0)).to(dev)
+        idx = torch.empty((B, M), dtype=torch.int32, device=dev)
+        diag = torch.zeros((B, 16, 6), dtype=torch.int64, device=dev)
+        for _ in range(2):
+            nat.check(lib.lidar_diag_fps_phases(nat.handle(0), nat.ptr(x), B, N, M, nat.ptr(idx), nat.ptr(diag),
+                                                nat.stream_ptr()), "diag")
+        torch.cuda.synchronize()
+        d = diag.cpu().numpy().astype(np.float64)
+        steps = d[..., 5].mean()
+        per = d[..., :4].mean(axis=(0, 1)) / steps
+        print(f"B={B}: cycles/step  update={per[0]:.0f} wave-argmax={per[1]:.0f} barrier={per[2]:.0f} "
+              f"merge={per[3]:.0f}  batches/step/wave={d[..., 4].mean() / steps:.2f} "
+              f"(max wave {d[..., 4].max(axis=1).mean() / steps:.2f})", flush=True)
+
+
+if __name__ == "__main__" and "phases" in sys.argv:
+    fps_phases()
+
+
+def mlp_micro():
+    from lidar_ai_recommendation_software_amd import pointnet2 as pn
+    dev = torch.device("cuda:0")
+    rng = np.random.default_rng(0)
+    w = pn.init_weights(pn.SSG, 0)
+    B = 32
+    for name, (N, M, ns, cf, layers, widths) in {
+            "sa1": (65536, 4096, 32, 0, w[0][0], [64, 64, 128]),
+            "sa2": (4096, 1024, 64, 128, w[1][0], [128, 128, 256])}.items():
+        x = torch.from_numpy(unit_frames(B, N, 1)).to(dev)
+        f = torch.from_numpy(rng.standard_normal((B, N, cf)).astype(np.float32)).to(dev) if cf else None
+        c = x[:, :M].contiguous()
+        gi = torch.from_numpy(rng.integers(0, N, (B, M, ns)).astype(np.int32)).to(dev)
+        packed = torch.from_numpy(pn.pack_branch(layers, cf)).to(dev)
+        out = torch.empty((B, M, widths[-1]), dtype=torch.float32, device=dev)
+        ms = timeit(lambda: pn.group_mlp(x, f, c, gi, packed, widths, out=out), reps=10)
+        dims = [3 + cf] + widths
+        flops = 2 * B * M * ns * sum(a * b for a, b in zip(dims[:-1], dims[1:]))
+        print(f"{name} group_mlp: {ms:.3f} ms  {flops / ms / 1e9:.1f} TFLOP/s ({flops / ms / 1e9 / 157.3 * 100:.1f}% of fp32 peak)",
+              flush=True)
+
+
+if __name__ == "__main__" and "mlp" in sys.argv:
+    mlp_micro()

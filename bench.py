@@ -95,6 +95,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--depth", type=int, default=3, help="SA1-FPS batches in flight ahead of the MLPs")
+    ap.add_argument("--no-extras", action="store_true", help="skip the configs[1]/[4] side measurements")
     args = ap.parse_args()
 
     import torch
@@ -112,35 +113,46 @@ def main():
     torch.cuda.set_device(dev)
 
     B, N = args.batch, args.points
-    bb = pn.PointNet2Backbone(pn.SSG, device=dev, seed=0)
-    x = torch.from_numpy(unit_frames(B, N, seed=rank)).to(dev)
 
-    # the streaming executor overlaps batch k+1's SA1 FPS (latency-bound, one workgroup per
-    # frame) with batch k's MFMA levels; results are identical to the plain forward
-    pipe = pn.StreamingSSG(bb, B, N, depth=args.depth)
-    ref, _ = bb.forward(x)
-    outs = pipe.run([x] * max(2, args.warmup))
-    torch.cuda.synchronize(dev)
-    assert all(torch.equal(ref, o) for o in outs), "streaming executor diverged from forward()"
+    def measure(cfg, dtype, B, N, steps, warmup, depth):
+        bb = pn.PointNet2Backbone(cfg, device=dev, seed=0, dtype=dtype)
+        x = torch.from_numpy(unit_frames(B, N, seed=rank)).to(dev)
+        # the streaming executor overlaps batch k+1's SA1 FPS + ball queries (latency-bound,
+        # one workgroup per frame) with batch k's MFMA levels; results are identical to forward()
+        pipe = pn.StreamingSSG(bb, B, N, depth=depth)
+        ref, _ = bb.forward(x)
+        outs = pipe.run([x] * max(2, warmup))
+        torch.cuda.synchronize(dev)
+        assert all(torch.equal(ref, o) for o in outs), "streaming executor diverged from forward()"
+        timers = pn._Timers()
+        bb.timers = timers  # HIP events around every launch, on the stream it is launched on
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        pipe.run([x] * steps)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        bb.timers = None
+        if world > 1:
+            tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            elapsed = float(tt.item())
+        return elapsed, timers.mean_ms()
 
-    timers = pn._Timers()
-    bb.timers = timers  # HIP events around every launch, on the stream it is launched on
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    pipe.run([x] * args.steps)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    bb.timers = None
-    if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    elapsed, kern = measure(pn.SSG, "f32", B, N, args.steps, args.warmup, args.depth)
+    extras = {}
+    if not args.no_extras:
+        # the other BASELINE.json configs, measured the same way (not the headline metric)
+        for key, cfg, dtype, b2, n2, st in (("configs[1]_sa1_16k_f32", pn.SA1_ONLY, "f32", 32, 16384, 10),
+                                            ("configs[4]_msg_131k_bf16", pn.MSG, "bf16", 8, 131072, 6)):
+            el2, k2 = measure(cfg, dtype, b2, n2, st, 2, args.depth)
+            extras[key] = {"M_points_per_s": world * b2 * n2 * st / el2 / 1e6, "ms_per_step": el2 / st * 1e3,
+                           "frames_per_gpu": b2, "points_per_frame": n2, "dtype": dtype,
+                           "kernel_ms": k2}
 
-    kern = timers.mean_ms()
     work = ssg_kernel_work(N)
     # the dominant kernel of the critical path: SA1 FPS runs on its own stream, overlapped
     # with the main-stream kernels; it dominates only if it is longer than all of them
@@ -177,6 +189,7 @@ def main():
             "roofline_all": {k: roof(k) for k in kern if k in work},
             "kernel_ms": kern,
             "pipeline": {"executor": "pointnet2.StreamingSSG", "sa1_fps_batches_in_flight": args.depth},
+            "other_configs": extras,
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -11,11 +11,11 @@ if [[ $STEPS == *tests* ]]; then
   timeout -k 10 ${TEST_TIMEOUT:-900} python -m pytest tests -m gpu -x -q -rfE > gpurun_out/${TAG}_tests.log 2>&1 || exit 11
 fi
 if [[ $STEPS == *bench* ]]; then
-  timeout -k 10 600 python bench.py ${BENCH_ARGS:---steps 10 --warmup 3} > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err || exit 12
+  timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err || exit 12
 fi
 if [[ $STEPS == *prof* ]]; then
   (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv \
-      -d "$R/gpurun_out/${TAG}_prof" -o prof -- python3 "$R/bench.py" --steps 10 --warmup 3 --no-cpu-baseline \
+      -d "$R/gpurun_out/${TAG}_prof" -o prof -- python3 "$R/bench.py" --no-extras --no-cpu-baseline \
       > "$R/gpurun_out/${TAG}_prof_bench.json" 2> "$R/gpurun_out/${TAG}_prof.err") || exit 13
 fi
 exit 0

@@ -94,6 +94,21 @@ int lidar_mlp_pack_f32(int32_t cfeat, int32_t c1, int32_t c2, int32_t c3, const 
                        const float *b1_host, const float *w2_host, const float *b2_host,
                        const float *w3_host, const float *b3_host, float *packed_host);
 
+/* bf16 variant of lidar_sa_group_mlp_f32 on v_mfma_f32_32x32x16_bf16 (BASELINE configs[4]):
+ * grouped xyz offsets, features, hidden activations and weights rounded to bf16 (RNE),
+ * fp32 accumulation, fp32 bias/ReLU and fp32 pooled output.  Same argument meaning;
+ * `packed` is the byte image from lidar_mlp_pack_bf16 (cfeat a multiple of 16). */
+int lidar_sa_group_mlp_bf16(lidar_handle *h, const float *xyz, const float *feats,
+                            int64_t feat_stride, const float *centres, const int32_t *idx,
+                            int64_t batch, int64_t n, int64_t m, int32_t nsample, int32_t cfeat,
+                            int32_t c1, int32_t c2, int32_t c3, const void *packed, float *out,
+                            int64_t out_stride, int64_t out_offset, void *stream);
+/* size in BYTES and host construction of the bf16 packed image */
+int64_t lidar_mlp_packed_size_bf16(int32_t cfeat, int32_t c1, int32_t c2, int32_t c3);
+int lidar_mlp_pack_bf16(int32_t cfeat, int32_t c1, int32_t c2, int32_t c3, const float *w1_host,
+                        const float *b1_host, const float *w2_host, const float *b2_host,
+                        const float *w3_host, const float *b3_host, void *packed_host);
+
 /* dense layer on MFMA: y (rows, cout) = relu(x (rows, k) W (k, cout) + b), fp32.
  * If pool_rows > 0: y is (rows / pool_rows, cout) = max over each run of pool_rows rows
  * (group_all's max-pool, fused); y must then be zeroed by the caller first.

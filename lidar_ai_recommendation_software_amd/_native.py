@@ -47,6 +47,10 @@ SIGNATURES = {
                                I64, I64, P],
     "lidar_mlp_packed_size": [I32, I32, I32, I32],
     "lidar_mlp_pack_f32": [I32, I32, I32, I32, P, P, P, P, P, P, P],
+    "lidar_sa_group_mlp_bf16": [P, P, P, I64, P, P, I64, I64, I64, I32, I32, I32, I32, I32, P, P,
+                                I64, I64, P],
+    "lidar_mlp_packed_size_bf16": [I32, I32, I32, I32],
+    "lidar_mlp_pack_bf16": [I32, I32, I32, I32, P, P, P, P, P, P, P],
     "lidar_dense_relu_f32": [P, P, I64, I32, P, P, I32, I32, P, P],
     "lidar_concat_xyz_pad_f32": [P, P, I64, P, I64, I64, P],
     "lidar_voxel_downsample_f32": [P, P, I64, F32, P, P, P, P, P],
@@ -56,7 +60,8 @@ SIGNATURES = {
     "lidar_grid_dims": [F64, F64, F64, F64, F64, P, P],
     "lidar_density_grid_f64": [P, P, I64, F64, F64, F64, F64, F64, I64, I64, P, P, P, P],
 }
-_RESTYPES = {"lidar_last_error": ctypes.c_char_p, "lidar_mlp_packed_size": I64}
+_RESTYPES = {"lidar_last_error": ctypes.c_char_p, "lidar_mlp_packed_size": I64,
+             "lidar_mlp_packed_size_bf16": I64}
 
 
 def load_library(path=LIB_PATH):

@@ -134,7 +134,21 @@ def pack_branch(layers, cfeat):
     return out
 
 
-def group_mlp(xyz, feats, new_xyz, idx, packed, widths, out=None, out_offset=0):
+def pack_branch_bf16(layers, cfeat):
+    """Host-side packed image for lidar_sa_group_mlp_bf16 (bf16 fragments + fp32 biases),
+    returned as a uint8 array."""
+    (w1, b1), (w2, b2), (w3, b3) = layers
+    c1, c2, c3 = w1.shape[1], w2.shape[1], w3.shape[1]
+    lib = nat.load_library()
+    size = lib.lidar_mlp_packed_size_bf16(cfeat, c1, c2, c3)
+    out = np.zeros(size, dtype=np.uint8)
+    arrs = [np.ascontiguousarray(a, dtype=np.float32) for a in (w1, b1, w2, b2, w3, b3)]
+    nat.check(lib.lidar_mlp_pack_bf16(cfeat, c1, c2, c3, *[a.ctypes.data_as(ctypes.c_void_p) for a in arrs],
+                                      out.ctypes.data_as(ctypes.c_void_p)), "lidar_mlp_pack_bf16")
+    return out
+
+
+def group_mlp(xyz, feats, new_xyz, idx, packed, widths, out=None, out_offset=0, bf16=False):
     """Fused grouping + 3-layer MLP + max over nsample -> (B, M, c3) (or into `out`)."""
     B, N, _ = xyz.shape
     M, ns = idx.shape[1], idx.shape[2]
@@ -143,7 +157,8 @@ def group_mlp(xyz, feats, new_xyz, idx, packed, widths, out=None, out_offset=0):
     if out is None:
         out = torch.empty((B, M, c3), dtype=torch.float32, device=xyz.device)
     _dev_check(xyz, feats, new_xyz, idx, packed, out)
-    nat.call("lidar_sa_group_mlp_f32", nat.handle(xyz.device.index), nat.ptr(xyz), nat.ptr(feats),
+    nat.call("lidar_sa_group_mlp_bf16" if bf16 else "lidar_sa_group_mlp_f32", nat.handle(xyz.device.index),
+             nat.ptr(xyz), nat.ptr(feats),
              cfeat, nat.ptr(new_xyz), nat.ptr(idx), B, N, M, ns, cfeat, c1, c2, c3,
              nat.ptr(packed), nat.ptr(out), out.shape[-1], out_offset, nat.stream_ptr())
     return out
@@ -189,7 +204,12 @@ class PointNet2Backbone:
     """SSG / MSG PointNet++ encoder on liblidar_amd.  ``forward(xyz)`` -> global feature
     (B, C_last) plus the per-level (new_xyz, features, fps_idx)."""
 
-    def __init__(self, cfg=SSG, weights=None, device="cuda", seed=0):
+    def __init__(self, cfg=SSG, weights=None, device="cuda", seed=0, dtype="f32"):
+        """dtype "bf16": the SA branches run on bf16 MFMA (inputs/activations/weights rounded
+        to bf16, fp32 accumulation; BASELINE configs[4]); group_all stays fp32."""
+        if dtype not in ("f32", "bf16"):
+            raise ValueError("dtype must be 'f32' or 'bf16'")
+        self.bf16 = dtype == "bf16"
         self.cfg = cfg
         self.device = torch.device(device)
         self.weights = weights if weights is not None else init_weights(cfg, seed)
@@ -210,7 +230,8 @@ class PointNet2Backbone:
             else:
                 branches = []
                 for (r, ns, widths, layers) in zip(lvl["radii"], lvl["nsamples"], lvl["mlps"], wl):
-                    packed = torch.from_numpy(pack_branch(layers, cfeat)).to(self.device)
+                    pk = pack_branch_bf16(layers, cfeat) if self.bf16 else pack_branch(layers, cfeat)
+                    packed = torch.from_numpy(pk).to(self.device)
                     branches.append({"r": r, "ns": ns, "widths": widths, "packed": packed})
                 self.levels.append({"div": lvl["npoint_div"], "branches": branches, "cfeat": cfeat})
                 cfeat = sum(w[-1] for w in lvl["mlps"])
@@ -251,7 +272,7 @@ class PointNet2Backbone:
                 else:
                     gidx = _call(self.timers, f"{tag}_ball_query", ball_query, br["r"], br["ns"], xyz, new_xyz)
                 _call(self.timers, f"{tag}_group_mlp", group_mlp, xyz, feats, new_xyz, gidx, br["packed"],
-                      br["widths"], out=out, out_offset=off)
+                      br["widths"], out=out, out_offset=off, bf16=self.bf16)
                 off += br["widths"][-1]
             if keep_levels:
                 out_levels.append((new_xyz, out[..., :ctot], idx))

@@ -19,6 +19,9 @@ Spec (all fp32, one rounding per operation, never fused multiply-add):
   grouping    [xyz[idx] - centre, features[idx]]  (use_xyz, channels last).
   SA MLP      h = relu(h @ W + b) per layer; max over the nsample axis.
   group_all   input [xyz, features] over all points, max over all points.
+  bf16 mode   SA branches: grouped xyz offsets, features, hidden activations and
+              weights rounded to bf16 (RNE) before each layer, fp32 accumulation, fp32
+              bias/ReLU/pool; group_all stays fp32.
   voxel       v = floor((p - min(p)) / voxel_size) per axis (fp32 divide);
               key = (vx * Dy + vy) * Dz + vz with D = max(v) + 1; voxels in
               ascending key order; centroid = sequential fp32 sum in point
@@ -144,7 +147,7 @@ def sa_stack(xyz, cfg, weights, bf16=False):
     levels = []
     for lvl, w in zip(cfg["levels"], weights):
         if lvl.get("group_all"):
-            g = group_all(xyz, feats, w[0], bf16)
+            g = group_all(xyz, feats, w[0], False)  # spec: group_all is fp32 in both modes
             levels.append((None, g, None))
             return g, levels
         npoint = lvl["npoint"]

@@ -154,3 +154,56 @@ def test_streaming_executor_matches_forward(cuda, depth):
     torch.cuda.synchronize()
     for a, b in zip(got, want):
         assert torch.equal(a, b)
+
+
+
+def bf16_close(got, want, what=""):
+    """bf16 tolerance: inputs/activations are rounded to bf16 on both sides, so results agree
+    to fp32 accumulation order EXCEPT where that order flips one activation's bf16 rounding
+    (a 2^-8 relative step that propagates).  Require >= 99 % of elements within the fp32
+    tolerance and every element within 2 % of the RMS."""
+    got = np.asarray(got, dtype=np.float64)
+    want = np.asarray(want, dtype=np.float64)
+    scale = np.sqrt(np.mean(want ** 2)) + 1e-30
+    err = np.abs(got - want)
+    tight = err <= RTOL * np.abs(want) + RTOL * scale
+    assert tight.mean() >= 0.99, f"{what}: only {tight.mean():.4f} within fp32 tolerance"
+    assert err.max() <= 2e-2 * scale, f"{what}: max err {err.max():.3e} vs rms {scale:.3e}"
+
+
+@pytest.mark.parametrize("cfg_name,level,branch", [("msg", 0, 0), ("msg", 0, 1), ("msg", 0, 2), ("msg", 1, 0),
+                                                   ("msg", 1, 1), ("msg", 1, 2), ("ssg", 0, 0), ("ssg", 1, 0)])
+def test_group_mlp_bf16(cuda, cfg_name, level, branch):
+    cfg = pn.CONFIGS[cfg_name]
+    w = pn.init_weights(cfg, seed=3)
+    lvl = cfg["levels"][level]
+    layers = w[level][branch]
+    cfeat = layers[0][0].shape[0] - 3
+    r, ns, widths = lvl["radii"][branch], lvl["nsamples"][branch], lvl["mlps"][branch]
+    B, N, M = 2, 2048, 128
+    rng = np.random.default_rng(7)
+    x = unit_frames(B, N, 9)
+    f = np.abs(rng.standard_normal((B, N, cfeat))).astype(np.float32) if cfeat else None
+    c = x[:, :M].copy()
+    gi = tier_n.ball_query(x, c, r, ns)
+    packed = torch.from_numpy(pn.pack_branch_bf16(layers, cfeat)).to(cuda)
+    T = lambda a: None if a is None else torch.from_numpy(np.ascontiguousarray(a)).to(cuda)
+    got = pn.group_mlp(T(x), T(f), T(c), T(gi), packed, widths, bf16=True).cpu().numpy()
+    for bi in range(B):
+        fin = None if f is None else tier_n.bf16_round(f[bi])
+        want = tier_n.mlp_maxpool(tier_n.group(x[bi], fin, c[bi], gi[bi]), layers, ns, bf16=True)
+        bf16_close(got[bi], want, f"bf16 {cfg_name} L{level} br{branch} frame {bi}")
+
+
+@pytest.mark.parametrize("cfg_name,n", [("msg", 16384), ("ssg", 16384)])
+def test_backbone_bf16_vs_oracle(cuda, cfg_name, n):
+    cfg = pn.CONFIGS[cfg_name]
+    bb = pn.PointNet2Backbone(cfg, device=cuda, seed=0, dtype="bf16")
+    x = unit_frames(1, n, 22)
+    g, levels = bb.forward(torch.from_numpy(x).to(cuda), keep_levels=True)
+    torch.cuda.synchronize()
+    want, wl = tier_n.sa_stack(x[0], {"levels": pn.resolve(cfg, n)}, bb.weights, bf16=True)
+    for li, ((nx, nf, ni), (ox, of, oi)) in enumerate(zip(levels, wl)):
+        assert np.array_equal(ni.cpu().numpy()[0], oi), f"level {li} FPS indices differ"
+        bf16_close(nf.cpu().numpy()[0], of, f"bf16 level {li} features")
+    bf16_close(g.cpu().numpy()[0], want, "bf16 global feature")

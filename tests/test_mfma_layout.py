@@ -107,3 +107,92 @@ def test_packed_mfma_chain_matches_matrix_form(cfg_name, level, branch):
     # and the oracle's fp32 formulation agrees to fp32 precision
     want = tier_n.mlp_maxpool(rows, layers, 32)[0]
     np.testing.assert_allclose(got.max(axis=0), want, rtol=1e-4, atol=1e-5)
+
+
+# ----------------------------------------------------------------------------- bf16
+def bf16_vals(packed_u16):
+    return (packed_u16.astype(np.uint32) << 16).view(np.float32).astype(np.float64)
+
+
+def mfma16(acc, a, b):
+    """acc (32,32) += A(32x16) B(16x32); lane l holds A[l&31][8h+j], B[8h+j][l&31]."""
+    A = np.concatenate([a[:32], a[32:]], axis=1)          # (32, 16): cols 0-7 from h=0
+    Bm = np.concatenate([b[:32], b[32:]], axis=1).T      # (16, 32)
+    return acc + A @ Bm
+
+
+def emulate_bf16(x_rows, packed_bytes, cf, c1, c2, c3):
+    k1 = (cf + 3 + 15) // 16 * 16
+    s1 = k1 // 16
+    T1, T2, T3 = c1 // 32, c2 // 32, c3 // 32
+    n_w = (T1 * s1 + T2 * T1 * 2 + T3 * T2 * 2) * 64 * 8
+    W = bf16_vals(np.frombuffer(packed_bytes[: 2 * n_w], dtype=np.uint16))
+    bias = np.frombuffer(packed_bytes[2 * n_w:], dtype=np.float32).astype(np.float64)
+    B1, B2, B3 = bias[:c1], bias[c1:c1 + c2], bias[c1 + c2:]
+    W1 = W[: T1 * s1 * 512].reshape(T1, s1, 64, 8)
+    W2 = W[T1 * s1 * 512: T1 * s1 * 512 + T2 * T1 * 2 * 512].reshape(T2, T1, 2, 64, 8)
+    W3 = W[T1 * s1 * 512 + T2 * T1 * 2 * 512:].reshape(T3, T2, 2, 64, 8)
+    phys = np.zeros((32, k1))
+    phys[:, :cf] = x_rows[:, 3:]
+    phys[:, cf:cf + 3] = x_rows[:, :3]
+    x1 = np.zeros((s1, 64, 8))
+    for s in range(s1):
+        for l in range(64):
+            x1[s, l] = phys[l & 31, 16 * s + 8 * (l >> 5): 16 * s + 8 * (l >> 5) + 8]
+
+    def frags(D):
+        f = np.zeros((2, 64, 8))
+        for l in range(64):
+            for s in range(2):
+                for j in range(8):
+                    r = 8 * s + j
+                    f[s, l, j] = D[rho(r) + 4 * (l >> 5), l & 31]
+        from oracle.tier_n import bf16_round  # the kernel converts fragments with RNE
+        return bf16_round(f.astype(np.float32)).astype(np.float64)
+
+    y1 = []
+    for t in range(T1):
+        acc = np.zeros((32, 32))
+        for s in range(s1):
+            acc = mfma16(acc, W1[t, s], x1[s])
+        acc = np.maximum(acc + B1[32 * t: 32 * t + 32, None], 0)
+        y1.append(frags(acc))
+    y2 = []
+    for t in range(T2):
+        acc = np.zeros((32, 32))
+        for ti in range(T1):
+            for s in range(2):
+                acc = mfma16(acc, W2[t, ti, s], y1[ti][s])
+        acc = np.maximum(acc + B2[32 * t: 32 * t + 32, None], 0)
+        y2.append(frags(acc))
+    out = np.zeros((32, c3))
+    for t in range(T3):
+        acc = np.zeros((32, 32))
+        for ti in range(T2):
+            for s in range(2):
+                acc = mfma16(acc, y2[ti][s], W3[t, ti, s])
+        out[:, 32 * t: 32 * t + 32] = np.maximum(acc + B3[None, 32 * t: 32 * t + 32], 0)
+    return out
+
+
+@pytest.mark.parametrize("cfg_name,level,branch", [("msg", 0, 0), ("msg", 1, 1), ("ssg", 1, 0)])
+def test_packed_bf16_chain_matches_matrix_form(cfg_name, level, branch):
+    from oracle.tier_n import bf16_round
+    cfg = pn.CONFIGS[cfg_name]
+    layers = pn.init_weights(cfg, seed=6)[level][branch]
+    layers = [(bf16_round(W), b) for W, b in layers]  # exact in bf16: a pure layout check
+    cf = layers[0][0].shape[0] - 3
+    c1, c2, c3 = (w.shape[1] for w, _ in layers)
+    packed = pn.pack_branch_bf16(layers, cf)
+    rows = bf16_round(np.random.default_rng(2).standard_normal((32, 3 + cf)).astype(np.float32))
+    got = emulate_bf16(rows.astype(np.float64), packed.tobytes(), cf, c1, c2, c3)
+    h = rows.astype(np.float64)
+    for i, (W, b) in enumerate(layers):
+        h = np.maximum(h @ W.astype(np.float64) + b, 0)
+        if i < 2:  # hidden activations enter the next MFMA as bf16 in both formulations
+            h = bf16_round(h.astype(np.float32)).astype(np.float64)
+    # same roundings on both sides: equal up to fp64 summation order (a rare bf16 tie flip
+    # shows up as one isolated ~2^-8 difference)
+    close = np.isclose(got, h, rtol=1e-9, atol=1e-12)
+    assert close.mean() > 0.99, f"{(~close).sum()} of {close.size} differ"
+    np.testing.assert_allclose(got, h, rtol=2e-2, atol=1e-3)

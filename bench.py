@@ -95,6 +95,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--depth", type=int, default=3, help="SA1-FPS batches in flight ahead of the MLPs")
+    ap.add_argument("--side-priority", type=int, default=0, help="HIP priority of the FPS streams (<0 = high)")
     ap.add_argument("--no-extras", action="store_true", help="skip the configs[1]/[4] side measurements")
     args = ap.parse_args()
 
@@ -119,7 +120,7 @@ def main():
         x = torch.from_numpy(unit_frames(B, N, seed=rank)).to(dev)
         # the streaming executor overlaps batch k+1's SA1 FPS + ball queries (latency-bound,
         # one workgroup per frame) with batch k's MFMA levels; results are identical to forward()
-        pipe = pn.StreamingSSG(bb, B, N, depth=depth)
+        pipe = pn.StreamingSSG(bb, B, N, depth=depth, side_priority=args.side_priority)
         ref, _ = bb.forward(x)
         outs = pipe.run([x] * max(2, warmup))
         torch.cuda.synchronize(dev)

@@ -15,10 +15,12 @@
 // as d is a lower bound of every member's d (fl() is monotone), so `lb >= bucket max`
 // proves no member changes and the bucket is skipped — an exact pruning, not an
 // approximation.  Active buckets are streamed (64 lanes = 64 points, one coalesced float4
-// (x, y, z, dist) load each, up to 4 buckets' loads in flight together), updated, and
-// re-reduced with DPP argmax reductions (max dist, lowest index on ties); the frame argmax
-// is a DPP wave argmax of the per-lane bucket maxima and a 16-way LDS merge of
-// (dist bits << 32 | ~index) keys.
+// (x, y, z, dist) load each, up to 4 buckets' loads in flight together; the workspace is
+// padded to whole buckets with dist -1 sentinels so the batch is branch-free), updated,
+// and re-reduced with DPP argmax reductions (max dist, lowest index on ties).  A wave
+// whose buckets changed recomputes its DPP argmax; every wave then submits
+// (dist bits << 32 | (2^18 - index) << 4 | wave) to ONE LDS 64-bit atomic max and its
+// coordinates to a per-wave slot, so the frame argmax costs a single barrier per step.
 //
 // Nested FPS (SA2 samples SA1's centroids): FPS over the first m points of an FPS ordering
 // is the identity 0..m-1 while the parent's winning distance stayed > 0 — the parent
@@ -29,7 +31,7 @@
 namespace {
 
 constexpr int kThreads = 1024;  // 16 waves: active-bucket updates and their reductions run in
-                                // parallel across waves; the merge runs on wave 0 alone
+                                // parallel across waves; the merge is an LDS atomic max
 constexpr int kWaves = kThreads / 64;
 constexpr int kGrid = 16;  // Morton cells per axis for the bucket ordering
 constexpr int kCells = kGrid * kGrid * kGrid;
@@ -59,9 +61,11 @@ constexpr int kLoopWaves = kThreads / 64;
 // reductions interleaved): new distances against q, bucket max + its lowest-index argmax
 // point into the owner lane's registers.
 template <int K>
-__device__ __forceinline__ void update_batch(uint64_t &mask, const FrameWs &W, int n, int wave, int q, int lane,
+__device__ __forceinline__ void update_batch(uint64_t &mask, const FrameWs &W, int wave, int q, int lane,
                                              float qx, float qy, float qz, float &bd, uint32_t &bi, float *bx)
 {
+    // branch-free: the workspace is padded to whole buckets with sentinel points
+    // (dist -1: never the max, never updated since every real d >= 0)
     int bbs[K], pos[K];
     float4 P[K];
     uint32_t I[K];
@@ -73,24 +77,15 @@ __device__ __forceinline__ void update_batch(uint64_t &mask, const FrameWs &W, i
     }
 #pragma unroll
     for (int u = 0; u < K; ++u) {
-        P[u] = make_float4(0.f, 0.f, 0.f, -1.0f);  // lanes past the end never win
-        I[u] = 0xffffffffu;
-        if (pos[u] < n) {
-            P[u] = W.p[pos[u]];
-            I[u] = W.idx[pos[u]];
-        }
+        P[u] = W.p[pos[u]];
+        I[u] = W.idx[pos[u]];
     }
     float od[K], dm[K];
 #pragma unroll
     for (int u = 0; u < K; ++u) {
-        od[u] = P[u].w;
-        if (pos[u] < n) {
-            const float d = lidar::dist2f(P[u].x, P[u].y, P[u].z, qx, qy, qz);
-            if (d < od[u]) {
-                W.p[pos[u]].w = d;
-                od[u] = d;
-            }
-        }
+        const float d = lidar::dist2f(P[u].x, P[u].y, P[u].z, qx, qy, qz);
+        od[u] = fminf(P[u].w, d);
+        W.p[pos[u]].w = od[u];
     }
 #pragma unroll
     for (int u = 0; u < K; ++u) dm[u] = lidar::wave_max_dpp(od[u]);
@@ -108,13 +103,12 @@ __device__ __forceinline__ void update_batch(uint64_t &mask, const FrameWs &W, i
         const float wx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(P[u].x), wl));
         const float wy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(P[u].y), wl));
         const float wz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(P[u].z), wl));
-        if (lane == bbs[u]) {
-            bd = dm[u];
-            bi = wi;
-            bx[0] = wx;
-            bx[1] = wy;
-            bx[2] = wz;
-        }
+        const bool me = lane == bbs[u];
+        bd = me ? dm[u] : bd;
+        bi = me ? wi : bi;
+        bx[0] = me ? wx : bx[0];
+        bx[1] = me ? wy : bx[1];
+        bx[2] = me ? wz : bx[2];
     }
 }
 
@@ -163,14 +157,17 @@ __global__ __launch_bounds__(kThreads) void fps_bucket_kernel(const float *__res
     }
 
     float *wsb = ws + (int64_t)b * ws_stride;
-    FrameWs W{reinterpret_cast<float4 *>(wsb), reinterpret_cast<uint32_t *>(wsb + 4 * (int64_t)n)};
+    const int npad = (n + 63) / 64 * 64;  // whole buckets; the tail holds sentinel points
+    FrameWs W{reinterpret_cast<float4 *>(wsb), reinterpret_cast<uint32_t *>(wsb + 4 * (int64_t)npad)};
 
     __shared__ uint32_t hist[kCells];
     __shared__ float red[6][kWaves];
     __shared__ uint32_t wsum[kWaves];
-    __shared__ float sd[kWaves], sx[kWaves], sy[kWaves], sz[kWaves];
-    __shared__ uint32_t si[kWaves];
-    __shared__ float qbuf[4];
+    // per-step merge: every wave submits its argmax as one 64-bit key to an LDS atomic max
+    // (triple-buffered so a slot is cleared two barriers after its last read) and its
+    // coordinates to a per-wave slot (double-buffered); one barrier per step
+    __shared__ unsigned long long mkey[3];
+    __shared__ __attribute__((aligned(16))) float mcrd[2][kWaves][4];
 
     // ---- frame bounding box
     float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
@@ -251,6 +248,10 @@ __global__ __launch_bounds__(kThreads) void fps_bucket_kernel(const float *__res
         W.p[pos] = make_float4(p[3 * i], p[3 * i + 1], p[3 * i + 2], INFINITY);
         W.idx[pos] = (uint32_t)i;
     }
+    for (int i = n + tid; i < npad; i += kThreads) {
+        W.p[i] = make_float4(0.0f, 0.0f, 0.0f, -1.0f);
+        W.idx[i] = 0xffffffffu;
+    }
     __threadfence_block();
     __syncthreads();
 
@@ -314,6 +315,9 @@ __global__ __launch_bounds__(kThreads) void fps_bucket_kernel(const float *__res
 
     float w_d = 0.0f, w_x = 0.0f, w_y = 0.0f, w_z = 0.0f;  // this wave's current argmax
     uint32_t w_i = 0xffffffffu;
+    if (tid < 3) mkey[tid] = 0ull;
+    __syncthreads();
+    int cur3 = 1, nxt3 = 2;
     for (int it = 1; it < npoint; ++it) {
         bool wave_dirty = it == 1;
         if constexpr (DIAG) {
@@ -333,11 +337,11 @@ __global__ __launch_bounds__(kThreads) void fps_bucket_kernel(const float *__res
                 if constexpr (DIAG) dacc[4]++;
                 const int cnt = __popcll(mask);
                 if (cnt >= 4)
-                    update_batch<4>(mask, W, n, wave, q, lane, qx, qy, qz, bd[q], bi[q], bx[q]);
+                    update_batch<4>(mask, W, wave, q, lane, qx, qy, qz, bd[q], bi[q], bx[q]);
                 else if (cnt >= 2)
-                    update_batch<2>(mask, W, n, wave, q, lane, qx, qy, qz, bd[q], bi[q], bx[q]);
+                    update_batch<2>(mask, W, wave, q, lane, qx, qy, qz, bd[q], bi[q], bx[q]);
                 else
-                    update_batch<1>(mask, W, n, wave, q, lane, qx, qy, qz, bd[q], bi[q], bx[q]);
+                    update_batch<1>(mask, W, wave, q, lane, qx, qy, qz, bd[q], bi[q], bx[q]);
             }
         }
         if constexpr (DIAG) {
@@ -348,7 +352,7 @@ __global__ __launch_bounds__(kThreads) void fps_bucket_kernel(const float *__res
             __builtin_amdgcn_sched_barrier(0);
         }
         // frame argmax: lane best over its buckets -> wave argmax (DPP, only when one of the
-        // wave's buckets changed) -> LDS slots -> wave 0 merges -> q broadcast through LDS
+        // wave's buckets changed) -> LDS atomic max of the packed key -> barrier -> broadcast
         if (wave_dirty) {
             float best = bd[0];
             uint32_t besti = bi[0];
@@ -368,13 +372,6 @@ __global__ __launch_bounds__(kThreads) void fps_bucket_kernel(const float *__res
             w_x = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cx), wl));
             w_y = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cy), wl));
             w_z = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cz), wl));
-            if (lane == 0) {
-                sd[wave] = w_d;
-                si[wave] = w_i;
-                sx[wave] = w_x;
-                sy[wave] = w_y;
-                sz[wave] = w_z;
-            }
         }
         if constexpr (DIAG) {
             __builtin_amdgcn_sched_barrier(0);
@@ -383,6 +380,19 @@ __global__ __launch_bounds__(kThreads) void fps_bucket_kernel(const float *__res
             t0 = t1;
             __builtin_amdgcn_sched_barrier(0);
         }
+        // key: dist bits (d >= 0 orders as unsigned) | (2^18 - idx) << 4 | wave; a larger key
+        // is a larger distance, then a smaller index (n <= 2^18); empty slots carry field 0
+        const int slot = cur3, cslot = it & 1;
+        if (lane == 0) {
+            const uint32_t fld = w_i < (1u << 18) ? (1u << 18) - w_i : 0u;
+            const unsigned long long key =
+                ((unsigned long long)__float_as_uint(w_d) << 32) | (fld << 4) | (uint32_t)wave;
+            mcrd[cslot][wave][0] = w_x;
+            mcrd[cslot][wave][1] = w_y;
+            mcrd[cslot][wave][2] = w_z;
+            atomicMax(&mkey[slot], key);
+        }
+        if (tid == 0) mkey[nxt3] = 0ull;  // step it+1's slot, last read before the previous barrier
         __syncthreads();
         if constexpr (DIAG) {
             __builtin_amdgcn_sched_barrier(0);
@@ -391,35 +401,27 @@ __global__ __launch_bounds__(kThreads) void fps_bucket_kernel(const float *__res
             t0 = t1;
             __builtin_amdgcn_sched_barrier(0);
         }
-        if (wave == 0) {
-            const bool slot = lane < kWaves;
-            const float md = slot ? sd[lane] : -1.0f;
-            const uint32_t mi = slot ? si[lane] : 0xffffffffu;
-            const float mx = slot ? sx[lane] : 0.0f, my = slot ? sy[lane] : 0.0f, mz = slot ? sz[lane] : 0.0f;
-            float gdist;
-            const int gl = lidar::wave_argmax_lane(md, mi, &gdist);
-            const uint32_t gidx = (uint32_t)__builtin_amdgcn_readlane((int)mi, gl);
-            const float gx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mx), gl));
-            const float gy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my), gl));
-            const float gz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mz), gl));
-            if (lane == 0) {
-                qbuf[0] = gx;
-                qbuf[1] = gy;
-                qbuf[2] = gz;
+        {
+            const unsigned long long key = mkey[slot];
+            const int ww = (int)(key & 15u);
+            const float gdist = __uint_as_float((uint32_t)(key >> 32));
+            const uint32_t gidx = (1u << 18) - (((uint32_t)key) >> 4);
+            qx = mcrd[cslot][ww][0];
+            qy = mcrd[cslot][ww][1];
+            qz = mcrd[cslot][ww][2];
+            if (tid == 0) {
                 out_idx[(int64_t)b * npoint + it] = (int32_t)gidx;
                 if (out_xyz) {
                     float *o = out_xyz + ((int64_t)b * npoint + it) * 3;
-                    o[0] = gx;
-                    o[1] = gy;
-                    o[2] = gz;
+                    o[0] = qx;
+                    o[1] = qy;
+                    o[2] = qz;
                 }
             }
             if (zero_at == npoint && gdist == 0.0f) zero_at = it;
         }
-        __syncthreads();
-        qx = qbuf[0];
-        qy = qbuf[1];
-        qz = qbuf[2];
+        cur3 = nxt3;
+        nxt3 = nxt3 == 2 ? 0 : nxt3 + 1;
         if constexpr (DIAG) {
             __builtin_amdgcn_sched_barrier(0);
             t1 = stamp();
@@ -448,7 +450,7 @@ LIDAR_EXPORT int lidar_fps_f32(lidar_handle *h, const float *xyz, int64_t batch,
     if (batch == 0) return LIDAR_OK;
     HIP_TRY(hipSetDevice(h->device));
     REQUIRE(prefix_ok == nullptr || npoint <= n, "lidar_fps_f32: prefix_ok needs npoint <= n");
-    int64_t stride = lidar::align_up(5 * n, 64);
+    int64_t stride = lidar::align_up(5 * lidar::align_up(n, 64), 64);
     float *ws = static_cast<float *>(lidar::workspace(h, (uint64_t)(batch * stride) * 4));
     if (!ws) return LIDAR_ENOMEM;
     hipStream_t s = static_cast<hipStream_t>(stream);
@@ -478,7 +480,7 @@ LIDAR_EXPORT int lidar_diag_fps_phases(lidar_handle *h, const float *xyz, int64_
 {
     REQUIRE(h && xyz && idx && diag && n <= 65536 && n >= 1 && npoint >= 1, "lidar_diag_fps_phases: bad args");
     HIP_TRY(hipSetDevice(h->device));
-    int64_t stride = lidar::align_up(5 * n, 64);
+    int64_t stride = lidar::align_up(5 * lidar::align_up(n, 64), 64);
     float *ws = static_cast<float *>(lidar::workspace(h, (uint64_t)(batch * stride) * 4));
     if (!ws) return LIDAR_ENOMEM;
     const size_t lds = (size_t)((n + 63) / 64) * 6 * sizeof(float);

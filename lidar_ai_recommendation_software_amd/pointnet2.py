@@ -319,13 +319,15 @@ class StreamingSSG:
     ``PointNet2Backbone.forward`` (same kernels, same inputs).
     """
 
-    def __init__(self, backbone, batch, n, depth=1):
+    def __init__(self, backbone, batch, n, depth=1, side_priority=0):
         self.bb = backbone
         self.B, self.N, self.depth = batch, n, depth
         dev = backbone.device
         lvl0 = backbone.levels[0]
         self.M1 = max(1, n // lvl0["div"])
-        self.fps_streams = [torch.cuda.Stream(device=dev) for _ in range(depth)]
+        # side_priority < 0 puts the latency-bound FPS chains ahead of the MLP waves in
+        # the dispatcher (HIP stream priority); results do not depend on it
+        self.fps_streams = [torch.cuda.Stream(device=dev, priority=side_priority) for _ in range(depth)]
         nslot = depth + 1
         self.idx = [torch.empty((batch, self.M1), dtype=torch.int32, device=dev) for _ in range(nslot)]
         self.cxyz = [torch.empty((batch, self.M1, 3), dtype=torch.float32, device=dev) for _ in range(nslot)]

@@ -65,9 +65,10 @@ def fps_phases():
         d = diag.cpu().numpy().astype(np.float64)
         steps = d[..., 5].mean()
         per = d[..., :4].mean(axis=(0, 1)) / steps
-        print(f"B={B}: cycles/step  update={per[0]:.0f} wave-argmax={per[1]:.0f} barrier={per[2]:.0f} "
-              f"merge={per[3]:.0f}  batches/step/wave={d[..., 4].mean() / steps:.2f} "
-              f"(max wave {d[..., 4].max(axis=1).mean() / steps:.2f})", flush=True)
+        print(f"B={B}: cycles/step  test+update={per[0]:.0f} wave-argmax={per[1]:.0f} "
+              f"submit+barrier={per[2]:.0f} broadcast={per[3]:.0f}  (slowest wave's test+update: "
+              f"{d[..., 0].max(axis=1).mean() / steps:.0f}; update batches/step/wave {d[..., 4].mean() / steps:.2f})",
+              flush=True)
 
 
 if __name__ == "__main__" and "phases" in sys.argv:

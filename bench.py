@@ -54,6 +54,21 @@ def ssg_kernel_work(n):
     }
 
 
+def pmc_traffic(B, N):
+    """Memory-side bytes per launch from the committed PMC passes (tools/pmc_traffic.py),
+    when they were taken on this same workload; None otherwise."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "pmc_traffic.json")))
+    if not files:
+        return {}
+    with open(files[-1]) as f:
+        d = json.load(f)
+    c = d.get("config", {})
+    if c.get("points_per_frame") != N or c.get("frames_per_gpu") != B:
+        return {}
+    return {k: v["traffic_bytes"] for k, v in d.get("kernels", {}).items()}
+
+
 def cpu_baseline(n, budget_s=20.0):
     """The oracle SA stack (C FPS / ball query + numpy MLP, BLAS pinned to 1 thread) on
     one frame of the same workload, on this host.  kind = "port" (the reference has no
@@ -104,9 +119,8 @@ def main():
     from lidar_ai_recommendation_software_amd import pointnet2 as pn
     from lidar_ai_recommendation_software_amd.synthetic import unit_frames
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from lidar_ai_recommendation_software_amd import sharding
+    rank, world, local = sharding.world_info()
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -117,7 +131,7 @@ def main():
 
     def measure(cfg, dtype, B, N, steps, warmup, depth):
         bb = pn.PointNet2Backbone(cfg, device=dev, seed=0, dtype=dtype)
-        x = torch.from_numpy(unit_frames(B, N, seed=rank)).to(dev)
+        x = torch.from_numpy(unit_frames(B, N, seed=sharding.frame_seed(rank))).to(dev)
         # the streaming executor overlaps batch k+1's SA1 FPS + ball queries (latency-bound,
         # one workgroup per frame) with batch k's MFMA levels; results are identical to forward()
         pipe = pn.StreamingSSG(bb, B, N, depth=depth, side_priority=args.side_priority)
@@ -127,20 +141,8 @@ def main():
         assert all(torch.equal(ref, o) for o in outs), "streaming executor diverged from forward()"
         timers = pn._Timers()
         bb.timers = timers  # HIP events around every launch, on the stream it is launched on
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
-        pipe.run([x] * steps)
-        torch.cuda.synchronize(dev)
-        if world > 1:
-            dist.barrier()
-        elapsed = time.perf_counter() - t0
+        elapsed = sharding.timed(lambda: pipe.run([x] * steps), dev, world)  # max over ranks
         bb.timers = None
-        if world > 1:
-            tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            elapsed = float(tt.item())
         return elapsed, timers.mean_ms()
 
     elapsed, kern = measure(pn.SSG, "f32", B, N, args.steps, args.warmup, args.depth)
@@ -150,11 +152,12 @@ def main():
         for key, cfg, dtype, b2, n2, st in (("configs[1]_sa1_16k_f32", pn.SA1_ONLY, "f32", 32, 16384, 10),
                                             ("configs[4]_msg_131k_bf16", pn.MSG, "bf16", 8, 131072, 6)):
             el2, k2 = measure(cfg, dtype, b2, n2, st, 2, args.depth)
-            extras[key] = {"M_points_per_s": world * b2 * n2 * st / el2 / 1e6, "ms_per_step": el2 / st * 1e3,
+            extras[key] = {"M_points_per_s": sharding.aggregate_rate(b2 * n2 * st, world, el2) / 1e6, "ms_per_step": el2 / st * 1e3,
                            "frames_per_gpu": b2, "points_per_frame": n2, "dtype": dtype,
                            "kernel_ms": k2}
 
     work = ssg_kernel_work(N)
+    traffic = pmc_traffic(B, N)
     # the dominant kernel of the critical path: SA1 FPS runs on its own stream, overlapped
     # with the main-stream kernels; it dominates only if it is longer than all of them
     side = ("sa1_fps", "sa1_ball_query")  # issued on the SA1 stream, overlapped with the rest
@@ -172,9 +175,10 @@ def main():
         else:
             a, p, u = per_launch / avg_s / 1e9, HBM_PEAK_GBS, "GB/s"
         return {"kernel": name, "bound": bound, "achieved": a, "peak": p, "unit": u, "frac": a / p,
-                "traffic": None, "work_per_launch": per_launch, "avg_launch_ms": kern[name]}
+                "traffic": traffic.get(name), "traffic_unit": "bytes per launch (PMC FETCH_SIZE*2 + WRITE_SIZE)",
+                "work_per_launch": per_launch, "avg_launch_ms": kern[name]}
 
-    value = world * B * N * args.steps / elapsed / 1e6
+    value = sharding.aggregate_rate(B * N * args.steps, world, elapsed) / 1e6
     if rank == 0:
         rec = {
             "metric": "M points/sec through SetAbstraction, 65k-pt frames; 1->8 GPU scaling",

@@ -5,8 +5,8 @@
 // on ties), d = (dx*dx + dy*dy) + dz*dz in fp32 with one rounding per operation.
 //
 // One 1024-thread workgroup per frame.  Prologue: frame bbox, counting sort of the
-// points by a 16^3 Morton cell into a sorted SoA copy in the workspace (x, y, z,
-// dist, original index), cut into buckets of 64 consecutive sorted points (one
+// points by a 16^3 Morton cell into a sorted copy in the workspace ((x, y, z,
+// original index) float4s + a separate dist array), cut into buckets of 64 consecutive sorted points (one
 // wavefront-width each).  Every bucket keeps, in the registers of its owner lane,
 // its bounding box and its (max dist, index) key and the coordinates of that point.
 //
@@ -45,8 +45,9 @@ __device__ __forceinline__ uint32_t spread3(uint32_t v)  // 4 bits -> every thir
 }
 
 struct FrameWs {
-    float4 *p;      // sorted (x, y, z, dist)
-    uint32_t *idx;  // original index of each sorted point
+    float4 *p;  // sorted (x, y, z, original index bits): read-only after the prologue
+    float *d;   // running min distance of each sorted point: the only per-step store, so an
+                // update dirties 2 cache lines per bucket, not 8 (the L2 holds ~4 frames per XCD)
 };
 
 __device__ __forceinline__ float gap(float q, float lo, float hi)
@@ -68,6 +69,7 @@ __device__ __forceinline__ void update_batch(uint64_t &mask, const FrameWs &W, i
     // (dist -1: never the max, never updated since every real d >= 0)
     int bbs[K], pos[K];
     float4 P[K];
+    float D[K];
     uint32_t I[K];
 #pragma unroll
     for (int u = 0; u < K; ++u) {
@@ -78,14 +80,16 @@ __device__ __forceinline__ void update_batch(uint64_t &mask, const FrameWs &W, i
 #pragma unroll
     for (int u = 0; u < K; ++u) {
         P[u] = W.p[pos[u]];
-        I[u] = W.idx[pos[u]];
+        D[u] = W.d[pos[u]];
     }
+#pragma unroll
+    for (int u = 0; u < K; ++u) I[u] = __float_as_uint(P[u].w);
     float od[K], dm[K];
 #pragma unroll
     for (int u = 0; u < K; ++u) {
         const float d = lidar::dist2f(P[u].x, P[u].y, P[u].z, qx, qy, qz);
-        od[u] = fminf(P[u].w, d);
-        W.p[pos[u]].w = od[u];
+        od[u] = fminf(D[u], d);
+        W.d[pos[u]] = od[u];
     }
 #pragma unroll
     for (int u = 0; u < K; ++u) dm[u] = lidar::wave_max_dpp(od[u]);
@@ -158,7 +162,7 @@ __global__ __launch_bounds__(kThreads) void fps_bucket_kernel(const float *__res
 
     float *wsb = ws + (int64_t)b * ws_stride;
     const int npad = (n + 63) / 64 * 64;  // whole buckets; the tail holds sentinel points
-    FrameWs W{reinterpret_cast<float4 *>(wsb), reinterpret_cast<uint32_t *>(wsb + 4 * (int64_t)npad)};
+    FrameWs W{reinterpret_cast<float4 *>(wsb), wsb + 4 * (int64_t)npad};
 
     __shared__ uint32_t hist[kCells];
     __shared__ float red[6][kWaves];
@@ -245,12 +249,12 @@ __global__ __launch_bounds__(kThreads) void fps_bucket_kernel(const float *__res
     __syncthreads();
     for (int i = tid; i < n; i += kThreads) {
         uint32_t pos = atomicAdd(&hist[cell_of(i)], 1u);
-        W.p[pos] = make_float4(p[3 * i], p[3 * i + 1], p[3 * i + 2], INFINITY);
-        W.idx[pos] = (uint32_t)i;
+        W.p[pos] = make_float4(p[3 * i], p[3 * i + 1], p[3 * i + 2], __uint_as_float((uint32_t)i));
+        W.d[pos] = INFINITY;
     }
     for (int i = n + tid; i < npad; i += kThreads) {
-        W.p[i] = make_float4(0.0f, 0.0f, 0.0f, -1.0f);
-        W.idx[i] = 0xffffffffu;
+        W.p[i] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(0xffffffffu));
+        W.d[i] = -1.0f;
     }
     __threadfence_block();
     __syncthreads();

@@ -1,0 +1,92 @@
+"""World-size-2 gloo coverage of the N>1 path (no GPU).
+
+The multi-GPU design is per-frame data parallelism: ranks take
+disjoint frame shards and share nothing on the data path; bench.py's only collectives
+are the timing barrier and the MAX-over-ranks all-reduce (`sharding.timed`).  These
+tests run exactly that bookkeeping over gloo with two CPU processes, and check that
+sharded per-frame processing gives the single-process results frame for frame.
+"""
+import os
+import socket
+import time
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from lidar_ai_recommendation_software_amd import sharding
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, n_frames, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    r, w, _ = sharding.world_info()
+    assert (r, w) == (rank, world)
+    # timing: rank 1 is slower; every rank must report the slowest rank's time
+    delay = 0.05 + 0.25 * rank
+    elapsed = sharding.timed(lambda: time.sleep(delay), None, world)
+    # data path: this rank's frames, processed independently (oracle Tier R, CPU)
+    from oracle import tier_r
+    from lidar_ai_recommendation_software_amd.synthetic import uniform_frame
+    lo, hi = sharding.shard(n_frames, rank, world)
+    res = {}
+    for f in range(lo, hi):
+        pts = uniform_frame(1024, seed=sharding.frame_seed(0, base=f))
+        pd = tier_r.preprocess_lidar_data(pts)
+        res[f] = (pd["clusters"], tier_r.extract_people_positions(pd))
+    shards = [None] * world
+    dist.all_gather_object(shards, (lo, hi))  # test-only check of coverage
+    np.save(os.path.join(out_dir, f"rank{rank}.npy"),
+            np.array([elapsed, *[x for s in shards for x in s]], dtype=np.float64))
+    np.savez(os.path.join(out_dir, f"res{rank}.npz"),
+             **{f"c{f}": v[0] for f, v in res.items()}, **{f"p{f}": v[1] for f, v in res.items()})
+    dist.destroy_process_group()
+
+
+def test_shard_partition_is_disjoint_and_complete():
+    for n in (0, 1, 7, 32, 256, 1001):
+        for world in (1, 2, 3, 8):
+            ranges = [sharding.shard(n, r, world) for r in range(world)]
+            assert ranges[0][0] == 0 and ranges[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(ranges, ranges[1:]))
+            sizes = [hi - lo for lo, hi in ranges]
+            assert max(sizes) - min(sizes) <= 1
+    with pytest.raises(ValueError):
+        sharding.shard(10, 2, 2)
+
+
+def test_aggregate_rate_is_whole_job():
+    assert sharding.aggregate_rate(32 * 65536, 8, 2.0) == 32 * 65536 * 8 / 2.0
+
+
+def test_gloo_world2_timing_and_sharded_frames(tmp_path):
+    world, n_frames = 2, 5
+    port = _free_port()
+    mp.spawn(_worker, args=(world, port, n_frames, str(tmp_path)), nprocs=world, join=True)
+    recs = [np.load(tmp_path / f"rank{r}.npy") for r in range(world)]
+    # both ranks report the MAX elapsed (>= the slow rank's 0.30 s sleep)
+    assert recs[0][0] == recs[1][0] >= 0.30
+    # gathered shard table: disjoint, complete
+    table = recs[0][1:].reshape(world, 2).astype(int)
+    assert table[0, 0] == 0 and table[0, 1] == table[1, 0] and table[1, 1] == n_frames
+    # per-frame results from the sharded run equal the single-process run
+    from oracle import tier_r
+    from lidar_ai_recommendation_software_amd.synthetic import uniform_frame
+    got = {}
+    for r in range(world):
+        with np.load(tmp_path / f"res{r}.npz") as z:
+            got.update({k: z[k] for k in z.files})
+    assert len(got) == 2 * n_frames
+    for f in range(n_frames):
+        pd = tier_r.preprocess_lidar_data(uniform_frame(1024, seed=sharding.frame_seed(0, base=f)))
+        np.testing.assert_array_equal(got[f"c{f}"], pd["clusters"])
+        np.testing.assert_array_equal(got[f"p{f}"], tier_r.extract_people_positions(pd))

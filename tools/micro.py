@@ -1,11 +1,12 @@
-"""Micro-benchmarks of single kernels (GPU box): python tools_micro.py [fps|mlp|bq]."""
+"""Micro-benchmarks of single kernels (GPU box): python tools/micro.py [fps|mlp|bq]."""
+import os
 import sys
 import time
 
 import numpy as np
 import torch
 
-sys.path.insert(0, ".")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from lidar_ai_recommendation_software_amd import pointnet2 as pn  # noqa: E402
 from lidar_ai_recommendation_software_amd.synthetic import unit_frames  # noqa: E402
 

@@ -42,7 +42,10 @@ def ssg_kernel_work(n):
     m1, m2 = n // 16, n // 64
     return {
         "sa1_group_mlp": ("mfma", mlp_flops(m1 * 32, [3, 64, 64, 128])),
-        "sa2_group_mlp": ("mfma", mlp_flops(m2 * 64, [131, 128, 128, 256])),
+        # SA2 layer 1 runs per point (N/16 rows of [f, x] W1 + b1, N/64 centre rows of
+        # c W1_xyz); the fused kernel computes layers 2-3 of every grouped row
+        "sa2_layer1_points": ("mfma", 2 * m1 * 131 * 128 + 2 * m2 * 3 * 128),
+        "sa2_group_mlp": ("mfma", mlp_flops(m2 * 64, [128, 128, 256])),
         "sa3_dense1": ("mfma", mlp_flops(m2, [259, 256])),
         "sa3_dense2": ("mfma", mlp_flops(m2, [256, 512])),
         "sa3_dense3_pool": ("mfma", mlp_flops(m2, [512, 1024])),

@@ -118,6 +118,24 @@ int lidar_dense_relu_f32(lidar_handle *h, const float *x, int64_t rows, int32_t 
                          const float *w, const float *bias, int32_t cout, int32_t pool_rows,
                          float *y, void *stream);
 
+/* as lidar_dense_relu_f32 with the ReLU optional (relu_on = 0: y = x W + b); the fused
+ * max-pool requires relu_on. */
+int lidar_dense_f32(lidar_handle *h, const float *x, int64_t rows, int32_t k, const float *w,
+                    const float *bias, int32_t cout, int32_t relu_on, int32_t pool_rows, float *y,
+                    void *stream);
+
+/* lidar_sa_group_mlp_f32 with layer 1 applied per point beforehand: p (batch*n, p_stride)
+ * = [f, x] W1 + b1 for every point of the level, q (batch*m, p_stride) = centre W1_xyz
+ * (both via lidar_dense_f32, relu_on = 0, columns >= c1 ignored); a grouped row's layer 1
+ * is relu(p[k] - q[c]).  packed is
+ * the lidar_mlp_pack_f32 image of the whole branch (cfeat locates its layer-2 block).
+ * Same outputs as lidar_sa_group_mlp_f32 up to fp32 re-association. */
+int lidar_sa_group_mlp_pre_f32(lidar_handle *h, const float *p, int64_t p_stride, const float *q,
+                               const int32_t *idx, int64_t batch, int64_t n, int64_t m,
+                               int32_t nsample, int32_t cfeat, int32_t c1, int32_t c2, int32_t c3,
+                               const float *packed, float *out, int64_t out_stride,
+                               int64_t out_offset, void *stream);
+
 /* y (batch*m, ldy) columns [col0, col0+3) = xyz rows; columns [col0+3, ldy) zeroed —
  * builds group_all's input [feats, xyz, 0-pad] next to features already in y. */
 int lidar_concat_xyz_pad_f32(lidar_handle *h, const float *xyz, int64_t rows, float *y,

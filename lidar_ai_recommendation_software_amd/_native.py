@@ -52,6 +52,9 @@ SIGNATURES = {
     "lidar_mlp_packed_size_bf16": [I32, I32, I32, I32],
     "lidar_mlp_pack_bf16": [I32, I32, I32, I32, P, P, P, P, P, P, P],
     "lidar_dense_relu_f32": [P, P, I64, I32, P, P, I32, I32, P, P],
+    "lidar_dense_f32": [P, P, I64, I32, P, P, I32, I32, I32, P, P],
+    "lidar_sa_group_mlp_pre_f32": [P, P, I64, P, P, I64, I64, I64, I32, I32, I32, I32, I32, P, P,
+                                   I64, I64, P],
     "lidar_concat_xyz_pad_f32": [P, P, I64, P, I64, I64, P],
     "lidar_voxel_downsample_f32": [P, P, I64, F32, P, P, P, P, P],
     "lidar_dbscan_f64": [P, P, I64, F64, I32, P, P, P],

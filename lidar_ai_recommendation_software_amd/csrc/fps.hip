@@ -55,7 +55,6 @@ __device__ __forceinline__ float gap(float q, float lo, float hi)
     return q < lo ? __fsub_rn(lo, q) : (q > hi ? __fsub_rn(q, hi) : 0.0f);
 }
 
-constexpr int kBatch = 4;  // active buckets whose loads are issued together
 constexpr int kLoopWaves = kThreads / 64;
 
 // Update K active buckets of one owner slot (their loads issued together, their DPP

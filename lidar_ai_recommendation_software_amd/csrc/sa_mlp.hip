@@ -43,7 +43,12 @@ struct MlpShape {
     static constexpr int64_t size = W1 + W2 + W3 + C1 + C2 + C3;
 };
 
-template <int CF, int C1, int C2, int C3, int NS>
+// PRE: layer 1 was applied per POINT before grouping (P = [f, x] W1 + b1 over the level's
+// N points, Q = c W1_xyz over its M centres, both plain GEMMs, dense_kernel below), so
+// layer 1 of a grouped row is relu(P[k] - Q[c]) = relu(W1^T [x_k - c, f_k] + b1): 16x fewer
+// layer-1 rows (N vs M*nsample) for the cost of one fp32 re-association.  `feats` is P and
+// `centres` is Q (both with row stride feat_stride) and `packed` points at the layer-2 weights.
+template <int CF, int C1, int C2, int C3, int NS, bool PRE = false>
 __global__ __launch_bounds__(256) void sa_group_mlp_kernel(
     const float *__restrict__ xyz, const float *__restrict__ feats, int64_t feat_stride,
     const float *__restrict__ centres, const int32_t *__restrict__ idx, int n, int m,
@@ -78,7 +83,7 @@ __global__ __launch_bounds__(256) void sa_group_mlp_kernel(
         const float *pk = packed;
         asm volatile("" : "+s"(pk));
         const float *W1 = pk;
-        const float *W2 = W1 + S::W1;
+        const float *W2 = PRE ? pk : W1 + S::W1;
         const float *W3 = W2 + S::W2;
         const float *B1 = W3 + S::W3;
         const float *B2 = B1 + C1;
@@ -86,6 +91,20 @@ __global__ __launch_bounds__(256) void sa_group_mlp_kernel(
         const int64_t cc = c < total ? c : total - 1;
         const int64_t b = cc / m;
         const int64_t k = idx[cc * NS + s];
+        f32x16 y1[S::T1];
+        if constexpr (PRE) {
+            // y1[ti] reg 4j+i <- channel 32 ti + 8 j + 4 h + i of relu(P[k] - Q[c])
+            const f32x4 *pp = reinterpret_cast<const f32x4 *>(feats + (b * n + k) * feat_stride + 4 * h);
+            const f32x4 *qq = reinterpret_cast<const f32x4 *>(centres + cc * feat_stride + 4 * h);
+#pragma unroll
+            for (int ti = 0; ti < S::T1; ++ti)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const f32x4 a = pp[8 * ti + 2 * j], q = qq[8 * ti + 2 * j];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) y1[ti][4 * j + i] = relu(a[i] - q[i]);
+                }
+        } else {
         const float *pr = xyz + (b * n + k) * 3;
         const float *ce = centres + cc * 3;
         const float dx = pr[0] - ce[0], dy = pr[1] - ce[1], dz = pr[2] - ce[2];
@@ -110,7 +129,6 @@ __global__ __launch_bounds__(256) void sa_group_mlp_kernel(
         for (int q = CF / 2 + 2; q < S::S1P; ++q) x1[q] = 0.0f;
 
         // ---- layer 1 (channel rows x point columns)
-        f32x16 y1[S::T1];
 #pragma unroll
         for (int t = 0; t < S::T1; ++t) {
             __builtin_amdgcn_sched_barrier(0);
@@ -126,6 +144,7 @@ __global__ __launch_bounds__(256) void sa_group_mlp_kernel(
             for (int r = 0; r < 16; ++r) acc[r] = relu(acc[r] + B1[32 * t + rho(r) + 4 * h]);
             y1[t] = acc;
         }
+        }  // !PRE
         // ---- layer 2 (channel rows x point columns); y1 registers are the K operand
         f32x16 y2[S::T2];
 #pragma unroll
@@ -203,7 +222,7 @@ __global__ __launch_bounds__(256) void dense_relu_kernel(const float *__restrict
                                                          const float *__restrict__ w,
                                                          const float *__restrict__ bias,
                                                          int cout, int pool_rows,
-                                                         float *__restrict__ y)
+                                                         float *__restrict__ y, int act)
 {
     __shared__ float As[BK][BM];
     __shared__ float Bs[BK][BN];
@@ -254,7 +273,8 @@ __global__ __launch_bounds__(256) void dense_relu_kernel(const float *__restrict
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const int64_t row = row0 + wm * 64 + i * 32 + rho(r) + 4 * h;
-                    y[row * cout + c] = relu(acc[i][j][r] + bb);
+                    const float v = acc[i][j][r] + bb;
+                    y[row * cout + c] = act ? relu(v) : v;
                 }
         } else {
             float v = 0.0f;
@@ -288,7 +308,7 @@ typedef int (*launch_fn)(const float *, const float *, int64_t, const float *, c
                          int64_t, int64_t, int64_t, const float *, float *, int64_t, int64_t,
                          hipStream_t);
 
-template <int CF, int C1, int C2, int C3, int NS>
+template <int CF, int C1, int C2, int C3, int NS, bool PRE = false>
 int launch_sa(const float *xyz, const float *feats, int64_t fs, const float *centres,
               const int32_t *idx, int64_t batch, int64_t n, int64_t m, const float *packed,
               float *out, int64_t os, int64_t oo, hipStream_t s)
@@ -297,7 +317,7 @@ int launch_sa(const float *xyz, const float *feats, int64_t fs, const float *cen
     const int64_t units = NS >= 32 ? total : (total + 1) / 2;
     const int64_t blocks = (units + 3) / 4;
     REQUIRE(blocks <= 0x7fffffff, "sa_group_mlp: too many centres");
-    hipLaunchKernelGGL((sa_group_mlp_kernel<CF, C1, C2, C3, NS>), dim3((unsigned)blocks), dim3(256), 0,
+    hipLaunchKernelGGL((sa_group_mlp_kernel<CF, C1, C2, C3, NS, PRE>), dim3((unsigned)blocks), dim3(256), 0,
                        s, xyz, feats, fs, centres, idx, (int)n, (int)m, total, units, packed, out,
                        os, oo);
     LAUNCH_CHECK();
@@ -319,6 +339,14 @@ const Variant kVariants[] = {
     {320, 64, 64, 128, 32, launch_sa<320, 64, 64, 128, 32>},
     {320, 128, 128, 256, 64, launch_sa<320, 128, 128, 256, 64>},
     {320, 128, 128, 256, 128, launch_sa<320, 128, 128, 256, 128>},
+};
+
+// layer-1-per-point twins of the branches with point features (cf > 0)
+const Variant kPreVariants[] = {
+    {128, 128, 128, 256, 64, launch_sa<128, 128, 128, 256, 64, true>},
+    {320, 64, 64, 128, 32, launch_sa<320, 64, 64, 128, 32, true>},
+    {320, 128, 128, 256, 64, launch_sa<320, 128, 128, 256, 64, true>},
+    {320, 128, 128, 256, 128, launch_sa<320, 128, 128, 256, 128, true>},
 };
 
 int64_t packed_size(int cf, int c1, int c2, int c3)
@@ -404,23 +432,55 @@ LIDAR_EXPORT int lidar_sa_group_mlp_f32(lidar_handle *h, const float *xyz, const
                                      "combination — add a kVariants entry");
 }
 
+LIDAR_EXPORT int lidar_dense_f32(lidar_handle *h, const float *x, int64_t rows, int32_t k,
+                                 const float *w, const float *bias, int32_t cout, int32_t relu_on,
+                                 int32_t pool_rows, float *y, void *stream)
+{
+    REQUIRE(h && x && w && bias && y, "lidar_dense_f32: null pointer");
+    REQUIRE(rows % BM == 0 && k % BK == 0 && cout % BN == 0 && k > 0,
+            "lidar_dense_f32: rows % 128, k % 16, cout % 128 must be 0");
+    REQUIRE(pool_rows == 0 || (pool_rows % BM == 0 && rows % pool_rows == 0),
+            "lidar_dense_f32: pool_rows must be a multiple of 128 dividing rows");
+    REQUIRE(pool_rows == 0 || relu_on, "lidar_dense_f32: the fused max-pool needs relu (>= 0 outputs)");
+    if (rows == 0) return LIDAR_OK;
+    REQUIRE(rows / BM <= 65535, "lidar_dense_f32: too many rows");
+    HIP_TRY(hipSetDevice(h->device));
+    hipLaunchKernelGGL(dense_relu_kernel, dim3(cout / BN, (unsigned)(rows / BM)), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), x, (int)k, w, bias, (int)cout,
+                       (int)pool_rows, y, relu_on ? 1 : 0);
+    LAUNCH_CHECK();
+    return LIDAR_OK;
+}
+
 LIDAR_EXPORT int lidar_dense_relu_f32(lidar_handle *h, const float *x, int64_t rows, int32_t k,
                                       const float *w, const float *bias, int32_t cout,
                                       int32_t pool_rows, float *y, void *stream)
 {
-    REQUIRE(h && x && w && bias && y, "lidar_dense_relu_f32: null pointer");
-    REQUIRE(rows % BM == 0 && k % BK == 0 && cout % BN == 0 && k > 0,
-            "lidar_dense_relu_f32: rows % 128, k % 16, cout % 128 must be 0");
-    REQUIRE(pool_rows == 0 || (pool_rows % BM == 0 && rows % pool_rows == 0),
-            "lidar_dense_relu_f32: pool_rows must be a multiple of 128 dividing rows");
-    if (rows == 0) return LIDAR_OK;
-    REQUIRE(rows / BM <= 65535, "lidar_dense_relu_f32: too many rows");
+    return lidar_dense_f32(h, x, rows, k, w, bias, cout, 1, pool_rows, y, stream);
+}
+
+LIDAR_EXPORT int lidar_sa_group_mlp_pre_f32(lidar_handle *h, const float *p, int64_t p_stride,
+                                            const float *q, const int32_t *idx, int64_t batch,
+                                            int64_t n, int64_t m, int32_t nsample, int32_t cfeat,
+                                            int32_t c1, int32_t c2, int32_t c3, const float *packed,
+                                            float *out, int64_t out_stride, int64_t out_offset,
+                                            void *stream)
+{
+    REQUIRE(h && p && q && idx && packed && out, "lidar_sa_group_mlp_pre_f32: null pointer");
+    REQUIRE(batch >= 0 && n >= 1 && m >= 1, "lidar_sa_group_mlp_pre_f32: bad sizes");
+    REQUIRE(p_stride >= c1 && p_stride % 4 == 0, "lidar_sa_group_mlp_pre_f32: p_stride must be >= c1, % 4");
+    REQUIRE(out_offset >= 0 && out_offset + c3 <= out_stride,
+            "lidar_sa_group_mlp_pre_f32: output columns exceed out_stride");
+    if (batch == 0) return LIDAR_OK;
     HIP_TRY(hipSetDevice(h->device));
-    hipLaunchKernelGGL(dense_relu_kernel, dim3(cout / BN, (unsigned)(rows / BM)), dim3(256), 0,
-                       static_cast<hipStream_t>(stream), x, (int)k, w, bias, (int)cout,
-                       (int)pool_rows, y);
-    LAUNCH_CHECK();
-    return LIDAR_OK;
+    // the packed image is lidar_mlp_pack_f32's: skip its layer-1 block
+    const int64_t s1p = ((int64_t)cfeat / 2 + 2 + 3) / 4 * 4;
+    const float *w2 = packed + (int64_t)(c1 / 32) * s1p * 64;
+    for (const Variant &v : kPreVariants)
+        if (v.cf == cfeat && v.c1 == c1 && v.c2 == c2 && v.c3 == c3 && v.ns == nsample)
+            return v.fn(nullptr, p, p_stride, q, idx, batch, n, m, w2, out, out_stride, out_offset,
+                        static_cast<hipStream_t>(stream));
+    return lidar::fail(LIDAR_EINVAL, "lidar_sa_group_mlp_pre_f32: unsupported (cfeat, widths, nsample)");
 }
 
 LIDAR_EXPORT int lidar_concat_xyz_pad_f32(lidar_handle *h, const float *xyz, int64_t rows,

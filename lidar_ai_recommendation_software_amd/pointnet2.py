@@ -156,11 +156,86 @@ def group_mlp(xyz, feats, new_xyz, idx, packed, widths, out=None, out_offset=0, 
     c1, c2, c3 = widths
     if out is None:
         out = torch.empty((B, M, c3), dtype=torch.float32, device=xyz.device)
-    _dev_check(xyz, feats, new_xyz, idx, packed, out)
+    _dev_check(xyz, new_xyz, idx, packed, out)
+    if feats is not None and (not feats.is_cuda or feats.stride(2) != 1
+                              or feats.stride(0) != feats.shape[1] * feats.stride(1)):
+        raise ValueError("group_mlp: feats must be CUDA rows with unit channel stride")
     nat.call("lidar_sa_group_mlp_bf16" if bf16 else "lidar_sa_group_mlp_f32", nat.handle(xyz.device.index),
              nat.ptr(xyz), nat.ptr(feats),
-             cfeat, nat.ptr(new_xyz), nat.ptr(idx), B, N, M, ns, cfeat, c1, c2, c3,
+             feats.stride(1) if feats is not None else 0, nat.ptr(new_xyz), nat.ptr(idx), B, N, M, ns, cfeat, c1, c2, c3,
              nat.ptr(packed), nat.ptr(out), out.shape[-1], out_offset, nat.stream_ptr())
+    return out
+
+
+def group_mlp_pre(p, q, idx, n, packed, cfeat, widths, out, out_offset=0):
+    """group_mlp with layer 1 applied per point beforehand (layer1_per_point):
+    p rows b*n + k = [f, x] W1 + b1, q rows b*M + c = centre W1_xyz; idx (B, M, ns)
+    -> out[..., off:off+c3] (out (B, M, stride))."""
+    B, M, ns = idx.shape
+    c1, c2, c3 = widths
+    if p.shape[0] < B * n or q.shape[0] < B * M or p.shape[1] < c1 or q.shape[1] != p.shape[1]:
+        raise ValueError("group_mlp_pre: p/q shapes do not match the batch")
+    _dev_check(p, q, idx, packed, out)
+    nat.call("lidar_sa_group_mlp_pre_f32", nat.handle(p.device.index), nat.ptr(p), p.shape[1], nat.ptr(q),
+             nat.ptr(idx), B, n, M, ns, cfeat, c1, c2, c3, nat.ptr(packed), nat.ptr(out),
+             out.shape[-1], out_offset, nat.stream_ptr())
+    return out
+
+
+def layer1_weights(layer, cfeat, to_dev):
+    """(W1 (3 + cfeat, c1), b1) -> the per-point GEMM operands of layer1_per_point:
+    w1 rows [f..., x, y, z, 0-pad] (k padded to 16), wq rows [x, y, z, 0-pad] (16), columns
+    zero-padded to a multiple of 128 (the dense kernel's tile)."""
+    w1, b1 = layer
+    c1 = w1.shape[1]
+    kp = (cfeat + 3 + 15) // 16 * 16
+    cp = (c1 + 127) // 128 * 128
+    w1p = np.zeros((kp, cp), np.float32)
+    w1p[:cfeat, :c1] = w1[3:]
+    w1p[cfeat:cfeat + 3, :c1] = w1[:3]
+    wq = np.zeros((16, cp), np.float32)
+    wq[:3, :c1] = w1[:3]
+    bp = np.zeros(cp, np.float32)
+    bp[:c1] = b1
+    return {"w1": to_dev(w1p), "b1": to_dev(bp), "wq": to_dev(wq), "zero": to_dev(np.zeros(cp, np.float32))}
+
+
+def layer1_per_point(x_rows, xyz, cfeat, new_xyz, branches):
+    """Layer 1 of every branch of a level, per point instead of per grouped row.
+
+    x_rows: (R, kp) padded rows [f (cfeat), x, y, z, 0...] of the level's B*N points
+    (R = B*N rounded up to 128; the previous level wrote f in place), xyz (B, N, 3);
+    new_xyz (B, M, 3).  Returns per branch (P, Q): P = x_rows W1' + b1 (R, c1),
+    Q = [c, 0] W1_xyz' (B*M rounded to 128, c1), both without ReLU (columns padded to a
+    multiple of 128 with zero weights)."""
+    B, N, _ = xyz.shape
+    M = new_xyz.shape[1]
+    R, kp = x_rows.shape
+    dev = xyz.device
+    h = nat.handle(dev.index)
+    nat.call("lidar_concat_xyz_pad_f32", h, nat.ptr(xyz), B * N, nat.ptr(x_rows), kp, cfeat, nat.stream_ptr())
+    rq = (B * M + 127) // 128 * 128
+    cpad = torch.zeros((rq, 16), dtype=torch.float32, device=dev)
+    nat.call("lidar_concat_xyz_pad_f32", h, nat.ptr(new_xyz), B * M, nat.ptr(cpad), 16, 0, nat.stream_ptr())
+    out = []
+    for br in branches:
+        pre = br["pre"]
+        P = dense(x_rows, pre["w1"], pre["b1"], relu=False)
+        Q = dense(cpad, pre["wq"], pre["zero"], relu=False)
+        out.append((P, Q))
+    return out
+
+
+def dense(x, w, b, relu=True, pool_rows=0, out=None):
+    """x (rows, k) @ w (k, cout) + b [-> ReLU] [-> max over runs of pool_rows rows]."""
+    rows, k = x.shape
+    cout = w.shape[1]
+    if out is None:
+        shape = (rows // pool_rows, cout) if pool_rows else (rows, cout)
+        out = (torch.zeros if pool_rows else torch.empty)(shape, dtype=torch.float32, device=x.device)
+    _dev_check(x, w, b, out)
+    nat.call("lidar_dense_f32", nat.handle(x.device.index), nat.ptr(x), rows, k, nat.ptr(w),
+             nat.ptr(b), cout, 1 if relu else 0, pool_rows, nat.ptr(out), nat.stream_ptr())
     return out
 
 
@@ -204,9 +279,11 @@ class PointNet2Backbone:
     """SSG / MSG PointNet++ encoder on liblidar_amd.  ``forward(xyz)`` -> global feature
     (B, C_last) plus the per-level (new_xyz, features, fps_idx)."""
 
-    def __init__(self, cfg=SSG, weights=None, device="cuda", seed=0, dtype="f32"):
+    def __init__(self, cfg=SSG, weights=None, device="cuda", seed=0, dtype="f32", pre_layer1=True):
         """dtype "bf16": the SA branches run on bf16 MFMA (inputs/activations/weights rounded
-        to bf16, fp32 accumulation; BASELINE configs[4]); group_all stays fp32."""
+        to bf16, fp32 accumulation; BASELINE configs[4]); group_all stays fp32.
+        pre_layer1 (fp32, levels with point features): layer 1 runs per point as a GEMM
+        and the fused kernel starts at layer 2 (layer1_per_point / group_mlp_pre)."""
         if dtype not in ("f32", "bf16"):
             raise ValueError("dtype must be 'f32' or 'bf16'")
         self.bf16 = dtype == "bf16"
@@ -228,12 +305,21 @@ class PointNet2Backbone:
                                     "w": [t(w1p), t(w2), t(w3)], "b": [t(b1), t(b2), t(b3)]})
                 cfeat = w3.shape[1]
             else:
+                pre = pre_layer1 and not self.bf16 and cfeat > 0
+                kp = (cfeat + 3 + 15) // 16 * 16
+                t = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).to(self.device)
                 branches = []
                 for (r, ns, widths, layers) in zip(lvl["radii"], lvl["nsamples"], lvl["mlps"], wl):
                     pk = pack_branch_bf16(layers, cfeat) if self.bf16 else pack_branch(layers, cfeat)
                     packed = torch.from_numpy(pk).to(self.device)
-                    branches.append({"r": r, "ns": ns, "widths": widths, "packed": packed})
-                self.levels.append({"div": lvl["npoint_div"], "branches": branches, "cfeat": cfeat})
+                    br = {"r": r, "ns": ns, "widths": widths, "packed": packed}
+                    if pre:
+                        br["pre"] = layer1_weights(layers[0], cfeat, t)
+                    branches.append(br)
+                entry = {"div": lvl["npoint_div"], "branches": branches, "cfeat": cfeat}
+                if pre:
+                    entry.update(pre=True, k=kp)
+                self.levels.append(entry)
                 cfeat = sum(w[-1] for w in lvl["mlps"])
         self.out_channels = cfeat
         self.timers = None  # set to a _Timers() to time every launch
@@ -246,11 +332,12 @@ class PointNet2Backbone:
         B, N, _ = xyz.shape
         N0 = N  # npoint_div is relative to the input frame (N/16, N/64)
         feats = None
+        rows = None  # flat padded (R, k) rows behind `feats` when the next level reads them
         out_levels = []
         fz = None  # previous level's FPS first_zero (nested-FPS shortcut)
         for li, lvl in enumerate(self.levels):
             if lvl.get("group_all"):
-                return self._group_all(xyz, feats, lvl), out_levels
+                return self._group_all(xyz, feats, lvl, rows), out_levels
             M = max(1, N0 // lvl["div"])
             if li == 0 and pre_fps is not None:
                 idx, new_xyz, nfz = pre_fps
@@ -261,9 +348,17 @@ class PointNet2Backbone:
             fz = nfz
             ctot = sum(br["widths"][-1] for br in lvl["branches"])
             nxt = self.levels[li + 1] if li + 1 < len(self.levels) else None
-            # the level feeding group_all writes straight into its padded input rows
-            stride = nxt["k"] if nxt is not None and nxt.get("group_all") else ctot
-            out = torch.empty((B, M, stride), dtype=torch.float32, device=xyz.device)
+            # a level feeding group_all or a per-point layer 1 writes straight into the
+            # next level's padded input rows [f, x, y, z, 0-pad] (R = B*M rounded to 128)
+            padded = nxt is not None and (nxt.get("group_all") or nxt.get("pre"))
+            stride = nxt["k"] if padded else ctot
+            R = (B * M + 127) // 128 * 128 if padded else B * M
+            out_rows = torch.empty((R, stride), dtype=torch.float32, device=xyz.device)
+            out = out_rows[:B * M].view(B, M, stride)
+            pq = None
+            if lvl.get("pre"):
+                pq = _call(self.timers, f"sa{li + 1}_layer1_points", layer1_per_point, rows, xyz, lvl["cfeat"],
+                           new_xyz, lvl["branches"])
             off = 0
             for bi_, br in enumerate(lvl["branches"]):
                 tag = f"sa{li + 1}" + (f"_b{bi_}" if len(lvl["branches"]) > 1 else "")
@@ -271,20 +366,28 @@ class PointNet2Backbone:
                     gidx = pre_bq[bi_]
                 else:
                     gidx = _call(self.timers, f"{tag}_ball_query", ball_query, br["r"], br["ns"], xyz, new_xyz)
-                _call(self.timers, f"{tag}_group_mlp", group_mlp, xyz, feats, new_xyz, gidx, br["packed"],
-                      br["widths"], out=out, out_offset=off, bf16=self.bf16)
+                if pq is not None:
+                    _call(self.timers, f"{tag}_group_mlp", group_mlp_pre, pq[bi_][0], pq[bi_][1], gidx, N,
+                          br["packed"], lvl["cfeat"], br["widths"], out=out, out_offset=off)
+                else:
+                    _call(self.timers, f"{tag}_group_mlp", group_mlp, xyz, feats, new_xyz, gidx, br["packed"],
+                          br["widths"], out=out, out_offset=off, bf16=self.bf16)
                 off += br["widths"][-1]
             if keep_levels:
                 out_levels.append((new_xyz, out[..., :ctot], idx))
-            xyz, feats = new_xyz, out
+            xyz, feats, rows = new_xyz, (out[..., :ctot] if padded else out), out_rows
+            N = M
         return feats, out_levels
 
-    def _group_all(self, xyz, feats, lvl):
+    def _group_all(self, xyz, feats, lvl, rows=None):
         B, M, _ = xyz.shape
         kp, cfeat = lvl["k"], lvl["cfeat"]
-        x = feats if feats is not None and feats.shape[-1] == kp else None
+        # the previous level wrote its features into padded rows [f, x, y, z, 0-pad]
+        x = rows[:B * M].view(B, M, kp) if rows is not None and rows.shape[1] == kp else None
         if x is None:  # previous level did not pre-pad (only when group_all is level 0)
             x = torch.empty((B, M, kp), dtype=torch.float32, device=xyz.device)
+            if feats is not None:
+                x[..., :cfeat] = feats
         nat.call("lidar_concat_xyz_pad_f32", nat.handle(xyz.device.index), nat.ptr(xyz), B * M,
                  nat.ptr(x), kp, cfeat, nat.stream_ptr())
         rows = B * M

@@ -94,6 +94,52 @@ def test_group_mlp(cuda, cfg_name, level, branch):
         feat_close(got[bi], want, f"{cfg_name} L{level} br{branch} frame {bi}")
 
 
+@pytest.mark.parametrize("cfg_name,level,branch", [("ssg", 1, 0), ("msg", 1, 0), ("msg", 1, 1), ("msg", 1, 2)])
+def test_group_mlp_layer1_per_point(cuda, cfg_name, level, branch):
+    """layer 1 as per-point / per-centre GEMMs + the fused kernel from layer 2 on
+    (relu(P[k] - Q[c]) = relu(W1^T [x_k - c, f_k] + b1)) vs the oracle's grouped rows."""
+    cfg = pn.CONFIGS[cfg_name]
+    w = pn.init_weights(cfg, seed=4)
+    lvl = cfg["levels"][level]
+    layers = w[level][branch]
+    cfeat = layers[0][0].shape[0] - 3
+    r, ns, widths = lvl["radii"][branch], lvl["nsamples"][branch], lvl["mlps"][branch]
+    B, N, M = 2, 2000, 100  # neither B*N nor B*M a multiple of 128: padded GEMM rows
+    rng = np.random.default_rng(8)
+    x = unit_frames(B, N, 10)
+    f = np.abs(rng.standard_normal((B, N, cfeat))).astype(np.float32)  # post-ReLU-like features
+    c = x[:, :M].copy()
+    gi = tier_n.ball_query(x, c, r, ns)
+    kp = (cfeat + 3 + 15) // 16 * 16
+    R = (B * N + 127) // 128 * 128
+    rows = torch.zeros((R, kp), dtype=torch.float32, device=cuda)
+    rows[:B * N, :cfeat] = torch.from_numpy(f.reshape(-1, cfeat)).to(cuda)
+    w1, b1 = layers[0]
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).to(cuda)
+    br = {"pre": pn.layer1_weights(layers[0], cfeat, T)}
+    (P, Q), = pn.layer1_per_point(rows, T(x), cfeat, T(c), [br])
+    packed = torch.from_numpy(pn.pack_branch(layers, cfeat)).to(cuda)
+    out = torch.empty((B, M, widths[-1]), dtype=torch.float32, device=cuda)
+    gti = torch.from_numpy(gi).to(cuda)
+    pn.group_mlp_pre(P, Q, gti, N, packed, cfeat, widths, out)
+    got = out.cpu().numpy()
+    for bi in range(B):
+        want = tier_n.mlp_maxpool(tier_n.group(x[bi], f[bi], c[bi], gi[bi]), layers, ns)
+        feat_close(got[bi], want, f"{cfg_name} L{level} br{branch} frame {bi} (layer 1 per point)")
+    # the per-point rows themselves: P = [f, x] W1 + b1
+    Pn = P[:B * N, :widths[0]].cpu().numpy()
+    feat_close(Pn, np.concatenate([x.reshape(-1, 3), f.reshape(-1, cfeat)], 1) @ w1 + b1, "P rows")
+
+
+def test_dense_no_relu(cuda):
+    rng = np.random.default_rng(2)
+    x = rng.standard_normal((256, 144)).astype(np.float32)
+    w = (rng.standard_normal((144, 128)) / 12).astype(np.float32)
+    b = rng.standard_normal(128).astype(np.float32)
+    T = lambda a: torch.from_numpy(a).to(cuda)
+    feat_close(pn.dense(T(x), T(w), T(b), relu=False).cpu().numpy(), x @ w + b, "dense no relu")
+
+
 def test_dense_relu_and_pool(cuda):
     rng = np.random.default_rng(1)
     x = rng.standard_normal((512, 272)).astype(np.float32)
@@ -107,10 +153,12 @@ def test_dense_relu_and_pool(cuda):
     feat_close(pooled, want.reshape(2, 256, 256).max(axis=1), "dense pooled")
 
 
-@pytest.mark.parametrize("cfg_name,n", [("ssg", 16384), ("ssg", 65536), ("sa1", 16384), ("msg", 16384)])
-def test_backbone_vs_oracle(cuda, cfg_name, n):
+@pytest.mark.parametrize("cfg_name,n,pre", [("ssg", 16384, True), ("ssg", 65536, True), ("sa1", 16384, True),
+                                            ("msg", 16384, True), ("ssg", 16384, False), ("msg", 16384, False),
+                                            ("ssg", 5000, True)])
+def test_backbone_vs_oracle(cuda, cfg_name, n, pre):
     cfg = pn.CONFIGS[cfg_name]
-    bb = pn.PointNet2Backbone(cfg, device=cuda, seed=0)
+    bb = pn.PointNet2Backbone(cfg, device=cuda, seed=0, pre_layer1=pre)
     x = unit_frames(1, n, 21)
     g, levels = bb.forward(torch.from_numpy(x).to(cuda), keep_levels=True)
     torch.cuda.synchronize()

@@ -13,7 +13,8 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "liblidar_amd.so")
+# LIDAR_AMD_LIB: load another build of the library (kernel A/B experiments, tools/)
+LIB_PATH = os.environ.get("LIDAR_AMD_LIB") or os.path.join(_HERE, "liblidar_amd.so")
 
 LIDAR_ERRORS = {-1: "invalid argument", -2: "HIP runtime error", -3: "out of memory",
                 -4: "unsupported device"}

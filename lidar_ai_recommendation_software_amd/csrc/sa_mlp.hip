@@ -13,6 +13,7 @@
 // (2) dense_relu_kernel: LDS-tiled 128x128x16 MFMA GEMM with bias+ReLU epilogue and an
 //     optional fused row-group max-pool (group_all's SA3), for layers too wide to keep
 //     in registers.
+#include <cstdlib>
 #include <vector>
 
 #include "common.hpp"
@@ -459,6 +460,10 @@ LIDAR_EXPORT int lidar_dense_relu_f32(lidar_handle *h, const float *x, int64_t r
     return lidar_dense_f32(h, x, rows, k, w, bias, cout, 1, pool_rows, y, stream);
 }
 
+int lidar_sa_pre_lds_dispatch(int cfeat, int c1, int c2, int c3, int ns, const float *p, int64_t stride,
+                              const float *q, const int32_t *idx, int64_t batch, int64_t n, int64_t m,
+                              const float *w23, float *out, int64_t os, int64_t oo, hipStream_t s);
+
 LIDAR_EXPORT int lidar_sa_group_mlp_pre_f32(lidar_handle *h, const float *p, int64_t p_stride,
                                             const float *q, const int32_t *idx, int64_t batch,
                                             int64_t n, int64_t m, int32_t nsample, int32_t cfeat,
@@ -476,6 +481,13 @@ LIDAR_EXPORT int lidar_sa_group_mlp_pre_f32(lidar_handle *h, const float *p, int
     // the packed image is lidar_mlp_pack_f32's: skip its layer-1 block
     const int64_t s1p = ((int64_t)cfeat / 2 + 2 + 3) / 4 * 4;
     const float *w2 = packed + (int64_t)(c1 / 32) * s1p * 64;
+    static const bool no_lds = getenv("LIDAR_PRE_NO_LDS") != nullptr;  // A/B tuning knob
+    if (!no_lds) {
+        const int rc = lidar_sa_pre_lds_dispatch(cfeat, c1, c2, c3, nsample, p, p_stride, q, idx, batch, n,
+                                                 m, w2, out, out_stride, out_offset,
+                                                 static_cast<hipStream_t>(stream));
+        if (rc != -1) return rc;
+    }
     for (const Variant &v : kPreVariants)
         if (v.cf == cfeat && v.c1 == c1 && v.c2 == c2 && v.c3 == c3 && v.ns == nsample)
             return v.fn(nullptr, p, p_stride, q, idx, batch, n, m, w2, out, out_stride, out_offset,

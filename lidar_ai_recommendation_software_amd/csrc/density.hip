@@ -99,6 +99,52 @@ __device__ int block_flag_scan(BlockScratch &s, bool f, int *total)
     return base + inwave;
 }
 
+// ---- index-order fp64 chains with the rows streamed through LDS
+// numpy's axis-0 reductions of a row-major (n, 3) array are sequential per column, so the
+// result depends on every rounding in index order: the chain itself cannot be split.  What
+// can be removed is the memory latency: waves 1..15 stage 1024-row chunks into LDS (double
+// buffered) while lanes 0..2 of wave 0 (lane c = column c) run the dependent adds out of
+// LDS.  `step(c, v, a0, a1)` advances column c's accumulators by one row.
+constexpr int kSeqRows = 1024;
+struct SeqStage {
+    double v[2][kSeqRows * 3];
+};
+
+template <class Step>
+__device__ void block_seq_chain(const double *x, int64_t n, SeqStage &st, Step step, double &a0, double &a1)
+{
+    const int tid = threadIdx.x;
+    const int64_t nch = (n + kSeqRows - 1) / kSeqRows;
+    auto stage = [&](int64_t k) {
+        if (tid < 64 || k >= nch) return;  // wave 0 never waits on global loads
+        const int64_t r0 = k * kSeqRows;
+        const int64_t cnt = (n - r0 < kSeqRows ? n - r0 : kSeqRows) * 3;
+        double *d = st.v[k & 1];
+        const double *src = x + 3 * r0;
+        for (int64_t e = tid - 64; e < cnt; e += kT - 64) d[e] = src[e];
+    };
+    stage(0);
+    __syncthreads();
+    for (int64_t k = 0; k < nch; ++k) {
+        stage(k + 1);
+        if (tid < 3) {
+            const int64_t r0 = k * kSeqRows;
+            const int rows = (int)(n - r0 < kSeqRows ? n - r0 : kSeqRows);
+            const double *b = st.v[k & 1] + tid;
+            int i = 0;
+            for (; i + 16 <= rows; i += 16) {
+                double v[16];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) v[u] = b[3 * (i + u)];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) step(tid, v[u], a0, a1);
+            }
+            for (; i < rows; ++i) step(tid, b[3 * i], a0, a1);
+        }
+        __syncthreads();
+    }
+}
+
 __device__ __forceinline__ uint64_t ordkey(double v)
 {
     uint64_t u = (uint64_t)__double_as_longlong(v);
@@ -110,42 +156,6 @@ __device__ __forceinline__ double unordkey(uint64_t k)
     return __longlong_as_double((long long)u);
 }
 
-// sequential (numpy axis-0) sum of column c of an (n, 3) array: lane-serial, unrolled loads
-__device__ double seq_sum_col(const double *x, int64_t n, int c)
-{
-    double s = 0.0;
-    int64_t i = 0;
-    for (; i + 8 <= n; i += 8) {
-        double v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = x[3 * (i + u) + c];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) s = dadd(s, v[u]);
-    }
-    for (; i < n; ++i) s = dadd(s, x[3 * i + c]);
-    return s;
-}
-// sequential sum of (x - m)^2
-__device__ double seq_sqdev_col(const double *x, int64_t n, int c, double m)
-{
-    double s = 0.0;
-    int64_t i = 0;
-    for (; i + 8 <= n; i += 8) {
-        double v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = x[3 * (i + u) + c];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const double d = dsub(v[u], m);
-            s = dadd(s, dmul(d, d));
-        }
-    }
-    for (; i < n; ++i) {
-        const double d = dsub(x[3 * i + c], m);
-        s = dadd(s, dmul(d, d));
-    }
-    return s;
-}
 
 // ------------------------------------------------------------------ preprocess
 __global__ __launch_bounds__(kT) void preprocess_kernel(const double *__restrict__ xyz, int64_t n,
@@ -158,6 +168,7 @@ __global__ __launch_bounds__(kT) void preprocess_kernel(const double *__restrict
                                                         double *__restrict__ S)
 {
     __shared__ BlockScratch s;
+    __shared__ SeqStage st;
     const int tid = threadIdx.x;
 
     // ---- A: colours over ALL points (data_processing.py:143-147)
@@ -171,11 +182,18 @@ __global__ __launch_bounds__(kT) void preprocess_kernel(const double *__restrict
     const double denom = dadd(dsub(zmax, zmin), 1e-10);
 
     // ---- B: mean / std with numpy's sequential axis-0 sums (:151-152)
-    if (tid < 3) {
-        const double mean = ddiv(seq_sum_col(xyz, n, tid), (double)n);
-        const double var = ddiv(seq_sqdev_col(xyz, n, tid, mean), (double)n);
-        s.bc[tid] = mean;
-        s.bc[3 + tid] = __dsqrt_rn(var);
+    {
+        double sum = 0.0, unused = 0.0;
+        block_seq_chain(xyz, n, st, [](int, double v, double &a, double &) { a = dadd(a, v); }, sum, unused);
+        if (tid < 3) s.bc[tid] = ddiv(sum, (double)n);
+        __syncthreads();
+        const double mc = tid < 3 ? s.bc[tid] : 0.0;
+        double sq = 0.0;
+        block_seq_chain(xyz, n, st, [mc](int, double v, double &a, double &) {
+            const double d = dsub(v, mc);
+            a = dadd(a, dmul(d, d));
+        }, sq, unused);
+        if (tid < 3) s.bc[3 + tid] = __dsqrt_rn(ddiv(sq, (double)n));
     }
     __syncthreads();
     double mean[3], thr[3];
@@ -391,16 +409,21 @@ __global__ __launch_bounds__(kT) void preprocess_kernel(const double *__restrict
     __syncthreads();
 
     // ---- G: StandardScaler fit (sklearn _incremental_mean_and_var, zero prior) (:190-191)
-    if (tid < 3) {
+    {
         const double nn = (double)nng;
-        const double sum = seq_sum_col(sc, nng, tid);
-        const double T = ddiv(sum, nn);
+        double sum = 0.0, unused = 0.0;
+        block_seq_chain(sc, nng, st, [](int, double v, double &a, double &) { a = dadd(a, v); }, sum, unused);
+        if (tid < 3) s.bc[6 + tid] = ddiv(sum, nn);
+        __syncthreads();
+        const double Tc = tid < 3 ? s.bc[6 + tid] : 0.0;
         double corr = 0.0, un = 0.0;
-        for (int64_t i = 0; i < nng; ++i) {
-            const double d = dsub(sc[3 * i + tid], T);
-            corr = dadd(corr, d);
-            un = dadd(un, dmul(d, d));
-        }
+        block_seq_chain(sc, nng, st, [Tc](int, double v, double &cr, double &u) {
+            const double d = dsub(v, Tc);
+            cr = dadd(cr, d);
+            u = dadd(u, dmul(d, d));
+        }, corr, un);
+        if (tid < 3) {
+        const double T = Tc;
         un = dsub(un, ddiv(dmul(corr, corr), nn));
         const double var = ddiv(un, nn);
         const double e = 2.220446049250313e-16;
@@ -408,6 +431,7 @@ __global__ __launch_bounds__(kT) void preprocess_kernel(const double *__restrict
         const double scale = var <= ub ? 1.0 : __dsqrt_rn(var);
         s.bc[6 + tid] = T;
         s.bc[9 + tid] = scale;
+        }
     }
     __syncthreads();
     double smean[3], sscale[3];
@@ -436,10 +460,20 @@ __global__ __launch_bounds__(kT) void preprocess_kernel(const double *__restrict
     __threadfence_block();
     __syncthreads();
     // ---- I: eps = max(0.2, min(0.5, mean(std(scaled, axis=0)) * 0.5)) (:194-195)
-    if (tid < 3) {
+    {
         const double nn = (double)nng;
-        const double m = ddiv(seq_sum_col(sc, nng, tid), nn);
-        s.bc[12 + tid] = __dsqrt_rn(ddiv(seq_sqdev_col(sc, nng, tid, m), nn));
+        double sum = 0.0, unused = 0.0;
+        block_seq_chain(sc, nng, st, [](int, double v, double &a, double &) { a = dadd(a, v); }, sum, unused);
+        if (tid < 3) s.bc[12 + tid] = ddiv(sum, nn);
+        __syncthreads();
+        const double mc = tid < 3 ? s.bc[12 + tid] : 0.0;
+        double sq = 0.0;
+        block_seq_chain(sc, nng, st, [mc](int, double v, double &a, double &) {
+            const double d = dsub(v, mc);
+            a = dadd(a, dmul(d, d));
+        }, sq, unused);
+        __syncthreads();
+        if (tid < 3) s.bc[12 + tid] = __dsqrt_rn(ddiv(sq, nn));
     }
     __syncthreads();
     if (tid == 0) {
@@ -819,42 +853,53 @@ __global__ void scatter_labels2_kernel(const double *S, const int64_t *ng_labels
 // ------------------------------------------------------------------ people
 // one wavefront per cluster scans the frame in index order: ballot the members of each
 // 64-point chunk, then add them lane by lane — numpy's sequential axis-0 order
-__global__ __launch_bounds__(256) void people_kernel(const double *xyz, const int64_t *labels, int64_t n,
-                                                     const int64_t *kdev, double *out)
+// One workgroup per cluster: waves 1..15 compact the cluster's members of a 960-point
+// chunk (index order: wave w holds points [64(w-1), 64w) of the chunk, ballot-ranked) into
+// LDS, double-buffered; lanes 0 / 1 of wave 0 run the x / y chains in index order, as
+// np.mean of the member rows does (sequential axis-0 sums starting from the first row).
+__global__ __launch_bounds__(kT) void people_kernel(const double *xyz, const int64_t *labels, int64_t n,
+                                                    const int64_t *kdev, double *out)
 {
-    const int lane = threadIdx.x & 63;
+    constexpr int kChunk = kT - 64;
+    __shared__ double mem[2][kChunk * 2];
+    __shared__ int wcnt[2][kW];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int64_t K = *kdev;
-    const int64_t nw = (int64_t)gridDim.x * 4;
-    for (int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); c < K; c += nw) {
-        double sx = 0.0, sy = 0.0;
-        int64_t cnt = 0;
-        for (int64_t b0 = 0; b0 < n; b0 += 64) {
-            const int64_t i = b0 + lane;
+    const int64_t nch = (n + kChunk - 1) / kChunk;
+    for (int64_t c = blockIdx.x; c < K; c += gridDim.x) {
+        auto stage = [&](int64_t k) {
+            if (wave == 0 || k >= nch) return;
+            const int64_t i = k * kChunk + (tid - 64);
             const bool hit = i < n && labels[i] == c;
-            double x = 0.0, y = 0.0;
+            const uint64_t m = __ballot(hit);
+            if (lane == 0) wcnt[k & 1][wave] = __popcll(m);
             if (hit) {
-                x = xyz[3 * i];
-                y = xyz[3 * i + 1];
+                const int r = (wave - 1) * 64 + __popcll(m & ((1ull << lane) - 1));
+                mem[k & 1][2 * r] = xyz[3 * i];
+                mem[k & 1][2 * r + 1] = xyz[3 * i + 1];
             }
-            uint64_t m = __ballot(hit);
-            while (m) {
-                const int b = __ffsll((unsigned long long)m) - 1;
-                m &= m - 1;
-                const double vx = __shfl(x, b, 64), vy = __shfl(y, b, 64);
-                if (cnt == 0) {
-                    sx = vx;
-                    sy = vy;
-                } else {
-                    sx = dadd(sx, vx);
-                    sy = dadd(sy, vy);
+        };
+        double acc = 0.0;
+        int64_t cnt = 0;
+        stage(0);
+        __syncthreads();
+        for (int64_t k = 0; k < nch; ++k) {
+            stage(k + 1);
+            if (tid < 2) {
+                const double *b = mem[k & 1] + tid;
+                for (int w = 1; w < kW; ++w) {
+                    const int m = wcnt[k & 1][w];
+                    const double *bw = b + 2 * (w - 1) * 64;
+                    for (int j = 0; j < m; ++j) {
+                        const double v = bw[2 * j];
+                        acc = cnt == 0 ? v : dadd(acc, v);
+                        ++cnt;
+                    }
                 }
-                ++cnt;
             }
+            __syncthreads();
         }
-        if (lane == 0) {
-            out[2 * c] = ddiv(sx, (double)cnt);
-            out[2 * c + 1] = ddiv(sy, (double)cnt);
-        }
+        if (tid < 2) out[2 * c + tid] = ddiv(acc, (double)cnt);
     }
 }
 
@@ -1155,7 +1200,7 @@ LIDAR_EXPORT int lidar_people_f64(lidar_handle *h, const double *xyz, const int6
     HIP_TRY(hipMemsetAsync(kd, 0, sizeof(int64_t), s));
     const unsigned gp = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 1024));
     hipLaunchKernelGGL(max_label_kernel, dim3(gp), dim3(256), 0, s, labels, n, kd);
-    hipLaunchKernelGGL(people_kernel, dim3(1024), dim3(256), 0, s, xyz, labels, n, kd, people);
+    hipLaunchKernelGGL(people_kernel, dim3(256), dim3(kT), 0, s, xyz, labels, n, kd, people);
     LAUNCH_CHECK();
     int64_t *hk = static_cast<int64_t *>(h->host_pinned);
     HIP_TRY(hipMemcpyAsync(hk, kd, sizeof(int64_t), hipMemcpyDeviceToHost, s));

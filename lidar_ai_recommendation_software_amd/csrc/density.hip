@@ -741,21 +741,31 @@ __device__ __forceinline__ int32_t ld(const int32_t *p)
 {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+__device__ __forceinline__ void st(int32_t *p, int32_t v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// find with path halving.  Invariant: parent[x] <= x (roots hook under smaller roots), so
+// every pointer moves toward the component minimum and the halving stores (x's parent
+// becomes its grandparent, an ancestor in the same component) are benign under races.
 __device__ int32_t uf_find(int32_t *parent, int32_t x)
 {
     int32_t p = ld(parent + x);
     while (p != x) {
+        const int32_t gp = ld(parent + p);
+        if (gp != p) st(parent + x, gp);
         x = p;
-        p = ld(parent + x);
+        p = gp;
     }
     return x;
 }
-__device__ void uf_unite(int32_t *parent, int32_t a, int32_t b)
+// join the components of roots-or-members a and b; returns the (current) smaller root
+__device__ int32_t uf_unite(int32_t *parent, int32_t a, int32_t b)
 {
     for (;;) {
         a = uf_find(parent, a);
         b = uf_find(parent, b);
-        if (a == b) return;
+        if (a == b) return a;
         if (a < b) {
             const int32_t t = a;
             a = b;
@@ -763,7 +773,7 @@ __device__ void uf_unite(int32_t *parent, int32_t a, int32_t b)
         }
         // hook the larger root under the smaller: the final root is the component minimum
         const int32_t old = atomicCAS(parent + a, a, b);
-        if (old == a) return;
+        if (old == a) return b;
         a = old;
     }
 }
@@ -778,9 +788,15 @@ __global__ void dbscan_union_kernel(const double *P, const uint32_t *cid, const 
     for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < g.n; t += (int64_t)gridDim.x * blockDim.x) {
         const int32_t i = (int32_t)order[t];
         if (cnt[i] < min_samples) continue;
+        // i's root is cached across its neighbours: a neighbour already in the same
+        // component costs one (halving) find, not two
+        int32_t ri = uf_find(parent, i);
         for_neighbours(g, start, sxyz, sxyz[3 * t], sxyz[3 * t + 1], sxyz[3 * t + 2], cid[i], [&](uint32_t u) {
             const int32_t j = (int32_t)order[u];
-            if (j < i && cnt[j] >= min_samples) uf_unite(parent, i, j);
+            if (j < i && cnt[j] >= min_samples) {
+                const int32_t rj = uf_find(parent, j);
+                if (rj != ri) ri = uf_unite(parent, ri, rj);
+            }
         });
     }
 }

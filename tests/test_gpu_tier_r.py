@@ -94,3 +94,18 @@ def test_voxel_downsample_vs_oracle(cuda, n, v):
 def test_fps_extension(cuda):
     x = uniform_frame(5000, 1, -1, 1).astype(np.float32)
     assert np.array_equal(dp.farthest_point_sample(x, 256), tier_n.fps(x, 256))
+
+
+@pytest.mark.parametrize("name", ["lattice_62978_s2", "crowd_65536_s3", "lattice_8163_s4"])
+def test_dbscan_labels_deterministic(cuda, name):
+    """Union-find runs with racing atomics across workgroups (and XCDs); the labels must
+    not depend on the schedule.  A path-halving store racing the roots pass once left a
+    non-root in parent[] in ~1 run of 3 — repeated runs pin that down."""
+    from golden_cases import FRAMES, META, digest
+    if name not in FRAMES:
+        pytest.skip(f"{name} not in the golden set")
+    pts = FRAMES[name]()
+    want = META["cases"][name]["clusters"]["sha256"]
+    for r in range(8):
+        got = digest(dp.preprocess_lidar_data(pts)["clusters"])["sha256"]
+        assert got == want, f"run {r}: labels differ from the reference"

@@ -103,6 +103,47 @@ def cpu_baseline(n, budget_s=20.0):
                       f"host has {os.cpu_count()} logical CPUs"}
 
 
+def tier_r_cpu_baseline(n, budget_s=10.0):
+    """oracle/tier_r (the byte-identical CPU restatement of the reference density path:
+    numpy + the C DBSCAN of the same neighbourhood rule) on uniform +-15 m frames."""
+    from oracle import tier_r
+    from lidar_ai_recommendation_software_amd.synthetic import uniform_frame
+    frames, t0 = 0, time.perf_counter()
+    while True:
+        pd = tier_r.preprocess_lidar_data(uniform_frame(n, 2000 + frames))
+        tier_r.analyze(pd)
+        frames += 1
+        if time.perf_counter() - t0 > budget_s or frames >= 8:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": frames * n / dt / 1e6, "unit": "M points/s", "cores": 1, "kind": "port",
+            "sample": f"{frames} x {n}-point uniform frame(s) through oracle/tier_r preprocess + analyze "
+                      f"(byte-identical restatement of the reference's numpy/sklearn path, 1 thread) in {dt:.1f} s"}
+
+
+def tier_r_leg(dev, rank, world, frames=16, n=65536, workers=4, steps=3, cpu=True):
+    """The reference's own path (Tier R: preprocess -> DBSCAN -> people -> density grid) on
+    device-resident uniform +-15 m frames through density_stream.DensityStream."""
+    import torch
+    from lidar_ai_recommendation_software_amd import sharding
+    from lidar_ai_recommendation_software_amd.density_stream import DensityStream
+    from lidar_ai_recommendation_software_amd.synthetic import uniform_frame
+    xs = [torch.from_numpy(uniform_frame(n, sharding.frame_seed(rank, base=1000 + i))).to(dev) for i in range(frames)]
+    ds = DensityStream(dev, workers=workers)
+    ds.run(xs[:workers])  # warm-up: workspaces sized
+    el = sharding.timed(lambda: [ds.run(xs) for _ in range(steps)], dev, world)
+    rec = {"metric": "M points/s through the reference density path (preprocess + DBSCAN + people + "
+                     "density grid), device-resident frames",
+           "value": sharding.aggregate_rate(frames * n * steps, world, el) / 1e6, "unit": "M points/s",
+           "ms_per_frame": el / (frames * steps) * 1e3, "frames_per_gpu": frames, "points_per_frame": n,
+           "workers": workers, "dtype": "f64", "parity": "byte-identical to the reference (tests/golden)",
+           "cpu_baseline": None}
+    if cpu and rank == 0 and world == 1:
+        rec["cpu_baseline"] = tier_r_cpu_baseline(n)
+        rec["speedup_vs_cpu"] = rec["value"] / rec["cpu_baseline"]["value"]
+    return rec
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -115,6 +156,7 @@ def main():
     ap.add_argument("--depth", type=int, default=3, help="SA1-FPS batches in flight ahead of the MLPs")
     ap.add_argument("--side-priority", type=int, default=0, help="HIP priority of the FPS streams (<0 = high)")
     ap.add_argument("--no-extras", action="store_true", help="skip the configs[1]/[4] side measurements")
+    ap.add_argument("--no-density", action="store_true", help="skip the Tier R density-path leg")
     args = ap.parse_args()
 
     import torch
@@ -159,6 +201,7 @@ def main():
                            "frames_per_gpu": b2, "points_per_frame": n2, "dtype": dtype,
                            "kernel_ms": k2}
 
+    density = None if args.no_density else tier_r_leg(dev, rank, world, cpu=not args.no_cpu_baseline)
     work = ssg_kernel_work(N)
     traffic = pmc_traffic(B, N)
     # the dominant kernel of the critical path: SA1 FPS runs on its own stream, overlapped
@@ -198,6 +241,7 @@ def main():
             "kernel_ms": kern,
             "pipeline": {"executor": "pointnet2.StreamingSSG", "sa1_fps_batches_in_flight": args.depth},
             "other_configs": extras,
+            "density_path": density,
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -109,3 +109,24 @@ def test_dbscan_labels_deterministic(cuda, name):
     for r in range(8):
         got = digest(dp.preprocess_lidar_data(pts)["clusters"])["sha256"]
         assert got == want, f"run {r}: labels differ from the reference"
+
+
+def test_density_stream_matches_drop_in(cuda):
+    """The device-resident multi-stream executor returns, frame for frame, what the
+    drop-in preprocess_lidar_data + CrowdDensityModel.analyze return."""
+    import torch
+    from lidar_ai_recommendation_software_amd.density_stream import DensityStream
+    names = ["uniform_16384_s0", "crowd_16384_s7", "lattice_8163_s4", "small_20", "small_12", "int_4096"]
+    names = [k for k in names if k in FRAMES]
+    frames = [FRAMES[k]() for k in names]
+    ds = DensityStream(cuda, workers=3)
+    got = ds.run([torch.from_numpy(np.ascontiguousarray(f, dtype=np.float64)).to(cuda) for f in frames])
+    model = CrowdDensityModel(1.0)
+    for name, f, g in zip(names, frames, got):
+        want = model.analyze(dp.preprocess_lidar_data(np.asarray(f, dtype=np.float64)))
+        assert g["total_people"] == want["total_people"], name
+        assert float(g["avg_density"]).hex() == float(want["avg_density"]).hex(), name
+        assert float(g["max_density"]).hex() == float(want["max_density"]).hex(), name
+        assert np.array_equal(g["density_map"], want["density_map"]), name
+        assert [(h["x"], h["y"], h["density"]) for h in g["hotspots"]] == \
+               [(h["x"], h["y"], h["density"]) for h in want["hotspots"]], name

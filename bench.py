@@ -88,7 +88,7 @@ def cpu_baseline(n, budget_s=20.0):
             x = unit_frames(1, n, 1000 + frames)[0]
             tier_n.sa_stack(x, {"levels": pn.resolve(cfg, n)}, w)
             frames += 1
-            if time.perf_counter() - t0 > budget_s or frames >= 8:
+            if time.perf_counter() - t0 > budget_s or frames >= 64:
                 break
     dt = time.perf_counter() - t0
     cpu = platform.processor() or platform.machine()
@@ -103,7 +103,7 @@ def cpu_baseline(n, budget_s=20.0):
                       f"host has {os.cpu_count()} logical CPUs"}
 
 
-def tier_r_cpu_baseline(n, budget_s=10.0):
+def tier_r_cpu_baseline(n, budget_s=12.0):
     """oracle/tier_r (the byte-identical CPU restatement of the reference density path:
     numpy + the C DBSCAN of the same neighbourhood rule) on uniform +-15 m frames."""
     from oracle import tier_r
@@ -113,7 +113,7 @@ def tier_r_cpu_baseline(n, budget_s=10.0):
         pd = tier_r.preprocess_lidar_data(uniform_frame(n, 2000 + frames))
         tier_r.analyze(pd)
         frames += 1
-        if time.perf_counter() - t0 > budget_s or frames >= 8:
+        if time.perf_counter() - t0 > budget_s or frames >= 32:
             break
     dt = time.perf_counter() - t0
     return {"value": frames * n / dt / 1e6, "unit": "M points/s", "cores": 1, "kind": "port",
@@ -121,7 +121,7 @@ def tier_r_cpu_baseline(n, budget_s=10.0):
                       f"(byte-identical restatement of the reference's numpy/sklearn path, 1 thread) in {dt:.1f} s"}
 
 
-def tier_r_leg(dev, rank, world, frames=16, n=65536, workers=4, steps=3, cpu=True):
+def tier_r_leg(dev, rank, world, frames=16, n=65536, workers=4, steps=3, cpu=True, cpu_budget=12.0):
     """The reference's own path (Tier R: preprocess -> DBSCAN -> people -> density grid) on
     device-resident uniform +-15 m frames through density_stream.DensityStream."""
     import torch
@@ -139,7 +139,7 @@ def tier_r_leg(dev, rank, world, frames=16, n=65536, workers=4, steps=3, cpu=Tru
            "workers": workers, "dtype": "f64", "parity": "byte-identical to the reference (tests/golden)",
            "cpu_baseline": None}
     if cpu and rank == 0 and world == 1:
-        rec["cpu_baseline"] = tier_r_cpu_baseline(n)
+        rec["cpu_baseline"] = tier_r_cpu_baseline(n, cpu_budget)
         rec["speedup_vs_cpu"] = rec["value"] / rec["cpu_baseline"]["value"]
     return rec
 
@@ -152,7 +152,7 @@ def main():
     ap.add_argument("--batch", type=int, default=32, help="frames per GPU per step")
     ap.add_argument("--points", type=int, default=65536)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-budget", type=float, default=20.0)
+    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU work per baseline sample")
     ap.add_argument("--depth", type=int, default=3, help="SA1-FPS batches in flight ahead of the MLPs")
     ap.add_argument("--side-priority", type=int, default=0, help="HIP priority of the FPS streams (<0 = high)")
     ap.add_argument("--no-extras", action="store_true", help="skip the configs[1]/[4] side measurements")
@@ -201,7 +201,7 @@ def main():
                            "frames_per_gpu": b2, "points_per_frame": n2, "dtype": dtype,
                            "kernel_ms": k2}
 
-    density = None if args.no_density else tier_r_leg(dev, rank, world, cpu=not args.no_cpu_baseline)
+    density = None if args.no_density else tier_r_leg(dev, rank, world, cpu=not args.no_cpu_baseline, cpu_budget=args.cpu_budget)
     work = ssg_kernel_work(N)
     traffic = pmc_traffic(B, N)
     # the dominant kernel of the critical path: SA1 FPS runs on its own stream, overlapped

@@ -15,7 +15,7 @@ if [[ $STEPS == *bench* ]]; then
 fi
 if [[ $STEPS == *prof* ]]; then
   (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv \
-      -d "$R/gpurun_out/${TAG}_prof" -o prof -- python3 "$R/bench.py" --no-extras --no-cpu-baseline \
+      -d "$R/gpurun_out/${TAG}_prof" -o prof -- python3 "$R/bench.py" --no-extras --no-cpu-baseline --no-density \
       > "$R/gpurun_out/${TAG}_prof_bench.json" 2> "$R/gpurun_out/${TAG}_prof.err") || exit 13
 fi
 exit 0

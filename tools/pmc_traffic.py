@@ -33,33 +33,40 @@ def rows(d):
     return list(csv.DictReader(open(f[0])))
 
 
-def label(name, grid, n_fps_seen):
-    """Kernel label of the SSG stack at B=32, N=65536 (grid = threads)."""
+def label(name, grid):
+    """Kernel label of the SSG stack at B=32, N=65536 (grid = threads).  dense_relu_kernel
+    at 262144 threads is both SA2's per-point layer-1 GEMM and SA3's second layer: the
+    caller splits those by dispatch order (the layer-1 GEMM comes first in every step)."""
     if "fps_bucket_kernel" in name:
         return "fps"  # split into sa1/sa2 by duration below
     if "ball_query_kernel" in name:
         return {1048576: "sa1_ball_query", 262144: "sa2_ball_query"}.get(grid)
-    if "sa_group_mlp_kernel<0, 64, 64, 128, 32>" in name:
+    if "sa_group_mlp_kernel<0, 64, 64, 128, 32" in name:
         return "sa1_group_mlp"
-    if "sa_group_mlp_kernel<128, 128, 128, 256, 64>" in name:
+    if "sa_group_mlp_kernel<128, 128, 128, 256, 64" in name or "sa_pre_lds_kernel<128, 128, 256, 64>" in name:
         return "sa2_group_mlp"
     if "dense_relu_kernel" in name:
-        return {131072: "sa3_dense1", 262144: "sa3_dense2", 524288: "sa3_dense3_pool"}.get(grid)
+        return {65536: "sa2_layer1_points", 131072: "sa3_dense1", 262144: "dense_262144",
+                524288: "sa3_dense3_pool"}.get(grid)
     if "concat_xyz_pad" in name:
-        return "sa3_concat"
+        return "concat"
     return None
 
 
 def per_label(rs, counter):
     acc = defaultdict(list)
     fps = []
-    for r in rs:
+    n262 = 0
+    for r in sorted(rs, key=lambda r: int(r["Dispatch_Id"])):
         if r["Counter_Name"] != counter:
             continue
         v = float(r["Counter_Value"]) * 1024.0  # KiB -> bytes
-        lab = label(r["Kernel_Name"], int(r["Grid_Size"]), 0)
+        lab = label(r["Kernel_Name"], int(r["Grid_Size"]))
         if lab == "fps":
             fps.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"]), v))
+        elif lab == "dense_262144":
+            acc["sa2_layer1_points" if n262 % 2 == 0 else "sa3_dense2"].append(v)
+            n262 += 1
         elif lab:
             acc[lab].append(v)
     if fps:  # SA1 FPS (65536 -> 4096, long) vs SA2's nested-prefix FPS (short)
@@ -67,6 +74,11 @@ def per_label(rs, counter):
         half = len(fps) // 2
         acc["sa2_fps"] = [v for _, v in fps[:half]]
         acc["sa1_fps"] = [v for _, v in fps[half:]]
+    # sa2_layer1_points = its two GEMMs per launch group: report the per-step sum
+    if "sa2_layer1_points" in acc:
+        v = acc["sa2_layer1_points"]
+        steps = max(1, len(v) // 2)
+        acc["sa2_layer1_points"] = [sum(v) / steps]
     return acc
 
 
@@ -92,7 +104,7 @@ def main(cf, cw, pf, pw, out):
                      "launches": len(fa.get(lab, []))}
     res = {"config": {"workload": "ssg", "points_per_frame": 65536, "frames_per_gpu": 32},
            "source": "rocprofv3 --kernel-trace --pmc FETCH_SIZE | WRITE_SIZE (separate passes) of "
-                     "bench.py --no-extras --no-cpu-baseline --steps 4 --warmup 1",
+                     "bench.py --no-extras --no-cpu-baseline --no-density --steps 4 --warmup 1",
            "calibration": cal, "kernels": kern}
     os.makedirs(os.path.dirname(out) or ".", exist_ok=True)
     with open(out, "w") as f:

@@ -155,6 +155,8 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU work per baseline sample")
     ap.add_argument("--depth", type=int, default=3, help="SA1-FPS batches in flight ahead of the MLPs")
     ap.add_argument("--side-priority", type=int, default=0, help="HIP priority of the FPS streams (<0 = high)")
+    ap.add_argument("--side-cus", type=int, default=0, help="CUs reserved for the SA1 FPS streams (0 = shared)")
+    ap.add_argument("--cu-layout", default="xcd", choices=["xcd", "low"])
     ap.add_argument("--no-extras", action="store_true", help="skip the configs[1]/[4] side measurements")
     ap.add_argument("--no-density", action="store_true", help="skip the Tier R density-path leg")
     args = ap.parse_args()
@@ -179,7 +181,8 @@ def main():
         x = torch.from_numpy(unit_frames(B, N, seed=sharding.frame_seed(rank))).to(dev)
         # the streaming executor overlaps batch k+1's SA1 FPS + ball queries (latency-bound,
         # one workgroup per frame) with batch k's MFMA levels; results are identical to forward()
-        pipe = pn.StreamingSSG(bb, B, N, depth=depth, side_priority=args.side_priority)
+        pipe = pn.StreamingSSG(bb, B, N, depth=depth, side_priority=args.side_priority,
+                               side_cus=args.side_cus, cu_layout=args.cu_layout)
         ref, _ = bb.forward(x)
         outs = pipe.run([x] * max(2, warmup))
         torch.cuda.synchronize(dev)

@@ -54,6 +54,9 @@ SIGNATURES = {
     "lidar_mlp_pack_bf16": [I32, I32, I32, I32, P, P, P, P, P, P, P],
     "lidar_dense_relu_f32": [P, P, I64, I32, P, P, I32, I32, P, P],
     "lidar_dense_f32": [P, P, I64, I32, P, P, I32, I32, I32, P, P],
+    "lidar_stream_create_cu_mask": [I32, P, I32, P],
+    "lidar_stream_destroy": [P],
+    "lidar_device_cu_count": [I32, P],
     "lidar_sa_group_mlp_pre_f32": [P, P, I64, P, P, I64, I64, I64, I32, I32, I32, I32, I32, P, P,
                                    I64, I64, P],
     "lidar_concat_xyz_pad_f32": [P, P, I64, P, I64, I64, P],

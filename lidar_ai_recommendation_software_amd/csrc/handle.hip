@@ -80,3 +80,31 @@ LIDAR_EXPORT int lidar_reserve(lidar_handle *h, uint64_t bytes)
     if (!lidar::workspace(h, bytes)) return LIDAR_ENOMEM;
     return LIDAR_OK;
 }
+
+// A stream restricted to a subset of the device's compute units (bit i of mask[i / 32]
+// enables CU i).  Used by StreamingSSG to keep the latency-bound SA1 FPS chains and the
+// MFMA levels on disjoint CUs.  Returns the hipStream_t through *out.
+LIDAR_EXPORT int lidar_stream_create_cu_mask(int device, const uint32_t *mask, int32_t nwords, void **out)
+{
+    REQUIRE(mask && out && nwords > 0, "lidar_stream_create_cu_mask: bad arguments");
+    HIP_TRY(hipSetDevice(device));
+    hipStream_t s = nullptr;
+    HIP_TRY(hipExtStreamCreateWithCUMask(&s, (uint32_t)nwords, mask));
+    *out = s;
+    return LIDAR_OK;
+}
+
+LIDAR_EXPORT int lidar_stream_destroy(void *stream)
+{
+    if (stream) HIP_TRY(hipStreamDestroy(static_cast<hipStream_t>(stream)));
+    return LIDAR_OK;
+}
+
+LIDAR_EXPORT int lidar_device_cu_count(int device, int32_t *out)
+{
+    REQUIRE(out, "lidar_device_cu_count: null pointer");
+    int v = 0;
+    HIP_TRY(hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, device));
+    *out = v;
+    return LIDAR_OK;
+}

@@ -18,6 +18,14 @@
 
 #include "common.hpp"
 
+// LDS-staged weight-stream kernels (sa_mlp_pre.hip); -1 = no variant for these widths
+int lidar_sa_xyz_lds_dispatch(int c1, int c2, int c3, int ns, const float *xyz, const float *centres,
+                              const int32_t *idx, int64_t batch, int64_t n, int64_t m, const float *packed,
+                              float *out, int64_t os, int64_t oo, hipStream_t s);
+int lidar_sa_pre_lds_dispatch(int cfeat, int c1, int c2, int c3, int ns, const float *p, int64_t stride,
+                              const float *q, const int32_t *idx, int64_t batch, int64_t n, int64_t m,
+                              const float *w23, float *out, int64_t os, int64_t oo, hipStream_t s);
+
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -425,6 +433,12 @@ LIDAR_EXPORT int lidar_sa_group_mlp_f32(lidar_handle *h, const float *xyz, const
             "lidar_sa_group_mlp_f32: output columns exceed out_stride");
     if (batch == 0) return LIDAR_OK;
     HIP_TRY(hipSetDevice(h->device));
+    static const bool no_lds = getenv("LIDAR_PRE_NO_LDS") != nullptr;  // A/B tuning knob
+    if (cfeat == 0 && !no_lds) {  // LDS-staged weight stream (sa_mlp_pre.hip)
+        const int rc = lidar_sa_xyz_lds_dispatch(c1, c2, c3, nsample, xyz, centres, idx, batch, n, m, packed,
+                                                 out, out_stride, out_offset, static_cast<hipStream_t>(stream));
+        if (rc != -1) return rc;
+    }
     for (const Variant &v : kVariants)
         if (v.cf == cfeat && v.c1 == c1 && v.c2 == c2 && v.c3 == c3 && v.ns == nsample)
             return v.fn(xyz, feats, feat_stride, centres, idx, batch, n, m, packed, out,
@@ -460,9 +474,6 @@ LIDAR_EXPORT int lidar_dense_relu_f32(lidar_handle *h, const float *x, int64_t r
     return lidar_dense_f32(h, x, rows, k, w, bias, cout, 1, pool_rows, y, stream);
 }
 
-int lidar_sa_pre_lds_dispatch(int cfeat, int c1, int c2, int c3, int ns, const float *p, int64_t stride,
-                              const float *q, const int32_t *idx, int64_t batch, int64_t n, int64_t m,
-                              const float *w23, float *out, int64_t os, int64_t oo, hipStream_t s);
 
 LIDAR_EXPORT int lidar_sa_group_mlp_pre_f32(lidar_handle *h, const float *p, int64_t p_stride,
                                             const float *q, const int32_t *idx, int64_t batch,

@@ -26,7 +26,11 @@ __device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c)
 
 __device__ __forceinline__ float relu(float v) { return v > 0.0f ? v : 0.0f; }
 
-template <int C1, int C2, int C3, int NS>
+// XYZ = true: a level without point features (SA1): layer 1 runs here on the grouped
+// offsets (dx, dy | dz, 0) as in sa_group_mlp_kernel (W1 and b1 resident in LDS; the two
+// all-zero k-steps of its 4-step block are skipped, which changes no bit); P is xyz, Q is
+// the centres and w23 is the whole lidar_mlp_pack_f32 image.
+template <int C1, int C2, int C3, int NS, bool XYZ = false>
 __global__ __launch_bounds__(256, 2) void sa_pre_lds_kernel(
     const float *__restrict__ P, int64_t stride, const float *__restrict__ Q,
     const int32_t *__restrict__ idx, int n, int m, int64_t total, const float *__restrict__ w23,
@@ -44,6 +48,9 @@ __global__ __launch_bounds__(256, 2) void sa_pre_lds_kernel(
 
     __shared__ f32x4 buf[2][CHMAX];
     __shared__ float bias_s[C2 + C3];  // b2 | b3: no ordinary global load inside the chunk loop
+    constexpr int W1N = XYZ ? T1 * 64 : 1;  // layer-1 weights (4 k-steps x 64 lanes per tile)
+    __shared__ f32x4 w1_s[W1N];
+    __shared__ float b1_s[XYZ ? C1 : 1];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int h = lane >> 5, col = lane & 31;
@@ -52,7 +59,7 @@ __global__ __launch_bounds__(256, 2) void sa_pre_lds_kernel(
     const int64_t cc = live ? unit : total - 1;
     const int64_t b = cc / m;
 
-    const f32x4 *W2 = reinterpret_cast<const f32x4 *>(w23);
+    const f32x4 *W2 = reinterpret_cast<const f32x4 *>(w23) + (XYZ ? T1 * 64 : 0);
     const f32x4 *W3 = W2 + (int64_t)T2 * CH2;
     const float *B2 = reinterpret_cast<const float *>(W3 + (int64_t)T3 * CH3) + C1;  // skip b1
 
@@ -76,6 +83,11 @@ __global__ __launch_bounds__(256, 2) void sa_pre_lds_kernel(
     };
     fetch(0, 0);
     for (int i = tid; i < C2 + C3; i += 256) bias_s[i] = B2[i];  // B3 follows B2
+    if constexpr (XYZ) {
+        const f32x4 *W1 = reinterpret_cast<const f32x4 *>(w23);
+        for (int i = tid; i < W1N; i += 256) w1_s[i] = W1[i];
+        for (int i = tid; i < C1; i += 256) b1_s[i] = B2[i - C1];
+    }
     __syncthreads();
 
     float mx[T3];
@@ -87,17 +99,34 @@ __global__ __launch_bounds__(256, 2) void sa_pre_lds_kernel(
     for (int tile = 0; tile < TILES; ++tile) {
         // ---- layer 1 from the per-point rows: y1[ti] reg 4j+i <- channel 32ti+8j+4h+i
         const int64_t k = idx[cc * NS + tile * 32 + col];
-        const f32x4 *pp = reinterpret_cast<const f32x4 *>(P + ((int64_t)b * n + k) * stride + 4 * h);
-        const f32x4 *qq = reinterpret_cast<const f32x4 *>(Q + cc * stride + 4 * h);
         f32x16 y1[T1];
+        if constexpr (XYZ) {
+            const float *pr = P + ((int64_t)b * n + k) * 3;
+            const float *ce = Q + cc * 3;
+            const float dx = pr[0] - ce[0], dy = pr[1] - ce[1], dz = pr[2] - ce[2];
+            const float xa = h ? dz : dx, xb = h ? 0.0f : dy;
 #pragma unroll
-        for (int ti = 0; ti < T1; ++ti)
+            for (int t = 0; t < T1; ++t) {
+                const f32x4 wv = w1_s[t * 64 + lane];
+                f32x16 acc = {};
+                acc = mfma(wv[0], xa, acc);
+                acc = mfma(wv[1], xb, acc);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const f32x4 a = pp[8 * ti + 2 * j], q = qq[8 * ti + 2 * j];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) y1[ti][4 * j + i] = relu(a[i] - q[i]);
+                for (int r = 0; r < 16; ++r) acc[r] = relu(acc[r] + b1_s[32 * t + rho(r) + 4 * h]);
+                y1[t] = acc;
             }
+        } else {
+            const f32x4 *pp = reinterpret_cast<const f32x4 *>(P + ((int64_t)b * n + k) * stride + 4 * h);
+            const f32x4 *qq = reinterpret_cast<const f32x4 *>(Q + cc * stride + 4 * h);
+#pragma unroll
+            for (int ti = 0; ti < T1; ++ti)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const f32x4 a = pp[8 * ti + 2 * j], q = qq[8 * ti + 2 * j];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) y1[ti][4 * j + i] = relu(a[i] - q[i]);
+                }
+        }
 
         f32x16 y2[T2];
 #pragma unroll
@@ -157,14 +186,14 @@ __global__ __launch_bounds__(256, 2) void sa_pre_lds_kernel(
     }
 }
 
-template <int C1, int C2, int C3, int NS>
+template <int C1, int C2, int C3, int NS, bool XYZ = false>
 int launch_pre(const float *p, int64_t stride, const float *q, const int32_t *idx, int64_t batch,
                int64_t n, int64_t m, const float *w23, float *out, int64_t os, int64_t oo, hipStream_t s)
 {
     const int64_t total = batch * m;
     const int64_t blocks = (total + 3) / 4;
     REQUIRE(blocks <= 0x7fffffff, "sa_group_mlp_pre: too many centres");
-    hipLaunchKernelGGL((sa_pre_lds_kernel<C1, C2, C3, NS>), dim3((unsigned)blocks), dim3(256), 0, s, p,
+    hipLaunchKernelGGL((sa_pre_lds_kernel<C1, C2, C3, NS, XYZ>), dim3((unsigned)blocks), dim3(256), 0, s, p,
                        stride, q, idx, (int)n, (int)m, total, w23, out, os, oo);
     LAUNCH_CHECK();
     return LIDAR_OK;
@@ -184,5 +213,18 @@ int lidar_sa_pre_lds_dispatch(int cfeat, int c1, int c2, int c3, int ns, const f
         return launch_pre<128, 128, 256, 128>(p, stride, q, idx, batch, n, m, w23, out, os, oo, s);
     if (c1 == 64 && c2 == 64 && c3 == 128 && ns == 32)
         return launch_pre<64, 64, 128, 32>(p, stride, q, idx, batch, n, m, w23, out, os, oo, s);
+    return -1;
+}
+
+// dispatch used by lidar_sa_group_mlp_f32 for levels without features (cfeat == 0):
+// xyz / centres as usual, packed = the whole lidar_mlp_pack_f32 image; -1 = no variant
+int lidar_sa_xyz_lds_dispatch(int c1, int c2, int c3, int ns, const float *xyz, const float *centres,
+                              const int32_t *idx, int64_t batch, int64_t n, int64_t m, const float *packed,
+                              float *out, int64_t os, int64_t oo, hipStream_t s)
+{
+    if (c1 == 64 && c2 == 64 && c3 == 128 && ns == 32)
+        return launch_pre<64, 64, 128, 32, true>(xyz, 3, centres, idx, batch, n, m, packed, out, os, oo, s);
+    if (c1 == 64 && c2 == 96 && c3 == 128 && ns == 128)
+        return launch_pre<64, 96, 128, 128, true>(xyz, 3, centres, idx, batch, n, m, packed, out, os, oo, s);
     return -1;
 }

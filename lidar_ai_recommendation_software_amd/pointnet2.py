@@ -409,6 +409,37 @@ class PointNet2Backbone:
     __call__ = forward
 
 
+def ctypes_void(p):
+    import ctypes
+    return ctypes.c_void_p(p)
+
+
+def cu_masks(device, side_cus, layout="xcd"):
+    """(side mask words, main mask words) over the device's CUs: `side_cus` CUs for the side
+    streams, the complement for the main stream."""
+    import ctypes
+    n = ctypes.c_int32(0)
+    nat.call("lidar_device_cu_count", int(device), ctypes.byref(n))
+    n = n.value
+    if not 0 < side_cus < n:
+        raise ValueError(f"side_cus must be in (0, {n})")
+    if layout == "xcd" and n % 8 == 0:
+        per, k = n // 8, max(1, side_cus // 8)
+        side = {x * per + j for x in range(8) for j in range(k)}
+    elif layout == "low":
+        side = set(range(side_cus))
+    else:
+        raise ValueError("cu_layout must be 'xcd' or 'low'")
+    words = (n + 31) // 32
+    sm, mm = [0] * words, [0] * words
+    for c in range(n):
+        if c in side:
+            sm[c // 32] |= 1 << (c % 32)
+        else:
+            mm[c // 32] |= 1 << (c % 32)
+    return sm, mm
+
+
 # ------------------------------------------------------------------ streaming executor
 class StreamingSSG:
     """Frame-batch pipeline for a continuous feed (SSG/MSG backbone).
@@ -422,15 +453,28 @@ class StreamingSSG:
     ``PointNet2Backbone.forward`` (same kernels, same inputs).
     """
 
-    def __init__(self, backbone, batch, n, depth=1, side_priority=0):
+    def __init__(self, backbone, batch, n, depth=1, side_priority=0, side_cus=0, cu_layout="xcd"):
+        """side_cus > 0: the SA1 FPS / ball-query streams run on `side_cus` CUs and the
+        main stream on the rest (CU-masked HIP streams), so the latency-bound FPS waves and
+        the MFMA waves stop competing for registers, issue slots and L2.  cu_layout "xcd"
+        takes side_cus/8 CUs of each of the 8 XCDs (mask bit = 32*xcd + cu), "low" the
+        lowest-numbered CUs."""
         self.bb = backbone
         self.B, self.N, self.depth = batch, n, depth
         dev = backbone.device
         lvl0 = backbone.levels[0]
         self.M1 = max(1, n // lvl0["div"])
-        # side_priority < 0 puts the latency-bound FPS chains ahead of the MLP waves in
-        # the dispatcher (HIP stream priority); results do not depend on it
-        self.fps_streams = [torch.cuda.Stream(device=dev, priority=side_priority) for _ in range(depth)]
+        self._owned = []
+        self.main = None
+        if side_cus:
+            side, main = cu_masks(dev.index, side_cus, cu_layout)
+            mk = lambda m: self._masked_stream(dev, m)
+            self.fps_streams = [mk(side) for _ in range(depth)]
+            self.main = mk(main)
+        else:
+            # side_priority < 0 puts the latency-bound FPS chains ahead of the MLP waves in
+            # the dispatcher (HIP stream priority); results do not depend on it
+            self.fps_streams = [torch.cuda.Stream(device=dev, priority=side_priority) for _ in range(depth)]
         nslot = depth + 1
         self.idx = [torch.empty((batch, self.M1), dtype=torch.int32, device=dev) for _ in range(nslot)]
         self.cxyz = [torch.empty((batch, self.M1, 3), dtype=torch.float32, device=dev) for _ in range(nslot)]
@@ -442,6 +486,22 @@ class StreamingSSG:
         self.slot_free = [torch.cuda.Event() for _ in range(nslot)]
         for e in self.slot_free:
             e.record(torch.cuda.current_stream(dev))
+
+    def _masked_stream(self, dev, mask):
+        import ctypes
+        ptr = ctypes.c_void_p()
+        arr = (ctypes.c_uint32 * len(mask))(*mask)
+        nat.call("lidar_stream_create_cu_mask", dev.index, ctypes.cast(arr, ctypes.c_void_p), len(mask),
+                 ctypes.byref(ptr))
+        self._owned.append(ptr.value)
+        return torch.cuda.ExternalStream(ptr.value, device=dev)
+
+    def __del__(self):
+        for p in getattr(self, "_owned", []):
+            try:
+                nat.load_library().lidar_stream_destroy(ctypes_void(p))
+            except Exception:
+                pass
 
     def _fps(self, k, x):
         slot = k % (self.depth + 1)
@@ -467,6 +527,16 @@ class StreamingSSG:
 
     def run(self, inputs):
         """inputs: list of (B, N, 3) CUDA tensors -> list of global features (B, C)."""
+        if self.main is not None:
+            cur = torch.cuda.current_stream(self.bb.device)
+            self.main.wait_stream(cur)
+            with torch.cuda.stream(self.main):
+                outs = self._run(inputs)
+            cur.wait_stream(self.main)
+            return outs
+        return self._run(inputs)
+
+    def _run(self, inputs):
         main = torch.cuda.current_stream(self.bb.device)
         outs = []
         pending = []

@@ -4,9 +4,9 @@
 // point indices in ascending order with d < r*r (fp32, d = (dx*dx+dy*dy)+dz*dz, one
 // rounding per op), unused slots repeat the first hit, no hit -> 0.
 //
-// One wavefront serves 8 centres of a frame: it scans the frame in index order, 64
-// points per step (one coalesced load), tests the chunk against all 8 centres (the
-// load is shared 8 ways), __ballot collects each centre's hits, popcount ranks them,
+// One wavefront serves 8 centres of a frame: it scans the frame in index order, 128
+// points per step (two coalesced 64-point chunks, the next pair prefetched), tests them
+// against all 8 centres (the loads are shared 8 ways), __ballot collects each centre's hits, popcount ranks them,
 // and the scan stops once every centre has nsample hits — for uniform frames at
 // r = 0.2 that is ~12 % of the frame.
 #include "common.hpp"
@@ -40,29 +40,43 @@ __global__ __launch_bounds__(256) void ball_query_kernel(const float *__restrict
         first[j] = -1;
     }
     const uint64_t below = (1ull << lane) - 1;
-    for (int base = 0; base < n; base += 64) {
+    // the scan is load-latency bound (a wave waits on its chunk ~half the time): the next
+    // chunk's 12-byte point is in flight while the current one is tested
+    struct P3 {
+        float x, y, z;
+    };
+    const P3 *pp = reinterpret_cast<const P3 *>(p);
+    const P3 zero{0.f, 0.f, 0.f};
+    // two 64-point chunks per iteration (each lane tests two points against the 8 centres:
+    // independent work in flight), the next pair prefetched.  Hand-unrolled: a generic
+    // k-chunk loop measured slower (0.96 / 0.93 ms for 2 / 4 chunks vs 0.86, B=32 SA1).
+    P3 c0p = lane < n ? pp[lane] : zero, c1p = lane + 64 < n ? pp[lane + 64] : zero;
+    for (int base = 0; base < n; base += 128) {
         bool open = false;
 #pragma unroll
         for (int j = 0; j < kC; ++j) open |= cnt[j] < ns;
         if (!open) break;  // wave-uniform
-        const int k = base + lane;
-        float px = 0.f, py = 0.f, pz = 0.f;
-        if (k < n) {
-            px = p[3 * k];
-            py = p[3 * k + 1];
-            pz = p[3 * k + 2];
-        }
+        const int k0 = base + lane, k1 = k0 + 64;
+        const P3 n0 = k0 + 128 < n ? pp[k0 + 128] : zero, n1 = k1 + 128 < n ? pp[k1 + 128] : zero;
+        const P3 a0 = c0p, a1 = c1p;
+        c0p = n0;
+        c1p = n1;
 #pragma unroll
         for (int j = 0; j < kC; ++j) {
             if (cnt[j] >= ns) continue;  // wave-uniform
-            const bool hit = k < n && lidar::dist2f(px, py, pz, cx[j], cy[j], cz[j]) < r2;
-            const uint64_t mask = __ballot(hit);
-            if (mask) {
+            const bool h0 = k0 < n && lidar::dist2f(a0.x, a0.y, a0.z, cx[j], cy[j], cz[j]) < r2;
+            const bool h1 = k1 < n && lidar::dist2f(a1.x, a1.y, a1.z, cx[j], cy[j], cz[j]) < r2;
+            const uint64_t m0 = __ballot(h0), m1 = __ballot(h1);
+            if (m0 | m1) {
                 int32_t *o = out + (b * m + c0 + j) * (int64_t)ns;
-                if (first[j] < 0) first[j] = base + __ffsll((unsigned long long)mask) - 1;
-                const int rank = cnt[j] + __popcll(mask & below);
-                if (hit && rank < ns) o[rank] = k;
-                cnt[j] += __popcll(mask);
+                if (first[j] < 0)
+                    first[j] = m0 ? base + __ffsll((unsigned long long)m0) - 1
+                                  : base + 64 + __ffsll((unsigned long long)m1) - 1;
+                const int r0 = cnt[j] + __popcll(m0 & below);
+                const int r1 = cnt[j] + __popcll(m0) + __popcll(m1 & below);  // chunk 1 after chunk 0
+                if (h0 && r0 < ns) o[r0] = k0;
+                if (h1 && r1 < ns) o[r1] = k1;
+                cnt[j] += __popcll(m0) + __popcll(m1);
             }
         }
     }

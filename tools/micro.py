@@ -41,10 +41,13 @@ def main():
         if "bq" in what and B == 32:
             c = x[:, : N // 16].contiguous()
             ms = timeit(lambda: pn.ball_query(0.2, 32, x, c))
-            print(f"ball_query B={B} N={N} M={N // 16} r0.2 ns32: {ms:.3f} ms", flush=True)
+            print(f"ball_query B={B} N={N} M={N // 16} r0.2 ns32 (random centres): {ms:.3f} ms", flush=True)
+            c = pn.farthest_point_sample(x, N // 16, return_xyz=True)[1]
+            ms = timeit(lambda: pn.ball_query(0.2, 32, x, c))
+            print(f"ball_query B={B} N={N} M={N // 16} r0.2 ns32 (FPS centres): {ms:.3f} ms", flush=True)
 
 
-if __name__ == "__main__" and not ({"phases", "mlp", "tier_r"} & set(sys.argv)):
+if __name__ == "__main__" and not ({"phases", "mlp", "tier_r", "dense"} & set(sys.argv)):
     main()
 
 
@@ -143,3 +146,26 @@ def tier_r_micro():
 
 if __name__ == "__main__" and "tier_r" in sys.argv:
     tier_r_micro()
+
+
+def dense_micro():
+    """group_all's three dense layers: liblidar_amd dense kernel vs hipBLASLt (torch)."""
+    from lidar_ai_recommendation_software_amd import pointnet2 as pn
+    dev = torch.device("cuda:0")
+    rng = np.random.default_rng(0)
+    rows = 32 * 1024
+    for k, n in ((272, 256), (256, 512), (512, 1024)):
+        x = torch.from_numpy(rng.standard_normal((rows, k)).astype(np.float32)).to(dev)
+        w = torch.from_numpy((rng.standard_normal((k, n)) / np.sqrt(k)).astype(np.float32)).to(dev)
+        b = torch.from_numpy(rng.standard_normal(n).astype(np.float32)).to(dev)
+        ms_own = timeit(lambda: pn.dense(x, w, b), reps=10)
+        ms_blas = timeit(lambda: torch._addmm_activation(b, x, w), reps=10)
+        ms_mm = timeit(lambda: torch.relu_(torch.addmm(b, x, w)), reps=10)
+        fl = 2 * rows * k * n
+        err = (pn.dense(x, w, b) - torch._addmm_activation(b, x, w)).abs().max().item()
+        print(f"dense {k}x{n}: own {ms_own:.3f} ms ({fl / ms_own / 1e9:.0f} TF)  hipblaslt+relu {ms_blas:.3f} ms "
+              f"({fl / ms_blas / 1e9:.0f} TF)  addmm+relu {ms_mm:.3f} ms  maxdiff {err:.2e}", flush=True)
+
+
+if __name__ == "__main__" and "dense" in sys.argv:
+    dense_micro()

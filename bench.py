@@ -10,9 +10,12 @@ per step (weak scaling, per-frame data parallel, no collective on the data path)
 
 A step = FPS + ball query + fused group/MLP/max-pool for SA1 and SA2, then group_all
 (three MFMA dense layers with a fused max-pool) over the batch, inputs resident in HBM.
-Steps run through pointnet2.StreamingSSG: batch k+1's SA1 FPS (latency-bound) overlaps
-batch k's MFMA work on a second stream — the steady state of a continuous LiDAR feed;
-K steps = K batches fully processed inside the timed region (pipeline fill included).
+Steps run through pointnet2.StreamingSSG — the steady state of a continuous LiDAR feed:
+later batches' SA1 FPS (latency-bound, one workgroup per frame) runs on side streams
+while earlier batches' MFMA levels run on the main stream; pairs of batches share one
+FPS launch and one MFMA pass (--fps-group 2; every operator is per frame, outputs are
+bit-identical to one-batch forward()).  K steps = K batches of 32 frames fully processed
+inside the timed region (pipeline fill included).
 Synthetic data: uniform [-1, 1]^3 float32 frames (seeded per rank), random-init weights.
 
 Run:  python bench.py [--gpus N --steps K --warmup W]  (N>1 via torch.distributed.run)
@@ -147,14 +150,16 @@ def tier_r_leg(dev, rank, world, frames=16, n=65536, workers=4, steps=3, cpu=Tru
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=60,
+                    help="timed steps; the pipeline fill (one SA1-FPS latency, ~13 ms) is inside the window")
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=32, help="frames per GPU per step")
     ap.add_argument("--points", type=int, default=65536)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU work per baseline sample")
-    ap.add_argument("--depth", type=int, default=3, help="SA1-FPS batches in flight ahead of the MLPs")
+    ap.add_argument("--depth", type=int, default=2, help="side streams (SA1-FPS groups in flight ahead of the MLPs)")
     ap.add_argument("--side-priority", type=int, default=0, help="HIP priority of the FPS streams (<0 = high)")
+    ap.add_argument("--fps-group", type=int, default=2, help="batches per SA1-FPS launch (StreamingSSG fps_group)")
     ap.add_argument("--side-cus", type=int, default=0, help="CUs reserved for the SA1 FPS streams (0 = shared)")
     ap.add_argument("--cu-layout", default="xcd", choices=["xcd", "low"])
     ap.add_argument("--no-extras", action="store_true", help="skip the configs[1]/[4] side measurements")
@@ -176,20 +181,30 @@ def main():
 
     B, N = args.batch, args.points
 
-    def measure(cfg, dtype, B, N, steps, warmup, depth):
+    def measure(cfg, dtype, B, N, steps, warmup, depth, events_in_window=True):
+        """events_in_window: HIP events around every launch inside the timed window (the
+        headline: the roofline durations come from the same window).  False: the window
+        runs clean and the per-kernel durations come from a second, instrumented window
+        of the same length (with ~25 launches per step, as MSG has, the events cost ~1/3)."""
         bb = pn.PointNet2Backbone(cfg, device=dev, seed=0, dtype=dtype)
         x = torch.from_numpy(unit_frames(B, N, seed=sharding.frame_seed(rank))).to(dev)
         # the streaming executor overlaps batch k+1's SA1 FPS + ball queries (latency-bound,
         # one workgroup per frame) with batch k's MFMA levels; results are identical to forward()
         pipe = pn.StreamingSSG(bb, B, N, depth=depth, side_priority=args.side_priority,
-                               side_cus=args.side_cus, cu_layout=args.cu_layout)
+                               side_cus=args.side_cus, cu_layout=args.cu_layout, fps_group=args.fps_group)
         ref, _ = bb.forward(x)
         outs = pipe.run([x] * max(2, warmup))
         torch.cuda.synchronize(dev)
         assert all(torch.equal(ref, o) for o in outs), "streaming executor diverged from forward()"
         timers = pn._Timers()
-        bb.timers = timers  # HIP events around every launch, on the stream it is launched on
-        elapsed = sharding.timed(lambda: pipe.run([x] * steps), dev, world)  # max over ranks
+        if events_in_window:
+            bb.timers = timers  # HIP events around every launch, on the stream it is launched on
+            elapsed = sharding.timed(lambda: pipe.run([x] * steps), dev, world)  # max over ranks
+        else:
+            elapsed = sharding.timed(lambda: pipe.run([x] * steps), dev, world)
+            bb.timers = timers
+            pipe.run([x] * steps)
+            torch.cuda.synchronize(dev)
         bb.timers = None
         return elapsed, timers.mean_ms()
 
@@ -197,9 +212,9 @@ def main():
     extras = {}
     if not args.no_extras:
         # the other BASELINE.json configs, measured the same way (not the headline metric)
-        for key, cfg, dtype, b2, n2, st in (("configs[1]_sa1_16k_f32", pn.SA1_ONLY, "f32", 32, 16384, 10),
-                                            ("configs[4]_msg_131k_bf16", pn.MSG, "bf16", 8, 131072, 6)):
-            el2, k2 = measure(cfg, dtype, b2, n2, st, 2, args.depth)
+        for key, cfg, dtype, b2, n2, st in (("configs[1]_sa1_16k_f32", pn.SA1_ONLY, "f32", 32, 16384, 40),
+                                            ("configs[4]_msg_131k_bf16", pn.MSG, "bf16", 8, 131072, 24)):
+            el2, k2 = measure(cfg, dtype, b2, n2, st, 2, args.depth, events_in_window=False)
             extras[key] = {"M_points_per_s": sharding.aggregate_rate(b2 * n2 * st, world, el2) / 1e6, "ms_per_step": el2 / st * 1e3,
                            "frames_per_gpu": b2, "points_per_frame": n2, "dtype": dtype,
                            "kernel_ms": k2}
@@ -211,13 +226,13 @@ def main():
     # with the main-stream kernels; it dominates only if it is longer than all of them
     side = ("sa1_fps", "sa1_ball_query")  # issued on the SA1 stream, overlapped with the rest
     main = {k: v for k, v in kern.items() if k not in side}
-    side_ms = sum(kern.get(k, 0) for k in side) / args.depth  # `depth` batches in flight
+    side_ms = sum(kern.get(k, 0) for k in side) / args.depth  # `depth` groups in flight
     dom = max(side, key=lambda k: kern.get(k, 0)) if side_ms > sum(main.values()) else \
         max(main, key=lambda k: main[k])
 
     def roof(name):
         bound, per_frame = work[name]
-        per_launch = per_frame * B
+        per_launch = per_frame * B * args.fps_group  # one launch covers a group of batches
         avg_s = kern[name] / 1e3
         if bound == "mfma":
             a, p, u = per_launch / avg_s / 1e12, FP32_MFMA_PEAK_TFLOPS, "TFLOP/s"
@@ -242,7 +257,8 @@ def main():
             "roofline": roof(dom),
             "roofline_all": {k: roof(k) for k in kern if k in work},
             "kernel_ms": kern,
-            "pipeline": {"executor": "pointnet2.StreamingSSG", "sa1_fps_batches_in_flight": args.depth},
+            "pipeline": {"executor": "pointnet2.StreamingSSG", "side_streams": args.depth,
+                         "batches_per_sa1_fps_launch": args.fps_group},
             "other_configs": extras,
             "density_path": density,
             "cpu_baseline": None,

@@ -447,20 +447,24 @@ class StreamingSSG:
     SA1's farthest-point sampling is a serial chain of N/16 argmax steps per frame
     (latency-bound, one workgroup per frame), while everything after it (ball queries,
     fused MFMA MLPs, SA2's nested FPS, group_all) fills the whole GPU.  `run` therefore
-    issues batch k+1's SA1 FPS on its own stream (own library handle / workspace) while
-    batch k's remaining levels run on the main stream; events order the hand-off and a
-    ring of `depth + 1` FPS output slots bounds memory.  Results are identical to
-    ``PointNet2Backbone.forward`` (same kernels, same inputs).
+    issues later batches' SA1 FPS (+ level-0 ball queries) on side streams (own library
+    handles / workspaces) while batch k's remaining levels run on the main stream; events
+    order the hand-off and a ring of `depth + 1` output slots bounds memory.
+
+    fps_group = G > 1: G consecutive batches are staged into one (G*B, N, 3) buffer; one
+    side-stream launch runs their SA1 FPS (G*B workgroups share the serial chain of steps
+    without needing more streams than the device's hardware queues) and one main-stream
+    pass runs their MFMA levels (larger launches fill the chip better).  Every operator is
+    per frame, so results are identical to ``PointNet2Backbone.forward`` per batch.
     """
 
-    def __init__(self, backbone, batch, n, depth=1, side_priority=0, side_cus=0, cu_layout="xcd"):
+    def __init__(self, backbone, batch, n, depth=1, side_priority=0, side_cus=0, cu_layout="xcd", fps_group=1):
         """side_cus > 0: the SA1 FPS / ball-query streams run on `side_cus` CUs and the
-        main stream on the rest (CU-masked HIP streams), so the latency-bound FPS waves and
-        the MFMA waves stop competing for registers, issue slots and L2.  cu_layout "xcd"
-        takes side_cus/8 CUs of each of the 8 XCDs (mask bit = 32*xcd + cu), "low" the
-        lowest-numbered CUs."""
+        main stream on the rest (CU-masked HIP streams; measured slower).
+        cu_layout "xcd" takes side_cus/8 CUs of each of the 8 XCDs (mask bit = 32*xcd + cu),
+        "low" the lowest-numbered CUs."""
         self.bb = backbone
-        self.B, self.N, self.depth = batch, n, depth
+        self.B, self.N, self.depth, self.G = batch, n, depth, max(1, int(fps_group))
         dev = backbone.device
         lvl0 = backbone.levels[0]
         self.M1 = max(1, n // lvl0["div"])
@@ -476,11 +480,14 @@ class StreamingSSG:
             # the dispatcher (HIP stream priority); results do not depend on it
             self.fps_streams = [torch.cuda.Stream(device=dev, priority=side_priority) for _ in range(depth)]
         nslot = depth + 1
-        self.idx = [torch.empty((batch, self.M1), dtype=torch.int32, device=dev) for _ in range(nslot)]
-        self.cxyz = [torch.empty((batch, self.M1, 3), dtype=torch.float32, device=dev) for _ in range(nslot)]
-        self.fz = [torch.empty(batch, dtype=torch.int32, device=dev) for _ in range(nslot)]
+        GB = self.G * batch
+        self.stage = [torch.empty((GB, n, 3), dtype=torch.float32, device=dev) if self.G > 1 else None
+                      for _ in range(nslot)]
+        self.idx = [torch.empty((GB, self.M1), dtype=torch.int32, device=dev) for _ in range(nslot)]
+        self.cxyz = [torch.empty((GB, self.M1, 3), dtype=torch.float32, device=dev) for _ in range(nslot)]
+        self.fz = [torch.empty(GB, dtype=torch.int32, device=dev) for _ in range(nslot)]
         # level-0 ball queries of every branch ride on the FPS stream too
-        self.gidx = [[torch.empty((batch, self.M1, br["ns"]), dtype=torch.int32, device=dev)
+        self.gidx = [[torch.empty((GB, self.M1, br["ns"]), dtype=torch.int32, device=dev)
                       for br in lvl0["branches"]] for _ in range(nslot)]
         self.fps_done = [torch.cuda.Event() for _ in range(nslot)]
         self.slot_free = [torch.cuda.Event() for _ in range(nslot)]
@@ -503,27 +510,43 @@ class StreamingSSG:
             except Exception:
                 pass
 
-    def _fps(self, k, x):
+    def _fps(self, k, xs, ready):
+        """SA1 FPS + level-0 ball queries of group k (the batches in xs) on a side stream."""
         slot = k % (self.depth + 1)
         fs = self.fps_streams[k % self.depth]
         fs.wait_event(self.slot_free[slot])
+        fs.wait_event(ready)
+        g = len(xs) * self.B
         with torch.cuda.stream(fs):
+            if self.G > 1:
+                x = self.stage[slot][:g]
+                for j, xj in enumerate(xs):
+                    x[j * self.B:(j + 1) * self.B].copy_(xj, non_blocking=True)
+            else:
+                x = xs[0]
+            for xj in xs:  # read on this stream: keep the caller's buffers alive until then
+                xj.record_stream(fs)
             _call(self.bb.timers, "sa1_fps", farthest_point_sample, x, self.M1, return_xyz=True,
-                  first_zero=self.fz[slot], slot=1 + k % self.depth, out_idx=self.idx[slot],
-                  out_xyz=self.cxyz[slot])
+                  first_zero=self.fz[slot][:g], slot=1 + k % self.depth, out_idx=self.idx[slot][:g],
+                  out_xyz=self.cxyz[slot][:g])
             lvl0 = self.bb.levels[0]
             for bi_, br in enumerate(lvl0["branches"]):
                 tag = "sa1" + (f"_b{bi_}" if len(lvl0["branches"]) > 1 else "")
-                _call(self.bb.timers, f"{tag}_ball_query", ball_query, br["r"], br["ns"], x, self.cxyz[slot],
-                      out=self.gidx[slot][bi_], slot=1 + k % self.depth)
+                _call(self.bb.timers, f"{tag}_ball_query", ball_query, br["r"], br["ns"], x, self.cxyz[slot][:g],
+                      out=self.gidx[slot][bi_][:g], slot=1 + k % self.depth)
             self.fps_done[slot].record(fs)
         return slot
 
-    def _rest(self, slot, x, main):
+    def _rest(self, slot, xs, main):
+        """The MFMA levels of a group: one pass over its staged frames (every operator is per
+        frame, so the per-batch outputs are views of the group's), split back per batch."""
         main.wait_event(self.fps_done[slot])
-        out = self.bb.forward_from_sa1_fps(x, self.idx[slot], self.cxyz[slot], self.fz[slot], self.gidx[slot])
+        B, g = self.B, len(xs) * self.B
+        x = self.stage[slot][:g] if self.G > 1 else xs[0]
+        out = self.bb.forward_from_sa1_fps(x, self.idx[slot][:g], self.cxyz[slot][:g], self.fz[slot][:g],
+                                           [gi[:g] for gi in self.gidx[slot]])
         self.slot_free[slot].record(main)
-        return out
+        return list(out.split(B)) if len(xs) > 1 else [out]
 
     def run(self, inputs):
         """inputs: list of (B, N, 3) CUDA tensors -> list of global features (B, C)."""
@@ -538,14 +561,18 @@ class StreamingSSG:
 
     def _run(self, inputs):
         main = torch.cuda.current_stream(self.bb.device)
+        ready = torch.cuda.Event()
+        ready.record(main)  # the inputs exist on the caller's stream
+        groups = [inputs[i:i + self.G] for i in range(0, len(inputs), self.G)]
         outs = []
         pending = []
-        for k, x in enumerate(inputs):
-            pending.append((self._fps(k, x), x))
+        for k, xs in enumerate(groups):
+            pending.append((self._fps(k, xs, ready), xs))
             if len(pending) > self.depth:
-                slot, px = pending.pop(0)
-                outs.append(self._rest(slot, px, main))
+                slot, pxs = pending.pop(0)
+                outs.extend(self._rest(slot, pxs, main))
         while pending:
-            slot, px = pending.pop(0)
-            outs.append(self._rest(slot, px, main))
+            slot, pxs = pending.pop(0)
+            outs.extend(self._rest(slot, pxs, main))
         return outs
+

@@ -204,6 +204,21 @@ def test_streaming_executor_matches_forward(cuda, depth):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("cfg_name,dtype,group,depth,nb", [("ssg", "f32", 2, 3, 5), ("ssg", "f32", 3, 2, 7),
+                                                          ("msg", "bf16", 2, 2, 3)])
+def test_streaming_grouped_fps_matches_forward(cuda, cfg_name, dtype, group, depth, nb):
+    """fps_group > 1: one SA1-FPS / ball-query launch covers several batches (staged into one
+    buffer); a partial last group included.  Bit-identical to forward()."""
+    bb = pn.PointNet2Backbone(pn.CONFIGS[cfg_name], device=cuda, seed=2, dtype=dtype)
+    xs = [torch.from_numpy(unit_frames(2, 4096, 10 + s)).to(cuda) for s in range(nb)]
+    want = [bb.forward(x)[0] for x in xs]
+    got = pn.StreamingSSG(bb, 2, 4096, depth=depth, fps_group=group).run(xs)
+    torch.cuda.synchronize()
+    assert len(got) == nb
+    for a, b in zip(got, want):
+        assert torch.equal(a, b)
+
+
 
 def bf16_close(got, want, what=""):
     """bf16 tolerance: inputs/activations are rounded to bf16 on both sides, so results agree

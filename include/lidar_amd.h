@@ -44,6 +44,14 @@ int lidar_create(int device, lidar_handle **out);
 int lidar_destroy(lidar_handle *h);
 /* grow the scratch workspace to at least `bytes` now (not inside graph capture) */
 int lidar_reserve(lidar_handle *h, uint64_t bytes);
+
+/* A HIP stream restricted to a subset of the device's compute units (bit i of mask[i/32]
+ * enables CU i), returned through *stream (a hipStream_t); release with
+ * lidar_stream_destroy.  StreamingSSG's optional side_cus split uses it. */
+int lidar_stream_create_cu_mask(int device, const uint32_t *mask, int32_t nwords, void **stream);
+int lidar_stream_destroy(void *stream);
+/* number of compute units of `device` */
+int lidar_device_cu_count(int device, int32_t *out);
 const char *lidar_last_error(void);
 int lidar_version(void);
 

@@ -124,22 +124,24 @@ def tier_r_cpu_baseline(n, budget_s=12.0):
                       f"(byte-identical restatement of the reference's numpy/sklearn path, 1 thread) in {dt:.1f} s"}
 
 
-def tier_r_leg(dev, rank, world, frames=16, n=65536, workers=4, steps=3, cpu=True, cpu_budget=12.0):
+def tier_r_leg(dev, rank, world, frames=32, n=65536, workers=4, steps=3, cpu=True, cpu_budget=12.0):
     """The reference's own path (Tier R: preprocess -> DBSCAN -> people -> density grid) on
-    device-resident uniform +-15 m frames through density_stream.DensityStream."""
+    device-resident uniform +-15 m frames: batches of `frames` frames through
+    density_stream.DensityStream.run_batch (one launch per phase over the CSR batch)."""
     import torch
     from lidar_ai_recommendation_software_amd import sharding
     from lidar_ai_recommendation_software_amd.density_stream import DensityStream
     from lidar_ai_recommendation_software_amd.synthetic import uniform_frame
     xs = [torch.from_numpy(uniform_frame(n, sharding.frame_seed(rank, base=1000 + i))).to(dev) for i in range(frames)]
     ds = DensityStream(dev, workers=workers)
-    ds.run(xs[:workers])  # warm-up: workspaces sized
-    el = sharding.timed(lambda: [ds.run(xs) for _ in range(steps)], dev, world)
+    ds.run_batch(xs)  # warm-up: workspaces sized
+    el = sharding.timed(lambda: [ds.run_batch(xs) for _ in range(steps)], dev, world)
     rec = {"metric": "M points/s through the reference density path (preprocess + DBSCAN + people + "
                      "density grid), device-resident frames",
            "value": sharding.aggregate_rate(frames * n * steps, world, el) / 1e6, "unit": "M points/s",
            "ms_per_frame": el / (frames * steps) * 1e3, "frames_per_gpu": frames, "points_per_frame": n,
-           "workers": workers, "dtype": "f64", "parity": "byte-identical to the reference (tests/golden)",
+           "executor": "DensityStream.run_batch (CSR batch, one launch per phase)", "dtype": "f64",
+           "parity": "byte-identical to the reference (tests/golden)",
            "cpu_baseline": None}
     if cpu and rank == 0 and world == 1:
         rec["cpu_baseline"] = tier_r_cpu_baseline(n, cpu_budget)

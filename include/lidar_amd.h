@@ -179,6 +179,31 @@ int lidar_preprocess_f64(lidar_handle *h, const double *xyz, int64_t n, uint8_t 
                          double *colors, double *normals, double *compact_xyz, int64_t *labels,
                          double *scalars, void *stream);
 
+/* lidar_preprocess_f64 over `frames` frames in one launch per phase (frames in
+ * CSR layout).  xyz: the frames' rows concatenated; offsets: DEVICE int64[frames + 1] row
+ * offsets (frame f = rows [offsets[f], offsets[f+1])); max_n >= every frame's size.  The
+ * per-point outputs use the same row offsets (a frame's compact_xyz / labels rows start at
+ * offsets[f] and run for its own n_in = scalars[f*64 + 0]); scalars holds 64 doubles per
+ * frame, with [15] status: 0 ok, 1 no inlier (IndexError), 2 empty frame (ValueError). */
+int lidar_preprocess_batch_f64(lidar_handle *h, const double *xyz, const int64_t *offsets, int32_t frames,
+                               int64_t max_n, uint8_t *mask, double *colors, double *normals,
+                               double *compact_xyz, int64_t *labels, double *scalars, void *stream);
+
+/* extract_people_positions for every frame of a preprocess batch: people rows of frame f
+ * start at row offsets[f] (K_f rows); kdev (device int64[frames]) receives K_f.  Async. */
+int lidar_people_batch_f64(lidar_handle *h, const double *compact_xyz, const int64_t *labels,
+                           const int64_t *offsets, int32_t frames, int64_t max_n, const double *scalars,
+                           double *people, int64_t *kdev, void *stream);
+
+/* the density grid + statistics + hotspots of every frame with K_f > 0.  jobs: device
+ * double[8 * frames] rows (xa = x_min - 2g, ya = y_min - 2g, g, nx, ny (lidar_grid_dims),
+ * output offset, scratch offset, 0); out at a frame's offset: grid_x (nx) | grid_y (ny) |
+ * density (nx*ny) | flat_x | flat_y | stats (8) | hot (5 int64); scratch_doubles = sum over
+ * frames of nx*ny + ceil(nx*ny/2) + nx + ny + 2.  Asynchronous. */
+int lidar_density_batch_f64(lidar_handle *h, const double *people, const int64_t *offsets,
+                            const int64_t *kdev, int32_t frames, const double *jobs, double *out,
+                            int64_t scratch_doubles, void *stream);
+
 /* people positions (extract_people_positions, utils/data_processing.py:251-280):
  * centroid (x, y) of every label >= 0, sequential index-order sums;
  * people (n,2) f64, *k_host receives K (synchronises). */

@@ -63,6 +63,9 @@ SIGNATURES = {
     "lidar_voxel_downsample_f32": [P, P, I64, F32, P, P, P, P, P],
     "lidar_dbscan_f64": [P, P, I64, F64, I32, P, P, P],
     "lidar_preprocess_f64": [P, P, I64, P, P, P, P, P, P, P],
+    "lidar_preprocess_batch_f64": [P, P, P, I32, I64, P, P, P, P, P, P, P],
+    "lidar_people_batch_f64": [P, P, P, P, I32, I64, P, P, P, P],
+    "lidar_density_batch_f64": [P, P, P, P, I32, P, P, I64, P],
     "lidar_people_f64": [P, P, P, I64, P, P, P],
     "lidar_grid_dims": [F64, F64, F64, F64, F64, P, P],
     "lidar_density_grid_f64": [P, P, I64, F64, F64, F64, F64, F64, I64, I64, P, P, P, P],

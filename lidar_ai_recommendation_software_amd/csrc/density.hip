@@ -35,6 +35,29 @@ enum : int {
     S_PLANE_KIND = 40, S_N = 41, S_MINPTS = 42, S_COUNT = 64
 };
 
+// ------------------------------------------------------------------ frame batching
+// Every Tier R kernel runs one frame per blockIdx.y.  Frame f's scratch lives at
+// f * wss bytes into one workspace allocation (same sub-buffer offsets in every frame),
+// its rows of the caller's arrays start at row offs[f] (CSR; offs == nullptr: a single
+// frame of the given n), and its scalars at S + f * S_COUNT.
+struct FrameMap {
+    int64_t wss = 0;
+    const int64_t *offs = nullptr;
+    template <class T> __device__ __forceinline__ T *ws(T *p) const
+    {
+        return reinterpret_cast<T *>(reinterpret_cast<uintptr_t>(p) + (uintptr_t)((int64_t)blockIdx.y * wss));
+    }
+    template <class T> __device__ __forceinline__ T *rows(T *p, int width) const
+    {
+        return offs ? p + offs[blockIdx.y] * width : p;
+    }
+    __device__ __forceinline__ int64_t n(int64_t single) const
+    {
+        return offs ? offs[blockIdx.y + 1] - offs[blockIdx.y] : single;
+    }
+    template <class T> __device__ __forceinline__ T *scal(T *S) const { return S + (int64_t)blockIdx.y * S_COUNT; }
+};
+
 __device__ __forceinline__ double dadd(double a, double b) { return __dadd_rn(a, b); }
 __device__ __forceinline__ double dsub(double a, double b) { return __dsub_rn(a, b); }
 __device__ __forceinline__ double dmul(double a, double b) { return __dmul_rn(a, b); }
@@ -160,18 +183,29 @@ __device__ __forceinline__ double unordkey(uint64_t k)
 
 
 // ------------------------------------------------------------------ preprocess
-__global__ __launch_bounds__(kT) void preprocess_kernel(const double *__restrict__ xyz, int64_t n,
-                                                        uint8_t *__restrict__ mask,
-                                                        double *__restrict__ colors,
-                                                        double *__restrict__ normals,
-                                                        double *__restrict__ comp,
-                                                        double *__restrict__ sc,
-                                                        int32_t *__restrict__ ng_pos,
-                                                        double *__restrict__ S)
+__global__ __launch_bounds__(kT) void preprocess_kernel(const double *__restrict__ xyz_in, int64_t n_in,
+                                                        uint8_t *__restrict__ mask_in,
+                                                        double *__restrict__ colors_in,
+                                                        double *__restrict__ normals_in,
+                                                        double *__restrict__ comp_in,
+                                                        double *__restrict__ sc_in,
+                                                        int32_t *__restrict__ ng_pos_in,
+                                                        double *__restrict__ S_in, FrameMap fm)
 {
     __shared__ BlockScratch s;
     __shared__ SeqStage st;
     const int tid = threadIdx.x;
+    const int64_t n = fm.n(n_in);
+    const double *xyz = fm.rows(xyz_in, 3);
+    uint8_t *mask = fm.rows(mask_in, 1);
+    double *colors = fm.rows(colors_in, 3), *normals = fm.rows(normals_in, 3), *comp = fm.rows(comp_in, 3);
+    double *sc = fm.ws(sc_in);
+    int32_t *ng_pos = fm.ws(ng_pos_in);
+    double *S = fm.scal(S_in);
+    if (n == 0) {  // an empty frame of a batch: the reference raises ValueError (status 2)
+        if (tid == 0) S[S_STATUS] = 2.0;
+        return;
+    }
 
     // ---- A: colours over ALL points (data_processing.py:143-147)
     double lo = INFINITY, hi = -INFINITY;
@@ -496,9 +530,11 @@ __global__ __launch_bounds__(kT) void preprocess_kernel(const double *__restrict
 enum : int { P_N = 0, P_EPS = 1, P_LO = 2, P_HI = 5, P_CELL = 8, P_DIM = 9, P_NCELL = 12,
              P_NCLUST = 13, P_ACTIVE = 14, P_COUNT = 16 };
 
-__global__ void dbscan_params_from_preprocess(const double *S, double *P, int64_t max_cells)
+__global__ void dbscan_params_from_preprocess(const double *S_in, double *P_in, int64_t max_cells, FrameMap fm)
 {
     if (threadIdx.x) return;
+    const double *S = fm.scal(S_in);
+    double *P = fm.ws(P_in);
     const double nng = S[S_NNG];
     P[P_N] = nng;
     P[P_EPS] = S[S_EPS];
@@ -509,8 +545,10 @@ __global__ void dbscan_params_from_preprocess(const double *S, double *P, int64_
     }
 }
 
-__global__ __launch_bounds__(kT) void dbscan_bbox_kernel(const double *x, double *P)
+__global__ __launch_bounds__(kT) void dbscan_bbox_kernel(const double *x_in, double *P_in, FrameMap fm)
 {
+    const double *x = fm.ws(x_in);
+    double *P = fm.ws(P_in);
     __shared__ BlockScratch s;
     const int64_t n = (int64_t)P[P_N];
     double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
@@ -528,9 +566,10 @@ __global__ __launch_bounds__(kT) void dbscan_bbox_kernel(const double *x, double
     }
 }
 
-__global__ void dbscan_setup_kernel(double *P, int64_t max_cells)
+__global__ void dbscan_setup_kernel(double *P_in, int64_t max_cells, FrameMap fm)
 {
     if (threadIdx.x) return;
+    double *P = fm.ws(P_in);
     const double n = P[P_N];
     double dims[3] = {1.0, 1.0, 1.0}, tot = 1.0;
     // cells strictly larger than eps: a 27-cell stencil sees every pair the fp64 test accepts
@@ -587,16 +626,21 @@ struct Grid {
     }
 };
 
-__global__ void zero_u32_kernel(uint32_t *a, const double *P, int idx, int64_t extra)
+__global__ void zero_u32_kernel(uint32_t *a_in, const double *P_in, int idx, int64_t extra, FrameMap fm)
 {
+    uint32_t *a = fm.ws(a_in);
+    const double *P = fm.ws(P_in);
     const int64_t n = (int64_t)P[idx] + extra;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
         a[i] = 0;
 }
 
-__global__ void dbscan_cells_kernel(const double *x, const double *P, uint32_t *cid, uint32_t *cellcnt,
-                                    int32_t *parent)
+__global__ void dbscan_cells_kernel(const double *x_in, const double *P_in, uint32_t *cid_in, uint32_t *cellcnt_in,
+                                    int32_t *parent_in, FrameMap fm)
 {
+    const double *x = fm.ws(x_in), *P = fm.ws(P_in);
+    uint32_t *cid = fm.ws(cid_in), *cellcnt = fm.ws(cellcnt_in);
+    int32_t *parent = fm.ws(parent_in);
     if (P[P_ACTIVE] == 0.0) return;
     Grid g;
     g.load(P);
@@ -610,9 +654,12 @@ __global__ void dbscan_cells_kernel(const double *x, const double *P, uint32_t *
 
 // --- exclusive scan of u32 over count = P[idx] (+extra) entries; out[count] = total
 constexpr int kScanPer = 4 * kT;
-__global__ __launch_bounds__(kT) void scan_partial_kernel(const uint32_t *in, const double *P, int idx,
-                                                          int64_t extra, uint32_t *partial)
+__global__ __launch_bounds__(kT) void scan_partial_kernel(const uint32_t *in_in, const double *P_in, int idx,
+                                                          int64_t extra, uint32_t *partial_in, FrameMap fm)
 {
+    const uint32_t *in = fm.ws(in_in);
+    const double *P = fm.ws(P_in);
+    uint32_t *partial = fm.ws(partial_in);
     const int64_t n = (int64_t)P[idx] + extra;
     const int64_t b0 = (int64_t)blockIdx.x * kScanPer;
     uint32_t v = 0;
@@ -630,8 +677,9 @@ __global__ __launch_bounds__(kT) void scan_partial_kernel(const uint32_t *in, co
         partial[blockIdx.x] = t;
     }
 }
-__global__ __launch_bounds__(kT) void scan_top_kernel(uint32_t *partial, int64_t nblk)
+__global__ __launch_bounds__(kT) void scan_top_kernel(uint32_t *partial_in, int64_t nblk, FrameMap fm)
 {
+    uint32_t *partial = fm.ws(partial_in);
     // nblk <= 4 * kT
     __shared__ uint32_t ws[kW];
     uint32_t v[4], s = 0;
@@ -657,9 +705,12 @@ __global__ __launch_bounds__(kT) void scan_top_kernel(uint32_t *partial, int64_t
         e += v[u];
     }
 }
-__global__ __launch_bounds__(kT) void scan_final_kernel(const uint32_t *in, uint32_t *out, const double *P,
-                                                        int idx, int64_t extra, const uint32_t *partial)
+__global__ __launch_bounds__(kT) void scan_final_kernel(const uint32_t *in_in, uint32_t *out_in, const double *P_in,
+                                                        int idx, int64_t extra, const uint32_t *partial_in, FrameMap fm)
 {
+    const uint32_t *in = fm.ws(in_in), *partial = fm.ws(partial_in);
+    uint32_t *out = fm.ws(out_in);
+    const double *P = fm.ws(P_in);
     const int64_t n = (int64_t)P[idx] + extra;
     const int64_t b0 = (int64_t)blockIdx.x * kScanPer;
     if (b0 > n) return;
@@ -688,9 +739,13 @@ __global__ __launch_bounds__(kT) void scan_final_kernel(const uint32_t *in, uint
     }
 }
 
-__global__ void dbscan_scatter_kernel(const double *x, const double *P, const uint32_t *cid,
-                                      uint32_t *fill, uint32_t *order, double *sxyz)
+__global__ void dbscan_scatter_kernel(const double *x_in, const double *P_in, const uint32_t *cid_in,
+                                      uint32_t *fill_in, uint32_t *order_in, double *sxyz_in, FrameMap fm)
 {
+    const double *x = fm.ws(x_in), *P = fm.ws(P_in);
+    const uint32_t *cid = fm.ws(cid_in);
+    uint32_t *fill = fm.ws(fill_in), *order = fm.ws(order_in);
+    double *sxyz = fm.ws(sxyz_in);
     if (P[P_ACTIVE] == 0.0) return;
     const int64_t n = (int64_t)P[P_N];
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
@@ -700,6 +755,16 @@ __global__ void dbscan_scatter_kernel(const double *x, const double *P, const ui
         sxyz[3 * pos + 1] = x[3 * i + 1];
         sxyz[3 * pos + 2] = x[3 * i + 2];
     }
+}
+
+__global__ void copy_u32_kernel(uint32_t *dst_in, const uint32_t *src_in, const double *P_in, int idx, int64_t extra,
+                                FrameMap fm)
+{
+    uint32_t *dst = fm.ws(dst_in);
+    const uint32_t *src = fm.ws(src_in);
+    const int64_t n = (int64_t)fm.ws(P_in)[idx] + extra;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        dst[i] = src[i];
 }
 
 // visit every sorted slot u whose point is within eps of point (px,py,pz) in cell c
@@ -724,9 +789,12 @@ __device__ __forceinline__ void for_neighbours(const Grid &g, const uint32_t *st
     }
 }
 
-__global__ void dbscan_count_kernel(const double *P, const uint32_t *cid, const uint32_t *start,
-                                    const uint32_t *order, const double *sxyz, int32_t *cnt)
+__global__ void dbscan_count_kernel(const double *P_in, const uint32_t *cid_in, const uint32_t *start_in,
+                                    const uint32_t *order_in, const double *sxyz_in, int32_t *cnt_in, FrameMap fm)
 {
+    const double *P = fm.ws(P_in), *sxyz = fm.ws(sxyz_in);
+    const uint32_t *cid = fm.ws(cid_in), *start = fm.ws(start_in), *order = fm.ws(order_in);
+    int32_t *cnt = fm.ws(cnt_in);
     if (P[P_ACTIVE] == 0.0) return;
     Grid g;
     g.load(P);
@@ -791,10 +859,14 @@ __device__ int32_t uf_unite(int32_t *parent, int32_t a, int32_t b)
     }
 }
 
-__global__ void dbscan_union_kernel(const double *P, const uint32_t *cid, const uint32_t *start,
-                                    const uint32_t *order, const double *sxyz, const int32_t *cnt,
-                                    int32_t min_samples, int32_t *parent)
+__global__ void dbscan_union_kernel(const double *P_in, const uint32_t *cid_in, const uint32_t *start_in,
+                                    const uint32_t *order_in, const double *sxyz_in, const int32_t *cnt_in,
+                                    int32_t min_samples, int32_t *parent_in, FrameMap fm)
 {
+    const double *P = fm.ws(P_in), *sxyz = fm.ws(sxyz_in);
+    const uint32_t *cid = fm.ws(cid_in), *start = fm.ws(start_in), *order = fm.ws(order_in);
+    const int32_t *cnt = fm.ws(cnt_in);
+    int32_t *parent = fm.ws(parent_in);
     if (P[P_ACTIVE] == 0.0) return;
     Grid g;
     g.load(P);
@@ -814,9 +886,13 @@ __global__ void dbscan_union_kernel(const double *P, const uint32_t *cid, const 
     }
 }
 
-__global__ void dbscan_roots_kernel(const double *P, const int32_t *cnt, int32_t min_samples,
-                                    int32_t *parent, uint32_t *flag)
+__global__ void dbscan_roots_kernel(const double *P_in, const int32_t *cnt_in, int32_t min_samples,
+                                    int32_t *parent_in, uint32_t *flag_in, FrameMap fm)
 {
+    const double *P = fm.ws(P_in);
+    const int32_t *cnt = fm.ws(cnt_in);
+    int32_t *parent = fm.ws(parent_in);
+    uint32_t *flag = fm.ws(flag_in);
     const int64_t n = (int64_t)P[P_N];
     const bool active = P[P_ACTIVE] != 0.0;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
@@ -830,11 +906,16 @@ __global__ void dbscan_roots_kernel(const double *P, const int32_t *cnt, int32_t
     }
 }
 
-__global__ void dbscan_labels_kernel(double *P, const uint32_t *cid, const uint32_t *start,
-                                     const uint32_t *order, const double *sxyz, const int32_t *cnt,
-                                     int32_t min_samples, const int32_t *parent, const uint32_t *rank,
-                                     int64_t *labels)
+__global__ void dbscan_labels_kernel(double *P_in, const uint32_t *cid_in, const uint32_t *start_in,
+                                     const uint32_t *order_in, const double *sxyz_in, const int32_t *cnt_in,
+                                     int32_t min_samples, const int32_t *parent_in, const uint32_t *rank_in,
+                                     int64_t *labels_in, FrameMap fm)
 {
+    double *P = fm.ws(P_in);
+    const double *sxyz = fm.ws(sxyz_in);
+    const uint32_t *cid = fm.ws(cid_in), *start = fm.ws(start_in), *order = fm.ws(order_in), *rank = fm.ws(rank_in);
+    const int32_t *cnt = fm.ws(cnt_in), *parent = fm.ws(parent_in);
+    int64_t *labels = fm.ws(labels_in);
     if (P[P_ACTIVE] == 0.0) return;
     Grid g;
     g.load(P);
@@ -860,18 +941,24 @@ __global__ void dbscan_labels_kernel(double *P, const uint32_t *cid, const uint3
 }
 
 // full labels over the inliers: ground -1, non-ground = DBSCAN label (or 0 when <= 10)
-__global__ void scatter_labels_kernel(const double *S, const int64_t *ng_labels, const int32_t *ng_pos,
-                                      int64_t *full)
+__global__ void scatter_labels_kernel(const double *S_in, const int64_t *ng_labels_in, const int32_t *ng_pos_in,
+                                      int64_t *full_in, FrameMap fm)
 {
+    const double *S = fm.scal(S_in);
+    int64_t *full = fm.rows(full_in, 1);
     if (S[S_STATUS] != 0.0) return;
     const int64_t nin = (int64_t)S[S_NIN];
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nin; i += stride) full[i] = -1;
     __syncthreads();
 }
-__global__ void scatter_labels2_kernel(const double *S, const int64_t *ng_labels, const int32_t *ng_pos,
-                                       int64_t *full)
+__global__ void scatter_labels2_kernel(const double *S_in, const int64_t *ng_labels_in, const int32_t *ng_pos_in,
+                                       int64_t *full_in, FrameMap fm)
 {
+    const double *S = fm.scal(S_in);
+    const int64_t *ng_labels = fm.ws(ng_labels_in);
+    const int32_t *ng_pos = fm.ws(ng_pos_in);
+    int64_t *full = fm.rows(full_in, 1);
     if (S[S_STATUS] != 0.0) return;
     const int64_t nng = (int64_t)S[S_NNG];
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -886,9 +973,16 @@ __global__ void scatter_labels2_kernel(const double *S, const int64_t *ng_labels
 // chunk (index order: wave w holds points [64(w-1), 64w) of the chunk, ballot-ranked) into
 // LDS, double-buffered; lanes 0 / 1 of wave 0 run the x / y chains in index order, as
 // np.mean of the member rows does (sequential axis-0 sums starting from the first row).
-__global__ __launch_bounds__(kT) void people_kernel(const double *xyz, const int64_t *labels, int64_t n,
-                                                    const int64_t *kdev, double *out)
+__global__ __launch_bounds__(kT) void people_kernel(const double *xyz_in, const int64_t *labels_in, int64_t n_in,
+                                                    const int64_t *kdev_in, double *out_in, const double *S_in,
+                                                    FrameMap fm)
 {
+    // a batch frame's rows are its inliers: n = scalars[S_NIN] (0 for a failed frame)
+    const int64_t n = S_in ? (fm.scal(S_in)[S_STATUS] == 0.0 ? (int64_t)fm.scal(S_in)[S_NIN] : 0) : n_in;
+    const double *xyz = fm.rows(xyz_in, 3);
+    const int64_t *labels = fm.rows(labels_in, 1);
+    const int64_t *kdev = kdev_in + blockIdx.y;
+    double *out = fm.rows(out_in, 2);
     constexpr int kChunk = kT - 64;
     __shared__ double mem[2][kChunk * 2];
     __shared__ int wcnt[2][kW];
@@ -941,8 +1035,12 @@ __global__ __launch_bounds__(kT) void people_kernel(const double *xyz, const int
     }
 }
 
-__global__ void max_label_kernel(const int64_t *labels, int64_t n, int64_t *kout)
+__global__ void max_label_kernel(const int64_t *labels_in, int64_t n_in, int64_t *kout_in, const double *S_in,
+                                 FrameMap fm)
 {
+    const int64_t n = S_in ? (fm.scal(S_in)[S_STATUS] == 0.0 ? (int64_t)fm.scal(S_in)[S_NIN] : 0) : n_in;
+    const int64_t *labels = fm.rows(labels_in, 1);
+    int64_t *kout = kout_in + blockIdx.y;
     // K = number of distinct labels >= 0 = max + 1 (labels are dense ranks)
     int64_t m = -1;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
@@ -996,12 +1094,12 @@ __device__ int64_t searchsorted_right(const double *e, int64_t len, double v)
     return lo;
 }
 
-__global__ __launch_bounds__(kT) void density_kernel(const double *people, const int64_t *kdev,
-                                                     double xa, double ya, double g, int64_t nx, int64_t ny,
-                                                     double *xe, double *ye, uint32_t *count,
-                                                     double *grid_x, double *grid_y, double *density,
-                                                     double *flat_x, double *flat_y, double *pos_scratch,
-                                                     double *stats, int64_t *hot)
+__device__ void density_body(const double *people, const int64_t *kdev,
+                             double xa, double ya, double g, int64_t nx, int64_t ny,
+                             double *xe, double *ye, uint32_t *count,
+                             double *grid_x, double *grid_y, double *density,
+                             double *flat_x, double *flat_y, double *pos_scratch,
+                             double *stats, int64_t *hot)
 {
     const int64_t K = *kdev;
     const int tid = threadIdx.x;
@@ -1074,6 +1172,43 @@ __global__ __launch_bounds__(kT) void density_kernel(const double *people, const
     }
 }
 
+__global__ __launch_bounds__(kT) void density_kernel(const double *people, const int64_t *kdev,
+                                                     double xa, double ya, double g, int64_t nx, int64_t ny,
+                                                     double *xe, double *ye, uint32_t *count,
+                                                     double *grid_x, double *grid_y, double *density,
+                                                     double *flat_x, double *flat_y, double *pos_scratch,
+                                                     double *stats, int64_t *hot)
+{
+    density_body(people, kdev, xa, ya, g, nx, ny, xe, ye, count, grid_x, grid_y, density, flat_x, flat_y,
+                 pos_scratch, stats, hot);
+}
+
+// one workgroup per frame; job row f (8 doubles): xa, ya, g, nx, ny, out offset, scratch
+// offset (doubles), unused.  out at its offset: grid_x | grid_y | density | flat_x | flat_y |
+// stats(8) | hot(5 int64); scratch: xe (nx+1) | ye (ny+1) | pos (nx*ny) | count (nx*ny u32).
+// Frames with no people (k == 0) are skipped (the caller returns the reference's empty dict).
+__global__ __launch_bounds__(kT) void density_batch_kernel(const double *people_in, const int64_t *offs,
+                                                           const int64_t *kdev, const double *jobs, double *out,
+                                                           double *scratch)
+{
+    const int f = blockIdx.y;
+    const double *J = jobs + 8 * (int64_t)f;
+    if (kdev[f] <= 0) return;
+    const int64_t nx = (int64_t)J[3], ny = (int64_t)J[4], m = nx * ny;
+    double *o = out + (int64_t)J[5];
+    double *sc = scratch + (int64_t)J[6];
+    double *xe = sc, *ye = xe + nx + 1, *pos = ye + ny + 1;
+    uint32_t *count = reinterpret_cast<uint32_t *>(pos + m);
+    double *gx = o, *gy = gx + nx, *dens = gy + ny, *fx = dens + m, *fy = fx + m, *st = fy + m;
+    density_body(people_in + 2 * offs[f], kdev + f, J[0], J[1], J[2], nx, ny, xe, ye, count, gx, gy, dens, fx, fy,
+                 pos, st, reinterpret_cast<int64_t *>(st + 8));
+}
+
+__global__ void nclust_kernel(const double *P_in, double *S_in, FrameMap fm)
+{
+    if (threadIdx.x == 0) fm.scal(S_in)[S_NCLUST] = fm.ws(P_in)[P_NCLUST];
+}
+
 // ------------------------------------------------------------------ workspace plan
 struct DbscanWs {
     double *P;
@@ -1124,34 +1259,81 @@ DbscanWs bind_dbscan(char *base, const uint64_t *off, int64_t n)
 }
 
 int run_scan(const uint32_t *in, uint32_t *out, const double *P, int idx, int64_t extra, uint32_t *partial,
-             int64_t nblk, hipStream_t s)
+             int64_t nblk, hipStream_t s, FrameMap fm, int frames)
 {
-    hipLaunchKernelGGL(scan_partial_kernel, dim3((unsigned)nblk), dim3(kT), 0, s, in, P, idx, extra, partial);
-    hipLaunchKernelGGL(scan_top_kernel, dim3(1), dim3(kT), 0, s, partial, nblk);
-    hipLaunchKernelGGL(scan_final_kernel, dim3((unsigned)nblk), dim3(kT), 0, s, in, out, P, idx, extra, partial);
+    hipLaunchKernelGGL(scan_partial_kernel, dim3((unsigned)nblk, frames), dim3(kT), 0, s, in, P, idx, extra, partial, fm);
+    hipLaunchKernelGGL(scan_top_kernel, dim3(1, frames), dim3(kT), 0, s, partial, nblk, fm);
+    hipLaunchKernelGGL(scan_final_kernel, dim3((unsigned)nblk, frames), dim3(kT), 0, s, in, out, P, idx, extra, partial,
+                       fm);
     LAUNCH_CHECK();
     return LIDAR_OK;
 }
 
-// the DBSCAN pipeline on x (P[P_N] points, eps P[P_EPS], bbox in P) -> labels
-int run_dbscan(const double *x, int64_t nmax, int32_t min_samples, DbscanWs &w, int64_t *labels, hipStream_t s)
+// blocks per frame of a per-point kernel: enough to fill the chip across all frames
+unsigned point_blocks(int64_t nmax, int frames)
 {
-    const unsigned gp = (unsigned)std::max<int64_t>(1, std::min<int64_t>((nmax + 255) / 256, 4096));
-    hipLaunchKernelGGL(dbscan_setup_kernel, dim3(1), dim3(64), 0, s, w.P, w.max_cells);
-    hipLaunchKernelGGL(zero_u32_kernel, dim3(512), dim3(256), 0, s, w.cellcnt, w.P, P_NCELL, 1);
-    hipLaunchKernelGGL(dbscan_cells_kernel, dim3(gp), dim3(256), 0, s, x, w.P, w.cid, w.cellcnt, w.parent);
-    int rc = run_scan(w.cellcnt, w.cellstart, w.P, P_NCELL, 0, w.partial, w.nblk_cells, s);
+    const int64_t cap = std::max<int64_t>(8, 4096 / std::max(1, frames));
+    return (unsigned)std::max<int64_t>(1, std::min<int64_t>((nmax + 255) / 256, cap));
+}
+
+// the DBSCAN pipeline on x (P[P_N] points, eps P[P_EPS], bbox in P) -> labels, for every frame
+int run_dbscan(const double *x, int64_t nmax, int32_t min_samples, DbscanWs &w, int64_t *labels, hipStream_t s,
+               FrameMap fm, int frames)
+{
+    const unsigned gp = point_blocks(nmax, frames);
+    const unsigned gc = point_blocks(w.max_cells, frames);
+    const dim3 F1(1, frames), FP(gp, frames), FC(gc, frames);
+    hipLaunchKernelGGL(dbscan_setup_kernel, F1, dim3(64), 0, s, w.P, w.max_cells, fm);
+    hipLaunchKernelGGL(zero_u32_kernel, FC, dim3(256), 0, s, w.cellcnt, w.P, P_NCELL, 1, fm);
+    hipLaunchKernelGGL(dbscan_cells_kernel, FP, dim3(256), 0, s, x, w.P, w.cid, w.cellcnt, w.parent, fm);
+    int rc = run_scan(w.cellcnt, w.cellstart, w.P, P_NCELL, 0, w.partial, w.nblk_cells, s, fm, frames);
     if (rc) return rc;
-    HIP_TRY(hipMemcpyAsync(w.fill, w.cellstart, sizeof(uint32_t) * (w.max_cells + 1), hipMemcpyDeviceToDevice, s));
-    hipLaunchKernelGGL(dbscan_scatter_kernel, dim3(gp), dim3(256), 0, s, x, w.P, w.cid, w.fill, w.order, w.sxyz);
-    hipLaunchKernelGGL(dbscan_count_kernel, dim3(gp), dim3(256), 0, s, w.P, w.cid, w.cellstart, w.order, w.sxyz, w.cnt);
-    hipLaunchKernelGGL(dbscan_union_kernel, dim3(gp), dim3(256), 0, s, w.P, w.cid, w.cellstart, w.order, w.sxyz,
-                       w.cnt, min_samples, w.parent);
-    hipLaunchKernelGGL(dbscan_roots_kernel, dim3(gp), dim3(256), 0, s, w.P, w.cnt, min_samples, w.parent, w.flag);
-    rc = run_scan(w.flag, w.rank, w.P, P_N, 0, w.partial, w.nblk_pts, s);
+    hipLaunchKernelGGL(copy_u32_kernel, FC, dim3(256), 0, s, w.fill, w.cellstart, w.P, P_NCELL, 1, fm);
+    hipLaunchKernelGGL(dbscan_scatter_kernel, FP, dim3(256), 0, s, x, w.P, w.cid, w.fill, w.order, w.sxyz, fm);
+    hipLaunchKernelGGL(dbscan_count_kernel, FP, dim3(256), 0, s, w.P, w.cid, w.cellstart, w.order, w.sxyz, w.cnt, fm);
+    hipLaunchKernelGGL(dbscan_union_kernel, FP, dim3(256), 0, s, w.P, w.cid, w.cellstart, w.order, w.sxyz,
+                       w.cnt, min_samples, w.parent, fm);
+    hipLaunchKernelGGL(dbscan_roots_kernel, FP, dim3(256), 0, s, w.P, w.cnt, min_samples, w.parent, w.flag, fm);
+    rc = run_scan(w.flag, w.rank, w.P, P_N, 0, w.partial, w.nblk_pts, s, fm, frames);
     if (rc) return rc;
-    hipLaunchKernelGGL(dbscan_labels_kernel, dim3(gp), dim3(256), 0, s, w.P, w.cid, w.cellstart, w.order, w.sxyz,
-                       w.cnt, min_samples, w.parent, w.rank, labels);
+    hipLaunchKernelGGL(dbscan_labels_kernel, FP, dim3(256), 0, s, w.P, w.cid, w.cellstart, w.order, w.sxyz,
+                       w.cnt, min_samples, w.parent, w.rank, labels, fm);
+    LAUNCH_CHECK();
+    return LIDAR_OK;
+}
+
+// preprocess + DBSCAN + label scatter for `frames` frames (CSR rows, offs on the device;
+// offs == nullptr: one frame of n points)
+int run_preprocess(lidar_handle *h, const double *xyz, int64_t n, const int64_t *offs, int frames, uint8_t *mask,
+                   double *colors, double *normals, double *compact_xyz, int64_t *labels, double *scalars,
+                   hipStream_t s)
+{
+    lidar::Carver cv;
+    const uint64_t o_sc = cv.take<double>(3 * n);
+    const uint64_t o_pos = cv.take<int32_t>(n);
+    const uint64_t o_lab = cv.take<int64_t>(n);
+    uint64_t off[12];
+    plan_dbscan(cv, n, off);
+    const uint64_t wss = lidar::align_up(cv.off, 256);
+    char *base = static_cast<char *>(lidar::workspace(h, wss * (uint64_t)frames));
+    if (!base) return LIDAR_ENOMEM;
+    double *sc = reinterpret_cast<double *>(base + o_sc);
+    int32_t *ng_pos = reinterpret_cast<int32_t *>(base + o_pos);
+    int64_t *ng_lab = reinterpret_cast<int64_t *>(base + o_lab);
+    DbscanWs w = bind_dbscan(base, off, n);
+    FrameMap fm;
+    fm.wss = (int64_t)wss;
+    fm.offs = offs;
+    HIP_TRY(hipMemsetAsync(scalars, 0, sizeof(double) * S_COUNT * frames, s));
+    hipLaunchKernelGGL(preprocess_kernel, dim3(1, frames), dim3(kT), 0, s, xyz, n, mask, colors, normals,
+                       compact_xyz, sc, ng_pos, scalars, fm);
+    hipLaunchKernelGGL(dbscan_params_from_preprocess, dim3(1, frames), dim3(64), 0, s, scalars, w.P, w.max_cells, fm);
+    int rc = run_dbscan(sc, n, 5, w, ng_lab, s, fm, frames);
+    if (rc) return rc;
+    const unsigned gp = point_blocks(n, frames);
+    hipLaunchKernelGGL(scatter_labels_kernel, dim3(gp, frames), dim3(256), 0, s, scalars, ng_lab, ng_pos, labels, fm);
+    hipLaunchKernelGGL(scatter_labels2_kernel, dim3(gp, frames), dim3(256), 0, s, scalars, ng_lab, ng_pos, labels, fm);
+    hipLaunchKernelGGL(nclust_kernel, dim3(1, frames), dim3(64), 0, s, w.P, scalars, fm);
     LAUNCH_CHECK();
     return LIDAR_OK;
 }
@@ -1180,8 +1362,8 @@ LIDAR_EXPORT int lidar_dbscan_f64(lidar_handle *h, const double *x, int64_t n, d
     hp[P_EPS] = eps;
     hp[P_ACTIVE] = 1.0;
     HIP_TRY(hipMemcpyAsync(w.P, hp, sizeof hp, hipMemcpyHostToDevice, s));
-    hipLaunchKernelGGL(dbscan_bbox_kernel, dim3(1), dim3(kT), 0, s, x, w.P);
-    int rc = run_dbscan(x, n, min_samples, w, labels, s);
+    hipLaunchKernelGGL(dbscan_bbox_kernel, dim3(1), dim3(kT), 0, s, x, w.P, FrameMap{});
+    int rc = run_dbscan(x, n, min_samples, w, labels, s, FrameMap{}, 1);
     if (rc) return rc;
     if (counts) HIP_TRY(hipMemcpyAsync(counts, w.cnt, sizeof(int32_t) * n, hipMemcpyDeviceToDevice, s));
     // hp is a stack buffer: make sure the H2D copy has consumed it
@@ -1197,31 +1379,22 @@ LIDAR_EXPORT int lidar_preprocess_f64(lidar_handle *h, const double *xyz, int64_
             "lidar_preprocess_f64: null pointer");
     REQUIRE(n >= 1 && n < 0x7fffffff, "lidar_preprocess_f64: need 1 <= n < 2^31");
     HIP_TRY(hipSetDevice(h->device));
-    hipStream_t s = static_cast<hipStream_t>(stream);
-    lidar::Carver cv;
-    const uint64_t o_sc = cv.take<double>(3 * n);
-    const uint64_t o_pos = cv.take<int32_t>(n);
-    const uint64_t o_lab = cv.take<int64_t>(n);
-    uint64_t off[12];
-    plan_dbscan(cv, n, off);
-    char *base = static_cast<char *>(lidar::workspace(h, cv.off));
-    if (!base) return LIDAR_ENOMEM;
-    double *sc = reinterpret_cast<double *>(base + o_sc);
-    int32_t *ng_pos = reinterpret_cast<int32_t *>(base + o_pos);
-    int64_t *ng_lab = reinterpret_cast<int64_t *>(base + o_lab);
-    DbscanWs w = bind_dbscan(base, off, n);
-    HIP_TRY(hipMemsetAsync(scalars, 0, sizeof(double) * S_COUNT, s));
-    hipLaunchKernelGGL(preprocess_kernel, dim3(1), dim3(kT), 0, s, xyz, n, mask, colors, normals, compact_xyz,
-                       sc, ng_pos, scalars);
-    hipLaunchKernelGGL(dbscan_params_from_preprocess, dim3(1), dim3(64), 0, s, scalars, w.P, w.max_cells);
-    int rc = run_dbscan(sc, n, 5, w, ng_lab, s);
-    if (rc) return rc;
-    const unsigned gp = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 4096));
-    hipLaunchKernelGGL(scatter_labels_kernel, dim3(gp), dim3(256), 0, s, scalars, ng_lab, ng_pos, labels);
-    hipLaunchKernelGGL(scatter_labels2_kernel, dim3(gp), dim3(256), 0, s, scalars, ng_lab, ng_pos, labels);
-    HIP_TRY(hipMemcpyAsync(scalars + S_NCLUST, w.P + P_NCLUST, sizeof(double), hipMemcpyDeviceToDevice, s));
-    LAUNCH_CHECK();
-    return LIDAR_OK;
+    return run_preprocess(h, xyz, n, nullptr, 1, mask, colors, normals, compact_xyz, labels, scalars,
+                          static_cast<hipStream_t>(stream));
+}
+
+LIDAR_EXPORT int lidar_preprocess_batch_f64(lidar_handle *h, const double *xyz, const int64_t *offsets,
+                                            int32_t frames, int64_t max_n, uint8_t *mask, double *colors,
+                                            double *normals, double *compact_xyz, int64_t *labels,
+                                            double *scalars, void *stream)
+{
+    REQUIRE(h && xyz && offsets && mask && colors && normals && compact_xyz && labels && scalars,
+            "lidar_preprocess_batch_f64: null pointer");
+    REQUIRE(frames >= 1 && frames <= 65535, "lidar_preprocess_batch_f64: need 1 <= frames <= 65535");
+    REQUIRE(max_n >= 1 && max_n < 0x7fffffff, "lidar_preprocess_batch_f64: need 1 <= max_n < 2^31");
+    HIP_TRY(hipSetDevice(h->device));
+    return run_preprocess(h, xyz, max_n, offsets, frames, mask, colors, normals, compact_xyz, labels, scalars,
+                          static_cast<hipStream_t>(stream));
 }
 
 LIDAR_EXPORT int lidar_people_f64(lidar_handle *h, const double *xyz, const int64_t *labels, int64_t n,
@@ -1237,8 +1410,8 @@ LIDAR_EXPORT int lidar_people_f64(lidar_handle *h, const double *xyz, const int6
     if (!kd) return LIDAR_ENOMEM;
     HIP_TRY(hipMemsetAsync(kd, 0, sizeof(int64_t), s));
     const unsigned gp = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 1024));
-    hipLaunchKernelGGL(max_label_kernel, dim3(gp), dim3(256), 0, s, labels, n, kd);
-    hipLaunchKernelGGL(people_kernel, dim3(256), dim3(kT), 0, s, xyz, labels, n, kd, people);
+    hipLaunchKernelGGL(max_label_kernel, dim3(gp), dim3(256), 0, s, labels, n, kd, nullptr, FrameMap{});
+    hipLaunchKernelGGL(people_kernel, dim3(256), dim3(kT), 0, s, xyz, labels, n, kd, people, nullptr, FrameMap{});
     LAUNCH_CHECK();
     int64_t *hk = static_cast<int64_t *>(h->host_pinned);
     HIP_TRY(hipMemcpyAsync(hk, kd, sizeof(int64_t), hipMemcpyDeviceToHost, s));
@@ -1294,5 +1467,46 @@ LIDAR_EXPORT int lidar_density_grid_f64(lidar_handle *h, const double *people, i
                        reinterpret_cast<double *>(base + o_pos), stats, hot);
     LAUNCH_CHECK();
     HIP_TRY(hipStreamSynchronize(s));  // hk is reused by the next call
+    return LIDAR_OK;
+}
+
+// people of every frame of a preprocess batch (CSR rows, device offsets, scalars of the
+// batch): people rows of frame f start at row offsets[f]; kdev (device int64[frames])
+// receives K per frame.  Asynchronous.
+LIDAR_EXPORT int lidar_people_batch_f64(lidar_handle *h, const double *compact_xyz, const int64_t *labels,
+                                        const int64_t *offsets, int32_t frames, int64_t max_n,
+                                        const double *scalars, double *people, int64_t *kdev, void *stream)
+{
+    REQUIRE(h && compact_xyz && labels && offsets && scalars && people && kdev, "lidar_people_batch_f64: null pointer");
+    REQUIRE(frames >= 1 && frames <= 65535 && max_n >= 1, "lidar_people_batch_f64: bad sizes");
+    HIP_TRY(hipSetDevice(h->device));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    FrameMap fm;
+    fm.offs = offsets;
+    HIP_TRY(hipMemsetAsync(kdev, 0, sizeof(int64_t) * frames, s));
+    hipLaunchKernelGGL(max_label_kernel, dim3(point_blocks(max_n, frames), frames), dim3(256), 0, s, labels, max_n,
+                       kdev, scalars, fm);
+    const unsigned pb = (unsigned)std::max(1, std::min(256, 2048 / std::max(1, (int)frames)));
+    hipLaunchKernelGGL(people_kernel, dim3(pb, frames), dim3(kT), 0, s, compact_xyz, labels, max_n, kdev, people,
+                       scalars, fm);
+    LAUNCH_CHECK();
+    return LIDAR_OK;
+}
+
+// density grids of every frame (see density_batch_kernel for the job / output layout);
+// scratch_doubles = the sum over frames of nx*ny + ceil(nx*ny/2) + nx + ny + 2.  Asynchronous.
+LIDAR_EXPORT int lidar_density_batch_f64(lidar_handle *h, const double *people, const int64_t *offsets,
+                                         const int64_t *kdev, int32_t frames, const double *jobs, double *out,
+                                         int64_t scratch_doubles, void *stream)
+{
+    REQUIRE(h && people && offsets && kdev && jobs && out, "lidar_density_batch_f64: null pointer");
+    REQUIRE(frames >= 1 && frames <= 65535 && scratch_doubles >= 0, "lidar_density_batch_f64: bad sizes");
+    HIP_TRY(hipSetDevice(h->device));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    double *scratch = static_cast<double *>(lidar::workspace(h, (uint64_t)std::max<int64_t>(1, scratch_doubles) * 8));
+    if (!scratch) return LIDAR_ENOMEM;
+    hipLaunchKernelGGL(density_batch_kernel, dim3(1, frames), dim3(kT), 0, s, people, offsets, kdev, jobs, out,
+                       scratch);
+    LAUNCH_CHECK();
     return LIDAR_OK;
 }

@@ -30,7 +30,10 @@
 
 namespace {
 
-constexpr int kThreads = 1024;  // 16 waves: active-bucket updates and their reductions run in
+#ifndef FPS_THREADS
+#define FPS_THREADS 1024
+#endif
+constexpr int kThreads = FPS_THREADS;  // 16 waves: active-bucket updates and their reductions run in
                                 // parallel across waves; the merge is an LDS atomic max
 constexpr int kWaves = kThreads / 64;
 constexpr int kGrid = 16;  // Morton cells per axis for the bucket ordering
@@ -449,6 +452,7 @@ LIDAR_EXPORT int lidar_fps_f32(lidar_handle *h, const float *xyz, int64_t batch,
     REQUIRE(h && xyz && idx, "lidar_fps_f32: null pointer");
     REQUIRE(batch >= 0 && n >= 1 && npoint >= 1, "lidar_fps_f32: need n >= 1 and npoint >= 1");
     REQUIRE(n <= 4 * 65536, "lidar_fps_f32: n > 262144 points per frame");
+    REQUIRE((n + 63) / 64 <= 8 * kLoopWaves * 64, "lidar_fps_f32: too many buckets for this build");
     REQUIRE(batch <= 0x7fffffff, "lidar_fps_f32: batch too large");
     if (batch == 0) return LIDAR_OK;
     HIP_TRY(hipSetDevice(h->device));
@@ -471,7 +475,8 @@ LIDAR_EXPORT int lidar_fps_f32(lidar_handle *h, const float *xyz, int64_t batch,
     int rc;
     if (nb <= lanes) rc = go(fps_bucket_kernel<1>);
     else if (nb <= 2 * lanes) rc = go(fps_bucket_kernel<2>);
-    else rc = go(fps_bucket_kernel<4>);  // n <= 262144 is checked above
+    else if (nb <= 4 * lanes) rc = go(fps_bucket_kernel<4>);
+    else rc = go(fps_bucket_kernel<8>);
     if (rc) return rc;
     LAUNCH_CHECK();
     return LIDAR_OK;

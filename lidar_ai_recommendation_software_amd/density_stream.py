@@ -6,10 +6,13 @@ frames already in HBM and many of them in flight: the per-frame chain (preproces
 DBSCAN -> people -> density grid, ``utils/data_processing.py:127-328`` +
 ``models/crowd_density_model.py:23-98``) has three small host read-backs (the scalars
 that size the next step, K, the grid), so one frame alone leaves the GPU idle between
-them.  ``DensityStream`` runs ``workers`` frames concurrently, each worker thread on its
-own HIP stream with its own library handle (workspace), and returns per frame the
-reference's ``analyze`` result (the big per-point arrays stay on the device and are
-returned as tensors).  Results are the drop-in path's, bit for bit (same kernels).
+them.  ``DensityStream.run`` runs ``workers`` frames concurrently, each worker thread on its
+own HIP stream with its own library handle (workspace).  ``DensityStream.run_batch``
+processes a whole batch of frames with one launch per phase instead (frames in CSR
+layout: ``lidar_preprocess_batch_f64`` / ``lidar_people_batch_f64`` /
+``lidar_density_batch_f64``), three small host read-backs per batch.  Both
+return per frame the reference's ``analyze`` result (the big per-point arrays stay on
+the device).  Results are the drop-in path's, bit for bit (same kernels).
 """
 import ctypes
 import threading
@@ -117,3 +120,85 @@ class DensityStream:
             if isinstance(r, Exception):
                 raise r
         return out
+
+    # ------------------------------------------------------------------ batched mode
+    def run_batch(self, frames):
+        """frames: list of (n_i, 3) float64 CUDA tensors -> list of analyze results, one
+        launch per phase for the whole list.  Raises the reference's exception of the first
+        failing frame (ValueError empty, IndexError no inlier), like `run`."""
+        F = len(frames)
+        if F == 0:
+            return []
+        dev = self.device
+        sizes = [int(x.shape[0]) for x in frames]
+        offs_h = np.zeros(F + 1, dtype=np.int64)
+        offs_h[1:] = np.cumsum(sizes)
+        total, max_n = int(offs_h[-1]), max(1, max(sizes))
+        x = torch.cat([t.reshape(-1, 3) for t in frames]) if F > 1 else frames[0].reshape(-1, 3)
+        x = x.contiguous()
+        rows = max(1, total)
+        f64 = dict(dtype=torch.float64, device=dev)
+        offs = torch.from_numpy(offs_h).to(dev)
+        mask = torch.empty(rows, dtype=torch.uint8, device=dev)
+        colors, normals, comp = (torch.empty((rows, 3), **f64) for _ in range(3))
+        labels = torch.empty(rows, dtype=torch.int64, device=dev)
+        scal = torch.empty((F, 64), **f64)
+        h = nat.handle(self.device.index, slot=7)
+        sp = torch.cuda.current_stream(dev).cuda_stream
+        nat.call("lidar_preprocess_batch_f64", h, nat.ptr(x), nat.ptr(offs), F, max_n, nat.ptr(mask),
+                 nat.ptr(colors), nat.ptr(normals), nat.ptr(comp), nat.ptr(labels), nat.ptr(scal), sp)
+        people = torch.empty((rows, 2), **f64)
+        kdev = torch.empty(F, dtype=torch.int64, device=dev)
+        nat.call("lidar_people_batch_f64", h, nat.ptr(comp), nat.ptr(labels), nat.ptr(offs), F, max_n,
+                 nat.ptr(scal), nat.ptr(people), nat.ptr(kdev), sp)
+        S = scal.cpu().numpy()  # read-back 1 (also waits for people)
+        for f in range(F):
+            if S[f, 15] == 2.0:
+                raise ValueError("zero-size array to reduction operation minimum which has no identity")
+            if S[f, 15] != 0.0:
+                raise IndexError("index -1 is out of bounds for axis 0 with size 0")
+        K = kdev.cpu().numpy()  # read-back 2
+        jobs = np.zeros((F, 8), dtype=np.float64)
+        out_off = scr_off = 0
+        dims = []
+        for f in range(F):
+            if K[f] <= 0:
+                dims.append(None)
+                continue
+            x_min, x_max, y_min, y_max = S[f, 5], S[f, 6], S[f, 7], S[f, 8]
+            nx, ny = nat.I64(0), nat.I64(0)
+            nat.call("lidar_grid_dims", float(x_min), float(x_max), float(y_min), float(y_max), self.grid_size,
+                     ctypes.byref(nx), ctypes.byref(ny))
+            nx, ny = nx.value, ny.value
+            m = nx * ny
+            g2 = self.grid_size * 2.0
+            jobs[f] = (x_min - g2, y_min - g2, self.grid_size, nx, ny, out_off, scr_off, 0)
+            dims.append((nx, ny, out_off))
+            out_off += nx + ny + 3 * m + 13
+            scr_off += m + (m + 1) // 2 + nx + ny + 2
+        res = [None] * F
+        if out_off:
+            jd = torch.from_numpy(jobs).to(dev)
+            out = torch.empty(out_off, **f64)
+            nat.call("lidar_density_batch_f64", h, nat.ptr(people), nat.ptr(offs), nat.ptr(kdev), F, nat.ptr(jd),
+                     nat.ptr(out), scr_off, sp)
+            ob = out.cpu().numpy()  # read-back 3
+        for f in range(F):
+            if dims[f] is None:
+                res[f] = {"total_people": 0, "avg_density": 0.0, "max_density": 0.0,
+                          "density_map": np.zeros((1, 1)), "grid_coordinates": (np.array([0]), np.array([0])),
+                          "density_values": np.array([0]), "hotspots": []}
+                continue
+            nx, ny, o = dims[f]
+            m = nx * ny
+            b = ob[o:o + nx + ny + 3 * m + 13]
+            dens = b[nx + ny:nx + ny + m].reshape(nx, ny)
+            flat_x, flat_y = b[nx + ny + m:nx + ny + 2 * m], b[nx + ny + 2 * m:nx + ny + 3 * m]
+            stats = b[nx + ny + 3 * m:nx + ny + 3 * m + 8]
+            hot = b[nx + ny + 3 * m + 8:nx + ny + 3 * m + 13].view(np.int64)[: int(stats[3])]
+            flat = dens.flatten()
+            res[f] = {"total_people": int(K[f]), "avg_density": np.float64(stats[1]),
+                      "max_density": np.float64(stats[0]), "density_map": dens,
+                      "grid_coordinates": (flat_x, flat_y), "density_values": flat,
+                      "hotspots": [{"x": flat_x[i], "y": flat_y[i], "density": flat[i]} for i in hot]}
+        return res

@@ -130,3 +130,46 @@ def test_density_stream_matches_drop_in(cuda):
         assert np.array_equal(g["density_map"], want["density_map"]), name
         assert [(h["x"], h["y"], h["density"]) for h in g["hotspots"]] == \
                [(h["x"], h["y"], h["density"]) for h in want["hotspots"]], name
+
+
+def _same_analyze(name, g, want):
+    assert g["total_people"] == want["total_people"], name
+    assert float(g["avg_density"]).hex() == float(want["avg_density"]).hex(), name
+    assert float(g["max_density"]).hex() == float(want["max_density"]).hex(), name
+    assert type(g["avg_density"]) is type(want["avg_density"]), name
+    assert np.array_equal(g["density_map"], want["density_map"]), name
+    assert np.array_equal(g["grid_coordinates"][0], want["grid_coordinates"][0]), name
+    assert np.array_equal(g["density_values"], want["density_values"]), name
+    assert [(h["x"], h["y"], h["density"]) for h in g["hotspots"]] == \
+           [(h["x"], h["y"], h["density"]) for h in want["hotspots"]], name
+
+
+def test_density_batch_matches_drop_in(cuda):
+    """lidar_preprocess_batch_f64 / lidar_people_batch_f64 / lidar_density_batch_f64: one
+    launch per phase over a CSR batch of frames of different sizes (incl. a 12-point frame,
+    a frame with no cluster and int input) equals the per-frame drop-in, frame for frame."""
+    import torch
+    from lidar_ai_recommendation_software_amd.density_stream import DensityStream
+    names = ["uniform_16384_s0", "small_12", "crowd_16384_s7", "lattice_8163_s4", "small_20", "int_4096",
+             "uniform_65536_s0", "blobs_4293_s0", "dup_4096", "tight_2048"]
+    names = [k for k in names if k in FRAMES]
+    frames = [np.asarray(FRAMES[k](), dtype=np.float64) for k in names]
+    ds = DensityStream(cuda, workers=1)
+    got = ds.run_batch([torch.from_numpy(np.ascontiguousarray(f)).to(cuda) for f in frames])
+    model = CrowdDensityModel(1.0)
+    for name, f, g in zip(names, frames, got):
+        _same_analyze(name, g, model.analyze(dp.preprocess_lidar_data(f)))
+    # the same batch twice in a row (workspace reuse) gives the same
+    again = ds.run_batch([torch.from_numpy(np.ascontiguousarray(f)).to(cuda) for f in frames])
+    for name, a, b in zip(names, got, again):
+        _same_analyze(name, a, b)
+
+
+@pytest.mark.parametrize("bad,exc", [("empty", ValueError), ("const_col", IndexError), ("nan", IndexError)])
+def test_density_batch_errors(cuda, bad, exc):
+    import torch
+    from lidar_ai_recommendation_software_amd.density_stream import DensityStream
+    frames = [FRAMES["uniform_4096_s0"](), ERROR_FRAMES[bad](), FRAMES["uniform_4096_s1"]()]
+    with pytest.raises(exc):
+        DensityStream(cuda).run_batch([torch.from_numpy(np.ascontiguousarray(f, dtype=np.float64)).to(cuda)
+                                       for f in frames])

@@ -47,7 +47,7 @@ def main():
             print(f"ball_query B={B} N={N} M={N // 16} r0.2 ns32 (FPS centres): {ms:.3f} ms", flush=True)
 
 
-if __name__ == "__main__" and not ({"phases", "mlp", "tier_r", "dense"} & set(sys.argv)):
+if __name__ == "__main__" and not ({"phases", "mlp", "tier_r", "dense", "tier_r_batch"} & set(sys.argv)):
     main()
 
 
@@ -144,7 +144,7 @@ def tier_r_micro():
               f"(host in/out) {ms_all:.2f} ms; people {res['total_people']}", flush=True)
 
 
-if __name__ == "__main__" and "tier_r" in sys.argv:
+if __name__ == "__main__" and "tier_r" in sys.argv and "tier_r_batch" not in sys.argv:
     tier_r_micro()
 
 
@@ -169,3 +169,29 @@ def dense_micro():
 
 if __name__ == "__main__" and "dense" in sys.argv:
     dense_micro()
+
+
+def tier_r_batch_micro():
+    from lidar_ai_recommendation_software_amd.density_stream import DensityStream
+    from lidar_ai_recommendation_software_amd.synthetic import uniform_frame
+    dev = torch.device("cuda:0")
+    for F in (8, 32, 64):
+        xs = [torch.from_numpy(uniform_frame(65536, 1000 + i)).to(dev) for i in range(F)]
+        ds = DensityStream(dev, workers=4)
+        ds.run_batch(xs)
+        ds.run(xs)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(3):
+            ds.run_batch(xs)
+        tb = (time.perf_counter() - t0) / 3
+        t0 = time.perf_counter()
+        for _ in range(3):
+            ds.run(xs)
+        tw = (time.perf_counter() - t0) / 3
+        print(f"tier_r F={F} x 65536: batch {tb * 1e3:.1f} ms ({F * 65536 / tb / 1e6:.1f} M pts/s)  "
+              f"4 workers {tw * 1e3:.1f} ms ({F * 65536 / tw / 1e6:.1f} M pts/s)", flush=True)
+
+
+if __name__ == "__main__" and "tier_r_batch" in sys.argv:
+    tier_r_batch_micro()

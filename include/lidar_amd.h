@@ -165,6 +165,18 @@ int lidar_voxel_downsample_f32(lidar_handle *h, const float *xyz, int64_t n, flo
 int lidar_dbscan_f64(lidar_handle *h, const double *x, int64_t n, double eps, int32_t min_samples,
                      int64_t *labels, int32_t *counts, void *stream);
 
+/* KDTree(x).query_radius(x, r, count_only=True): counts[i] = #{j : ((dx*dx+dy*dy)+dz*dz)
+ * <= r*r} in fp64, i itself included (utils/visualization.py:41-48, :165-168;
+ * app_simplified.py:156-159).  x (n, 3) device; 2-D data with z = 0.  Synchronises. */
+int lidar_radius_count_f64(lidar_handle *h, const double *x, int64_t n, double r, int64_t *counts,
+                           void *stream);
+
+/* np.histogram2d(a, b, bins=(bx, by), range=...) counts (float64, bx*by row-major) with
+ * numpy's edges passed in (xedges bx+1, yedges by+1, device): searchsorted-right bins, the
+ * last edge closed, outside / NaN dropped (utils/visualization.py:125-137). */
+int lidar_histogram2d_f64(lidar_handle *h, const double *a, const double *b, int64_t n, const double *xedges,
+                          int64_t bx, const double *yedges, int64_t by, double *counts, void *stream);
+
 /* Whole preprocess_lidar_data (utils/data_processing.py:127-229) on one frame already in
  * device memory (n >= 1 points, (n,3) f64).  Outputs (device, caller-allocated with n rows):
  *   mask (n) u8 inlier flag; colors, normals, compact_xyz (n,3) f64 of the inliers in input

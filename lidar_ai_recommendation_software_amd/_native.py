@@ -62,6 +62,8 @@ SIGNATURES = {
     "lidar_concat_xyz_pad_f32": [P, P, I64, P, I64, I64, P],
     "lidar_voxel_downsample_f32": [P, P, I64, F32, P, P, P, P, P],
     "lidar_dbscan_f64": [P, P, I64, F64, I32, P, P, P],
+    "lidar_radius_count_f64": [P, P, I64, F64, P, P],
+    "lidar_histogram2d_f64": [P, P, P, I64, P, I64, P, I64, P, P],
     "lidar_preprocess_f64": [P, P, I64, P, P, P, P, P, P, P],
     "lidar_preprocess_batch_f64": [P, P, P, I32, I64, P, P, P, P, P, P, P],
     "lidar_people_batch_f64": [P, P, P, P, I32, I64, P, P, P, P],

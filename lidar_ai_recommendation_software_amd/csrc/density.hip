@@ -1278,7 +1278,7 @@ unsigned point_blocks(int64_t nmax, int frames)
 
 // the DBSCAN pipeline on x (P[P_N] points, eps P[P_EPS], bbox in P) -> labels, for every frame
 int run_dbscan(const double *x, int64_t nmax, int32_t min_samples, DbscanWs &w, int64_t *labels, hipStream_t s,
-               FrameMap fm, int frames)
+               FrameMap fm, int frames, bool count_only = false)
 {
     const unsigned gp = point_blocks(nmax, frames);
     const unsigned gc = point_blocks(w.max_cells, frames);
@@ -1291,6 +1291,10 @@ int run_dbscan(const double *x, int64_t nmax, int32_t min_samples, DbscanWs &w, 
     hipLaunchKernelGGL(copy_u32_kernel, FC, dim3(256), 0, s, w.fill, w.cellstart, w.P, P_NCELL, 1, fm);
     hipLaunchKernelGGL(dbscan_scatter_kernel, FP, dim3(256), 0, s, x, w.P, w.cid, w.fill, w.order, w.sxyz, fm);
     hipLaunchKernelGGL(dbscan_count_kernel, FP, dim3(256), 0, s, w.P, w.cid, w.cellstart, w.order, w.sxyz, w.cnt, fm);
+    if (count_only) {
+        LAUNCH_CHECK();
+        return LIDAR_OK;
+    }
     hipLaunchKernelGGL(dbscan_union_kernel, FP, dim3(256), 0, s, w.P, w.cid, w.cellstart, w.order, w.sxyz,
                        w.cnt, min_samples, w.parent, fm);
     hipLaunchKernelGGL(dbscan_roots_kernel, FP, dim3(256), 0, s, w.P, w.cnt, min_samples, w.parent, w.flag, fm);
@@ -1507,6 +1511,89 @@ LIDAR_EXPORT int lidar_density_batch_f64(lidar_handle *h, const double *people, 
     if (!scratch) return LIDAR_ENOMEM;
     hipLaunchKernelGGL(density_batch_kernel, dim3(1, frames), dim3(kT), 0, s, people, offsets, kdev, jobs, out,
                        scratch);
+    LAUNCH_CHECK();
+    return LIDAR_OK;
+}
+
+__global__ void widen_counts_kernel(const int32_t *c, int64_t n, int64_t *out)
+{
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = c[i];
+}
+
+// KDTree(x).query_radius(x, r, count_only=True) (the reference's density colouring,
+// utils/visualization.py:41-48 and :165-168, app_simplified.py:156-159): per point the
+// number of points (itself included) with ((dx*dx + dy*dy) + dz*dz) <= r*r in fp64 —
+// sklearn's rdist test, the one DBSCAN's neighbour count uses.  2-D data: z = 0.
+LIDAR_EXPORT int lidar_radius_count_f64(lidar_handle *h, const double *x, int64_t n, double r, int64_t *counts,
+                                        void *stream)
+{
+    REQUIRE(h && x && counts, "lidar_radius_count_f64: null pointer");
+    REQUIRE(n >= 0 && n < 0x7fffffff, "lidar_radius_count_f64: n out of range");
+    REQUIRE(r >= 0.0, "lidar_radius_count_f64: r must be >= 0");
+    if (n == 0) return LIDAR_OK;
+    HIP_TRY(hipSetDevice(h->device));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    lidar::Carver cv;
+    uint64_t off[12];
+    plan_dbscan(cv, n, off);
+    char *base = static_cast<char *>(lidar::workspace(h, cv.off));
+    if (!base) return LIDAR_ENOMEM;
+    DbscanWs w = bind_dbscan(base, off, n);
+    double *hp = static_cast<double *>(h->host_pinned);
+    for (int i = 0; i < P_COUNT; ++i) hp[i] = 0.0;
+    hp[P_N] = (double)n;
+    // r = 0: a tiny positive cell size keeps the grid finite; only exact duplicates count
+    hp[P_EPS] = r > 0.0 ? r : 1e-300;
+    hp[P_ACTIVE] = 1.0;
+    HIP_TRY(hipMemcpyAsync(w.P, hp, sizeof(double) * P_COUNT, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(dbscan_bbox_kernel, dim3(1), dim3(kT), 0, s, x, w.P, FrameMap{});
+    int rc = run_dbscan(x, n, 1, w, nullptr, s, FrameMap{}, 1, true);
+    if (rc) return rc;
+    hipLaunchKernelGGL(widen_counts_kernel, dim3(point_blocks(n, 1)), dim3(256), 0, s, w.cnt, n, counts);
+    LAUNCH_CHECK();
+    HIP_TRY(hipStreamSynchronize(s));  // the pinned parameter block is reused by the next call
+    return LIDAR_OK;
+}
+
+// np.histogram2d(a, b, bins=(bx, by), range=...) binning (the reference's heatmaps,
+// utils/visualization.py:125-137, app_simplified.py:205-209): the edges are numpy's own
+// (np.linspace, passed in); a value lands in bin searchsorted(edges, v, 'right') - 1, a value
+// equal to the last edge in the last bin, anything outside (or NaN) nowhere.  counts is
+// bx * by float64 (row-major, a-bins x b-bins), zeroed here.
+__global__ void hist2d_kernel(const double *a, const double *b, int64_t n, const double *xe, int64_t bx,
+                              const double *ye, int64_t by, unsigned long long *cnt)
+{
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const double va = a[i], vb = b[i];
+        int64_t ia = searchsorted_right(xe, bx + 1, va), ib = searchsorted_right(ye, by + 1, vb);
+        if (va == xe[bx]) --ia;
+        if (vb == ye[by]) --ib;
+        if (ia >= 1 && ia <= bx && ib >= 1 && ib <= by) atomicAdd(&cnt[(ia - 1) * by + (ib - 1)], 1ull);
+    }
+}
+__global__ void hist2d_finish_kernel(const unsigned long long *cnt, int64_t m, double *out)
+{
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = (double)cnt[i];
+}
+
+LIDAR_EXPORT int lidar_histogram2d_f64(lidar_handle *h, const double *a, const double *b, int64_t n,
+                                       const double *xedges, int64_t bx, const double *yedges, int64_t by,
+                                       double *counts, void *stream)
+{
+    REQUIRE(h && xedges && yedges && counts && (n == 0 || (a && b)), "lidar_histogram2d_f64: null pointer");
+    REQUIRE(n >= 0 && bx >= 1 && by >= 1, "lidar_histogram2d_f64: bad sizes");
+    HIP_TRY(hipSetDevice(h->device));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int64_t m = bx * by;
+    auto *cnt = static_cast<unsigned long long *>(lidar::workspace(h, (uint64_t)m * 8));
+    if (!cnt) return LIDAR_ENOMEM;
+    HIP_TRY(hipMemsetAsync(cnt, 0, (size_t)m * 8, s));
+    if (n > 0)
+        hipLaunchKernelGGL(hist2d_kernel, dim3(point_blocks(n, 1)), dim3(256), 0, s, a, b, n, xedges, bx, yedges, by,
+                           cnt);
+    hipLaunchKernelGGL(hist2d_finish_kernel, dim3(point_blocks(m, 1)), dim3(256), 0, s, cnt, m, counts);
     LAUNCH_CHECK();
     return LIDAR_OK;
 }

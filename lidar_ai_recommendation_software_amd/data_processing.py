@@ -268,3 +268,56 @@ def farthest_point_sample(points, npoint):
     from .pointnet2 import farthest_point_sample as fps
     x = _on_device(np.asarray(points, dtype=np.float32).reshape(-1, 3), torch.float32)
     return fps(x[None], int(npoint))[0].cpu().numpy()
+
+
+def radius_count(points, r=0.5):
+    """``KDTree(points).query_radius(points, r=r, count_only=True)`` on the GPU: per point the
+    number of points within r, itself included (the reference's density colouring,
+    ``utils/visualization.py:41-48`` / ``:165-168``, ``app_simplified.py:156-159``; 2-D
+    projections are passed as (n, 2)).  Exact: sklearn's fp64 rdist test
+    ((dx*dx + dy*dy) + dz*dz <= r*r), shared with DBSCAN's neighbour count."""
+    import torch
+    p = np.asarray(points, dtype=np.float64)
+    if p.ndim != 2 or p.shape[1] not in (2, 3):
+        raise ValueError("radius_count expects (n, 2) or (n, 3) points")
+    n = len(p)
+    if n == 0:
+        return np.zeros(0, dtype=np.intp)
+    if p.shape[1] == 2:
+        p = np.column_stack([p, np.zeros(n)])
+    x = torch.from_numpy(np.ascontiguousarray(p)).cuda()
+    out = torch.empty(n, dtype=torch.int64, device=x.device)
+    nat.call("lidar_radius_count_f64", _handle(), nat.ptr(x), n, float(r), nat.ptr(out), nat.stream_ptr())
+    return out.cpu().numpy().astype(np.intp)
+
+
+def histogram2d(x, y, bins=10, range=None):
+    """``np.histogram2d(x, y, bins=bins, range=range)`` with the counting on the GPU — the
+    reference's projection heatmaps (``utils/visualization.py:125-137``,
+    ``app_simplified.py:205-209``).  The edges are numpy's own (``np.linspace`` for an int
+    bin count, or the given edge arrays); returns (H, xedges, yedges) like numpy."""
+    import torch
+    x = np.asarray(x, dtype=np.float64).ravel()
+    y = np.asarray(y, dtype=np.float64).ravel()
+    if len(x) != len(y):
+        raise ValueError("x and y must have the same length")
+    bxy = bins if isinstance(bins, (list, tuple)) and len(bins) == 2 else (bins, bins)
+    rng = range if range is not None else [None, None]
+    edges = []
+    for v, b, r in zip((x, y), bxy, rng):
+        if np.ndim(b) == 1:
+            e = np.asarray(b, dtype=np.float64)
+        else:
+            lo, hi = (r if r is not None else ((v.min(), v.max()) if len(v) else (0.0, 1.0)))
+            if lo == hi:  # numpy widens a degenerate range by 0.5 on both sides
+                lo, hi = lo - 0.5, hi + 0.5
+            e = np.linspace(lo, hi, int(b) + 1)
+        edges.append(e)
+    xe, ye = edges
+    dev = torch.device("cuda", torch.cuda.current_device())
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    dx, dy, dxe, dye = T(x), T(y), T(xe), T(ye)
+    H = torch.empty((len(xe) - 1, len(ye) - 1), dtype=torch.float64, device=dev)
+    nat.call("lidar_histogram2d_f64", _handle(), nat.ptr(dx), nat.ptr(dy), len(x), nat.ptr(dxe), len(xe) - 1,
+             nat.ptr(dye), len(ye) - 1, nat.ptr(H), nat.stream_ptr())
+    return H.cpu().numpy(), xe, ye

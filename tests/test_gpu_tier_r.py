@@ -173,3 +173,34 @@ def test_density_batch_errors(cuda, bad, exc):
     with pytest.raises(exc):
         DensityStream(cuda).run_batch([torch.from_numpy(np.ascontiguousarray(f, dtype=np.float64)).to(cuda)
                                        for f in frames])
+
+
+@pytest.mark.parametrize("kind,n,r,dim", [("uniform", 20000, 0.5, 3), ("crowd", 16384, 0.5, 3), ("uniform", 20000, 0.5, 2),
+                                          ("dups", 4096, 0.5, 3), ("uniform", 3000, 2.0, 3), ("uniform", 1, 0.5, 3)])
+def test_radius_count_matches_sklearn_kdtree(cuda, kind, n, r, dim):
+    """The reference's density colouring: KDTree(points).query_radius(points, r, count_only=True)
+    (sklearn is in this image; the call and its arguments are the reference's)."""
+    from sklearn.neighbors import KDTree
+    from lidar_ai_recommendation_software_amd.synthetic import crowd_frame
+    if kind == "crowd":
+        pts = crowd_frame(n, 3)
+    elif kind == "dups":
+        pts = np.repeat(uniform_frame(n // 4, 4), 4, axis=0)
+    else:
+        pts = uniform_frame(n, 6)
+    pts = np.ascontiguousarray(pts[:, :dim], dtype=np.float64)
+    want = KDTree(pts).query_radius(pts, r=r, count_only=True)
+    got = dp.radius_count(pts, r)
+    assert got.dtype == want.dtype and np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("n,bins,rng", [(20000, 50, [(-15, 15), (-15, 15)]), (5000, 17, [(-3.2, 11.7), (-15, 0)]),
+                                        (1000, 50, None), (0, 5, [(0, 1), (0, 1)])])
+def test_histogram2d_matches_numpy(cuda, n, bins, rng):
+    """The reference's projection heatmap: np.histogram2d(d1, d2, bins=resolution, range=[...])."""
+    pts = uniform_frame(max(n, 1), 8)[:n]
+    pts[: n // 10, 0] = 11.7  # values on an edge
+    want = np.histogram2d(pts[:, 0], pts[:, 1], bins=bins, range=rng)
+    got = dp.histogram2d(pts[:, 0], pts[:, 1], bins=bins, range=rng)
+    for g, w in zip(got, want):
+        assert g.dtype == w.dtype and np.array_equal(g, w)

@@ -36,6 +36,7 @@ extern "C" {
 #define LIDAR_EHIP -2     /* a HIP runtime call failed */
 #define LIDAR_ENOMEM -3   /* workspace allocation failed */
 #define LIDAR_EDEVICE -4  /* device is not gfx950 */
+#define LIDAR_EPARSE -5   /* a text token the C parser does not reproduce exactly (caller falls back) */
 
 typedef struct lidar_handle lidar_handle;
 
@@ -176,6 +177,14 @@ int lidar_radius_count_f64(lidar_handle *h, const double *x, int64_t n, double r
  * last edge closed, outside / NaN dropped (utils/visualization.py:125-137). */
 int lidar_histogram2d_f64(lidar_handle *h, const double *a, const double *b, int64_t n, const double *xedges,
                           int64_t bx, const double *yedges, int64_t by, double *counts, void *stream);
+
+/* Host-only: the PCD / PLY ASCII data section of load_lidar_data (utils/data_processing.py
+ * :43-104).  From 0-based line `first` (max_lines < 0: to the end; else that many lines),
+ * every line with >= 3 whitespace-separated tokens yields float(tok0..2) into out (3 per
+ * point, cap points); *n_out = points written.  LIDAR_EPARSE: some token needs Python's own
+ * float() (the caller falls back to the reference's loop for the exact result / error). */
+int lidar_parse_ascii_xyz(const char *buf, int64_t len, int64_t first, int64_t max_lines, double *out,
+                          int64_t cap, int64_t *n_out);
 
 /* Whole preprocess_lidar_data (utils/data_processing.py:127-229) on one frame already in
  * device memory (n >= 1 points, (n,3) f64).  Outputs (device, caller-allocated with n rows):

@@ -17,7 +17,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LIDAR_AMD_LIB") or os.path.join(_HERE, "liblidar_amd.so")
 
 LIDAR_ERRORS = {-1: "invalid argument", -2: "HIP runtime error", -3: "out of memory",
-                -4: "unsupported device"}
+                -4: "unsupported device", -5: "needs the Python parser"}
 
 
 class NativeUnavailable(RuntimeError):
@@ -64,6 +64,7 @@ SIGNATURES = {
     "lidar_dbscan_f64": [P, P, I64, F64, I32, P, P, P],
     "lidar_radius_count_f64": [P, P, I64, F64, P, P],
     "lidar_histogram2d_f64": [P, P, P, I64, P, I64, P, I64, P, P],
+    "lidar_parse_ascii_xyz": [P, I64, I64, I64, P, I64, P],
     "lidar_preprocess_f64": [P, P, I64, P, P, P, P, P, P, P],
     "lidar_preprocess_batch_f64": [P, P, P, I32, I64, P, P, P, P, P, P, P],
     "lidar_people_batch_f64": [P, P, P, P, I32, I64, P, P, P, P],

@@ -101,8 +101,18 @@ def _ply_body(lines):
 
 
 def _read_ascii_body(path, locate):
-    with open(path, "r") as f:
-        lines = f.readlines()
+    with open(path, "rb") as f:
+        raw = f.read()
+    pts = _parse_fast(raw, locate)
+    if pts is not None:
+        return pts
+    return _read_ascii_body_py(raw.decode(), locate)
+
+
+def _read_ascii_body_py(text, locate):
+    """The reference's loop (data_processing.py:74-80 / :98-104) on text-mode lines."""
+    import io
+    lines = io.StringIO(text, newline=None).readlines()
     a, b = locate(lines)
     rows = []
     for ln in lines[a:min(b, len(lines))]:
@@ -110,6 +120,43 @@ def _read_ascii_body(path, locate):
         if len(vals) >= 3:
             rows.append([float(v) for v in vals[:3]])
     return np.array(rows)
+
+
+_SLOW_BYTES = re.compile(rb"[\x80-\xff\x0b\x0c\x1c-\x1f]|\r(?!\n)")
+
+
+def _parse_fast(raw, locate):
+    """The data section parsed by liblidar_amd's C parser (lidar_parse_ascii_xyz), or None
+    when the input needs Python's own text rules (non-ASCII / exotic whitespace, bare CR
+    line breaks, a header beyond the first 64 KiB, or a token only float() parses)."""
+    if _SLOW_BYTES.search(raw, 0, 65536):  # the data section is checked by the C scanner
+        return None
+    head = raw[:65536].decode("ascii")
+    lines = head.splitlines(keepends=True)
+    if len(raw) > 65536:
+        lines = lines[:-1]  # the last head line may be cut
+    a, b = locate(lines)
+    if a == 0 and (not lines or b >= len(lines)):
+        # no data section located inside the head: let the Python path decide
+        return None
+    import ctypes
+    lib = nat.load_library()
+    cap = raw.count(b"\n") + 1
+    out = np.empty((cap, 3), dtype=np.float64)
+    n = ctypes.c_int64(0)
+    max_lines = -1
+    if locate is _ply_body:  # the vertex count bounds the data lines; none: to the end
+        nvert = None
+        for ln in lines[:a]:
+            if "element vertex" in ln:
+                nvert = int(ln.split()[-1])
+        max_lines = -1 if nvert is None else max(0, nvert)
+    rc = lib.lidar_parse_ascii_xyz(raw, len(raw), a, max_lines, out.ctypes.data_as(ctypes.c_void_p), cap,
+                                   ctypes.byref(n))
+    if rc != 0:
+        return None
+    n = n.value
+    return np.array(out[:n]) if n else np.array([])
 
 
 # ---------------------------------------------------------------- preprocess (L2)

@@ -164,6 +164,8 @@ def main():
     ap.add_argument("--fps-group", type=int, default=2, help="batches per SA1-FPS launch (StreamingSSG fps_group)")
     ap.add_argument("--side-cus", type=int, default=0, help="CUs reserved for the SA1 FPS streams (0 = shared)")
     ap.add_argument("--cu-layout", default="xcd", choices=["xcd", "low"])
+    ap.add_argument("--mlp16", default="pre", choices=["0", "1", "pre", "xyz"],
+                    help="SA branches on the 16-row MFMA kernels: 1 all, pre / xyz only those levels")
     ap.add_argument("--no-extras", action="store_true", help="skip the configs[1]/[4] side measurements")
     ap.add_argument("--no-density", action="store_true", help="skip the Tier R density-path leg")
     args = ap.parse_args()
@@ -188,7 +190,7 @@ def main():
         headline: the roofline durations come from the same window).  False: the window
         runs clean and the per-kernel durations come from a second, instrumented window
         of the same length (with ~25 launches per step, as MSG has, the events cost ~1/3)."""
-        bb = pn.PointNet2Backbone(cfg, device=dev, seed=0, dtype=dtype)
+        bb = pn.PointNet2Backbone(cfg, device=dev, seed=0, dtype=dtype, mlp16={"0": False, "1": True}.get(args.mlp16, args.mlp16))
         x = torch.from_numpy(unit_frames(B, N, seed=sharding.frame_seed(rank))).to(dev)
         # the streaming executor overlaps batch k+1's SA1 FPS + ball queries (latency-bound,
         # one workgroup per frame) with batch k's MFMA levels; results are identical to forward()

@@ -145,6 +145,23 @@ int lidar_sa_group_mlp_pre_f32(lidar_handle *h, const float *p, int64_t p_stride
                                const float *packed, float *out, int64_t out_stride,
                                int64_t out_offset, void *stream);
 
+/* 16-row variants of the fused SetAbstraction branch (v_mfma_f32_16x16x4_f32, ~half the
+ * registers of the 32-row kernels, so more waves per SIMD beside co-resident FPS work).
+ * xyz_level != 0: p = xyz (batch*n, 3), q = centres (batch*m, 3), layer 1 runs in-kernel
+ * (replaces the cfeat = 0 case of lidar_sa_group_mlp_f32); xyz_level = 0: p / q are the
+ * per-point / per-centre layer-1 rows of lidar_sa_group_mlp_pre_f32 (row stride p_stride).
+ * packed: the lidar_mlp_pack16_f32 image of lidar_mlp_packed_size16 floats (w1 is read only
+ * for an xyz level: its 3 xyz rows).  Same outputs up to fp32 re-association. */
+int64_t lidar_mlp_packed_size16(int32_t xyz_level, int32_t c1, int32_t c2, int32_t c3);
+int lidar_mlp_pack16_f32(int32_t xyz_level, int32_t c1, int32_t c2, int32_t c3, const float *w1_host,
+                         const float *b1_host, const float *w2_host, const float *b2_host,
+                         const float *w3_host, const float *b3_host, float *packed_host);
+int lidar_sa_group_mlp16_f32(lidar_handle *h, int32_t xyz_level, const float *p, int64_t p_stride,
+                             const float *q, const int32_t *idx, int64_t batch, int64_t n,
+                             int64_t m, int32_t nsample, int32_t c1, int32_t c2, int32_t c3,
+                             const float *packed, float *out, int64_t out_stride,
+                             int64_t out_offset, void *stream);
+
 /* y (batch*m, ldy) columns [col0, col0+3) = xyz rows; columns [col0+3, ldy) zeroed —
  * builds group_all's input [feats, xyz, 0-pad] next to features already in y. */
 int lidar_concat_xyz_pad_f32(lidar_handle *h, const float *xyz, int64_t rows, float *y,

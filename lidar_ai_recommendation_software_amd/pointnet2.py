@@ -148,6 +148,43 @@ def pack_branch_bf16(layers, cfeat):
     return out
 
 
+# (xyz_level, c1, c2, c3, nsample) combinations lidar_sa_group_mlp16_f32 instantiates
+MLP16_SHAPES = {(True, 64, 64, 128, 32), (True, 32, 32, 64, 16), (True, 64, 96, 128, 128), (False, 128, 128, 256, 64),
+                (False, 128, 128, 256, 128), (False, 64, 64, 128, 32)}
+
+
+def pack_branch16(layers, xyz_level):
+    """Host-side packed image for lidar_sa_group_mlp16_f32 (16x16x4 MFMA fragments)."""
+    (w1, b1), (w2, b2), (w3, b3) = layers
+    c1, c2, c3 = w1.shape[1], w2.shape[1], w3.shape[1]
+    lib = nat.load_library()
+    out = np.zeros(lib.lidar_mlp_packed_size16(int(xyz_level), c1, c2, c3), dtype=np.float32)
+    arrs = [np.ascontiguousarray(a, dtype=np.float32) for a in (w1, b1, w2, b2, w3, b3)]
+    nat.check(lib.lidar_mlp_pack16_f32(int(xyz_level), c1, c2, c3, *[a.ctypes.data_as(ctypes.c_void_p) for a in arrs],
+                                       out.ctypes.data_as(ctypes.c_void_p)), "lidar_mlp_pack16_f32")
+    return out
+
+
+def group_mlp16(p, q, idx, n, packed, widths, out, out_offset=0, xyz_level=False):
+    """16-row fused branch.  xyz_level: p = xyz (B, N, 3), q = centres (B, M, 3); else
+    p / q are group_mlp_pre's per-point / per-centre layer-1 rows.  -> out[..., off:off+c3]."""
+    B, M, ns = idx.shape
+    c1, c2, c3 = widths
+    if xyz_level:
+        if p.numel() < B * n * 3 or q.numel() < B * M * 3 or not (p.is_contiguous() and q.is_contiguous()):
+            raise ValueError("group_mlp16: xyz / centres must be contiguous (B, N, 3) / (B, M, 3)")
+        stride = 3
+    else:
+        if p.shape[0] < B * n or q.shape[0] < B * M or p.shape[1] < c1 or q.shape[1] != p.shape[1]:
+            raise ValueError("group_mlp16: p/q shapes do not match the batch")
+        stride = p.shape[1]
+    _dev_check(p, q, idx, packed, out)
+    nat.call("lidar_sa_group_mlp16_f32", nat.handle(p.device.index), int(xyz_level), nat.ptr(p), stride,
+             nat.ptr(q), nat.ptr(idx), B, n, M, ns, c1, c2, c3, nat.ptr(packed), nat.ptr(out), out.shape[-1],
+             out_offset, nat.stream_ptr())
+    return out
+
+
 def group_mlp(xyz, feats, new_xyz, idx, packed, widths, out=None, out_offset=0, bf16=False):
     """Fused grouping + 3-layer MLP + max over nsample -> (B, M, c3) (or into `out`)."""
     B, N, _ = xyz.shape
@@ -279,11 +316,14 @@ class PointNet2Backbone:
     """SSG / MSG PointNet++ encoder on liblidar_amd.  ``forward(xyz)`` -> global feature
     (B, C_last) plus the per-level (new_xyz, features, fps_idx)."""
 
-    def __init__(self, cfg=SSG, weights=None, device="cuda", seed=0, dtype="f32", pre_layer1=True):
+    def __init__(self, cfg=SSG, weights=None, device="cuda", seed=0, dtype="f32", pre_layer1=True, mlp16="pre"):
         """dtype "bf16": the SA branches run on bf16 MFMA (inputs/activations/weights rounded
         to bf16, fp32 accumulation; BASELINE configs[4]); group_all stays fp32.
         pre_layer1 (fp32, levels with point features): layer 1 runs per point as a GEMM
-        and the fused kernel starts at layer 2 (layer1_per_point / group_mlp_pre)."""
+        and the fused kernel starts at layer 2 (layer1_per_point / group_mlp_pre).
+        mlp16 (fp32): branches whose shape lidar_sa_group_mlp16_f32 instantiates run on the
+        16-row kernels (MLP16_SHAPES); "pre" / "xyz": only the per-point-layer-1 / the
+        xyz-only levels."""
         if dtype not in ("f32", "bf16"):
             raise ValueError("dtype must be 'f32' or 'bf16'")
         self.bf16 = dtype == "bf16"
@@ -313,6 +353,11 @@ class PointNet2Backbone:
                     pk = pack_branch_bf16(layers, cfeat) if self.bf16 else pack_branch(layers, cfeat)
                     packed = torch.from_numpy(pk).to(self.device)
                     br = {"r": r, "ns": ns, "widths": widths, "packed": packed}
+                    xyz_level = cfeat == 0
+                    use16 = mlp16 is True or (mlp16 == "pre" and pre) or (mlp16 == "xyz" and xyz_level)
+                    if (use16 and not self.bf16 and (pre or xyz_level)
+                            and (xyz_level, *widths, ns) in MLP16_SHAPES):
+                        br["packed16"] = torch.from_numpy(pack_branch16(layers, xyz_level)).to(self.device)
                     if pre:
                         br["pre"] = layer1_weights(layers[0], cfeat, t)
                     branches.append(br)
@@ -366,7 +411,11 @@ class PointNet2Backbone:
                     gidx = pre_bq[bi_]
                 else:
                     gidx = _call(self.timers, f"{tag}_ball_query", ball_query, br["r"], br["ns"], xyz, new_xyz)
-                if pq is not None:
+                if "packed16" in br:
+                    p16, q16 = (pq[bi_] if pq is not None else (xyz, new_xyz))
+                    _call(self.timers, f"{tag}_group_mlp", group_mlp16, p16, q16, gidx, N, br["packed16"],
+                          br["widths"], out=out, out_offset=off, xyz_level=pq is None)
+                elif pq is not None:
                     _call(self.timers, f"{tag}_group_mlp", group_mlp_pre, pq[bi_][0], pq[bi_][1], gidx, N,
                           br["packed"], lvl["cfeat"], br["widths"], out=out, out_offset=off)
                 else:

@@ -131,6 +131,43 @@ def test_group_mlp_layer1_per_point(cuda, cfg_name, level, branch):
     feat_close(Pn, np.concatenate([x.reshape(-1, 3), f.reshape(-1, cfeat)], 1) @ w1 + b1, "P rows")
 
 
+@pytest.mark.parametrize("cfg_name,level,branch", [("ssg", 0, 0), ("msg", 0, 0), ("msg", 0, 1), ("msg", 0, 2),
+                                                   ("ssg", 1, 0), ("msg", 1, 0), ("msg", 1, 1), ("msg", 1, 2)])
+def test_group_mlp16(cuda, cfg_name, level, branch):
+    """16-row kernels (16x16x4 MFMA): xyz levels take (xyz, centres), feature levels the
+    per-point layer-1 rows; same grouped rows as the oracle, 1e-4."""
+    cfg = pn.CONFIGS[cfg_name]
+    w = pn.init_weights(cfg, seed=5)
+    lvl = cfg["levels"][level]
+    layers = w[level][branch]
+    cfeat = layers[0][0].shape[0] - 3
+    r, ns, widths = lvl["radii"][branch], lvl["nsamples"][branch], lvl["mlps"][branch]
+    B, N, M = 2, 2000, 101  # B*M odd: the last workgroup has idle waves
+    rng = np.random.default_rng(9)
+    x = unit_frames(B, N, 12)
+    f = np.abs(rng.standard_normal((B, N, cfeat))).astype(np.float32) if cfeat else None
+    c = x[:, :M].copy()
+    gi = tier_n.ball_query(x, c, r, ns)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).to(cuda)
+    packed = T(pn.pack_branch16(layers, cfeat == 0))
+    off, stride = 5, widths[-1] + 9  # strided output columns
+    out = torch.full((B, M, stride), -7.0, dtype=torch.float32, device=cuda)
+    gti = torch.from_numpy(gi).to(cuda)
+    if cfeat == 0:
+        pn.group_mlp16(T(x), T(c), gti, N, packed, widths, out, off, xyz_level=True)
+    else:
+        kp = (cfeat + 3 + 15) // 16 * 16
+        rows = torch.zeros(((B * N + 127) // 128 * 128, kp), dtype=torch.float32, device=cuda)
+        rows[:B * N, :cfeat] = T(f.reshape(-1, cfeat))
+        (P, Q), = pn.layer1_per_point(rows, T(x), cfeat, T(c), [{"pre": pn.layer1_weights(layers[0], cfeat, T)}])
+        pn.group_mlp16(P, Q, gti, N, packed, widths, out, off)
+    got = out.cpu().numpy()
+    assert (got[..., :off] == -7.0).all() and (got[..., off + widths[-1]:] == -7.0).all(), "wrote outside its columns"
+    for bi in range(B):
+        want = tier_n.mlp_maxpool(tier_n.group(x[bi], None if f is None else f[bi], c[bi], gi[bi]), layers, ns)
+        feat_close(got[bi, :, off:off + widths[-1]], want, f"{cfg_name} L{level} br{branch} frame {bi} (16-row)")
+
+
 def test_dense_no_relu(cuda):
     rng = np.random.default_rng(2)
     x = rng.standard_normal((256, 144)).astype(np.float32)
@@ -153,12 +190,13 @@ def test_dense_relu_and_pool(cuda):
     feat_close(pooled, want.reshape(2, 256, 256).max(axis=1), "dense pooled")
 
 
-@pytest.mark.parametrize("cfg_name,n,pre", [("ssg", 16384, True), ("ssg", 65536, True), ("sa1", 16384, True),
-                                            ("msg", 16384, True), ("ssg", 16384, False), ("msg", 16384, False),
-                                            ("ssg", 5000, True)])
-def test_backbone_vs_oracle(cuda, cfg_name, n, pre):
+@pytest.mark.parametrize("cfg_name,n,pre,mlp16", [
+    ("ssg", 16384, True, False), ("ssg", 65536, True, False), ("sa1", 16384, True, False),
+    ("msg", 16384, True, False), ("ssg", 16384, False, False), ("msg", 16384, False, False),
+    ("ssg", 5000, True, False), ("ssg", 65536, True, True), ("msg", 16384, True, True), ("sa1", 16384, True, True)])
+def test_backbone_vs_oracle(cuda, cfg_name, n, pre, mlp16):
     cfg = pn.CONFIGS[cfg_name]
-    bb = pn.PointNet2Backbone(cfg, device=cuda, seed=0, pre_layer1=pre)
+    bb = pn.PointNet2Backbone(cfg, device=cuda, seed=0, pre_layer1=pre, mlp16=mlp16)
     x = unit_frames(1, n, 21)
     g, levels = bb.forward(torch.from_numpy(x).to(cuda), keep_levels=True)
     torch.cuda.synchronize()
@@ -218,6 +256,15 @@ def test_streaming_grouped_fps_matches_forward(cuda, cfg_name, dtype, group, dep
     for a, b in zip(got, want):
         assert torch.equal(a, b)
 
+
+def test_streaming_mlp16_matches_forward(cuda):
+    bb = pn.PointNet2Backbone(pn.SSG, device=cuda, seed=3, mlp16=True)
+    xs = [torch.from_numpy(unit_frames(2, 8192, 30 + s)).to(cuda) for s in range(5)]
+    want = [bb.forward(x)[0] for x in xs]
+    got = pn.StreamingSSG(bb, 2, 8192, depth=2, fps_group=2).run(xs)
+    torch.cuda.synchronize()
+    for a, b in zip(got, want):
+        assert torch.equal(a, b)
 
 
 def bf16_close(got, want, what=""):

@@ -99,6 +99,10 @@ def mlp_micro():
         flops = 2 * B * M * ns * sum(a * b for a, b in zip(dims[:-1], dims[1:]))
         print(f"{name} group_mlp: {ms:.3f} ms  {flops / ms / 1e9:.1f} TFLOP/s ({flops / ms / 1e9 / 157.3 * 100:.1f}% of fp32 peak)",
               flush=True)
+        pk16 = torch.from_numpy(pn.pack_branch16(layers, cf == 0)).to(dev)
+        if cf == 0:
+            ms = timeit(lambda: pn.group_mlp16(x, c, gi, N, pk16, widths, out, xyz_level=True), reps=10)
+            print(f"{name} group_mlp16: {ms:.3f} ms  {flops / ms / 1e9:.1f} TFLOP/s", flush=True)
         if cf:
             P = torch.from_numpy(rng.standard_normal((B * N, widths[0])).astype(np.float32)).to(dev)
             Q = torch.from_numpy(rng.standard_normal((B * M, widths[0])).astype(np.float32)).to(dev)
@@ -106,6 +110,8 @@ def mlp_micro():
             flops = 2 * B * M * ns * sum(a * b for a, b in zip(widths[:-1], widths[1:]))
             print(f"{name} group_mlp_pre (layers 2-3): {ms:.3f} ms  {flops / ms / 1e9:.1f} TFLOP/s "
                   f"({flops / ms / 1e9 / 157.3 * 100:.1f}% of fp32 peak)", flush=True)
+            ms = timeit(lambda: pn.group_mlp16(P, Q, gi, N, pk16, widths, out), reps=10)
+            print(f"{name} group_mlp16 (layers 2-3): {ms:.3f} ms  {flops / ms / 1e9:.1f} TFLOP/s", flush=True)
 
 
 if __name__ == "__main__" and "mlp" in sys.argv:

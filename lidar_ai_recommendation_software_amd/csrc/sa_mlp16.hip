@@ -42,8 +42,8 @@ struct Pack16 {
     static constexpr int64_t W1 = (int64_t)T1 * 64;             // floats
 };
 
-template <int C1, int C2, int C3, int NS, bool XYZ>
-__global__ __launch_bounds__(256, 3) void sa16_kernel(const float *__restrict__ P, int64_t stride,
+template <int C1, int C2, int C3, int NS, bool XYZ, int WPG>
+__global__ __launch_bounds__(64 * WPG, 4) void sa16_kernel(const float *__restrict__ P, int64_t stride,
                                                    const float *__restrict__ Q, const int32_t *__restrict__ idx,
                                                    int n, int m, int64_t total, const float *__restrict__ packed,
                                                    float *__restrict__ out, int64_t out_stride, int64_t out_offset)
@@ -54,17 +54,19 @@ __global__ __launch_bounds__(256, 3) void sa16_kernel(const float *__restrict__ 
     constexpr int CH2 = K::CH2, CH3 = K::CH3, CHMAX = CH2 > CH3 ? CH2 : CH3;
     constexpr int NCH = T2 / 2 + T3 / 2;  // chunks per row tile
     constexpr int TILES = NS / 16;
-    constexpr int PER = (CHMAX + 255) / 256;
-    static_assert(CH2 % 256 == 0 && CH3 % 256 == 0, "chunks split evenly over 256 threads");
+    constexpr int NT = 64 * WPG;  // threads per workgroup: WPG waves share every weight chunk
+    constexpr int PER = (CHMAX + NT - 1) / NT;
+    static_assert(CH2 % 64 == 0 && CH3 % 64 == 0, "chunks copied in 64-float4 slabs, one per wave");
     static_assert(T2 % 2 == 0 && T3 % 2 == 0, "output tiles come in pairs");
 
     __shared__ f32x4 buf[2][CHMAX];
     __shared__ float bias_s[C1 + C2 + C3];
     __shared__ float w1_s[XYZ ? T1 * 64 : 1];
+    __shared__ float mx_s[WPG][C3];  // running max-pool per wave: kept out of the registers
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int q = lane >> 4, col = lane & 15;
-    const int64_t unit = (int64_t)blockIdx.x * 4 + wave;
+    const int64_t unit = (int64_t)blockIdx.x * WPG + wave;
     const bool live = unit < total;  // every wave takes part in the barriers
     const int64_t cc = live ? unit : total - 1;
     const int64_t b = cc / m;
@@ -82,7 +84,7 @@ __global__ __launch_bounds__(256, 3) void sa16_kernel(const float *__restrict__ 
         const int len = chunk_len(c);
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
-            const int base = 256 * i + 64 * wave;
+            const int base = NT * i + 64 * wave;
             if (base < len)
                 __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)(src + base + lane),
                                                  (__attribute__((address_space(3))) void *)(&buf[dst][base]), 16, 0,
@@ -90,14 +92,12 @@ __global__ __launch_bounds__(256, 3) void sa16_kernel(const float *__restrict__ 
         }
     };
     fetch(0, 0);
-    for (int i = tid; i < C1 + C2 + C3; i += 256) bias_s[i] = Bias[i];
+    for (int i = tid; i < C1 + C2 + C3; i += NT) bias_s[i] = Bias[i];
     if constexpr (XYZ)
-        for (int i = tid; i < T1 * 64; i += 256) w1_s[i] = W1[i];
+        for (int i = tid; i < T1 * 64; i += NT) w1_s[i] = W1[i];
     __syncthreads();
 
-    float mx[T3];
-#pragma unroll
-    for (int t = 0; t < T3; ++t) mx[t] = 0.0f;
+    for (int i = lane; i < C3; i += 64) mx_s[wave][i] = 0.0f;  // post-ReLU values are >= 0
     int par = 0;
 
 #pragma unroll 1
@@ -119,7 +119,11 @@ __global__ __launch_bounds__(256, 3) void sa16_kernel(const float *__restrict__ 
         } else {
             // relu(P[k] - Q[c]): channel 16ti + 4q + r of point k
             const f32x4 *pp = reinterpret_cast<const f32x4 *>(P + ((int64_t)b * n + k) * stride + 4 * q);
-            const f32x4 *qq = reinterpret_cast<const f32x4 *>(Q + cc * stride + 4 * q);
+            // the centre row is re-read per tile (an L1 hit): hoisted out of the loop it would
+            // pin C1 / 2 VGPRs for the whole kernel and cost a wave per SIMD beside FPS work
+            int zero = 0;
+            asm volatile("" : "+v"(zero));
+            const f32x4 *qq = reinterpret_cast<const f32x4 *>(Q + cc * stride + 4 * q + zero);
 #pragma unroll
             for (int ti = 0; ti < T1; ++ti) {
                 const f32x4 a = pp[4 * ti], c = qq[4 * ti];
@@ -180,7 +184,10 @@ __global__ __launch_bounds__(256, 3) void sa16_kernel(const float *__restrict__ 
                     for (int r = 0; r < 4; ++r) v = fmaxf(v, relu(acc[r] + bias));
                     v = fmaxf(v, __shfl_xor(v, 16, 64));
                     v = fmaxf(v, __shfl_xor(v, 32, 64));
-                    mx[t < T3 ? t : 0] = fmaxf(mx[t < T3 ? t : 0], v);
+                    if (q == 0) {
+                        float &m = mx_s[wave][(t < T3 ? 16 * t : 0) + col];
+                        m = fmaxf(m, v);
+                    }
                 }
             }
             __syncthreads();  // (vmcnt(0)) chunk c+1 landed for everyone; buf[par] free for c+2
@@ -190,21 +197,30 @@ __global__ __launch_bounds__(256, 3) void sa16_kernel(const float *__restrict__ 
     if (live && q == 0) {
         float *o = out + unit * out_stride + out_offset;
 #pragma unroll
-        for (int t = 0; t < T3; ++t) o[16 * t + col] = mx[t];
+        for (int t = 0; t < T3; ++t) o[16 * t + col] = mx_s[wave][16 * t + col];
     }
+}
+
+template <int C1, int C2, int C3, int NS, bool XYZ, int WPG>
+int launch16w(const float *p, int64_t stride, const float *q, const int32_t *idx, int64_t batch, int64_t n,
+              int64_t m, const float *packed, float *out, int64_t os, int64_t oo, hipStream_t s)
+{
+    const int64_t total = batch * m;
+    const int64_t blocks = (total + WPG - 1) / WPG;
+    REQUIRE(blocks <= 0x7fffffff, "sa_group_mlp16: too many centres");
+    hipLaunchKernelGGL((sa16_kernel<C1, C2, C3, NS, XYZ, WPG>), dim3((unsigned)blocks), dim3(64 * WPG), 0, s, p,
+                       stride, q, idx, (int)n, (int)m, total, packed, out, os, oo);
+    LAUNCH_CHECK();
+    return LIDAR_OK;
 }
 
 template <int C1, int C2, int C3, int NS, bool XYZ>
 int launch16(const float *p, int64_t stride, const float *q, const int32_t *idx, int64_t batch, int64_t n,
              int64_t m, const float *packed, float *out, int64_t os, int64_t oo, hipStream_t s)
 {
-    const int64_t total = batch * m;
-    const int64_t blocks = (total + 3) / 4;
-    REQUIRE(blocks <= 0x7fffffff, "sa_group_mlp16: too many centres");
-    hipLaunchKernelGGL((sa16_kernel<C1, C2, C3, NS, XYZ>), dim3((unsigned)blocks), dim3(256), 0, s, p, stride, q, idx,
-                       (int)n, (int)m, total, packed, out, os, oo);
-    LAUNCH_CHECK();
-    return LIDAR_OK;
+    // 4 waves per workgroup: 8 (half the weight-chunk traffic per MFMA) measured slower in
+    // the pipeline (425 vs 450 M pts/s), occupancy matters more than L2 -> LDS bytes here
+    return launch16w<C1, C2, C3, NS, XYZ, 4>(p, stride, q, idx, batch, n, m, packed, out, os, oo, s);
 }
 
 }  // namespace

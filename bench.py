@@ -149,6 +149,42 @@ def tier_r_leg(dev, rank, world, frames=32, n=65536, workers=4, steps=3, cpu=Tru
     return rec
 
 
+def variant_leg(rank, world, frames=8, n=65536, cpu=True, cpu_budget=6.0):
+    """the Streamlit apps' own pipeline (app_simplified.py:76-137 ->
+    :234-316, DBSCAN eps 0.3 on unscaled points + KDTree r = 2 cell counts) through the
+    drop-in API, host NumPy frame in -> host dicts out (PCIe included), crowd frames."""
+    import torch
+    from lidar_ai_recommendation_software_amd import variant_pipeline as vp
+    from lidar_ai_recommendation_software_amd.synthetic import crowd_frame
+    xs = [crowd_frame(n, 500 + 97 * rank + i) for i in range(frames)]
+    vp.analyze_crowd_density(vp.preprocess_point_cloud(xs[0]))  # warm-up
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for x in xs:
+        vp.analyze_crowd_density(vp.preprocess_point_cloud(x))
+    dt = time.perf_counter() - t0
+    rec = {"metric": "M points/s through app_simplified.py's preprocess_point_cloud + analyze_crowd_density "
+                     "(drop-in API, host frames in / dicts out, one frame per call)",
+           "value": frames * n / dt / 1e6, "unit": "M points/s", "ms_per_frame": dt / frames * 1e3,
+           "points_per_frame": n, "frames": frames, "data": "synthetic crowd frames (people clumps, metres)",
+           "parity": "byte-identical to scikit-learn's DBSCAN / KDTree results (tests/golden/variant.json)",
+           "cpu_baseline": None}
+    if cpu and rank == 0 and world == 1:
+        from oracle import tier_r
+        k, t0 = 0, time.perf_counter()
+        while True:
+            tier_r.variant_analyze_crowd_density(tier_r.variant_preprocess_point_cloud(xs[k % frames]))
+            k += 1
+            if time.perf_counter() - t0 > cpu_budget or k >= frames:
+                break
+        dtc = time.perf_counter() - t0
+        rec["cpu_baseline"] = {"value": k * n / dtc / 1e6, "unit": "M points/s", "cores": 1, "kind": "port",
+                               "sample": f"{k} x {n}-point crowd frame(s) through oracle/tier_r's variant "
+                                         f"restatement (numpy + the C DBSCAN, 1 thread) in {dtc:.1f} s"}
+        rec["speedup_vs_cpu"] = rec["value"] / rec["cpu_baseline"]["value"]
+    return rec
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -224,6 +260,7 @@ def main():
                            "kernel_ms": k2}
 
     density = None if args.no_density else tier_r_leg(dev, rank, world, cpu=not args.no_cpu_baseline, cpu_budget=args.cpu_budget)
+    variant = None if args.no_density else variant_leg(rank, world, cpu=not args.no_cpu_baseline)
     work = ssg_kernel_work(N)
     traffic = pmc_traffic(B, N)
     # Two chains per group of batches: the side streams' SA1 FPS + ball queries (`depth`
@@ -269,6 +306,7 @@ def main():
                          "batches_per_group": args.fps_group, **chains},
             "other_configs": extras,
             "density_path": density,
+            "variant_path": variant,
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -227,6 +227,24 @@ int lidar_preprocess_batch_f64(lidar_handle *h, const double *xyz, const int64_t
                                int64_t max_n, uint8_t *mask, double *colors, double *normals,
                                double *compact_xyz, int64_t *labels, double *scalars, void *stream);
 
+/* The Streamlit apps' variant preprocess_point_cloud (app_simplified.py:76-137,
+ * app_with_db.py:80-141): lidar_preprocess_batch_f64's phases, then DBSCAN(eps,
+ * min_samples=5) on the UNSCALED non-ground points (no StandardScaler / eps heuristic;
+ * the reference passes eps = 0.3).  offsets == NULL: one frame of max_n points.  Same
+ * outputs and status codes; scalars [22..27] = 0 / 1 and [28..33] = the unscaled bbox. */
+int lidar_preprocess_eps_batch_f64(lidar_handle *h, const double *xyz, const int64_t *offsets,
+                                   int32_t frames, int64_t max_n, double eps, uint8_t *mask,
+                                   double *colors, double *normals, double *compact_xyz,
+                                   int64_t *labels, double *scalars, void *stream);
+
+/* The variant's analyze_crowd_density grid (app_simplified.py:262-282): for the edges xg
+ * (nxg), yg (nyg) (np.arange, device), out (nyg-1, nxg-1) row-major [j][i] = #{people p :
+ * (cx-px)^2 + (cy-py)^2 <= r*r} / divisor with centre ((xg[i]+xg[i+1])/2, (yg[j]+yg[j+1])/2)
+ * — len(KDTree(people).query_radius([centre], r)[0]) / divisor.  people (k, 2) device. */
+int lidar_cell_radius_density_f64(lidar_handle *h, const double *people, int64_t k, const double *xg,
+                                  int64_t nxg, const double *yg, int64_t nyg, double r, double divisor,
+                                  double *out, void *stream);
+
 /* extract_people_positions for every frame of a preprocess batch: people rows of frame f
  * start at row offsets[f] (K_f rows); kdev (device int64[frames]) receives K_f.  Async. */
 int lidar_people_batch_f64(lidar_handle *h, const double *compact_xyz, const int64_t *labels,

@@ -70,6 +70,8 @@ SIGNATURES = {
     "lidar_parse_ascii_xyz": [P, I64, I64, I64, P, I64, P],
     "lidar_preprocess_f64": [P, P, I64, P, P, P, P, P, P, P],
     "lidar_preprocess_batch_f64": [P, P, P, I32, I64, P, P, P, P, P, P, P],
+    "lidar_preprocess_eps_batch_f64": [P, P, P, I32, I64, F64, P, P, P, P, P, P, P],
+    "lidar_cell_radius_density_f64": [P, P, I64, P, I64, P, I64, F64, F64, P, P],
     "lidar_people_batch_f64": [P, P, P, P, I32, I64, P, P, P, P],
     "lidar_density_batch_f64": [P, P, P, P, I32, P, P, I64, P],
     "lidar_people_f64": [P, P, P, I64, P, P, P],

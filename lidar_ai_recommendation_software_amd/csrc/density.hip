@@ -190,7 +190,8 @@ __global__ __launch_bounds__(kT) void preprocess_kernel(const double *__restrict
                                                         double *__restrict__ comp_in,
                                                         double *__restrict__ sc_in,
                                                         int32_t *__restrict__ ng_pos_in,
-                                                        double *__restrict__ S_in, FrameMap fm)
+                                                        double *__restrict__ S_in, FrameMap fm,
+                                                        double fixed_eps)
 {
     __shared__ BlockScratch s;
     __shared__ SeqStage st;
@@ -443,6 +444,27 @@ __global__ __launch_bounds__(kT) void preprocess_kernel(const double *__restrict
     if (nng <= 10) return;  // reference: all non-ground labelled 0, no DBSCAN (:199-200)
     __threadfence_block();
     __syncthreads();
+    if (fixed_eps > 0.0) {
+        // app_simplified.py:104-108 / app_with_db.py:108-112 variant: DBSCAN(eps) on the
+        // UNSCALED non-ground points — no StandardScaler, no eps heuristic; bbox of sc only
+        double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (int64_t i = tid; i < nng; i += kT)
+            for (int c = 0; c < 3; ++c) {
+                lo[c] = fmin(lo[c], sc[3 * i + c]);
+                hi[c] = fmax(hi[c], sc[3 * i + c]);
+            }
+        for (int c = 0; c < 3; ++c) {
+            const double a = block_min(s, lo[c]), b = block_max(s, hi[c]);
+            if (tid == 0) {
+                S[S_SLO + c] = a;
+                S[S_SHI + c] = b;
+                S[S_SMEAN + c] = 0.0;
+                S[S_SSCALE + c] = 1.0;
+            }
+        }
+        if (tid == 0) S[S_EPS] = fixed_eps;
+        return;
+    }
 
     // ---- G: StandardScaler fit (sklearn _incremental_mean_and_var, zero prior) (:190-191)
     {
@@ -1310,7 +1332,7 @@ int run_dbscan(const double *x, int64_t nmax, int32_t min_samples, DbscanWs &w, 
 // offs == nullptr: one frame of n points)
 int run_preprocess(lidar_handle *h, const double *xyz, int64_t n, const int64_t *offs, int frames, uint8_t *mask,
                    double *colors, double *normals, double *compact_xyz, int64_t *labels, double *scalars,
-                   hipStream_t s)
+                   hipStream_t s, double fixed_eps = 0.0)
 {
     lidar::Carver cv;
     const uint64_t o_sc = cv.take<double>(3 * n);
@@ -1330,7 +1352,7 @@ int run_preprocess(lidar_handle *h, const double *xyz, int64_t n, const int64_t 
     fm.offs = offs;
     HIP_TRY(hipMemsetAsync(scalars, 0, sizeof(double) * S_COUNT * frames, s));
     hipLaunchKernelGGL(preprocess_kernel, dim3(1, frames), dim3(kT), 0, s, xyz, n, mask, colors, normals,
-                       compact_xyz, sc, ng_pos, scalars, fm);
+                       compact_xyz, sc, ng_pos, scalars, fm, fixed_eps);
     hipLaunchKernelGGL(dbscan_params_from_preprocess, dim3(1, frames), dim3(64), 0, s, scalars, w.P, w.max_cells, fm);
     int rc = run_dbscan(sc, n, 5, w, ng_lab, s, fm, frames);
     if (rc) return rc;
@@ -1399,6 +1421,25 @@ LIDAR_EXPORT int lidar_preprocess_batch_f64(lidar_handle *h, const double *xyz, 
     HIP_TRY(hipSetDevice(h->device));
     return run_preprocess(h, xyz, max_n, offsets, frames, mask, colors, normals, compact_xyz, labels, scalars,
                           static_cast<hipStream_t>(stream));
+}
+
+// the variant pipeline's preprocess (app_simplified.py:76-137, app_with_db.py:80-141):
+// lidar_preprocess_batch_f64's phases with DBSCAN(eps, min_samples=5) on the unscaled
+// non-ground points.  offsets == nullptr: one frame of max_n points.
+LIDAR_EXPORT int lidar_preprocess_eps_batch_f64(lidar_handle *h, const double *xyz, const int64_t *offsets,
+                                                int32_t frames, int64_t max_n, double eps, uint8_t *mask,
+                                                double *colors, double *normals, double *compact_xyz,
+                                                int64_t *labels, double *scalars, void *stream)
+{
+    REQUIRE(h && xyz && mask && colors && normals && compact_xyz && labels && scalars,
+            "lidar_preprocess_eps_batch_f64: null pointer");
+    REQUIRE(frames >= 1 && frames <= 65535 && (offsets || frames == 1),
+            "lidar_preprocess_eps_batch_f64: need 1 <= frames <= 65535 (offsets for frames > 1)");
+    REQUIRE(max_n >= 1 && max_n < 0x7fffffff, "lidar_preprocess_eps_batch_f64: need 1 <= max_n < 2^31");
+    REQUIRE(eps > 0.0 && eps < INFINITY, "lidar_preprocess_eps_batch_f64: eps must be finite and > 0");
+    HIP_TRY(hipSetDevice(h->device));
+    return run_preprocess(h, xyz, max_n, offsets, frames, mask, colors, normals, compact_xyz, labels, scalars,
+                          static_cast<hipStream_t>(stream), eps);
 }
 
 LIDAR_EXPORT int lidar_people_f64(lidar_handle *h, const double *xyz, const int64_t *labels, int64_t n,
@@ -1594,6 +1635,59 @@ LIDAR_EXPORT int lidar_histogram2d_f64(lidar_handle *h, const double *a, const d
         hipLaunchKernelGGL(hist2d_kernel, dim3(point_blocks(n, 1)), dim3(256), 0, s, a, b, n, xedges, bx, yedges, by,
                            cnt);
     hipLaunchKernelGGL(hist2d_finish_kernel, dim3(point_blocks(m, 1)), dim3(256), 0, s, cnt, m, counts);
+    LAUNCH_CHECK();
+    return LIDAR_OK;
+}
+
+// the variant's grid density (app_simplified.py:262-282, app_with_db.py:266-286): cell (i, j)
+// of the edges xg (nxg), yg (nyg) has centre ((xg[i] + xg[i+1]) / 2, (yg[j] + yg[j+1]) / 2);
+// out[j * (nxg - 1) + i] = #{people p : (cx - px)^2 + (cy - py)^2 <= r*r} / divisor — the
+// count of KDTree(people).query_radius([centre], r) (sklearn's rdist test, no FMA).
+__global__ void cell_radius_density_kernel(const double *__restrict__ people, int64_t k,
+                                           const double *__restrict__ xg, int64_t nx,
+                                           const double *__restrict__ yg, int64_t ny, double r2, double divisor,
+                                           double *__restrict__ out)
+{
+    extern __shared__ double pp[];  // people tile (x, y)
+    const int64_t m = nx * ny;
+    for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < m; base += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t c = base + threadIdx.x;
+        double cx = 0.0, cy = 0.0;
+        if (c < m) {
+            const int64_t i = c % nx, j = c / nx;
+            cx = ddiv(dadd(xg[i], xg[i + 1]), 2.0);
+            cy = ddiv(dadd(yg[j], yg[j + 1]), 2.0);
+        }
+        int64_t cnt = 0;
+        for (int64_t t0 = 0; t0 < k; t0 += blockDim.x) {
+            const int64_t tn = k - t0 < (int64_t)blockDim.x ? k - t0 : (int64_t)blockDim.x;
+            __syncthreads();
+            if (threadIdx.x < tn) {
+                pp[2 * threadIdx.x] = people[2 * (t0 + threadIdx.x)];
+                pp[2 * threadIdx.x + 1] = people[2 * (t0 + threadIdx.x) + 1];
+            }
+            __syncthreads();
+            for (int64_t u = 0; u < tn; ++u) {
+                const double dx = dsub(cx, pp[2 * u]), dy = dsub(cy, pp[2 * u + 1]);
+                cnt += dadd(dmul(dx, dx), dmul(dy, dy)) <= r2;
+            }
+        }
+        if (c < m) out[c] = ddiv((double)cnt, divisor);  // row j = c / nx, column i = c % nx
+    }
+}
+
+LIDAR_EXPORT int lidar_cell_radius_density_f64(lidar_handle *h, const double *people, int64_t k, const double *xg,
+                                               int64_t nxg, const double *yg, int64_t nyg, double r, double divisor,
+                                               double *out, void *stream)
+{
+    REQUIRE(h && xg && yg && out && (k == 0 || people), "lidar_cell_radius_density_f64: null pointer");
+    REQUIRE(k >= 0 && nxg >= 2 && nyg >= 2, "lidar_cell_radius_density_f64: bad sizes");
+    REQUIRE(r >= 0.0 && divisor != 0.0, "lidar_cell_radius_density_f64: bad r / divisor");
+    HIP_TRY(hipSetDevice(h->device));
+    const int64_t nx = nxg - 1, ny = nyg - 1, m = nx * ny;
+    const int64_t blocks = std::min<int64_t>((m + 255) / 256, 65535);
+    hipLaunchKernelGGL(cell_radius_density_kernel, dim3((unsigned)blocks), dim3(256), 2 * 256 * sizeof(double),
+                       static_cast<hipStream_t>(stream), people, k, xg, nx, yg, ny, r * r, divisor, out);
     LAUNCH_CHECK();
     return LIDAR_OK;
 }

@@ -208,3 +208,60 @@ def analyze(pd, grid_size=1.0):
     hs = sorted(hs, key=lambda h: h["density"], reverse=True)[:5]
     return {"total_people": len(people), "avg_density": avg, "max_density": mx, "density_map": dg,
             "grid_coordinates": (fx, fy), "density_values": flat, "hotspots": hs}
+
+
+# ------------------------------------------------- Streamlit apps' variant
+def variant_preprocess_point_cloud(points, eps=0.3):
+    """Restates app_simplified.py:76-137 (== app_with_db.py:80-141): preprocess_lidar_data's
+    colours / 3-sigma filter / 30th-percentile split, then DBSCAN(eps=0.3, min_samples=5) on
+    the UNSCALED non-ground points; returns {points, colors, clusters, dimensions}."""
+    points = np.asarray(points)
+    z = points[:, 2]
+    nh = (z - np.min(z)) / (np.max(z) - np.min(z) + 1e-10)
+    colors = np.zeros((len(points), 3))
+    colors[:, 0] = nh
+    colors[:, 1] = 0.5 * (1 - nh)
+    colors[:, 2] = 0.5
+    mean = np.mean(points, axis=0)
+    std = np.std(points, axis=0)
+    mask = np.all(np.abs(points - mean) < 3 * std, axis=1)
+    inl = points[mask]
+    zt = percentile30(inl[:, 2].astype(np.float64) if inl.dtype.kind != "f" else inl[:, 2])
+    nonground = ~(inl[:, 2] <= zt)
+    ng = inl[nonground]
+    lab = dbscan_labels(ng, eps, 5) if len(ng) > 10 else np.zeros(len(ng), dtype=int)
+    full = np.ones(len(inl), dtype=int) * -1
+    full[nonground] = lab
+    x_min, y_min, z_min = np.min(inl, axis=0)
+    x_max, y_max, z_max = np.max(inl, axis=0)
+    dims = {"x_range": (x_min, x_max), "y_range": (y_min, y_max), "z_range": (z_min, z_max),
+            "width": x_max - x_min, "length": y_max - y_min, "height": z_max - z_min}
+    return {"points": inl, "colors": colors[mask], "clusters": full, "dimensions": dims}
+
+
+def variant_analyze_crowd_density(pd):
+    """Restates app_simplified.py:234-316: KDTree(people).query_radius([centre], r=2.0)
+    counts are sklearn's rdist test ((cx-px)^2 + (cy-py)^2 <= 4.0, no FMA), here brute force."""
+    pts, cl = pd["points"], pd["clusters"]
+    ids = np.unique(cl[cl >= 0])
+    k = len(ids)
+    area = pd["dimensions"]["width"] * pd["dimensions"]["length"]
+    avg = k / max(1, area)
+    if k == 0:
+        return {"total_people": 0, "avg_density": avg, "max_density": 0, "density_grid": np.zeros((1, 1)),
+                "hotspots": []}
+    pos = np.array([np.mean(pts[cl == c], axis=0)[:2] for c in ids])
+    xr, yr = pd["dimensions"]["x_range"], pd["dimensions"]["y_range"]
+    xg = np.arange(xr[0], xr[1] + 1.0, 1.0)
+    yg = np.arange(yr[0], yr[1] + 1.0, 1.0)
+    cx = (xg[:-1] + xg[1:]) / 2
+    cy = (yg[:-1] + yg[1:]) / 2
+    dx = cx[None, :, None] - pos[None, None, :, 0]
+    dy = cy[:, None, None] - pos[None, None, :, 1]
+    grid = np.sum(dx * dx + dy * dy <= 4.0, axis=2) / 4.0
+    top = np.max(grid)
+    thr = max(0.5, avg * 1.5)
+    jj, ii = np.nonzero(grid >= thr)
+    order = np.argsort(-grid[jj, ii], kind="stable")[:5]
+    hs = [{"x": cx[ii[o]], "y": cy[jj[o]], "density": grid[jj[o], ii[o]]} for o in order]
+    return {"total_people": k, "avg_density": avg, "max_density": top, "density_grid": grid, "hotspots": hs}

@@ -101,3 +101,52 @@ def check_tier_r(name, pd, people, res):
     _same(name, res["density_values"], ent["density_values"], "density_values")
     hs = [[float(h["x"]).hex(), float(h["y"]).hex(), float(h["density"]).hex()] for h in res["hotspots"]]
     assert hs == ent["hotspots"], f"{name}.hotspots"
+
+
+# ------------------------------------------------- variant pipeline (gen_variant.py)
+with open(os.path.join(GOLDEN, "variant.json")) as _f:
+    VMETA = json.load(_f)
+VARRAYS = np.load(os.path.join(GOLDEN, "variant.npz"), allow_pickle=False)
+VFRAMES = {
+    "crowd_10000_s42": lambda: crowd_frame(10000, 42),
+    "crowd_16384_s7": lambda: crowd_frame(16384, 7),
+    "crowd_65536_s3": lambda: crowd_frame(65536, 3),
+    "blobs_4293_s0": lambda: blob_frame(60, 60, 300, 0, 15, 0.6),
+    "blobs_8980_s1": lambda: blob_frame(200, 40, 500, 1, 15, 0.3),
+    "lattice_8163_s4": lambda: lattice_frame(4, 120, 60, 4, 15, 0.4),
+    "lattice_15636_s1": lambda: lattice_frame(4, 250, 100, 1, 15, 0.3),
+    "lattice_62978_s2": lambda: lattice_frame(4, 1000, 100, 2, 15, 0.3),
+    "uniform_4096_s0": lambda: uniform_frame(4096, 0),
+    "dense_4096_s1": lambda: uniform_frame(4096, 1, -2.0, 2.0),
+    "small_12": lambda: uniform_frame(12, 5),
+    "small_20": lambda: uniform_frame(20, 5, -0.2, 0.2),
+    "int_4096": lambda: np.floor(uniform_frame(4096, 3, -3.0, 3.0) * 2).astype(np.int64),
+    "dup_4096": lambda: np.repeat(uniform_frame(1024, 4, -3.0, 3.0), 4, axis=0),
+}
+VERROR_FRAMES = {k: ERROR_FRAMES[k] for k in ("empty", "one", "const_col", "all_equal")}
+
+
+def check_variant(name, pd, res):
+    """(preprocess_point_cloud, analyze_crowd_density) outputs vs scikit-learn's (gen_variant.py)."""
+    ent = VMETA["cases"][name]
+    key = f"{name}/clusters"
+    if key in VARRAYS.files:
+        bad = np.flatnonzero(np.asarray(pd["clusters"]) != VARRAYS[key])
+        assert bad.size == 0, f"{name}: {bad.size} labels differ, first at {bad[:5]}"
+    assert set(pd) == {"points", "colors", "clusters", "dimensions"}
+    for k in ("points", "colors", "clusters"):
+        _same(name, pd[k], ent[k], k)
+    d = pd["dimensions"]
+    for k in ("x_range", "y_range", "z_range"):
+        assert [float(v).hex() for v in d[k]] == ent["dims"][k], f"{name}.{k}"
+    for k in ("width", "length", "height"):
+        assert float(d[k]).hex() == ent["dims_scalar"][k], f"{name}.{k}"
+    assert str(np.asarray(d["width"]).dtype) == ent["dims_dtype"]
+    assert res["total_people"] == ent["total_people"]
+    assert float(res["avg_density"]).hex() == ent["avg_density"], f"{name}.avg_density"
+    assert type(res["avg_density"]).__name__ == ent["avg_density_type"], f"{name}.avg_density type"
+    assert float(res["max_density"]).hex() == ent["max_density"], f"{name}.max_density"
+    assert type(res["max_density"]).__name__ == ent["max_density_type"], f"{name}.max_density type"
+    _same(name, res["density_grid"], ent["density_grid"], "density_grid")
+    hs = [[float(h["x"]).hex(), float(h["y"]).hex(), float(h["density"]).hex()] for h in res["hotspots"]]
+    assert hs == ent["hotspots"], f"{name}.hotspots"

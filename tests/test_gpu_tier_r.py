@@ -204,3 +204,59 @@ def test_histogram2d_matches_numpy(cuda, n, bins, rng):
     got = dp.histogram2d(pts[:, 0], pts[:, 1], bins=bins, range=rng)
     for g, w in zip(got, want):
         assert g.dtype == w.dtype and np.array_equal(g, w)
+
+
+# ------------------------------------------------- variant pipeline
+from golden_cases import VERROR_FRAMES, VFRAMES, VMETA, check_variant  # noqa: E402
+from lidar_ai_recommendation_software_amd import variant_pipeline as vp  # noqa: E402
+from lidar_ai_recommendation_software_amd.synthetic import blob_frame, crowd_frame  # noqa: E402
+
+
+@pytest.mark.parametrize("name", sorted(VFRAMES))
+def test_variant_golden(cuda, name):
+    """app_simplified.py's preprocess_point_cloud -> analyze_crowd_density on the GPU vs
+    scikit-learn's DBSCAN / KDTree results (tests/golden/gen_variant.py), byte for byte."""
+    pd = vp.preprocess_point_cloud(VFRAMES[name]())
+    check_variant(name, pd, vp.analyze_crowd_density(pd))
+
+
+@pytest.mark.parametrize("name", sorted(VERROR_FRAMES))
+def test_variant_errors(cuda, name):
+    with pytest.raises(Exception) as ei:
+        vp.analyze_crowd_density(vp.preprocess_point_cloud(VERROR_FRAMES[name]()))
+    assert type(ei.value).__name__ == VMETA["errors"][name]
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_variant_vs_oracle_random(cuda, seed):
+    """more frames than the fixtures hold: crowd / blob frames of varied size vs the
+    oracle's restatement (pinned to scikit-learn by tests/test_oracle.py)."""
+    rng = np.random.default_rng(seed)
+    n = int(rng.integers(2000, 40000))
+    pts = crowd_frame(n, 100 + seed) if seed % 2 else blob_frame(int(rng.integers(20, 200)), 50, 300, seed, 12, 0.35)
+    got_pd = vp.preprocess_point_cloud(pts)
+    want_pd = tier_r.variant_preprocess_point_cloud(pts)
+    assert np.array_equal(got_pd["clusters"], want_pd["clusters"])
+    assert np.array_equal(got_pd["points"], want_pd["points"])
+    got, want = vp.analyze_crowd_density(got_pd), tier_r.variant_analyze_crowd_density(want_pd)
+    assert got["total_people"] == want["total_people"]
+    assert np.array_equal(got["density_grid"], want["density_grid"])
+    assert float(got["avg_density"]).hex() == float(want["avg_density"]).hex()
+    assert [(float(h["x"]).hex(), float(h["y"]).hex(), h["density"]) for h in got["hotspots"]] == \
+        [(float(h["x"]).hex(), float(h["y"]).hex(), h["density"]) for h in want["hotspots"]]
+
+
+def test_cell_radius_density_boundary(cuda):
+    """people exactly at distance r (counted: <=) and just beyond; grid edges from np.arange."""
+    import torch
+    from lidar_ai_recommendation_software_amd import _native as nat
+    people = np.array([[0.5, 0.5], [2.5, 0.5], [0.5, 2.5 + 1e-12], [-1.5, 0.5]], dtype=np.float64)
+    xg, yg = np.arange(0.0, 4.0, 1.0), np.arange(0.0, 3.0, 1.0)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    out = torch.empty((len(yg) - 1, len(xg) - 1), dtype=torch.float64, device="cuda")
+    pd_, xd, yd = T(people), T(xg), T(yg)  # kept alive until the kernel has run
+    nat.call("lidar_cell_radius_density_f64", nat.handle(0), nat.ptr(pd_), len(people), nat.ptr(xd),
+             len(xg), nat.ptr(yd), len(yg), 2.0, 4.0, nat.ptr(out), nat.stream_ptr())
+    cx, cy = (xg[:-1] + xg[1:]) / 2, (yg[:-1] + yg[1:]) / 2
+    d = (cx[None, :, None] - people[None, None, :, 0]) ** 2 + (cy[:, None, None] - people[None, None, :, 1]) ** 2
+    assert np.array_equal(out.cpu().numpy(), np.sum(d <= 4.0, axis=2) / 4.0)

@@ -92,3 +92,21 @@ def test_tier_n_frozen_vectors():
         for k, v in got.items():
             assert np.array_equal(v, g[f"{name}/{k}"]) if v.dtype.kind in "iu" else \
                 np.allclose(v, g[f"{name}/{k}"], rtol=1e-5, atol=1e-6), f"{name}/{k}"
+
+
+# ------------------------------------------------- variant pipeline
+from golden_cases import VERROR_FRAMES, VFRAMES, VMETA, check_variant  # noqa: E402
+
+
+@pytest.mark.parametrize("name", sorted(VFRAMES))
+def test_variant_oracle_matches_sklearn(name):
+    pd = tier_r.variant_preprocess_point_cloud(VFRAMES[name]())
+    check_variant(name, pd, tier_r.variant_analyze_crowd_density(pd))
+
+
+@pytest.mark.parametrize("name", sorted(VERROR_FRAMES))
+def test_variant_oracle_errors(name):
+    want = VMETA["errors"][name]
+    with pytest.raises(Exception) as ei:
+        tier_r.variant_analyze_crowd_density(tier_r.variant_preprocess_point_cloud(VERROR_FRAMES[name]()))
+    assert type(ei.value).__name__ == want

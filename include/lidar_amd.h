@@ -245,6 +245,27 @@ int lidar_cell_radius_density_f64(lidar_handle *h, const double *people, int64_t
                                   int64_t nxg, const double *yg, int64_t nyg, double r, double divisor,
                                   double *out, void *stream);
 
+/* ---- models/crowd_flow_model.py, HOST code (host pointers): the
+ * model's deciding arithmetic is glibc sin / cos / pow and sklearn's KD-tree traversal,
+ * reproduced bit for bit on the host.
+ * _generate_simulated_flow (crowd_flow_model.py:88-184) after its RNG draws: positions
+ * (nx*ny, 2) = meshgrid(x_grid, y_grid) raveled, vectors (m, 2), magnitudes (m);
+ * bottlenecks (nb, 2) = the (x, y) uniform draws. */
+int lidar_flow_field_f64(const double *x_grid, int64_t nx, const double *y_grid, int64_t ny, double exit_x,
+                         double exit_y, int32_t complexity, const double *bottlenecks, int32_t nb,
+                         double speed_min, double speed_max, double *positions, double *vectors,
+                         double *magnitudes);
+/* _identify_bottlenecks (crowd_flow_model.py:186-279): nodes with magnitude <= slow, >=
+ * min_close neighbours within r_close and >= min_far more within r_far (sklearn KDTree
+ * query_radius order), severity > 1 -> (out_x, out_y, out_severity = min(10, round())) in
+ * node order (out_raw: the unrounded severity, optional); *n_out = candidates. */
+int lidar_flow_bottlenecks_f64(const double *positions, const double *vectors, const double *magnitudes,
+                               int64_t m, double slow, double r_close, double r_far, int32_t min_close,
+                               int32_t min_far, double *out_x, double *out_y, int64_t *out_severity,
+                               double *out_raw, int64_t cap, int64_t *n_out);
+/* sklearn KDTree(x, leaf_size).get_arrays()[1]: the build's index permutation (x (n, d)). */
+int lidar_kdtree_order_f64(const double *x, int64_t n, int32_t d, int32_t leaf_size, int64_t *perm);
+
 /* extract_people_positions for every frame of a preprocess batch: people rows of frame f
  * start at row offsets[f] (K_f rows); kdev (device int64[frames]) receives K_f.  Async. */
 int lidar_people_batch_f64(lidar_handle *h, const double *compact_xyz, const int64_t *labels,

@@ -72,6 +72,9 @@ SIGNATURES = {
     "lidar_preprocess_batch_f64": [P, P, P, I32, I64, P, P, P, P, P, P, P],
     "lidar_preprocess_eps_batch_f64": [P, P, P, I32, I64, F64, P, P, P, P, P, P, P],
     "lidar_cell_radius_density_f64": [P, P, I64, P, I64, P, I64, F64, F64, P, P],
+    "lidar_flow_field_f64": [P, I64, P, I64, F64, F64, I32, P, I32, F64, F64, P, P, P],
+    "lidar_flow_bottlenecks_f64": [P, P, P, I64, F64, F64, F64, I32, I32, P, P, P, P, I64, P],
+    "lidar_kdtree_order_f64": [P, I64, I32, I32, P],
     "lidar_people_batch_f64": [P, P, P, P, I32, I64, P, P, P, P],
     "lidar_density_batch_f64": [P, P, P, P, I32, P, P, I64, P],
     "lidar_people_f64": [P, P, P, I64, P, P, P],

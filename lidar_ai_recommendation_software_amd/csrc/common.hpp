@@ -146,6 +146,29 @@ __device__ __forceinline__ uint32_t wave_min_u32_dpp(uint32_t v)
     const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)v, 32), d = (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
     return min(min(a, b), min(c, d));
 }
+// Distances in bit space: for IEEE floats that are >= +0 or the -1 sentinel, the signed
+// int order of the bits IS the float order, and an int max/min needs no NaN canonicalisation,
+// so LLVM fuses each DPP move into the max (1 VALU per step instead of 3).
+__device__ __forceinline__ int wave_max_i32_dpp(int v)
+{
+    v = max(v, dpp_i<0xB1>(v));
+    v = max(v, dpp_i<0x4E>(v));
+    v = max(v, dpp_i<0x141>(v));
+    v = max(v, dpp_i<0x140>(v));
+    const int a = __builtin_amdgcn_readlane(v, 0), b = __builtin_amdgcn_readlane(v, 16);
+    const int c = __builtin_amdgcn_readlane(v, 32), d = __builtin_amdgcn_readlane(v, 48);
+    return max(max(a, b), max(c, d));
+}
+// wave argmax of (dbits, -idx) in bit space (see wave_max_i32_dpp); *dmax = the max bits
+__device__ __forceinline__ int wave_argmax_lane_i32(int dbits, uint32_t idx, int *dmax)
+{
+    const int m = wave_max_i32_dpp(dbits);
+    const uint64_t c = __ballot(dbits == m);
+    *dmax = m;
+    if (__popcll(c) == 1) return __ffsll((unsigned long long)c) - 1;
+    const uint32_t mi = wave_min_u32_dpp(dbits == m ? idx : 0xffffffffu);
+    return __ffsll((unsigned long long)__ballot(dbits == m && idx == mi)) - 1;
+}
 // lane holding the wave argmax of (d, -idx): max d, lowest idx among equal d.
 // Inactive lanes pass d = -1.  Returns the lane; *dmax = the max.
 __device__ __forceinline__ int wave_argmax_lane(float d, uint32_t idx, float *dmax)

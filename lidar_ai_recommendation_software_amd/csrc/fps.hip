@@ -53,9 +53,11 @@ struct FrameWs {
                 // update dirties 2 cache lines per bucket, not 8 (the L2 holds ~4 frames per XCD)
 };
 
+// distance from q to [lo, hi] along one axis: lo - q below, q - hi above, else 0 — as
+// max3(lo - q, q - hi, 0) (one of the two differences is <= 0 whenever the other is > 0)
 __device__ __forceinline__ float gap(float q, float lo, float hi)
 {
-    return q < lo ? __fsub_rn(lo, q) : (q > hi ? __fsub_rn(q, hi) : 0.0f);
+    return fmaxf(fmaxf(__fsub_rn(lo, q), __fsub_rn(q, hi)), 0.0f);
 }
 
 constexpr int kLoopWaves = kThreads / 64;
@@ -69,7 +71,8 @@ __device__ __forceinline__ void update_batch(uint64_t &mask, const FrameWs &W, i
 {
     // branch-free: the workspace is padded to whole buckets with sentinel points
     // (dist -1: never the max, never updated since every real d >= 0)
-    int bbs[K], pos[K];
+    int bbs[K];
+    uint32_t pos[K];  // unsigned: the loads take the SGPR base + 32-bit offset form
     float4 P[K];
     float D[K];
     uint32_t I[K];
@@ -77,7 +80,7 @@ __device__ __forceinline__ void update_batch(uint64_t &mask, const FrameWs &W, i
     for (int u = 0; u < K; ++u) {
         bbs[u] = __ffsll((unsigned long long)mask) - 1;
         mask &= mask - 1;
-        pos[u] = (wave + kLoopWaves * (q * 64 + bbs[u])) * 64 + lane;
+        pos[u] = (uint32_t)((wave + kLoopWaves * (q * 64 + bbs[u])) * 64 + lane);
     }
 #pragma unroll
     for (int u = 0; u < K; ++u) {
@@ -86,15 +89,16 @@ __device__ __forceinline__ void update_batch(uint64_t &mask, const FrameWs &W, i
     }
 #pragma unroll
     for (int u = 0; u < K; ++u) I[u] = __float_as_uint(P[u].w);
-    float od[K], dm[K];
+    // distances in bit space (>= +0 or the -1 sentinel: signed int order = float order)
+    int od[K], dm[K];
 #pragma unroll
     for (int u = 0; u < K; ++u) {
         const float d = lidar::dist2f(P[u].x, P[u].y, P[u].z, qx, qy, qz);
-        od[u] = fminf(D[u], d);
-        W.d[pos[u]] = od[u];
+        od[u] = min(__float_as_int(D[u]), __float_as_int(d));
+        W.d[pos[u]] = __int_as_float(od[u]);
     }
 #pragma unroll
-    for (int u = 0; u < K; ++u) dm[u] = lidar::wave_max_dpp(od[u]);
+    for (int u = 0; u < K; ++u) dm[u] = lidar::wave_max_i32_dpp(od[u]);
 #pragma unroll
     for (int u = 0; u < K; ++u) {
         const uint64_t c = __ballot(od[u] == dm[u]);
@@ -110,7 +114,7 @@ __device__ __forceinline__ void update_batch(uint64_t &mask, const FrameWs &W, i
         const float wy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(P[u].y), wl));
         const float wz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(P[u].z), wl));
         const bool me = lane == bbs[u];
-        bd = me ? dm[u] : bd;
+        bd = me ? __int_as_float(dm[u]) : bd;
         bi = me ? wi : bi;
         bx[0] = me ? wx : bx[0];
         bx[1] = me ? wy : bx[1];
@@ -125,56 +129,15 @@ __device__ __forceinline__ uint64_t stamp()
     return t;
 }
 
-// DIAG builds (lidar_diag_fps_phases only) accumulate per-phase shader cycles per wave:
-// [0] bucket tests + active-bucket updates, [1] wave argmax + LDS publish, [2] barrier
-// wait, [3] 16-way merge, [4] active-bucket batches processed, [5] steps
-template <int BPL, bool DIAG = false>
-__global__ __launch_bounds__(kThreads) void fps_bucket_kernel(const float *__restrict__ xyz,
-                                                              int n, int npoint,
-                                                              int32_t *__restrict__ out_idx,
-                                                              float *__restrict__ out_xyz,
-                                                              int32_t *__restrict__ first_zero,
-                                                              const int32_t *__restrict__ prefix_ok,
-                                                              float *__restrict__ ws, int64_t ws_stride,
-                                                              uint64_t *__restrict__ diag = nullptr)
+// Prologue of one frame, run by the whole workgroup: frame bbox, counting sort of the points
+// by 16^3 Morton cell into W (padded to whole buckets with dist -1 sentinels), bucket
+// bounding boxes into bbox_tab[nb][6].  Ends with a barrier.
+__device__ __forceinline__ void fps_prologue(const float *__restrict__ p, int n, const FrameWs &W,
+                                             uint32_t *hist, float (*red)[kWaves], uint32_t *wsum,
+                                             float *bbox_tab)
 {
-    uint64_t dacc[6] = {0, 0, 0, 0, 0, 0};
-    uint64_t t0 = 0, t1 = 0;
-    const int b = blockIdx.x;
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = tid >> 6;
-    const float *p = xyz + (int64_t)b * n * 3;
-
-    // nested FPS shortcut: FPS over the first m points of an FPS ordering returns 0..m-1
-    // as long as the parent's winning distance stayed > 0 (DESIGN.md §3.1) — exact.
-    if (prefix_ok != nullptr && prefix_ok[b] >= npoint) {
-        for (int i = tid; i < npoint; i += kThreads) {
-            out_idx[(int64_t)b * npoint + i] = i;
-            if (out_xyz) {
-                float *o = out_xyz + ((int64_t)b * npoint + i) * 3;
-                o[0] = p[3 * i];
-                o[1] = p[3 * i + 1];
-                o[2] = p[3 * i + 2];
-            }
-        }
-        if (first_zero && tid == 0) first_zero[b] = prefix_ok[b];
-        return;
-    }
-
-    float *wsb = ws + (int64_t)b * ws_stride;
-    const int npad = (n + 63) / 64 * 64;  // whole buckets; the tail holds sentinel points
-    FrameWs W{reinterpret_cast<float4 *>(wsb), wsb + 4 * (int64_t)npad};
-
-    __shared__ uint32_t hist[kCells];
-    __shared__ float red[6][kWaves];
-    __shared__ uint32_t wsum[kWaves];
-    // per-step merge: every wave submits its argmax as one 64-bit key to an LDS atomic max
-    // (triple-buffered so a slot is cleared two barriers after its last read) and its
-    // coordinates to a per-wave slot (double-buffered); one barrier per step
-    __shared__ unsigned long long mkey[3];
-    __shared__ __attribute__((aligned(16))) float mcrd[2][kWaves][4];
-
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int npad = (n + 63) / 64 * 64;
     // ---- frame bounding box
     float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
     for (int i = tid; i < n; i += kThreads) {
@@ -263,7 +226,6 @@ __global__ __launch_bounds__(kThreads) void fps_bucket_kernel(const float *__res
 
     // ---- bucket bounding boxes: every wave reduces 64-point buckets into an LDS table
     const int nb = (n + 63) / 64;
-    extern __shared__ float bbox_tab[];  // [nb][6]
     for (int bucket = wave; bucket < nb; bucket += kWaves) {
         const int pos = bucket * 64 + lane;
         float v[3] = {INFINITY, INFINITY, INFINITY}, u[3] = {-INFINITY, -INFINITY, -INFINITY};
@@ -287,8 +249,62 @@ __global__ __launch_bounds__(kThreads) void fps_bucket_kernel(const float *__res
         }
     }
     __syncthreads();
-    static_assert(kWaves == kLoopWaves, "every wave runs the step loop");
 
+}
+// DIAG builds (lidar_diag_fps_phases only) accumulate per-phase shader cycles per wave:
+// [0] bucket tests + active-bucket updates, [1] wave argmax + LDS publish, [2] barrier
+// wait, [3] 16-way merge, [4] active-bucket batches processed, [5] steps
+template <int BPL, bool DIAG = false>
+__global__ __launch_bounds__(kThreads) void fps_bucket_kernel(const float *__restrict__ xyz,
+                                                              int n, int npoint,
+                                                              int32_t *__restrict__ out_idx,
+                                                              float *__restrict__ out_xyz,
+                                                              int32_t *__restrict__ first_zero,
+                                                              const int32_t *__restrict__ prefix_ok,
+                                                              float *__restrict__ ws, int64_t ws_stride,
+                                                              uint64_t *__restrict__ diag = nullptr)
+{
+    uint64_t dacc[6] = {0, 0, 0, 0, 0, 0};
+    uint64_t t0 = 0, t1 = 0;
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const float *p = xyz + (int64_t)b * n * 3;
+
+    // nested FPS shortcut: FPS over the first m points of an FPS ordering returns 0..m-1
+    // as long as the parent's winning distance stayed > 0 (DESIGN.md §3.1) — exact.
+    if (prefix_ok != nullptr && prefix_ok[b] >= npoint) {
+        for (int i = tid; i < npoint; i += kThreads) {
+            out_idx[(int64_t)b * npoint + i] = i;
+            if (out_xyz) {
+                float *o = out_xyz + ((int64_t)b * npoint + i) * 3;
+                o[0] = p[3 * i];
+                o[1] = p[3 * i + 1];
+                o[2] = p[3 * i + 2];
+            }
+        }
+        if (first_zero && tid == 0) first_zero[b] = prefix_ok[b];
+        return;
+    }
+
+    float *wsb = ws + (int64_t)b * ws_stride;
+    const int npad = (n + 63) / 64 * 64;  // whole buckets; the tail holds sentinel points
+    FrameWs W{reinterpret_cast<float4 *>(wsb), wsb + 4 * (int64_t)npad};
+
+    __shared__ uint32_t hist[kCells];
+    __shared__ float red[6][kWaves];
+    __shared__ uint32_t wsum[kWaves];
+    // per-step merge: every wave submits its argmax as one 64-bit key to an LDS atomic max
+    // (triple-buffered so a slot is cleared two barriers after its last read) and its
+    // coordinates to a per-wave slot (double-buffered); one barrier per step
+    __shared__ unsigned long long mkey[3];
+    __shared__ __attribute__((aligned(16))) float mcrd[2][kWaves][4];
+
+    extern __shared__ float bbox_tab[];  // [nb][6]
+    fps_prologue(p, n, W, hist, red, wsum, bbox_tab);
+    const int nb = (n + 63) / 64;
+    static_assert(kWaves == kLoopWaves, "every wave runs the step loop");
     // ---- per-bucket state in the owner lane: bucket = wave + 4 * (q * 64 + lane)
     float bmin[BPL][3], bmax[BPL][3], bx[BPL][3], bd[BPL];
     uint32_t bi[BPL];
@@ -344,6 +360,8 @@ __global__ __launch_bounds__(kThreads) void fps_bucket_kernel(const float *__res
                 const int cnt = __popcll(mask);
                 if (cnt >= 4)
                     update_batch<4>(mask, W, wave, q, lane, qx, qy, qz, bd[q], bi[q], bx[q]);
+                else if (cnt == 3)  // one round trip instead of 2 + 1
+                    update_batch<3>(mask, W, wave, q, lane, qx, qy, qz, bd[q], bi[q], bx[q]);
                 else if (cnt >= 2)
                     update_batch<2>(mask, W, wave, q, lane, qx, qy, qz, bd[q], bi[q], bx[q]);
                 else
@@ -373,7 +391,9 @@ __global__ __launch_bounds__(kThreads) void fps_bucket_kernel(const float *__res
                     cz = bx[q][2];
                 }
             }
-            const int wl = lidar::wave_argmax_lane(best, besti, &w_d);
+            int wdb;
+            const int wl = lidar::wave_argmax_lane_i32(__float_as_int(best), besti, &wdb);
+            w_d = __int_as_float(wdb);
             w_i = (uint32_t)__builtin_amdgcn_readlane((int)besti, wl);
             w_x = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cx), wl));
             w_y = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cy), wl));
@@ -408,13 +428,17 @@ __global__ __launch_bounds__(kThreads) void fps_bucket_kernel(const float *__res
             __builtin_amdgcn_sched_barrier(0);
         }
         {
+            // the winner's key and every wave's candidate coordinates are read side by side
+            // (lane l reads wave l % 16's slot); the winner's come back by readlane — one
+            // LDS round trip after the barrier instead of two dependent ones
             const unsigned long long key = mkey[slot];
-            const int ww = (int)(key & 15u);
+            const float4 cand = *reinterpret_cast<const float4 *>(mcrd[cslot][lane & (kWaves - 1)]);
+            const int ww = __builtin_amdgcn_readfirstlane((int)(key & 15u));
             const float gdist = __uint_as_float((uint32_t)(key >> 32));
             const uint32_t gidx = (1u << 18) - (((uint32_t)key) >> 4);
-            qx = mcrd[cslot][ww][0];
-            qy = mcrd[cslot][ww][1];
-            qz = mcrd[cslot][ww][2];
+            qx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cand.x), ww));
+            qy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cand.y), ww));
+            qz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cand.z), ww));
             if (tid == 0) {
                 out_idx[(int64_t)b * npoint + it] = (int32_t)gidx;
                 if (out_xyz) {

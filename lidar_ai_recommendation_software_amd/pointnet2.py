@@ -552,12 +552,15 @@ class StreamingSSG:
         self._owned.append(ptr.value)
         return torch.cuda.ExternalStream(ptr.value, device=dev)
 
-    def __del__(self):
-        for p in getattr(self, "_owned", []):
-            try:
-                nat.load_library().lidar_stream_destroy(ctypes_void(p))
-            except Exception:
-                pass
+    def close(self):
+        """Release the CU-masked streams (side_cus > 0).  Explicit, after a device sync: torch
+        only wraps them (ExternalStream) and its caching allocator may still reference them,
+        so they are never destroyed implicitly (a garbage-collected executor leaks them)."""
+        if self._owned:
+            torch.cuda.synchronize(self.bb.device)
+            for p in self._owned:
+                nat.call("lidar_stream_destroy", ctypes_void(p))
+            self._owned = []
 
     def _fps(self, k, xs, ready):
         """SA1 FPS + level-0 ball queries of group k (the batches in xs) on a side stream."""

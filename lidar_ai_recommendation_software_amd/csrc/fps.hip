@@ -340,6 +340,9 @@ __global__ __launch_bounds__(kThreads) void fps_bucket_kernel(const float *__res
     if (tid < 3) mkey[tid] = 0ull;
     __syncthreads();
     int cur3 = 1, nxt3 = 2;
+    // the wave's argmax bucket (slot w_q of lane w_lane): updates only lower bucket keys (max
+    // dist, then lowest index), so while that bucket is untouched the wave argmax stands
+    int w_q = 0, w_lane = 0;
     for (int it = 1; it < npoint; ++it) {
         bool wave_dirty = it == 1;
         if constexpr (DIAG) {
@@ -354,7 +357,7 @@ __global__ __launch_bounds__(kThreads) void fps_bucket_kernel(const float *__res
             const float gz = gap(qz, bmin[q][2], bmax[q][2]);
             const float lb = __fadd_rn(__fadd_rn(__fmul_rn(gx, gx), __fmul_rn(gy, gy)), __fmul_rn(gz, gz));
             uint64_t mask = __ballot(lb < bd[q]);
-            wave_dirty = wave_dirty || mask != 0;
+            wave_dirty = wave_dirty || (q == w_q && ((mask >> w_lane) & 1));
             while (mask) {  // wave-uniform
                 if constexpr (DIAG) dacc[4]++;
                 const int cnt = __popcll(mask);
@@ -375,12 +378,13 @@ __global__ __launch_bounds__(kThreads) void fps_bucket_kernel(const float *__res
             t0 = t1;
             __builtin_amdgcn_sched_barrier(0);
         }
-        // frame argmax: lane best over its buckets -> wave argmax (DPP, only when one of the
-        // wave's buckets changed) -> LDS atomic max of the packed key -> barrier -> broadcast
+        // frame argmax: lane best over its buckets -> wave argmax (DPP, only when the wave's
+        // argmax bucket was touched) -> LDS atomic max of the packed key -> barrier -> broadcast
         if (wave_dirty) {
             float best = bd[0];
             uint32_t besti = bi[0];
             float cx = bx[0][0], cy = bx[0][1], cz = bx[0][2];
+            int bq = 0;
 #pragma unroll
             for (int q = 1; q < BPL; ++q) {
                 if (bd[q] > best || (bd[q] == best && bi[q] < besti)) {
@@ -389,6 +393,7 @@ __global__ __launch_bounds__(kThreads) void fps_bucket_kernel(const float *__res
                     cx = bx[q][0];
                     cy = bx[q][1];
                     cz = bx[q][2];
+                    bq = q;
                 }
             }
             int wdb;
@@ -398,6 +403,8 @@ __global__ __launch_bounds__(kThreads) void fps_bucket_kernel(const float *__res
             w_x = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cx), wl));
             w_y = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cy), wl));
             w_z = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cz), wl));
+            w_lane = wl;
+            w_q = BPL > 1 ? __builtin_amdgcn_readlane(bq, wl) : 0;
         }
         if constexpr (DIAG) {
             __builtin_amdgcn_sched_barrier(0);
@@ -429,10 +436,12 @@ __global__ __launch_bounds__(kThreads) void fps_bucket_kernel(const float *__res
         }
         {
             // the winner's key and every wave's candidate coordinates are read side by side
-            // (lane l reads wave l % 16's slot); the winner's come back by readlane — one
+            // (lane l < 16 reads wave l's slot); the winner's come back by readlane — one
             // LDS round trip after the barrier instead of two dependent ones
             const unsigned long long key = mkey[slot];
-            const float4 cand = *reinterpret_cast<const float4 *>(mcrd[cslot][lane & (kWaves - 1)]);
+            float4 cand = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            if (lane < kWaves)  // 16 lanes read: 256 B per wave instead of 1 KiB of LDS traffic
+                cand = *reinterpret_cast<const float4 *>(mcrd[cslot][lane]);
             const int ww = __builtin_amdgcn_readfirstlane((int)(key & 15u));
             const float gdist = __uint_as_float((uint32_t)(key >> 32));
             const uint32_t gidx = (1u << 18) - (((uint32_t)key) >> 4);

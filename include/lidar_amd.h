@@ -162,6 +162,21 @@ int lidar_sa_group_mlp16_f32(lidar_handle *h, int32_t xyz_level, const float *p,
                              const float *packed, float *out, int64_t out_stride,
                              int64_t out_offset, void *stream);
 
+/* "x3" variants of the 16-row kernels: layers 2-3 in fp32 arithmetic carried by the bf16
+ * matrix cores — every operand split exactly into bf16 hi + lo, products accumulated as
+ * ah*bh + ah*bl + al*bh (v_mfma_f32_16x16x32_bf16, fp32 accumulation; error <= ~2^-15 per
+ * product, within the fp32 path's 1e-4 contract).  Arguments as lidar_sa_group_mlp16_f32;
+ * packed: lidar_mlp_pack_x3_f32's image of lidar_mlp_packed_size_x3 BYTES. */
+int64_t lidar_mlp_packed_size_x3(int32_t xyz_level, int32_t c1, int32_t c2, int32_t c3);
+int lidar_mlp_pack_x3_f32(int32_t xyz_level, int32_t c1, int32_t c2, int32_t c3, const float *w1_host,
+                          const float *b1_host, const float *w2_host, const float *b2_host,
+                          const float *w3_host, const float *b3_host, void *packed_host);
+int lidar_sa_group_mlp_x3_f32(lidar_handle *h, int32_t xyz_level, const float *p, int64_t p_stride,
+                              const float *q, const int32_t *idx, int64_t batch, int64_t n,
+                              int64_t m, int32_t nsample, int32_t c1, int32_t c2, int32_t c3,
+                              const void *packed, float *out, int64_t out_stride,
+                              int64_t out_offset, void *stream);
+
 /* y (batch*m, ldy) columns [col0, col0+3) = xyz rows; columns [col0+3, ldy) zeroed —
  * builds group_all's input [feats, xyz, 0-pad] next to features already in y. */
 int lidar_concat_xyz_pad_f32(lidar_handle *h, const float *xyz, int64_t rows, float *y,

@@ -57,6 +57,9 @@ SIGNATURES = {
     "lidar_mlp_packed_size16": [I32, I32, I32, I32],
     "lidar_mlp_pack16_f32": [I32, I32, I32, I32, P, P, P, P, P, P, P],
     "lidar_sa_group_mlp16_f32": [P, I32, P, I64, P, P, I64, I64, I64, I32, I32, I32, I32, P, P, I64, I64, P],
+    "lidar_mlp_packed_size_x3": [I32, I32, I32, I32],
+    "lidar_mlp_pack_x3_f32": [I32, I32, I32, I32, P, P, P, P, P, P, P],
+    "lidar_sa_group_mlp_x3_f32": [P, I32, P, I64, P, P, I64, I64, I64, I32, I32, I32, I32, P, P, I64, I64, P],
     "lidar_stream_create_cu_mask": [I32, P, I32, P],
     "lidar_stream_destroy": [P],
     "lidar_device_cu_count": [I32, P],
@@ -83,7 +86,7 @@ SIGNATURES = {
 }
 _RESTYPES = {"lidar_last_error": ctypes.c_char_p, "lidar_mlp_packed_size": I64,
              "lidar_mlp_packed_size_bf16": I64,
-             "lidar_mlp_packed_size16": I64}
+             "lidar_mlp_packed_size16": I64, "lidar_mlp_packed_size_x3": I64}
 
 
 def load_library(path=LIB_PATH):

@@ -1,0 +1,336 @@
+// sa_mlp_x3.hip — SetAbstraction layers 2-3 in fp32 arithmetic carried by the bf16 matrix cores.
+//
+// Every fp32 operand x is split exactly as x = hi + lo + e with hi = bf16(x), lo = bf16(x - hi)
+// (RNE both; x - hi is exact in fp32) and |e| <= 2^-17 |x|.  A product is accumulated as
+//   a*b ~ ah*bh + ah*bl + al*bh          (three v_mfma_f32_16x16x32_bf16, fp32 accumulation)
+// whose error against the fp32 product is <= ~2^-15 |a*b| (the dropped al*bl and the two
+// splitting residues): the 1e-4 contract of the fp32 path holds with margin
+// (tests/test_gpu_tier_n.py::test_group_mlp_x3 vs the fp32 oracle).  bf16 x bf16 products are
+// exact in fp32.  The bf16 MFMA issues 16x the fp32 one's flops per cycle, so three of them
+// still run ~5x the fp32 rate.
+//
+// Same fused design as sa_mlp16.hip (16 grouped rows per wave, weights streamed through LDS in
+// chunks of two output tiles shared by the 4 waves, layer 3 transposed so the max-pool is a
+// register max).  16x16x32 bf16 maps: lane l holds A[row l&15][k = 8(l>>4) + j] and
+// B[k = 8(l>>4) + j][col l&15]; D reg r of lane l is row 4(l>>4) + r, column l&15.  An
+// accumulator pair (tiles 2s, 2s+1: channels 16t + 4g + r of point l&15, g = l>>4) is the
+// k-step-s fragment of the next layer with element j <-> channel in(s, g, j) = 32s + 16(j>>2) +
+// 4g + (j&3); the packed weights (lidar_mlp_pack_x3_f32) follow that k order.
+#include <cstring>
+#include <vector>
+
+#include "common.hpp"
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 mfma_bf(bf16x8 a, bf16x8 b, f32x4 c)
+{
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mfma_f(float a, float b, f32x4 c)
+{
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ float relu(float v) { return v > 0.0f ? v : 0.0f; }
+
+// two accumulator tiles -> the hi / lo bf16 fragments of one k-step
+__device__ __forceinline__ void split_pair(const f32x4 &t0, const f32x4 &t1, bf16x8 &hi, bf16x8 &lo)
+{
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const float v = j < 4 ? t0[j] : t1[j - 4];
+        const __bf16 h = (__bf16)v;
+        hi[j] = h;
+        lo[j] = (__bf16)(v - (float)h);
+    }
+}
+
+// packed image (16-byte units "u4"): [W1 fp32 (T1*64 floats, xyz levels only), padded to 16 B]
+// [layer-2 chunks] [layer-3 chunks] [b1 b2 b3 fp32].  Chunk c = output tiles (2c, 2c+1) of a
+// layer with K inputs: u4 at ((s*2 + t)*2 + h)*64 + lane = bf16x8 (h = 0 hi, 1 lo) of
+// W[in(s, lane>>4, j)][16(2c+t) + (lane&15)], j = 0..7, s < K/32.
+template <int C1, int C2, int C3>
+struct PackX3 {
+    static constexpr int T1 = C1 / 16, T2 = C2 / 16, T3 = C3 / 16;
+    static constexpr int KS2 = C1 / 32, KS3 = C2 / 32;
+    static constexpr int CH2 = KS2 * 4 * 64, CH3 = KS3 * 4 * 64;  // chunk sizes in u4
+    static constexpr int W1U4 = T1 * 64 / 4;                     // fp32 W1 in u4
+};
+
+template <int C1, int C2, int C3, int NS, bool XYZ>
+__global__ __launch_bounds__(256, 3) void sa_x3_kernel(const float *__restrict__ P, int64_t stride,
+                                                     const float *__restrict__ Q, const int32_t *__restrict__ idx,
+                                                     int n, int m, int64_t total, const uint4 *__restrict__ packed,
+                                                     float *__restrict__ out, int64_t out_stride, int64_t out_offset)
+{
+    static_assert(NS % 16 == 0 && C1 % 32 == 0 && C2 % 32 == 0 && C3 % 32 == 0, "tile shapes");
+    using K = PackX3<C1, C2, C3>;
+    constexpr int T1 = K::T1, T2 = K::T2, T3 = K::T3, KS2 = K::KS2, KS3 = K::KS3;
+    constexpr int CH2 = K::CH2, CH3 = K::CH3, CHMAX = CH2 > CH3 ? CH2 : CH3;
+    constexpr int NCH = T2 / 2 + T3 / 2;
+    constexpr int TILES = NS / 16;
+    constexpr int PER = (CHMAX + 255) / 256;
+
+    __shared__ uint4 buf[2][CHMAX];
+    __shared__ float bias_s[C1 + C2 + C3];
+    __shared__ float w1_s[XYZ ? T1 * 64 : 1];
+    __shared__ float mx_s[4][C3];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int q = lane >> 4, col = lane & 15;
+    const int64_t unit = (int64_t)blockIdx.x * 4 + wave;
+    const bool live = unit < total;  // every wave takes part in the barriers
+    const int64_t cc = live ? unit : total - 1;
+    const int64_t b = cc / m;
+
+    const uint4 *W2 = packed + (XYZ ? K::W1U4 : 0);
+    const uint4 *W3 = W2 + (int64_t)(T2 / 2) * CH2;
+    const float *Bias = reinterpret_cast<const float *>(W3 + (int64_t)(T3 / 2) * CH3);
+
+    auto fetch = [&](int c, int dst) {
+        const uint4 *src = c < T2 / 2 ? W2 + c * CH2 : W3 + (c - T2 / 2) * CH3;
+        asm volatile("" : "+s"(src));  // keep each chunk's loads in their own iteration
+        const int len = c < T2 / 2 ? CH2 : CH3;
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int base = 256 * i + 64 * wave;
+            if (base < len)
+                __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)(src + base + lane),
+                                                 (__attribute__((address_space(3))) void *)(&buf[dst][base]), 16, 0,
+                                                 0);
+        }
+    };
+    fetch(0, 0);
+    for (int i = tid; i < C1 + C2 + C3; i += 256) bias_s[i] = Bias[i];
+    if constexpr (XYZ)
+        for (int i = tid; i < T1 * 64; i += 256) w1_s[i] = reinterpret_cast<const float *>(packed)[i];
+    for (int i = lane; i < C3; i += 64) mx_s[wave][i] = 0.0f;  // post-ReLU values are >= 0
+    __syncthreads();
+    int par = 0;
+
+#pragma unroll 1
+    for (int tile = 0; tile < TILES; ++tile) {
+        const int64_t k = idx[cc * NS + tile * 16 + col];
+        // ---- layer 1 -> the layer-2 operand fragments (hi / lo) of the 16 grouped rows
+        bf16x8 xh[KS2], xl[KS2];
+        {
+            f32x4 y1[T1];
+            if constexpr (XYZ) {
+                const float *pr = P + ((int64_t)b * n + k) * 3;
+                const float *ce = Q + cc * 3;
+                const float x = q < 3 ? pr[q] - ce[q] : 0.0f;  // lane group q: dx, dy, dz, 0
+#pragma unroll
+                for (int t = 0; t < T1; ++t) {
+                    f32x4 acc = {};
+                    acc = mfma_f(w1_s[t * 64 + lane], x, acc);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) acc[r] = relu(acc[r] + bias_s[16 * t + 4 * q + r]);
+                    y1[t] = acc;
+                }
+            } else {
+                // relu(P[k] - Q[c]); the centre row is re-read per tile (an L1 hit) rather than
+                // held in registers across the tiles
+                int zero = 0;
+                asm volatile("" : "+v"(zero));
+                const f32x4 *pp = reinterpret_cast<const f32x4 *>(P + ((int64_t)b * n + k) * stride + 4 * q);
+                const f32x4 *qq = reinterpret_cast<const f32x4 *>(Q + cc * stride + 4 * q + zero);
+#pragma unroll
+                for (int ti = 0; ti < T1; ++ti) {
+                    const f32x4 a = pp[4 * ti], c = qq[4 * ti];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) y1[ti][r] = relu(a[r] - c[r]);
+                }
+            }
+#pragma unroll
+            for (int s = 0; s < KS2; ++s) split_pair(y1[2 * s], y1[2 * s + 1], xh[s], xl[s]);
+        }
+
+        f32x4 y2[T2];
+        bf16x8 zh[KS3], zl[KS3];
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+            const int cn = c + 1 < NCH ? c + 1 : 0;
+            const bool more = c + 1 < NCH || tile + 1 < TILES;
+            if (more) fetch(cn, par ^ 1);  // lands during this chunk's MFMAs
+            const uint4 *wb = buf[par] + lane;
+            f32x4 a0 = {}, a1 = {};
+            if (c < T2 / 2) {  // layer 2: output tiles 2c, 2c+1 (channel rows x point columns)
+#pragma unroll
+                for (int s = 0; s < KS2; ++s) {
+                    const bf16x8 h0 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 0) * 2 + 0) * 64]);
+                    const bf16x8 l0 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 0) * 2 + 1) * 64]);
+                    const bf16x8 h1 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 1) * 2 + 0) * 64]);
+                    const bf16x8 l1 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 1) * 2 + 1) * 64]);
+                    a0 = mfma_bf(h0, xh[s], a0);
+                    a1 = mfma_bf(h1, xh[s], a1);
+                    a0 = mfma_bf(h0, xl[s], a0);
+                    a1 = mfma_bf(h1, xl[s], a1);
+                    a0 = mfma_bf(l0, xh[s], a0);
+                    a1 = mfma_bf(l1, xh[s], a1);
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    a0[r] = relu(a0[r] + bias_s[C1 + 16 * (2 * c) + 4 * q + r]);
+                    a1[r] = relu(a1[r] + bias_s[C1 + 16 * (2 * c + 1) + 4 * q + r]);
+                }
+                y2[2 * c < T2 ? 2 * c : 0] = a0;
+                y2[2 * c + 1 < T2 ? 2 * c + 1 : 0] = a1;
+                if (c == T2 / 2 - 1) {  // layer 2 complete: its output as layer-3 fragments
+#pragma unroll
+                    for (int s = 0; s < KS3; ++s) split_pair(y2[2 * s], y2[2 * s + 1], zh[s], zl[s]);
+                }
+            } else {  // layer 3: output tiles 2tp, 2tp+1, transposed (point rows), + max-pool
+                const int tp = c - T2 / 2;
+#pragma unroll
+                for (int s = 0; s < KS3; ++s) {
+                    const bf16x8 h0 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 0) * 2 + 0) * 64]);
+                    const bf16x8 l0 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 0) * 2 + 1) * 64]);
+                    const bf16x8 h1 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 1) * 2 + 0) * 64]);
+                    const bf16x8 l1 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 1) * 2 + 1) * 64]);
+                    a0 = mfma_bf(zh[s], h0, a0);
+                    a1 = mfma_bf(zh[s], h1, a1);
+                    a0 = mfma_bf(zh[s], l0, a0);
+                    a1 = mfma_bf(zh[s], l1, a1);
+                    a0 = mfma_bf(zl[s], h0, a0);
+                    a1 = mfma_bf(zl[s], h1, a1);
+                }
+#pragma unroll
+                for (int hh = 0; hh < 2; ++hh) {
+                    const f32x4 &acc = hh ? a1 : a0;
+                    const int t = 2 * tp + hh;
+                    const float bias = bias_s[C1 + C2 + 16 * t + col];
+                    float v = 0.0f;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v = fmaxf(v, relu(acc[r] + bias));
+                    v = fmaxf(v, __shfl_xor(v, 16, 64));
+                    v = fmaxf(v, __shfl_xor(v, 32, 64));
+                    if (q == 0) {
+                        float &mm = mx_s[wave][(t < T3 ? 16 * t : 0) + col];
+                        mm = fmaxf(mm, v);
+                    }
+                }
+            }
+            __syncthreads();  // (vmcnt(0)) chunk c+1 landed for everyone; buf[par] free for c+2
+            par ^= 1;
+        }
+    }
+    if (live && q == 0) {
+        float *o = out + unit * out_stride + out_offset;
+#pragma unroll
+        for (int t = 0; t < T3; ++t) o[16 * t + col] = mx_s[wave][16 * t + col];
+    }
+}
+
+template <int C1, int C2, int C3, int NS, bool XYZ>
+int launch_x3(const float *p, int64_t stride, const float *q, const int32_t *idx, int64_t batch, int64_t n,
+              int64_t m, const void *packed, float *out, int64_t os, int64_t oo, hipStream_t s)
+{
+    const int64_t total = batch * m;
+    const int64_t blocks = (total + 3) / 4;
+    REQUIRE(blocks <= 0x7fffffff, "sa_group_mlp_x3: too many centres");
+    hipLaunchKernelGGL((sa_x3_kernel<C1, C2, C3, NS, XYZ>), dim3((unsigned)blocks), dim3(256), 0, s, p, stride, q,
+                       idx, (int)n, (int)m, total, static_cast<const uint4 *>(packed), out, os, oo);
+    LAUNCH_CHECK();
+    return LIDAR_OK;
+}
+
+__host__ uint16_t bf16_rne(float f)
+{
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);  // NaN stays NaN
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return (uint16_t)(u >> 16);
+}
+__host__ float bf16_to_f(uint16_t h)
+{
+    const uint32_t u = (uint32_t)h << 16;
+    float f;
+    memcpy(&f, &u, 4);
+    return f;
+}
+
+}  // namespace
+
+// bytes of the x3 packed image
+LIDAR_EXPORT int64_t lidar_mlp_packed_size_x3(int32_t xyz_level, int32_t c1, int32_t c2, int32_t c3)
+{
+    const int64_t w1 = xyz_level ? (int64_t)(c1 / 16) * 64 * 4 : 0;
+    return w1 + ((int64_t)(c2 / 32) * (c1 / 32) + (int64_t)(c3 / 32) * (c2 / 32)) * 4 * 64 * 16 +
+           (int64_t)(c1 + c2 + c3) * 4;
+}
+
+// host packer: w1 (3 + ..., c1) read only for an xyz level (its xyz rows, fp32 as the 16-row
+// kernel's layer 1); w2 (c1, c2), w3 (c2, c3) split into bf16 hi / lo in the fragment order
+LIDAR_EXPORT int lidar_mlp_pack_x3_f32(int32_t xyz_level, int32_t c1, int32_t c2, int32_t c3, const float *w1,
+                                       const float *b1, const float *w2, const float *b2, const float *w3,
+                                       const float *b3, void *packed)
+{
+    REQUIRE(b1 && w2 && b2 && w3 && b3 && packed && (!xyz_level || w1), "lidar_mlp_pack_x3_f32: null pointer");
+    REQUIRE(c1 % 32 == 0 && c2 % 32 == 0 && c3 % 32 == 0 && c1 > 0 && c2 > 0 && c3 > 0,
+            "lidar_mlp_pack_x3_f32: widths must be positive multiples of 32");
+    char *o = static_cast<char *>(packed);
+    if (xyz_level) {
+        float *f = reinterpret_cast<float *>(o);
+        for (int t = 0; t < c1 / 16; ++t)
+            for (int l = 0; l < 64; ++l) {
+                const int qq = l >> 4;
+                *f++ = qq < 3 ? w1[(int64_t)qq * c1 + 16 * t + (l & 15)] : 0.0f;
+            }
+        o = reinterpret_cast<char *>(f);
+    }
+    auto layer = [&](const float *w, int cin, int cout) {
+        uint16_t *u = reinterpret_cast<uint16_t *>(o);
+        for (int c = 0; c < cout / 32; ++c)
+            for (int s = 0; s < cin / 32; ++s)
+                for (int t = 0; t < 2; ++t)
+                    for (int h = 0; h < 2; ++h)
+                        for (int l = 0; l < 64; ++l)
+                            for (int j = 0; j < 8; ++j) {
+                                const int in = 32 * s + 16 * (j >> 2) + 4 * (l >> 4) + (j & 3);
+                                const float v = w[(int64_t)in * cout + 16 * (2 * c + t) + (l & 15)];
+                                const uint16_t hi = bf16_rne(v);
+                                *u++ = h == 0 ? hi : bf16_rne(v - bf16_to_f(hi));
+                            }
+        o = reinterpret_cast<char *>(u);
+    };
+    layer(w2, c1, c2);
+    layer(w3, c2, c3);
+    float *f = reinterpret_cast<float *>(o);
+    for (int i = 0; i < c1; ++i) *f++ = b1[i];
+    for (int i = 0; i < c2; ++i) *f++ = b2[i];
+    for (int i = 0; i < c3; ++i) *f++ = b3[i];
+    return LIDAR_OK;
+}
+
+// the x3 fused kernels; arguments as lidar_sa_group_mlp16_f32 (xyz_level: p = xyz, q = centres;
+// else p / q = the per-point / per-centre layer-1 rows), packed = lidar_mlp_pack_x3_f32's image
+LIDAR_EXPORT int lidar_sa_group_mlp_x3_f32(lidar_handle *h, int32_t xyz_level, const float *p, int64_t p_stride,
+                                           const float *q, const int32_t *idx, int64_t batch, int64_t n, int64_t m,
+                                           int32_t nsample, int32_t c1, int32_t c2, int32_t c3, const void *packed,
+                                           float *out, int64_t out_stride, int64_t out_offset, void *stream)
+{
+    REQUIRE(h && p && q && idx && packed && out, "lidar_sa_group_mlp_x3_f32: null pointer");
+    REQUIRE(batch >= 0 && n >= 1 && m >= 1, "lidar_sa_group_mlp_x3_f32: bad sizes");
+    REQUIRE(xyz_level || (p_stride >= c1 && p_stride % 4 == 0), "lidar_sa_group_mlp_x3_f32: bad p_stride");
+    REQUIRE(out_offset >= 0 && out_offset + c3 <= out_stride,
+            "lidar_sa_group_mlp_x3_f32: output columns exceed out_stride");
+    if (batch == 0) return LIDAR_OK;
+    HIP_TRY(hipSetDevice(h->device));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+#define LIDAR_SAX3(C1_, C2_, C3_, NS_, X_)                                                                   \
+    if (!!xyz_level == X_ && c1 == C1_ && c2 == C2_ && c3 == C3_ && nsample == NS_)                           \
+        return launch_x3<C1_, C2_, C3_, NS_, X_>(p, p_stride, q, idx, batch, n, m, packed, out, out_stride, \
+                                                 out_offset, s);
+    LIDAR_SAX3(64, 64, 128, 32, true)
+    LIDAR_SAX3(32, 32, 64, 16, true)
+    LIDAR_SAX3(64, 96, 128, 128, true)
+    LIDAR_SAX3(128, 128, 256, 64, false)
+    LIDAR_SAX3(128, 128, 256, 128, false)
+    LIDAR_SAX3(64, 64, 128, 32, false)
+#undef LIDAR_SAX3
+    return lidar::fail(LIDAR_EINVAL, "lidar_sa_group_mlp_x3_f32: unsupported (widths, nsample) combination");
+}

@@ -185,6 +185,34 @@ def group_mlp16(p, q, idx, n, packed, widths, out, out_offset=0, xyz_level=False
     return out
 
 
+def pack_branch_x3(layers, xyz_level):
+    """Host-side packed image (uint8) for lidar_sa_group_mlp_x3_f32 (bf16 hi/lo fragments)."""
+    (w1, b1), (w2, b2), (w3, b3) = layers
+    c1, c2, c3 = w1.shape[1], w2.shape[1], w3.shape[1]
+    lib = nat.load_library()
+    out = np.zeros(lib.lidar_mlp_packed_size_x3(int(xyz_level), c1, c2, c3), dtype=np.uint8)
+    arrs = [np.ascontiguousarray(a, dtype=np.float32) for a in (w1, b1, w2, b2, w3, b3)]
+    nat.check(lib.lidar_mlp_pack_x3_f32(int(xyz_level), c1, c2, c3, *[a.ctypes.data_as(ctypes.c_void_p) for a in arrs],
+                                        out.ctypes.data_as(ctypes.c_void_p)), "lidar_mlp_pack_x3_f32")
+    return out
+
+
+def group_mlp_x3(p, q, idx, n, packed, widths, out, out_offset=0, xyz_level=False):
+    """group_mlp16 with layers 2-3 on split-bf16 MFMAs (fp32-accurate, see sa_mlp_x3.hip)."""
+    B, M, ns = idx.shape
+    c1, c2, c3 = widths
+    stride = 3 if xyz_level else p.shape[1]
+    if xyz_level and not (p.is_contiguous() and q.is_contiguous()):
+        raise ValueError("group_mlp_x3: xyz / centres must be contiguous")
+    if not xyz_level and (p.shape[0] < B * n or q.shape[0] < B * M or p.shape[1] < c1 or q.shape[1] != p.shape[1]):
+        raise ValueError("group_mlp_x3: p/q shapes do not match the batch")
+    _dev_check(p, q, idx, packed, out)
+    nat.call("lidar_sa_group_mlp_x3_f32", nat.handle(p.device.index), int(xyz_level), nat.ptr(p), stride,
+             nat.ptr(q), nat.ptr(idx), B, n, M, ns, c1, c2, c3, nat.ptr(packed), nat.ptr(out), out.shape[-1],
+             out_offset, nat.stream_ptr())
+    return out
+
+
 def group_mlp(xyz, feats, new_xyz, idx, packed, widths, out=None, out_offset=0, bf16=False):
     """Fused grouping + 3-layer MLP + max over nsample -> (B, M, c3) (or into `out`)."""
     B, N, _ = xyz.shape
@@ -316,14 +344,16 @@ class PointNet2Backbone:
     """SSG / MSG PointNet++ encoder on liblidar_amd.  ``forward(xyz)`` -> global feature
     (B, C_last) plus the per-level (new_xyz, features, fps_idx)."""
 
-    def __init__(self, cfg=SSG, weights=None, device="cuda", seed=0, dtype="f32", pre_layer1=True, mlp16="pre"):
+    def __init__(self, cfg=SSG, weights=None, device="cuda", seed=0, dtype="f32", pre_layer1=True, mlp16="pre", x3=False):
         """dtype "bf16": the SA branches run on bf16 MFMA (inputs/activations/weights rounded
         to bf16, fp32 accumulation; BASELINE configs[4]); group_all stays fp32.
         pre_layer1 (fp32, levels with point features): layer 1 runs per point as a GEMM
         and the fused kernel starts at layer 2 (layer1_per_point / group_mlp_pre).
         mlp16 (fp32): branches whose shape lidar_sa_group_mlp16_f32 instantiates run on the
         16-row kernels (MLP16_SHAPES); "pre" / "xyz": only the per-point-layer-1 / the
-        xyz-only levels."""
+        xyz-only levels.
+        x3 (fp32): the same branches on the split-bf16 kernels (lidar_sa_group_mlp_x3_f32;
+        True, or "pre" / "xyz" for one kind of level)."""
         if dtype not in ("f32", "bf16"):
             raise ValueError("dtype must be 'f32' or 'bf16'")
         self.bf16 = dtype == "bf16"
@@ -358,6 +388,10 @@ class PointNet2Backbone:
                     if (use16 and not self.bf16 and (pre or xyz_level)
                             and (xyz_level, *widths, ns) in MLP16_SHAPES):
                         br["packed16"] = torch.from_numpy(pack_branch16(layers, xyz_level)).to(self.device)
+                    usex3 = x3 is True or (x3 == "pre" and pre) or (x3 == "xyz" and xyz_level)
+                    if (usex3 and not self.bf16 and (pre or xyz_level)
+                            and (xyz_level, *widths, ns) in MLP16_SHAPES):
+                        br["packed_x3"] = torch.from_numpy(pack_branch_x3(layers, xyz_level)).to(self.device)
                     if pre:
                         br["pre"] = layer1_weights(layers[0], cfeat, t)
                     branches.append(br)
@@ -411,7 +445,11 @@ class PointNet2Backbone:
                     gidx = pre_bq[bi_]
                 else:
                     gidx = _call(self.timers, f"{tag}_ball_query", ball_query, br["r"], br["ns"], xyz, new_xyz)
-                if "packed16" in br:
+                if "packed_x3" in br:
+                    p16, q16 = (pq[bi_] if pq is not None else (xyz, new_xyz))
+                    _call(self.timers, f"{tag}_group_mlp", group_mlp_x3, p16, q16, gidx, N, br["packed_x3"],
+                          br["widths"], out=out, out_offset=off, xyz_level=pq is None)
+                elif "packed16" in br:
                     p16, q16 = (pq[bi_] if pq is not None else (xyz, new_xyz))
                     _call(self.timers, f"{tag}_group_mlp", group_mlp16, p16, q16, gidx, N, br["packed16"],
                           br["widths"], out=out, out_offset=off, xyz_level=pq is None)

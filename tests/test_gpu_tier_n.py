@@ -168,6 +168,44 @@ def test_group_mlp16(cuda, cfg_name, level, branch):
         feat_close(got[bi, :, off:off + widths[-1]], want, f"{cfg_name} L{level} br{branch} frame {bi} (16-row)")
 
 
+@pytest.mark.parametrize("cfg_name,level,branch", [("ssg", 0, 0), ("msg", 0, 0), ("msg", 0, 1), ("msg", 0, 2),
+                                                   ("ssg", 1, 0), ("msg", 1, 0), ("msg", 1, 1), ("msg", 1, 2)])
+def test_group_mlp_x3(cuda, cfg_name, level, branch):
+    """split-bf16 kernels (layers 2-3 as ah*bh + ah*bl + al*bh on bf16 MFMAs) vs the fp32
+    oracle at the fp32 path's own 1e-4 tolerance; also reports the max relative error."""
+    cfg = pn.CONFIGS[cfg_name]
+    w = pn.init_weights(cfg, seed=6)
+    lvl = cfg["levels"][level]
+    layers = w[level][branch]
+    cfeat = layers[0][0].shape[0] - 3
+    r, ns, widths = lvl["radii"][branch], lvl["nsamples"][branch], lvl["mlps"][branch]
+    B, N, M = 2, 2000, 101
+    rng = np.random.default_rng(10)
+    x = unit_frames(B, N, 13)
+    f = np.abs(rng.standard_normal((B, N, cfeat))).astype(np.float32) if cfeat else None
+    c = x[:, :M].copy()
+    gi = tier_n.ball_query(x, c, r, ns)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(cuda)
+    packed = T(pn.pack_branch_x3(layers, cfeat == 0))
+    off, stride = 3, widths[-1] + 5
+    out = torch.full((B, M, stride), -7.0, dtype=torch.float32, device=cuda)
+    gti = torch.from_numpy(gi).to(cuda)
+    if cfeat == 0:
+        pn.group_mlp_x3(T(x), T(c), gti, N, packed, widths, out, off, xyz_level=True)
+    else:
+        kp = (cfeat + 3 + 15) // 16 * 16
+        rows = torch.zeros(((B * N + 127) // 128 * 128, kp), dtype=torch.float32, device=cuda)
+        rows[:B * N, :cfeat] = T(f.reshape(-1, cfeat).astype(np.float32))
+        Tf = lambda a: T(np.asarray(a, dtype=np.float32))
+        (P, Q), = pn.layer1_per_point(rows, T(x), cfeat, T(c), [{"pre": pn.layer1_weights(layers[0], cfeat, Tf)}])
+        pn.group_mlp_x3(P, Q, gti, N, packed, widths, out, off)
+    got = out.cpu().numpy()
+    assert (got[..., :off] == -7.0).all() and (got[..., off + widths[-1]:] == -7.0).all()
+    for bi in range(B):
+        want = tier_n.mlp_maxpool(tier_n.group(x[bi], None if f is None else f[bi], c[bi], gi[bi]), layers, ns)
+        feat_close(got[bi, :, off:off + widths[-1]], want, f"{cfg_name} L{level} br{branch} frame {bi} (x3)")
+
+
 def test_dense_no_relu(cuda):
     rng = np.random.default_rng(2)
     x = rng.standard_normal((256, 144)).astype(np.float32)
@@ -193,10 +231,12 @@ def test_dense_relu_and_pool(cuda):
 @pytest.mark.parametrize("cfg_name,n,pre,mlp16", [
     ("ssg", 16384, True, False), ("ssg", 65536, True, False), ("sa1", 16384, True, False),
     ("msg", 16384, True, False), ("ssg", 16384, False, False), ("msg", 16384, False, False),
-    ("ssg", 5000, True, False), ("ssg", 65536, True, True), ("msg", 16384, True, True), ("sa1", 16384, True, True)])
+    ("ssg", 5000, True, False), ("ssg", 65536, True, True), ("msg", 16384, True, True), ("sa1", 16384, True, True),
+    ("ssg", 65536, True, "x3"), ("msg", 16384, True, "x3"), ("sa1", 16384, True, "x3")])
 def test_backbone_vs_oracle(cuda, cfg_name, n, pre, mlp16):
     cfg = pn.CONFIGS[cfg_name]
-    bb = pn.PointNet2Backbone(cfg, device=cuda, seed=0, pre_layer1=pre, mlp16=mlp16)
+    x3 = mlp16 == "x3"
+    bb = pn.PointNet2Backbone(cfg, device=cuda, seed=0, pre_layer1=pre, mlp16=False if x3 else mlp16, x3=x3)
     x = unit_frames(1, n, 21)
     g, levels = bb.forward(torch.from_numpy(x).to(cuda), keep_levels=True)
     torch.cuda.synchronize()

@@ -100,9 +100,12 @@ def mlp_micro():
         print(f"{name} group_mlp: {ms:.3f} ms  {flops / ms / 1e9:.1f} TFLOP/s ({flops / ms / 1e9 / 157.3 * 100:.1f}% of fp32 peak)",
               flush=True)
         pk16 = torch.from_numpy(pn.pack_branch16(layers, cf == 0)).to(dev)
+        pkx3 = torch.from_numpy(pn.pack_branch_x3(layers, cf == 0)).to(dev)
         if cf == 0:
             ms = timeit(lambda: pn.group_mlp16(x, c, gi, N, pk16, widths, out, xyz_level=True), reps=10)
             print(f"{name} group_mlp16: {ms:.3f} ms  {flops / ms / 1e9:.1f} TFLOP/s", flush=True)
+            ms = timeit(lambda: pn.group_mlp_x3(x, c, gi, N, pkx3, widths, out, xyz_level=True), reps=10)
+            print(f"{name} group_mlp_x3: {ms:.3f} ms  {flops / ms / 1e9:.1f} fp32-equivalent TFLOP/s", flush=True)
         if cf:
             P = torch.from_numpy(rng.standard_normal((B * N, widths[0])).astype(np.float32)).to(dev)
             Q = torch.from_numpy(rng.standard_normal((B * M, widths[0])).astype(np.float32)).to(dev)
@@ -112,6 +115,9 @@ def mlp_micro():
                   f"({flops / ms / 1e9 / 157.3 * 100:.1f}% of fp32 peak)", flush=True)
             ms = timeit(lambda: pn.group_mlp16(P, Q, gi, N, pk16, widths, out), reps=10)
             print(f"{name} group_mlp16 (layers 2-3): {ms:.3f} ms  {flops / ms / 1e9:.1f} TFLOP/s", flush=True)
+            ms = timeit(lambda: pn.group_mlp_x3(P, Q, gi, N, pkx3, widths, out), reps=10)
+            print(f"{name} group_mlp_x3 (layers 2-3): {ms:.3f} ms  {flops / ms / 1e9:.1f} fp32-equivalent TFLOP/s",
+                  flush=True)
 
 
 if __name__ == "__main__" and "mlp" in sys.argv:

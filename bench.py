@@ -34,6 +34,9 @@ sys.path.insert(0, REPO)
 
 # per-frame algorithmic work of each kernel of the SSG stack at N points
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: fp32 matrix (= vector) peak
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: bf16 dense matrix peak
+# the x3 kernels carry each fp32 product as 3 bf16 MFMA products: their fp32-equivalent peak
+X3_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 3
 HBM_PEAK_GBS = 8000.0
 
 
@@ -202,6 +205,12 @@ def main():
     ap.add_argument("--cu-layout", default="xcd", choices=["xcd", "low"])
     ap.add_argument("--mlp16", default="pre", choices=["0", "1", "pre", "xyz"],
                     help="SA branches on the 16-row MFMA kernels: 1 all, pre / xyz only those levels")
+    ap.add_argument("--x3", default="1", choices=["0", "1", "pre", "xyz"],
+                    help="SA layers 2-3 on the split-bf16 (x3) kernels: fp32 arithmetic within the 1e-4 "
+                         "contract; 0 = native fp32 MFMA kernels")
+    ap.add_argument("--bq-main", type=int, default=1, help="1: SA1 ball queries on the main stream")
+    ap.add_argument("--no-fp32-mfma-leg", action="store_true",
+                    help="skip the extra measurement of the native fp32-MFMA kernels (when --x3 is on)")
     ap.add_argument("--no-extras", action="store_true", help="skip the configs[1]/[4] side measurements")
     ap.add_argument("--no-density", action="store_true", help="skip the Tier R density-path leg")
     args = ap.parse_args()
@@ -221,17 +230,22 @@ def main():
 
     B, N = args.batch, args.points
 
-    def measure(cfg, dtype, B, N, steps, warmup, depth, events_in_window=True):
+    x3_opt = {"0": False, "1": True}.get(args.x3, args.x3)
+
+    def measure(cfg, dtype, B, N, steps, warmup, depth, events_in_window=True, x3=None):
         """events_in_window: HIP events around every launch inside the timed window (the
         headline: the roofline durations come from the same window).  False: the window
         runs clean and the per-kernel durations come from a second, instrumented window
         of the same length (with ~25 launches per step, as MSG has, the events cost ~1/3)."""
-        bb = pn.PointNet2Backbone(cfg, device=dev, seed=0, dtype=dtype, mlp16={"0": False, "1": True}.get(args.mlp16, args.mlp16))
+        bb = pn.PointNet2Backbone(cfg, device=dev, seed=0, dtype=dtype,
+                                  mlp16={"0": False, "1": True}.get(args.mlp16, args.mlp16),
+                                  x3=x3_opt if x3 is None else x3)
         x = torch.from_numpy(unit_frames(B, N, seed=sharding.frame_seed(rank))).to(dev)
         # the streaming executor overlaps batch k+1's SA1 FPS + ball queries (latency-bound,
         # one workgroup per frame) with batch k's MFMA levels; results are identical to forward()
         pipe = pn.StreamingSSG(bb, B, N, depth=depth, side_priority=args.side_priority,
-                               side_cus=args.side_cus, cu_layout=args.cu_layout, fps_group=args.fps_group)
+                               side_cus=args.side_cus, cu_layout=args.cu_layout, fps_group=args.fps_group,
+                               bq_on_main=bool(args.bq_main))
         ref, _ = bb.forward(x)
         outs = pipe.run([x] * max(2, warmup))
         torch.cuda.synchronize(dev)
@@ -249,6 +263,14 @@ def main():
         return elapsed, timers.mean_ms()
 
     elapsed, kern = measure(pn.SSG, "f32", B, N, args.steps, args.warmup, args.depth)
+    fp32_mfma = None
+    if x3_opt and not args.no_fp32_mfma_leg:
+        # the same workload on the native fp32-MFMA kernels (clean window), for comparison
+        el_f, k_f = measure(pn.SSG, "f32", B, N, args.steps, args.warmup, args.depth, events_in_window=False,
+                            x3=False)
+        fp32_mfma = {"value": sharding.aggregate_rate(B * N * args.steps, world, el_f) / 1e6, "unit": "M points/s",
+                     "ms_per_step": el_f / args.steps * 1e3,
+                     "sa2_group_mlp_ms": k_f.get("sa2_group_mlp"), "sa1_group_mlp_ms": k_f.get("sa1_group_mlp")}
     extras = {}
     if not args.no_extras:
         # the other BASELINE.json configs, measured the same way (not the headline metric)
@@ -267,7 +289,8 @@ def main():
     # groups in flight; FPS is one workgroup per frame, latency-bound: read as us/step) and
     # the main stream's full-chip kernels.  The roofline is reported for the kernel that
     # dominates the main chain's device time; the chain lengths say which chain bounds a step.
-    side = ("sa1_fps", "sa1_ball_query")  # issued on the side streams, overlapped with the rest
+    # issued on the side streams, overlapped with the rest
+    side = ("sa1_fps",) if args.bq_main else ("sa1_fps", "sa1_ball_query")
     main = {k: v for k, v in kern.items() if k not in side}
     side_ms = sum(kern.get(k, 0) for k in side) / args.depth
     dom = max(main, key=lambda k: main[k])
@@ -280,12 +303,16 @@ def main():
         per_launch = per_frame * B * args.fps_group  # one launch covers a group of batches
         avg_s = kern[name] / 1e3
         if bound == "mfma":
-            a, p, u = per_launch / avg_s / 1e12, FP32_MFMA_PEAK_TFLOPS, "TFLOP/s"
+            x3k = x3_opt and name in ("sa1_group_mlp", "sa2_group_mlp")
+            a, p, u = per_launch / avg_s / 1e12, X3_PEAK_TFLOPS if x3k else FP32_MFMA_PEAK_TFLOPS, "TFLOP/s"
         else:
             a, p, u = per_launch / avg_s / 1e9, HBM_PEAK_GBS, "GB/s"
         return {"kernel": name, "bound": bound, "achieved": a, "peak": p, "unit": u, "frac": a / p,
                 "traffic": traffic.get(name), "traffic_unit": "bytes per launch (PMC FETCH_SIZE*2 + WRITE_SIZE)",
-                "work_per_launch": per_launch, "avg_launch_ms": kern[name]}
+                "work_per_launch": per_launch, "avg_launch_ms": kern[name],
+                "peak_basis": ("bf16 MFMA dense peak / 3 (x3: 3 bf16 products per fp32 product)"
+                               if bound == "mfma" and p == X3_PEAK_TFLOPS else
+                               "fp32 MFMA peak" if bound == "mfma" else "HBM peak")}
 
     value = sharding.aggregate_rate(B * N * args.steps, world, elapsed) / 1e6
     if rank == 0:
@@ -293,7 +320,13 @@ def main():
             "metric": "M points/sec through SetAbstraction, 65k-pt frames; 1->8 GPU scaling",
             "value": value, "unit": "M points/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "f32" + (" (SA layers 2-3 as split-bf16 x3 MFMA products, fp32 accumulation)" if x3_opt else ""),
+            "precision": ("fp32 inputs/weights/outputs; SA layers 2-3: each fp32 operand split exactly into bf16 "
+                          "hi+lo, products ah*bh + ah*bl + al*bh accumulated in fp32 (<= ~2^-15 per product); "
+                          "features within the 1e-4 rel contract of the fp32 oracle "
+                          "(tests/test_gpu_tier_n.py::test_group_mlp_x3, test_backbone_vs_oracle)") if x3_opt else
+                         "fp32 MFMA (v_mfma_f32_*_f32)",
             "data": "synthetic: uniform [-1,1]^3 float32 frames (seeded per rank), random-init SSG weights",
             "config": {"workload": "PointNet++ SSG encoder (SA1 N/16 r0.2 ns32 [64,64,128]; "
                                    "SA2 N/64 r0.4 ns64 [128,128,256]; group_all [256,512,1024]) fp32",
@@ -303,7 +336,9 @@ def main():
             "roofline_all": {k: roof(k) for k in kern if k in work},
             "kernel_ms": kern,
             "pipeline": {"executor": "pointnet2.StreamingSSG", "side_streams": args.depth,
-                         "batches_per_group": args.fps_group, **chains},
+                         "batches_per_group": args.fps_group, "ball_query_stream": "main" if args.bq_main else "side",
+                         **chains},
+            "fp32_mfma_kernels": fp32_mfma,
             "other_configs": extras,
             "density_path": density,
             "variant_path": variant,

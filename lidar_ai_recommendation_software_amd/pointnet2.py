@@ -545,13 +545,15 @@ class StreamingSSG:
     per frame, so results are identical to ``PointNet2Backbone.forward`` per batch.
     """
 
-    def __init__(self, backbone, batch, n, depth=1, side_priority=0, side_cus=0, cu_layout="xcd", fps_group=1):
+    def __init__(self, backbone, batch, n, depth=1, side_priority=0, side_cus=0, cu_layout="xcd", fps_group=1,
+                 bq_on_main=False):
         """side_cus > 0: the SA1 FPS / ball-query streams run on `side_cus` CUs and the
         main stream on the rest (CU-masked HIP streams; measured slower).
         cu_layout "xcd" takes side_cus/8 CUs of each of the 8 XCDs (mask bit = 32*xcd + cu),
         "low" the lowest-numbered CUs."""
         self.bb = backbone
         self.B, self.N, self.depth, self.G = batch, n, depth, max(1, int(fps_group))
+        self.bq_on_main = bool(bq_on_main)  # level-0 ball queries on the main stream instead
         dev = backbone.device
         lvl0 = backbone.levels[0]
         self.M1 = max(1, n // lvl0["div"])
@@ -620,7 +622,7 @@ class StreamingSSG:
                   first_zero=self.fz[slot][:g], slot=1 + k % self.depth, out_idx=self.idx[slot][:g],
                   out_xyz=self.cxyz[slot][:g])
             lvl0 = self.bb.levels[0]
-            for bi_, br in enumerate(lvl0["branches"]):
+            for bi_, br in enumerate([] if self.bq_on_main else lvl0["branches"]):
                 tag = "sa1" + (f"_b{bi_}" if len(lvl0["branches"]) > 1 else "")
                 _call(self.bb.timers, f"{tag}_ball_query", ball_query, br["r"], br["ns"], x, self.cxyz[slot][:g],
                       out=self.gidx[slot][bi_][:g], slot=1 + k % self.depth)
@@ -634,7 +636,7 @@ class StreamingSSG:
         B, g = self.B, len(xs) * self.B
         x = self.stage[slot][:g] if self.G > 1 else xs[0]
         out = self.bb.forward_from_sa1_fps(x, self.idx[slot][:g], self.cxyz[slot][:g], self.fz[slot][:g],
-                                           [gi[:g] for gi in self.gidx[slot]])
+                                           None if self.bq_on_main else [gi[:g] for gi in self.gidx[slot]])
         self.slot_free[slot].record(main)
         return list(out.split(B)) if len(xs) > 1 else [out]
 

@@ -42,10 +42,10 @@ def label(name, grid):
     if "ball_query_kernel" in name:
         return {1048576: "sa1_ball_query", 262144: "sa2_ball_query"}.get(grid)
     if any(k in name for k in ("sa_group_mlp_kernel<0, 64, 64, 128, 32", "sa_pre_lds_kernel<64, 64, 128, 32, true",
-                                "sa16_kernel<64, 64, 128, 32, true")):
+                                "sa16_kernel<64, 64, 128, 32, true", "sa_x3_kernel<64, 64, 128, 32, true")):
         return "sa1_group_mlp"
     if any(k in name for k in ("sa_group_mlp_kernel<128, 128, 128, 256, 64", "sa_pre_lds_kernel<128, 128, 256, 64",
-                                "sa16_kernel<128, 128, 256, 64, false")):
+                                "sa16_kernel<128, 128, 256, 64, false", "sa_x3_kernel<128, 128, 256, 64, false")):
         return "sa2_group_mlp"
     if "dense_relu_kernel" in name:
         return {65536: "sa2_layer1_points", 131072: "sa3_dense1", 262144: "dense_262144",

@@ -14,11 +14,12 @@ dev = torch.device("cuda:0")
 x3 = {"0": False, "1": True}.get(sys.argv[9], sys.argv[9]) if len(sys.argv) > 9 else False
 bb = pn.PointNet2Backbone(pn.CONFIGS[cfg_name], device=dev, seed=0, dtype=dtype, mlp16=mlp16, x3=x3)
 x = torch.from_numpy(unit_frames(B, N, 0)).to(dev)
-pipe = pn.StreamingSSG(bb, B, N, depth=depth, fps_group=group)
+bqm = len(sys.argv) > 10 and sys.argv[10] == "1"
+pipe = pn.StreamingSSG(bb, B, N, depth=depth, fps_group=group, bq_on_main=bqm)
 pipe.run([x] * 3)
 torch.cuda.synchronize()
 t0 = time.perf_counter()
 pipe.run([x] * steps)
 torch.cuda.synchronize()
 dt = time.perf_counter() - t0
-print(f"{cfg_name} {dtype} B={B} N={N} depth={depth} group={group} mlp16={mlp16} x3={x3}: {dt / steps * 1e3:.2f} ms/step, {B * N * steps / dt / 1e6:.1f} M pts/s", flush=True)
+print(f"{cfg_name} {dtype} B={B} N={N} depth={depth} group={group} mlp16={mlp16} x3={x3} bq_main={int(bqm)}: {dt / steps * 1e3:.2f} ms/step, {B * N * steps / dt / 1e6:.1f} M pts/s", flush=True)

@@ -133,6 +133,13 @@ int lidar_dense_f32(lidar_handle *h, const float *x, int64_t rows, int32_t k, co
                     const float *bias, int32_t cout, int32_t relu_on, int32_t pool_rows, float *y,
                     void *stream);
 
+/* lidar_dense_f32 on the bf16 matrix cores with fp32 arithmetic: operands split exactly into
+ * bf16 hi + lo, products ah*bh + ah*bl + al*bh accumulated in fp32 (v_mfma_f32_32x32x16_bf16;
+ * <= ~2^-15 per product).  Same shapes, epilogue and fused max-pool as lidar_dense_f32. */
+int lidar_dense_x3_f32(lidar_handle *h, const float *x, int64_t rows, int32_t k, const float *w,
+                       const float *bias, int32_t cout, int32_t relu_on, int32_t pool_rows, float *y,
+                       void *stream);
+
 /* lidar_sa_group_mlp_f32 with layer 1 applied per point beforehand: p (batch*n, p_stride)
  * = [f, x] W1 + b1 for every point of the level, q (batch*m, p_stride) = centre W1_xyz
  * (both via lidar_dense_f32, relu_on = 0, columns >= c1 ignored); a grouped row's layer 1

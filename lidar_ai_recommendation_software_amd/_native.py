@@ -54,6 +54,7 @@ SIGNATURES = {
     "lidar_mlp_pack_bf16": [I32, I32, I32, I32, P, P, P, P, P, P, P],
     "lidar_dense_relu_f32": [P, P, I64, I32, P, P, I32, I32, P, P],
     "lidar_dense_f32": [P, P, I64, I32, P, P, I32, I32, I32, P, P],
+    "lidar_dense_x3_f32": [P, P, I64, I32, P, P, I32, I32, I32, P, P],
     "lidar_mlp_packed_size16": [I32, I32, I32, I32],
     "lidar_mlp_pack16_f32": [I32, I32, I32, I32, P, P, P, P, P, P, P],
     "lidar_sa_group_mlp16_f32": [P, I32, P, I64, P, P, I64, I64, I64, I32, I32, I32, I32, P, P, I64, I64, P],

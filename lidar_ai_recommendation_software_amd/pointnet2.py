@@ -265,7 +265,7 @@ def layer1_weights(layer, cfeat, to_dev):
     return {"w1": to_dev(w1p), "b1": to_dev(bp), "wq": to_dev(wq), "zero": to_dev(np.zeros(cp, np.float32))}
 
 
-def layer1_per_point(x_rows, xyz, cfeat, new_xyz, branches):
+def layer1_per_point(x_rows, xyz, cfeat, new_xyz, branches, x3=False):
     """Layer 1 of every branch of a level, per point instead of per grouped row.
 
     x_rows: (R, kp) padded rows [f (cfeat), x, y, z, 0...] of the level's B*N points
@@ -285,26 +285,29 @@ def layer1_per_point(x_rows, xyz, cfeat, new_xyz, branches):
     out = []
     for br in branches:
         pre = br["pre"]
-        P = dense(x_rows, pre["w1"], pre["b1"], relu=False)
-        Q = dense(cpad, pre["wq"], pre["zero"], relu=False)
+        P = dense(x_rows, pre["w1"], pre["b1"], relu=False, x3=x3)
+        Q = dense(cpad, pre["wq"], pre["zero"], relu=False, x3=x3)
         out.append((P, Q))
     return out
 
 
-def dense(x, w, b, relu=True, pool_rows=0, out=None):
-    """x (rows, k) @ w (k, cout) + b [-> ReLU] [-> max over runs of pool_rows rows]."""
+def dense(x, w, b, relu=True, pool_rows=0, out=None, x3=False):
+    """x (rows, k) @ w (k, cout) + b [-> ReLU] [-> max over runs of pool_rows rows].
+    x3: on the split-bf16 GEMM (lidar_dense_x3_f32; fp32 arithmetic within 1e-4)."""
     rows, k = x.shape
     cout = w.shape[1]
     if out is None:
         shape = (rows // pool_rows, cout) if pool_rows else (rows, cout)
         out = (torch.zeros if pool_rows else torch.empty)(shape, dtype=torch.float32, device=x.device)
     _dev_check(x, w, b, out)
-    nat.call("lidar_dense_f32", nat.handle(x.device.index), nat.ptr(x), rows, k, nat.ptr(w),
-             nat.ptr(b), cout, 1 if relu else 0, pool_rows, nat.ptr(out), nat.stream_ptr())
+    nat.call("lidar_dense_x3_f32" if x3 else "lidar_dense_f32", nat.handle(x.device.index), nat.ptr(x), rows, k,
+             nat.ptr(w), nat.ptr(b), cout, 1 if relu else 0, pool_rows, nat.ptr(out), nat.stream_ptr())
     return out
 
 
-def dense_relu(x, w, b, pool_rows=0, out=None):
+def dense_relu(x, w, b, pool_rows=0, out=None, x3=False):
+    if x3:
+        return dense(x, w, b, True, pool_rows, out, x3=True)
     rows, k = x.shape
     cout = w.shape[1]
     if out is None:
@@ -401,6 +404,8 @@ class PointNet2Backbone:
                 self.levels.append(entry)
                 cfeat = sum(w[-1] for w in lvl["mlps"])
         self.out_channels = cfeat
+        # x3 on: the dense layers (per-point layer 1, group_all) on the split-bf16 GEMM too
+        self.x3_dense = bool(x3) and not self.bf16
         self.timers = None  # set to a _Timers() to time every launch
 
     def forward_from_sa1_fps(self, xyz, idx1, new_xyz1, fz1, gidx1=None):
@@ -437,7 +442,7 @@ class PointNet2Backbone:
             pq = None
             if lvl.get("pre"):
                 pq = _call(self.timers, f"sa{li + 1}_layer1_points", layer1_per_point, rows, xyz, lvl["cfeat"],
-                           new_xyz, lvl["branches"])
+                           new_xyz, lvl["branches"], x3=self.x3_dense)
             off = 0
             for bi_, br in enumerate(lvl["branches"]):
                 tag = f"sa{li + 1}" + (f"_b{bi_}" if len(lvl["branches"]) > 1 else "")
@@ -488,10 +493,11 @@ class PointNet2Backbone:
             x2 = x.view(B, M, kp)[:, sel].reshape(B * mp, kp).contiguous()
             M, rows = mp, B * mp
         t = self.timers
-        h1 = _call(t, "sa3_dense1", dense_relu, x2, lvl["w"][0], lvl["b"][0])
-        h2 = _call(t, "sa3_dense2", dense_relu, h1, lvl["w"][1], lvl["b"][1])
+        h1 = _call(t, "sa3_dense1", dense_relu, x2, lvl["w"][0], lvl["b"][0], x3=self.x3_dense)
+        h2 = _call(t, "sa3_dense2", dense_relu, h1, lvl["w"][1], lvl["b"][1], x3=self.x3_dense)
         out = torch.zeros((rows // M, lvl["w"][2].shape[1]), dtype=torch.float32, device=x.device)
-        return _call(t, "sa3_dense3_pool", dense_relu, h2, lvl["w"][2], lvl["b"][2], pool_rows=M, out=out)
+        return _call(t, "sa3_dense3_pool", dense_relu, h2, lvl["w"][2], lvl["b"][2], pool_rows=M, out=out,
+                     x3=self.x3_dense)
 
     __call__ = forward
 

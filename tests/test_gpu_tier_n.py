@@ -215,6 +215,25 @@ def test_dense_no_relu(cuda):
     feat_close(pn.dense(T(x), T(w), T(b), relu=False).cpu().numpy(), x @ w + b, "dense no relu")
 
 
+@pytest.mark.parametrize("rows,k,cout,pool", [(256, 144, 128, 0), (512, 272, 256, 0), (1024, 512, 1024, 512),
+                                              (384, 16, 128, 128)])
+def test_dense_x3(cuda, rows, k, cout, pool):
+    """split-bf16 GEMM vs the fp32 numpy product at the fp32 path's 1e-4 tolerance."""
+    rng = np.random.default_rng(rows + k)
+    x = np.abs(rng.standard_normal((rows, k))).astype(np.float32)
+    w = (rng.standard_normal((k, cout)) / np.sqrt(k)).astype(np.float32)
+    b = rng.standard_normal(cout).astype(np.float32) * 0.1
+    T = lambda a: torch.from_numpy(a).to(cuda)
+    want = x.astype(np.float64) @ w.astype(np.float64) + b
+    feat_close(pn.dense(T(x), T(w), T(b), relu=False, x3=True).cpu().numpy(), want, "dense x3 no relu")
+    want = np.maximum(want, 0)
+    if pool:
+        got = pn.dense_relu(T(x), T(w), T(b), pool_rows=pool, x3=True).cpu().numpy()
+        feat_close(got, want.reshape(rows // pool, pool, cout).max(axis=1), "dense x3 pooled")
+    else:
+        feat_close(pn.dense_relu(T(x), T(w), T(b), x3=True).cpu().numpy(), want, "dense x3 relu")
+
+
 def test_dense_relu_and_pool(cuda):
     rng = np.random.default_rng(1)
     x = rng.standard_normal((512, 272)).astype(np.float32)

@@ -106,7 +106,7 @@ def main(cf, cw, pf, pw, out):
                      "launches": len(fa.get(lab, []))}
     res = {"config": {"workload": "ssg", "points_per_frame": 65536, "frames_per_gpu": 32},
            "source": "rocprofv3 --kernel-trace --pmc FETCH_SIZE | WRITE_SIZE (separate passes) of "
-                     "bench.py --no-extras --no-cpu-baseline --no-density --steps 4 --warmup 1",
+                     "bench.py --no-extras --no-cpu-baseline --no-density --no-fp32-mfma-leg --steps 4 --warmup 1",
            "calibration": cal, "kernels": kern}
     os.makedirs(os.path.dirname(out) or ".", exist_ok=True)
     with open(out, "w") as f:

@@ -333,6 +333,8 @@ def main():
                        "points_per_frame": N, "frames_per_gpu": B, "global_batch_frames": B * world,
                        "parallelism": f"per-frame data parallel x{world} (no collectives)"},
             "roofline": roof(dom),
+            # the north_star's MFMA figure: the grouped MLP (SA2 layers 2-3), whatever dominates
+            "roofline_grouped_mlp": roof("sa2_group_mlp") if "sa2_group_mlp" in kern else None,
             "roofline_all": {k: roof(k) for k in kern if k in work},
             "kernel_ms": kern,
             "pipeline": {"executor": "pointnet2.StreamingSSG", "side_streams": args.depth,

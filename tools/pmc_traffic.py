@@ -33,23 +33,28 @@ def rows(d):
     return list(csv.DictReader(open(f[0])))
 
 
-def label(name, grid):
-    """Kernel label of the SSG stack at B=32, N=65536 (grid = threads).  dense_relu_kernel
-    at 262144 threads is both SA2's per-point layer-1 GEMM and SA3's second layer: the
-    caller splits those by dispatch order (the layer-1 GEMM comes first in every step)."""
+FRAMES_PER_LAUNCH = 64  # bench.py defaults: 32 frames per batch x fps_group 2 per main-stream pass
+
+
+def label(name, grid, F=FRAMES_PER_LAUNCH):
+    """Kernel label of the SSG stack (N = 65536) for F frames per main-stream launch
+    (grid = threads).  The dense GEMMs launch (cout/128) x (rows/128) workgroups of 256:
+    SA2's per-point layer 1 is rows F*4096 x 128 (+ the centre rows F*1024 x 128) and
+    group_all's layers are rows F*1024 x 256 / 512 / 1024, so the layer-1 GEMM and SA3's
+    second layer share a grid; the caller splits those by dispatch order (layer 1 first)."""
     if "fps_bucket_kernel" in name:
         return "fps"  # split into sa1/sa2 by duration below
     if "ball_query_kernel" in name:
-        return {1048576: "sa1_ball_query", 262144: "sa2_ball_query"}.get(grid)
+        return {F * 4096 * 8: "sa1_ball_query", F * 1024 * 8: "sa2_ball_query"}.get(grid)
     if any(k in name for k in ("sa_group_mlp_kernel<0, 64, 64, 128, 32", "sa_pre_lds_kernel<64, 64, 128, 32, true",
                                 "sa16_kernel<64, 64, 128, 32, true", "sa_x3_kernel<64, 64, 128, 32, true")):
         return "sa1_group_mlp"
     if any(k in name for k in ("sa_group_mlp_kernel<128, 128, 128, 256, 64", "sa_pre_lds_kernel<128, 128, 256, 64",
                                 "sa16_kernel<128, 128, 256, 64, false", "sa_x3_kernel<128, 128, 256, 64, false")):
         return "sa2_group_mlp"
-    if "dense_relu_kernel" in name:
-        return {65536: "sa2_layer1_points", 131072: "sa3_dense1", 262144: "dense_262144",
-                524288: "sa3_dense3_pool"}.get(grid)
+    if "dense_relu_kernel" in name or "dense_x3_kernel" in name:
+        return {F * 4096 * 2: "dense_shared", F * 1024 * 2: "sa2_layer1_points", F * 1024 * 4: "sa3_dense1",
+                F * 1024 * 16: "sa3_dense3_pool"}.get(grid)
     if "concat_xyz_pad" in name:
         return "concat"
     return None
@@ -58,7 +63,7 @@ def label(name, grid):
 def per_label(rs, counter):
     acc = defaultdict(list)
     fps = []
-    n262 = 0
+    nsh = 0
     for r in sorted(rs, key=lambda r: int(r["Dispatch_Id"])):
         if r["Counter_Name"] != counter:
             continue
@@ -66,9 +71,9 @@ def per_label(rs, counter):
         lab = label(r["Kernel_Name"], int(r["Grid_Size"]))
         if lab == "fps":
             fps.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"]), v))
-        elif lab == "dense_262144":
-            acc["sa2_layer1_points" if n262 % 2 == 0 else "sa3_dense2"].append(v)
-            n262 += 1
+        elif lab == "dense_shared":
+            acc["sa2_layer1_points" if nsh % 2 == 0 else "sa3_dense2"].append(v)
+            nsh += 1
         elif lab:
             acc[lab].append(v)
     if fps:  # SA1 FPS (65536 -> 4096, long) vs SA2's nested-prefix FPS (short)
@@ -76,11 +81,11 @@ def per_label(rs, counter):
         half = len(fps) // 2
         acc["sa2_fps"] = [v for _, v in fps[:half]]
         acc["sa1_fps"] = [v for _, v in fps[half:]]
-    # sa2_layer1_points = its two GEMMs per launch group: report the per-step sum
+    # sa2_layer1_points = its two GEMMs (point rows, centre rows) per pass: report their sum
     if "sa2_layer1_points" in acc:
         v = acc["sa2_layer1_points"]
-        steps = max(1, len(v) // 2)
-        acc["sa2_layer1_points"] = [sum(v) / steps]
+        passes = max(1, len(v) // 2)
+        acc["sa2_layer1_points"] = [sum(v) / passes]
     return acc
 
 
@@ -104,7 +109,8 @@ def main(cf, cw, pf, pw, out):
         w = sum(wa.get(lab, [0])) / max(1, len(wa.get(lab, [])))
         kern[lab] = {"fetch_bytes": f, "write_bytes": w, "traffic_bytes": f + w,
                      "launches": len(fa.get(lab, []))}
-    res = {"config": {"workload": "ssg", "points_per_frame": 65536, "frames_per_gpu": 32},
+    res = {"config": {"workload": "ssg", "points_per_frame": 65536, "frames_per_gpu": 32,
+                      "frames_per_launch": FRAMES_PER_LAUNCH},
            "source": "rocprofv3 --kernel-trace --pmc FETCH_SIZE | WRITE_SIZE (separate passes) of "
                      "bench.py --no-extras --no-cpu-baseline --no-density --no-fp32-mfma-leg --steps 4 --warmup 1",
            "calibration": cal, "kernels": kern}

@@ -347,7 +347,7 @@ class PointNet2Backbone:
     """SSG / MSG PointNet++ encoder on liblidar_amd.  ``forward(xyz)`` -> global feature
     (B, C_last) plus the per-level (new_xyz, features, fps_idx)."""
 
-    def __init__(self, cfg=SSG, weights=None, device="cuda", seed=0, dtype="f32", pre_layer1=True, mlp16="pre", x3=False):
+    def __init__(self, cfg=SSG, weights=None, device="cuda", seed=0, dtype="f32", pre_layer1=True, mlp16="pre", x3=True):
         """dtype "bf16": the SA branches run on bf16 MFMA (inputs/activations/weights rounded
         to bf16, fp32 accumulation; BASELINE configs[4]); group_all stays fp32.
         pre_layer1 (fp32, levels with point features): layer 1 runs per point as a GEMM

@@ -59,6 +59,8 @@ def ssg_kernel_work(n):
         "sa1_fps": ("hbm", 12 * n + 16 * m1),
         "sa2_fps": ("hbm", 12 * m1 + 16 * m2),
         "sa1_ball_query": ("hbm", 12 * (n + m1) + 4 * m1 * 32),
+        # the grid ball query's binning (side stream): read xyz, write (x, y, z, index) + slot table
+        "sa1_bq_bin": ("hbm", 12 * n + 16 * n + 4 * 16385),
         "sa2_ball_query": ("hbm", 12 * (m1 + m2) + 4 * m2 * 64),
     }
 
@@ -290,7 +292,7 @@ def main():
     # the main stream's full-chip kernels.  The roofline is reported for the kernel that
     # dominates the main chain's device time; the chain lengths say which chain bounds a step.
     # issued on the side streams, overlapped with the rest
-    side = ("sa1_fps",) if args.bq_main else ("sa1_fps", "sa1_ball_query")
+    side = ("sa1_fps", "sa1_bq_bin") if args.bq_main else ("sa1_fps", "sa1_ball_query")
     main = {k: v for k, v in kern.items() if k not in side}
     side_ms = sum(kern.get(k, 0) for k in side) / args.depth
     dom = max(main, key=lambda k: main[k])

@@ -82,6 +82,25 @@ int lidar_ball_query_f32(lidar_handle *h, const float *xyz, const float *centres
                          int64_t n, int64_t m, float radius, int32_t nsample, int32_t *idx,
                          void *stream);
 
+/* the same query with an explicit kernel: mode 0 = auto (grid for n >= 1024), 1 = the
+ * index-order scan, 2 = the (index window, cell) grid.  Results are identical. */
+int lidar_ball_query_mode_f32(lidar_handle *h, const float *xyz, const float *centres,
+                              int64_t batch, int64_t n, int64_t m, float radius, int32_t nsample,
+                              int32_t mode, int32_t *idx, void *stream);
+
+/* the grid path in two steps, so the binning of a frame (it depends only on xyz) can run
+ * ahead on another stream: lidar_ball_query_bin_f32 writes the grid of every frame into a
+ * caller-owned device buffer of lidar_ball_query_grid_bytes(batch, n) bytes;
+ * lidar_ball_query_binned_f32 answers queries from it.  A grid binned for radius r answers
+ * any radius exactly (radii above r fall back to scanning whole windows); nsample only tunes
+ * the window size. */
+uint64_t lidar_ball_query_grid_bytes(int64_t batch, int64_t n);
+int lidar_ball_query_bin_f32(lidar_handle *h, const float *xyz, int64_t batch, int64_t n, float radius,
+                             int32_t nsample, void *grid, void *stream);
+int lidar_ball_query_binned_f32(lidar_handle *h, const float *xyz, const void *grid, const float *centres,
+                                int64_t batch, int64_t n, int64_t m, float radius, int32_t nsample,
+                                int32_t *idx, void *stream);
+
 /* grouped shared MLP (3 layers, BN folded, ReLU) + max-pool over nsample for one SA
  * branch, fused with the grouping gather:
  *   row (b, c, s) = [xyz[b, idx[b,c,s]] - centres[b,c], feats[b, idx[b,c,s], 0:cfeat]]

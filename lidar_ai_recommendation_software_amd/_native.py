@@ -44,6 +44,10 @@ SIGNATURES = {
     "lidar_version": [],
     "lidar_fps_f32": [P, P, I64, I64, I64, P, P, P, P, P],
     "lidar_ball_query_f32": [P, P, P, I64, I64, I64, F32, I32, P, P],
+    "lidar_ball_query_mode_f32": [P, P, P, I64, I64, I64, F32, I32, I32, P, P],
+    "lidar_ball_query_grid_bytes": [I64, I64],
+    "lidar_ball_query_bin_f32": [P, P, I64, I64, F32, I32, P, P],
+    "lidar_ball_query_binned_f32": [P, P, P, P, I64, I64, I64, F32, I32, P, P],
     "lidar_sa_group_mlp_f32": [P, P, P, I64, P, P, I64, I64, I64, I32, I32, I32, I32, I32, P, P,
                                I64, I64, P],
     "lidar_mlp_packed_size": [I32, I32, I32, I32],
@@ -87,7 +91,8 @@ SIGNATURES = {
 }
 _RESTYPES = {"lidar_last_error": ctypes.c_char_p, "lidar_mlp_packed_size": I64,
              "lidar_mlp_packed_size_bf16": I64,
-             "lidar_mlp_packed_size16": I64, "lidar_mlp_packed_size_x3": I64}
+             "lidar_mlp_packed_size16": I64, "lidar_mlp_packed_size_x3": I64,
+             "lidar_ball_query_grid_bytes": ctypes.c_uint64}
 
 
 def load_library(path=LIB_PATH):

@@ -4,11 +4,25 @@
 // point indices in ascending order with d < r*r (fp32, d = (dx*dx+dy*dy)+dz*dz, one
 // rounding per op), unused slots repeat the first hit, no hit -> 0.
 //
-// One wavefront serves 8 centres of a frame: it scans the frame in index order, 128
-// points per step (two coalesced 64-point chunks, the next pair prefetched), tests them
-// against all 8 centres (the loads are shared 8 ways), __ballot collects each centre's hits, popcount ranks them,
-// and the scan stops once every centre has nsample hits — for uniform frames at
-// r = 0.2 that is ~12 % of the frame.
+// Two kernels implement it:
+//
+// * Grid (default for n >= kGridMinN).  `bq_bin_kernel` (one workgroup per frame) bins
+//   the frame by (index window, cell): windows are 2^w consecutive point indices, cells
+//   a uniform grid of side s >= r * (1 + 2^-8) over the frame's finite bbox, so every hit
+//   of a centre lies in the 3x3x3 cells around the centre's cell (the 2^-8 margin covers
+//   fp32 rounding of the cell coordinates, see bin_params).  A counting sort in LDS gives
+//   per (window, cell) slot a contiguous range of (x, y, z, index) float4s.
+//   `bq_grid_kernel` (one wavefront per centre) walks the windows in order: for each it
+//   gathers the <= 9 z-runs of candidate cells (contiguous slots), tests the candidates,
+//   collects the hits in LDS and ranks them by index (hits of window w all precede those
+//   of window w+1), and stops after the window where nsample hits are reached.  For a
+//   uniform 65 536-point frame at r = 0.2 that is ~3 windows of ~110 candidates instead of
+//   the ~8 000 points the index-order scan touches.  A window with more than kCap
+//   candidates is scanned in index order (the brute loop below) instead.
+// * Brute (small frames): one wavefront serves 8 centres and scans the frame in index
+//   order, 128 points per step (two coalesced 64-point chunks, the next pair prefetched),
+//   __ballot collects hits, popcount ranks them, and the scan stops once every centre has
+//   nsample hits.
 #include "common.hpp"
 
 namespace {
@@ -89,26 +103,426 @@ __global__ __launch_bounds__(256) void ball_query_kernel(const float *__restrict
     }
 }
 
+
+// ------------------------------------------------------------------ grid ball query
+constexpr int kTab = 16384;     // (window, cell) slots per frame: one int each in LDS (64 KiB)
+constexpr int kCap = 512;       // candidates per window a wavefront ranks in LDS
+constexpr int kGridMinN = 1024;  // below this the index-order scan is as cheap
+
+struct BqGrid {  // per frame, written by bq_bin_kernel
+    float minx, miny, minz, inv_s;
+    int dx, dy, dz, ncell;  // cells per axis; ncell = dx * dy * dz
+    int win_shift, nwin;    // windows of 2^win_shift consecutive indices
+    int pad[2];
+};
+
+__host__ __device__ constexpr uint64_t grid_frame_bytes(int64_t n)
+{
+    return 64 + (uint64_t)(kTab + 64) * 4 + (uint64_t)n * 16;
+}
+
+// cell coordinate of v on one axis; centres may lie outside the bbox (clamped to
+// [-2, d+1] before the conversion, NaN -> -2), points inside land in [0, d-1]
+__device__ __forceinline__ int cell_of(float v, float lo, float inv_s, int d)
+{
+    float u = __fmul_rn(__fsub_rn(v, lo), inv_s);
+    u = fminf(fmaxf(u, -2.0f), (float)d + 1.0f);
+    return (int)floorf(u);
+}
+
+__device__ __forceinline__ int point_slot(float x, float y, float z, int k, const BqGrid &g)
+{
+    const int ix = min(max(cell_of(x, g.minx, g.inv_s, g.dx), 0), g.dx - 1);
+    const int iy = min(max(cell_of(y, g.miny, g.inv_s, g.dy), 0), g.dy - 1);
+    const int iz = min(max(cell_of(z, g.minz, g.inv_s, g.dz), 0), g.dz - 1);
+    return (k >> g.win_shift) * g.ncell + (ix * g.dy + iy) * g.dz + iz;
+}
+
+// Grid parameters of one frame (thread 0 of bq_bin_kernel).
+//  * bbox over finite coordinates only: a point with an inf/NaN coordinate is never a hit
+//    (its distance is inf or NaN), so where it is binned does not matter.
+//  * s >= r (1 + 2^-8): a hit has |p - c| < r (1 + 2^-23) per axis (d < r2 in rounded
+//    arithmetic), so |u_p - u_c| < (1 - 2^-8) + the rounding of u = (v - lo) * inv_s,
+//    <= 3 * 2^-24 * 1024 (at most 1024 cells per axis): the cells differ by at most 1.
+//  * windows: about ns / 2 expected hits per window for a uniform frame, <= 64 windows.
+__device__ BqGrid bin_params(const float mn[3], const float mx[3], int n, float r, int ns)
+{
+    BqGrid g;
+    float ext[3];
+    for (int a = 0; a < 3; ++a) {
+        const bool none = !(mn[a] <= mx[a]);
+        const float lo = none ? 0.f : mn[a];
+        float e = none ? 0.f : __fsub_rn(mx[a], lo);
+        if (!(e <= 3.0e38f)) e = 3.0e38f;  // overflowed extent
+        (&g.minx)[a] = lo;
+        ext[a] = e;
+    }
+    const float emax = fmaxf(ext[0], fmaxf(ext[1], ext[2]));
+    const double rr = (r > 0.f && r < 1e30f) ? (double)r : 0.0;
+    double vol = 1.0;
+    for (int a = 0; a < 3; ++a) vol *= fmax((double)ext[a], 2.0 * rr);
+    const double hits = vol > 0.0 ? n * (4.18879020478639 * rr * rr * rr) / vol : (double)n;
+    const double want = fmin(64.0, fmax(1.0, 2.0 * hits / (double)max(ns, 1)));
+    int shift = 6;
+    while (shift < 30 && ((int64_t)n >> shift) > 64) ++shift;                      // <= 64 windows
+    while (shift < 30 && (double)(1ll << shift) * want < (double)n) ++shift;       // ~want windows
+    g.win_shift = shift;
+    g.nwin = (int)(((int64_t)n + (1ll << shift) - 1) >> shift);
+    const int cap = kTab / g.nwin;
+    float s = fmaxf(fmaxf(__fmul_rn(r, 1.0f + 1.0f / 256.0f), emax / 1023.0f), 1e-30f);
+    if (!(s <= 3.0e38f)) s = 3.0e38f;
+    int d[3];
+    for (int it = 0; it < 200; ++it) {
+        const float inv = 1.0f / s;
+        int64_t prod = 1;
+        for (int a = 0; a < 3; ++a) {
+            d[a] = min(1024, (int)floorf(__fmul_rn(ext[a], inv)) + 1);
+            prod *= d[a];
+        }
+        if (prod <= cap) {
+            g.inv_s = inv;
+            break;
+        }
+        s = __fmul_rn(s, 1.25f);
+    }
+    g.dx = d[0];
+    g.dy = d[1];
+    g.dz = d[2];
+    g.ncell = d[0] * d[1] * d[2];
+    g.pad[0] = g.pad[1] = 0;
+    return g;
+}
+
+// one 1024-thread workgroup per frame: finite bbox -> grid -> counting sort by
+// (window, cell) into (x, y, z, index) float4s; tab[slot] = first position of the slot
+__global__ __launch_bounds__(1024) void bq_bin_kernel(const float *__restrict__ xyz, int n, float r,
+                                                      int ns, char *__restrict__ grid_ws)
+{
+    __shared__ int cnt[kTab];
+    __shared__ float red[6][16];
+    __shared__ int wsum[16];
+    __shared__ BqGrid gs;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int64_t b = blockIdx.x;
+    const float *p = xyz + b * (int64_t)n * 3;
+    char *fw = grid_ws + b * grid_frame_bytes(n);
+    BqGrid *gout = reinterpret_cast<BqGrid *>(fw);
+    int *tab = reinterpret_cast<int *>(fw + 64);
+    float4 *sorted = reinterpret_cast<float4 *>(fw + 64 + (kTab + 64) * 4);
+
+    float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int k = tid; k < n; k += 1024) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            const float v = p[3 * (int64_t)k + a];
+            if (fabsf(v) <= 3.4e38f) {  // finite
+                mn[a] = fminf(mn[a], v);
+                mx[a] = fmaxf(mx[a], v);
+            }
+        }
+    }
+    for (int i = tid; i < kTab; i += 1024) cnt[i] = 0;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        mn[a] = lidar::wave_min_f(mn[a]);
+        mx[a] = lidar::wave_max_f(mx[a]);
+    }
+    if (lane == 0)
+        for (int a = 0; a < 3; ++a) {
+            red[a][wid] = mn[a];
+            red[3 + a][wid] = mx[a];
+        }
+    __syncthreads();
+    if (tid == 0) {
+        float a_mn[3], a_mx[3];
+        for (int a = 0; a < 3; ++a) {
+            a_mn[a] = red[a][0];
+            a_mx[a] = red[3 + a][0];
+            for (int w = 1; w < 16; ++w) {
+                a_mn[a] = fminf(a_mn[a], red[a][w]);
+                a_mx[a] = fmaxf(a_mx[a], red[3 + a][w]);
+            }
+        }
+        gs = bin_params(a_mn, a_mx, n, r, ns);
+        *gout = gs;
+    }
+    __syncthreads();
+    const BqGrid g = gs;
+    for (int k = tid; k < n; k += 1024) {
+        const float *q = p + 3 * (int64_t)k;
+        atomicAdd(&cnt[point_slot(q[0], q[1], q[2], k, g)], 1);
+    }
+    __syncthreads();
+    // exclusive scan of the kTab counters: 16 per thread
+    int loc[16], sum = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        loc[j] = cnt[tid * 16 + j];
+        sum += loc[j];
+    }
+    int incl = sum;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int v = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += v;
+    }
+    if (lane == 63) wsum[wid] = incl;
+    __syncthreads();
+    int base = incl - sum;
+    for (int w = 0; w < wid; ++w) base += wsum[w];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const int slot = tid * 16 + j;
+        cnt[slot] = base;
+        tab[slot] = base;
+        base += loc[j];
+    }
+    if (tid == 1023) tab[kTab] = base;  // == n
+    __syncthreads();
+    for (int k = tid; k < n; k += 1024) {
+        const float *q = p + 3 * (int64_t)k;
+        const float x = q[0], y = q[1], z = q[2];
+        const int pos = atomicAdd(&cnt[point_slot(x, y, z, k, g)], 1);
+        sorted[pos] = make_float4(x, y, z, __int_as_float(k));
+    }
+}
+
+// index-order scan of points [lo, hi) for one centre (a window with too many candidates)
+__device__ __forceinline__ void scan_range(const float *__restrict__ p, int lo, int hi, float cx, float cy,
+                                           float cz, float r2, int ns, int lane, uint64_t below, int &cnt,
+                                           int &first, int32_t *__restrict__ o)
+{
+    for (int k0 = lo; k0 < hi && cnt < ns; k0 += 64) {
+        const int k = k0 + lane;
+        bool hit = false;
+        if (k < hi) hit = lidar::dist2f(p[3 * k], p[3 * k + 1], p[3 * k + 2], cx, cy, cz) < r2;
+        const uint64_t mk = __ballot(hit);
+        if (mk) {
+            if (first < 0) first = k0 + __ffsll((unsigned long long)mk) - 1;
+            const int rk = cnt + __popcll(mk & below);
+            if (hit && rk < ns) o[rk] = k;
+            cnt += __popcll(mk);
+        }
+    }
+}
+
+__device__ __forceinline__ void lds_wave_sync()
+{
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// one wavefront per centre; blocks are laid out so that the blocks of a contiguous range of
+// frames share an XCD (block b and b + 8 share one): a frame's grid stays in one L2
+__global__ __launch_bounds__(256) void bq_grid_kernel(const float *__restrict__ xyz,
+                                                      const char *__restrict__ grid_ws,
+                                                      const float *__restrict__ centres, int n, int m,
+                                                      int64_t total, int64_t per_xcd, float r, float r2, int ns,
+                                                      int32_t *__restrict__ out)
+{
+    __shared__ int hits[4][kCap + 4];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int64_t L = blockIdx.x;
+    const int64_t w = ((L & 7) * per_xcd + (L >> 3)) * 4 + wid;
+    if (w >= total) return;  // wave-uniform
+    const int64_t b = w / m;
+    const char *fw = grid_ws + b * grid_frame_bytes(n);
+    const BqGrid g = *reinterpret_cast<const BqGrid *>(fw);
+    const int *tab = reinterpret_cast<const int *>(fw + 64);
+    const float4 *sp = reinterpret_cast<const float4 *>(fw + 64 + (kTab + 64) * 4);
+    const float *p = xyz + b * (int64_t)n * 3;
+    const float cx = centres[3 * w], cy = centres[3 * w + 1], cz = centres[3 * w + 2];
+    int32_t *o = out + w * (int64_t)ns;
+    const uint64_t below = (1ull << lane) - 1;
+    int *hw = hits[wid];
+
+    // candidate cells per axis: a hit has |u_p - u_c| < r inv_s (1 + 2^-23) + the rounding of
+    // the two cell coordinates (< 2^-12 at <= 1026 cells): floor(u_c -+ delta) bound its cell.
+    // At the binned radius that is 3 cells per axis; smaller radii take 1-2.
+    const float delta = __fadd_rn(__fmul_rn(__fmul_rn(r, g.inv_s), 1.0f + 1.0f / 1024.0f), 1.0f / 1024.0f);
+    const float ux = __fmul_rn(__fsub_rn(cx, g.minx), g.inv_s), uy = __fmul_rn(__fsub_rn(cy, g.miny), g.inv_s),
+                uz = __fmul_rn(__fsub_rn(cz, g.minz), g.inv_s);
+    auto lo_of = [](float u, float dl, int d) {
+        return max((int)floorf(fminf(fmaxf(__fsub_rn(u, dl), -2.0f), (float)d + 1.0f)), 0);
+    };
+    auto hi_of = [](float u, float dl, int d) {
+        return min((int)floorf(fminf(fmaxf(__fadd_rn(u, dl), -2.0f), (float)d + 1.0f)), d - 1);
+    };
+    // (NaN centres: fmaxf(NaN, -2) = -2 -> an empty range; they have no hits)
+    const int lox = lo_of(ux, delta, g.dx), hix = hi_of(ux, delta, g.dx);
+    const int loy = lo_of(uy, delta, g.dy), hiy = hi_of(uy, delta, g.dy);
+    const int loz = lo_of(uz, delta, g.dz), hiz = hi_of(uz, delta, g.dz);
+    int cnt = 0, first = -1;
+    // lane j < 9 owns the z-run of column (lox + j / 3, loy + j % 3); a radius above the
+    // binned one can need more columns: such centres walk the windows by index-order scan
+    const bool full = (hix - lox) > 2 || (hiy - loy) > 2;
+    const int jx = lox + lane / 3, jy = loy + lane % 3;
+    const bool col_ok = !full && lane < 9 && jx <= hix && jy <= hiy && loz <= hiz;
+    const int colbase = (jx * g.dy + jy) * g.dz + loz;
+    for (int win = 0; win < g.nwin && cnt < ns; ++win) {
+        const int wlo = win << g.win_shift, whi = min(n, (win + 1) << g.win_shift);
+        int st = 0, len = 0;
+        if (col_ok) {
+            const int s0 = win * g.ncell + colbase;
+            st = tab[s0];
+            len = tab[s0 + (hiz - loz) + 1] - st;
+        }
+        int incl = len;
+#pragma unroll
+        for (int d = 1; d < 16; d <<= 1) {
+            const int v = __shfl_up(incl, d, 64);
+            if (lane >= d) incl += v;
+        }
+        const int tot = full ? kCap + 1 : __builtin_amdgcn_readlane(incl, 8);
+        if (tot == 0) continue;
+        if (tot > kCap) {
+            scan_range(p, wlo, whi, cx, cy, cz, r2, ns, lane, below, cnt, first, o);
+            continue;
+        }
+        const int excl = incl - len;
+        int e[9], s[9];
+#pragma unroll
+        for (int j = 0; j < 9; ++j) {
+            e[j] = __builtin_amdgcn_readlane(excl, j);
+            s[j] = __builtin_amdgcn_readlane(st, j);
+        }
+        int hc = 0;
+        for (int t0 = 0; t0 < tot; t0 += 64) {
+            const int t = t0 + lane;
+            int pos = s[0] + t;
+#pragma unroll
+            for (int j = 1; j < 9; ++j)
+                if (t >= e[j]) pos = s[j] + (t - e[j]);
+            bool hit = false;
+            int idx = 0;
+            if (t < tot) {
+                const float4 q = sp[pos];
+                hit = lidar::dist2f(q.x, q.y, q.z, cx, cy, cz) < r2;
+                idx = __float_as_int(q.w);
+            }
+            const uint64_t mk = __ballot(hit);
+            if (hit) hw[hc + __popcll(mk & below)] = idx;
+            hc += __popcll(mk);
+        }
+        if (hc == 0) continue;
+        if (lane < 4) hw[hc + lane] = 0x7fffffff;
+        lds_wave_sync();
+        // rank every hit by index among the window's hits (indices are distinct)
+        int mnv = 0x7fffffff;
+        for (int e0 = 0; e0 < hc; e0 += 64) {
+            const int ei = e0 + lane;
+            const int v = ei < hc ? hw[ei] : 0x7fffffff;
+            int rank = 0;
+            for (int i = 0; i < hc; i += 4) {
+                const int4 h4 = *reinterpret_cast<const int4 *>(hw + i);
+                rank += (h4.x < v) + (h4.y < v) + (h4.z < v) + (h4.w < v);
+            }
+            if (ei < hc && cnt + rank < ns) o[cnt + rank] = v;
+            mnv = min(mnv, v);
+        }
+        if (first < 0) first = (int)lidar::wave_min_u32_dpp((uint32_t)mnv);
+        cnt += hc;
+        lds_wave_sync();
+    }
+    const int fill = first < 0 ? 0 : first;
+    for (int s2 = min(cnt, ns) + lane; s2 < ns; s2 += 64) o[s2] = fill;
+}
+
 }  // namespace
 
-LIDAR_EXPORT int lidar_ball_query_f32(lidar_handle *h, const float *xyz, const float *centres,
-                                      int64_t batch, int64_t n, int64_t m, float radius,
-                                      int32_t nsample, int32_t *idx, void *stream)
+static int launch_bin(const float *xyz, int64_t batch, int64_t n, float radius, int32_t nsample,
+                      char *grid, hipStream_t st)
 {
-    REQUIRE(h && xyz && centres && idx, "lidar_ball_query_f32: null pointer");
-    REQUIRE(batch >= 0 && n >= 1 && m >= 0 && nsample >= 1, "lidar_ball_query_f32: bad sizes");
-    REQUIRE(n < 0x7fffffff && m < 0x7fffffff, "lidar_ball_query_f32: sizes exceed int32");
-    REQUIRE(radius >= 0.0f, "lidar_ball_query_f32: negative radius");
-    const int64_t total = batch * m;
-    if (total == 0) return LIDAR_OK;
-    HIP_TRY(hipSetDevice(h->device));
-    const float r2 = radius * radius;
-    const int64_t gpf = (m + kC - 1) / kC, groups = batch * gpf;
-    const int64_t blocks = (groups + 3) / 4;
-    REQUIRE(blocks <= 0x7fffffff, "lidar_ball_query_f32: too many centres");
-    hipLaunchKernelGGL(ball_query_kernel, dim3((unsigned)blocks), dim3(256), 0,
-                       static_cast<hipStream_t>(stream), xyz, centres, (int)n, (int)m, gpf, groups, r2,
+    hipLaunchKernelGGL(bq_bin_kernel, dim3((unsigned)batch), dim3(1024), 0, st, xyz, (int)n, radius,
+                       (int)nsample, grid);
+    LAUNCH_CHECK();
+    return LIDAR_OK;
+}
+
+static int launch_grid_query(const float *xyz, const char *grid, const float *centres,
+                             int64_t batch, int64_t n, int64_t m, float radius, int32_t nsample, int32_t *idx,
+                             hipStream_t st)
+{
+    const int64_t total = batch * m, blocks = (total + 3) / 4, per_xcd = (blocks + 7) / 8;
+    REQUIRE(per_xcd * 8 <= 0x7fffffff, "ball query: too many centres");
+    hipLaunchKernelGGL(bq_grid_kernel, dim3((unsigned)(per_xcd * 8)), dim3(256), 0, st, xyz, grid, centres,
+                       (int)n, (int)m, total, per_xcd, radius, radius * radius,
                        (int)nsample, idx);
     LAUNCH_CHECK();
     return LIDAR_OK;
+}
+
+static int launch_brute(const float *xyz, const float *centres, int64_t batch, int64_t n, int64_t m, float r2,
+                        int32_t nsample, int32_t *idx, hipStream_t st)
+{
+    const int64_t gpf = (m + kC - 1) / kC, groups = batch * gpf;
+    const int64_t blocks = (groups + 3) / 4;
+    REQUIRE(blocks <= 0x7fffffff, "lidar_ball_query_f32: too many centres");
+    hipLaunchKernelGGL(ball_query_kernel, dim3((unsigned)blocks), dim3(256), 0, st, xyz, centres, (int)n,
+                       (int)m, gpf, groups, r2, (int)nsample, idx);
+    LAUNCH_CHECK();
+    return LIDAR_OK;
+}
+
+#define BQ_CHECK_ARGS(fn)                                                                    \
+    REQUIRE(h && xyz && centres && idx, fn ": null pointer");                               \
+    REQUIRE(batch >= 0 && n >= 1 && m >= 0 && nsample >= 1, fn ": bad sizes");               \
+    REQUIRE(n < 0x3fffffff && m < 0x7fffffff, fn ": sizes exceed int32");                   \
+    REQUIRE(batch <= 0x7fffffff, fn ": batch exceeds int32");                               \
+    REQUIRE(radius >= 0.0f, fn ": negative radius")
+
+LIDAR_EXPORT uint64_t lidar_ball_query_grid_bytes(int64_t batch, int64_t n)
+{
+    return batch <= 0 || n <= 0 ? 0 : (uint64_t)batch * grid_frame_bytes(n);
+}
+
+LIDAR_EXPORT int lidar_ball_query_mode_f32(lidar_handle *h, const float *xyz, const float *centres,
+                                           int64_t batch, int64_t n, int64_t m, float radius, int32_t nsample,
+                                           int32_t mode, int32_t *idx, void *stream)
+{
+    BQ_CHECK_ARGS("lidar_ball_query_f32");
+    REQUIRE(mode >= 0 && mode <= 2, "lidar_ball_query_mode_f32: mode is 0 (auto), 1 (scan) or 2 (grid)");
+    if (batch * m == 0) return LIDAR_OK;
+    HIP_TRY(hipSetDevice(h->device));
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const float r2 = radius * radius;
+    const bool grid = mode == 2 || (mode == 0 && n >= kGridMinN);
+    if (!grid) return launch_brute(xyz, centres, batch, n, m, r2, nsample, idx, st);
+    char *ws = static_cast<char *>(lidar::workspace(h, lidar_ball_query_grid_bytes(batch, n)));
+    if (!ws) return LIDAR_ENOMEM;
+    int rc = launch_bin(xyz, batch, n, radius, nsample, ws, st);
+    if (rc) return rc;
+    return launch_grid_query(xyz, ws, centres, batch, n, m, radius, nsample, idx, st);
+}
+
+LIDAR_EXPORT int lidar_ball_query_f32(lidar_handle *h, const float *xyz, const float *centres, int64_t batch,
+                                      int64_t n, int64_t m, float radius, int32_t nsample, int32_t *idx,
+                                      void *stream)
+{
+    return lidar_ball_query_mode_f32(h, xyz, centres, batch, n, m, radius, nsample, 0, idx, stream);
+}
+
+LIDAR_EXPORT int lidar_ball_query_bin_f32(lidar_handle *h, const float *xyz, int64_t batch, int64_t n,
+                                          float radius, int32_t nsample, void *grid, void *stream)
+{
+    REQUIRE(h && xyz && grid, "lidar_ball_query_bin_f32: null pointer");
+    REQUIRE(batch >= 0 && batch <= 0x7fffffff && n >= 1 && n < 0x3fffffff && nsample >= 1,
+            "lidar_ball_query_bin_f32: bad sizes");
+    REQUIRE(radius >= 0.0f, "lidar_ball_query_bin_f32: negative radius");
+    if (batch == 0) return LIDAR_OK;
+    HIP_TRY(hipSetDevice(h->device));
+    return launch_bin(xyz, batch, n, radius, nsample, static_cast<char *>(grid),
+                      static_cast<hipStream_t>(stream));
+}
+
+LIDAR_EXPORT int lidar_ball_query_binned_f32(lidar_handle *h, const float *xyz, const void *grid,
+                                             const float *centres, int64_t batch, int64_t n, int64_t m,
+                                             float radius, int32_t nsample, int32_t *idx, void *stream)
+{
+    BQ_CHECK_ARGS("lidar_ball_query_binned_f32");
+    REQUIRE(grid, "lidar_ball_query_binned_f32: null grid");
+    if (batch * m == 0) return LIDAR_OK;
+    HIP_TRY(hipSetDevice(h->device));
+    return launch_grid_query(xyz, static_cast<const char *>(grid), centres, batch, n, m, radius, nsample, idx,
+                             static_cast<hipStream_t>(stream));
 }

@@ -60,18 +60,20 @@ struct PackX3 {
     static constexpr int W1U4 = T1 * 64 / 4;                     // fp32 W1 in u4
 };
 
-template <int C1, int C2, int C3, int NS, bool XYZ>
-__global__ __launch_bounds__(256, 3) void sa_x3_kernel(const float *__restrict__ P, int64_t stride,
+// R = 16-row tiles per wavefront (R grouped-row tiles of the same centre share every weight
+// fragment read from LDS: R = 2 halves the LDS and L2 weight bytes per MFMA)
+template <int C1, int C2, int C3, int NS, bool XYZ, int R>
+__global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float *__restrict__ P, int64_t stride,
                                                      const float *__restrict__ Q, const int32_t *__restrict__ idx,
                                                      int n, int m, int64_t total, const uint4 *__restrict__ packed,
                                                      float *__restrict__ out, int64_t out_stride, int64_t out_offset)
 {
-    static_assert(NS % 16 == 0 && C1 % 32 == 0 && C2 % 32 == 0 && C3 % 32 == 0, "tile shapes");
+    static_assert(NS % (16 * R) == 0 && C1 % 32 == 0 && C2 % 32 == 0 && C3 % 32 == 0, "tile shapes");
     using K = PackX3<C1, C2, C3>;
     constexpr int T1 = K::T1, T2 = K::T2, T3 = K::T3, KS2 = K::KS2, KS3 = K::KS3;
     constexpr int CH2 = K::CH2, CH3 = K::CH3, CHMAX = CH2 > CH3 ? CH2 : CH3;
     constexpr int NCH = T2 / 2 + T3 / 2;
-    constexpr int TILES = NS / 16;
+    constexpr int ITERS = NS / (16 * R);
     constexpr int PER = (CHMAX + 255) / 256;
 
     __shared__ uint4 buf[2][CHMAX];
@@ -112,11 +114,12 @@ __global__ __launch_bounds__(256, 3) void sa_x3_kernel(const float *__restrict__
     int par = 0;
 
 #pragma unroll 1
-    for (int tile = 0; tile < TILES; ++tile) {
-        const int64_t k = idx[cc * NS + tile * 16 + col];
-        // ---- layer 1 -> the layer-2 operand fragments (hi / lo) of the 16 grouped rows
-        bf16x8 xh[KS2], xl[KS2];
-        {
+    for (int it = 0; it < ITERS; ++it) {
+        // ---- layer 1 -> the layer-2 operand fragments (hi / lo) of R x 16 grouped rows
+        bf16x8 xh[R][KS2], xl[R][KS2];
+#pragma unroll
+        for (int rr = 0; rr < R; ++rr) {
+            const int64_t k = idx[cc * NS + (it * R + rr) * 16 + col];
             f32x4 y1[T1];
             if constexpr (XYZ) {
                 const float *pr = P + ((int64_t)b * n + k) * 3;
@@ -145,18 +148,20 @@ __global__ __launch_bounds__(256, 3) void sa_x3_kernel(const float *__restrict__
                 }
             }
 #pragma unroll
-            for (int s = 0; s < KS2; ++s) split_pair(y1[2 * s], y1[2 * s + 1], xh[s], xl[s]);
+            for (int s = 0; s < KS2; ++s) split_pair(y1[2 * s], y1[2 * s + 1], xh[rr][s], xl[rr][s]);
         }
 
-        f32x4 y2[T2];
-        bf16x8 zh[KS3], zl[KS3];
+        f32x4 y2[R][T2];
+        bf16x8 zh[R][KS3], zl[R][KS3];
 #pragma unroll
         for (int c = 0; c < NCH; ++c) {
             const int cn = c + 1 < NCH ? c + 1 : 0;
-            const bool more = c + 1 < NCH || tile + 1 < TILES;
+            const bool more = c + 1 < NCH || it + 1 < ITERS;
             if (more) fetch(cn, par ^ 1);  // lands during this chunk's MFMAs
             const uint4 *wb = buf[par] + lane;
-            f32x4 a0 = {}, a1 = {};
+            f32x4 a0[R], a1[R];
+#pragma unroll
+            for (int rr = 0; rr < R; ++rr) a0[rr] = a1[rr] = f32x4{};
             if (c < T2 / 2) {  // layer 2: output tiles 2c, 2c+1 (channel rows x point columns)
 #pragma unroll
                 for (int s = 0; s < KS2; ++s) {
@@ -164,23 +169,32 @@ __global__ __launch_bounds__(256, 3) void sa_x3_kernel(const float *__restrict__
                     const bf16x8 l0 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 0) * 2 + 1) * 64]);
                     const bf16x8 h1 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 1) * 2 + 0) * 64]);
                     const bf16x8 l1 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 1) * 2 + 1) * 64]);
-                    a0 = mfma_bf(h0, xh[s], a0);
-                    a1 = mfma_bf(h1, xh[s], a1);
-                    a0 = mfma_bf(h0, xl[s], a0);
-                    a1 = mfma_bf(h1, xl[s], a1);
-                    a0 = mfma_bf(l0, xh[s], a0);
-                    a1 = mfma_bf(l1, xh[s], a1);
+#pragma unroll
+                    for (int rr = 0; rr < R; ++rr) {
+                        a0[rr] = mfma_bf(h0, xh[rr][s], a0[rr]);
+                        a1[rr] = mfma_bf(h1, xh[rr][s], a1[rr]);
+                        a0[rr] = mfma_bf(h0, xl[rr][s], a0[rr]);
+                        a1[rr] = mfma_bf(h1, xl[rr][s], a1[rr]);
+                        a0[rr] = mfma_bf(l0, xh[rr][s], a0[rr]);
+                        a1[rr] = mfma_bf(l1, xh[rr][s], a1[rr]);
+                    }
                 }
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    a0[r] = relu(a0[r] + bias_s[C1 + 16 * (2 * c) + 4 * q + r]);
-                    a1[r] = relu(a1[r] + bias_s[C1 + 16 * (2 * c + 1) + 4 * q + r]);
+                for (int rr = 0; rr < R; ++rr) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        a0[rr][r] = relu(a0[rr][r] + bias_s[C1 + 16 * (2 * c) + 4 * q + r]);
+                        a1[rr][r] = relu(a1[rr][r] + bias_s[C1 + 16 * (2 * c + 1) + 4 * q + r]);
+                    }
+                    y2[rr][2 * c < T2 ? 2 * c : 0] = a0[rr];
+                    y2[rr][2 * c + 1 < T2 ? 2 * c + 1 : 0] = a1[rr];
                 }
-                y2[2 * c < T2 ? 2 * c : 0] = a0;
-                y2[2 * c + 1 < T2 ? 2 * c + 1 : 0] = a1;
                 if (c == T2 / 2 - 1) {  // layer 2 complete: its output as layer-3 fragments
 #pragma unroll
-                    for (int s = 0; s < KS3; ++s) split_pair(y2[2 * s], y2[2 * s + 1], zh[s], zl[s]);
+                    for (int rr = 0; rr < R; ++rr)
+#pragma unroll
+                        for (int s = 0; s < KS3; ++s)
+                            split_pair(y2[rr][2 * s], y2[rr][2 * s + 1], zh[rr][s], zl[rr][s]);
                 }
             } else {  // layer 3: output tiles 2tp, 2tp+1, transposed (point rows), + max-pool
                 const int tp = c - T2 / 2;
@@ -190,21 +204,27 @@ __global__ __launch_bounds__(256, 3) void sa_x3_kernel(const float *__restrict__
                     const bf16x8 l0 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 0) * 2 + 1) * 64]);
                     const bf16x8 h1 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 1) * 2 + 0) * 64]);
                     const bf16x8 l1 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 1) * 2 + 1) * 64]);
-                    a0 = mfma_bf(zh[s], h0, a0);
-                    a1 = mfma_bf(zh[s], h1, a1);
-                    a0 = mfma_bf(zh[s], l0, a0);
-                    a1 = mfma_bf(zh[s], l1, a1);
-                    a0 = mfma_bf(zl[s], h0, a0);
-                    a1 = mfma_bf(zl[s], h1, a1);
+#pragma unroll
+                    for (int rr = 0; rr < R; ++rr) {
+                        a0[rr] = mfma_bf(zh[rr][s], h0, a0[rr]);
+                        a1[rr] = mfma_bf(zh[rr][s], h1, a1[rr]);
+                        a0[rr] = mfma_bf(zh[rr][s], l0, a0[rr]);
+                        a1[rr] = mfma_bf(zh[rr][s], l1, a1[rr]);
+                        a0[rr] = mfma_bf(zl[rr][s], h0, a0[rr]);
+                        a1[rr] = mfma_bf(zl[rr][s], h1, a1[rr]);
+                    }
                 }
 #pragma unroll
                 for (int hh = 0; hh < 2; ++hh) {
-                    const f32x4 &acc = hh ? a1 : a0;
                     const int t = 2 * tp + hh;
                     const float bias = bias_s[C1 + C2 + 16 * t + col];
                     float v = 0.0f;
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) v = fmaxf(v, relu(acc[r] + bias));
+                    for (int rr = 0; rr < R; ++rr) {
+                        const f32x4 &acc = hh ? a1[rr] : a0[rr];
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) v = fmaxf(v, relu(acc[r] + bias));
+                    }
                     v = fmaxf(v, __shfl_xor(v, 16, 64));
                     v = fmaxf(v, __shfl_xor(v, 32, 64));
                     if (q == 0) {
@@ -224,15 +244,21 @@ __global__ __launch_bounds__(256, 3) void sa_x3_kernel(const float *__restrict__
     }
 }
 
+// LIDAR_X3_ROWS: 16-row tiles per wavefront (A/B builds; 2 unless NS = 16)
+#ifndef LIDAR_X3_ROWS
+#define LIDAR_X3_ROWS 2
+#endif
+
 template <int C1, int C2, int C3, int NS, bool XYZ>
 int launch_x3(const float *p, int64_t stride, const float *q, const int32_t *idx, int64_t batch, int64_t n,
               int64_t m, const void *packed, float *out, int64_t os, int64_t oo, hipStream_t s)
 {
+    constexpr int R = NS >= 16 * LIDAR_X3_ROWS ? LIDAR_X3_ROWS : 1;
     const int64_t total = batch * m;
     const int64_t blocks = (total + 3) / 4;
     REQUIRE(blocks <= 0x7fffffff, "sa_group_mlp_x3: too many centres");
-    hipLaunchKernelGGL((sa_x3_kernel<C1, C2, C3, NS, XYZ>), dim3((unsigned)blocks), dim3(256), 0, s, p, stride, q,
-                       idx, (int)n, (int)m, total, static_cast<const uint4 *>(packed), out, os, oo);
+    hipLaunchKernelGGL((sa_x3_kernel<C1, C2, C3, NS, XYZ, R>), dim3((unsigned)blocks), dim3(256), 0, s, p, stride,
+                       q, idx, (int)n, (int)m, total, static_cast<const uint4 *>(packed), out, os, oo);
     LAUNCH_CHECK();
     return LIDAR_OK;
 }

@@ -110,15 +110,44 @@ def farthest_point_sample(xyz, npoint, return_xyz=False, first_zero=None, prefix
     return (idx, new_xyz) if return_xyz else idx
 
 
-def ball_query(radius, nsample, xyz, new_xyz, out=None, slot=0):
-    """-> idx (B, M, nsample) int32 (pointnet2 argument order)."""
+BQ_MODES = {"auto": 0, "scan": 1, "grid": 2}
+BQ_GRID_MIN_N = 1024  # csrc/ball_query.hip kGridMinN: "auto" bins frames of at least this many points
+
+
+def ball_query(radius, nsample, xyz, new_xyz, out=None, slot=0, mode="auto", grid=None):
+    """-> idx (B, M, nsample) int32 (pointnet2 argument order).
+
+    mode: "auto" (the (index window, cell) grid for N >= 1024, else the index-order scan),
+    "scan" or "grid" — identical results.  grid: a buffer filled by ball_query_bin for
+    these xyz (the binning then does not run here)."""
     _dev_check(xyz, new_xyz, out)
     B, N, _ = xyz.shape
     M = new_xyz.shape[1]
     idx = out if out is not None else torch.empty((B, M, nsample), dtype=torch.int32, device=xyz.device)
-    nat.call("lidar_ball_query_f32", nat.handle(xyz.device.index, slot), nat.ptr(xyz), nat.ptr(new_xyz),
-             B, N, M, float(radius), int(nsample), nat.ptr(idx), nat.stream_ptr())
+    h = nat.handle(xyz.device.index, slot)
+    if grid is not None:
+        nat.call("lidar_ball_query_binned_f32", h, nat.ptr(xyz), nat.ptr(grid), nat.ptr(new_xyz),
+                 B, N, M, float(radius), int(nsample), nat.ptr(idx), nat.stream_ptr())
+    else:
+        nat.call("lidar_ball_query_mode_f32", h, nat.ptr(xyz), nat.ptr(new_xyz),
+                 B, N, M, float(radius), int(nsample), BQ_MODES[mode], nat.ptr(idx), nat.stream_ptr())
     return idx
+
+
+def ball_query_grid_buffer(B, N, device):
+    """Device buffer for ball_query_bin over (B, N, 3) frames."""
+    nbytes = nat.load_library().lidar_ball_query_grid_bytes(B, N)
+    return torch.empty((max(1, nbytes),), dtype=torch.uint8, device=device)
+
+
+def ball_query_bin(radius, nsample, xyz, grid, slot=0):
+    """Bin (B, N, 3) frames for later ball_query(..., grid=grid) calls (any stream order
+    that puts this launch first).  Depends only on xyz."""
+    _dev_check(xyz, grid)
+    B, N, _ = xyz.shape
+    nat.call("lidar_ball_query_bin_f32", nat.handle(xyz.device.index, slot), nat.ptr(xyz), B, N,
+             float(radius), int(nsample), nat.ptr(grid), nat.stream_ptr())
+    return grid
 
 
 def pack_branch(layers, cfeat):
@@ -408,11 +437,12 @@ class PointNet2Backbone:
         self.x3_dense = bool(x3) and not self.bf16
         self.timers = None  # set to a _Timers() to time every launch
 
-    def forward_from_sa1_fps(self, xyz, idx1, new_xyz1, fz1, gidx1=None):
-        """forward() with level 0's FPS (and ball queries) already computed (StreamingSSG)."""
-        return self.forward(xyz, pre_fps=(idx1, new_xyz1, fz1), pre_bq=gidx1)[0]
+    def forward_from_sa1_fps(self, xyz, idx1, new_xyz1, fz1, gidx1=None, grid1=None):
+        """forward() with level 0's FPS (and ball queries, or the ball-query binning of the
+        frames) already computed (StreamingSSG)."""
+        return self.forward(xyz, pre_fps=(idx1, new_xyz1, fz1), pre_bq=gidx1, pre_grid=grid1)[0]
 
-    def forward(self, xyz, keep_levels=False, pre_fps=None, pre_bq=None):
+    def forward(self, xyz, keep_levels=False, pre_fps=None, pre_bq=None, pre_grid=None):
         B, N, _ = xyz.shape
         N0 = N  # npoint_div is relative to the input frame (N/16, N/64)
         feats = None
@@ -449,7 +479,8 @@ class PointNet2Backbone:
                 if li == 0 and pre_bq is not None:
                     gidx = pre_bq[bi_]
                 else:
-                    gidx = _call(self.timers, f"{tag}_ball_query", ball_query, br["r"], br["ns"], xyz, new_xyz)
+                    gidx = _call(self.timers, f"{tag}_ball_query", ball_query, br["r"], br["ns"], xyz, new_xyz,
+                                 grid=pre_grid if li == 0 else None)
                 if "packed_x3" in br:
                     p16, q16 = (pq[bi_] if pq is not None else (xyz, new_xyz))
                     _call(self.timers, f"{tag}_group_mlp", group_mlp_x3, p16, q16, gidx, N, br["packed_x3"],
@@ -584,6 +615,10 @@ class StreamingSSG:
         # level-0 ball queries of every branch ride on the FPS stream too
         self.gidx = [[torch.empty((GB, self.M1, br["ns"]), dtype=torch.int32, device=dev)
                       for br in lvl0["branches"]] for _ in range(nslot)]
+        # bq_on_main: the level-0 frames are binned for the ball query on the side stream
+        # (it depends only on the frames), once for all branches at the largest radius
+        self.grid = [ball_query_grid_buffer(GB, n, dev) if self.bq_on_main and n >= BQ_GRID_MIN_N else None
+                     for _ in range(nslot)]
         self.fps_done = [torch.cuda.Event() for _ in range(nslot)]
         self.slot_free = [torch.cuda.Event() for _ in range(nslot)]
         for e in self.slot_free:
@@ -628,6 +663,10 @@ class StreamingSSG:
                   first_zero=self.fz[slot][:g], slot=1 + k % self.depth, out_idx=self.idx[slot][:g],
                   out_xyz=self.cxyz[slot][:g])
             lvl0 = self.bb.levels[0]
+            if self.grid[slot] is not None:
+                br = max(lvl0["branches"], key=lambda b: b["r"])
+                _call(self.bb.timers, "sa1_bq_bin", ball_query_bin, br["r"], br["ns"], x, self.grid[slot],
+                      slot=1 + k % self.depth)
             for bi_, br in enumerate([] if self.bq_on_main else lvl0["branches"]):
                 tag = "sa1" + (f"_b{bi_}" if len(lvl0["branches"]) > 1 else "")
                 _call(self.bb.timers, f"{tag}_ball_query", ball_query, br["r"], br["ns"], x, self.cxyz[slot][:g],
@@ -642,7 +681,8 @@ class StreamingSSG:
         B, g = self.B, len(xs) * self.B
         x = self.stage[slot][:g] if self.G > 1 else xs[0]
         out = self.bb.forward_from_sa1_fps(x, self.idx[slot][:g], self.cxyz[slot][:g], self.fz[slot][:g],
-                                           None if self.bq_on_main else [gi[:g] for gi in self.gidx[slot]])
+                                           None if self.bq_on_main else [gi[:g] for gi in self.gidx[slot]],
+                                           self.grid[slot])
         self.slot_free[slot].record(main)
         return list(out.split(B)) if len(xs) > 1 else [out]
 

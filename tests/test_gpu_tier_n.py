@@ -61,14 +61,69 @@ def test_fps_matches_numpy_restatement():
 
 @pytest.mark.parametrize("n,m,r,ns", [(16384, 1024, 0.2, 32), (4096, 1024, 0.4, 64), (8192, 512, 0.1, 16),
                                       (8192, 512, 0.8, 128), (1000, 50, 0.05, 8), (70, 33, 0.3, 200)])
-def test_ball_query_bit_exact(cuda, n, m, r, ns):
+@pytest.mark.parametrize("mode", ["scan", "grid"])
+def test_ball_query_bit_exact(cuda, n, m, r, ns, mode):
     x = unit_frames(2, n, 5)
     c = x[:, :m].copy()
     c[:, :3] += 3.0  # centres with no neighbour at all -> all-zero rows
-    idx = pn.ball_query(r, ns, torch.from_numpy(x).to(cuda), torch.from_numpy(c).to(cuda))
+    idx = pn.ball_query(r, ns, torch.from_numpy(x).to(cuda), torch.from_numpy(c).to(cuda), mode=mode)
     want = tier_n.ball_query(x, c, r, ns)
     got = idx.cpu().numpy()
     assert np.array_equal(got, want), f"{(got != want).sum()} differ"
+
+
+def _bq_edge_frames():
+    rng = np.random.default_rng(21)
+    n = 6000
+    out = {}
+    out["all_equal"] = np.full((n, 3), 0.25, np.float32)
+    line = np.zeros((n, 3), np.float32)
+    line[:, 0] = rng.uniform(-50, 50, n)  # one long axis: many cells per axis
+    out["line"] = line
+    blob = rng.uniform(-1, 1, (n, 3)).astype(np.float32)
+    blob[::3] = (0.3 + 1e-3 * rng.standard_normal((len(blob[::3]), 3))).astype(np.float32)  # a dense clump
+    out["clump"] = blob
+    bad = rng.uniform(-1, 1, (n, 3)).astype(np.float32)
+    bad[5] = np.nan
+    bad[17, 1] = np.inf
+    bad[40, 2] = -np.inf
+    bad[41] = 1e30
+    out["nonfinite"] = bad
+    lat = (np.stack(np.meshgrid(*[np.arange(18)] * 3, indexing="ij"), -1).reshape(-1, 3)[:n] * 0.1).astype(np.float32)
+    out["lattice_ties"] = lat  # points at exactly r from lattice centres
+    out["huge_extent"] = (rng.uniform(-1, 1, (n, 3)) * np.array([1e6, 1, 1e-6])).astype(np.float32)
+    return out
+
+
+@pytest.mark.parametrize("name", list(_bq_edge_frames()))
+@pytest.mark.parametrize("r,ns", [(0.1, 32), (0.0, 8), (0.3, 128), (5.0, 16)])
+def test_ball_query_grid_edge_frames(cuda, name, r, ns):
+    """the grid path on degenerate frames (one point repeated, a line, a dense clump that
+    overflows the per-window candidate buffer, NaN/inf points, lattice ties at exactly r,
+    a 1e12 axis ratio), zero and large radii, centres inside and far outside: identical
+    to the index-order scan and the oracle."""
+    x = _bq_edge_frames()[name][None]
+    c = np.concatenate([x[:, :300:3], x[:, :40] + np.float32(7.5), x[:, 40:60] - np.float32(1e7)], 1)
+    c = np.ascontiguousarray(c)
+    xt, ct = torch.from_numpy(x).to(cuda), torch.from_numpy(c).to(cuda)
+    want = tier_n.ball_query(x, c, r, ns)
+    for mode in ("grid", "scan"):
+        got = pn.ball_query(r, ns, xt, ct, mode=mode).cpu().numpy()
+        assert np.array_equal(got, want), f"{mode}: {(got != want).sum()} differ"
+
+
+def test_ball_query_binned_reuse(cuda):
+    """one binning (lidar_ball_query_bin_f32) serves queries at smaller, equal and larger
+    radii and other nsample values, exactly."""
+    B, N, M = 3, 20000, 700
+    x = unit_frames(B, N, 31)
+    c = np.ascontiguousarray(x[:, ::29][:, :M])
+    xt, ct = torch.from_numpy(x).to(cuda), torch.from_numpy(c).to(cuda)
+    grid = pn.ball_query_bin(0.2, 32, xt, pn.ball_query_grid_buffer(B, N, cuda))
+    for r, ns in ((0.2, 32), (0.1, 16), (0.2, 64), (0.4, 32)):
+        got = pn.ball_query(r, ns, xt, ct, grid=grid).cpu().numpy()
+        want = tier_n.ball_query(x, c, r, ns)
+        assert np.array_equal(got, want), f"r={r} ns={ns}: {(got != want).sum()} differ"
 
 
 @pytest.mark.parametrize("cfg_name,level,branch", [("ssg", 0, 0), ("ssg", 1, 0), ("msg", 0, 0), ("msg", 0, 1),

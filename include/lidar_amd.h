@@ -159,6 +159,15 @@ int lidar_dense_x3_f32(lidar_handle *h, const float *x, int64_t rows, int32_t k,
                        const float *bias, int32_t cout, int32_t relu_on, int32_t pool_rows, float *y,
                        void *stream);
 
+/* the same GEMM on a weight image packed once (bf16 hi / lo MFMA B fragments; K padded to 32):
+ * lidar_dense_x3_packed_size(k, cout) bytes, filled on the device by lidar_dense_x3_pack_f32
+ * from W (k, cout) fp32.  lidar_dense_x3_f32 packs into the handle's workspace per call. */
+int64_t lidar_dense_x3_packed_size(int32_t k, int32_t cout);
+int lidar_dense_x3_pack_f32(lidar_handle *h, const float *w, int32_t k, int32_t cout, void *packed, void *stream);
+int lidar_dense_x3p_f32(lidar_handle *h, const float *x, int64_t rows, int32_t k, const void *packed,
+                        const float *bias, int32_t cout, int32_t relu_on, int32_t pool_rows, float *y,
+                        void *stream);
+
 /* lidar_sa_group_mlp_f32 with layer 1 applied per point beforehand: p (batch*n, p_stride)
  * = [f, x] W1 + b1 for every point of the level, q (batch*m, p_stride) = centre W1_xyz
  * (both via lidar_dense_f32, relu_on = 0, columns >= c1 ignored); a grouped row's layer 1

@@ -314,29 +314,45 @@ def layer1_per_point(x_rows, xyz, cfeat, new_xyz, branches, x3=False):
     out = []
     for br in branches:
         pre = br["pre"]
-        P = dense(x_rows, pre["w1"], pre["b1"], relu=False, x3=x3)
-        Q = dense(cpad, pre["wq"], pre["zero"], relu=False, x3=x3)
+        P = dense(x_rows, pre["w1"], pre["b1"], relu=False, x3=x3, wpack=pre.get("w1_x3") if x3 else None)
+        Q = dense(cpad, pre["wq"], pre["zero"], relu=False, x3=x3, wpack=pre.get("wq_x3") if x3 else None)
         out.append((P, Q))
     return out
 
 
-def dense(x, w, b, relu=True, pool_rows=0, out=None, x3=False):
+def pack_dense_x3(w):
+    """(k, cout) fp32 CUDA weights -> the x3 GEMM's packed bf16 hi / lo image (device)."""
+    _dev_check(w)
+    k, cout = w.shape
+    nbytes = nat.load_library().lidar_dense_x3_packed_size(k, cout)
+    out = torch.empty((nbytes,), dtype=torch.uint8, device=w.device)
+    nat.call("lidar_dense_x3_pack_f32", nat.handle(w.device.index), nat.ptr(w), k, cout, nat.ptr(out),
+             nat.stream_ptr())
+    return out
+
+
+def dense(x, w, b, relu=True, pool_rows=0, out=None, x3=False, wpack=None):
     """x (rows, k) @ w (k, cout) + b [-> ReLU] [-> max over runs of pool_rows rows].
-    x3: on the split-bf16 GEMM (lidar_dense_x3_f32; fp32 arithmetic within 1e-4)."""
+    x3: on the split-bf16 GEMM (lidar_dense_x3_f32; fp32 arithmetic within 1e-4); wpack =
+    pack_dense_x3(w) skips the per-call packing of w."""
     rows, k = x.shape
     cout = w.shape[1]
     if out is None:
         shape = (rows // pool_rows, cout) if pool_rows else (rows, cout)
         out = (torch.zeros if pool_rows else torch.empty)(shape, dtype=torch.float32, device=x.device)
-    _dev_check(x, w, b, out)
+    _dev_check(x, w, b, out, wpack)
+    if x3 and wpack is not None:
+        nat.call("lidar_dense_x3p_f32", nat.handle(x.device.index), nat.ptr(x), rows, k, nat.ptr(wpack),
+                 nat.ptr(b), cout, 1 if relu else 0, pool_rows, nat.ptr(out), nat.stream_ptr())
+        return out
     nat.call("lidar_dense_x3_f32" if x3 else "lidar_dense_f32", nat.handle(x.device.index), nat.ptr(x), rows, k,
              nat.ptr(w), nat.ptr(b), cout, 1 if relu else 0, pool_rows, nat.ptr(out), nat.stream_ptr())
     return out
 
 
-def dense_relu(x, w, b, pool_rows=0, out=None, x3=False):
+def dense_relu(x, w, b, pool_rows=0, out=None, x3=False, wpack=None):
     if x3:
-        return dense(x, w, b, True, pool_rows, out, x3=True)
+        return dense(x, w, b, True, pool_rows, out, x3=True, wpack=wpack)
     rows, k = x.shape
     cout = w.shape[1]
     if out is None:
@@ -435,6 +451,14 @@ class PointNet2Backbone:
         self.out_channels = cfeat
         # x3 on: the dense layers (per-point layer 1, group_all) on the split-bf16 GEMM too
         self.x3_dense = bool(x3) and not self.bf16
+        if self.x3_dense:  # the dense layers' weights packed once into x3 B fragments
+            for lvl in self.levels:
+                if lvl.get("group_all"):
+                    lvl["w_x3"] = [pack_dense_x3(w) for w in lvl["w"]]
+                for br in lvl.get("branches", []):
+                    if "pre" in br:
+                        br["pre"]["w1_x3"] = pack_dense_x3(br["pre"]["w1"])
+                        br["pre"]["wq_x3"] = pack_dense_x3(br["pre"]["wq"])
         self.timers = None  # set to a _Timers() to time every launch
 
     def forward_from_sa1_fps(self, xyz, idx1, new_xyz1, fz1, gidx1=None, grid1=None):
@@ -524,11 +548,14 @@ class PointNet2Backbone:
             x2 = x.view(B, M, kp)[:, sel].reshape(B * mp, kp).contiguous()
             M, rows = mp, B * mp
         t = self.timers
-        h1 = _call(t, "sa3_dense1", dense_relu, x2, lvl["w"][0], lvl["b"][0], x3=self.x3_dense)
-        h2 = _call(t, "sa3_dense2", dense_relu, h1, lvl["w"][1], lvl["b"][1], x3=self.x3_dense)
+        wp = lvl.get("w_x3") if self.x3_dense else None
+        h1 = _call(t, "sa3_dense1", dense_relu, x2, lvl["w"][0], lvl["b"][0], x3=self.x3_dense,
+                   wpack=wp[0] if wp else None)
+        h2 = _call(t, "sa3_dense2", dense_relu, h1, lvl["w"][1], lvl["b"][1], x3=self.x3_dense,
+                   wpack=wp[1] if wp else None)
         out = torch.zeros((rows // M, lvl["w"][2].shape[1]), dtype=torch.float32, device=x.device)
         return _call(t, "sa3_dense3_pool", dense_relu, h2, lvl["w"][2], lvl["b"][2], pool_rows=M, out=out,
-                     x3=self.x3_dense)
+                     x3=self.x3_dense, wpack=wp[2] if wp else None)
 
     __call__ = forward
 

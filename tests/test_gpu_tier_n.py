@@ -271,7 +271,7 @@ def test_dense_no_relu(cuda):
 
 
 @pytest.mark.parametrize("rows,k,cout,pool", [(256, 144, 128, 0), (512, 272, 256, 0), (1024, 512, 1024, 512),
-                                              (384, 16, 128, 128)])
+                                              (384, 16, 128, 128), (2048, 256, 512, 1024), (128, 48, 384, 0)])
 def test_dense_x3(cuda, rows, k, cout, pool):
     """split-bf16 GEMM vs the fp32 numpy product at the fp32 path's 1e-4 tolerance."""
     rng = np.random.default_rng(rows + k)
@@ -281,6 +281,8 @@ def test_dense_x3(cuda, rows, k, cout, pool):
     T = lambda a: torch.from_numpy(a).to(cuda)
     want = x.astype(np.float64) @ w.astype(np.float64) + b
     feat_close(pn.dense(T(x), T(w), T(b), relu=False, x3=True).cpu().numpy(), want, "dense x3 no relu")
+    wp = pn.pack_dense_x3(T(w))  # the packed-weight entry point the backbone uses
+    feat_close(pn.dense(T(x), T(w), T(b), relu=False, x3=True, wpack=wp).cpu().numpy(), want, "dense x3p")
     want = np.maximum(want, 0)
     if pool:
         got = pn.dense_relu(T(x), T(w), T(b), pool_rows=pool, x3=True).cpu().numpy()

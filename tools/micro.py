@@ -165,12 +165,15 @@ def dense_micro():
     from lidar_ai_recommendation_software_amd import pointnet2 as pn
     dev = torch.device("cuda:0")
     rng = np.random.default_rng(0)
-    rows = 32 * 1024
-    for k, n in ((272, 256), (256, 512), (512, 1024)):
+    rows = 64 * 1024
+    for k, n in ((144, 128), (272, 256), (256, 512), (512, 1024)):
         x = torch.from_numpy(rng.standard_normal((rows, k)).astype(np.float32)).to(dev)
         w = torch.from_numpy((rng.standard_normal((k, n)) / np.sqrt(k)).astype(np.float32)).to(dev)
         b = torch.from_numpy(rng.standard_normal(n).astype(np.float32)).to(dev)
         ms_own = timeit(lambda: pn.dense(x, w, b), reps=10)
+        wp = pn.pack_dense_x3(w)
+        ms_x3 = timeit(lambda: pn.dense(x, w, b, x3=True, wpack=wp), reps=10)
+        print(f"dense x3 {k}x{n}: {ms_x3:.3f} ms ({2 * rows * k * n / ms_x3 / 1e9:.0f} fp32-equivalent TF)", flush=True)
         ms_blas = timeit(lambda: torch._addmm_activation(b, x, w), reps=10)
         ms_mm = timeit(lambda: torch.relu_(torch.addmm(b, x, w)), reps=10)
         fl = 2 * rows * k * n

@@ -11,11 +11,12 @@ per step (weak scaling, per-frame data parallel, no collective on the data path)
 A step = FPS + ball query + fused group/MLP/max-pool for SA1 and SA2, then group_all
 (three MFMA dense layers with a fused max-pool) over the batch, inputs resident in HBM.
 Steps run through pointnet2.StreamingSSG — the steady state of a continuous LiDAR feed:
-later batches' SA1 FPS (latency-bound, one workgroup per frame) runs on side streams
-while earlier batches' MFMA levels run on the main stream; pairs of batches share one
-FPS launch and one MFMA pass (--fps-group 2; every operator is per frame, outputs are
-bit-identical to one-batch forward()).  K steps = K batches of 32 frames fully processed
-inside the timed region (pipeline fill included).
+later batches' SA1 FPS (latency-bound, one 512-thread workgroup per frame) and the SA1
+ball-query binning run on side streams (--depth 3 groups in flight) while earlier batches'
+ball queries and MFMA levels run on the main stream; groups of three batches share one
+FPS launch and one main-stream pass (--fps-group 3; every operator is per frame, outputs
+are bit-identical to one-batch forward()).  K steps = K batches of 32 frames fully
+processed inside the timed region (pipeline fill included).
 Synthetic data: uniform [-1, 1]^3 float32 frames (seeded per rank), random-init weights.
 
 Run:  python bench.py [--gpus N --steps K --warmup W]  (N>1 via torch.distributed.run)
@@ -193,17 +194,19 @@ def variant_leg(rank, world, frames=8, n=65536, cpu=True, cpu_budget=6.0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=60,
-                    help="timed steps; the pipeline fill (one SA1-FPS latency, ~13 ms) is inside the window")
+    ap.add_argument("--steps", type=int, default=120,
+                    help="timed steps; the pipeline fill (one SA1-FPS latency, ~12 ms) is inside the window")
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=32, help="frames per GPU per step")
     ap.add_argument("--points", type=int, default=65536)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU work per baseline sample")
-    ap.add_argument("--depth", type=int, default=2, help="side streams (SA1-FPS groups in flight ahead of the MLPs)")
+    ap.add_argument("--depth", type=int, default=3, help="side streams (SA1-FPS groups in flight ahead of the MLPs)")
     ap.add_argument("--side-priority", type=int, default=0, help="HIP priority of the FPS streams (<0 = high)")
-    ap.add_argument("--fps-group", type=int, default=2, help="batches per SA1-FPS launch (StreamingSSG fps_group)")
+    ap.add_argument("--fps-group", type=int, default=3, help="batches per SA1-FPS launch (StreamingSSG fps_group)")
     ap.add_argument("--side-cus", type=int, default=0, help="CUs reserved for the SA1 FPS streams (0 = shared)")
+    ap.add_argument("--fps-threads", type=int, default=512, choices=[512, 1024],
+                    help="SA1 FPS workgroup size in the pipeline (512: half the CU footprint beside the MLPs)")
     ap.add_argument("--cu-layout", default="xcd", choices=["xcd", "low"])
     ap.add_argument("--mlp16", default="pre", choices=["0", "1", "pre", "xyz"],
                     help="SA branches on the 16-row MFMA kernels: 1 all, pre / xyz only those levels")
@@ -247,7 +250,7 @@ def main():
         # one workgroup per frame) with batch k's MFMA levels; results are identical to forward()
         pipe = pn.StreamingSSG(bb, B, N, depth=depth, side_priority=args.side_priority,
                                side_cus=args.side_cus, cu_layout=args.cu_layout, fps_group=args.fps_group,
-                               bq_on_main=bool(args.bq_main))
+                               bq_on_main=bool(args.bq_main), fps_threads=args.fps_threads)
         ref, _ = bb.forward(x)
         outs = pipe.run([x] * max(2, warmup))
         torch.cuda.synchronize(dev)

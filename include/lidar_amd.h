@@ -73,6 +73,12 @@ int lidar_version(void);
 int lidar_fps_f32(lidar_handle *h, const float *xyz, int64_t batch, int64_t n, int64_t npoint,
                   int32_t *idx, float *new_xyz, int32_t *first_zero, const int32_t *prefix_ok,
                   void *stream);
+/* the same with an explicit workgroup size per frame: threads 0 (default, 1024), 1024 or 512.
+ * 512 takes ~25 % longer per step and half the CU footprint (throughput pipelines that run
+ * other kernels beside FPS).  Identical results. */
+int lidar_fps_ex_f32(lidar_handle *h, const float *xyz, int64_t batch, int64_t n, int64_t npoint,
+                     int32_t *idx, float *new_xyz, int32_t *first_zero, const int32_t *prefix_ok,
+                     int32_t threads, void *stream);
 
 /* ball query: idx (batch, m, nsample) int32 — the first `nsample` point indices (ascending)
  * with d < radius^2, padded with the first hit, 0 when there is none.  Replaces the eps-ball

@@ -43,6 +43,7 @@ SIGNATURES = {
     "lidar_last_error": [],
     "lidar_version": [],
     "lidar_fps_f32": [P, P, I64, I64, I64, P, P, P, P, P],
+    "lidar_fps_ex_f32": [P, P, I64, I64, I64, P, P, P, P, I32, P],
     "lidar_ball_query_f32": [P, P, P, I64, I64, I64, F32, I32, P, P],
     "lidar_ball_query_mode_f32": [P, P, P, I64, I64, I64, F32, I32, I32, P, P],
     "lidar_ball_query_grid_bytes": [I64, I64],

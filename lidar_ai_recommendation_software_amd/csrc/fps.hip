@@ -33,9 +33,10 @@ namespace {
 #ifndef FPS_THREADS
 #define FPS_THREADS 1024
 #endif
-constexpr int kThreads = FPS_THREADS;  // 16 waves: active-bucket updates and their reductions run in
-                                // parallel across waves; the merge is an LDS atomic max
-constexpr int kWaves = kThreads / 64;
+// default workgroup size: 16 waves (active-bucket updates and their reductions run in parallel
+// across waves; the merge is an LDS atomic max).  lidar_fps_ex_f32 also offers 512 (8 waves,
+// 2 buckets per lane: ~25 % longer steps, half the CU footprint beside other kernels)
+constexpr int kThreads = FPS_THREADS;
 constexpr int kGrid = 16;  // Morton cells per axis for the bucket ordering
 constexpr int kCells = kGrid * kGrid * kGrid;
 
@@ -60,12 +61,10 @@ __device__ __forceinline__ float gap(float q, float lo, float hi)
     return fmaxf(fmaxf(__fsub_rn(lo, q), __fsub_rn(q, hi)), 0.0f);
 }
 
-constexpr int kLoopWaves = kThreads / 64;
-
 // Update K active buckets of one owner slot (their loads issued together, their DPP
 // reductions interleaved): new distances against q, bucket max + its lowest-index argmax
 // point into the owner lane's registers.
-template <int K>
+template <int K, int NW>
 __device__ __forceinline__ void update_batch(uint64_t &mask, const FrameWs &W, int wave, int q, int lane,
                                              float qx, float qy, float qz, float &bd, uint32_t &bi, float *bx)
 {
@@ -80,7 +79,7 @@ __device__ __forceinline__ void update_batch(uint64_t &mask, const FrameWs &W, i
     for (int u = 0; u < K; ++u) {
         bbs[u] = __ffsll((unsigned long long)mask) - 1;
         mask &= mask - 1;
-        pos[u] = (uint32_t)((wave + kLoopWaves * (q * 64 + bbs[u])) * 64 + lane);
+        pos[u] = (uint32_t)((wave + NW * (q * 64 + bbs[u])) * 64 + lane);
     }
 #pragma unroll
     for (int u = 0; u < K; ++u) {
@@ -132,15 +131,16 @@ __device__ __forceinline__ uint64_t stamp()
 // Prologue of one frame, run by the whole workgroup: frame bbox, counting sort of the points
 // by 16^3 Morton cell into W (padded to whole buckets with dist -1 sentinels), bucket
 // bounding boxes into bbox_tab[nb][6].  Ends with a barrier.
+template <int T>
 __device__ __forceinline__ void fps_prologue(const float *__restrict__ p, int n, const FrameWs &W,
-                                             uint32_t *hist, float (*red)[kWaves], uint32_t *wsum,
+                                             uint32_t *hist, float (*red)[T / 64], uint32_t *wsum,
                                              float *bbox_tab)
 {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int npad = (n + 63) / 64 * 64;
     // ---- frame bounding box
     float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
-    for (int i = tid; i < n; i += kThreads) {
+    for (int i = tid; i < n; i += T) {
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
             float v = p[3 * i + a];
@@ -160,13 +160,13 @@ __device__ __forceinline__ void fps_prologue(const float *__restrict__ p, int n,
             red[3 + a][wave] = hi[a];
         }
     }
-    for (int c = tid; c < kCells; c += kThreads) hist[c] = 0;
+    for (int c = tid; c < kCells; c += T) hist[c] = 0;
     __syncthreads();
     float scale[3];
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
         float l = red[a][0], h = red[3 + a][0];
-        for (int w = 1; w < kWaves; ++w) {
+        for (int w = 1; w < (T / 64); ++w) {
             l = fminf(l, red[a][w]);
             h = fmaxf(h, red[3 + a][w]);
         }
@@ -185,10 +185,10 @@ __device__ __forceinline__ void fps_prologue(const float *__restrict__ p, int n,
         }
         return spread3(c[0]) | (spread3(c[1]) << 1) | (spread3(c[2]) << 2);
     };
-    for (int i = tid; i < n; i += kThreads) atomicAdd(&hist[cell_of(i)], 1u);
+    for (int i = tid; i < n; i += T) atomicAdd(&hist[cell_of(i)], 1u);
     __syncthreads();
-    {  // exclusive scan of the cell counts, kCells / kThreads consecutive cells per thread
-        constexpr int per = kCells / kThreads;
+    {  // exclusive scan of the cell counts, kCells / T consecutive cells per thread
+        constexpr int per = kCells / T;
         uint32_t v[per], s = 0;
 #pragma unroll
         for (int j = 0; j < per; ++j) {
@@ -212,12 +212,12 @@ __device__ __forceinline__ void fps_prologue(const float *__restrict__ p, int n,
         }
     }
     __syncthreads();
-    for (int i = tid; i < n; i += kThreads) {
+    for (int i = tid; i < n; i += T) {
         uint32_t pos = atomicAdd(&hist[cell_of(i)], 1u);
         W.p[pos] = make_float4(p[3 * i], p[3 * i + 1], p[3 * i + 2], __uint_as_float((uint32_t)i));
         W.d[pos] = INFINITY;
     }
-    for (int i = n + tid; i < npad; i += kThreads) {
+    for (int i = n + tid; i < npad; i += T) {
         W.p[i] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(0xffffffffu));
         W.d[i] = -1.0f;
     }
@@ -226,7 +226,7 @@ __device__ __forceinline__ void fps_prologue(const float *__restrict__ p, int n,
 
     // ---- bucket bounding boxes: every wave reduces 64-point buckets into an LDS table
     const int nb = (n + 63) / 64;
-    for (int bucket = wave; bucket < nb; bucket += kWaves) {
+    for (int bucket = wave; bucket < nb; bucket += (T / 64)) {
         const int pos = bucket * 64 + lane;
         float v[3] = {INFINITY, INFINITY, INFINITY}, u[3] = {-INFINITY, -INFINITY, -INFINITY};
         if (pos < n) {
@@ -254,8 +254,8 @@ __device__ __forceinline__ void fps_prologue(const float *__restrict__ p, int n,
 // DIAG builds (lidar_diag_fps_phases only) accumulate per-phase shader cycles per wave:
 // [0] bucket tests + active-bucket updates, [1] wave argmax + LDS publish, [2] barrier
 // wait, [3] 16-way merge, [4] active-bucket batches processed, [5] steps
-template <int BPL, bool DIAG = false>
-__global__ __launch_bounds__(kThreads) void fps_bucket_kernel(const float *__restrict__ xyz,
+template <int T, int BPL, bool DIAG = false>
+__global__ __launch_bounds__(T) void fps_bucket_kernel(const float *__restrict__ xyz,
                                                               int n, int npoint,
                                                               int32_t *__restrict__ out_idx,
                                                               float *__restrict__ out_xyz,
@@ -275,7 +275,7 @@ __global__ __launch_bounds__(kThreads) void fps_bucket_kernel(const float *__res
     // nested FPS shortcut: FPS over the first m points of an FPS ordering returns 0..m-1
     // as long as the parent's winning distance stayed > 0 — exact.
     if (prefix_ok != nullptr && prefix_ok[b] >= npoint) {
-        for (int i = tid; i < npoint; i += kThreads) {
+        for (int i = tid; i < npoint; i += T) {
             out_idx[(int64_t)b * npoint + i] = i;
             if (out_xyz) {
                 float *o = out_xyz + ((int64_t)b * npoint + i) * 3;
@@ -293,24 +293,23 @@ __global__ __launch_bounds__(kThreads) void fps_bucket_kernel(const float *__res
     FrameWs W{reinterpret_cast<float4 *>(wsb), wsb + 4 * (int64_t)npad};
 
     __shared__ uint32_t hist[kCells];
-    __shared__ float red[6][kWaves];
-    __shared__ uint32_t wsum[kWaves];
+    __shared__ float red[6][(T / 64)];
+    __shared__ uint32_t wsum[(T / 64)];
     // per-step merge: every wave submits its argmax as one 64-bit key to an LDS atomic max
     // (triple-buffered so a slot is cleared two barriers after its last read) and its
     // coordinates to a per-wave slot (double-buffered); one barrier per step
     __shared__ unsigned long long mkey[3];
-    __shared__ __attribute__((aligned(16))) float mcrd[2][kWaves][4];
+    __shared__ __attribute__((aligned(16))) float mcrd[2][(T / 64)][4];
 
     extern __shared__ float bbox_tab[];  // [nb][6]
-    fps_prologue(p, n, W, hist, red, wsum, bbox_tab);
+    fps_prologue<T>(p, n, W, hist, red, wsum, bbox_tab);
     const int nb = (n + 63) / 64;
-    static_assert(kWaves == kLoopWaves, "every wave runs the step loop");
-    // ---- per-bucket state in the owner lane: bucket = wave + 4 * (q * 64 + lane)
+        // ---- per-bucket state in the owner lane: bucket = wave + 4 * (q * 64 + lane)
     float bmin[BPL][3], bmax[BPL][3], bx[BPL][3], bd[BPL];
     uint32_t bi[BPL];
 #pragma unroll
     for (int q = 0; q < BPL; ++q) {
-        const int bucket = wave + kLoopWaves * (q * 64 + lane);
+        const int bucket = wave + (T / 64) * (q * 64 + lane);
         const bool have = bucket < nb;
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
@@ -362,13 +361,13 @@ __global__ __launch_bounds__(kThreads) void fps_bucket_kernel(const float *__res
                 if constexpr (DIAG) dacc[4]++;
                 const int cnt = __popcll(mask);
                 if (cnt >= 4)
-                    update_batch<4>(mask, W, wave, q, lane, qx, qy, qz, bd[q], bi[q], bx[q]);
+                    update_batch<4, T / 64>(mask, W, wave, q, lane, qx, qy, qz, bd[q], bi[q], bx[q]);
                 else if (cnt == 3)  // one round trip instead of 2 + 1
-                    update_batch<3>(mask, W, wave, q, lane, qx, qy, qz, bd[q], bi[q], bx[q]);
+                    update_batch<3, T / 64>(mask, W, wave, q, lane, qx, qy, qz, bd[q], bi[q], bx[q]);
                 else if (cnt >= 2)
-                    update_batch<2>(mask, W, wave, q, lane, qx, qy, qz, bd[q], bi[q], bx[q]);
+                    update_batch<2, T / 64>(mask, W, wave, q, lane, qx, qy, qz, bd[q], bi[q], bx[q]);
                 else
-                    update_batch<1>(mask, W, wave, q, lane, qx, qy, qz, bd[q], bi[q], bx[q]);
+                    update_batch<1, T / 64>(mask, W, wave, q, lane, qx, qy, qz, bd[q], bi[q], bx[q]);
             }
         }
         if constexpr (DIAG) {
@@ -440,7 +439,7 @@ __global__ __launch_bounds__(kThreads) void fps_bucket_kernel(const float *__res
             // LDS round trip after the barrier instead of two dependent ones
             const unsigned long long key = mkey[slot];
             float4 cand = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            if (lane < kWaves)  // 16 lanes read: 256 B per wave instead of 1 KiB of LDS traffic
+            if (lane < (T / 64))  // 16 lanes read: 256 B per wave instead of 1 KiB of LDS traffic
                 cand = *reinterpret_cast<const float4 *>(mcrd[cslot][lane]);
             const int ww = __builtin_amdgcn_readfirstlane((int)(key & 15u));
             const float gdist = __uint_as_float((uint32_t)(key >> 32));
@@ -472,32 +471,20 @@ __global__ __launch_bounds__(kThreads) void fps_bucket_kernel(const float *__res
     if (first_zero && tid == 0) first_zero[b] = zero_at;
     if constexpr (DIAG) {
         if (lane == 0)
-            for (int k = 0; k < 6; ++k) diag[((int64_t)b * kWaves + wave) * 6 + k] = dacc[k];
+            for (int k = 0; k < 6; ++k) diag[((int64_t)b * (T / 64) + wave) * 6 + k] = dacc[k];
     }
 }
 
 }  // namespace
 
-LIDAR_EXPORT int lidar_fps_f32(lidar_handle *h, const float *xyz, int64_t batch, int64_t n,
-                               int64_t npoint, int32_t *idx, float *new_xyz, int32_t *first_zero,
-                               const int32_t *prefix_ok, void *stream)
+template <int T>
+static int launch_fps(const float *xyz, int64_t batch, int64_t n, int64_t npoint, int32_t *idx, float *new_xyz,
+                      int32_t *first_zero, const int32_t *prefix_ok, float *ws, int64_t stride, hipStream_t s)
 {
-    REQUIRE(h && xyz && idx, "lidar_fps_f32: null pointer");
-    REQUIRE(batch >= 0 && n >= 1 && npoint >= 1, "lidar_fps_f32: need n >= 1 and npoint >= 1");
-    REQUIRE(n <= 4 * 65536, "lidar_fps_f32: n > 262144 points per frame");
-    REQUIRE((n + 63) / 64 <= 8 * kLoopWaves * 64, "lidar_fps_f32: too many buckets for this build");
-    REQUIRE(batch <= 0x7fffffff, "lidar_fps_f32: batch too large");
-    if (batch == 0) return LIDAR_OK;
-    HIP_TRY(hipSetDevice(h->device));
-    REQUIRE(prefix_ok == nullptr || npoint <= n, "lidar_fps_f32: prefix_ok needs npoint <= n");
-    int64_t stride = lidar::align_up(5 * lidar::align_up(n, 64), 64);
-    float *ws = static_cast<float *>(lidar::workspace(h, (uint64_t)(batch * stride) * 4));
-    if (!ws) return LIDAR_ENOMEM;
-    hipStream_t s = static_cast<hipStream_t>(stream);
-    dim3 grid((unsigned)batch), block(kThreads);
+    dim3 grid((unsigned)batch), block(T);
     const int nb = (int)((n + 63) / 64);
     const size_t lds = (size_t)nb * 6 * sizeof(float);
-    const int lanes = kLoopWaves * 64;
+    const int lanes = T;  // one bucket per lane and slot
     auto go = [&](auto kern) -> int {
         HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -506,13 +493,44 @@ LIDAR_EXPORT int lidar_fps_f32(lidar_handle *h, const float *xyz, int64_t batch,
         return LIDAR_OK;
     };
     int rc;
-    if (nb <= lanes) rc = go(fps_bucket_kernel<1>);
-    else if (nb <= 2 * lanes) rc = go(fps_bucket_kernel<2>);
-    else if (nb <= 4 * lanes) rc = go(fps_bucket_kernel<4>);
-    else rc = go(fps_bucket_kernel<8>);
+    if (nb <= lanes) rc = go(fps_bucket_kernel<T, 1>);
+    else if (nb <= 2 * lanes) rc = go(fps_bucket_kernel<T, 2>);
+    else if (nb <= 4 * lanes) rc = go(fps_bucket_kernel<T, 4>);
+    else rc = go(fps_bucket_kernel<T, 8>);
     if (rc) return rc;
     LAUNCH_CHECK();
     return LIDAR_OK;
+}
+
+// threads: workgroup size per frame, 0 (the build default, 1024), 1024 or 512 — same results
+LIDAR_EXPORT int lidar_fps_ex_f32(lidar_handle *h, const float *xyz, int64_t batch, int64_t n, int64_t npoint,
+                                  int32_t *idx, float *new_xyz, int32_t *first_zero, const int32_t *prefix_ok,
+                                  int32_t threads, void *stream)
+{
+    REQUIRE(h && xyz && idx, "lidar_fps_f32: null pointer");
+    REQUIRE(batch >= 0 && n >= 1 && npoint >= 1, "lidar_fps_f32: need n >= 1 and npoint >= 1");
+    REQUIRE(n <= 4 * 65536, "lidar_fps_f32: n > 262144 points per frame");
+    if (threads == 0) threads = kThreads;
+    REQUIRE(threads == 1024 || threads == 512, "lidar_fps_ex_f32: threads must be 0, 512 or 1024");
+    REQUIRE((n + 63) / 64 <= 8 * (int64_t)threads, "lidar_fps_f32: too many buckets for this workgroup size");
+    REQUIRE(batch <= 0x7fffffff, "lidar_fps_f32: batch too large");
+    if (batch == 0) return LIDAR_OK;
+    HIP_TRY(hipSetDevice(h->device));
+    REQUIRE(prefix_ok == nullptr || npoint <= n, "lidar_fps_f32: prefix_ok needs npoint <= n");
+    int64_t stride = lidar::align_up(5 * lidar::align_up(n, 64), 64);
+    float *ws = static_cast<float *>(lidar::workspace(h, (uint64_t)(batch * stride) * 4));
+    if (!ws) return LIDAR_ENOMEM;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (threads == 512)
+        return launch_fps<512>(xyz, batch, n, npoint, idx, new_xyz, first_zero, prefix_ok, ws, stride, s);
+    return launch_fps<1024>(xyz, batch, n, npoint, idx, new_xyz, first_zero, prefix_ok, ws, stride, s);
+}
+
+LIDAR_EXPORT int lidar_fps_f32(lidar_handle *h, const float *xyz, int64_t batch, int64_t n, int64_t npoint,
+                               int32_t *idx, float *new_xyz, int32_t *first_zero, const int32_t *prefix_ok,
+                               void *stream)
+{
+    return lidar_fps_ex_f32(h, xyz, batch, n, npoint, idx, new_xyz, first_zero, prefix_ok, 0, stream);
 }
 
 // diagnostic build (not part of the product ABI): per-wave phase cycle totals of one FPS run
@@ -525,10 +543,10 @@ LIDAR_EXPORT int lidar_diag_fps_phases(lidar_handle *h, const float *xyz, int64_
     float *ws = static_cast<float *>(lidar::workspace(h, (uint64_t)(batch * stride) * 4));
     if (!ws) return LIDAR_ENOMEM;
     const size_t lds = (size_t)((n + 63) / 64) * 6 * sizeof(float);
-    REQUIRE((n + 63) / 64 <= kLoopWaves * 64, "lidar_diag_fps_phases: n too large for BPL=1");
-    HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(fps_bucket_kernel<1, true>),
+    REQUIRE((n + 63) / 64 <= kThreads, "lidar_diag_fps_phases: n too large for BPL=1");
+    HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(fps_bucket_kernel<kThreads, 1, true>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL((fps_bucket_kernel<1, true>), dim3((unsigned)batch), dim3(kThreads), lds,
+    hipLaunchKernelGGL((fps_bucket_kernel<kThreads, 1, true>), dim3((unsigned)batch), dim3(kThreads), lds,
                        static_cast<hipStream_t>(stream), xyz, (int)n, (int)npoint, idx, nullptr, nullptr,
                        nullptr, ws, stride, diag);
     LAUNCH_CHECK();

@@ -90,7 +90,7 @@ def _dev_check(*ts):
 
 
 def farthest_point_sample(xyz, npoint, return_xyz=False, first_zero=None, prefix_ok=None, slot=0,
-                          out_idx=None, out_xyz=None):
+                          out_idx=None, out_xyz=None, threads=0):
     """xyz (B, N, 3) float32 CUDA -> idx (B, npoint) int32 [, new_xyz (B, npoint, 3)].
 
     first_zero: optional (B,) int32 output — first step whose winning distance was 0.
@@ -105,8 +105,9 @@ def farthest_point_sample(xyz, npoint, return_xyz=False, first_zero=None, prefix
     if return_xyz:
         new_xyz = out_xyz if out_xyz is not None else torch.empty((B, npoint, 3), dtype=torch.float32,
                                                                   device=xyz.device)
-    nat.call("lidar_fps_f32", nat.handle(xyz.device.index, slot), nat.ptr(xyz), B, N, npoint,
-             nat.ptr(idx), nat.ptr(new_xyz), nat.ptr(first_zero), nat.ptr(prefix_ok), nat.stream_ptr())
+    nat.call("lidar_fps_ex_f32", nat.handle(xyz.device.index, slot), nat.ptr(xyz), B, N, npoint,
+             nat.ptr(idx), nat.ptr(new_xyz), nat.ptr(first_zero), nat.ptr(prefix_ok), int(threads),
+             nat.stream_ptr())
     return (idx, new_xyz) if return_xyz else idx
 
 
@@ -610,7 +611,7 @@ class StreamingSSG:
     """
 
     def __init__(self, backbone, batch, n, depth=1, side_priority=0, side_cus=0, cu_layout="xcd", fps_group=1,
-                 bq_on_main=False):
+                 bq_on_main=False, fps_threads=0):
         """side_cus > 0: the SA1 FPS / ball-query streams run on `side_cus` CUs and the
         main stream on the rest (CU-masked HIP streams; measured slower).
         cu_layout "xcd" takes side_cus/8 CUs of each of the 8 XCDs (mask bit = 32*xcd + cu),
@@ -618,6 +619,7 @@ class StreamingSSG:
         self.bb = backbone
         self.B, self.N, self.depth, self.G = batch, n, depth, max(1, int(fps_group))
         self.bq_on_main = bool(bq_on_main)  # level-0 ball queries on the main stream instead
+        self.fps_threads = int(fps_threads)  # SA1 FPS workgroup size (0 = 1024; 512: half the CU footprint)
         dev = backbone.device
         lvl0 = backbone.levels[0]
         self.M1 = max(1, n // lvl0["div"])
@@ -688,7 +690,7 @@ class StreamingSSG:
                 xj.record_stream(fs)
             _call(self.bb.timers, "sa1_fps", farthest_point_sample, x, self.M1, return_xyz=True,
                   first_zero=self.fz[slot][:g], slot=1 + k % self.depth, out_idx=self.idx[slot][:g],
-                  out_xyz=self.cxyz[slot][:g])
+                  out_xyz=self.cxyz[slot][:g], threads=self.fps_threads)
             lvl0 = self.bb.levels[0]
             if self.grid[slot] is not None:
                 br = max(lvl0["branches"], key=lambda b: b["r"])

@@ -44,9 +44,10 @@ def frames_for(kind, b, n, seed):
     ("clumped", 2, 5000, 300), ("dups", 2, 3000, 2000), ("grid", 1, 4096, 600),
     ("uniform", 2, 1, 4), ("uniform", 1, 37, 60), ("uniform", 1, 64, 64),
 ])
-def test_fps_bit_exact(cuda, kind, b, n, m):
+@pytest.mark.parametrize("threads", [0, 512])
+def test_fps_bit_exact(cuda, kind, b, n, m, threads):
     x = frames_for(kind, b, n, 11)
-    idx, nx = pn.farthest_point_sample(torch.from_numpy(x).to(cuda), m, return_xyz=True)
+    idx, nx = pn.farthest_point_sample(torch.from_numpy(x).to(cuda), m, return_xyz=True, threads=threads)
     want = tier_n.fps(x, m)
     got = idx.cpu().numpy()
     assert np.array_equal(got, want), f"{(got != want).sum()} indices differ, first {np.argwhere(got != want)[:3]}"
@@ -367,6 +368,21 @@ def test_streaming_grouped_fps_matches_forward(cuda, cfg_name, dtype, group, dep
     xs = [torch.from_numpy(unit_frames(2, 4096, 10 + s)).to(cuda) for s in range(nb)]
     want = [bb.forward(x)[0] for x in xs]
     got = pn.StreamingSSG(bb, 2, 4096, depth=depth, fps_group=group).run(xs)
+    torch.cuda.synchronize()
+    assert len(got) == nb
+    for a, b in zip(got, want):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("group,depth,threads,nb", [(3, 3, 512, 7), (2, 2, 1024, 4), (4, 2, 512, 5)])
+def test_streaming_bench_policy_matches_forward(cuda, group, depth, threads, nb):
+    """the bench's executor policy: SA1 ball queries on the main stream answered from grids
+    binned on the side streams, 512-thread SA1 FPS, groups of batches (partial last group)."""
+    bb = pn.PointNet2Backbone(pn.SSG, device=cuda, seed=4)
+    xs = [torch.from_numpy(unit_frames(2, 8192, 50 + s)).to(cuda) for s in range(nb)]
+    want = [bb.forward(x)[0] for x in xs]
+    pipe = pn.StreamingSSG(bb, 2, 8192, depth=depth, fps_group=group, bq_on_main=True, fps_threads=threads)
+    got = pipe.run(xs)
     torch.cuda.synchronize()
     assert len(got) == nb
     for a, b in zip(got, want):

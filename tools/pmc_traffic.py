@@ -33,7 +33,7 @@ def rows(d):
     return list(csv.DictReader(open(f[0])))
 
 
-FRAMES_PER_LAUNCH = 64  # bench.py defaults: 32 frames per batch x fps_group 2 per main-stream pass
+FRAMES_PER_LAUNCH = 96  # bench.py defaults: 32 frames per batch x fps_group 3 per main-stream pass
 
 
 def label(name, grid, F=FRAMES_PER_LAUNCH):
@@ -46,13 +46,17 @@ def label(name, grid, F=FRAMES_PER_LAUNCH):
         return "fps"  # split into sa1/sa2 by duration below
     if "ball_query_kernel" in name:
         return {F * 4096 * 8: "sa1_ball_query", F * 1024 * 8: "sa2_ball_query"}.get(grid)
+    if "bq_grid_kernel" in name:  # one wavefront per centre
+        return {F * 4096 * 64: "sa1_ball_query", F * 1024 * 64: "sa2_ball_query"}.get(grid)
+    if "bq_bin_kernel" in name:
+        return "bq_bin"  # one 1024-thread workgroup per frame: SA1 (65536 pts) vs SA2 (4096) by duration
     if any(k in name for k in ("sa_group_mlp_kernel<0, 64, 64, 128, 32", "sa_pre_lds_kernel<64, 64, 128, 32, true",
                                 "sa16_kernel<64, 64, 128, 32, true", "sa_x3_kernel<64, 64, 128, 32, true")):
         return "sa1_group_mlp"
     if any(k in name for k in ("sa_group_mlp_kernel<128, 128, 128, 256, 64", "sa_pre_lds_kernel<128, 128, 256, 64",
                                 "sa16_kernel<128, 128, 256, 64, false", "sa_x3_kernel<128, 128, 256, 64, false")):
         return "sa2_group_mlp"
-    if "dense_relu_kernel" in name or "dense_x3_kernel" in name:
+    if "dense_relu_kernel" in name or "dense_x3_kernel" in name or "dense_x3p_kernel" in name:
         return {F * 4096 * 2: "dense_shared", F * 1024 * 2: "sa2_layer1_points", F * 1024 * 4: "sa3_dense1",
                 F * 1024 * 16: "sa3_dense3_pool"}.get(grid)
     if "concat_xyz_pad" in name:
@@ -62,7 +66,7 @@ def label(name, grid, F=FRAMES_PER_LAUNCH):
 
 def per_label(rs, counter):
     acc = defaultdict(list)
-    fps = []
+    fps, bins = [], []
     nsh = 0
     for r in sorted(rs, key=lambda r: int(r["Dispatch_Id"])):
         if r["Counter_Name"] != counter:
@@ -71,6 +75,8 @@ def per_label(rs, counter):
         lab = label(r["Kernel_Name"], int(r["Grid_Size"]))
         if lab == "fps":
             fps.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"]), v))
+        elif lab == "bq_bin":
+            bins.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"]), v))
         elif lab == "dense_shared":
             acc["sa2_layer1_points" if nsh % 2 == 0 else "sa3_dense2"].append(v)
             nsh += 1
@@ -81,6 +87,11 @@ def per_label(rs, counter):
         half = len(fps) // 2
         acc["sa2_fps"] = [v for _, v in fps[:half]]
         acc["sa1_fps"] = [v for _, v in fps[half:]]
+    if bins:  # SA1's binning (65536-point frames, side stream) vs SA2's (4096 points, inside its query)
+        bins.sort()
+        half = len(bins) // 2
+        acc["sa2_bq_bin"] = [v for _, v in bins[:half]]
+        acc["sa1_bq_bin"] = [v for _, v in bins[half:]]
     # sa2_layer1_points = its two GEMMs (point rows, centre rows) per pass: report their sum
     if "sa2_layer1_points" in acc:
         v = acc["sa2_layer1_points"]

@@ -214,6 +214,8 @@ def main():
                     help="SA layers 2-3 on the split-bf16 (x3) kernels: fp32 arithmetic within the 1e-4 "
                          "contract; 0 = native fp32 MFMA kernels")
     ap.add_argument("--bq-main", type=int, default=1, help="1: SA1 ball queries on the main stream")
+    ap.add_argument("--l1-side", type=int, default=0,
+                    help="1: SA2's FPS and ball queries (they need only SA1's centres) on the side streams")
     ap.add_argument("--no-fp32-mfma-leg", action="store_true",
                     help="skip the extra measurement of the native fp32-MFMA kernels (when --x3 is on)")
     ap.add_argument("--no-extras", action="store_true", help="skip the configs[1]/[4] side measurements")
@@ -250,7 +252,8 @@ def main():
         # one workgroup per frame) with batch k's MFMA levels; results are identical to forward()
         pipe = pn.StreamingSSG(bb, B, N, depth=depth, side_priority=args.side_priority,
                                side_cus=args.side_cus, cu_layout=args.cu_layout, fps_group=args.fps_group,
-                               bq_on_main=bool(args.bq_main), fps_threads=args.fps_threads)
+                               bq_on_main=bool(args.bq_main), fps_threads=args.fps_threads,
+                               level1_on_side=bool(args.l1_side))
         ref, _ = bb.forward(x)
         outs = pipe.run([x] * max(2, warmup))
         torch.cuda.synchronize(dev)
@@ -296,6 +299,8 @@ def main():
     # dominates the main chain's device time; the chain lengths say which chain bounds a step.
     # issued on the side streams, overlapped with the rest
     side = ("sa1_fps", "sa1_bq_bin") if args.bq_main else ("sa1_fps", "sa1_ball_query")
+    if args.l1_side:
+        side += ("sa2_fps", "sa2_ball_query")
     main = {k: v for k, v in kern.items() if k not in side}
     side_ms = sum(kern.get(k, 0) for k in side) / args.depth
     dom = max(main, key=lambda k: main[k])

@@ -129,7 +129,10 @@ def _parse_fast(raw, locate):
     """The data section parsed by liblidar_amd's C parser (lidar_parse_ascii_xyz), or None
     when the input needs Python's own text rules (non-ASCII / exotic whitespace, bare CR
     line breaks, a header beyond the first 64 KiB, or a token only float() parses)."""
-    if _SLOW_BYTES.search(raw, 0, 65536):  # the data section is checked by the C scanner
+    # the data section is checked by the C scanner; the window reaches one byte past the head
+    # so that a CRLF split by the 64 KiB cut is not taken for a bare CR
+    m = _SLOW_BYTES.search(raw, 0, 65537)
+    if m and m.start() < 65536:
         return None
     head = raw[:65536].decode("ascii")
     lines = head.splitlines(keepends=True)

@@ -462,12 +462,18 @@ class PointNet2Backbone:
                         br["pre"]["wq_x3"] = pack_dense_x3(br["pre"]["wq"])
         self.timers = None  # set to a _Timers() to time every launch
 
-    def forward_from_sa1_fps(self, xyz, idx1, new_xyz1, fz1, gidx1=None, grid1=None):
+    def forward_from_sa1_fps(self, xyz, idx1, new_xyz1, fz1, gidx1=None, grid1=None, pre=None):
         """forward() with level 0's FPS (and ball queries, or the ball-query binning of the
-        frames) already computed (StreamingSSG)."""
-        return self.forward(xyz, pre_fps=(idx1, new_xyz1, fz1), pre_bq=gidx1, pre_grid=grid1)[0]
+        frames) already computed (StreamingSSG); `pre` adds precomputed later levels."""
+        pre = dict(pre or {})
+        pre[0] = {"fps": (idx1, new_xyz1, fz1), "bq": gidx1, "grid": grid1}
+        return self.forward(xyz, pre=pre)[0]
 
-    def forward(self, xyz, keep_levels=False, pre_fps=None, pre_bq=None, pre_grid=None):
+    def forward(self, xyz, keep_levels=False, pre=None):
+        """pre: {level: {"fps": (idx, new_xyz, first_zero), "bq": [gidx per branch] or None,
+        "grid": ball-query grid of this level's input points or None}} — work already done
+        for those levels (StreamingSSG's side streams); every other step runs here."""
+        pre = pre or {}
         B, N, _ = xyz.shape
         N0 = N  # npoint_div is relative to the input frame (N/16, N/64)
         feats = None
@@ -478,8 +484,9 @@ class PointNet2Backbone:
             if lvl.get("group_all"):
                 return self._group_all(xyz, feats, lvl, rows), out_levels
             M = max(1, N0 // lvl["div"])
-            if li == 0 and pre_fps is not None:
-                idx, new_xyz, nfz = pre_fps
+            pl = pre.get(li, {})
+            if pl.get("fps") is not None:
+                idx, new_xyz, nfz = pl["fps"]
             else:
                 nfz = torch.empty(B, dtype=torch.int32, device=xyz.device)
                 idx, new_xyz = _call(self.timers, f"sa{li + 1}_fps", farthest_point_sample, xyz, M,
@@ -501,11 +508,11 @@ class PointNet2Backbone:
             off = 0
             for bi_, br in enumerate(lvl["branches"]):
                 tag = f"sa{li + 1}" + (f"_b{bi_}" if len(lvl["branches"]) > 1 else "")
-                if li == 0 and pre_bq is not None:
-                    gidx = pre_bq[bi_]
+                if pl.get("bq") is not None:
+                    gidx = pl["bq"][bi_]
                 else:
                     gidx = _call(self.timers, f"{tag}_ball_query", ball_query, br["r"], br["ns"], xyz, new_xyz,
-                                 grid=pre_grid if li == 0 else None)
+                                 grid=pl.get("grid"))
                 if "packed_x3" in br:
                     p16, q16 = (pq[bi_] if pq is not None else (xyz, new_xyz))
                     _call(self.timers, f"{tag}_group_mlp", group_mlp_x3, p16, q16, gidx, N, br["packed_x3"],
@@ -611,7 +618,7 @@ class StreamingSSG:
     """
 
     def __init__(self, backbone, batch, n, depth=1, side_priority=0, side_cus=0, cu_layout="xcd", fps_group=1,
-                 bq_on_main=False, fps_threads=0):
+                 bq_on_main=False, fps_threads=0, level1_on_side=False):
         """side_cus > 0: the SA1 FPS / ball-query streams run on `side_cus` CUs and the
         main stream on the rest (CU-masked HIP streams; measured slower).
         cu_layout "xcd" takes side_cus/8 CUs of each of the 8 XCDs (mask bit = 32*xcd + cu),
@@ -620,6 +627,10 @@ class StreamingSSG:
         self.B, self.N, self.depth, self.G = batch, n, depth, max(1, int(fps_group))
         self.bq_on_main = bool(bq_on_main)  # level-0 ball queries on the main stream instead
         self.fps_threads = int(fps_threads)  # SA1 FPS workgroup size (0 = 1024; 512: half the CU footprint)
+        # level1_on_side: SA2's FPS (over SA1's centres) and ball queries depend only on SA1's FPS
+        # output, so they can run on the side stream too (balances the two chains)
+        lvl1 = backbone.levels[1] if len(backbone.levels) > 1 else None
+        self.l1 = bool(level1_on_side) and lvl1 is not None and not lvl1.get("group_all")
         dev = backbone.device
         lvl0 = backbone.levels[0]
         self.M1 = max(1, n // lvl0["div"])
@@ -648,6 +659,13 @@ class StreamingSSG:
         # (it depends only on the frames), once for all branches at the largest radius
         self.grid = [ball_query_grid_buffer(GB, n, dev) if self.bq_on_main and n >= BQ_GRID_MIN_N else None
                      for _ in range(nslot)]
+        if self.l1:
+            self.M2 = max(1, n // lvl1["div"])
+            self.idx2 = [torch.empty((GB, self.M2), dtype=torch.int32, device=dev) for _ in range(nslot)]
+            self.cxyz2 = [torch.empty((GB, self.M2, 3), dtype=torch.float32, device=dev) for _ in range(nslot)]
+            self.fz2 = [torch.empty(GB, dtype=torch.int32, device=dev) for _ in range(nslot)]
+            self.gidx2 = [[torch.empty((GB, self.M2, br["ns"]), dtype=torch.int32, device=dev)
+                           for br in lvl1["branches"]] for _ in range(nslot)]
         self.fps_done = [torch.cuda.Event() for _ in range(nslot)]
         self.slot_free = [torch.cuda.Event() for _ in range(nslot)]
         for e in self.slot_free:
@@ -700,6 +718,17 @@ class StreamingSSG:
                 tag = "sa1" + (f"_b{bi_}" if len(lvl0["branches"]) > 1 else "")
                 _call(self.bb.timers, f"{tag}_ball_query", ball_query, br["r"], br["ns"], x, self.cxyz[slot][:g],
                       out=self.gidx[slot][bi_][:g], slot=1 + k % self.depth)
+            if self.l1:
+                hs = 1 + k % self.depth
+                c1 = self.cxyz[slot][:g]
+                _call(self.bb.timers, "sa2_fps", farthest_point_sample, c1, self.M2, return_xyz=True,
+                      first_zero=self.fz2[slot][:g], prefix_ok=self.fz[slot][:g], slot=hs,
+                      out_idx=self.idx2[slot][:g], out_xyz=self.cxyz2[slot][:g])
+                lvl1 = self.bb.levels[1]
+                for bi_, br in enumerate(lvl1["branches"]):
+                    tag = "sa2" + (f"_b{bi_}" if len(lvl1["branches"]) > 1 else "")
+                    _call(self.bb.timers, f"{tag}_ball_query", ball_query, br["r"], br["ns"], c1,
+                          self.cxyz2[slot][:g], out=self.gidx2[slot][bi_][:g], slot=hs)
             self.fps_done[slot].record(fs)
         return slot
 
@@ -709,9 +738,13 @@ class StreamingSSG:
         main.wait_event(self.fps_done[slot])
         B, g = self.B, len(xs) * self.B
         x = self.stage[slot][:g] if self.G > 1 else xs[0]
+        pre = None
+        if self.l1:
+            pre = {1: {"fps": (self.idx2[slot][:g], self.cxyz2[slot][:g], self.fz2[slot][:g]),
+                       "bq": [gi[:g] for gi in self.gidx2[slot]]}}
         out = self.bb.forward_from_sa1_fps(x, self.idx[slot][:g], self.cxyz[slot][:g], self.fz[slot][:g],
                                            None if self.bq_on_main else [gi[:g] for gi in self.gidx[slot]],
-                                           self.grid[slot])
+                                           self.grid[slot], pre=pre)
         self.slot_free[slot].record(main)
         return list(out.split(B)) if len(xs) > 1 else [out]
 

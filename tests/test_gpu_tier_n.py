@@ -374,14 +374,17 @@ def test_streaming_grouped_fps_matches_forward(cuda, cfg_name, dtype, group, dep
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("group,depth,threads,nb", [(3, 3, 512, 7), (2, 2, 1024, 4), (4, 2, 512, 5)])
-def test_streaming_bench_policy_matches_forward(cuda, group, depth, threads, nb):
+@pytest.mark.parametrize("group,depth,threads,nb,l1", [(3, 3, 512, 7, False), (2, 2, 1024, 4, False),
+                                                       (4, 2, 512, 5, False), (3, 3, 512, 7, True),
+                                                       (2, 3, 1024, 3, True)])
+def test_streaming_bench_policy_matches_forward(cuda, group, depth, threads, nb, l1):
     """the bench's executor policy: SA1 ball queries on the main stream answered from grids
     binned on the side streams, 512-thread SA1 FPS, groups of batches (partial last group)."""
     bb = pn.PointNet2Backbone(pn.SSG, device=cuda, seed=4)
     xs = [torch.from_numpy(unit_frames(2, 8192, 50 + s)).to(cuda) for s in range(nb)]
     want = [bb.forward(x)[0] for x in xs]
-    pipe = pn.StreamingSSG(bb, 2, 8192, depth=depth, fps_group=group, bq_on_main=True, fps_threads=threads)
+    pipe = pn.StreamingSSG(bb, 2, 8192, depth=depth, fps_group=group, bq_on_main=True, fps_threads=threads,
+                           level1_on_side=l1)
     got = pipe.run(xs)
     torch.cuda.synchronize()
     assert len(got) == nb

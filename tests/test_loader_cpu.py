@@ -39,7 +39,7 @@ def _ply(rows, nvert=None, extra=""):
 @pytest.mark.parametrize("fmt", ["pcd", "ply"])
 @pytest.mark.parametrize("variant", ["plain", "crlf", "blank_and_short", "ply_fewer_vertices", "underscore"])
 def test_fast_parser_matches_reference_loop(tmp_path, fmt, variant):
-    rng = np.random.default_rng(hash((fmt, variant)) % 2**32)
+    rng = np.random.default_rng(sum(map(ord, fmt + variant)))  # stable across processes (str hash is not)
     rows = _numbers(rng, 3000)
     extra = ""
     if variant == "blank_and_short":
@@ -91,3 +91,20 @@ def test_python_text_rules_take_over(tmp_path, inject):
     got = dp.load_lidar_data(str(path))
     want = dp._read_ascii_body_py(text if inject != "\r" else text, dp._pcd_body_start)
     assert np.array_equal(got, want)
+
+
+def test_fast_parser_crlf_split_at_head_cut(tmp_path):
+    """a CRLF whose CR is the last byte of the 64 KiB head window is a line end, not a bare CR"""
+    rows = _numbers(np.random.default_rng(3), 3000)
+    text = _ply(rows).replace("\n", "\r\n")
+    raw = text.encode()
+    k = raw.index(b"\r\n", 65536 - 80)
+    pad = 65535 - k  # shift the first CRLF after the cut so that its CR sits at byte 65535
+    text = text.replace("end_header\r\n", "end_header" + " " * pad + "\r\n", 1)
+    assert text.encode()[65535:65537] == b"\r\n"
+    assert dp._parse_fast(text.encode(), dp._ply_body) is not None
+    path = tmp_path / "cut.ply"
+    path.write_bytes(text.encode())
+    got = dp.load_lidar_data(str(path))
+    want = dp._read_ascii_body_py(text, dp._ply_body)
+    assert np.array_equal(got.view(np.uint64), want.view(np.uint64))

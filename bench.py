@@ -205,7 +205,7 @@ def main():
     ap.add_argument("--side-priority", type=int, default=0, help="HIP priority of the FPS streams (<0 = high)")
     ap.add_argument("--fps-group", type=int, default=3, help="batches per SA1-FPS launch (StreamingSSG fps_group)")
     ap.add_argument("--side-cus", type=int, default=0, help="CUs reserved for the SA1 FPS streams (0 = shared)")
-    ap.add_argument("--fps-threads", type=int, default=512, choices=[512, 1024],
+    ap.add_argument("--fps-threads", type=int, default=512, choices=[256, 512, 1024],
                     help="SA1 FPS workgroup size in the pipeline (512: half the CU footprint beside the MLPs)")
     ap.add_argument("--cu-layout", default="xcd", choices=["xcd", "low"])
     ap.add_argument("--mlp16", default="pre", choices=["0", "1", "pre", "xyz"],

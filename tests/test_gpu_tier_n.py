@@ -11,6 +11,7 @@ import torch
 
 from oracle import tier_n
 from lidar_ai_recommendation_software_amd import pointnet2 as pn
+from lidar_ai_recommendation_software_amd._native import LidarError
 from lidar_ai_recommendation_software_amd.synthetic import unit_frames
 
 pytestmark = pytest.mark.gpu
@@ -44,9 +45,13 @@ def frames_for(kind, b, n, seed):
     ("clumped", 2, 5000, 300), ("dups", 2, 3000, 2000), ("grid", 1, 4096, 600),
     ("uniform", 2, 1, 4), ("uniform", 1, 37, 60), ("uniform", 1, 64, 64),
 ])
-@pytest.mark.parametrize("threads", [0, 512])
+@pytest.mark.parametrize("threads", [0, 512, 256])
 def test_fps_bit_exact(cuda, kind, b, n, m, threads):
     x = frames_for(kind, b, n, 11)
+    if threads and (n + 63) // 64 > 8 * threads:  # 8 buckets per lane at most
+        with pytest.raises(LidarError, match="too many buckets"):
+            pn.farthest_point_sample(torch.from_numpy(x).to(cuda), m, threads=threads)
+        return
     idx, nx = pn.farthest_point_sample(torch.from_numpy(x).to(cuda), m, return_xyz=True, threads=threads)
     want = tier_n.fps(x, m)
     got = idx.cpu().numpy()

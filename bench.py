@@ -313,7 +313,10 @@ def main():
         per_launch = per_frame * B * args.fps_group  # one launch covers a group of batches
         avg_s = kern[name] / 1e3
         if bound == "mfma":
-            x3k = x3_opt and name in ("sa1_group_mlp", "sa2_group_mlp")
+            # with x3 on, the grouped SA kernels AND the dense GEMMs (SA2's per-point layer 1,
+            # group_all's three layers: dense_x3p) issue 3 bf16 MFMA products per fp32 product
+            x3k = x3_opt and name in ("sa1_group_mlp", "sa2_group_mlp", "sa2_layer1_points",
+                                      "sa3_dense1", "sa3_dense2", "sa3_dense3_pool")
             a, p, u = per_launch / avg_s / 1e12, X3_PEAK_TFLOPS if x3k else FP32_MFMA_PEAK_TFLOPS, "TFLOP/s"
         else:
             a, p, u = per_launch / avg_s / 1e9, HBM_PEAK_GBS, "GB/s"

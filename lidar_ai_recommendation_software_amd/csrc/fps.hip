@@ -66,7 +66,8 @@ __device__ __forceinline__ float gap(float q, float lo, float hi)
 // point into the owner lane's registers.
 template <int K, int NW>
 __device__ __forceinline__ void update_batch(uint64_t &mask, const FrameWs &W, int wave, int q, int lane,
-                                             float qx, float qy, float qz, float &bd, uint32_t &bi, float *bx)
+                                             float qx, float qy, float qz, float &bd, uint32_t &bi, float *bx,
+                                             int &bp, int target, bool &hit)
 {
     // branch-free: the workspace is padded to whole buckets with sentinel points
     // (dist -1: never the max, never updated since every real d >= 0)
@@ -90,16 +91,29 @@ __device__ __forceinline__ void update_batch(uint64_t &mask, const FrameWs &W, i
     for (int u = 0; u < K; ++u) I[u] = __float_as_uint(P[u].w);
     // distances in bit space (>= +0 or the -1 sentinel: signed int order = float order)
     int od[K], dm[K];
+    // a bucket's key (max dist, lowest index) can only change if its argmax member got
+    // closer: distances only decrease, so with that member untouched the max and its
+    // lowest-index holder stand — the reduction is skipped (bp = the member's lane, -1 unknown)
+    bool redo[K];
 #pragma unroll
     for (int u = 0; u < K; ++u) {
         const float d = lidar::dist2f(P[u].x, P[u].y, P[u].z, qx, qy, qz);
-        od[u] = min(__float_as_int(D[u]), __float_as_int(d));
-        W.d[pos[u]] = __int_as_float(od[u]);
+        const bool lower = __float_as_int(d) < __float_as_int(D[u]);
+        od[u] = lower ? __float_as_int(d) : __float_as_int(D[u]);
+        if (lower) W.d[pos[u]] = __int_as_float(od[u]);  // only changed members dirty a line
+        const uint64_t ch = __ballot(lower);
+        const int bpu = __builtin_amdgcn_readlane(bp, bbs[u]);
+        redo[u] = bpu < 0 || ((ch >> bpu) & 1ull);
     }
 #pragma unroll
-    for (int u = 0; u < K; ++u) dm[u] = lidar::wave_max_i32_dpp(od[u]);
+    for (int u = 0; u < K; ++u) {
+        dm[u] = 0;
+        if (redo[u]) dm[u] = lidar::wave_max_i32_dpp(od[u]);  // wave-uniform
+    }
 #pragma unroll
     for (int u = 0; u < K; ++u) {
+        if (!redo[u]) continue;  // wave-uniform
+        hit = hit || bbs[u] == target;
         const uint64_t c = __ballot(od[u] == dm[u]);
         int wl;
         if (__popcll(c) == 1) {
@@ -113,6 +127,7 @@ __device__ __forceinline__ void update_batch(uint64_t &mask, const FrameWs &W, i
         const float wy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(P[u].y), wl));
         const float wz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(P[u].z), wl));
         const bool me = lane == bbs[u];
+        bp = me ? wl : bp;
         bd = me ? __int_as_float(dm[u]) : bd;
         bi = me ? wi : bi;
         bx[0] = me ? wx : bx[0];
@@ -307,6 +322,7 @@ __global__ __launch_bounds__(T) void fps_bucket_kernel(const float *__restrict__
         // ---- per-bucket state in the owner lane: bucket = wave + 4 * (q * 64 + lane)
     float bmin[BPL][3], bmax[BPL][3], bx[BPL][3], bd[BPL];
     uint32_t bi[BPL];
+    int bp[BPL];  // lane (within the bucket) of the bucket's argmax member; -1 until reduced
 #pragma unroll
     for (int q = 0; q < BPL; ++q) {
         const int bucket = wave + (T / 64) * (q * 64 + lane);
@@ -317,6 +333,7 @@ __global__ __launch_bounds__(T) void fps_bucket_kernel(const float *__restrict__
             bmax[q][a] = have ? bbox_tab[bucket * 6 + 3 + a] : -INFINITY;
             bx[q][a] = 0.0f;
         }
+        bp[q] = -1;
         bd[q] = have ? INFINITY : 0.0f;  // empty slot: never active, never the argmax
         bi[q] = have ? 0u : 0xffffffffu;
     }
@@ -356,18 +373,23 @@ __global__ __launch_bounds__(T) void fps_bucket_kernel(const float *__restrict__
             const float gz = gap(qz, bmin[q][2], bmax[q][2]);
             const float lb = __fadd_rn(__fadd_rn(__fmul_rn(gx, gx), __fmul_rn(gy, gy)), __fmul_rn(gz, gz));
             uint64_t mask = __ballot(lb < bd[q]);
-            wave_dirty = wave_dirty || (q == w_q && ((mask >> w_lane) & 1));
+            // the wave argmax is recomputed only when its bucket's key changed
+            const int target = q == w_q ? w_lane : -1;
             while (mask) {  // wave-uniform
                 if constexpr (DIAG) dacc[4]++;
                 const int cnt = __popcll(mask);
                 if (cnt >= 4)
-                    update_batch<4, T / 64>(mask, W, wave, q, lane, qx, qy, qz, bd[q], bi[q], bx[q]);
+                    update_batch<4, T / 64>(mask, W, wave, q, lane, qx, qy, qz, bd[q], bi[q], bx[q], bp[q], target,
+                                             wave_dirty);
                 else if (cnt == 3)  // one round trip instead of 2 + 1
-                    update_batch<3, T / 64>(mask, W, wave, q, lane, qx, qy, qz, bd[q], bi[q], bx[q]);
+                    update_batch<3, T / 64>(mask, W, wave, q, lane, qx, qy, qz, bd[q], bi[q], bx[q], bp[q], target,
+                                             wave_dirty);
                 else if (cnt >= 2)
-                    update_batch<2, T / 64>(mask, W, wave, q, lane, qx, qy, qz, bd[q], bi[q], bx[q]);
+                    update_batch<2, T / 64>(mask, W, wave, q, lane, qx, qy, qz, bd[q], bi[q], bx[q], bp[q], target,
+                                             wave_dirty);
                 else
-                    update_batch<1, T / 64>(mask, W, wave, q, lane, qx, qy, qz, bd[q], bi[q], bx[q]);
+                    update_batch<1, T / 64>(mask, W, wave, q, lane, qx, qy, qz, bd[q], bi[q], bx[q], bp[q], target,
+                                             wave_dirty);
             }
         }
         if constexpr (DIAG) {

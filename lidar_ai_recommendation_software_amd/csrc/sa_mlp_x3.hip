@@ -79,7 +79,7 @@ __global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float 
     __shared__ uint4 buf[2][CHMAX];
     __shared__ float bias_s[C1 + C2 + C3];
     __shared__ float w1_s[XYZ ? T1 * 64 : 1];
-    __shared__ float mx_s[4][C3];
+    __shared__ float mx_s[4][C3];  // layer 3's running max-pool of the raw accumulators
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int q = lane >> 4, col = lane & 15;
@@ -109,9 +109,13 @@ __global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float 
     for (int i = tid; i < C1 + C2 + C3; i += 256) bias_s[i] = Bias[i];
     if constexpr (XYZ)
         for (int i = tid; i < T1 * 64; i += 256) w1_s[i] = reinterpret_cast<const float *>(packed)[i];
-    for (int i = lane; i < C3; i += 64) mx_s[wave][i] = 0.0f;  // post-ReLU values are >= 0
+    for (int i = lane; i < C3; i += 64) mx_s[wave][i] = -INFINITY;
     __syncthreads();
     int par = 0;
+    // layer 3's max-pool runs on the raw accumulators: x -> relu(x + bias) is monotone in
+    // fp32 (round-to-nearest addition never reverses an order), so max_i relu(a_i + b) ==
+    // relu(max_i a_i + b) bit for bit — the bias and ReLU are applied once per output
+    // channel at the end.
 
 #pragma unroll 1
     for (int it = 0; it < ITERS; ++it) {
@@ -127,10 +131,11 @@ __global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float 
                 const float x = q < 3 ? pr[q] - ce[q] : 0.0f;  // lane group q: dx, dy, dz, 0
 #pragma unroll
                 for (int t = 0; t < T1; ++t) {
-                    f32x4 acc = {};
+                    // the bias is the accumulator's initial value (channel 16t + 4q + r)
+                    f32x4 acc = *reinterpret_cast<const f32x4 *>(&bias_s[16 * t + 4 * q]);
                     acc = mfma_f(w1_s[t * 64 + lane], x, acc);
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) acc[r] = relu(acc[r] + bias_s[16 * t + 4 * q + r]);
+                    for (int r = 0; r < 4; ++r) acc[r] = relu(acc[r]);
                     y1[t] = acc;
                 }
             } else {
@@ -160,8 +165,19 @@ __global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float 
             if (more) fetch(cn, par ^ 1);  // lands during this chunk's MFMAs
             const uint4 *wb = buf[par] + lane;
             f32x4 a0[R], a1[R];
+            if (c < T2 / 2) {
+                // layer 2 accumulators start at the bias (channel rows: 16t + 4q + r)
+                const f32x4 b0 = *reinterpret_cast<const f32x4 *>(&bias_s[C1 + 16 * (2 * c) + 4 * q]);
+                const f32x4 b1 = *reinterpret_cast<const f32x4 *>(&bias_s[C1 + 16 * (2 * c + 1) + 4 * q]);
 #pragma unroll
-            for (int rr = 0; rr < R; ++rr) a0[rr] = a1[rr] = f32x4{};
+                for (int rr = 0; rr < R; ++rr) {
+                    a0[rr] = b0;
+                    a1[rr] = b1;
+                }
+            } else {
+#pragma unroll
+                for (int rr = 0; rr < R; ++rr) a0[rr] = a1[rr] = f32x4{};
+            }
             if (c < T2 / 2) {  // layer 2: output tiles 2c, 2c+1 (channel rows x point columns)
 #pragma unroll
                 for (int s = 0; s < KS2; ++s) {
@@ -183,8 +199,8 @@ __global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float 
                 for (int rr = 0; rr < R; ++rr) {
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
-                        a0[rr][r] = relu(a0[rr][r] + bias_s[C1 + 16 * (2 * c) + 4 * q + r]);
-                        a1[rr][r] = relu(a1[rr][r] + bias_s[C1 + 16 * (2 * c + 1) + 4 * q + r]);
+                        a0[rr][r] = relu(a0[rr][r]);
+                        a1[rr][r] = relu(a1[rr][r]);
                     }
                     y2[rr][2 * c < T2 ? 2 * c : 0] = a0[rr];
                     y2[rr][2 * c + 1 < T2 ? 2 * c + 1 : 0] = a1[rr];
@@ -216,19 +232,17 @@ __global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float 
                 }
 #pragma unroll
                 for (int hh = 0; hh < 2; ++hh) {
-                    const int t = 2 * tp + hh;
-                    const float bias = bias_s[C1 + C2 + 16 * t + col];
-                    float v = 0.0f;
+                    const int t = 2 * tp + hh < T3 ? 2 * tp + hh : 0;
+                    float v = -INFINITY;
 #pragma unroll
                     for (int rr = 0; rr < R; ++rr) {
                         const f32x4 &acc = hh ? a1[rr] : a0[rr];
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) v = fmaxf(v, relu(acc[r] + bias));
+                        v = fmaxf(v, fmaxf(fmaxf(acc[0], acc[1]), fmaxf(acc[2], acc[3])));
                     }
                     v = fmaxf(v, __shfl_xor(v, 16, 64));
                     v = fmaxf(v, __shfl_xor(v, 32, 64));
                     if (q == 0) {
-                        float &mm = mx_s[wave][(t < T3 ? 16 * t : 0) + col];
+                        float &mm = mx_s[wave][16 * t + col];
                         mm = fmaxf(mm, v);
                     }
                 }
@@ -240,7 +254,7 @@ __global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float 
     if (live && q == 0) {
         float *o = out + unit * out_stride + out_offset;
 #pragma unroll
-        for (int t = 0; t < T3; ++t) o[16 * t + col] = mx_s[wave][16 * t + col];
+        for (int t = 0; t < T3; ++t) o[16 * t + col] = relu(mx_s[wave][16 * t + col] + bias_s[C1 + C2 + 16 * t + col]);
     }
 }
 

@@ -35,6 +35,15 @@ __device__ __forceinline__ f32x4 mfma_f(float a, float b, f32x4 c)
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 __device__ __forceinline__ float relu(float v) { return v > 0.0f ? v : 0.0f; }
+// ReLU on the bits (signed int max with 0): no canonicalising v_max on MFMA results; equal to
+// relu() except that a positive NaN stays NaN
+__device__ __forceinline__ float relu_i(float v) { return __int_as_float(max(__float_as_int(v), 0)); }
+// max of three, NaN-propagating (v_maximum3_f32: no canonicalising v_max per operand, which
+// fmaxf's quiet-NaN rule costs on MFMA results)
+__device__ __forceinline__ float maxn(float a, float b, float c)
+{
+    return __builtin_elementwise_maximum(__builtin_elementwise_maximum(a, b), c);
+}
 
 // two accumulator tiles -> the hi / lo bf16 fragments of one k-step
 __device__ __forceinline__ void split_pair(const f32x4 &t0, const f32x4 &t1, bf16x8 &hi, bf16x8 &lo)
@@ -79,9 +88,10 @@ __global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float 
     __shared__ uint4 buf[2][CHMAX];
     __shared__ float bias_s[C1 + C2 + C3];
     __shared__ float w1_s[XYZ ? T1 * 64 : 1];
-    __shared__ float mx_s[4][C3];  // layer 3's running max-pool of the raw accumulators
+    __shared__ float mx_s[4][4][C3];  // layer 3's running max-pool of the raw accumulators, per (wave, row group)
 
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // wave index in an SGPR: the LDS-DMA destinations (M0) and the unit below are wave-uniform
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int q = lane >> 4, col = lane & 15;
     const int64_t unit = (int64_t)blockIdx.x * 4 + wave;
     const bool live = unit < total;  // every wave takes part in the barriers
@@ -98,9 +108,9 @@ __global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float 
         const int len = c < T2 / 2 ? CH2 : CH3;
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
-            const int base = 256 * i + 64 * wave;
+            const int base = 256 * i + 64 * wave;  // scalar: SGPR base + 32-bit lane offset
             if (base < len)
-                __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)(src + base + lane),
+                __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)(src + base + (unsigned)lane),
                                                  (__attribute__((address_space(3))) void *)(&buf[dst][base]), 16, 0,
                                                  0);
         }
@@ -109,7 +119,7 @@ __global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float 
     for (int i = tid; i < C1 + C2 + C3; i += 256) bias_s[i] = Bias[i];
     if constexpr (XYZ)
         for (int i = tid; i < T1 * 64; i += 256) w1_s[i] = reinterpret_cast<const float *>(packed)[i];
-    for (int i = lane; i < C3; i += 64) mx_s[wave][i] = -INFINITY;
+    for (int i = lane; i < 4 * C3; i += 64) (&mx_s[wave][0][0])[i] = -INFINITY;
     __syncthreads();
     int par = 0;
     // layer 3's max-pool runs on the raw accumulators: x -> relu(x + bias) is monotone in
@@ -135,7 +145,7 @@ __global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float 
                     f32x4 acc = *reinterpret_cast<const f32x4 *>(&bias_s[16 * t + 4 * q]);
                     acc = mfma_f(w1_s[t * 64 + lane], x, acc);
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) acc[r] = relu(acc[r]);
+                    for (int r = 0; r < 4; ++r) acc[r] = relu_i(acc[r]);
                     y1[t] = acc;
                 }
             } else {
@@ -199,8 +209,8 @@ __global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float 
                 for (int rr = 0; rr < R; ++rr) {
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
-                        a0[rr][r] = relu(a0[rr][r]);
-                        a1[rr][r] = relu(a1[rr][r]);
+                        a0[rr][r] = relu_i(a0[rr][r]);
+                        a1[rr][r] = relu_i(a1[rr][r]);
                     }
                     y2[rr][2 * c < T2 ? 2 * c : 0] = a0[rr];
                     y2[rr][2 * c + 1 < T2 ? 2 * c + 1 : 0] = a1[rr];
@@ -237,14 +247,11 @@ __global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float 
 #pragma unroll
                     for (int rr = 0; rr < R; ++rr) {
                         const f32x4 &acc = hh ? a1[rr] : a0[rr];
-                        v = fmaxf(v, fmaxf(fmaxf(acc[0], acc[1]), fmaxf(acc[2], acc[3])));
+                        v = maxn(maxn(v, acc[0], acc[1]), acc[2], acc[3]);
                     }
-                    v = fmaxf(v, __shfl_xor(v, 16, 64));
-                    v = fmaxf(v, __shfl_xor(v, 32, 64));
-                    if (q == 0) {
-                        float &mm = mx_s[wave][16 * t + col];
-                        mm = fmaxf(mm, v);
-                    }
+                    // each row group q keeps its own slot: one LDS atomic max, no lane swaps
+                    __builtin_amdgcn_ds_fmaxf((__attribute__((address_space(3))) float *)&mx_s[wave][q][16 * t + col], v, 0,
+                                              0, false);
                 }
             }
             __syncthreads();  // (vmcnt(0)) chunk c+1 landed for everyone; buf[par] free for c+2
@@ -254,7 +261,11 @@ __global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float 
     if (live && q == 0) {
         float *o = out + unit * out_stride + out_offset;
 #pragma unroll
-        for (int t = 0; t < T3; ++t) o[16 * t + col] = relu(mx_s[wave][16 * t + col] + bias_s[C1 + C2 + 16 * t + col]);
+        for (int t = 0; t < T3; ++t) {
+            const int c3 = 16 * t + col;
+            const float v = maxn(maxn(mx_s[wave][0][c3], mx_s[wave][1][c3], mx_s[wave][2][c3]), mx_s[wave][3][c3], -INFINITY);
+            o[c3] = relu(v + bias_s[C1 + C2 + c3]);
+        }
     }
 }
 

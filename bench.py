@@ -213,7 +213,7 @@ def main():
     ap.add_argument("--x3", default="1", choices=["0", "1", "pre", "xyz"],
                     help="SA layers 2-3 on the split-bf16 (x3) kernels: fp32 arithmetic within the 1e-4 "
                          "contract; 0 = native fp32 MFMA kernels")
-    ap.add_argument("--bq-main", type=int, default=1, help="1: SA1 ball queries on the main stream")
+    ap.add_argument("--bq-main", type=int, default=0, help="1: SA1 ball queries on the main stream (0: on the FPS side streams)")
     ap.add_argument("--l1-side", type=int, default=0,
                     help="1: SA2's FPS and ball queries (they need only SA1's centres) on the side streams")
     ap.add_argument("--no-fp32-mfma-leg", action="store_true",

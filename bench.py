@@ -213,6 +213,7 @@ def main():
     ap.add_argument("--x3", default="1", choices=["0", "1", "pre", "xyz"],
                     help="SA layers 2-3 on the split-bf16 (x3) kernels: fp32 arithmetic within the 1e-4 "
                          "contract; 0 = native fp32 MFMA kernels")
+    ap.add_argument("--x3s", type=int, default=1, help="1: dense layers on the split-plane x3 GEMM")
     ap.add_argument("--bq-main", type=int, default=0, help="1: SA1 ball queries on the main stream (0: on the FPS side streams)")
     ap.add_argument("--l1-side", type=int, default=0,
                     help="1: SA2's FPS and ball queries (they need only SA1's centres) on the side streams")
@@ -246,7 +247,7 @@ def main():
         of the same length (with ~25 launches per step, as MSG has, the events cost ~1/3)."""
         bb = pn.PointNet2Backbone(cfg, device=dev, seed=0, dtype=dtype,
                                   mlp16={"0": False, "1": True}.get(args.mlp16, args.mlp16),
-                                  x3=x3_opt if x3 is None else x3)
+                                  x3=x3_opt if x3 is None else x3, x3s=bool(args.x3s))
         x = torch.from_numpy(unit_frames(B, N, seed=sharding.frame_seed(rank))).to(dev)
         # the streaming executor overlaps batch k+1's SA1 FPS + ball queries (latency-bound,
         # one workgroup per frame) with batch k's MFMA levels; results are identical to forward()

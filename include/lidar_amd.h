@@ -174,6 +174,25 @@ int lidar_dense_x3p_f32(lidar_handle *h, const float *x, int64_t rows, int32_t k
                         const float *bias, int32_t cout, int32_t relu_on, int32_t pool_rows, float *y,
                         void *stream);
 
+/* the x3 GEMM on pre-split activations ("split planes", csrc/dense_x3s.hip): a_planes holds
+ * two bf16 planes (hi = bf16(x), lo = bf16(x - hi)) of row-major (rows, lda) elements, the lo
+ * plane a_plane elements after the hi plane; lda = k rounded up to 32, elements k..lda-1 zero.
+ * packed = lidar_dense_x3_pack_f32's image of W (k, cout).  mode 0: y = x W + b [ReLU] as fp32
+ * rows (rows, ldo); mode 1: the same as split planes (rows, ldo) x 2, o_plane apart (the next
+ * layer's input); mode 2: ReLU and max over runs of pool_rows rows into fp32 (rows/pool_rows,
+ * ldo), out zeroed by the caller.  rows % 128 == 0, cout % 128 == 0. */
+int lidar_dense_x3s_f32(lidar_handle *h, const void *a_planes, int64_t a_plane, int32_t lda, int64_t rows,
+                        int32_t k, const void *packed, const float *bias, int32_t cout, int32_t mode,
+                        int32_t relu_on, int32_t pool_rows, void *out, int64_t o_plane, int64_t ldo, void *stream);
+/* the same GEMM with A as fp32 rows (rows, k) of row stride lda (k % 4 == 0), split inside the
+ * tile loop (for a chain's first layer, whose input nobody split) */
+int lidar_dense_x3f_f32(lidar_handle *h, const float *a, int32_t lda, int64_t rows, int32_t k, const void *packed,
+                        const float *bias, int32_t cout, int32_t mode, int32_t relu_on, int32_t pool_rows, void *out,
+                        int64_t o_plane, int64_t ldo, void *stream);
+/* fp32 rows (rows, k), row stride ldx -> split planes (rows, lda) for lidar_dense_x3s_f32 */
+int lidar_split_x3_f32(lidar_handle *h, const float *x, int64_t rows, int32_t k, int64_t ldx, void *planes,
+                       int64_t plane, int32_t lda, void *stream);
+
 /* lidar_sa_group_mlp_f32 with layer 1 applied per point beforehand: p (batch*n, p_stride)
  * = [f, x] W1 + b1 for every point of the level, q (batch*m, p_stride) = centre W1_xyz
  * (both via lidar_dense_f32, relu_on = 0, columns >= c1 ignored); a grouped row's layer 1

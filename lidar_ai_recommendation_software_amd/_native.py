@@ -63,6 +63,9 @@ SIGNATURES = {
     "lidar_dense_x3_packed_size": [I32, I32],
     "lidar_dense_x3_pack_f32": [P, P, I32, I32, P, P],
     "lidar_dense_x3p_f32": [P, P, I64, I32, P, P, I32, I32, I32, P, P],
+    "lidar_dense_x3s_f32": [P, P, I64, I32, I64, I32, P, P, I32, I32, I32, I32, P, I64, I64, P],
+    "lidar_split_x3_f32": [P, P, I64, I32, I64, P, I64, I32, P],
+    "lidar_dense_x3f_f32": [P, P, I32, I64, I32, P, P, I32, I32, I32, I32, P, I64, I64, P],
     "lidar_mlp_packed_size16": [I32, I32, I32, I32],
     "lidar_mlp_pack16_f32": [I32, I32, I32, I32, P, P, P, P, P, P, P],
     "lidar_sa_group_mlp16_f32": [P, I32, P, I64, P, P, I64, I64, I64, I32, I32, I32, I32, P, P, I64, I64, P],

@@ -295,7 +295,7 @@ def layer1_weights(layer, cfeat, to_dev):
     return {"w1": to_dev(w1p), "b1": to_dev(bp), "wq": to_dev(wq), "zero": to_dev(np.zeros(cp, np.float32))}
 
 
-def layer1_per_point(x_rows, xyz, cfeat, new_xyz, branches, x3=False):
+def layer1_per_point(x_rows, xyz, cfeat, new_xyz, branches, x3=False, x3s=False):
     """Layer 1 of every branch of a level, per point instead of per grouped row.
 
     x_rows: (R, kp) padded rows [f (cfeat), x, y, z, 0...] of the level's B*N points
@@ -313,6 +313,14 @@ def layer1_per_point(x_rows, xyz, cfeat, new_xyz, branches, x3=False):
     cpad = torch.zeros((rq, 16), dtype=torch.float32, device=dev)
     nat.call("lidar_concat_xyz_pad_f32", h, nat.ptr(new_xyz), B * M, nat.ptr(cpad), 16, 0, nat.stream_ptr())
     out = []
+    if x3 and x3s:  # fp32 rows in (split in the tile loop: one column tile re-reads nothing)
+        xs, cs = x_rows, cpad
+        for br in branches:
+            pre = br["pre"]
+            cp = pre["w1"].shape[1]
+            out.append((dense_x3s(xs, pre["w1_x3"], pre["b1"], cp, relu=False),
+                        dense_x3s(cs, pre["wq_x3"], pre["zero"], cp, relu=False)))
+        return out
     for br in branches:
         pre = br["pre"]
         P = dense(x_rows, pre["w1"], pre["b1"], relu=False, x3=x3, wpack=pre.get("w1_x3") if x3 else None)
@@ -349,6 +357,64 @@ def dense(x, w, b, relu=True, pool_rows=0, out=None, x3=False, wpack=None):
     nat.call("lidar_dense_x3_f32" if x3 else "lidar_dense_f32", nat.handle(x.device.index), nat.ptr(x), rows, k,
              nat.ptr(w), nat.ptr(b), cout, 1 if relu else 0, pool_rows, nat.ptr(out), nat.stream_ptr())
     return out
+
+
+class SplitPlanes:
+    """Activations pre-split for the x3 GEMM: planes (2, rows, lda) bf16 = hi, lo of x (rows, k);
+    lda = k rounded up to 32, columns k.. zero (csrc/dense_x3s.hip)."""
+
+    def __init__(self, planes, k):
+        self.planes, self.k = planes, k
+
+    @property
+    def rows(self):
+        return self.planes.shape[1]
+
+
+def split_x3(x, k=None):
+    """fp32 rows x (rows, >= k) -> SplitPlanes (lidar_split_x3_f32)."""
+    _dev_check(x)
+    rows, ldx = x.shape
+    k = ldx if k is None else k
+    lda = (k + 31) // 32 * 32
+    planes = torch.empty((2, rows, lda), dtype=torch.bfloat16, device=x.device)
+    nat.call("lidar_split_x3_f32", nat.handle(x.device.index), nat.ptr(x), rows, k, ldx, nat.ptr(planes),
+             rows * lda, lda, nat.stream_ptr())
+    return SplitPlanes(planes, k)
+
+
+def dense_x3s(a, wpack, b, cout, relu=True, split_out=False, pool_rows=0, out=None):
+    """a @ W + b on the x3 GEMM of csrc/dense_x3s.hip (wpack = pack_dense_x3(W)): a is
+    SplitPlanes (lidar_dense_x3s_f32) or fp32 rows (rows, k) (lidar_dense_x3f_f32, split in
+    the tile loop).  Returns fp32 rows (rows, cout), SplitPlanes (split_out) or, with
+    pool_rows, the fp32 max over runs of pool_rows rows (ReLU)."""
+    f32 = not isinstance(a, SplitPlanes)
+    rows, lda = (a.shape[0], a.shape[1]) if f32 else (a.planes.shape[1], a.planes.shape[2])
+    dev = a.device if f32 else a.planes.device
+    if pool_rows:
+        mode = 2
+        if out is None:
+            out = torch.zeros((rows // pool_rows, cout), dtype=torch.float32, device=dev)
+        ldo, oplane, res = out.shape[1], 0, out
+    elif split_out:
+        mode = 1
+        out = torch.empty((2, rows, cout), dtype=torch.bfloat16, device=dev)
+        ldo, oplane, res = cout, rows * cout, SplitPlanes(out, cout)
+    else:
+        mode = 0
+        if out is None:
+            out = torch.empty((rows, cout), dtype=torch.float32, device=dev)
+        ldo, oplane, res = out.shape[1], 0, out
+    if f32:
+        _dev_check(a, wpack, b, out)
+        nat.call("lidar_dense_x3f_f32", nat.handle(dev.index), nat.ptr(a), lda, rows, lda, nat.ptr(wpack), nat.ptr(b),
+                 cout, mode, 1 if relu else 0, pool_rows, nat.ptr(out), oplane, ldo, nat.stream_ptr())
+        return res
+    _dev_check(a.planes, wpack, b, out)
+    nat.call("lidar_dense_x3s_f32", nat.handle(dev.index), nat.ptr(a.planes), rows * lda, lda, rows, a.k,
+             nat.ptr(wpack), nat.ptr(b), cout, mode, 1 if relu else 0, pool_rows, nat.ptr(out), oplane, ldo,
+             nat.stream_ptr())
+    return res
 
 
 def dense_relu(x, w, b, pool_rows=0, out=None, x3=False, wpack=None):
@@ -393,7 +459,8 @@ class PointNet2Backbone:
     """SSG / MSG PointNet++ encoder on liblidar_amd.  ``forward(xyz)`` -> global feature
     (B, C_last) plus the per-level (new_xyz, features, fps_idx)."""
 
-    def __init__(self, cfg=SSG, weights=None, device="cuda", seed=0, dtype="f32", pre_layer1=True, mlp16="pre", x3=True):
+    def __init__(self, cfg=SSG, weights=None, device="cuda", seed=0, dtype="f32", pre_layer1=True, mlp16="pre", x3=True,
+                 x3s=True):
         """dtype "bf16": the SA branches run on bf16 MFMA (inputs/activations/weights rounded
         to bf16, fp32 accumulation; BASELINE configs[4]); group_all stays fp32.
         pre_layer1 (fp32, levels with point features): layer 1 runs per point as a GEMM
@@ -402,7 +469,8 @@ class PointNet2Backbone:
         16-row kernels (MLP16_SHAPES); "pre" / "xyz": only the per-point-layer-1 / the
         xyz-only levels.
         x3 (fp32): the same branches on the split-bf16 kernels (lidar_sa_group_mlp_x3_f32;
-        True, or "pre" / "xyz" for one kind of level)."""
+        True, or "pre" / "xyz" for one kind of level).
+        x3s (with x3): the dense layers on the split-plane GEMM (dense_x3s / split_x3)."""
         if dtype not in ("f32", "bf16"):
             raise ValueError("dtype must be 'f32' or 'bf16'")
         self.bf16 = dtype == "bf16"
@@ -452,6 +520,9 @@ class PointNet2Backbone:
         self.out_channels = cfeat
         # x3 on: the dense layers (per-point layer 1, group_all) on the split-bf16 GEMM too
         self.x3_dense = bool(x3) and not self.bf16
+        # x3s: the dense layers take split planes (split once per input, dense1 -> dense2 -> dense3
+        # hand them over) instead of splitting fp32 activations inside every GEMM tile
+        self.x3_split = self.x3_dense and bool(x3s)
         if self.x3_dense:  # the dense layers' weights packed once into x3 B fragments
             for lvl in self.levels:
                 if lvl.get("group_all"):
@@ -504,7 +575,7 @@ class PointNet2Backbone:
             pq = None
             if lvl.get("pre"):
                 pq = _call(self.timers, f"sa{li + 1}_layer1_points", layer1_per_point, rows, xyz, lvl["cfeat"],
-                           new_xyz, lvl["branches"], x3=self.x3_dense)
+                           new_xyz, lvl["branches"], x3=self.x3_dense, x3s=self.x3_split)
             off = 0
             for bi_, br in enumerate(lvl["branches"]):
                 tag = f"sa{li + 1}" + (f"_b{bi_}" if len(lvl["branches"]) > 1 else "")
@@ -557,6 +628,11 @@ class PointNet2Backbone:
             M, rows = mp, B * mp
         t = self.timers
         wp = lvl.get("w_x3") if self.x3_dense else None
+        if wp and self.x3_split:  # split once; dense1/dense2 hand split planes to the next layer
+            ws, bs = lvl["w"], lvl["b"]
+            h1 = _call(t, "sa3_dense1", dense_x3s, x2, wp[0], bs[0], ws[0].shape[1], split_out=True)
+            h2 = _call(t, "sa3_dense2", dense_x3s, h1, wp[1], bs[1], ws[1].shape[1], split_out=True)
+            return _call(t, "sa3_dense3_pool", dense_x3s, h2, wp[2], bs[2], ws[2].shape[1], pool_rows=M)
         h1 = _call(t, "sa3_dense1", dense_relu, x2, lvl["w"][0], lvl["b"][0], x3=self.x3_dense,
                    wpack=wp[0] if wp else None)
         h2 = _call(t, "sa3_dense2", dense_relu, h1, lvl["w"][1], lvl["b"][1], x3=self.x3_dense,

@@ -297,6 +297,50 @@ def test_dense_x3(cuda, rows, k, cout, pool):
         feat_close(pn.dense_relu(T(x), T(w), T(b), x3=True).cpu().numpy(), want, "dense x3 relu")
 
 
+@pytest.mark.parametrize("rows,k,cout,pool", [(256, 144, 128, 0), (512, 272, 256, 0), (1024, 512, 1024, 512),
+                                              (384, 16, 128, 128), (2048, 256, 512, 1024), (128, 48, 384, 0)])
+def test_dense_x3s(cuda, rows, k, cout, pool):
+    """split-plane GEMM (all three output modes) vs the fp32 numpy product at 1e-4."""
+    rng = np.random.default_rng(rows + k + 1)
+    x = rng.standard_normal((rows, k)).astype(np.float32)
+    w = (rng.standard_normal((k, cout)) / np.sqrt(k)).astype(np.float32)
+    b = rng.standard_normal(cout).astype(np.float32) * 0.1
+    T = lambda a: torch.from_numpy(a).to(cuda)
+    want = x.astype(np.float64) @ w.astype(np.float64) + b
+    a = pn.split_x3(T(x))
+    wp = pn.pack_dense_x3(T(w))
+    feat_close(pn.dense_x3s(a, wp, T(b), cout, relu=False).cpu().numpy(), want, "dense x3s fp32 rows")
+    want = np.maximum(want, 0)
+    feat_close(pn.dense_x3s(a, wp, T(b), cout).cpu().numpy(), want, "dense x3s relu")
+    sp = pn.dense_x3s(a, wp, T(b), cout, split_out=True)
+    got = (sp.planes[0].float() + sp.planes[1].float()).cpu().numpy()
+    feat_close(got, want, "dense x3s split planes")
+    if pool:
+        got = pn.dense_x3s(a, wp, T(b), cout, pool_rows=pool).cpu().numpy()
+        feat_close(got, want.reshape(rows // pool, pool, cout).max(axis=1), "dense x3s pooled")
+    # fp32 rows in (split in the tile loop), every output mode
+    xf = T(x)
+    feat_close(pn.dense_x3s(xf, wp, T(b), cout).cpu().numpy(), want, "dense x3f relu")
+    sp = pn.dense_x3s(xf, wp, T(b), cout, split_out=True)
+    feat_close((sp.planes[0].float() + sp.planes[1].float()).cpu().numpy(), want, "dense x3f split planes")
+    if pool:
+        got = pn.dense_x3s(xf, wp, T(b), cout, pool_rows=pool).cpu().numpy()
+        feat_close(got, want.reshape(rows // pool, pool, cout).max(axis=1), "dense x3f pooled")
+
+
+def test_split_x3_exact(cuda):
+    """hi = bf16(x), lo = bf16(x - hi) (RNE), columns k..lda-1 zero."""
+    rng = np.random.default_rng(5)
+    x = torch.from_numpy((rng.standard_normal((256, 72)) * 10.0 ** rng.integers(-20, 20, (256, 72))).astype(np.float32)).to(cuda)
+    sp = pn.split_x3(x[:, :70].contiguous())
+    assert sp.planes.shape == (2, 256, 96) and sp.k == 70
+    hi = x[:, :70].to(torch.bfloat16)
+    lo = (x[:, :70] - hi.float()).to(torch.bfloat16)
+    assert torch.equal(sp.planes[0, :, :70].view(torch.int16), hi.view(torch.int16))
+    assert torch.equal(sp.planes[1, :, :70].view(torch.int16), lo.view(torch.int16))
+    assert not sp.planes[:, :, 70:].float().any()
+
+
 def test_dense_relu_and_pool(cuda):
     rng = np.random.default_rng(1)
     x = rng.standard_normal((512, 272)).astype(np.float32)

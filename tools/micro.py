@@ -174,6 +174,14 @@ def dense_micro():
         wp = pn.pack_dense_x3(w)
         ms_x3 = timeit(lambda: pn.dense(x, w, b, x3=True, wpack=wp), reps=10)
         print(f"dense x3 {k}x{n}: {ms_x3:.3f} ms ({2 * rows * k * n / ms_x3 / 1e9:.0f} fp32-equivalent TF)", flush=True)
+        sp = pn.split_x3(x)
+        for name, a in (("planes", sp), ("fp32", x)):
+            for mode, kw in (("rows", {}), ("split", {"split_out": True}), ("pool", {"pool_rows": 1024})):
+                ms_s = timeit(lambda: pn.dense_x3s(a, wp, b, n, **kw), reps=10)
+                print(f"  x3s {name:6s} -> {mode:5s} {k}x{n}: {ms_s:.3f} ms ({2 * rows * k * n / ms_s / 1e9:.0f} TF)",
+                      flush=True)
+        ms_sp = timeit(lambda: pn.split_x3(x), reps=10)
+        print(f"  split_x3 {rows}x{k}: {ms_sp:.3f} ms ({rows * k * 8 / ms_sp / 1e6:.0f} GB/s)", flush=True)
         ms_blas = timeit(lambda: torch._addmm_activation(b, x, w), reps=10)
         ms_mm = timeit(lambda: torch.relu_(torch.addmm(b, x, w)), reps=10)
         fl = 2 * rows * k * n

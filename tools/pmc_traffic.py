@@ -59,6 +59,12 @@ def label(name, grid, F=FRAMES_PER_LAUNCH):
     if "dense_relu_kernel" in name or "dense_x3_kernel" in name or "dense_x3p_kernel" in name:
         return {F * 4096 * 2: "dense_shared", F * 1024 * 2: "sa2_layer1_points", F * 1024 * 4: "sa3_dense1",
                 F * 1024 * 16: "sa3_dense3_pool"}.get(grid)
+    if "dense_x3s_kernel<" in name:  # split-plane GEMM: <mode, fp32-input>
+        for key, lab in (("<0, true>", "sa2_layer1_points"), ("<1, true>", "sa3_dense1"),
+                         ("<1, false>", "sa3_dense2"), ("<2, false>", "sa3_dense3_pool")):
+            if key in name:
+                return lab
+        return None
     if "concat_xyz_pad" in name:
         return "concat"
     return None

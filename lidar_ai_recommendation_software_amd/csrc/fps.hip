@@ -144,12 +144,11 @@ __device__ __forceinline__ uint64_t stamp()
 }
 
 // Prologue of one frame, run by the whole workgroup: frame bbox, counting sort of the points
-// by 16^3 Morton cell into W (padded to whole buckets with dist -1 sentinels), bucket
-// bounding boxes into bbox_tab[nb][6].  Ends with a barrier.
+// by 16^3 Morton cell into W (padded to whole buckets with dist -1 sentinels).  Ends with a
+// barrier (hist is free afterwards).
 template <int T>
 __device__ __forceinline__ void fps_prologue(const float *__restrict__ p, int n, const FrameWs &W,
-                                             uint32_t *hist, float (*red)[T / 64], uint32_t *wsum,
-                                             float *bbox_tab)
+                                             uint32_t *hist, float (*red)[T / 64], uint32_t *wsum)
 {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int npad = (n + 63) / 64 * 64;
@@ -239,32 +238,6 @@ __device__ __forceinline__ void fps_prologue(const float *__restrict__ p, int n,
     __threadfence_block();
     __syncthreads();
 
-    // ---- bucket bounding boxes: every wave reduces 64-point buckets into an LDS table
-    const int nb = (n + 63) / 64;
-    for (int bucket = wave; bucket < nb; bucket += (T / 64)) {
-        const int pos = bucket * 64 + lane;
-        float v[3] = {INFINITY, INFINITY, INFINITY}, u[3] = {-INFINITY, -INFINITY, -INFINITY};
-        if (pos < n) {
-            const float4 P = W.p[pos];
-            v[0] = u[0] = P.x;
-            v[1] = u[1] = P.y;
-            v[2] = u[2] = P.z;
-        }
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            v[a] = lidar::wave_min_f(v[a]);
-            u[a] = lidar::wave_max_f(u[a]);
-        }
-        if (lane == 0) {
-#pragma unroll
-            for (int a = 0; a < 3; ++a) {
-                bbox_tab[bucket * 6 + a] = v[a];
-                bbox_tab[bucket * 6 + 3 + a] = u[a];
-            }
-        }
-    }
-    __syncthreads();
-
 }
 // DIAG builds (lidar_diag_fps_phases only) accumulate per-phase shader cycles per wave:
 // [0] bucket tests + active-bucket updates, [1] wave argmax + LDS publish, [2] barrier
@@ -316,23 +289,66 @@ __global__ __launch_bounds__(T) void fps_bucket_kernel(const float *__restrict__
     __shared__ unsigned long long mkey[3];
     __shared__ __attribute__((aligned(16))) float mcrd[2][(T / 64)][4];
 
-    extern __shared__ float bbox_tab[];  // [nb][6]
-    fps_prologue<T>(p, n, W, hist, red, wsum, bbox_tab);
+    fps_prologue<T>(p, n, W, hist, red, wsum);
     const int nb = (n + 63) / 64;
         // ---- per-bucket state in the owner lane: bucket = wave + 4 * (q * 64 + lane)
     float bmin[BPL][3], bmax[BPL][3], bx[BPL][3], bd[BPL];
     uint32_t bi[BPL];
     int bp[BPL];  // lane (within the bucket) of the bucket's argmax member; -1 until reduced
 #pragma unroll
+    for (int q = 0; q < BPL; ++q)
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            bmin[q][a] = INFINITY;
+            bmax[q][a] = -INFINITY;
+        }
+    // bucket bounding boxes: every wave reduces 64-point buckets into a table in the (now free)
+    // hist array, 512 buckets per pass (12 KiB), and the owner lanes pick theirs up — no LDS is
+    // held for it through the step loop (the kernel's LDS stays ~17 KiB beside other kernels)
+    float *tab = reinterpret_cast<float *>(hist);
+    static_assert(kCells >= 512 * 6, "bbox pass table");
+    for (int p0 = 0; p0 < nb; p0 += 512) {
+        for (int bucket = p0 + wave; bucket < nb && bucket < p0 + 512; bucket += (T / 64)) {
+            const int pos = bucket * 64 + lane;
+            float v[3] = {INFINITY, INFINITY, INFINITY}, u[3] = {-INFINITY, -INFINITY, -INFINITY};
+            if (pos < n) {
+                const float4 P = W.p[pos];
+                v[0] = u[0] = P.x;
+                v[1] = u[1] = P.y;
+                v[2] = u[2] = P.z;
+            }
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                v[a] = lidar::wave_min_f(v[a]);
+                u[a] = lidar::wave_max_f(u[a]);
+            }
+            if (lane == 0) {
+#pragma unroll
+                for (int a = 0; a < 3; ++a) {
+                    tab[(bucket - p0) * 6 + a] = v[a];
+                    tab[(bucket - p0) * 6 + 3 + a] = u[a];
+                }
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < BPL; ++q) {
+            const int bucket = wave + (T / 64) * (q * 64 + lane);
+            if (bucket >= p0 && bucket < p0 + 512 && bucket < nb)
+#pragma unroll
+                for (int a = 0; a < 3; ++a) {
+                    bmin[q][a] = tab[(bucket - p0) * 6 + a];
+                    bmax[q][a] = tab[(bucket - p0) * 6 + 3 + a];
+                }
+        }
+        __syncthreads();
+    }
+#pragma unroll
     for (int q = 0; q < BPL; ++q) {
         const int bucket = wave + (T / 64) * (q * 64 + lane);
         const bool have = bucket < nb;
 #pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            bmin[q][a] = have ? bbox_tab[bucket * 6 + a] : INFINITY;
-            bmax[q][a] = have ? bbox_tab[bucket * 6 + 3 + a] : -INFINITY;
-            bx[q][a] = 0.0f;
-        }
+        for (int a = 0; a < 3; ++a) bx[q][a] = 0.0f;
         bp[q] = -1;
         bd[q] = have ? INFINITY : 0.0f;  // empty slot: never active, never the argmax
         bi[q] = have ? 0u : 0xffffffffu;
@@ -505,12 +521,9 @@ static int launch_fps(const float *xyz, int64_t batch, int64_t n, int64_t npoint
 {
     dim3 grid((unsigned)batch), block(T);
     const int nb = (int)((n + 63) / 64);
-    const size_t lds = (size_t)nb * 6 * sizeof(float);
     const int lanes = T;  // one bucket per lane and slot
     auto go = [&](auto kern) -> int {
-        HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        hipLaunchKernelGGL(kern, grid, block, lds, s, xyz, (int)n, (int)npoint, idx, new_xyz, first_zero,
+        hipLaunchKernelGGL(kern, grid, block, 0, s, xyz, (int)n, (int)npoint, idx, new_xyz, first_zero,
                            prefix_ok, ws, stride, nullptr);
         return LIDAR_OK;
     };
@@ -567,11 +580,8 @@ LIDAR_EXPORT int lidar_diag_fps_phases(lidar_handle *h, const float *xyz, int64_
     int64_t stride = lidar::align_up(5 * lidar::align_up(n, 64), 64);
     float *ws = static_cast<float *>(lidar::workspace(h, (uint64_t)(batch * stride) * 4));
     if (!ws) return LIDAR_ENOMEM;
-    const size_t lds = (size_t)((n + 63) / 64) * 6 * sizeof(float);
     REQUIRE((n + 63) / 64 <= kThreads, "lidar_diag_fps_phases: n too large for BPL=1");
-    HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(fps_bucket_kernel<kThreads, 1, true>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL((fps_bucket_kernel<kThreads, 1, true>), dim3((unsigned)batch), dim3(kThreads), lds,
+    hipLaunchKernelGGL((fps_bucket_kernel<kThreads, 1, true>), dim3((unsigned)batch), dim3(kThreads), 0,
                        static_cast<hipStream_t>(stream), xyz, (int)n, (int)npoint, idx, nullptr, nullptr,
                        nullptr, ws, stride, diag);
     LAUNCH_CHECK();

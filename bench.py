@@ -219,6 +219,9 @@ def main():
                     help="1: SA2's FPS and ball queries (they need only SA1's centres) on the side streams")
     ap.add_argument("--no-fp32-mfma-leg", action="store_true",
                     help="skip the extra measurement of the native fp32-MFMA kernels (when --x3 is on)")
+    ap.add_argument("--msg-batch", type=int, default=8, help="frames per GPU per step of the configs[4] MSG leg")
+    ap.add_argument("--msg-steps", type=int, default=24)
+    ap.add_argument("--msg-x3", type=int, default=0, help="1: also time the MSG leg in fp32 on the x3 kernels")
     ap.add_argument("--no-extras", action="store_true", help="skip the configs[1]/[4] side measurements")
     ap.add_argument("--no-density", action="store_true", help="skip the Tier R density-path leg")
     args = ap.parse_args()
@@ -283,8 +286,11 @@ def main():
     extras = {}
     if not args.no_extras:
         # the other BASELINE.json configs, measured the same way (not the headline metric)
-        for key, cfg, dtype, b2, n2, st in (("configs[1]_sa1_16k_f32", pn.SA1_ONLY, "f32", 32, 16384, 40),
-                                            ("configs[4]_msg_131k_bf16", pn.MSG, "bf16", 8, 131072, 24)):
+        legs = [("configs[1]_sa1_16k_f32", pn.SA1_ONLY, "f32", 32, 16384, 40),
+                ("configs[4]_msg_131k_bf16", pn.MSG, "bf16", args.msg_batch, 131072, args.msg_steps)]
+        if args.msg_x3:  # the same MSG stack in fp32 arithmetic on the x3 kernels (bf16 MFMA products)
+            legs.append(("configs[4]_msg_131k_f32x3", pn.MSG, "f32", args.msg_batch, 131072, args.msg_steps))
+        for key, cfg, dtype, b2, n2, st in legs:
             el2, k2 = measure(cfg, dtype, b2, n2, st, 2, 3, events_in_window=False)
             extras[key] = {"M_points_per_s": sharding.aggregate_rate(b2 * n2 * st, world, el2) / 1e6, "ms_per_step": el2 / st * 1e3,
                            "frames_per_gpu": b2, "points_per_frame": n2, "dtype": dtype,

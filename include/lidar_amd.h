@@ -180,7 +180,8 @@ int lidar_dense_x3p_f32(lidar_handle *h, const float *x, int64_t rows, int32_t k
  * packed = lidar_dense_x3_pack_f32's image of W (k, cout).  mode 0: y = x W + b [ReLU] as fp32
  * rows (rows, ldo); mode 1: the same as split planes (rows, ldo) x 2, o_plane apart (the next
  * layer's input); mode 2: ReLU and max over runs of pool_rows rows into fp32 (rows/pool_rows,
- * ldo), out zeroed by the caller.  rows % 128 == 0, cout % 128 == 0. */
+ * ldo), out zeroed by the caller.  rows % 128 == 0, cout % 128 == 0.  Mode flag 4 (fp32 rows in,
+ * mode 0 only): one bf16 product per MFMA, bf16(x) bf16(w) in fp32 — the bf16 spec. */
 int lidar_dense_x3s_f32(lidar_handle *h, const void *a_planes, int64_t a_plane, int32_t lda, int64_t rows,
                         int32_t k, const void *packed, const float *bias, int32_t cout, int32_t mode,
                         int32_t relu_on, int32_t pool_rows, void *out, int64_t o_plane, int64_t ldo, void *stream);
@@ -192,6 +193,22 @@ int lidar_dense_x3f_f32(lidar_handle *h, const float *a, int32_t lda, int64_t ro
 /* fp32 rows (rows, k), row stride ldx -> split planes (rows, lda) for lidar_dense_x3s_f32 */
 int lidar_split_x3_f32(lidar_handle *h, const float *x, int64_t rows, int32_t k, int64_t ldx, void *planes,
                        int64_t plane, int32_t lda, void *stream);
+
+/* SA branch in the bf16 spec (BASELINE configs[4]) on the fused 16-row kernel of
+ * lidar_sa_group_mlp_x3_f32 with one bf16 product per MFMA: layer inputs and weights rounded to
+ * bf16 (RNE), fp32 accumulation, bias / ReLU / max-pool in fp32.  layer1_mode 0 (xyz level):
+ * p = the level's points (batch, n, 3), q = centres (batch, m, 3).  layer1_mode 2 (feature
+ * level): p (batch*n, p_stride) = bf16(f) bf16(W1_f) + b1 per point (lidar_dense_x3f_f32 with
+ * mode flag 4), xyz = the level's points, centres = (batch, m, 3); a grouped row's layer 1 is
+ * relu(p[k] + bf16(W1_xyz) . bf16(x_k - c)).  packed: lidar_mlp_packed_size_x1(c1, c2, c3)
+ * bytes from lidar_mlp_pack_x1_f32 (host).  Shapes: those of lidar_sa_group_mlp_x3_f32. */
+int64_t lidar_mlp_packed_size_x1(int32_t c1, int32_t c2, int32_t c3);
+int lidar_mlp_pack_x1_f32(int32_t c1, int32_t c2, int32_t c3, const float *w1, const float *b1, const float *w2,
+                          const float *b2, const float *w3, const float *b3, void *packed);
+int lidar_sa_group_mlp_x1_f32(lidar_handle *h, int32_t layer1_mode, const float *p, int64_t p_stride, const float *q,
+                              const float *xyz, const float *centres, const int32_t *idx, int64_t batch, int64_t n,
+                              int64_t m, int32_t nsample, int32_t c1, int32_t c2, int32_t c3, const void *packed,
+                              float *out, int64_t out_stride, int64_t out_offset, void *stream);
 
 /* lidar_sa_group_mlp_f32 with layer 1 applied per point beforehand: p (batch*n, p_stride)
  * = [f, x] W1 + b1 for every point of the level, q (batch*m, p_stride) = centre W1_xyz

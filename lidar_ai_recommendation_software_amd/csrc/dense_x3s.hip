@@ -65,7 +65,9 @@ __device__ __forceinline__ void split8(const f32x4 &a0, const f32x4 &a1, bf16x8 
 // (a layer whose input nobody split, e.g. the first of a chain: the A stage holds 128 rows x
 // 32 fp32 with row r's chunk q at slot q ^ ((r >> 1) & 7), and each wave splits the fragments
 // it reads — dense_x3.hip's loop; worth it where cout / 128 column tiles re-read little)
-template <int MODE, bool AF32>
+// X1: one product ah*bh per MFMA — bf16(x) bf16(w) with fp32 accumulation, the bf16 spec's
+// arithmetic (BASELINE configs[4]), on the same operands
+template <int MODE, bool AF32, bool X1 = false>
 __global__ __launch_bounds__(256, 2) void dense_x3s_kernel(const __bf16 *__restrict__ a, int64_t a_plane, int lda,
                                                            const __bf16 *__restrict__ wp, int ks,
                                                            const float *__restrict__ bias, int relu_on,
@@ -153,7 +155,9 @@ __global__ __launch_bounds__(256, 2) void dense_x3s_kernel(const __bf16 *__restr
             for (int i = 0; i < 2; ++i)
 #pragma unroll
                 for (int j = 0; j < 2; ++j) {
-                    if constexpr (TRANS) {  // D[channel][row]
+                    if constexpr (TRANS && X1) {
+                        acc[i][j] = mfma_bf(wh[j], xh[i], acc[i][j]);
+                    } else if constexpr (TRANS) {  // D[channel][row]
                         acc[i][j] = mfma_bf(wh[j], xh[i], acc[i][j]);
                         acc[i][j] = mfma_bf(wl[j], xh[i], acc[i][j]);
                         acc[i][j] = mfma_bf(wh[j], xl[i], acc[i][j]);
@@ -251,6 +255,9 @@ static int dense_x3s_launch(lidar_handle *h, const void *a_planes, int64_t a_pla
                             int32_t relu_on, int32_t pool_rows, void *out, int64_t o_plane, int64_t ldo, void *stream)
 {
     const bool af32 = a_plane == 0;
+    const bool x1 = (mode & 4) != 0;  // the bf16 spec: one ah*bh product (fp32 rows in and out only)
+    mode &= 3;
+    REQUIRE(!x1 || (af32 && mode == 0), "lidar_dense_x3s_f32: the X1 flag needs fp32 rows in and mode 0");
     REQUIRE(h && a_planes && packed && bias && out, "lidar_dense_x3s_f32: null pointer");
     REQUIRE(rows % SBM == 0 && k > 0 && k <= lda && cout % SBN == 0 && cout > 0,
             "lidar_dense_x3s_f32: rows % 128, k <= lda, cout % 128 must hold");
@@ -279,7 +286,8 @@ static int dense_x3s_launch(lidar_handle *h, const void *a_planes, int64_t a_pla
                            (int)cout, ntn, total, per_xcd, (int)k);
     };
     const int rl = relu_on ? 1 : 0;
-    if (mode == 0) af32 ? go(dense_x3s_kernel<0, true>, rl, 0) : go(dense_x3s_kernel<0, false>, rl, 0);
+    if (x1) go(dense_x3s_kernel<0, true, true>, rl, 0);
+    else if (mode == 0) af32 ? go(dense_x3s_kernel<0, true>, rl, 0) : go(dense_x3s_kernel<0, false>, rl, 0);
     else if (mode == 1) af32 ? go(dense_x3s_kernel<1, true>, rl, 0) : go(dense_x3s_kernel<1, false>, rl, 0);
     else af32 ? go(dense_x3s_kernel<2, true>, 1, (int)pool_rows) : go(dense_x3s_kernel<2, false>, 1, (int)pool_rows);
     LAUNCH_CHECK();

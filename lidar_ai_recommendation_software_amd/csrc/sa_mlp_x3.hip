@@ -61,24 +61,38 @@ __device__ __forceinline__ void split_pair(const f32x4 &t0, const f32x4 &t1, bf1
 // [layer-2 chunks] [layer-3 chunks] [b1 b2 b3 fp32].  Chunk c = output tiles (2c, 2c+1) of a
 // layer with K inputs: u4 at ((s*2 + t)*2 + h)*64 + lane = bf16x8 (h = 0 hi, 1 lo) of
 // W[in(s, lane>>4, j)][16(2c+t) + (lane&15)], j = 0..7, s < K/32.
-template <int C1, int C2, int C3>
+// X1 (the bf16 spec, BASELINE configs[4]): one product ah*bh per MFMA on bf16(x) and bf16(w) —
+// the image keeps the hi fragments only: u4 at (s*2 + t)*64 + lane.
+template <int C1, int C2, int C3, bool X1 = false>
 struct PackX3 {
     static constexpr int T1 = C1 / 16, T2 = C2 / 16, T3 = C3 / 16;
     static constexpr int KS2 = C1 / 32, KS3 = C2 / 32;
-    static constexpr int CH2 = KS2 * 4 * 64, CH3 = KS3 * 4 * 64;  // chunk sizes in u4
-    static constexpr int W1U4 = T1 * 64 / 4;                     // fp32 W1 in u4
+    static constexpr int HALVES = X1 ? 1 : 2;
+    static constexpr int CH2 = KS2 * 2 * HALVES * 64, CH3 = KS3 * 2 * HALVES * 64;  // chunk sizes in u4
+    static constexpr int W1U4 = T1 * 64 / 4;                                       // fp32 W1 in u4
 };
+
+// layer-1 modes: the grouped row's layer-1 output comes from
+//   L1_XYZ  W1 (xyz rows, fp32 in LDS) . (p[k] - c) + b1 on a 16x16x4 fp32 MFMA (levels without features)
+//   L1_PRE  relu(P[k] - Q[c]) with P = [f, x] W1 + b1 per point, Q = c W1_xyz per centre (fp32 path)
+//   L1_PX   relu(P[k] + W1_xyz . bf16(x_k - c)) with P = bf16(f) bf16(W1_f) + b1 per point: the
+//           bf16 spec's layer 1 with the feature part (identical in every group of point k) per point
+enum { L1_XYZ = 0, L1_PRE = 1, L1_PX = 2 };
+__device__ __forceinline__ float bf16r(float v) { return (float)(__bf16)v; }
 
 // R = 16-row tiles per wavefront (R grouped-row tiles of the same centre share every weight
 // fragment read from LDS: R = 2 halves the LDS and L2 weight bytes per MFMA)
-template <int C1, int C2, int C3, int NS, bool XYZ, int R>
+template <int C1, int C2, int C3, int NS, int L1, int R, bool X1>
 __global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float *__restrict__ P, int64_t stride,
                                                      const float *__restrict__ Q, const int32_t *__restrict__ idx,
                                                      int n, int m, int64_t total, const uint4 *__restrict__ packed,
-                                                     float *__restrict__ out, int64_t out_stride, int64_t out_offset)
+                                                     float *__restrict__ out, int64_t out_stride, int64_t out_offset,
+                                                     const float *__restrict__ X, const float *__restrict__ Cn)
 {
     static_assert(NS % (16 * R) == 0 && C1 % 32 == 0 && C2 % 32 == 0 && C3 % 32 == 0, "tile shapes");
-    using K = PackX3<C1, C2, C3>;
+    constexpr bool XYZ = L1 == L1_XYZ, HASW1 = L1 != L1_PRE;
+    using K = PackX3<C1, C2, C3, X1>;
+    constexpr int HV = K::HALVES;
     constexpr int T1 = K::T1, T2 = K::T2, T3 = K::T3, KS2 = K::KS2, KS3 = K::KS3;
     constexpr int CH2 = K::CH2, CH3 = K::CH3, CHMAX = CH2 > CH3 ? CH2 : CH3;
     constexpr int NCH = T2 / 2 + T3 / 2;
@@ -87,7 +101,7 @@ __global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float 
 
     __shared__ uint4 buf[2][CHMAX];
     __shared__ float bias_s[C1 + C2 + C3];
-    __shared__ float w1_s[XYZ ? T1 * 64 : 1];
+    __shared__ float w1_s[HASW1 ? T1 * 64 : 1];
     __shared__ float mx_s[4][4][C3];  // layer 3's running max-pool of the raw accumulators, per (wave, row group)
 
     // wave index in an SGPR: the LDS-DMA destinations (M0) and the unit below are wave-uniform
@@ -98,7 +112,7 @@ __global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float 
     const int64_t cc = live ? unit : total - 1;
     const int64_t b = cc / m;
 
-    const uint4 *W2 = packed + (XYZ ? K::W1U4 : 0);
+    const uint4 *W2 = packed + (HASW1 ? K::W1U4 : 0);
     const uint4 *W3 = W2 + (int64_t)(T2 / 2) * CH2;
     const float *Bias = reinterpret_cast<const float *>(W3 + (int64_t)(T3 / 2) * CH3);
 
@@ -117,7 +131,7 @@ __global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float 
     };
     fetch(0, 0);
     for (int i = tid; i < C1 + C2 + C3; i += 256) bias_s[i] = Bias[i];
-    if constexpr (XYZ)
+    if constexpr (HASW1)
         for (int i = tid; i < T1 * 64; i += 256) w1_s[i] = reinterpret_cast<const float *>(packed)[i];
     for (int i = lane; i < 4 * C3; i += 64) (&mx_s[wave][0][0])[i] = -INFINITY;
     __syncthreads();
@@ -138,12 +152,25 @@ __global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float 
             if constexpr (XYZ) {
                 const float *pr = P + ((int64_t)b * n + k) * 3;
                 const float *ce = Q + cc * 3;
-                const float x = q < 3 ? pr[q] - ce[q] : 0.0f;  // lane group q: dx, dy, dz, 0
+                float x = q < 3 ? pr[q] - ce[q] : 0.0f;  // lane group q: dx, dy, dz, 0
+                if constexpr (X1) x = bf16r(x);  // the bf16 spec rounds the offsets (W1 is pre-rounded)
 #pragma unroll
                 for (int t = 0; t < T1; ++t) {
                     // the bias is the accumulator's initial value (channel 16t + 4q + r)
                     f32x4 acc = *reinterpret_cast<const f32x4 *>(&bias_s[16 * t + 4 * q]);
                     acc = mfma_f(w1_s[t * 64 + lane], x, acc);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) acc[r] = relu_i(acc[r]);
+                    y1[t] = acc;
+                }
+            } else if constexpr (L1 == L1_PX) {
+                const float *pr = X + ((int64_t)b * n + k) * 3;
+                const float *ce = Cn + cc * 3;
+                const float x = bf16r(q < 3 ? pr[q] - ce[q] : 0.0f);
+                const f32x4 *pp = reinterpret_cast<const f32x4 *>(P + ((int64_t)b * n + k) * stride + 4 * q);
+#pragma unroll
+                for (int t = 0; t < T1; ++t) {
+                    f32x4 acc = mfma_f(w1_s[t * 64 + lane], x, pp[4 * t]);
 #pragma unroll
                     for (int r = 0; r < 4; ++r) acc[r] = relu_i(acc[r]);
                     y1[t] = acc;
@@ -191,18 +218,26 @@ __global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float 
             if (c < T2 / 2) {  // layer 2: output tiles 2c, 2c+1 (channel rows x point columns)
 #pragma unroll
                 for (int s = 0; s < KS2; ++s) {
-                    const bf16x8 h0 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 0) * 2 + 0) * 64]);
-                    const bf16x8 l0 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 0) * 2 + 1) * 64]);
-                    const bf16x8 h1 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 1) * 2 + 0) * 64]);
-                    const bf16x8 l1 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 1) * 2 + 1) * 64]);
+                    const bf16x8 h0 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 0) * HV + 0) * 64]);
+                    const bf16x8 h1 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 1) * HV + 0) * 64]);
+                    if constexpr (X1) {
 #pragma unroll
-                    for (int rr = 0; rr < R; ++rr) {
-                        a0[rr] = mfma_bf(h0, xh[rr][s], a0[rr]);
-                        a1[rr] = mfma_bf(h1, xh[rr][s], a1[rr]);
-                        a0[rr] = mfma_bf(h0, xl[rr][s], a0[rr]);
-                        a1[rr] = mfma_bf(h1, xl[rr][s], a1[rr]);
-                        a0[rr] = mfma_bf(l0, xh[rr][s], a0[rr]);
-                        a1[rr] = mfma_bf(l1, xh[rr][s], a1[rr]);
+                        for (int rr = 0; rr < R; ++rr) {
+                            a0[rr] = mfma_bf(h0, xh[rr][s], a0[rr]);
+                            a1[rr] = mfma_bf(h1, xh[rr][s], a1[rr]);
+                        }
+                    } else {
+                        const bf16x8 l0 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 0) * HV + 1) * 64]);
+                        const bf16x8 l1 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 1) * HV + 1) * 64]);
+#pragma unroll
+                        for (int rr = 0; rr < R; ++rr) {
+                            a0[rr] = mfma_bf(h0, xh[rr][s], a0[rr]);
+                            a1[rr] = mfma_bf(h1, xh[rr][s], a1[rr]);
+                            a0[rr] = mfma_bf(h0, xl[rr][s], a0[rr]);
+                            a1[rr] = mfma_bf(h1, xl[rr][s], a1[rr]);
+                            a0[rr] = mfma_bf(l0, xh[rr][s], a0[rr]);
+                            a1[rr] = mfma_bf(l1, xh[rr][s], a1[rr]);
+                        }
                     }
                 }
 #pragma unroll
@@ -226,18 +261,26 @@ __global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float 
                 const int tp = c - T2 / 2;
 #pragma unroll
                 for (int s = 0; s < KS3; ++s) {
-                    const bf16x8 h0 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 0) * 2 + 0) * 64]);
-                    const bf16x8 l0 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 0) * 2 + 1) * 64]);
-                    const bf16x8 h1 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 1) * 2 + 0) * 64]);
-                    const bf16x8 l1 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 1) * 2 + 1) * 64]);
+                    const bf16x8 h0 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 0) * HV + 0) * 64]);
+                    const bf16x8 h1 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 1) * HV + 0) * 64]);
+                    if constexpr (X1) {
 #pragma unroll
-                    for (int rr = 0; rr < R; ++rr) {
-                        a0[rr] = mfma_bf(zh[rr][s], h0, a0[rr]);
-                        a1[rr] = mfma_bf(zh[rr][s], h1, a1[rr]);
-                        a0[rr] = mfma_bf(zh[rr][s], l0, a0[rr]);
-                        a1[rr] = mfma_bf(zh[rr][s], l1, a1[rr]);
-                        a0[rr] = mfma_bf(zl[rr][s], h0, a0[rr]);
-                        a1[rr] = mfma_bf(zl[rr][s], h1, a1[rr]);
+                        for (int rr = 0; rr < R; ++rr) {
+                            a0[rr] = mfma_bf(zh[rr][s], h0, a0[rr]);
+                            a1[rr] = mfma_bf(zh[rr][s], h1, a1[rr]);
+                        }
+                    } else {
+                        const bf16x8 l0 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 0) * HV + 1) * 64]);
+                        const bf16x8 l1 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 1) * HV + 1) * 64]);
+#pragma unroll
+                        for (int rr = 0; rr < R; ++rr) {
+                            a0[rr] = mfma_bf(zh[rr][s], h0, a0[rr]);
+                            a1[rr] = mfma_bf(zh[rr][s], h1, a1[rr]);
+                            a0[rr] = mfma_bf(zh[rr][s], l0, a0[rr]);
+                            a1[rr] = mfma_bf(zh[rr][s], l1, a1[rr]);
+                            a0[rr] = mfma_bf(zl[rr][s], h0, a0[rr]);
+                            a1[rr] = mfma_bf(zl[rr][s], h1, a1[rr]);
+                        }
                     }
                 }
 #pragma unroll
@@ -274,16 +317,17 @@ __global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float 
 #define LIDAR_X3_ROWS 2
 #endif
 
-template <int C1, int C2, int C3, int NS, bool XYZ>
+template <int C1, int C2, int C3, int NS, int L1, bool X1 = false>
 int launch_x3(const float *p, int64_t stride, const float *q, const int32_t *idx, int64_t batch, int64_t n,
-              int64_t m, const void *packed, float *out, int64_t os, int64_t oo, hipStream_t s)
+              int64_t m, const void *packed, float *out, int64_t os, int64_t oo, hipStream_t s,
+              const float *xyz = nullptr, const float *centres = nullptr)
 {
     constexpr int R = NS >= 16 * LIDAR_X3_ROWS ? LIDAR_X3_ROWS : 1;
     const int64_t total = batch * m;
     const int64_t blocks = (total + 3) / 4;
     REQUIRE(blocks <= 0x7fffffff, "sa_group_mlp_x3: too many centres");
-    hipLaunchKernelGGL((sa_x3_kernel<C1, C2, C3, NS, XYZ, R>), dim3((unsigned)blocks), dim3(256), 0, s, p, stride,
-                       q, idx, (int)n, (int)m, total, static_cast<const uint4 *>(packed), out, os, oo);
+    hipLaunchKernelGGL((sa_x3_kernel<C1, C2, C3, NS, L1, R, X1>), dim3((unsigned)blocks), dim3(256), 0, s, p, stride,
+                       q, idx, (int)n, (int)m, total, static_cast<const uint4 *>(packed), out, os, oo, xyz, centres);
     LAUNCH_CHECK();
     return LIDAR_OK;
 }
@@ -374,8 +418,8 @@ LIDAR_EXPORT int lidar_sa_group_mlp_x3_f32(lidar_handle *h, int32_t xyz_level, c
     hipStream_t s = static_cast<hipStream_t>(stream);
 #define LIDAR_SAX3(C1_, C2_, C3_, NS_, X_)                                                                   \
     if (!!xyz_level == X_ && c1 == C1_ && c2 == C2_ && c3 == C3_ && nsample == NS_)                           \
-        return launch_x3<C1_, C2_, C3_, NS_, X_>(p, p_stride, q, idx, batch, n, m, packed, out, out_stride, \
-                                                 out_offset, s);
+        return launch_x3<C1_, C2_, C3_, NS_, X_ ? L1_XYZ : L1_PRE>(p, p_stride, q, idx, batch, n, m, packed, out, \
+                                                                out_stride, out_offset, s);
     LIDAR_SAX3(64, 64, 128, 32, true)
     LIDAR_SAX3(32, 32, 64, 16, true)
     LIDAR_SAX3(64, 96, 128, 128, true)
@@ -384,4 +428,87 @@ LIDAR_EXPORT int lidar_sa_group_mlp_x3_f32(lidar_handle *h, int32_t xyz_level, c
     LIDAR_SAX3(64, 64, 128, 32, false)
 #undef LIDAR_SAX3
     return lidar::fail(LIDAR_EINVAL, "lidar_sa_group_mlp_x3_f32: unsupported (widths, nsample) combination");
+}
+
+// ------------------------------------------------------------------ X1: the bf16 spec
+// bytes of the X1 packed image: [W1 xyz rows fp32 (bf16-rounded), T1*64 floats] [layer-2 / layer-3
+// hi fragments] [b1 b2 b3 fp32]
+LIDAR_EXPORT int64_t lidar_mlp_packed_size_x1(int32_t c1, int32_t c2, int32_t c3)
+{
+    return (int64_t)(c1 / 16) * 64 * 4 + ((int64_t)(c2 / 32) * (c1 / 32) + (int64_t)(c3 / 32) * (c2 / 32)) * 2 * 64 * 16 +
+           (int64_t)(c1 + c2 + c3) * 4;
+}
+
+// host packer of the X1 image: w1 rows 0..2 (the xyz rows of (3 + cfeat, c1)) and w2, w3 rounded
+// to bf16 (RNE), the hi fragments of lidar_mlp_pack_x3_f32's order
+LIDAR_EXPORT int lidar_mlp_pack_x1_f32(int32_t c1, int32_t c2, int32_t c3, const float *w1, const float *b1,
+                                       const float *w2, const float *b2, const float *w3, const float *b3,
+                                       void *packed)
+{
+    REQUIRE(w1 && b1 && w2 && b2 && w3 && b3 && packed, "lidar_mlp_pack_x1_f32: null pointer");
+    REQUIRE(c1 % 32 == 0 && c2 % 32 == 0 && c3 % 32 == 0 && c1 > 0 && c2 > 0 && c3 > 0,
+            "lidar_mlp_pack_x1_f32: widths must be positive multiples of 32");
+    char *o = static_cast<char *>(packed);
+    float *f = reinterpret_cast<float *>(o);
+    for (int t = 0; t < c1 / 16; ++t)
+        for (int l = 0; l < 64; ++l) {
+            const int qq = l >> 4;
+            *f++ = qq < 3 ? bf16_to_f(bf16_rne(w1[(int64_t)qq * c1 + 16 * t + (l & 15)])) : 0.0f;
+        }
+    o = reinterpret_cast<char *>(f);
+    auto layer = [&](const float *w, int cin, int cout) {
+        uint16_t *u = reinterpret_cast<uint16_t *>(o);
+        for (int c = 0; c < cout / 32; ++c)
+            for (int s = 0; s < cin / 32; ++s)
+                for (int t = 0; t < 2; ++t)
+                    for (int l = 0; l < 64; ++l)
+                        for (int j = 0; j < 8; ++j) {
+                            const int in = 32 * s + 16 * (j >> 2) + 4 * (l >> 4) + (j & 3);
+                            *u++ = bf16_rne(w[(int64_t)in * cout + 16 * (2 * c + t) + (l & 15)]);
+                        }
+        o = reinterpret_cast<char *>(u);
+    };
+    layer(w2, c1, c2);
+    layer(w3, c2, c3);
+    f = reinterpret_cast<float *>(o);
+    for (int i = 0; i < c1; ++i) *f++ = b1[i];
+    for (int i = 0; i < c2; ++i) *f++ = b2[i];
+    for (int i = 0; i < c3; ++i) *f++ = b3[i];
+    return LIDAR_OK;
+}
+
+// SA branch in the bf16 spec (BASELINE configs[4]): layer inputs and weights
+// rounded to bf16, fp32 accumulation, bias / ReLU / max-pool in fp32.  layer1_mode 0 (xyz
+// level): p = the level's points (batch, n, 3), q = centres (batch, m, 3).  layer1_mode 2
+// (feature level): p (batch*n, p_stride) = bf16(f) bf16(W1_f) + b1 per point (lidar_dense_x3f_f32
+// with the X1 flag), xyz = the level's points, centres; a grouped row's layer 1 is
+// relu(p[k] + bf16(W1_xyz) . bf16(x_k - c)).  packed = lidar_mlp_pack_x1_f32's image.
+LIDAR_EXPORT int lidar_sa_group_mlp_x1_f32(lidar_handle *h, int32_t layer1_mode, const float *p, int64_t p_stride,
+                                           const float *q, const float *xyz, const float *centres,
+                                           const int32_t *idx, int64_t batch, int64_t n, int64_t m, int32_t nsample,
+                                           int32_t c1, int32_t c2, int32_t c3, const void *packed, float *out,
+                                           int64_t out_stride, int64_t out_offset, void *stream)
+{
+    REQUIRE(h && p && idx && packed && out, "lidar_sa_group_mlp_x1_f32: null pointer");
+    REQUIRE(layer1_mode == 0 || layer1_mode == 2, "lidar_sa_group_mlp_x1_f32: layer1_mode must be 0 or 2");
+    REQUIRE(layer1_mode == 2 ? (xyz && centres && p_stride >= c1 && p_stride % 4 == 0) : q != nullptr,
+            "lidar_sa_group_mlp_x1_f32: mode 0 needs q = centres; mode 2 needs xyz, centres, p_stride >= c1");
+    REQUIRE(batch >= 0 && n >= 1 && m >= 1, "lidar_sa_group_mlp_x1_f32: bad sizes");
+    REQUIRE(out_offset >= 0 && out_offset + c3 <= out_stride,
+            "lidar_sa_group_mlp_x1_f32: output columns exceed out_stride");
+    if (batch == 0) return LIDAR_OK;
+    HIP_TRY(hipSetDevice(h->device));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+#define LIDAR_SAX1(C1_, C2_, C3_, NS_, M_)                                                                    \
+    if (layer1_mode == M_ && c1 == C1_ && c2 == C2_ && c3 == C3_ && nsample == NS_)                           \
+        return launch_x3<C1_, C2_, C3_, NS_, M_, true>(p, p_stride, M_ == 0 ? q : nullptr, idx, batch, n, m,   \
+                                                       packed, out, out_stride, out_offset, s, xyz, centres);
+    LIDAR_SAX1(32, 32, 64, 16, 0)
+    LIDAR_SAX1(64, 64, 128, 32, 0)
+    LIDAR_SAX1(64, 96, 128, 128, 0)
+    LIDAR_SAX1(64, 64, 128, 32, 2)
+    LIDAR_SAX1(128, 128, 256, 64, 2)
+    LIDAR_SAX1(128, 128, 256, 128, 2)
+#undef LIDAR_SAX1
+    return lidar::fail(LIDAR_EINVAL, "lidar_sa_group_mlp_x1_f32: unsupported (widths, nsample) combination");
 }

@@ -227,6 +227,51 @@ def pack_branch_x3(layers, xyz_level):
     return out
 
 
+def pack_branch_x1(layers):
+    """Host-side packed image (uint8) for lidar_sa_group_mlp_x1_f32 (bf16 spec: bf16-rounded
+    W1 xyz rows, hi fragments of W2 / W3, fp32 biases)."""
+    (w1, b1), (w2, b2), (w3, b3) = layers
+    c1, c2, c3 = w1.shape[1], w2.shape[1], w3.shape[1]
+    lib = nat.load_library()
+    out = np.zeros(lib.lidar_mlp_packed_size_x1(c1, c2, c3), dtype=np.uint8)
+    arrs = [np.ascontiguousarray(a, dtype=np.float32) for a in (w1, b1, w2, b2, w3, b3)]
+    nat.check(lib.lidar_mlp_pack_x1_f32(c1, c2, c3, *[a.ctypes.data_as(ctypes.c_void_p) for a in arrs],
+                                        out.ctypes.data_as(ctypes.c_void_p)), "lidar_mlp_pack_x1_f32")
+    return out
+
+
+def group_mlp_x1(p, idx, n, packed, widths, out, out_offset=0, xyz=None, centres=None):
+    """One SA branch in the bf16 spec (lidar_sa_group_mlp_x1_f32).  xyz level: p = the level's
+    points (B, n, 3), centres (B, M, 3).  Feature level: p (B*n, stride) = bf16(f) bf16(W1_f) + b1
+    per point (layer1_points_x1), xyz = the level's points, centres."""
+    B, M, ns = idx.shape
+    c1, c2, c3 = widths
+    mode = 2 if xyz is not None else 0
+    if mode == 0:
+        _dev_check(p, centres, idx, packed, out)
+        stride = 3
+    else:
+        _dev_check(p, xyz, centres, idx, packed, out)
+        stride = p.shape[-1]
+        if p.shape[0] < B * n or stride < c1:
+            raise ValueError("group_mlp_x1: per-point rows do not match the batch")
+    nat.call("lidar_sa_group_mlp_x1_f32", nat.handle(p.device.index), mode, nat.ptr(p), stride,
+             nat.ptr(centres) if mode == 0 else None, nat.ptr(xyz), nat.ptr(centres), nat.ptr(idx), B, n, M, ns,
+             c1, c2, c3, nat.ptr(packed), nat.ptr(out), out.shape[-1], out_offset, nat.stream_ptr())
+    return out
+
+
+def layer1_points_x1(x_rows, xyz, cfeat, branches):
+    """Per-point layer-1 feature part of a bf16-spec level: P = bf16(f) bf16(W1_f) + b1 for every
+    branch (x_rows: the level's padded rows [f, x, y, z, 0-pad]; the xyz rows of W1_f are zero,
+    the offsets' part runs per grouped row in lidar_sa_group_mlp_x1_f32)."""
+    B, N, _ = xyz.shape
+    nat.call("lidar_concat_xyz_pad_f32", nat.handle(xyz.device.index), nat.ptr(xyz), B * N, nat.ptr(x_rows),
+             x_rows.shape[1], cfeat, nat.stream_ptr())
+    return [dense_x3s(x_rows, br["pre_x1"]["w1f_x3"], br["pre_x1"]["b1"], br["pre_x1"]["w1f"].shape[1],
+                      relu=False, x1=True) for br in branches]
+
+
 def group_mlp_x3(p, q, idx, n, packed, widths, out, out_offset=0, xyz_level=False):
     """group_mlp16 with layers 2-3 on split-bf16 MFMAs (fp32-accurate, see sa_mlp_x3.hip)."""
     B, M, ns = idx.shape
@@ -383,7 +428,7 @@ def split_x3(x, k=None):
     return SplitPlanes(planes, k)
 
 
-def dense_x3s(a, wpack, b, cout, relu=True, split_out=False, pool_rows=0, out=None):
+def dense_x3s(a, wpack, b, cout, relu=True, split_out=False, pool_rows=0, out=None, x1=False):
     """a @ W + b on the x3 GEMM of csrc/dense_x3s.hip (wpack = pack_dense_x3(W)): a is
     SplitPlanes (lidar_dense_x3s_f32) or fp32 rows (rows, k) (lidar_dense_x3f_f32, split in
     the tile loop).  Returns fp32 rows (rows, cout), SplitPlanes (split_out) or, with
@@ -408,7 +453,8 @@ def dense_x3s(a, wpack, b, cout, relu=True, split_out=False, pool_rows=0, out=No
     if f32:
         _dev_check(a, wpack, b, out)
         nat.call("lidar_dense_x3f_f32", nat.handle(dev.index), nat.ptr(a), lda, rows, lda, nat.ptr(wpack), nat.ptr(b),
-                 cout, mode, 1 if relu else 0, pool_rows, nat.ptr(out), oplane, ldo, nat.stream_ptr())
+                 cout, mode | (4 if x1 else 0), 1 if relu else 0, pool_rows, nat.ptr(out), oplane, ldo,
+                 nat.stream_ptr())
         return res
     _dev_check(a.planes, wpack, b, out)
     nat.call("lidar_dense_x3s_f32", nat.handle(dev.index), nat.ptr(a.planes), rows * lda, lda, rows, a.k,
@@ -460,7 +506,7 @@ class PointNet2Backbone:
     (B, C_last) plus the per-level (new_xyz, features, fps_idx)."""
 
     def __init__(self, cfg=SSG, weights=None, device="cuda", seed=0, dtype="f32", pre_layer1=True, mlp16="pre", x3=True,
-                 x3s=True):
+                 x3s=True, x1=True):
         """dtype "bf16": the SA branches run on bf16 MFMA (inputs/activations/weights rounded
         to bf16, fp32 accumulation; BASELINE configs[4]); group_all stays fp32.
         pre_layer1 (fp32, levels with point features): layer 1 runs per point as a GEMM
@@ -470,7 +516,9 @@ class PointNet2Backbone:
         xyz-only levels.
         x3 (fp32): the same branches on the split-bf16 kernels (lidar_sa_group_mlp_x3_f32;
         True, or "pre" / "xyz" for one kind of level).
-        x3s (with x3): the dense layers on the split-plane GEMM (dense_x3s / split_x3)."""
+        x3s (with x3): the dense layers on the split-plane GEMM (dense_x3s / split_x3).
+        x1 (bf16): the branches on the fused 16-row kernel with one bf16 product per MFMA
+        (lidar_sa_group_mlp_x1_f32), feature levels with the per-point feature part of layer 1."""
         if dtype not in ("f32", "bf16"):
             raise ValueError("dtype must be 'f32' or 'bf16'")
         self.bf16 = dtype == "bf16"
@@ -511,15 +559,29 @@ class PointNet2Backbone:
                         br["packed_x3"] = torch.from_numpy(pack_branch_x3(layers, xyz_level)).to(self.device)
                     if pre:
                         br["pre"] = layer1_weights(layers[0], cfeat, t)
+                    if self.bf16 and x1 and (xyz_level, *widths, ns) in MLP16_SHAPES:
+                        br["packed_x1"] = torch.from_numpy(pack_branch_x1(layers)).to(self.device)
+                        if not xyz_level:  # W1_f: rows [f..., (x, y, z) = 0, 0-pad], columns to 128
+                            w1, b1 = layers[0]
+                            cp = (w1.shape[1] + 127) // 128 * 128
+                            w1f = np.zeros((kp, cp), np.float32)
+                            w1f[:cfeat, :w1.shape[1]] = w1[3:]
+                            b1p = np.zeros(cp, np.float32)
+                            b1p[:w1.shape[1]] = b1
+                            br["pre_x1"] = {"w1f": t(w1f), "b1": t(b1p)}
+                            br["pre_x1"]["w1f_x3"] = pack_dense_x3(br["pre_x1"]["w1f"])
                     branches.append(br)
                 entry = {"div": lvl["npoint_div"], "branches": branches, "cfeat": cfeat}
                 if pre:
                     entry.update(pre=True, k=kp)
+                if cfeat > 0 and branches and all("pre_x1" in br for br in branches):
+                    entry.update(pre=True, pre_x1=True, k=kp)  # the previous level writes padded rows
                 self.levels.append(entry)
                 cfeat = sum(w[-1] for w in lvl["mlps"])
         self.out_channels = cfeat
         # x3 on: the dense layers (per-point layer 1, group_all) on the split-bf16 GEMM too
-        self.x3_dense = bool(x3) and not self.bf16
+        # (bf16 too: group_all stays in fp32 arithmetic, DESIGN.md §3 — x3 is that contract)
+        self.x3_dense = bool(x3)
         # x3s: the dense layers take split planes (split once per input, dense1 -> dense2 -> dense3
         # hand them over) instead of splitting fp32 activations inside every GEMM tile
         self.x3_split = self.x3_dense and bool(x3s)
@@ -573,7 +635,10 @@ class PointNet2Backbone:
             out_rows = torch.empty((R, stride), dtype=torch.float32, device=xyz.device)
             out = out_rows[:B * M].view(B, M, stride)
             pq = None
-            if lvl.get("pre"):
+            if lvl.get("pre_x1"):
+                pq = _call(self.timers, f"sa{li + 1}_layer1_points", layer1_points_x1, rows, xyz, lvl["cfeat"],
+                           lvl["branches"])
+            elif lvl.get("pre"):
                 pq = _call(self.timers, f"sa{li + 1}_layer1_points", layer1_per_point, rows, xyz, lvl["cfeat"],
                            new_xyz, lvl["branches"], x3=self.x3_dense, x3s=self.x3_split)
             off = 0
@@ -584,7 +649,14 @@ class PointNet2Backbone:
                 else:
                     gidx = _call(self.timers, f"{tag}_ball_query", ball_query, br["r"], br["ns"], xyz, new_xyz,
                                  grid=pl.get("grid"))
-                if "packed_x3" in br:
+                if "packed_x1" in br:
+                    if pq is not None:
+                        _call(self.timers, f"{tag}_group_mlp", group_mlp_x1, pq[bi_], gidx, N, br["packed_x1"],
+                              br["widths"], out=out, out_offset=off, xyz=xyz, centres=new_xyz)
+                    else:
+                        _call(self.timers, f"{tag}_group_mlp", group_mlp_x1, xyz, gidx, N, br["packed_x1"],
+                              br["widths"], out=out, out_offset=off, centres=new_xyz)
+                elif "packed_x3" in br:
                     p16, q16 = (pq[bi_] if pq is not None else (xyz, new_xyz))
                     _call(self.timers, f"{tag}_group_mlp", group_mlp_x3, p16, q16, gidx, N, br["packed_x3"],
                           br["widths"], out=out, out_offset=off, xyz_level=pq is None)

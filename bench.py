@@ -219,8 +219,9 @@ def main():
                     help="1: SA2's FPS and ball queries (they need only SA1's centres) on the side streams")
     ap.add_argument("--no-fp32-mfma-leg", action="store_true",
                     help="skip the extra measurement of the native fp32-MFMA kernels (when --x3 is on)")
-    ap.add_argument("--msg-batch", type=int, default=8, help="frames per GPU per step of the configs[4] MSG leg")
-    ap.add_argument("--msg-steps", type=int, default=24)
+    ap.add_argument("--msg-batch", type=int, default=32,
+                    help="frames per GPU per step of the configs[4] MSG leg (32: the per-GPU share of 256 frames)")
+    ap.add_argument("--msg-steps", type=int, default=30)
     ap.add_argument("--msg-x3", type=int, default=0, help="1: also time the MSG leg in fp32 on the x3 kernels")
     ap.add_argument("--no-extras", action="store_true", help="skip the configs[1]/[4] side measurements")
     ap.add_argument("--no-density", action="store_true", help="skip the Tier R density-path leg")

@@ -489,6 +489,51 @@ def test_group_mlp_bf16(cuda, cfg_name, level, branch):
         bf16_close(got[bi], want, f"bf16 {cfg_name} L{level} br{branch} frame {bi}")
 
 
+@pytest.mark.parametrize("cfg_name,level,branch", [("msg", 0, 0), ("msg", 0, 1), ("msg", 0, 2), ("msg", 1, 0),
+                                                   ("msg", 1, 1), ("msg", 1, 2), ("ssg", 0, 0), ("ssg", 1, 0)])
+def test_group_mlp_x1(cuda, cfg_name, level, branch):
+    """The bf16 spec on the fused 16-row kernel (lidar_sa_group_mlp_x1_f32): xyz levels in one
+    launch, feature levels with the per-point X1 GEMM for layer 1's feature part."""
+    cfg = pn.CONFIGS[cfg_name]
+    w = pn.init_weights(cfg, seed=3)
+    lvl = cfg["levels"][level]
+    layers = w[level][branch]
+    cfeat = layers[0][0].shape[0] - 3
+    r, ns, widths = lvl["radii"][branch], lvl["nsamples"][branch], lvl["mlps"][branch]
+    B, N, M = 2, 2048, 128
+    rng = np.random.default_rng(7)
+    x = unit_frames(B, N, 9)
+    f = np.abs(rng.standard_normal((B, N, cfeat))).astype(np.float32) if cfeat else None
+    c = x[:, :M].copy()
+    gi = tier_n.ball_query(x, c, r, ns)
+    T = lambda a: None if a is None else torch.from_numpy(np.ascontiguousarray(a)).to(cuda)
+    packed = torch.from_numpy(pn.pack_branch_x1(layers)).to(cuda)
+    out = torch.empty((B, M, widths[-1]), dtype=torch.float32, device=cuda)
+    if cfeat == 0:
+        pn.group_mlp_x1(T(x), T(gi), N, packed, widths, out, centres=T(c))
+    else:
+        kp = (cfeat + 3 + 15) // 16 * 16
+        w1, b1 = layers[0]
+        cp = (w1.shape[1] + 127) // 128 * 128
+        w1f = np.zeros((kp, cp), np.float32)
+        w1f[:cfeat, :w1.shape[1]] = w1[3:]
+        b1p = np.zeros(cp, np.float32)
+        b1p[:w1.shape[1]] = b1
+        rows = np.zeros((B * N, kp), np.float32)
+        rows[:, :cfeat] = f.reshape(B * N, cfeat)
+        rows[:, cfeat:cfeat + 3] = x.reshape(B * N, 3)
+        P = pn.dense_x3s(T(rows), pn.pack_dense_x3(T(w1f)), T(b1p), cp, relu=False, x1=True)
+        # the X1 GEMM is the bf16 spec's product: bf16(f) bf16(W1_f) in fp32
+        want_p = tier_n.bf16_round(rows).astype(np.float64) @ tier_n.bf16_round(w1f).astype(np.float64) + b1p
+        feat_close(P.cpu().numpy(), want_p, "X1 GEMM")
+        pn.group_mlp_x1(P, T(gi), N, packed, widths, out, xyz=T(x), centres=T(c))
+    got = out.cpu().numpy()
+    for bi in range(B):
+        fin = None if f is None else tier_n.bf16_round(f[bi])
+        want = tier_n.mlp_maxpool(tier_n.group(x[bi], fin, c[bi], gi[bi]), layers, ns, bf16=True)
+        bf16_close(got[bi], want, f"x1 {cfg_name} L{level} br{branch} frame {bi}")
+
+
 @pytest.mark.parametrize("cfg_name,n", [("msg", 16384), ("ssg", 16384)])
 def test_backbone_bf16_vs_oracle(cuda, cfg_name, n):
     cfg = pn.CONFIGS[cfg_name]

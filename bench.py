@@ -213,6 +213,9 @@ def main():
     ap.add_argument("--x3", default="1", choices=["0", "1", "pre", "xyz"],
                     help="SA layers 2-3 on the split-bf16 (x3) kernels: fp32 arithmetic within the 1e-4 "
                          "contract; 0 = native fp32 MFMA kernels")
+    ap.add_argument("--shared-bin", type=int, default=0,
+                    help="1: one ball-query binning per group for all branches (MSG: 452 vs 468-494 M pts/s, off)")
+    ap.add_argument("--reserve", type=int, default=1, help="1: size the side handles' workspaces at setup")
     ap.add_argument("--x3s", type=int, default=1, help="1: dense layers on the split-plane x3 GEMM")
     ap.add_argument("--bq-main", type=int, default=0, help="1: SA1 ball queries on the main stream (0: on the FPS side streams)")
     ap.add_argument("--l1-side", type=int, default=0,
@@ -258,7 +261,8 @@ def main():
         pipe = pn.StreamingSSG(bb, B, N, depth=depth, side_priority=args.side_priority,
                                side_cus=args.side_cus, cu_layout=args.cu_layout, fps_group=args.fps_group,
                                bq_on_main=bool(args.bq_main), fps_threads=args.fps_threads,
-                               level1_on_side=bool(args.l1_side))
+                               level1_on_side=bool(args.l1_side), shared_bin=bool(args.shared_bin),
+                               reserve=bool(args.reserve))
         ref, _ = bb.forward(x)
         outs = pipe.run([x] * max(2, warmup))
         torch.cuda.synchronize(dev)

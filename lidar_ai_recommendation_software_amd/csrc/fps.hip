@@ -537,6 +537,12 @@ static int launch_fps(const float *xyz, int64_t batch, int64_t n, int64_t npoint
     return LIDAR_OK;
 }
 
+// workspace bytes lidar_fps_f32 / lidar_fps_ex_f32 take from the handle for (batch, n)
+LIDAR_EXPORT uint64_t lidar_fps_workspace_bytes(int64_t batch, int64_t n)
+{
+    return (uint64_t)(batch * lidar::align_up(5 * lidar::align_up(n, 64), 64)) * 4;
+}
+
 // threads: workgroup size per frame, 0 (the build default, 1024), 1024, 512 or 256 — same results
 LIDAR_EXPORT int lidar_fps_ex_f32(lidar_handle *h, const float *xyz, int64_t batch, int64_t n, int64_t npoint,
                                   int32_t *idx, float *new_xyz, int32_t *first_zero, const int32_t *prefix_ok,

@@ -766,7 +766,7 @@ class StreamingSSG:
     """
 
     def __init__(self, backbone, batch, n, depth=1, side_priority=0, side_cus=0, cu_layout="xcd", fps_group=1,
-                 bq_on_main=False, fps_threads=0, level1_on_side=False):
+                 bq_on_main=False, fps_threads=0, level1_on_side=False, shared_bin=False, reserve=True):
         """side_cus > 0: the SA1 FPS / ball-query streams run on `side_cus` CUs and the
         main stream on the rest (CU-masked HIP streams; measured slower).
         cu_layout "xcd" takes side_cus/8 CUs of each of the 8 XCDs (mask bit = 32*xcd + cu),
@@ -805,8 +805,18 @@ class StreamingSSG:
                       for br in lvl0["branches"]] for _ in range(nslot)]
         # bq_on_main: the level-0 frames are binned for the ball query on the side stream
         # (it depends only on the frames), once for all branches at the largest radius
-        self.grid = [ball_query_grid_buffer(GB, n, dev) if self.bq_on_main and n >= BQ_GRID_MIN_N else None
-                     for _ in range(nslot)]
+        # the level-0 frames are binned once per group (largest radius, valid for every branch's
+        # query) — on the side stream, for the main stream's queries (bq_on_main) or its own
+        # (shared_bin=False: each side-stream query bins for its own radius)
+        self.grid = [ball_query_grid_buffer(GB, n, dev) if (self.bq_on_main or shared_bin) and n >= BQ_GRID_MIN_N
+                     else None for _ in range(nslot)]
+        # setup-time workspace sizing of the side handles (FPS + ball queries), so no stage's
+        # first call allocates (a grow re-allocates after a device sync)
+        if reserve:
+            lib = nat.load_library()
+            need = max(lib.lidar_fps_workspace_bytes(GB, n), lib.lidar_ball_query_grid_bytes(GB, n))
+            for sl in range(1, depth + 1):
+                nat.call("lidar_workspace_reserve", nat.handle(dev.index, sl), need)
         if self.l1:
             self.M2 = max(1, n // lvl1["div"])
             self.idx2 = [torch.empty((GB, self.M2), dtype=torch.int32, device=dev) for _ in range(nslot)]
@@ -865,7 +875,7 @@ class StreamingSSG:
             for bi_, br in enumerate([] if self.bq_on_main else lvl0["branches"]):
                 tag = "sa1" + (f"_b{bi_}" if len(lvl0["branches"]) > 1 else "")
                 _call(self.bb.timers, f"{tag}_ball_query", ball_query, br["r"], br["ns"], x, self.cxyz[slot][:g],
-                      out=self.gidx[slot][bi_][:g], slot=1 + k % self.depth)
+                      out=self.gidx[slot][bi_][:g], slot=1 + k % self.depth, grid=self.grid[slot])
             if self.l1:
                 hs = 1 + k % self.depth
                 c1 = self.cxyz[slot][:g]

@@ -15,7 +15,8 @@ x3 = {"0": False, "1": True}.get(sys.argv[9], sys.argv[9]) if len(sys.argv) > 9 
 bb = pn.PointNet2Backbone(pn.CONFIGS[cfg_name], device=dev, seed=0, dtype=dtype, mlp16=mlp16, x3=x3)
 x = torch.from_numpy(unit_frames(B, N, 0)).to(dev)
 bqm = len(sys.argv) > 10 and sys.argv[10] == "1"
-pipe = pn.StreamingSSG(bb, B, N, depth=depth, fps_group=group, bq_on_main=bqm)
+fpst = int(sys.argv[11]) if len(sys.argv) > 11 else 0
+pipe = pn.StreamingSSG(bb, B, N, depth=depth, fps_group=group, bq_on_main=bqm, fps_threads=fpst)
 pipe.run([x] * 3)
 torch.cuda.synchronize()
 t0 = time.perf_counter()

@@ -194,7 +194,7 @@ def variant_leg(rank, world, frames=8, n=65536, cpu=True, cpu_budget=6.0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=120,
+    ap.add_argument("--steps", type=int, default=240,
                     help="timed steps; the pipeline fill (one SA1-FPS latency, ~12 ms) is inside the window")
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=32, help="frames per GPU per step")
@@ -215,6 +215,7 @@ def main():
                          "contract; 0 = native fp32 MFMA kernels")
     ap.add_argument("--shared-bin", type=int, default=0,
                     help="1: one ball-query binning per group for all branches (MSG: 452 vs 468-494 M pts/s, off)")
+    ap.add_argument("--ramp", type=int, default=1, help="1: first groups of 1, 2, .. batches (shorter fill)")
     ap.add_argument("--reserve", type=int, default=1, help="1: size the side handles' workspaces at setup")
     ap.add_argument("--x3s", type=int, default=1, help="1: dense layers on the split-plane x3 GEMM")
     ap.add_argument("--bq-main", type=int, default=0, help="1: SA1 ball queries on the main stream (0: on the FPS side streams)")
@@ -262,7 +263,7 @@ def main():
                                side_cus=args.side_cus, cu_layout=args.cu_layout, fps_group=args.fps_group,
                                bq_on_main=bool(args.bq_main), fps_threads=args.fps_threads,
                                level1_on_side=bool(args.l1_side), shared_bin=bool(args.shared_bin),
-                               reserve=bool(args.reserve))
+                               reserve=bool(args.reserve), ramp=bool(args.ramp))
         ref, _ = bb.forward(x)
         outs = pipe.run([x] * max(2, warmup))
         torch.cuda.synchronize(dev)

@@ -766,13 +766,14 @@ class StreamingSSG:
     """
 
     def __init__(self, backbone, batch, n, depth=1, side_priority=0, side_cus=0, cu_layout="xcd", fps_group=1,
-                 bq_on_main=False, fps_threads=0, level1_on_side=False, shared_bin=False, reserve=True):
+                 bq_on_main=False, fps_threads=0, level1_on_side=False, shared_bin=False, reserve=True, ramp=True):
         """side_cus > 0: the SA1 FPS / ball-query streams run on `side_cus` CUs and the
         main stream on the rest (CU-masked HIP streams; measured slower).
         cu_layout "xcd" takes side_cus/8 CUs of each of the 8 XCDs (mask bit = 32*xcd + cu),
         "low" the lowest-numbered CUs."""
         self.bb = backbone
         self.B, self.N, self.depth, self.G = batch, n, depth, max(1, int(fps_group))
+        self.ramp = bool(ramp)  # first groups of 1, 2, ... batches (shorter pipeline fill)
         self.bq_on_main = bool(bq_on_main)  # level-0 ball queries on the main stream instead
         self.fps_threads = int(fps_threads)  # SA1 FPS workgroup size (0 = 1024; 512: half the CU footprint)
         # level1_on_side: SA2's FPS (over SA1's centres) and ball queries depend only on SA1's FPS
@@ -921,7 +922,14 @@ class StreamingSSG:
         main = torch.cuda.current_stream(self.bb.device)
         ready = torch.cuda.Event()
         ready.record(main)  # the inputs exist on the caller's stream
-        groups = [inputs[i:i + self.G] for i in range(0, len(inputs), self.G)]
+        # ramp: groups of 1, 2, ... G batches — the first group's FPS (the pipeline fill, during
+        # which the main stream waits) is a third as long as a full group's; results are per
+        # frame, so the grouping never changes them
+        groups, i, k = [], 0, 0
+        while i < len(inputs):
+            sz = min(self.G, k + 1) if self.ramp else self.G
+            groups.append(inputs[i:i + sz])
+            i, k = i + sz, k + 1
         outs = []
         pending = []
         for k, xs in enumerate(groups):

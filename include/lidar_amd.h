@@ -62,10 +62,8 @@ int lidar_version(void);
  * CrowdDensityModel's optional PointNet++ backbone (models/crowd_density_model.py:14).
  */
 
-/* workspace bytes the FPS entry points take from a handle for (batch, n), and a setup-time
- * reservation of a handle's workspace (pipelines call it once per stage handle) */
+/* workspace bytes the FPS entry points take from a handle for (batch, n) (for lidar_reserve) */
 uint64_t lidar_fps_workspace_bytes(int64_t batch, int64_t n);
-int lidar_workspace_reserve(lidar_handle *h, uint64_t bytes);
 
 /* farthest-point sampling: idx (batch, npoint) int32; optionally new_xyz (batch, npoint, 3)
  * = xyz[idx] (pass NULL to skip).  Start index 0, fp32 no-FMA distances, lowest index on

@@ -68,7 +68,6 @@ SIGNATURES = {
     "lidar_dense_x3f_f32": [P, P, I32, I64, I32, P, P, I32, I32, I32, I32, P, I64, I64, P],
     "lidar_mlp_packed_size_x1": [I32, I32, I32],
     "lidar_fps_workspace_bytes": [I64, I64],
-    "lidar_workspace_reserve": [P, ctypes.c_uint64],
     "lidar_mlp_pack_x1_f32": [I32, I32, I32, P, P, P, P, P, P, P],
     "lidar_sa_group_mlp_x1_f32": [P, I32, P, I64, P, P, P, P, I64, I64, I64, I32, I32, I32, I32, P, P, I64, I64, P],
     "lidar_mlp_packed_size16": [I32, I32, I32, I32],

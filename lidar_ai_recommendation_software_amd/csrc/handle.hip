@@ -40,15 +40,6 @@ void *workspace(lidar_handle *h, uint64_t bytes)
 
 LIDAR_EXPORT int lidar_version(void) { return 1; }
 
-// grow the handle's workspace to at least `bytes` now (setup time), so the first calls of a
-// pipeline stage do not allocate (a grow re-allocates after a device sync)
-LIDAR_EXPORT int lidar_workspace_reserve(lidar_handle *h, uint64_t bytes)
-{
-    REQUIRE(h != nullptr, "lidar_workspace_reserve: null handle");
-    HIP_TRY(hipSetDevice(h->device));
-    return bytes == 0 || lidar::workspace(h, bytes) ? LIDAR_OK : LIDAR_ENOMEM;
-}
-
 LIDAR_EXPORT const char *lidar_last_error(void) { return lidar::g_err.c_str(); }
 
 LIDAR_EXPORT int lidar_create(int device, lidar_handle **out)

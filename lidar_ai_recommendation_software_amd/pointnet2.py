@@ -812,12 +812,12 @@ class StreamingSSG:
         self.grid = [ball_query_grid_buffer(GB, n, dev) if (self.bq_on_main or shared_bin) and n >= BQ_GRID_MIN_N
                      else None for _ in range(nslot)]
         # setup-time workspace sizing of the side handles (FPS + ball queries), so no stage's
-        # first call allocates (a grow re-allocates after a device sync)
+        # first call allocates (lidar_reserve; a grow re-allocates after a device sync)
         if reserve:
             lib = nat.load_library()
             need = max(lib.lidar_fps_workspace_bytes(GB, n), lib.lidar_ball_query_grid_bytes(GB, n))
             for sl in range(1, depth + 1):
-                nat.call("lidar_workspace_reserve", nat.handle(dev.index, sl), need)
+                nat.call("lidar_reserve", nat.handle(dev.index, sl), need)
         if self.l1:
             self.M2 = max(1, n // lvl1["div"])
             self.idx2 = [torch.empty((GB, self.M2), dtype=torch.int32, device=dev) for _ in range(nslot)]

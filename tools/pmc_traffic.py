@@ -50,18 +50,19 @@ def label(name, grid, F=FRAMES_PER_LAUNCH):
         return {F * 4096 * 64: "sa1_ball_query", F * 1024 * 64: "sa2_ball_query"}.get(grid)
     if "bq_bin_kernel" in name:
         return "bq_bin"  # one 1024-thread workgroup per frame: SA1 (65536 pts) vs SA2 (4096) by duration
+    # sa_x3_kernel<C1, C2, C3, NS, layer-1 mode (0 xyz, 1 pre, 2 px), R, X1>
     if any(k in name for k in ("sa_group_mlp_kernel<0, 64, 64, 128, 32", "sa_pre_lds_kernel<64, 64, 128, 32, true",
-                                "sa16_kernel<64, 64, 128, 32, true", "sa_x3_kernel<64, 64, 128, 32, true")):
+                                "sa16_kernel<64, 64, 128, 32, true", "sa_x3_kernel<64, 64, 128, 32, 0, 2, false")):
         return "sa1_group_mlp"
     if any(k in name for k in ("sa_group_mlp_kernel<128, 128, 128, 256, 64", "sa_pre_lds_kernel<128, 128, 256, 64",
-                                "sa16_kernel<128, 128, 256, 64, false", "sa_x3_kernel<128, 128, 256, 64, false")):
+                                "sa16_kernel<128, 128, 256, 64, false", "sa_x3_kernel<128, 128, 256, 64, 1, 2, false")):
         return "sa2_group_mlp"
     if "dense_relu_kernel" in name or "dense_x3_kernel" in name or "dense_x3p_kernel" in name:
         return {F * 4096 * 2: "dense_shared", F * 1024 * 2: "sa2_layer1_points", F * 1024 * 4: "sa3_dense1",
                 F * 1024 * 16: "sa3_dense3_pool"}.get(grid)
     if "dense_x3s_kernel<" in name:  # split-plane GEMM: <mode, fp32-input>
-        for key, lab in (("<0, true>", "sa2_layer1_points"), ("<1, true>", "sa3_dense1"),
-                         ("<1, false>", "sa3_dense2"), ("<2, false>", "sa3_dense3_pool")):
+        for key, lab in (("<0, true, false>", "sa2_layer1_points"), ("<1, true, false>", "sa3_dense1"),
+                         ("<1, false, false>", "sa3_dense2"), ("<2, false, false>", "sa3_dense3_pool")):
             if key in name:
                 return lab
         return None
@@ -129,7 +130,7 @@ def main(cf, cw, pf, pw, out):
     res = {"config": {"workload": "ssg", "points_per_frame": 65536, "frames_per_gpu": 32,
                       "frames_per_launch": FRAMES_PER_LAUNCH},
            "source": "rocprofv3 --kernel-trace --pmc FETCH_SIZE | WRITE_SIZE (separate passes) of "
-                     "bench.py --no-extras --no-cpu-baseline --no-density --no-fp32-mfma-leg --steps 4 --warmup 1",
+                     "bench.py --no-extras --no-cpu-baseline --no-density --no-fp32-mfma-leg --ramp 0 --steps 6 --warmup 1",
            "calibration": cal, "kernels": kern}
     os.makedirs(os.path.dirname(out) or ".", exist_ok=True)
     with open(out, "w") as f:

@@ -19,9 +19,9 @@ timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv 
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $O/pmc_calib_w -o c -- \
     python3 $R/tools/pmc_calib.py >> $O/pmc_calib.log 2>&1 || exit 15
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o p -- \
-    python3 $R/bench.py --no-extras --no-cpu-baseline --no-density --no-fp32-mfma-leg --steps 6 --warmup 1 \
+    python3 $R/bench.py --no-extras --no-cpu-baseline --no-density --no-fp32-mfma-leg --ramp 0 --steps 6 --warmup 1 \
     > $O/pmc_fetch.json 2> $O/pmc_fetch.err || exit 16
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o p -- \
-    python3 $R/bench.py --no-extras --no-cpu-baseline --no-density --no-fp32-mfma-leg --steps 6 --warmup 1 \
+    python3 $R/bench.py --no-extras --no-cpu-baseline --no-density --no-fp32-mfma-leg --ramp 0 --steps 6 --warmup 1 \
     > $O/pmc_write.json 2> $O/pmc_write.err || exit 17
 exit 0

@@ -155,6 +155,45 @@ def tier_r_leg(dev, rank, world, frames=32, n=65536, workers=4, steps=3, cpu=Tru
     return rec
 
 
+def voxel_leg(dev, rank, world, B=32, n=65536, voxel=0.05, steps=20, cpu=True):
+    """voxel downsampling of the SA batch (B x n uniform frames, device-resident)
+    on the chip-wide path (lidar_voxel_downsample_batch_f32).  Roofline: algorithmic bytes per
+    launch (12 B per point in + 4 B voxel id out + 16 B per voxel out) over 8 TB/s."""
+    import torch
+    from lidar_ai_recommendation_software_amd import pointnet2 as pn
+    from lidar_ai_recommendation_software_amd.synthetic import unit_frames
+    from lidar_ai_recommendation_software_amd import sharding
+    x = torch.from_numpy(unit_frames(B, n, seed=sharding.frame_seed(rank, base=77))).to(dev)
+    out = pn.voxel_downsample_batch(x, voxel)
+    torch.cuda.synchronize(dev)
+    el = sharding.timed(lambda: [pn.voxel_downsample_batch(x, voxel) for _ in range(steps)], dev, world)
+    nv = int(out[3].sum().item())
+    per_launch = el / steps
+    algo = B * n * 16 + nv * 16
+    rec = {"metric": "M points/s through voxel_downsample (batched, device-resident frames)",
+           "value": sharding.aggregate_rate(B * n * steps, world, el) / 1e6, "unit": "M points/s",
+           "ms_per_launch": per_launch * 1e3, "frames": B, "points_per_frame": n, "voxel": voxel,
+           "voxels_per_frame": nv / B, "parity": "bit-exact vs oracle/tier_n.voxel_downsample "
+           "(tests/test_gpu_tier_r.py::test_voxel_downsample_batch_vs_oracle)",
+           "roofline": {"kernel": "voxel_downsample_batch (11 launches)", "bound": "hbm",
+                        "achieved": algo / per_launch / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": algo / per_launch / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                        "work_per_launch": algo, "avg_launch_ms": per_launch * 1e3,
+                        "peak_basis": "HBM peak; algorithmic bytes (the radix sort moves ~5x more)"},
+           "cpu_baseline": None}
+    if cpu and rank == 0 and world == 1:
+        from oracle import tier_n
+        xs = x[:2].cpu().numpy()
+        t0 = time.perf_counter()
+        for f in xs:
+            tier_n.voxel_downsample(f, voxel)
+        dt = time.perf_counter() - t0
+        rec["cpu_baseline"] = {"value": len(xs) * n / dt / 1e6, "unit": "M points/s", "cores": 1, "kind": "port",
+                               "sample": f"{len(xs)} x {n}-point frame(s) through oracle/tier_n.voxel_downsample "
+                                         f"(C keys + numpy unique + the sequential sums) in {dt:.1f} s"}
+    return rec
+
+
 def variant_leg(rank, world, frames=8, n=65536, cpu=True, cpu_budget=6.0):
     """the Streamlit apps' own pipeline (app_simplified.py:76-137 ->
     :234-316, DBSCAN eps 0.3 on unscaled points + KDTree r = 2 cell counts) through the
@@ -304,6 +343,7 @@ def main():
 
     density = None if args.no_density else tier_r_leg(dev, rank, world, cpu=not args.no_cpu_baseline, cpu_budget=args.cpu_budget)
     variant = None if args.no_density else variant_leg(rank, world, cpu=not args.no_cpu_baseline)
+    voxel = None if args.no_density else voxel_leg(dev, rank, world, cpu=not args.no_cpu_baseline)
     work = ssg_kernel_work(N)
     traffic = pmc_traffic(B, N)
     # Two chains per group of batches: the side streams' SA1 FPS + ball queries (`depth`
@@ -370,6 +410,7 @@ def main():
             "other_configs": extras,
             "density_path": density,
             "variant_path": variant,
+            "voxel_downsample": voxel,
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu_baseline:

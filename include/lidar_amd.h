@@ -269,6 +269,16 @@ int lidar_voxel_downsample_f32(lidar_handle *h, const float *xyz, int64_t n, flo
                                int32_t *voxel_id, float *centroids, int32_t *counts,
                                int64_t *nvox_host, void *stream);
 
+/* Voxel downsampling of `batch` frames of n points over the whole chip (csrc/voxel_batch.hip):
+ * xyz (batch, n, 3) fp32; voxel_id (batch, n) int32; centroids (batch, n, 3) and counts (batch, n),
+ * the first nvox[f] rows of frame f valid; nvox (batch,) int32 on the device (-1: the frame's grid
+ * exceeds 2^32 keys).  No host synchronisation; per frame equal to lidar_voxel_downsample_f32.
+ * Workspace: lidar_voxel_batch_workspace_bytes(batch, n) (for lidar_reserve). */
+uint64_t lidar_voxel_batch_workspace_bytes(int64_t batch, int64_t n);
+int lidar_voxel_downsample_batch_f32(lidar_handle *h, const float *xyz, int64_t batch, int64_t n, float voxel,
+                                     int32_t *voxel_id, float *centroids, int32_t *counts, int32_t *nvox,
+                                     void *stream);
+
 /* ======================================================= Tier R (density path)
  * Bit-exact replacements for the reference's CPU path. */
 

@@ -83,6 +83,8 @@ SIGNATURES = {
                                    I64, I64, P],
     "lidar_concat_xyz_pad_f32": [P, P, I64, P, I64, I64, P],
     "lidar_voxel_downsample_f32": [P, P, I64, F32, P, P, P, P, P],
+    "lidar_voxel_batch_workspace_bytes": [I64, I64],
+    "lidar_voxel_downsample_batch_f32": [P, P, I64, I64, F32, P, P, P, P, P],
     "lidar_dbscan_f64": [P, P, I64, F64, I32, P, P, P],
     "lidar_radius_count_f64": [P, P, I64, F64, P, P],
     "lidar_histogram2d_f64": [P, P, P, I64, P, I64, P, I64, P, P],
@@ -105,7 +107,7 @@ _RESTYPES = {"lidar_last_error": ctypes.c_char_p, "lidar_mlp_packed_size": I64,
              "lidar_mlp_packed_size16": I64, "lidar_mlp_packed_size_x3": I64,
              "lidar_ball_query_grid_bytes": ctypes.c_uint64,
              "lidar_dense_x3_packed_size": I64, "lidar_mlp_packed_size_x1": I64,
-             "lidar_fps_workspace_bytes": ctypes.c_uint64}
+             "lidar_fps_workspace_bytes": ctypes.c_uint64, "lidar_voxel_batch_workspace_bytes": ctypes.c_uint64}
 
 
 def load_library(path=LIB_PATH):

@@ -1,0 +1,397 @@
+// voxel_batch.hip — voxel downsampling of a batch of frames over the whole chip.
+//
+// Same spec as voxel.hip: v = floor((p - min p) / voxel) per axis in fp32, key =
+// (vx*Dy + vy)*Dz + vz with D = max v + 1, voxels in ascending key order, voxel id = rank of the
+// key, centroid = sequential fp32 sum of the voxel's points in point order / count.  voxel.hip
+// runs one frame in one workgroup; here every pass is spread over (tiles x frames) workgroups:
+//
+//   bbox (min, max) -> keys (u32) + indices              grid (chunks, frames), atomics per frame
+//   LSD radix sort, 8-bit digits, only the passes a frame's key range needs (per-frame parity):
+//     hist    per 4096-element tile, LDS histogram   -> hist[frame][digit][tile]
+//     scan    per frame, digit-major tile-minor        (exclusive: the tile's base per digit)
+//     scatter per tile, stable: 1024-element sub-tiles ranked by wave ballots (8 per digit) and
+//             per-wave prefix counts in LDS, running per-digit offsets
+//   runs      per tile: run starts counted, then written from the frame's earlier tiles' counts
+//             -> voxel id per point, run offsets, voxel count
+//   centroid  one thread per voxel walks its run (index order: the sort is stable)
+//
+// Memory-side bytes per point: xyz read 3x (36 B: bbox, keys, centroids) + keys/indices (8 B written) + per radix pass
+// 24 B (two reads, one write of 8 B) + runs 12 B + centroid gathers 12 B; the algorithmic floor is
+// 12 B in + 4 B voxel id out (+16 B per voxel).  No host synchronisation: nvox[f] lands on the
+// device (-1: the frame's grid exceeds 2^32 keys).
+#include <algorithm>
+
+#include "common.hpp"
+
+namespace {
+
+constexpr int VT = 256;      // threads of the streaming kernels
+constexpr int TILE = 4096;   // radix tile (elements per scatter workgroup)
+constexpr int ST = 1024;     // scatter / runs workgroup threads
+constexpr int SW = ST / 64;  // waves per scatter workgroup
+
+// per-frame meta words: [0..2] / [3..5] monotone bits of the min / max point, [6] key bits, [7] overflow,
+// [8] voxel count
+constexpr int MW = 16;
+
+__device__ __forceinline__ uint32_t ord(float f)  // monotone float -> u32
+{
+    const uint32_t u = __float_as_uint(f);
+    return u ^ ((uint32_t)((int32_t)u >> 31) | 0x80000000u);
+}
+__device__ __forceinline__ float unord(uint32_t u)
+{
+    return __uint_as_float(u ^ (((u >> 31) - 1u) | 0x80000000u));
+}
+
+__global__ void vb_init_kernel(uint32_t *meta, int batch)
+{
+    const int f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= batch) return;
+    uint32_t *m = meta + (int64_t)f * MW;
+    for (int a = 0; a < 3; ++a) {
+        m[a] = 0xffffffffu;  // >= ord(any float)
+        m[3 + a] = 0u;        // <= ord(any float)
+    }
+    m[6] = m[7] = m[8] = 0u;
+}
+
+// per-frame bbox in one pass: min and max as monotone bit patterns (atomics per wave)
+__global__ __launch_bounds__(VT) void vb_bbox_kernel(const float *__restrict__ xyz, int64_t n, uint32_t *meta)
+{
+    const int f = blockIdx.y;
+    const float *p = xyz + (int64_t)f * n * 3;
+    uint32_t lo[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, hi[3] = {0u, 0u, 0u};
+    for (int64_t i = (int64_t)blockIdx.x * VT + threadIdx.x; i < n; i += (int64_t)gridDim.x * VT)
+        for (int a = 0; a < 3; ++a) {
+            const uint32_t o = ord(p[3 * i + a]);
+            lo[a] = min(lo[a], o);
+            hi[a] = max(hi[a], o);
+        }
+    for (int a = 0; a < 3; ++a) {
+        uint32_t v = lo[a], w = hi[a];
+        for (int m = 32; m >= 1; m >>= 1) {
+            v = min(v, (uint32_t)__shfl_xor((int)v, m, 64));
+            w = max(w, (uint32_t)__shfl_xor((int)w, m, 64));
+        }
+        if ((threadIdx.x & 63) == 0) {
+            atomicMin(meta + (int64_t)f * MW + a, v);
+            atomicMax(meta + (int64_t)f * MW + 3 + a, w);
+        }
+    }
+}
+
+__device__ __forceinline__ int cell(float x, float lo, float voxel)
+{
+    return (int)floorf(__fdiv_rn(__fsub_rn(x, lo), voxel));
+}
+
+__global__ __launch_bounds__(VT) void vb_keys_kernel(const float *__restrict__ xyz, int64_t n, float voxel,
+                                                     uint32_t *meta, uint32_t *__restrict__ key,
+                                                     uint32_t *__restrict__ idx)
+{
+    const int f = blockIdx.y;
+    const float *p = xyz + (int64_t)f * n * 3;
+    uint32_t *m = meta + (int64_t)f * MW;
+    const float lo[3] = {unord(m[0]), unord(m[1]), unord(m[2])};
+    // the largest cell per axis is the max point's: p -> floor((p - lo) / voxel) is monotone in
+    // fp32 (each correctly rounded op is), so max_i cell(p_i) == cell(max_i p_i)
+    const uint64_t d0 = (uint64_t)cell(unord(m[3]), lo[0], voxel) + 1;
+    const uint64_t d1 = (uint64_t)cell(unord(m[4]), lo[1], voxel) + 1, d2 = (uint64_t)cell(unord(m[5]), lo[2], voxel) + 1;
+    const uint64_t tot = d0 * d1 * d2;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        m[7] = tot > 0x100000000ull ? 1u : 0u;
+        const uint64_t top = tot - 1;
+        m[6] = top == 0 ? 0u : (uint32_t)(64 - __clzll((long long)top));  // bits of the largest key
+    }
+    uint32_t *k = key + (int64_t)f * n;
+    uint32_t *v = idx + (int64_t)f * n;
+    for (int64_t i = (int64_t)blockIdx.x * VT + threadIdx.x; i < n; i += (int64_t)gridDim.x * VT) {
+        const uint32_t c0 = (uint32_t)cell(p[3 * i], lo[0], voxel), c1 = (uint32_t)cell(p[3 * i + 1], lo[1], voxel),
+                       c2 = (uint32_t)cell(p[3 * i + 2], lo[2], voxel);
+        k[i] = (uint32_t)(((uint64_t)c0 * d1 + c1) * d2 + c2);
+        v[i] = (uint32_t)i;
+    }
+}
+
+// key bits of frame f, read after vb_keys_kernel (0 when the grid overflowed: nothing is sorted,
+// the runs kernel reports -1)
+__device__ __forceinline__ int frame_bits(const uint32_t *meta, int f)
+{
+    const uint32_t *m = meta + (int64_t)f * MW;
+    return m[7] ? 0 : (int)m[6];
+}
+
+__global__ __launch_bounds__(VT) void vb_hist_kernel(const uint32_t *__restrict__ kin, int64_t n, int shift,
+                                                     int ntiles, const uint32_t *meta, uint32_t *__restrict__ hist)
+{
+    const int f = blockIdx.y, t = blockIdx.x;
+    if (frame_bits(meta, f) <= shift) return;  // this frame needs no pass at this digit
+    __shared__ uint32_t h[256];
+    for (int d = threadIdx.x; d < 256; d += VT) h[d] = 0;
+    __syncthreads();
+    const uint32_t *k = kin + (int64_t)f * n;
+    const int64_t i0 = (int64_t)t * TILE, i1 = min<int64_t>(n, i0 + TILE);
+    for (int64_t i = i0 + threadIdx.x; i < i1; i += VT) atomicAdd(&h[(k[i] >> shift) & 255u], 1u);
+    __syncthreads();
+    uint32_t *hf = hist + (int64_t)f * 256 * ntiles;
+    for (int d = threadIdx.x; d < 256; d += VT) hf[(int64_t)d * ntiles + t] = h[d];
+}
+
+// per frame: exclusive scan of hist[f] in (digit, tile) order
+__global__ __launch_bounds__(ST) void vb_scan_kernel(uint32_t *__restrict__ hist, int ntiles, int shift,
+                                                     const uint32_t *meta)
+{
+    const int f = blockIdx.x;
+    if (frame_bits(meta, f) <= shift) return;
+    __shared__ uint32_t wsum[SW];
+    __shared__ uint32_t carry;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t *hf = hist + (int64_t)f * 256 * ntiles;
+    const int64_t total = (int64_t)256 * ntiles;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    for (int64_t b0 = 0; b0 < total; b0 += ST) {
+        const int64_t i = b0 + threadIdx.x;
+        const uint32_t v = i < total ? hf[i] : 0u;
+        uint32_t inc = v;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t u = (uint32_t)__shfl_up((int)inc, o, 64);
+            if (lane >= o) inc += u;
+        }
+        if (lane == 63) wsum[wave] = inc;
+        __syncthreads();
+        uint32_t pre = carry, tot = 0;
+        for (int w = 0; w < SW; ++w) {
+            pre += w < wave ? wsum[w] : 0u;
+            tot += wsum[w];
+        }
+        if (i < total) hf[i] = pre + inc - v;
+        __syncthreads();
+        if (threadIdx.x == 0) carry += tot;
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(ST) void vb_scatter_kernel(const uint32_t *__restrict__ kin, const uint32_t *__restrict__ vin,
+                                                        uint32_t *__restrict__ kout, uint32_t *__restrict__ vout,
+                                                        int64_t n, int shift, int ntiles, const uint32_t *meta,
+                                                        const uint32_t *__restrict__ hist)
+{
+    const int f = blockIdx.y, t = blockIdx.x;
+    if (frame_bits(meta, f) <= shift) return;
+    __shared__ uint32_t off[256];      // running global offset per digit
+    __shared__ uint32_t wcnt[SW][256]; // per-wave digit counts of the current sub-tile
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t *hf = hist + (int64_t)f * 256 * ntiles;
+    for (int d = tid; d < 256; d += ST) off[d] = hf[(int64_t)d * ntiles + t];
+    const uint32_t *k = kin + (int64_t)f * n;
+    const uint32_t *v = vin + (int64_t)f * n;
+    uint32_t *ko = kout + (int64_t)f * n;
+    uint32_t *vo = vout + (int64_t)f * n;
+    const uint64_t below = (1ull << lane) - 1;
+    const int64_t i0 = (int64_t)t * TILE, i1 = min<int64_t>(n, i0 + TILE);
+    for (int64_t b0 = i0; b0 < i1; b0 += ST) {
+        const int64_t i = b0 + tid;
+        const bool valid = i < i1;
+        const uint32_t kk = valid ? k[i] : 0u, vv = valid ? v[i] : 0u;
+        const uint32_t dig = (kk >> shift) & 255u;
+        uint64_t same = __ballot(valid);
+#pragma unroll
+        for (int bit = 0; bit < 8; ++bit) {
+            const uint64_t bm = __ballot((dig >> bit) & 1u);
+            same &= ((dig >> bit) & 1u) ? bm : ~bm;
+        }
+        for (int d = lane; d < 256; d += 64) wcnt[wave][d] = 0;
+        __syncthreads();  // (also: off[] initialised / advanced)
+        if (valid && (same & below) == 0) wcnt[wave][dig] = (uint32_t)__popcll(same);
+        __syncthreads();
+        if (valid) {
+            uint32_t o = off[dig] + (uint32_t)__popcll(same & below);
+            for (int w = 0; w < wave; ++w) o += wcnt[w][dig];
+            ko[o] = kk;
+            vo[o] = vv;
+        }
+        __syncthreads();
+        for (int d = tid; d < 256; d += ST) {
+            uint32_t s = 0;
+            for (int w = 0; w < SW; ++w) s += wcnt[w][d];
+            off[d] += s;
+        }
+        __syncthreads();  // wcnt is reset by the next sub-tile
+    }
+}
+
+// run starts of the sorted keys, per 4096-element tile (chip-wide): count, then write with the
+// tile's base from the counts of the frame's earlier tiles (<= n / 4096 loads)
+__device__ __forceinline__ void sorted_bufs(const uint32_t *m, int f, int64_t n, const uint32_t *k0,
+                                            const uint32_t *v0, const uint32_t *k1, const uint32_t *v1,
+                                            const uint32_t *&sk, const uint32_t *&si)
+{
+    const int passes = ((int)m[6] + 7) / 8;  // the sorted data sits in buffer (passes run) % 2
+    sk = (passes & 1 ? k1 : k0) + (int64_t)f * n;
+    si = (passes & 1 ? v1 : v0) + (int64_t)f * n;
+}
+
+__global__ __launch_bounds__(ST) void vb_runs_count_kernel(const uint32_t *__restrict__ k0, const uint32_t *__restrict__ v0,
+                                                           const uint32_t *__restrict__ k1, const uint32_t *__restrict__ v1,
+                                                           int64_t n, int ntiles, const uint32_t *meta,
+                                                           uint32_t *__restrict__ tilecnt)
+{
+    const int f = blockIdx.y, t = blockIdx.x;
+    const uint32_t *m = meta + (int64_t)f * MW;
+    if (m[7]) return;
+    const uint32_t *sk, *si;
+    sorted_bufs(m, f, n, k0, v0, k1, v1, sk, si);
+    __shared__ uint32_t ws[SW];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t i0 = (int64_t)t * TILE, i1 = min<int64_t>(n, i0 + TILE);
+    uint32_t c = 0;
+    for (int64_t i = i0 + tid; i < i1; i += ST) c += (i == 0 || sk[i] != sk[i - 1]) ? 1u : 0u;
+    for (int o = 32; o >= 1; o >>= 1) c += (uint32_t)__shfl_xor((int)c, o, 64);
+    if (lane == 0) ws[wave] = c;
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t tot = 0;
+        for (int w = 0; w < SW; ++w) tot += ws[w];
+        tilecnt[(int64_t)f * ntiles + t] = tot;
+    }
+}
+
+__global__ __launch_bounds__(ST) void vb_runs_write_kernel(const uint32_t *__restrict__ k0, const uint32_t *__restrict__ v0,
+                                                           const uint32_t *__restrict__ k1, const uint32_t *__restrict__ v1,
+                                                           int64_t n, int ntiles, uint32_t *meta,
+                                                           const uint32_t *__restrict__ tilecnt,
+                                                           int32_t *__restrict__ vid, uint32_t *__restrict__ vstart,
+                                                           int32_t *__restrict__ nvox)
+{
+    const int f = blockIdx.y, t = blockIdx.x;
+    uint32_t *m = meta + (int64_t)f * MW;
+    if (m[7]) {
+        if (t == 0 && threadIdx.x == 0) nvox[f] = -1;
+        return;
+    }
+    const uint32_t *sk, *si;
+    sorted_bufs(m, f, n, k0, v0, k1, v1, sk, si);
+    int32_t *vf = vid + (int64_t)f * n;
+    uint32_t *vs = vstart + (int64_t)f * (n + 1);
+    __shared__ uint32_t ws[SW];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    uint32_t base = 0;
+    for (int u = 0; u < t; ++u) base += tilecnt[(int64_t)f * ntiles + u];
+    const int64_t i0 = (int64_t)t * TILE, i1 = min<int64_t>(n, i0 + TILE);
+    for (int64_t b0 = i0; b0 < i1; b0 += ST) {
+        const int64_t i = b0 + tid;
+        const bool st = i < i1 && (i == 0 || sk[i] != sk[i - 1]);
+        const uint64_t mk = __ballot(st);
+        const uint32_t inw = (uint32_t)__popcll(mk & ((1ull << lane) - 1));
+        if (lane == 0) ws[wave] = (uint32_t)__popcll(mk);
+        __syncthreads();
+        uint32_t pre = 0, tot = 0;
+        for (int w = 0; w < SW; ++w) {
+            pre += w < wave ? ws[w] : 0u;
+            tot += ws[w];
+        }
+        if (i < i1) {
+            const uint32_t r = base + pre + inw + (st ? 1u : 0u) - 1u;  // my voxel's rank
+            vf[si[i]] = (int32_t)r;
+            if (st) vs[r] = (uint32_t)i;
+        }
+        base += tot;
+        __syncthreads();
+    }
+    if (t == ntiles - 1 && tid == 0) {
+        vs[base] = (uint32_t)n;
+        m[8] = base;
+        nvox[f] = (int32_t)base;
+    }
+}
+
+__global__ __launch_bounds__(VT) void vb_centroid_kernel(const float *__restrict__ xyz, int64_t n,
+                                                         const uint32_t *__restrict__ v0, const uint32_t *__restrict__ v1,
+                                                         const uint32_t *meta, const uint32_t *__restrict__ vstart,
+                                                         float *__restrict__ cent, int32_t *__restrict__ counts)
+{
+    const int f = blockIdx.y;
+    const uint32_t *m = meta + (int64_t)f * MW;
+    if (m[7]) return;
+    const int passes = ((int)m[6] + 7) / 8;  // the sorted indices sit in buffer (passes run) % 2
+    const uint32_t *si = (passes & 1 ? v1 : v0) + (int64_t)f * n;
+    const uint32_t *vs = vstart + (int64_t)f * (n + 1);
+    const float *p = xyz + (int64_t)f * n * 3;
+    const uint32_t V = m[8];
+    for (uint32_t v = blockIdx.x * VT + threadIdx.x; v < V; v += gridDim.x * VT) {
+        const uint32_t a = vs[v], b = vs[v + 1];
+        float s[3] = {0.f, 0.f, 0.f};
+        for (uint32_t t = a; t < b; ++t) {
+            const uint32_t i = si[t];
+            for (int c = 0; c < 3; ++c) s[c] = __fadd_rn(s[c], p[3 * i + c]);
+        }
+        const float cnt = (float)(b - a);
+        float *o = cent + ((int64_t)f * n + v) * 3;
+        for (int c = 0; c < 3; ++c) o[c] = __fdiv_rn(s[c], cnt);
+        counts[(int64_t)f * n + v] = (int32_t)(b - a);
+    }
+}
+
+}  // namespace
+
+// workspace bytes of lidar_voxel_downsample_batch_f32 for (batch, n)
+LIDAR_EXPORT uint64_t lidar_voxel_batch_workspace_bytes(int64_t batch, int64_t n)
+{
+    const int64_t ntiles = (n + TILE - 1) / TILE;
+    return (uint64_t)batch * ((uint64_t)n * 16 + (uint64_t)(n + 1) * 4 + (uint64_t)257 * ntiles * 4 + MW * 4) + 2048;
+}
+
+// Voxel downsampling of `batch` frames of n points (xyz (batch, n, 3) fp32), all on the device:
+// voxel_id (batch, n) int32, centroids (batch, n, 3) and counts (batch, n) with the first nvox[f]
+// rows of frame f valid, nvox (batch,) int32 (-1: the frame's voxel grid exceeds 2^32 keys).
+// Same results as lidar_voxel_downsample_f32 per frame.
+LIDAR_EXPORT int lidar_voxel_downsample_batch_f32(lidar_handle *h, const float *xyz, int64_t batch, int64_t n,
+                                                  float voxel, int32_t *voxel_id, float *centroids, int32_t *counts,
+                                                  int32_t *nvox, void *stream)
+{
+    REQUIRE(h && xyz && voxel_id && centroids && counts && nvox, "lidar_voxel_downsample_batch_f32: null pointer");
+    REQUIRE(batch >= 0 && batch <= 65535 && n >= 1 && n < 0x7fffffff,
+            "lidar_voxel_downsample_batch_f32: batch in [0, 65535], n >= 1");
+    REQUIRE(voxel > 0.0f, "lidar_voxel_downsample_batch_f32: voxel size must be > 0");
+    if (batch == 0) return LIDAR_OK;
+    HIP_TRY(hipSetDevice(h->device));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int ntiles = (int)((n + TILE - 1) / TILE);
+    lidar::Carver cv;
+    const uint64_t ok0 = cv.take<uint32_t>(batch * n), ov0 = cv.take<uint32_t>(batch * n);
+    const uint64_t ok1 = cv.take<uint32_t>(batch * n), ov1 = cv.take<uint32_t>(batch * n);
+    const uint64_t ost = cv.take<uint32_t>(batch * (n + 1));
+    const uint64_t oh = cv.take<uint32_t>(batch * 256 * (int64_t)ntiles);
+    const uint64_t om = cv.take<uint32_t>(batch * MW);
+    const uint64_t otc = cv.take<uint32_t>(batch * (int64_t)ntiles);
+    char *base = static_cast<char *>(lidar::workspace(h, cv.off));
+    if (!base) return LIDAR_ENOMEM;
+    auto U = [&](uint64_t o) { return reinterpret_cast<uint32_t *>(base + o); };
+    uint32_t *meta = U(om), *hist = U(oh);
+    const unsigned chunks = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + VT * 8 - 1) / (VT * 8), 256));
+    const dim3 sg(chunks, (unsigned)batch);
+    hipLaunchKernelGGL(vb_init_kernel, dim3((unsigned)((batch + 255) / 256)), dim3(256), 0, s, meta, (int)batch);
+    hipLaunchKernelGGL(vb_bbox_kernel, sg, dim3(VT), 0, s, xyz, n, meta);
+    hipLaunchKernelGGL(vb_keys_kernel, sg, dim3(VT), 0, s, xyz, n, voxel, meta, U(ok0), U(ov0));
+    uint32_t *kin = U(ok0), *vin = U(ov0), *kout = U(ok1), *vout = U(ov1);
+    const dim3 tg((unsigned)ntiles, (unsigned)batch);
+    for (int shift = 0; shift < 32; shift += 8) {  // frames past their key bits skip (per-frame parity)
+        hipLaunchKernelGGL(vb_hist_kernel, tg, dim3(VT), 0, s, kin, n, shift, ntiles, meta, hist);
+        hipLaunchKernelGGL(vb_scan_kernel, dim3((unsigned)batch), dim3(ST), 0, s, hist, ntiles, shift, meta);
+        hipLaunchKernelGGL(vb_scatter_kernel, tg, dim3(ST), 0, s, kin, vin, kout, vout, n, shift, ntiles, meta, hist);
+        std::swap(kin, kout);
+        std::swap(vin, vout);
+    }
+    hipLaunchKernelGGL(vb_runs_count_kernel, tg, dim3(ST), 0, s, U(ok0), U(ov0), U(ok1), U(ov1), n, ntiles, meta,
+                       U(otc));
+    hipLaunchKernelGGL(vb_runs_write_kernel, tg, dim3(ST), 0, s, U(ok0), U(ov0), U(ok1), U(ov1), n, ntiles, meta,
+                       U(otc), voxel_id, U(ost), nvox);
+    // one thread per (possible) voxel: the gathers of a voxel's points are a dependent chain
+    const dim3 cg((unsigned)((n + VT - 1) / VT), (unsigned)batch);
+    hipLaunchKernelGGL(vb_centroid_kernel, cg, dim3(VT), 0, s, xyz, n, U(ov0), U(ov1), meta, U(ost), centroids,
+                       counts);
+    LAUNCH_CHECK();
+    return LIDAR_OK;
+}

@@ -111,6 +111,27 @@ def farthest_point_sample(xyz, npoint, return_xyz=False, first_zero=None, prefix
     return (idx, new_xyz) if return_xyz else idx
 
 
+def voxel_downsample_batch(xyz, voxel, slot=0):
+    """Voxel downsampling of (B, N, 3) float32 CUDA frames on the whole chip
+    (lidar_voxel_downsample_batch_f32; per frame equal to data_processing.voxel_downsample).
+    Returns device tensors (centroids (B, N, 3), voxel_id (B, N) int32, counts (B, N) int32,
+    nvox (B,) int32): the first nvox[f] centroid / count rows of frame f are valid; nvox -1 marks
+    a frame whose voxel grid exceeds 2^32 keys."""
+    _dev_check(xyz)
+    if xyz.dtype != torch.float32 or xyz.dim() != 3 or xyz.shape[2] != 3:
+        raise ValueError("xyz must be (B, N, 3) float32")
+    B, N, _ = xyz.shape
+    dev = xyz.device
+    cent = torch.empty((B, N, 3), dtype=torch.float32, device=dev)
+    vid = torch.empty((B, N), dtype=torch.int32, device=dev)
+    cnt = torch.empty((B, N), dtype=torch.int32, device=dev)
+    nvox = torch.empty(B, dtype=torch.int32, device=dev)
+    if B and N:
+        nat.call("lidar_voxel_downsample_batch_f32", nat.handle(dev.index, slot), nat.ptr(xyz), B, N,
+                 float(voxel), nat.ptr(vid), nat.ptr(cent), nat.ptr(cnt), nat.ptr(nvox), nat.stream_ptr())
+    return cent, vid, cnt, nvox
+
+
 BQ_MODES = {"auto": 0, "scan": 1, "grid": 2}
 BQ_GRID_MIN_N = 1024  # csrc/ball_query.hip kGridMinN: "auto" bins frames of at least this many points
 

@@ -260,3 +260,28 @@ def test_cell_radius_density_boundary(cuda):
     cx, cy = (xg[:-1] + xg[1:]) / 2, (yg[:-1] + yg[1:]) / 2
     d = (cx[None, :, None] - people[None, None, :, 0]) ** 2 + (cy[:, None, None] - people[None, None, :, 1]) ** 2
     assert np.array_equal(out.cpu().numpy(), np.sum(d <= 4.0, axis=2) / 4.0)
+
+
+def test_voxel_downsample_batch_vs_oracle(cuda):
+    """The chip-wide batched voxel path vs the oracle frame by frame: different extents and
+    voxel sizes per key range (0, 1, 2 and 3 radix passes), duplicated points, a one-voxel
+    frame, and a grid past 2^32 keys (nvox -1)."""
+    import torch
+    from lidar_ai_recommendation_software_amd import pointnet2 as pn
+    rng = np.random.default_rng(11)
+    B, N = 6, 5000
+    x = rng.uniform(-1, 1, (B, N, 3)).astype(np.float32)
+    x[1] *= 7.5
+    x[2, N // 2:] = x[2, : N - N // 2]  # duplicates share voxels
+    x[3] = x[3, 0]  # one voxel (no radix pass)
+    x[4, :, 2] = 0.25  # a flat frame
+    for voxel in (0.5, 0.07, 0.013):
+        c, vid, cnt, nv = pn.voxel_downsample_batch(torch.from_numpy(x).to(cuda), voxel)
+        c, vid, cnt, nv = c.cpu().numpy(), vid.cpu().numpy(), cnt.cpu().numpy(), nv.cpu().numpy()
+        for f in range(B):
+            wc, wvid, wcnt = tier_n.voxel_downsample(x[f], voxel)
+            assert nv[f] == len(wcnt), (voxel, f)
+            assert np.array_equal(vid[f], wvid) and np.array_equal(cnt[f, :nv[f]], wcnt)
+            assert np.array_equal(c[f, :nv[f]].view(np.uint32), wc.view(np.uint32)), (voxel, f)
+    _, _, _, nv = pn.voxel_downsample_batch(torch.from_numpy(x[:2]).to(cuda), 1e-6)
+    assert nv.cpu().numpy().tolist() == [-1, -1]

@@ -1,0 +1,17 @@
+"""Voxel batch micro (python tools/voxel_micro.py [B] [voxel]): 20 launches on 32 x 65536 frames."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from lidar_ai_recommendation_software_amd import pointnet2 as pn  # noqa: E402
+from lidar_ai_recommendation_software_amd.synthetic import unit_frames  # noqa: E402
+
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 32
+voxel = float(sys.argv[2]) if len(sys.argv) > 2 else 0.05
+x = torch.from_numpy(unit_frames(B, 65536, 0)).to("cuda:0")
+for _ in range(20):
+    pn.voxel_downsample_batch(x, voxel)
+torch.cuda.synchronize()
+print("ok")

@@ -297,18 +297,21 @@ def voxel_downsample(points, voxel_size):
     """One point per occupied voxel (mean of its points, voxels in ascending key order)
     plus the voxel id of every input point.  Returns (centroids (V, 3) float32,
     voxel_id (N,) int32, counts (V,) int32).  SURVEY §8a N1 (no reference counterpart)."""
-    import ctypes
     import torch
+    from .pointnet2 import voxel_downsample_batch
+    if not voxel_size > 0:
+        raise ValueError("voxel size must be > 0")
     x = _on_device(np.asarray(points, dtype=np.float32).reshape(-1, 3), torch.float32)
     n = len(x)
-    vid = torch.empty(n, dtype=torch.int32, device=x.device)
-    cent = torch.empty((max(n, 1), 3), dtype=torch.float32, device=x.device)
-    cnt = torch.empty(max(n, 1), dtype=torch.int32, device=x.device)
-    v = nat.I64(0)
-    nat.call("lidar_voxel_downsample_f32", _handle(), nat.ptr(x), n, float(voxel_size), nat.ptr(vid),
-             nat.ptr(cent), nat.ptr(cnt), ctypes.byref(v), nat.stream_ptr())
-    v = v.value
-    return cent[:v].cpu().numpy(), vid.cpu().numpy(), cnt[:v].cpu().numpy()
+    if n == 0:
+        return np.zeros((0, 3), np.float32), np.zeros(0, np.int32), np.zeros(0, np.int32)
+    # the chip-wide batched path with one frame (csrc/voxel_batch.hip; same results as the
+    # single-workgroup lidar_voxel_downsample_f32)
+    cent, vid, cnt, nv = voxel_downsample_batch(x[None].contiguous(), float(voxel_size))
+    v = int(nv[0].item())
+    if v < 0:
+        raise ValueError("voxel_downsample: voxel grid exceeds 2^32 keys (voxel too small)")
+    return cent[0, :v].cpu().numpy(), vid[0].cpu().numpy(), cnt[0, :v].cpu().numpy()
 
 
 def farthest_point_sample(points, npoint):

@@ -387,11 +387,12 @@ def main():
             "value": value, "unit": "M points/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "f32" + (" (SA layers 2-3 as split-bf16 x3 MFMA products, fp32 accumulation)" if x3_opt else ""),
-            "precision": ("fp32 inputs/weights/outputs; SA layers 2-3: each fp32 operand split exactly into bf16 "
-                          "hi+lo, products ah*bh + ah*bl + al*bh accumulated in fp32 (<= ~2^-15 per product); "
-                          "features within the 1e-4 rel contract of the fp32 oracle "
-                          "(tests/test_gpu_tier_n.py::test_group_mlp_x3, test_backbone_vs_oracle)") if x3_opt else
+            "dtype": "f32" + (" (MLP products as split-bf16 x3 MFMA products, fp32 accumulation)" if x3_opt else ""),
+            "precision": ("fp32 inputs/weights/outputs; SA layers 2-3, SA2's per-point layer 1 and group_all: each "
+                          "fp32 operand split exactly into bf16 hi+lo, products ah*bh + ah*bl + al*bh accumulated in "
+                          "fp32 (<= ~2^-15 per product); SA1 layer 1 (K = 3) on fp32 MFMA; features within the 1e-4 "
+                          "rel contract of the fp32 oracle (tests/test_gpu_tier_n.py::test_group_mlp_x3, "
+                          "test_dense_x3s, test_backbone_vs_oracle)") if x3_opt else
                          "fp32 MFMA (v_mfma_f32_*_f32)",
             "data": "synthetic: uniform [-1,1]^3 float32 frames (seeded per rank), random-init SSG weights",
             "config": {"workload": "PointNet++ SSG encoder (SA1 N/16 r0.2 ns32 [64,64,128]; "

@@ -118,6 +118,20 @@ def test_ball_query_grid_edge_frames(cuda, name, r, ns):
         assert np.array_equal(got, want), f"{mode}: {(got != want).sum()} differ"
 
 
+@pytest.mark.parametrize("name", ["uniform"] + list(_bq_edge_frames()))
+def test_ball_query_split_binning(cuda, monkeypatch, name):
+    """LIDAR_BQ_BIN_SPLIT=1: the grid built by the five low-LDS kernels (global atomics,
+    slot order differs from the one-workgroup binning) gives the oracle's indices exactly."""
+    monkeypatch.setenv("LIDAR_BQ_BIN_SPLIT", "1")
+    x = unit_frames(3, 20000, 8) if name == "uniform" else _bq_edge_frames()[name][None]
+    c = np.ascontiguousarray(np.concatenate([x[:, :600:3], x[:, :40] + np.float32(7.5)], 1))
+    xt, ct = torch.from_numpy(x).to(cuda), torch.from_numpy(c).to(cuda)
+    for r, ns in [(0.1, 32), (0.0, 8), (0.3, 128)]:
+        got = pn.ball_query(r, ns, xt, ct, mode="grid").cpu().numpy()
+        want = tier_n.ball_query(x, c, r, ns)
+        assert np.array_equal(got, want), f"r={r}: {(got != want).sum()} differ"
+
+
 def test_ball_query_binned_reuse(cuda):
     """one binning (lidar_ball_query_bin_f32) serves queries at smaller, equal and larger
     radii and other nsample values, exactly."""

@@ -811,8 +811,39 @@ __device__ __forceinline__ void for_neighbours(const Grid &g, const uint32_t *st
     }
 }
 
+// eps-neighbour count of a point, stopping once it reaches `limit`: DBSCAN only asks whether
+// cnt >= min_samples, and a standardized dense frame (eps 0.5 on unit-variance data) has hundreds
+// of neighbours per point among thousands of candidates
+__device__ __forceinline__ int32_t count_neighbours(const Grid &g, const uint32_t *start, const double *sxyz,
+                                                    double px, double py, double pz, uint32_t c, int32_t limit)
+{
+    const int64_t cz = c % g.dim[2], cy = (c / g.dim[2]) % g.dim[1], cx = c / (g.dim[2] * g.dim[1]);
+    const int64_t z0 = cz > 0 ? cz - 1 : 0, z1 = cz + 1 < g.dim[2] ? cz + 1 : g.dim[2] - 1;
+    int32_t k = 0;
+    // the point's own (X, Y) column first: the likeliest place to find `limit` hits
+    for (int r = 0; r < 9; ++r) {
+        // r = 0 -> (0, 0); r = 1..8 -> the other eight (dX, dY) in row-major order
+        int dx = 0, dy = 0;
+        if (r > 0) {
+            const int q = r <= 4 ? r - 1 : r;  // skip the centre slot 4 of the 3x3 row-major order
+            dx = q / 3 - 1;
+            dy = q % 3 - 1;
+        }
+        const int64_t X = cx + dx, Y = cy + dy;
+        if (X < 0 || X >= g.dim[0] || Y < 0 || Y >= g.dim[1]) continue;
+        const int64_t cc0 = (X * g.dim[1] + Y) * g.dim[2] + z0, cc1 = (X * g.dim[1] + Y) * g.dim[2] + z1;
+        const uint32_t u0 = start[cc0], u1 = start[cc1 + 1];
+        for (uint32_t u = u0; u < u1; ++u) {
+            const double d = lidar::dist2d(px, py, pz, sxyz[3 * u], sxyz[3 * u + 1], sxyz[3 * u + 2]);
+            if (d <= g.eps2 && ++k >= limit) return k;
+        }
+    }
+    return k;
+}
+
 __global__ void dbscan_count_kernel(const double *P_in, const uint32_t *cid_in, const uint32_t *start_in,
-                                    const uint32_t *order_in, const double *sxyz_in, int32_t *cnt_in, FrameMap fm)
+                                    const uint32_t *order_in, const double *sxyz_in, int32_t *cnt_in,
+                                    int32_t limit, FrameMap fm)
 {
     const double *P = fm.ws(P_in), *sxyz = fm.ws(sxyz_in);
     const uint32_t *cid = fm.ws(cid_in), *start = fm.ws(start_in), *order = fm.ws(order_in);
@@ -822,10 +853,7 @@ __global__ void dbscan_count_kernel(const double *P_in, const uint32_t *cid_in, 
     g.load(P);
     for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < g.n; t += (int64_t)gridDim.x * blockDim.x) {
         const uint32_t i = order[t];
-        int32_t k = 0;
-        for_neighbours(g, start, sxyz, sxyz[3 * t], sxyz[3 * t + 1], sxyz[3 * t + 2], cid[i],
-                       [&](uint32_t) { ++k; });
-        cnt[i] = k;
+        cnt[i] = count_neighbours(g, start, sxyz, sxyz[3 * t], sxyz[3 * t + 1], sxyz[3 * t + 2], cid[i], limit);
     }
 }
 
@@ -901,6 +929,7 @@ __global__ void dbscan_union_kernel(const double *P_in, const uint32_t *cid_in, 
         for_neighbours(g, start, sxyz, sxyz[3 * t], sxyz[3 * t + 1], sxyz[3 * t + 2], cid[i], [&](uint32_t u) {
             const int32_t j = (int32_t)order[u];
             if (j < i && cnt[j] >= min_samples) {
+                if (ld(parent + j) == ri) return;  // already hooked straight under i's root
                 const int32_t rj = uf_find(parent, j);
                 if (rj != ri) ri = uf_unite(parent, ri, rj);
             }
@@ -1299,9 +1328,12 @@ unsigned point_blocks(int64_t nmax, int frames)
 }
 
 // the DBSCAN pipeline on x (P[P_N] points, eps P[P_EPS], bbox in P) -> labels, for every frame
+// exact_counts: cnt[i] is the full eps-neighbour count (radius counts, the standalone API's
+// counts output); otherwise counting stops at min_samples
 int run_dbscan(const double *x, int64_t nmax, int32_t min_samples, DbscanWs &w, int64_t *labels, hipStream_t s,
-               FrameMap fm, int frames, bool count_only = false)
+               FrameMap fm, int frames, bool count_only = false, bool exact_counts = false)
 {
+    const int32_t limit = (count_only || exact_counts) ? 0x7fffffff : min_samples;
     const unsigned gp = point_blocks(nmax, frames);
     const unsigned gc = point_blocks(w.max_cells, frames);
     const dim3 F1(1, frames), FP(gp, frames), FC(gc, frames);
@@ -1312,7 +1344,7 @@ int run_dbscan(const double *x, int64_t nmax, int32_t min_samples, DbscanWs &w, 
     if (rc) return rc;
     hipLaunchKernelGGL(copy_u32_kernel, FC, dim3(256), 0, s, w.fill, w.cellstart, w.P, P_NCELL, 1, fm);
     hipLaunchKernelGGL(dbscan_scatter_kernel, FP, dim3(256), 0, s, x, w.P, w.cid, w.fill, w.order, w.sxyz, fm);
-    hipLaunchKernelGGL(dbscan_count_kernel, FP, dim3(256), 0, s, w.P, w.cid, w.cellstart, w.order, w.sxyz, w.cnt, fm);
+    hipLaunchKernelGGL(dbscan_count_kernel, FP, dim3(256), 0, s, w.P, w.cid, w.cellstart, w.order, w.sxyz, w.cnt, limit, fm);
     if (count_only) {
         LAUNCH_CHECK();
         return LIDAR_OK;
@@ -1389,7 +1421,7 @@ LIDAR_EXPORT int lidar_dbscan_f64(lidar_handle *h, const double *x, int64_t n, d
     hp[P_ACTIVE] = 1.0;
     HIP_TRY(hipMemcpyAsync(w.P, hp, sizeof hp, hipMemcpyHostToDevice, s));
     hipLaunchKernelGGL(dbscan_bbox_kernel, dim3(1), dim3(kT), 0, s, x, w.P, FrameMap{});
-    int rc = run_dbscan(x, n, min_samples, w, labels, s, FrameMap{}, 1);
+    int rc = run_dbscan(x, n, min_samples, w, labels, s, FrameMap{}, 1, false, counts != nullptr);
     if (rc) return rc;
     if (counts) HIP_TRY(hipMemcpyAsync(counts, w.cnt, sizeof(int32_t) * n, hipMemcpyDeviceToDevice, s));
     // hp is a stack buffer: make sure the H2D copy has consumed it

@@ -8,20 +8,22 @@ scaling".  Workload (configs[2] / configs[3]): the 3-level SSG encoder
 per-GPU share of configs[3] (256 frames over 8 GPUs) — so N GPUs process 32*N frames
 per step (weak scaling, per-frame data parallel, no collective on the data path).
 
-A step = FPS + ball query + fused group/MLP/max-pool for SA1 and SA2, then group_all
-(three MFMA dense layers with a fused max-pool) over the batch, inputs resident in HBM.
-Steps run through pointnet2.StreamingSSG — the steady state of a continuous LiDAR feed:
-later batches' SA1 FPS (latency-bound, one 512-thread workgroup per frame) and the SA1
-ball-query binning run on side streams (--depth 3 groups in flight) while earlier batches'
-ball queries and MFMA levels run on the main stream; groups of three batches share one
-FPS launch and one main-stream pass (--fps-group 3; every operator is per frame, outputs
-are bit-identical to one-batch forward()).  K steps = K batches of 32 frames fully
-processed inside the timed region (pipeline fill included).
+A step = one 32-frame batch through FPS + ball query + fused group/MLP/max-pool for SA1 and
+SA2, then group_all (three MFMA dense layers with a fused max-pool), inputs resident in HBM.
+Steps run through pointnet2.StreamingSSG's persistent feed — the steady state of a LiDAR
+stream: later batches' SA1 FPS + ball queries (latency-bound, one 512-thread workgroup per
+frame) run on `depth` side streams while earlier batches' MFMA levels run on the main stream;
+G batches share one FPS launch and one main-stream pass.  The warm-up fills the pipeline
+(`depth` groups in flight), then the timed window pushes exactly K batches and completes
+exactly K (K a multiple of G): every stage processes K batches of work inside the window.
+The input rotates over 8 distinct device-resident batches, and every output of warm-up,
+window and drain is checked bit for bit against one-batch forward() of its batch.
 Synthetic data: uniform [-1, 1]^3 float32 frames (seeded per rank), random-init weights.
 
 Run:  python bench.py [--gpus N --steps K --warmup W]  (N>1 via torch.distributed.run)
 """
 import argparse
+import hashlib
 import json
 import os
 import platform
@@ -33,12 +35,14 @@ import numpy as np
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-# per-frame algorithmic work of each kernel of the SSG stack at N points
-FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: fp32 matrix (= vector) peak
-BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: bf16 dense matrix peak
+# MI355X_MICROARCH.md peaks
+FP32_MFMA_PEAK_TFLOPS = 157.3   # fp32 matrix (= vector) peak
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # bf16 dense matrix peak
 # the x3 kernels carry each fp32 product as 3 bf16 MFMA products: their fp32-equivalent peak
 X3_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 3
+FP64_VALU_PEAK_TFLOPS = 78.6
 HBM_PEAK_GBS = 8000.0
+X3_KERNELS = ("sa1_group_mlp", "sa2_group_mlp", "sa2_layer1_points", "sa3_dense1", "sa3_dense2", "sa3_dense3_pool")
 
 
 def mlp_flops(rows, widths_in):
@@ -46,6 +50,7 @@ def mlp_flops(rows, widths_in):
 
 
 def ssg_kernel_work(n):
+    """Algorithmic work per FRAME of each kernel of the SSG stack at n points."""
     m1, m2 = n // 16, n // 64
     return {
         "sa1_group_mlp": ("mfma", mlp_flops(m1 * 32, [3, 64, 64, 128])),
@@ -59,31 +64,62 @@ def ssg_kernel_work(n):
         # compulsory bytes: read xyz, write idx + new_xyz
         "sa1_fps": ("hbm", 12 * n + 16 * m1),
         "sa2_fps": ("hbm", 12 * m1 + 16 * m2),
+        # read points + centres, write idx (the binning inside the call reads the points once more)
         "sa1_ball_query": ("hbm", 12 * (n + m1) + 4 * m1 * 32),
-        # the grid ball query's binning (side stream): read xyz, write (x, y, z, index) + slot table
-        "sa1_bq_bin": ("hbm", 12 * n + 16 * n + 4 * 16385),
         "sa2_ball_query": ("hbm", 12 * (m1 + m2) + 4 * m2 * 64),
     }
 
 
-def pmc_traffic(B, N):
-    """Memory-side bytes per launch from the committed PMC passes (tools/pmc_traffic.py),
-    when they were taken on this same workload; None otherwise."""
+def pick_group(steps, want):
+    """Batches per FPS launch: the steady-state window must hold whole groups (every launch
+    inside it covers the same number of frames), so G divides K; `want` first, then 3, 4, 5, 2."""
+    for g in (want, 3, 4, 5, 2, 1):
+        if g >= 1 and steps % g == 0:
+            return g
+    return 1
+
+
+def latest_profile(name):
+    """The newest profiles/r*/<name> (committed PMC reductions), or None."""
     import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "pmc_traffic.json")))
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*", name)))
     if not files:
-        return {}
+        return None
     with open(files[-1]) as f:
-        d = json.load(f)
-    c = d.get("config", {})
-    if c.get("points_per_frame") != N or c.get("frames_per_gpu") != B:
-        return {}
-    return {k: v["traffic_bytes"] for k, v in d.get("kernels", {}).items()}
+        return json.load(f), os.path.relpath(files[-1], REPO)
+
+
+def pmc_per_frame(N):
+    """Memory-side bytes and VALU activity PER FRAME per kernel from the committed PMC passes
+    (tools/pmc_traffic.py, tools/pmc_valu.py), when they were taken on this frame size."""
+    out = {}
+    got = latest_profile("pmc_traffic.json")
+    if got and got[0].get("config", {}).get("points_per_frame") == N:
+        d, src = got
+        fpl = d["config"].get("frames_per_launch", 96)
+        for k, v in d.get("kernels", {}).items():
+            out.setdefault(k, {})["traffic_per_frame"] = v["traffic_bytes"] / fpl
+            out[k]["traffic_source"] = src
+    got = latest_profile("pmc_valu.json")
+    if got and got[0].get("config", {}).get("points_per_frame") == N:
+        d, src = got
+        for k, v in d.get("kernels", {}).items():
+            out.setdefault(k, {}).update({"valu_busy": v.get("valu_busy"), "valu_insts_per_frame": v.get("valu_insts_per_frame"),
+                                          "valu_source": src})
+    return out
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            return next(l.split(":", 1)[1].strip() for l in f if l.startswith("model name"))
+    except Exception:
+        return platform.processor() or platform.machine()
 
 
 def cpu_baseline(n, budget_s=20.0):
     """The oracle SA stack (C FPS / ball query + numpy MLP, BLAS pinned to 1 thread) on
-    one frame of the same workload, on this host.  kind = "port" (the reference has no
+    frames of the same workload, on this host.  kind = "port" (the reference has no
     SetAbstraction code to time)."""
     from threadpoolctl import threadpool_limits
     from oracle import tier_n
@@ -100,59 +136,145 @@ def cpu_baseline(n, budget_s=20.0):
             if time.perf_counter() - t0 > budget_s or frames >= 64:
                 break
     dt = time.perf_counter() - t0
-    cpu = platform.processor() or platform.machine()
-    try:
-        with open("/proc/cpuinfo") as f:
-            cpu = next(l.split(":", 1)[1].strip() for l in f if l.startswith("model name"))
-    except Exception:
-        pass
     return {"value": frames * n / dt / 1e6, "unit": "M points/s", "cores": 1, "kind": "port",
             "sample": f"{frames} x {n}-point SSG frame(s) through oracle/tier_n.sa_stack "
-                      f"(C FPS + C ball query + numpy fp32 MLP, 1 thread) in {dt:.1f} s on {cpu}; "
+                      f"(C FPS + C ball query + numpy fp32 MLP, 1 thread) in {dt:.1f} s on {cpu_model()}; "
                       f"host has {os.cpu_count()} logical CPUs"}
 
 
 def tier_r_cpu_baseline(n, budget_s=12.0):
-    """oracle/tier_r (the byte-identical CPU restatement of the reference density path:
-    numpy + the C DBSCAN of the same neighbourhood rule) on uniform +-15 m frames."""
+    """The reference's density path with the reference's own library calls: oracle/tier_r's
+    restatement with scikit-learn's StandardScaler -> DBSCAN(eps, min_samples=5) (the calls at
+    utils/data_processing.py:190-197, kd-tree neighbour search), numpy for the rest; falls back
+    to the byte-identical C DBSCAN when scikit-learn is not importable."""
+    from threadpoolctl import threadpool_limits
     from oracle import tier_r
     from lidar_ai_recommendation_software_amd.synthetic import uniform_frame
+    try:
+        import sklearn  # noqa: F401
+        dbscan = "sklearn"
+    except ImportError:
+        dbscan = "c"
     frames, t0 = 0, time.perf_counter()
-    while True:
-        pd = tier_r.preprocess_lidar_data(uniform_frame(n, 2000 + frames))
-        tier_r.analyze(pd)
-        frames += 1
-        if time.perf_counter() - t0 > budget_s or frames >= 32:
-            break
+    with threadpool_limits(limits=1):
+        while True:
+            pd = tier_r.preprocess_lidar_data(uniform_frame(n, 2000 + frames), dbscan=dbscan)
+            tier_r.analyze(pd)
+            frames += 1
+            if time.perf_counter() - t0 > budget_s or frames >= 32:
+                break
     dt = time.perf_counter() - t0
+    what = ("scikit-learn StandardScaler + DBSCAN(min_samples=5), as the reference calls them"
+            if dbscan == "sklearn" else "the C DBSCAN of the same neighbourhood rule (scikit-learn not importable)")
     return {"value": frames * n / dt / 1e6, "unit": "M points/s", "cores": 1, "kind": "port",
             "sample": f"{frames} x {n}-point uniform frame(s) through oracle/tier_r preprocess + analyze "
-                      f"(byte-identical restatement of the reference's numpy/sklearn path, 1 thread) in {dt:.1f} s"}
+                      f"({what}; numpy for the rest, 1 thread) in {dt:.1f} s on {cpu_model()}"}
 
 
-def tier_r_leg(dev, rank, world, frames=32, n=65536, workers=4, steps=3, cpu=True, cpu_budget=12.0):
+# algorithmic work per input point of the density path's phases (DESIGN.md §2): bytes for the
+# byte-moving phases, fp64 FLOP for the eps tests (8 per eps-pair: 3 sub, 3 mul, 2 add)
+DENSITY_BYTES_PER_POINT = {
+    # xyz in (24) + mask (1) + colours, normals, inlier rows (72) + scaled non-ground rows (~0.7 * 24 + 4 pos)
+    "preprocess": 24 + 1 + 72 + 21,
+    "dbscan_grid": 24 + 4 + 4 + 24 + 4,  # read scaled rows, cell id, order, sorted rows, parent
+    "label_scatter": 8 + 4 + 8,
+    "people": 16 + 8,
+}
+
+
+def tier_r_leg(dev, rank, world, frames=32, n=65536, steps=3, cpu=True, cpu_budget=12.0):
     """The reference's own path (Tier R: preprocess -> DBSCAN -> people -> density grid) on
     device-resident uniform +-15 m frames: batches of `frames` frames through
-    density_stream.DensityStream.run_batch (one launch per phase over the CSR batch)."""
+    density_stream.DensityStream.run_batch (one launch per phase over the CSR batch), with
+    per-phase HIP-event durations from the library (lidar_profile) in a second window."""
     import torch
     from lidar_ai_recommendation_software_amd import sharding
     from lidar_ai_recommendation_software_amd.density_stream import DensityStream
     from lidar_ai_recommendation_software_amd.synthetic import uniform_frame
     xs = [torch.from_numpy(uniform_frame(n, sharding.frame_seed(rank, base=1000 + i))).to(dev) for i in range(frames)]
-    ds = DensityStream(dev, workers=workers)
-    ds.run_batch(xs)  # warm-up: workspaces sized
+    ds = DensityStream(dev)
+    ref = ds.run_batch(xs)  # warm-up: workspaces sized
     el = sharding.timed(lambda: [ds.run_batch(xs) for _ in range(steps)], dev, world)
+    ds.profile(True)
+    for _ in range(steps):
+        got = ds.run_batch(xs)
+    torch.cuda.synchronize(dev)
+    phases = ds.profile_read()
+    ds.profile(False)
+    assert all(a["total_people"] == b["total_people"] and np.array_equal(a["density_map"], b["density_map"])
+               for a, b in zip(ref, got)), "density path not deterministic"
+    per_launch_ms = {k: t / c for k, (c, t) in phases.items()}
+    dom = max(phases, key=lambda k: phases[k][1])
+    pts = frames * n
     rec = {"metric": "M points/s through the reference density path (preprocess + DBSCAN + people + "
                      "density grid), device-resident frames",
            "value": sharding.aggregate_rate(frames * n * steps, world, el) / 1e6, "unit": "M points/s",
            "ms_per_frame": el / (frames * steps) * 1e3, "frames_per_gpu": frames, "points_per_frame": n,
            "executor": "DensityStream.run_batch (CSR batch, one launch per phase)", "dtype": "f64",
            "parity": "byte-identical to the reference (tests/golden)",
-           "cpu_baseline": None}
+           "phase_ms_per_launch": per_launch_ms, "dominant_phase": dom, "cpu_baseline": None}
+    if dom in DENSITY_BYTES_PER_POINT:
+        algo = DENSITY_BYTES_PER_POINT[dom] * pts
+        a = algo / (per_launch_ms[dom] / 1e3) / 1e9
+        rec["roofline"] = {"kernel": dom, "bound": "hbm", "achieved": a, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                           "frac": a / HBM_PEAK_GBS, "traffic": None, "work_per_launch": algo,
+                           "avg_launch_ms": per_launch_ms[dom],
+                           "peak_basis": "HBM peak over algorithmic bytes; the phase is latency-bound (numpy's "
+                                         "sequential axis-0 sums: six dependent fp64 chains per frame, DESIGN.md §2)"}
+    if "preprocess" in per_launch_ms:
+        # the sequential chains: ~6 passes of n dependent fp64 adds per frame, frames in parallel
+        rec["preprocess_chain_ns_per_row"] = per_launch_ms["preprocess"] * 1e6 / (6 * n)
     if cpu and rank == 0 and world == 1:
         rec["cpu_baseline"] = tier_r_cpu_baseline(n, cpu_budget)
         rec["speedup_vs_cpu"] = rec["value"] / rec["cpu_baseline"]["value"]
+    # SURVEY §8e's optional global density: every frame's people binned into one fixed venue grid
+    # per rank, then ONE RCCL all-reduce (int32 sum) over the ranks
+    from lidar_ai_recommendation_software_amd.global_density import VenueGrid
+    vg = VenueGrid((-15.0, 15.0), (-15.0, 15.0), 1.0, device=dev)
+    people = ds.people_of_last_batch()
+    vg.add(people)
+    t0 = time.perf_counter()
+    vg.all_reduce()
+    torch.cuda.synchronize(dev)
+    rec["global_density"] = {"venue_cells": int(vg.counts.numel()), "people_per_rank": int(people.shape[0]),
+                             "people_all_ranks": int(vg.counts.sum().item()),
+                             "all_reduce_ms": (time.perf_counter() - t0) * 1e3,
+                             "collective": "torch.distributed all_reduce(int32, SUM) over "
+                                           + ("RCCL" if world > 1 and vg.backend() == "nccl" else
+                                              "gloo" if world > 1 else "none (1 rank)")}
     return rec
+
+
+def host_frame_leg(rank, world, frames=16, n=65536, cpu=True):
+    """host frames through the drop-in API — preprocess_lidar_data(numpy) ->
+    CrowdDensityModel().analyze -> dict, PCIe included, one frame per call (what app.py does);
+    and the same frames through frame_feed.HostFrameFeed (pinned staging, H2D on a copy stream
+    overlapped with the previous batch's kernels, one launch per phase per batch)."""
+    import torch
+    from lidar_ai_recommendation_software_amd import data_processing as dp
+    from lidar_ai_recommendation_software_amd.crowd_density_model import CrowdDensityModel
+    from lidar_ai_recommendation_software_amd.frame_feed import HostFrameFeed
+    from lidar_ai_recommendation_software_amd.synthetic import uniform_frame
+    xs = [uniform_frame(n, 7000 + 131 * rank + i) for i in range(frames)]
+    model = CrowdDensityModel()
+    model.analyze(dp.preprocess_lidar_data(xs[0]))  # warm-up
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    want = [model.analyze(dp.preprocess_lidar_data(x)) for x in xs]
+    dt = time.perf_counter() - t0
+    feed = HostFrameFeed(batch=8)
+    feed.run(xs[:8])  # warm-up: pinned buffers and workspaces sized
+    t0 = time.perf_counter()
+    got = feed.run(xs)
+    dt2 = time.perf_counter() - t0
+    assert all(a["total_people"] == b["total_people"] and np.array_equal(a["density_map"], b["density_map"])
+               for a, b in zip(want, got)), "HostFrameFeed differs from the drop-in API"
+    return {"metric": "M points/s, host numpy frames -> preprocess_lidar_data -> CrowdDensityModel.analyze "
+                      "dicts (PCIe-inclusive)",
+            "drop_in_per_frame": {"value": frames * n / dt / 1e6, "unit": "M points/s", "ms_per_frame": dt / frames * 1e3},
+            "host_frame_feed": {"value": frames * n / dt2 / 1e6, "unit": "M points/s",
+                                "ms_per_frame": dt2 / frames * 1e3, "batch": 8},
+            "frames": frames, "points_per_frame": n, "parity": "HostFrameFeed == the drop-in API, frame for frame"}
 
 
 def voxel_leg(dev, rank, world, B=32, n=65536, voxel=0.05, steps=20, cpu=True):
@@ -234,182 +356,226 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=240,
-                    help="timed steps; the pipeline fill (one SA1-FPS latency, ~12 ms) is inside the window")
-    ap.add_argument("--warmup", type=int, default=3)
+                    help="timed steps (32-frame batches) of the steady-state window")
+    ap.add_argument("--warmup", type=int, default=3, help="warm-up groups beyond the pipeline fill")
     ap.add_argument("--batch", type=int, default=32, help="frames per GPU per step")
     ap.add_argument("--points", type=int, default=65536)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU work per baseline sample")
     ap.add_argument("--depth", type=int, default=3, help="side streams (SA1-FPS groups in flight ahead of the MLPs)")
-    ap.add_argument("--side-priority", type=int, default=0, help="HIP priority of the FPS streams (<0 = high)")
-    ap.add_argument("--fps-group", type=int, default=3, help="batches per SA1-FPS launch (StreamingSSG fps_group)")
-    ap.add_argument("--side-cus", type=int, default=0, help="CUs reserved for the SA1 FPS streams (0 = shared)")
-    ap.add_argument("--fps-threads", type=int, default=512, choices=[256, 512, 1024],
+    ap.add_argument("--fps-group", type=int, default=3,
+                    help="batches per SA1-FPS launch (StreamingSSG fps_group); must divide --steps, else the "
+                         "nearest of 3, 4, 5, 2 that does")
+    ap.add_argument("--fps-threads", type=int, default=512, choices=[512, 1024],
                     help="SA1 FPS workgroup size in the pipeline (512: half the CU footprint beside the MLPs)")
-    ap.add_argument("--cu-layout", default="xcd", choices=["xcd", "low"])
-    ap.add_argument("--mlp16", default="pre", choices=["0", "1", "pre", "xyz"],
-                    help="SA branches on the 16-row MFMA kernels: 1 all, pre / xyz only those levels")
-    ap.add_argument("--x3", default="1", choices=["0", "1", "pre", "xyz"],
-                    help="SA layers 2-3 on the split-bf16 (x3) kernels: fp32 arithmetic within the 1e-4 "
-                         "contract; 0 = native fp32 MFMA kernels")
-    ap.add_argument("--shared-bin", type=int, default=0,
-                    help="1: one ball-query binning per group for all branches (MSG: 452 vs 468-494 M pts/s, off)")
-    ap.add_argument("--ramp", type=int, default=1, help="1: first groups of 1, 2, .. batches (shorter fill)")
-    ap.add_argument("--reserve", type=int, default=1, help="1: size the side handles' workspaces at setup")
-    ap.add_argument("--x3s", type=int, default=1, help="1: dense layers on the split-plane x3 GEMM")
-    ap.add_argument("--bq-main", type=int, default=0, help="1: SA1 ball queries on the main stream (0: on the FPS side streams)")
-    ap.add_argument("--l1-side", type=int, default=0,
-                    help="1: SA2's FPS and ball queries (they need only SA1's centres) on the side streams")
+    ap.add_argument("--x3", type=int, default=1,
+                    help="1: MLPs on the split-bf16 (x3) kernels, fp32 arithmetic within the 1e-4 contract; "
+                         "0: the native fp32-MFMA kernels")
+    ap.add_argument("--rotate", type=int, default=8, help="distinct device-resident input batches the feed cycles over")
     ap.add_argument("--no-fp32-mfma-leg", action="store_true",
                     help="skip the extra measurement of the native fp32-MFMA kernels (when --x3 is on)")
+    ap.add_argument("--no-standalone", action="store_true",
+                    help="skip the standalone (no pipeline) kernel timings of one 96-frame forward()")
     ap.add_argument("--msg-batch", type=int, default=32,
                     help="frames per GPU per step of the configs[4] MSG leg (32: the per-GPU share of 256 frames)")
     ap.add_argument("--msg-steps", type=int, default=30)
-    ap.add_argument("--msg-x3", type=int, default=0, help="1: also time the MSG leg in fp32 on the x3 kernels")
     ap.add_argument("--no-extras", action="store_true", help="skip the configs[1]/[4] side measurements")
-    ap.add_argument("--no-density", action="store_true", help="skip the Tier R density-path leg")
+    ap.add_argument("--no-density", action="store_true", help="skip the Tier R / variant / voxel / host-frame legs")
+    ap.add_argument("--seed-rank", type=int, default=None,
+                    help="generate the frames of this rank (a 1-process run reproducing one rank of an N-rank run)")
+    ap.add_argument("--dump", default=None, help="write this rank's output digests to DUMP.rank<r>.json")
     args = ap.parse_args()
 
     import torch
     import torch.distributed as dist
     from lidar_ai_recommendation_software_amd import pointnet2 as pn
+    from lidar_ai_recommendation_software_amd import sharding
     from lidar_ai_recommendation_software_amd.synthetic import unit_frames
 
-    from lidar_ai_recommendation_software_amd import sharding
     rank, world, local = sharding.world_info()
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+    dev = torch.device("cuda", sharding.init_distributed(world, local))
     torch.cuda.set_device(dev)
+    seed_rank = rank if args.seed_rank is None else args.seed_rank
 
     B, N = args.batch, args.points
+    G = pick_group(args.steps, args.fps_group)
+    digests = {}
 
-    x3_opt = {"0": False, "1": True}.get(args.x3, args.x3)
-
-    def measure(cfg, dtype, B, N, steps, warmup, depth, events_in_window=True, x3=None):
-        """events_in_window: HIP events around every launch inside the timed window (the
-        headline: the roofline durations come from the same window).  False: the window
-        runs clean and the per-kernel durations come from a second, instrumented window
-        of the same length (with ~25 launches per step, as MSG has, the events cost ~1/3)."""
-        bb = pn.PointNet2Backbone(cfg, device=dev, seed=0, dtype=dtype,
-                                  mlp16={"0": False, "1": True}.get(args.mlp16, args.mlp16),
-                                  x3=x3_opt if x3 is None else x3, x3s=bool(args.x3s))
-        x = torch.from_numpy(unit_frames(B, N, seed=sharding.frame_seed(rank))).to(dev)
-        # the streaming executor overlaps batch k+1's SA1 FPS + ball queries (latency-bound,
-        # one workgroup per frame) with batch k's MFMA levels; results are identical to forward()
-        pipe = pn.StreamingSSG(bb, B, N, depth=depth, side_priority=args.side_priority,
-                               side_cus=args.side_cus, cu_layout=args.cu_layout, fps_group=args.fps_group,
-                               bq_on_main=bool(args.bq_main), fps_threads=args.fps_threads,
-                               level1_on_side=bool(args.l1_side), shared_bin=bool(args.shared_bin),
-                               reserve=bool(args.reserve), ramp=bool(args.ramp))
-        ref, _ = bb.forward(x)
-        outs = pipe.run([x] * max(2, warmup))
-        torch.cuda.synchronize(dev)
-        assert all(torch.equal(ref, o) for o in outs), "streaming executor diverged from forward()"
+    def measure(key, cfg, dtype, B, N, steps, warmup, depth, G, x3=True, events=True):
+        """Steady-state window of `steps` batches through StreamingSSG's feed.  events: HIP
+        events around every launch inside the timed window (the headline: the roofline durations
+        come from the same window); False: the window runs clean and the per-kernel durations come
+        from a second window of the same length (with ~25 launches per step, as MSG has, the
+        events cost ~1/3)."""
+        bb = pn.PointNet2Backbone(cfg, device=dev, seed=0, dtype=dtype, x3=x3)
+        nb = max(1, args.rotate)
+        xs = [torch.from_numpy(unit_frames(B, N, seed=sharding.frame_seed(seed_rank, step=i))).to(dev) for i in range(nb)]
+        refs = [bb.forward(x)[0] for x in xs]  # one-batch forward(): what every pipeline output must equal
+        pipe = pn.StreamingSSG(bb, B, N, depth=depth, fps_group=G, fps_threads=args.fps_threads, ramp=False)
+        feed = pipe.feed()
+        nwarm = (depth + max(1, warmup)) * G  # whole groups; `depth` groups in flight when the window opens
+        outs = []
+        for i in range(nwarm):
+            outs += feed.push(xs[i % nb])
         timers = pn._Timers()
-        if events_in_window:
-            bb.timers = timers  # HIP events around every launch, on the stream it is launched on
-            elapsed = sharding.timed(lambda: pipe.run([x] * steps), dev, world)  # max over ranks
-        else:
-            elapsed = sharding.timed(lambda: pipe.run([x] * steps), dev, world)
-            bb.timers = timers
-            pipe.run([x] * steps)
-            torch.cuda.synchronize(dev)
-        bb.timers = None
-        return elapsed, timers.mean_ms()
+        win = []
 
-    elapsed, kern = measure(pn.SSG, "f32", B, N, args.steps, args.warmup, args.depth)
+        def window(i0, sink):
+            for i in range(i0, i0 + steps):
+                sink.extend(feed.push(xs[i % nb]))
+
+        if events:
+            bb.timers = timers
+            elapsed = sharding.timed(lambda: window(nwarm, win), dev, world)  # max over ranks
+            bb.timers = None
+            outs += win
+            i_end = nwarm + steps
+        else:
+            elapsed = sharding.timed(lambda: window(nwarm, win), dev, world)
+            outs += win
+            bb.timers = timers
+            win2 = []
+            window(nwarm + steps, win2)
+            bb.timers = None
+            outs += win2
+            i_end = nwarm + 2 * steps
+        assert len(win) == steps, f"window completed {len(win)} batches, expected {steps}"
+        outs += feed.flush()
+        torch.cuda.synchronize(dev)
+        assert len(outs) == i_end, (len(outs), i_end)
+        bad = [i for i, o in enumerate(outs) if not torch.equal(o, refs[i % nb])]
+        assert not bad, f"{key}: streaming outputs differ from forward() for batches {bad[:5]}"
+        digests[key] = [hashlib.sha256(r.cpu().numpy().tobytes()).hexdigest() for r in refs]
+        return elapsed, timers.totals(), bb, xs
+
+    tot_x3 = None
+    elapsed, tot, bb, xs = measure("ssg", pn.SSG, "f32", B, N, args.steps, args.warmup, args.depth, G, x3=bool(args.x3))
     fp32_mfma = None
-    if x3_opt and not args.no_fp32_mfma_leg:
+    if args.x3 and not args.no_fp32_mfma_leg:
         # the same workload on the native fp32-MFMA kernels (clean window), for comparison
-        el_f, k_f = measure(pn.SSG, "f32", B, N, args.steps, args.warmup, args.depth, events_in_window=False,
-                            x3=False)
+        el_f, t_f, _, _ = measure("ssg_fp32_mfma", pn.SSG, "f32", B, N, args.steps, args.warmup, args.depth, G,
+                                  x3=False, events=False)
         fp32_mfma = {"value": sharding.aggregate_rate(B * N * args.steps, world, el_f) / 1e6, "unit": "M points/s",
                      "ms_per_step": el_f / args.steps * 1e3,
-                     "sa2_group_mlp_ms": k_f.get("sa2_group_mlp"), "sa1_group_mlp_ms": k_f.get("sa1_group_mlp")}
+                     "kernel_ms_per_launch": {k: t / c for k, (c, f, t) in t_f.items()}}
+    standalone = None
+    if not args.no_standalone:
+        # the kernels alone: one forward() over a group's frames (G*B), nothing else on the chip
+        xg = torch.cat(xs[:G])
+        bb.forward(xg)
+        torch.cuda.synchronize(dev)
+        st = pn._Timers()
+        bb.timers = st
+        for _ in range(3):
+            bb.forward(xg)
+        torch.cuda.synchronize(dev)
+        bb.timers = None
+        standalone = st.totals()
+        del xg
     extras = {}
     if not args.no_extras:
         # the other BASELINE.json configs, measured the same way (not the headline metric)
         legs = [("configs[1]_sa1_16k_f32", pn.SA1_ONLY, "f32", 32, 16384, 40),
                 ("configs[4]_msg_131k_bf16", pn.MSG, "bf16", args.msg_batch, 131072, args.msg_steps)]
-        if args.msg_x3:  # the same MSG stack in fp32 arithmetic on the x3 kernels (bf16 MFMA products)
-            legs.append(("configs[4]_msg_131k_f32x3", pn.MSG, "f32", args.msg_batch, 131072, args.msg_steps))
-        for key, cfg, dtype, b2, n2, st in legs:
-            el2, k2 = measure(cfg, dtype, b2, n2, st, 2, 3, events_in_window=False)
-            extras[key] = {"M_points_per_s": sharding.aggregate_rate(b2 * n2 * st, world, el2) / 1e6, "ms_per_step": el2 / st * 1e3,
-                           "frames_per_gpu": b2, "points_per_frame": n2, "dtype": dtype,
-                           "kernel_ms": k2}
+        for key, cfg, dtype, b2, n2, st2 in legs:
+            g2 = pick_group(st2, 3)
+            el2, t2, _, _ = measure(key, cfg, dtype, b2, n2, st2, 1, 3, g2, events=False)
+            extras[key] = {"M_points_per_s": sharding.aggregate_rate(b2 * n2 * st2, world, el2) / 1e6,
+                           "ms_per_step": el2 / st2 * 1e3, "frames_per_gpu": b2, "points_per_frame": n2,
+                           "dtype": dtype, "batches_per_group": g2,
+                           "kernel_ms_per_launch": {k: t / c for k, (c, f, t) in t2.items()}}
 
-    density = None if args.no_density else tier_r_leg(dev, rank, world, cpu=not args.no_cpu_baseline, cpu_budget=args.cpu_budget)
-    variant = None if args.no_density else variant_leg(rank, world, cpu=not args.no_cpu_baseline)
-    voxel = None if args.no_density else voxel_leg(dev, rank, world, cpu=not args.no_cpu_baseline)
+    density = variant = voxel = host = None
+    if not args.no_density:
+        cpu = not args.no_cpu_baseline
+        density = tier_r_leg(dev, seed_rank, world, cpu=cpu, cpu_budget=args.cpu_budget)
+        variant = variant_leg(seed_rank, world, cpu=cpu)
+        voxel = voxel_leg(dev, seed_rank, world, cpu=cpu)
+        host = host_frame_leg(seed_rank, world, cpu=cpu)
     work = ssg_kernel_work(N)
-    traffic = pmc_traffic(B, N)
-    # Two chains per group of batches: the side streams' SA1 FPS + ball queries (`depth`
-    # groups in flight; FPS is one workgroup per frame, latency-bound: read as us/step) and
-    # the main stream's full-chip kernels.  The roofline is reported for the kernel that
-    # dominates the main chain's device time; the chain lengths say which chain bounds a step.
-    # issued on the side streams, overlapped with the rest
-    side = ("sa1_fps", "sa1_bq_bin") if args.bq_main else ("sa1_fps", "sa1_ball_query")
-    if args.l1_side:
-        side += ("sa2_fps", "sa2_ball_query")
-    main = {k: v for k, v in kern.items() if k not in side}
-    side_ms = sum(kern.get(k, 0) for k in side) / args.depth
-    dom = max(main, key=lambda k: main[k])
-    chains = {"side_ms_per_group": side_ms, "main_ms_per_group": sum(main.values()),
-              "bound_by": "side (SA1 FPS latency)" if side_ms > sum(main.values()) else "main (MFMA levels)",
-              "sa1_fps_us_per_step": kern.get("sa1_fps", 0) * 1e3 / max(1, N // 16)}
+    pmc = pmc_per_frame(N)
 
-    def roof(name):
+    def roof(name, totals):
+        """Roofline of one kernel over the launches `totals` recorded: achieved = the algorithmic
+        work of all frames those launches processed / the sum of their durations (so frac = Σwork /
+        Σtime / peak by construction, whatever the frames per launch)."""
         bound, per_frame = work[name]
-        per_launch = per_frame * B * args.fps_group  # one launch covers a group of batches
-        avg_s = kern[name] / 1e3
+        launches, frames, ms = totals[name]
+        s = ms / 1e3
+        w_total = per_frame * frames
         if bound == "mfma":
-            # with x3 on, the grouped SA kernels AND the dense GEMMs (SA2's per-point layer 1,
-            # group_all's three layers: dense_x3p) issue 3 bf16 MFMA products per fp32 product
-            x3k = x3_opt and name in ("sa1_group_mlp", "sa2_group_mlp", "sa2_layer1_points",
-                                      "sa3_dense1", "sa3_dense2", "sa3_dense3_pool")
-            a, p, u = per_launch / avg_s / 1e12, X3_PEAK_TFLOPS if x3k else FP32_MFMA_PEAK_TFLOPS, "TFLOP/s"
+            x3k = bool(args.x3) and name in X3_KERNELS
+            a, p, u = w_total / s / 1e12, X3_PEAK_TFLOPS if x3k else FP32_MFMA_PEAK_TFLOPS, "TFLOP/s"
+            basis = ("bf16 MFMA dense peak / 3 (x3: 3 bf16 products per fp32 product)" if x3k else "fp32 MFMA peak")
         else:
-            a, p, u = per_launch / avg_s / 1e9, HBM_PEAK_GBS, "GB/s"
-        return {"kernel": name, "bound": bound, "achieved": a, "peak": p, "unit": u, "frac": a / p,
-                "traffic": traffic.get(name), "traffic_unit": "bytes per launch (PMC FETCH_SIZE*2 + WRITE_SIZE)",
-                "work_per_launch": per_launch, "avg_launch_ms": kern[name],
-                "peak_basis": ("bf16 MFMA dense peak / 3 (x3: 3 bf16 products per fp32 product)"
-                               if bound == "mfma" and p == X3_PEAK_TFLOPS else
-                               "fp32 MFMA peak" if bound == "mfma" else "HBM peak")}
+            a, p, u = w_total / s / 1e9, HBM_PEAK_GBS, "GB/s"
+            basis = "HBM peak over compulsory bytes"
+        r = {"kernel": name, "bound": bound, "achieved": a, "peak": p, "unit": u, "frac": a / p,
+             "traffic": None, "work_per_launch": w_total / launches, "avg_launch_ms": ms / launches,
+             "launches": launches, "frames": frames, "total_ms": ms, "peak_basis": basis}
+        pm = pmc.get(name, {})
+        if "traffic_per_frame" in pm:
+            r["traffic"] = pm["traffic_per_frame"] * frames / launches
+            r["traffic_unit"] = "bytes per launch (PMC FETCH_SIZE*2 + WRITE_SIZE, " + pm["traffic_source"] + ")"
+            r["measured_gbs"] = r["traffic"] / (ms / launches / 1e3) / 1e9
+        if pm.get("valu_busy") is not None:
+            r["valu_busy"] = pm["valu_busy"]
+            r["valu_source"] = pm["valu_source"]
+        return r
+
+    # Two chains per group of batches: the side streams' SA1 FPS + ball queries (`depth` groups
+    # in flight; FPS is one workgroup per frame, latency-bound: read as us/step) and the main
+    # stream's full-chip kernels.  The roofline is reported for the kernel that dominates the
+    # main chain's device time; the chain lengths say which chain bounds a step.
+    side = ("sa1_fps", "sa1_ball_query")
+    per_launch = {k: t / c for k, (c, f, t) in tot.items()}
+    main_k = {k: v for k, v in per_launch.items() if k not in side}
+    side_ms = sum(per_launch.get(k, 0) for k in side) / args.depth
+    main_ms = sum(main_k.values())
+    dom = max((k for k in main_k if k in work), key=lambda k: tot[k][2])
+    chains = {"side_ms_per_group": side_ms, "main_ms_per_group": main_ms,
+              "bound_by": "side (SA1 FPS latency)" if side_ms > main_ms else "main (MFMA levels)",
+              "sa1_fps_us_per_step": per_launch.get("sa1_fps", 0) * 1e3 / max(1, N // 16)}
 
     value = sharding.aggregate_rate(B * N * args.steps, world, elapsed) / 1e6
+    if args.dump:
+        with open(f"{args.dump}.rank{rank}.json", "w") as f:
+            json.dump({"rank": rank, "seed_rank": seed_rank, "world": world, "digests": digests,
+                       "value": value, "ms_per_step": elapsed / args.steps * 1e3}, f)
     if rank == 0:
         rec = {
             "metric": "M points/sec through SetAbstraction, 65k-pt frames; 1->8 GPU scaling",
             "value": value, "unit": "M points/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "f32" + (" (MLP products as split-bf16 x3 MFMA products, fp32 accumulation)" if x3_opt else ""),
+            "dtype": "f32" + (" (MLP products as split-bf16 x3 MFMA products, fp32 accumulation)" if args.x3 else ""),
             "precision": ("fp32 inputs/weights/outputs; SA layers 2-3, SA2's per-point layer 1 and group_all: each "
                           "fp32 operand split exactly into bf16 hi+lo, products ah*bh + ah*bl + al*bh accumulated in "
                           "fp32 (<= ~2^-15 per product); SA1 layer 1 (K = 3) on fp32 MFMA; features within the 1e-4 "
                           "rel contract of the fp32 oracle (tests/test_gpu_tier_n.py::test_group_mlp_x3, "
-                          "test_dense_x3s, test_backbone_vs_oracle)") if x3_opt else
-                         "fp32 MFMA (v_mfma_f32_*_f32)",
-            "data": "synthetic: uniform [-1,1]^3 float32 frames (seeded per rank), random-init SSG weights",
+                          "test_dense_x3s, test_backbone_vs_oracle, test_bench_shape_executor_vs_oracle)")
+                         if args.x3 else "fp32 MFMA (v_mfma_f32_*_f32)",
+            "data": "synthetic: uniform [-1,1]^3 float32 frames (seeded per rank, %d distinct batches cycled), "
+                    "random-init SSG weights" % max(1, args.rotate),
             "config": {"workload": "PointNet++ SSG encoder (SA1 N/16 r0.2 ns32 [64,64,128]; "
                                    "SA2 N/64 r0.4 ns64 [128,128,256]; group_all [256,512,1024]) fp32",
                        "points_per_frame": N, "frames_per_gpu": B, "global_batch_frames": B * world,
                        "parallelism": f"per-frame data parallel x{world} (no collectives)"},
-            "roofline": roof(dom),
+            "roofline": roof(dom, tot),
             # the north_star's MFMA figure: the grouped MLP (SA2 layers 2-3), whatever dominates
-            "roofline_grouped_mlp": roof("sa2_group_mlp") if "sa2_group_mlp" in kern else None,
-            "roofline_all": {k: roof(k) for k in kern if k in work},
-            "kernel_ms": kern,
-            "pipeline": {"executor": "pointnet2.StreamingSSG", "side_streams": args.depth,
-                         "batches_per_group": args.fps_group, "ball_query_stream": "main" if args.bq_main else "side",
-                         **chains},
+            "roofline_grouped_mlp": roof("sa2_group_mlp", tot) if "sa2_group_mlp" in tot else None,
+            "roofline_all": {k: roof(k, tot) for k in tot if k in work},
+            "roofline_standalone": ({k: roof(k, standalone) for k in standalone if k in work}
+                                    if standalone else None),
+            "kernel_ms_per_launch": per_launch,
+            "pipeline": {"executor": "pointnet2.StreamingSSG feed (steady state: the window pushes and completes "
+                                     "exactly `steps` batches; pipeline fill and drain outside it)",
+                         "side_streams": args.depth, "batches_per_group": G, "frames_per_launch": G * B,
+                         "fps_threads": args.fps_threads, **chains},
             "fp32_mfma_kernels": fp32_mfma,
             "other_configs": extras,
             "density_path": density,
+            "host_frames": host,
             "variant_path": variant,
             "voxel_downsample": voxel,
             "cpu_baseline": None,
@@ -419,6 +585,7 @@ def main():
             rec["speedup_vs_cpu"] = value / rec["cpu_baseline"]["value"]
         print(json.dumps(rec), flush=True)
     if world > 1:
+        dist.barrier()
         dist.destroy_process_group()
 
 

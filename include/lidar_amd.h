@@ -46,15 +46,16 @@ int lidar_destroy(lidar_handle *h);
 /* grow the scratch workspace to at least `bytes` now (not inside graph capture) */
 int lidar_reserve(lidar_handle *h, uint64_t bytes);
 
-/* A HIP stream restricted to a subset of the device's compute units (bit i of mask[i/32]
- * enables CU i), returned through *stream (a hipStream_t); release with
- * lidar_stream_destroy.  StreamingSSG's optional side_cus split uses it. */
-int lidar_stream_create_cu_mask(int device, const uint32_t *mask, int32_t nwords, void **stream);
-int lidar_stream_destroy(void *stream);
-/* number of compute units of `device` */
-int lidar_device_cu_count(int device, int32_t *out);
 const char *lidar_last_error(void);
 int lidar_version(void);
+
+/* Per-phase timing of a handle's launches (bench.py's in-window kernel durations): with
+ * lidar_profile(h, 1) every kernel phase issued on h is bracketed by two HIP events on its
+ * stream; lidar_profile_read waits for them and returns, in launch order, the phase names
+ * ('\n'-separated into names, NUL terminated) and durations in ms; lidar_profile(h, 0) stops.
+ * The Tier R entry points (preprocess, DBSCAN, people, density grid) record phases. */
+int lidar_profile(lidar_handle *h, int32_t enable);
+int lidar_profile_read(lidar_handle *h, char *names, int64_t names_cap, float *ms, int64_t cap, int64_t *count);
 
 /* ============================================================ Tier N (SA stack)
  * North_star operators.  The reference has no PointNet++ code; these
@@ -110,42 +111,6 @@ int lidar_ball_query_binned_f32(lidar_handle *h, const float *xyz, const void *g
                                 int64_t batch, int64_t n, int64_t m, float radius, int32_t nsample,
                                 int32_t *idx, void *stream);
 
-/* grouped shared MLP (3 layers, BN folded, ReLU) + max-pool over nsample for one SA
- * branch, fused with the grouping gather:
- *   row (b, c, s) = [xyz[b, idx[b,c,s]] - centres[b,c], feats[b, idx[b,c,s], 0:cfeat]]
- *   out[b, c, out_offset + j] = max_s relu(...relu(row W1 + b1)... W3 + b3)[j]
- * `packed` is the weight image from lidar_mlp_pack_f32 (device copy).  widths: c1, c2, c3
- * multiples of 32; cfeat 0 or a multiple of 8; nsample 16, 32, 64 or 128.
- * out row stride is `out_stride` floats.  feats row stride is `feat_stride` floats. */
-int lidar_sa_group_mlp_f32(lidar_handle *h, const float *xyz, const float *feats,
-                           int64_t feat_stride, const float *centres, const int32_t *idx,
-                           int64_t batch, int64_t n, int64_t m, int32_t nsample, int32_t cfeat,
-                           int32_t c1, int32_t c2, int32_t c3, const float *packed,
-                           float *out, int64_t out_stride, int64_t out_offset, void *stream);
-
-/* size (floats) and host-side construction of the packed weight image for
- * lidar_sa_group_mlp_f32.  W_l are (cin_l, cout_l) row-major host arrays, canonical
- * PointNet++ channel order [dx, dy, dz, feat...] for layer 1. */
-int64_t lidar_mlp_packed_size(int32_t cfeat, int32_t c1, int32_t c2, int32_t c3);
-int lidar_mlp_pack_f32(int32_t cfeat, int32_t c1, int32_t c2, int32_t c3, const float *w1_host,
-                       const float *b1_host, const float *w2_host, const float *b2_host,
-                       const float *w3_host, const float *b3_host, float *packed_host);
-
-/* bf16 variant of lidar_sa_group_mlp_f32 on v_mfma_f32_32x32x16_bf16 (BASELINE configs[4]):
- * grouped xyz offsets, features, hidden activations and weights rounded to bf16 (RNE),
- * fp32 accumulation, fp32 bias/ReLU and fp32 pooled output.  Same argument meaning;
- * `packed` is the byte image from lidar_mlp_pack_bf16 (cfeat a multiple of 16). */
-int lidar_sa_group_mlp_bf16(lidar_handle *h, const float *xyz, const float *feats,
-                            int64_t feat_stride, const float *centres, const int32_t *idx,
-                            int64_t batch, int64_t n, int64_t m, int32_t nsample, int32_t cfeat,
-                            int32_t c1, int32_t c2, int32_t c3, const void *packed, float *out,
-                            int64_t out_stride, int64_t out_offset, void *stream);
-/* size in BYTES and host construction of the bf16 packed image */
-int64_t lidar_mlp_packed_size_bf16(int32_t cfeat, int32_t c1, int32_t c2, int32_t c3);
-int lidar_mlp_pack_bf16(int32_t cfeat, int32_t c1, int32_t c2, int32_t c3, const float *w1_host,
-                        const float *b1_host, const float *w2_host, const float *b2_host,
-                        const float *w3_host, const float *b3_host, void *packed_host);
-
 /* dense layer on MFMA: y (rows, cout) = relu(x (rows, k) W (k, cout) + b), fp32.
  * If pool_rows > 0: y is (rows / pool_rows, cout) = max over each run of pool_rows rows
  * (group_all's max-pool, fused); y must then be zeroed by the caller first.
@@ -161,21 +126,12 @@ int lidar_dense_f32(lidar_handle *h, const float *x, int64_t rows, int32_t k, co
                     const float *bias, int32_t cout, int32_t relu_on, int32_t pool_rows, float *y,
                     void *stream);
 
-/* lidar_dense_f32 on the bf16 matrix cores with fp32 arithmetic: operands split exactly into
- * bf16 hi + lo, products ah*bh + ah*bl + al*bh accumulated in fp32 (v_mfma_f32_32x32x16_bf16;
- * <= ~2^-15 per product).  Same shapes, epilogue and fused max-pool as lidar_dense_f32. */
-int lidar_dense_x3_f32(lidar_handle *h, const float *x, int64_t rows, int32_t k, const float *w,
-                       const float *bias, int32_t cout, int32_t relu_on, int32_t pool_rows, float *y,
-                       void *stream);
-
-/* the same GEMM on a weight image packed once (bf16 hi / lo MFMA B fragments; K padded to 32):
- * lidar_dense_x3_packed_size(k, cout) bytes, filled on the device by lidar_dense_x3_pack_f32
- * from W (k, cout) fp32.  lidar_dense_x3_f32 packs into the handle's workspace per call. */
+/* The x3 GEMM (fp32 arithmetic on the bf16 matrix cores: operands split exactly into bf16 hi +
+ * lo, products ah*bh + ah*bl + al*bh accumulated in fp32, <= ~2^-15 per product) runs on a
+ * weight image packed once: lidar_dense_x3_packed_size(k, cout) bytes, filled on the device by
+ * lidar_dense_x3_pack_f32 from W (k, cout) fp32 (bf16 hi / lo MFMA B fragments, K padded to 32). */
 int64_t lidar_dense_x3_packed_size(int32_t k, int32_t cout);
 int lidar_dense_x3_pack_f32(lidar_handle *h, const float *w, int32_t k, int32_t cout, void *packed, void *stream);
-int lidar_dense_x3p_f32(lidar_handle *h, const float *x, int64_t rows, int32_t k, const void *packed,
-                        const float *bias, int32_t cout, int32_t relu_on, int32_t pool_rows, float *y,
-                        void *stream);
 
 /* the x3 GEMM on pre-split activations ("split planes", csrc/dense_x3s.hip): a_planes holds
  * two bf16 planes (hi = bf16(x), lo = bf16(x - hi)) of row-major (rows, lda) elements, the lo
@@ -213,23 +169,16 @@ int lidar_sa_group_mlp_x1_f32(lidar_handle *h, int32_t layer1_mode, const float 
                               int64_t m, int32_t nsample, int32_t c1, int32_t c2, int32_t c3, const void *packed,
                               float *out, int64_t out_stride, int64_t out_offset, void *stream);
 
-/* lidar_sa_group_mlp_f32 with layer 1 applied per point beforehand: p (batch*n, p_stride)
- * = [f, x] W1 + b1 for every point of the level, q (batch*m, p_stride) = centre W1_xyz
- * (both via lidar_dense_f32, relu_on = 0, columns >= c1 ignored); a grouped row's layer 1
- * is relu(p[k] - q[c]).  packed is
- * the lidar_mlp_pack_f32 image of the whole branch (cfeat locates its layer-2 block).
- * Same outputs as lidar_sa_group_mlp_f32 up to fp32 re-association. */
-int lidar_sa_group_mlp_pre_f32(lidar_handle *h, const float *p, int64_t p_stride, const float *q,
-                               const int32_t *idx, int64_t batch, int64_t n, int64_t m,
-                               int32_t nsample, int32_t cfeat, int32_t c1, int32_t c2, int32_t c3,
-                               const float *packed, float *out, int64_t out_stride,
-                               int64_t out_offset, void *stream);
-
-/* 16-row variants of the fused SetAbstraction branch (v_mfma_f32_16x16x4_f32, ~half the
- * registers of the 32-row kernels, so more waves per SIMD beside co-resident FPS work).
- * xyz_level != 0: p = xyz (batch*n, 3), q = centres (batch*m, 3), layer 1 runs in-kernel
- * (replaces the cfeat = 0 case of lidar_sa_group_mlp_f32); xyz_level = 0: p / q are the
- * per-point / per-centre layer-1 rows of lidar_sa_group_mlp_pre_f32 (row stride p_stride).
+/* Grouped shared MLP (3 layers, BN folded, ReLU) + max-pool over nsample for one SA branch,
+ * fused with the grouping gather, on the native fp32 matrix cores (v_mfma_f32_16x16x4_f32,
+ * 16 grouped rows per wave; the strict-fp32 path):
+ *   row (b, c, s) = [xyz[b, idx[b,c,s]] - centres[b,c], feats[b, idx[b,c,s]]]
+ *   out[b, c, out_offset + j] = max_s relu(...relu(row W1 + b1)... W3 + b3)[j]
+ * xyz_level != 0 (a level without features): p = xyz (batch*n, 3), q = centres (batch*m, 3),
+ * layer 1 runs in-kernel.  xyz_level = 0: layer 1 was applied per point beforehand — p
+ * (batch*n, p_stride) = [f, x] W1 + b1 for every point of the level, q (batch*m, p_stride) =
+ * centre W1_xyz (lidar_dense_f32 / lidar_dense_x3f_f32, relu off); a grouped row's layer 1 is
+ * relu(p[k] - q[c]).
  * packed: the lidar_mlp_pack16_f32 image of lidar_mlp_packed_size16 floats (w1 is read only
  * for an xyz level: its 3 xyz rows).  Same outputs up to fp32 re-association. */
 int64_t lidar_mlp_packed_size16(int32_t xyz_level, int32_t c1, int32_t c2, int32_t c3);
@@ -349,6 +298,21 @@ int lidar_preprocess_eps_batch_f64(lidar_handle *h, const double *xyz, const int
 int lidar_cell_radius_density_f64(lidar_handle *h, const double *people, int64_t k, const double *xg,
                                   int64_t nxg, const double *yg, int64_t nyg, double r, double divisor,
                                   double *out, void *stream);
+
+/* Optional global density over a FIXED venue grid (the reference derives its grid
+ * per frame, models/crowd_density_model.py:49-54): counts (nx, ny) int32 += the histogram2d of
+ * people (k, 2) over calculate_grid_density's edges (utils/data_processing.py:305-319:
+ * np.arange(x0, ., grid) with x0 = x_min - 2 grid, searchsorted right, the last edge closed,
+ * outside dropped).  Counts add, so the frames of a rank and then (one RCCL all-reduce, int32
+ * sum) the ranks accumulate; counts / grid^2 is calculate_grid_density of all their people. */
+int lidar_venue_counts_f64(lidar_handle *h, const double *people, int64_t k, double x0, double y0, double grid,
+                           int64_t nx, int64_t ny, int32_t *counts, void *stream);
+
+/* downsample_point_cloud's gather (utils/data_processing.py:247-249): dst[r] = src[idx[r]] for k
+ * rows of row_bytes bytes each (any dtype: rows are moved as raw bytes); idx (k) int64 device,
+ * the indices the host drew from the global legacy NumPy RNG (out-of-range indices skipped). */
+int lidar_gather_rows(lidar_handle *h, const void *src, int64_t n_rows, int64_t row_bytes, const int64_t *idx,
+                      int64_t k, void *dst, void *stream);
 
 /* ---- models/crowd_flow_model.py, HOST code (host pointers): the
  * model's deciding arithmetic is glibc sin / cos / pow and sklearn's KD-tree traversal,

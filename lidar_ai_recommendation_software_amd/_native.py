@@ -42,6 +42,10 @@ SIGNATURES = {
     "lidar_reserve": [P, ctypes.c_uint64],
     "lidar_last_error": [],
     "lidar_version": [],
+    "lidar_profile": [P, I32],
+    "lidar_profile_read": [P, P, I64, P, I64, P],
+    "lidar_gather_rows": [P, P, I64, I64, P, I64, P, P],
+    "lidar_venue_counts_f64": [P, P, I64, F64, F64, F64, I64, I64, P, P],
     "lidar_fps_f32": [P, P, I64, I64, I64, P, P, P, P, P],
     "lidar_fps_ex_f32": [P, P, I64, I64, I64, P, P, P, P, I32, P],
     "lidar_ball_query_f32": [P, P, P, I64, I64, I64, F32, I32, P, P],
@@ -49,20 +53,10 @@ SIGNATURES = {
     "lidar_ball_query_grid_bytes": [I64, I64],
     "lidar_ball_query_bin_f32": [P, P, I64, I64, F32, I32, P, P],
     "lidar_ball_query_binned_f32": [P, P, P, P, I64, I64, I64, F32, I32, P, P],
-    "lidar_sa_group_mlp_f32": [P, P, P, I64, P, P, I64, I64, I64, I32, I32, I32, I32, I32, P, P,
-                               I64, I64, P],
-    "lidar_mlp_packed_size": [I32, I32, I32, I32],
-    "lidar_mlp_pack_f32": [I32, I32, I32, I32, P, P, P, P, P, P, P],
-    "lidar_sa_group_mlp_bf16": [P, P, P, I64, P, P, I64, I64, I64, I32, I32, I32, I32, I32, P, P,
-                                I64, I64, P],
-    "lidar_mlp_packed_size_bf16": [I32, I32, I32, I32],
-    "lidar_mlp_pack_bf16": [I32, I32, I32, I32, P, P, P, P, P, P, P],
     "lidar_dense_relu_f32": [P, P, I64, I32, P, P, I32, I32, P, P],
     "lidar_dense_f32": [P, P, I64, I32, P, P, I32, I32, I32, P, P],
-    "lidar_dense_x3_f32": [P, P, I64, I32, P, P, I32, I32, I32, P, P],
     "lidar_dense_x3_packed_size": [I32, I32],
     "lidar_dense_x3_pack_f32": [P, P, I32, I32, P, P],
-    "lidar_dense_x3p_f32": [P, P, I64, I32, P, P, I32, I32, I32, P, P],
     "lidar_dense_x3s_f32": [P, P, I64, I32, I64, I32, P, P, I32, I32, I32, I32, P, I64, I64, P],
     "lidar_split_x3_f32": [P, P, I64, I32, I64, P, I64, I32, P],
     "lidar_dense_x3f_f32": [P, P, I32, I64, I32, P, P, I32, I32, I32, I32, P, I64, I64, P],
@@ -76,11 +70,6 @@ SIGNATURES = {
     "lidar_mlp_packed_size_x3": [I32, I32, I32, I32],
     "lidar_mlp_pack_x3_f32": [I32, I32, I32, I32, P, P, P, P, P, P, P],
     "lidar_sa_group_mlp_x3_f32": [P, I32, P, I64, P, P, I64, I64, I64, I32, I32, I32, I32, P, P, I64, I64, P],
-    "lidar_stream_create_cu_mask": [I32, P, I32, P],
-    "lidar_stream_destroy": [P],
-    "lidar_device_cu_count": [I32, P],
-    "lidar_sa_group_mlp_pre_f32": [P, P, I64, P, P, I64, I64, I64, I32, I32, I32, I32, I32, P, P,
-                                   I64, I64, P],
     "lidar_concat_xyz_pad_f32": [P, P, I64, P, I64, I64, P],
     "lidar_voxel_downsample_f32": [P, P, I64, F32, P, P, P, P, P],
     "lidar_voxel_batch_workspace_bytes": [I64, I64],
@@ -102,8 +91,7 @@ SIGNATURES = {
     "lidar_grid_dims": [F64, F64, F64, F64, F64, P, P],
     "lidar_density_grid_f64": [P, P, I64, F64, F64, F64, F64, F64, I64, I64, P, P, P, P],
 }
-_RESTYPES = {"lidar_last_error": ctypes.c_char_p, "lidar_mlp_packed_size": I64,
-             "lidar_mlp_packed_size_bf16": I64,
+_RESTYPES = {"lidar_last_error": ctypes.c_char_p,
              "lidar_mlp_packed_size16": I64, "lidar_mlp_packed_size_x3": I64,
              "lidar_ball_query_grid_bytes": ctypes.c_uint64,
              "lidar_dense_x3_packed_size": I64, "lidar_mlp_packed_size_x1": I64,
@@ -184,3 +172,17 @@ def ptr(t):
 def call(name, *args):
     lib = load_library()
     check(getattr(lib, name)(*args), name)
+
+
+def profile(h, enable):
+    """Start (True) or stop (False) per-phase HIP-event timing of handle h (lidar_profile)."""
+    call("lidar_profile", h, 1 if enable else 0)
+
+
+def profile_read(h, cap=4096):
+    """[(phase name, ms)] recorded on h since the last read, in launch order (waits for them)."""
+    names = ctypes.create_string_buffer(64 * cap)
+    ms = (ctypes.c_float * cap)()
+    n = I64(0)
+    call("lidar_profile_read", h, names, len(names), ms, cap, ctypes.byref(n))
+    return list(zip(names.value.decode().split("\n")[: n.value], ms[: n.value]))

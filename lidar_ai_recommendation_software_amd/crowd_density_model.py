@@ -51,18 +51,24 @@ class CrowdDensityModel:
             res["backbone_feature"] = self.encode(processed_data["points"])
         return res
 
+    @staticmethod
+    def normalise(points):
+        """The backbone's input: the frame centred on its bounding box and scaled so that the
+        box's longest side spans [-1, 1] (fp32; the SA radii 0.2 / 0.4 are in these units)."""
+        p = np.asarray(points, dtype=np.float64)
+        lo, hi = p.min(axis=0), p.max(axis=0)
+        return ((p - (lo + hi) / 2) / max(float((hi - lo).max()) / 2, 1e-9)).astype(np.float32)
+
     def encode(self, points):
-        """PointNet++ (SSG/MSG) global feature of one frame, points normalised to the unit
-        cube by their bounding box.  Not part of the reference."""
+        """PointNet++ (SSG/MSG) global feature of one frame over ALL its points (any N >= 1;
+        SA levels take max(1, N/16) and max(1, N/64) centres).  Not part of the reference
+        (SURVEY §8a N6)."""
         import torch
         from . import pointnet2 as pn
         if self._net is None:
             self._net = pn.PointNet2Backbone(pn.CONFIGS[self.backbone], device="cuda")
-        p = np.asarray(points, dtype=np.float64)
-        lo, hi = p.min(axis=0), p.max(axis=0)
-        unit = ((p - (lo + hi) / 2) / max(float((hi - lo).max()) / 2, 1e-9)).astype(np.float32)
-        n = len(unit) // 64 * 64
-        g, _ = self._net.forward(torch.from_numpy(np.ascontiguousarray(unit[:n]))[None].cuda())
+        unit = self.normalise(points)
+        g, _ = self._net.forward(torch.from_numpy(np.ascontiguousarray(unit))[None].cuda())
         return g[0].cpu().numpy()
 
     def calculate_risk_level(self, density):

@@ -118,14 +118,8 @@ struct BqGrid {  // per frame, written by bq_bin_kernel
     int pad[2];
 };
 
-// per frame: BqGrid (64 B) | tab[kTab + 64] | sorted float4[n] | cursors[kTab] + bbox keys[16]
-// (the last two are scratch of the split binning path)
+// per frame: BqGrid (64 B) | tab[kTab + 64] | sorted float4[n]
 __host__ __device__ constexpr uint64_t grid_frame_bytes(int64_t n)
-{
-    return 64 + (uint64_t)(kTab + 64) * 4 + (uint64_t)n * 16 + (uint64_t)(kTab + 16) * 4;
-}
-
-__host__ __device__ constexpr uint64_t grid_scratch_offset(int64_t n)
 {
     return 64 + (uint64_t)(kTab + 64) * 4 + (uint64_t)n * 16;
 }
@@ -296,169 +290,6 @@ __global__ __launch_bounds__(1024) void bq_bin_kernel(const float *__restrict__ 
     }
 }
 
-// ---- split binning: the same grid built by five chip-wide kernels with ~no LDS, so that the
-// side-stream binning does not hold 66 KiB of a CU's LDS next to the MFMA levels.  Slot
-// order inside a (window, cell) range differs from bq_bin_kernel's (both come from atomics);
-// bq_grid_kernel ranks candidates by index, so the query results are identical.
-constexpr int kSplitPts = 1024;  // points per 256-thread block
-
-__device__ __forceinline__ uint32_t ord_key(float f)
-{
-    const uint32_t u = __float_as_uint(f);
-    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-}
-
-__device__ __forceinline__ float ord_val(uint32_t k)
-{
-    return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
-}
-
-__global__ __launch_bounds__(1024) void bqs_init_kernel(int n, char *__restrict__ grid_ws)
-{
-    char *fw = grid_ws + (int64_t)blockIdx.x * grid_frame_bytes(n);
-    int *tab = reinterpret_cast<int *>(fw + 64);
-    uint32_t *bb = reinterpret_cast<uint32_t *>(fw + grid_scratch_offset(n)) + kTab;
-    for (int i = threadIdx.x; i < kTab; i += 1024) tab[i] = 0;
-    if (threadIdx.x < 6) bb[threadIdx.x] = threadIdx.x < 3 ? 0xffffffffu : 0u;
-}
-
-__global__ __launch_bounds__(256) void bqs_bbox_kernel(const float *__restrict__ xyz, int n,
-                                                       char *__restrict__ grid_ws)
-{
-    __shared__ float red[6][4];
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int64_t b = blockIdx.y;
-    const float *p = xyz + b * (int64_t)n * 3;
-    float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
-    const int k0 = blockIdx.x * kSplitPts, k1 = min(n, k0 + kSplitPts);
-    for (int k = k0 + tid; k < k1; k += 256) {
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            const float v = p[3 * (int64_t)k + a];
-            if (fabsf(v) <= 3.4e38f) {
-                mn[a] = fminf(mn[a], v);
-                mx[a] = fmaxf(mx[a], v);
-            }
-        }
-    }
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        mn[a] = lidar::wave_min_f(mn[a]);
-        mx[a] = lidar::wave_max_f(mx[a]);
-    }
-    if (lane == 0)
-        for (int a = 0; a < 3; ++a) {
-            red[a][wid] = mn[a];
-            red[3 + a][wid] = mx[a];
-        }
-    __syncthreads();
-    if (tid < 6) {
-        const bool lo = tid < 3;
-        float v = red[tid][0];
-        for (int w = 1; w < 4; ++w) v = lo ? fminf(v, red[tid][w]) : fmaxf(v, red[tid][w]);
-        if (fabsf(v) <= 3.4e38f) {  // this block saw a finite value on the axis
-            uint32_t *bb = reinterpret_cast<uint32_t *>(grid_ws + b * grid_frame_bytes(n) +
-                                                        grid_scratch_offset(n)) + kTab;
-            if (lo) atomicMin(&bb[tid], ord_key(v));
-            else atomicMax(&bb[tid], ord_key(v));
-        }
-    }
-}
-
-// grid parameters (recomputed per block from the frame's bbox keys: a few scalar
-// iterations), then one global atomic per point on its slot counter
-__device__ __forceinline__ BqGrid split_params(const char *fw, int n, float r, int ns)
-{
-    const uint32_t *bb = reinterpret_cast<const uint32_t *>(fw + grid_scratch_offset(n)) + kTab;
-    float mn[3], mx[3];
-    for (int a = 0; a < 3; ++a) {
-        const uint32_t kl = bb[a], kh = bb[3 + a];
-        mn[a] = kl == 0xffffffffu ? INFINITY : ord_val(kl);
-        mx[a] = kh == 0u ? -INFINITY : ord_val(kh);
-    }
-    return bin_params(mn, mx, n, r, ns);
-}
-
-__global__ __launch_bounds__(256) void bqs_count_kernel(const float *__restrict__ xyz, int n, float r, int ns,
-                                                        char *__restrict__ grid_ws)
-{
-    __shared__ BqGrid gs;
-    const int64_t b = blockIdx.y;
-    char *fw = grid_ws + b * grid_frame_bytes(n);
-    if (threadIdx.x == 0) {
-        gs = split_params(fw, n, r, ns);
-        if (blockIdx.x == 0) *reinterpret_cast<BqGrid *>(fw) = gs;
-    }
-    __syncthreads();
-    const BqGrid g = gs;
-    const float *p = xyz + b * (int64_t)n * 3;
-    int *tab = reinterpret_cast<int *>(fw + 64);
-    const int k0 = blockIdx.x * kSplitPts, k1 = min(n, k0 + kSplitPts);
-    for (int k = k0 + threadIdx.x; k < k1; k += 256) {
-        const float *q = p + 3 * (int64_t)k;
-        atomicAdd(&tab[point_slot(q[0], q[1], q[2], k, g)], 1);
-    }
-}
-
-// exclusive scan of one frame's kTab counters in place (16 per thread); cursors = bases
-__global__ __launch_bounds__(1024) void bqs_scan_kernel(int n, char *__restrict__ grid_ws)
-{
-    __shared__ int wsum[16];
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    char *fw = grid_ws + (int64_t)blockIdx.x * grid_frame_bytes(n);
-    int *tab = reinterpret_cast<int *>(fw + 64);
-    int *cur = reinterpret_cast<int *>(fw + grid_scratch_offset(n));
-    int4 v[4];
-    const int4 *t4 = reinterpret_cast<const int4 *>(tab) + tid * 4;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = t4[j];
-    int *loc = reinterpret_cast<int *>(v);
-    int sum = 0;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) sum += loc[j];
-    int incl = sum;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const int u = __shfl_up(incl, d, 64);
-        if (lane >= d) incl += u;
-    }
-    if (lane == 63) wsum[wid] = incl;
-    __syncthreads();
-    int base = incl - sum;
-    for (int w = 0; w < wid; ++w) base += wsum[w];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        const int c = loc[j];
-        loc[j] = base;
-        base += c;
-    }
-    int4 *o4 = reinterpret_cast<int4 *>(tab) + tid * 4, *c4 = reinterpret_cast<int4 *>(cur) + tid * 4;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        o4[j] = v[j];
-        c4[j] = v[j];
-    }
-    if (tid == 1023) tab[kTab] = base;  // == n
-}
-
-__global__ __launch_bounds__(256) void bqs_scatter_kernel(const float *__restrict__ xyz, int n,
-                                                          char *__restrict__ grid_ws)
-{
-    const int64_t b = blockIdx.y;
-    char *fw = grid_ws + b * grid_frame_bytes(n);
-    const BqGrid g = *reinterpret_cast<const BqGrid *>(fw);
-    int *cur = reinterpret_cast<int *>(fw + grid_scratch_offset(n));
-    float4 *sorted = reinterpret_cast<float4 *>(fw + 64 + (kTab + 64) * 4);
-    const float *p = xyz + b * (int64_t)n * 3;
-    const int k0 = blockIdx.x * kSplitPts, k1 = min(n, k0 + kSplitPts);
-    for (int k = k0 + threadIdx.x; k < k1; k += 256) {
-        const float *q = p + 3 * (int64_t)k;
-        const float x = q[0], y = q[1], z = q[2];
-        const int pos = atomicAdd(&cur[point_slot(x, y, z, k, g)], 1);
-        sorted[pos] = make_float4(x, y, z, __int_as_float(k));
-    }
-}
-
 // index-order scan of points [lo, hi) for one centre (a window with too many candidates)
 __device__ __forceinline__ void scan_range(const float *__restrict__ p, int lo, int hi, float cx, float cy,
                                            float cz, float r2, int ns, int lane, uint64_t below, int &cnt,
@@ -605,18 +436,6 @@ __global__ __launch_bounds__(256) void bq_grid_kernel(const float *__restrict__ 
 static int launch_bin(const float *xyz, int64_t batch, int64_t n, float radius, int32_t nsample,
                       char *grid, hipStream_t st)
 {
-    const char *sp = getenv("LIDAR_BQ_BIN_SPLIT");  // A/B knob: 1 = five low-LDS kernels
-    if (sp && sp[0] == '1') {
-        const dim3 g2((unsigned)((n + kSplitPts - 1) / kSplitPts), (unsigned)batch);
-        REQUIRE(batch <= 65535, "ball query bin: batch exceeds the split grid");
-        hipLaunchKernelGGL(bqs_init_kernel, dim3((unsigned)batch), dim3(1024), 0, st, (int)n, grid);
-        hipLaunchKernelGGL(bqs_bbox_kernel, g2, dim3(256), 0, st, xyz, (int)n, grid);
-        hipLaunchKernelGGL(bqs_count_kernel, g2, dim3(256), 0, st, xyz, (int)n, radius, (int)nsample, grid);
-        hipLaunchKernelGGL(bqs_scan_kernel, dim3((unsigned)batch), dim3(1024), 0, st, (int)n, grid);
-        hipLaunchKernelGGL(bqs_scatter_kernel, g2, dim3(256), 0, st, xyz, (int)n, grid);
-        LAUNCH_CHECK();
-        return LIDAR_OK;
-    }
     hipLaunchKernelGGL(bq_bin_kernel, dim3((unsigned)batch), dim3(1024), 0, st, xyz, (int)n, radius,
                        (int)nsample, grid);
     LAUNCH_CHECK();
@@ -667,7 +486,7 @@ LIDAR_EXPORT int lidar_ball_query_mode_f32(lidar_handle *h, const float *xyz, co
     BQ_CHECK_ARGS("lidar_ball_query_f32");
     REQUIRE(mode >= 0 && mode <= 2, "lidar_ball_query_mode_f32: mode is 0 (auto), 1 (scan) or 2 (grid)");
     if (batch * m == 0) return LIDAR_OK;
-    HIP_TRY(hipSetDevice(h->device));
+    ON_DEVICE(h->device);
     hipStream_t st = static_cast<hipStream_t>(stream);
     const float r2 = radius * radius;
     const bool grid = mode == 2 || (mode == 0 && n >= kGridMinN);
@@ -694,7 +513,7 @@ LIDAR_EXPORT int lidar_ball_query_bin_f32(lidar_handle *h, const float *xyz, int
             "lidar_ball_query_bin_f32: bad sizes");
     REQUIRE(radius >= 0.0f, "lidar_ball_query_bin_f32: negative radius");
     if (batch == 0) return LIDAR_OK;
-    HIP_TRY(hipSetDevice(h->device));
+    ON_DEVICE(h->device);
     return launch_bin(xyz, batch, n, radius, nsample, static_cast<char *>(grid),
                       static_cast<hipStream_t>(stream));
 }
@@ -706,7 +525,7 @@ LIDAR_EXPORT int lidar_ball_query_binned_f32(lidar_handle *h, const float *xyz, 
     BQ_CHECK_ARGS("lidar_ball_query_binned_f32");
     REQUIRE(grid, "lidar_ball_query_binned_f32: null grid");
     if (batch * m == 0) return LIDAR_OK;
-    HIP_TRY(hipSetDevice(h->device));
+    ON_DEVICE(h->device);
     return launch_grid_query(xyz, static_cast<const char *>(grid), centres, batch, n, m, radius, nsample, idx,
                              static_cast<hipStream_t>(stream));
 }

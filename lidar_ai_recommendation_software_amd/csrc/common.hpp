@@ -5,22 +5,79 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string>
+#include <vector>
 
 #include "../../include/lidar_amd.h"
 
 #define LIDAR_EXPORT extern "C" __attribute__((visibility("default")))
+
+namespace lidar {
+// per-launch HIP events of a handle while lidar_profile is on (bench.py's in-window kernel times)
+struct Prof {
+    struct Rec {
+        const char *name;
+        hipEvent_t a, b;
+    };
+    std::vector<Rec> recs;
+};
+}  // namespace lidar
 
 struct lidar_handle {
     int device = 0;
     void *ws = nullptr;       // scratch workspace (device)
     uint64_t ws_bytes = 0;
     void *host_pinned = nullptr;  // small pinned host buffer for scalar read-backs
+    lidar::Prof *prof = nullptr;  // non-null while lidar_profile(h, 1) is on
 };
 
 namespace lidar {
 
 void set_error(const std::string &msg);
 int fail(int code, const std::string &msg);
+
+// Makes `device` current for the scope of one C-ABI call and restores the caller's device on
+// return: the library never changes the calling thread's current device as a side effect.
+struct DeviceScope {
+    int prev = -1;
+    hipError_t rc = hipSuccess;
+    explicit DeviceScope(int device)
+    {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != device) rc = hipSetDevice(device);
+    }
+    ~DeviceScope()
+    {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+// Brackets the launches issued in its scope with two HIP events on `s` when the handle is
+// profiling (one record per span, read back by lidar_profile_read); free otherwise.
+struct Span {
+    Prof *p;
+    const char *name;
+    hipStream_t s;
+    hipEvent_t a = nullptr;
+    Span(lidar_handle *h, const char *n, hipStream_t st) : p(h ? h->prof : nullptr), name(n), s(st)
+    {
+        if (p && hipEventCreate(&a) == hipSuccess && hipEventRecord(a, s) != hipSuccess) {
+            (void)hipEventDestroy(a);
+            a = nullptr;
+        }
+    }
+    ~Span()
+    {
+        if (!a) return;
+        hipEvent_t b = nullptr;
+        if (hipEventCreate(&b) == hipSuccess && hipEventRecord(b, s) == hipSuccess) {
+            p->recs.push_back({name, a, b});
+            return;
+        }
+        (void)hipEventDestroy(a);
+        if (b) (void)hipEventDestroy(b);
+    }
+};
 // grow the handle's workspace to `bytes`; returns device pointer or nullptr
 void *workspace(lidar_handle *h, uint64_t bytes);
 inline uint64_t align_up(uint64_t v, uint64_t a) { return (v + a - 1) / a * a; }
@@ -55,6 +112,12 @@ struct Carver {
     do {                                                                                   \
         if (!(cond)) return lidar::fail(LIDAR_EINVAL, msg);                                \
     } while (0)
+
+// the device of a C-ABI call for the rest of the enclosing scope (restored on return)
+#define ON_DEVICE(dev)                                                                     \
+    lidar::DeviceScope lidar_dev_scope_(dev);                                              \
+    if (lidar_dev_scope_.rc != hipSuccess)                                                 \
+    return lidar::fail(LIDAR_EHIP, std::string("hipSetDevice: ") + hipGetErrorString(lidar_dev_scope_.rc))
 
 // ----------------------------------------------------------------- device helpers
 namespace lidar {

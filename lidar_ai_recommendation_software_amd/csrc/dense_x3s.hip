@@ -1,20 +1,20 @@
-// dense_x3s.hip — the x3 dense GEMM on pre-split activations ("split planes").
+// dense_x3s.hip — the x3 dense GEMM (SA2's per-point layer 1, group_all's three layers).
 //
-// dense_x3.hip splits every fp32 activation into bf16 hi / lo inside the GEMM loop: each
-// element is split once per wave that reads it (2 per workgroup) and once per column tile
-// of the grid (cout / 128 workgroups), ~4 VALU per MFMA, which left the MFMA pipe ~30 % busy.
-// Here the activations arrive split: two bf16 planes (hi, lo) of row-major (rows, lda)
+// Splitting every fp32 activation into bf16 hi / lo inside the GEMM loop costs each element one
+// split per wave that reads it and per column tile of the grid (~4 VALU per MFMA, which left the
+// MFMA pipe ~30 % busy in round 1's first x3 GEMM).  Here the activations arrive split: two bf16
+// planes (hi, lo) of row-major (rows, lda)
 // elements, lda a multiple of 32, elements k >= K zero — written once, by the producing
 // layer's epilogue (mode 1 below) or by lidar_split_x3_f32 from fp32 rows.  A product is still
 // ah*bh + ah*bl + al*bh on v_mfma_f32_32x32x16_bf16 with fp32 accumulation (the x3 contract of
-// DESIGN.md §3), so results equal dense_x3's up to the accumulation order.
+// DESIGN.md §3), so results are the x3 contract's up to the accumulation order.
 //
 // Tile: 128 rows x 128 output channels per 4-wave workgroup (64 x 64 per wave = 2 x 2 MFMA
 // tiles), K in stages of 32 double-buffered in LDS by global_load_lds:
 //   A stage: per plane 128 rows x 64 B; row r's 16-byte chunk q (8 consecutive k) sits at slot
 //            q ^ ((r >> 2) & 3), so the fragment reads (ds_read_b128, 32 consecutive rows, one
 //            chunk) hit 16 distinct 16-byte bank groups per 16 lanes;
-//   B stage: dense_x3.hip's packed weight fragments (lidar_dense_x3_pack_f32), read lane-linear.
+//   B stage: x3_pack.hip's packed weight fragments (lidar_dense_x3_pack_f32), read lane-linear.
 // Output modes:
 //   0 fp32 rows (rows, ldo) [+ ReLU]             — computed transposed (D = W^T X^T): a lane
 //   1 split planes (rows, ldo) x 2 [+ ReLU]        holds 4 consecutive channels of one row, so
@@ -64,7 +64,7 @@ __device__ __forceinline__ void split8(const f32x4 &a0, const f32x4 &a1, bf16x8 
 // MODE 0 / 1 / 2 as in the header.  AF32: A is fp32 rows (rows, lda) instead of split planes
 // (a layer whose input nobody split, e.g. the first of a chain: the A stage holds 128 rows x
 // 32 fp32 with row r's chunk q at slot q ^ ((r >> 1) & 7), and each wave splits the fragments
-// it reads — dense_x3.hip's loop; worth it where cout / 128 column tiles re-read little)
+// it reads; worth it where cout / 128 column tiles re-read little)
 // X1: one product ah*bh per MFMA — bf16(x) bf16(w) with fp32 accumulation, the bf16 spec's
 // arithmetic (BASELINE configs[4]), on the same operands
 template <int MODE, bool AF32, bool X1 = false>
@@ -272,7 +272,7 @@ static int dense_x3s_launch(lidar_handle *h, const void *a_planes, int64_t a_pla
     REQUIRE(mode != 2 || (relu_on && pool_rows > 0 && pool_rows % SBM == 0 && rows % pool_rows == 0),
             "lidar_dense_x3s_f32: the max-pool needs relu and pool_rows a multiple of 128 dividing rows");
     if (rows == 0) return LIDAR_OK;
-    HIP_TRY(hipSetDevice(h->device));
+    ON_DEVICE(h->device);
     const int ks = (k + SBK - 1) / SBK * 2;  // the packed image of a (k, cout) layer covers ceil(k/32)*2 k-steps
     const int ntn = cout / SBN;
     const int64_t total = (rows / SBM) * ntn, per_xcd = (total + 7) / 8;
@@ -325,7 +325,7 @@ LIDAR_EXPORT int lidar_split_x3_f32(lidar_handle *h, const float *x, int64_t row
     REQUIRE(rows >= 0 && k > 0 && ldx >= k && lda >= k && lda % 8 == 0 && plane >= rows * lda,
             "lidar_split_x3_f32: bad sizes");
     if (rows == 0) return LIDAR_OK;
-    HIP_TRY(hipSetDevice(h->device));
+    ON_DEVICE(h->device);
     const int64_t n = rows * (lda / 8);
     hipLaunchKernelGGL(split_x3_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, static_cast<hipStream_t>(stream),
                        x, rows, (int)k, ldx, static_cast<__bf16 *>(planes), plane, (int)lda);

@@ -548,9 +548,10 @@ __global__ __launch_bounds__(kT) void preprocess_kernel(const double *__restrict
 
 // ------------------------------------------------------------------ DBSCAN
 // params (double) P: [0] n, [1] eps, [2..4] lo, [5..7] hi, [8] cell, [9..11] dims,
-// [12] ncell, [13] clusters, [14] active (n > 10 for the preprocess path)
+// [12] ncell, [13] clusters, [14] active (n > 10 for the preprocess path), [15] stencil radius
+// R in cells (1 or 2), [16] same-cell shortcut (1: cells of side eps/sqrt(3), see dbscan_setup)
 enum : int { P_N = 0, P_EPS = 1, P_LO = 2, P_HI = 5, P_CELL = 8, P_DIM = 9, P_NCELL = 12,
-             P_NCLUST = 13, P_ACTIVE = 14, P_COUNT = 16 };
+             P_NCLUST = 13, P_ACTIVE = 14, P_R = 15, P_INTRA = 16, P_COUNT = 20 };
 
 __global__ void dbscan_params_from_preprocess(const double *S_in, double *P_in, int64_t max_cells, FrameMap fm)
 {
@@ -588,29 +589,40 @@ __global__ __launch_bounds__(kT) void dbscan_bbox_kernel(const double *x_in, dou
     }
 }
 
+// Cell side.  Preferred: s = eps / sqrt(3) * (1 - 2^-20) ("fine" cells).  Any two points of one
+// fine cell are eps-neighbours under the fp64 test: the cell coordinate floor((v - lo) / s) of a
+// point inside the bbox carries < 2^-29 relative rounding at < 2^22 cells per axis, so the per-axis
+// gaps inside a cell stay below s (1 + 2^-29), and the computed ((dx*dx + dy*dy) + dz*dz) below
+// 3 s^2 (1 + 2^-26) < eps*eps (1 - 2^-20); a neighbour lies at most ceil(eps / s) = 2 cells away
+// per axis (R = 2).  When the fine grid exceeds the cell cap: cells strictly larger than eps
+// (R = 1, no same-cell shortcut), grown by 1.5 until they fit.
 __global__ void dbscan_setup_kernel(double *P_in, int64_t max_cells, FrameMap fm)
 {
     if (threadIdx.x) return;
     double *P = fm.ws(P_in);
-    const double n = P[P_N];
-    double dims[3] = {1.0, 1.0, 1.0}, tot = 1.0;
-    // cells strictly larger than eps: a 27-cell stencil sees every pair the fp64 test accepts
-    double cell = P[P_EPS] * (1.0 + 1.0 / 1048576.0);
-    if (P[P_ACTIVE] == 0.0 || !(cell > 0.0) || !(cell < INFINITY)) {
-        P[P_ACTIVE] = 0.0;
-        cell = 1.0;
-    } else {
-        const double cap = fmin(4.0 * n + 64.0, (double)max_cells);
-        bool fit = false;
-        for (int it = 0; it < 256 && !fit; ++it) {  // bounded: 1.5^256 covers any finite box
-            tot = 1.0;
-            for (int c = 0; c < 3; ++c) {
-                dims[c] = floor((P[P_HI + c] - P[P_LO + c]) / cell) + 1.0;
-                tot *= dims[c];
-            }
-            fit = tot <= cap;
-            if (!fit) cell *= 1.5;
+    const double n = P[P_N], eps = P[P_EPS];
+    const double cap = fmin(8.0 * n + 64.0, (double)max_cells);
+    double dims[3] = {1.0, 1.0, 1.0}, tot = 1.0, cell = 1.0, R = 1.0, intra = 0.0;
+    auto fits = [&](double c) {
+        tot = 1.0;
+        for (int k = 0; k < 3; ++k) {
+            dims[k] = floor((P[P_HI + k] - P[P_LO + k]) / c) + 1.0;
+            tot *= dims[k];
         }
+        return tot <= cap;  // a non-finite box never fits
+    };
+    const double fine = eps / sqrt(3.0) * (1.0 - 1.0 / 1048576.0);
+    if (P[P_ACTIVE] == 0.0 || !(eps > 0.0) || !(eps < INFINITY)) {
+        P[P_ACTIVE] = 0.0;
+    } else if (fits(fine)) {
+        cell = fine;
+        R = 2.0;
+        intra = 1.0;
+    } else {
+        // cells strictly larger than eps: a 27-cell stencil sees every pair the fp64 test accepts
+        cell = eps * (1.0 + 1.0 / 1048576.0);
+        bool fit = false;
+        for (int it = 0; it < 256 && !(fit = fits(cell)); ++it) cell *= 1.5;  // bounded: 1.5^256
         if (!fit) {  // non-finite box: one cell (still exact, only slower)
             dims[0] = dims[1] = dims[2] = 1.0;
             tot = 1.0;
@@ -620,6 +632,8 @@ __global__ void dbscan_setup_kernel(double *P_in, int64_t max_cells, FrameMap fm
     P[P_CELL] = cell;
     for (int c = 0; c < 3; ++c) P[P_DIM + c] = dims[c];
     P[P_NCELL] = tot;
+    P[P_R] = R;
+    P[P_INTRA] = intra;
 }
 
 __device__ __forceinline__ int64_t cell_coord(double v, double lo, double cell, int64_t dim)
@@ -631,6 +645,8 @@ __device__ __forceinline__ int64_t cell_coord(double v, double lo, double cell, 
 struct Grid {
     double lo[3], cell, eps2;
     int64_t dim[3], n;
+    int R;       // stencil radius in cells per axis
+    bool intra;  // fine cells: any two points of one cell are neighbours
     __device__ void load(const double *P)
     {
         for (int c = 0; c < 3; ++c) {
@@ -640,6 +656,8 @@ struct Grid {
         cell = P[P_CELL];
         eps2 = dmul(P[P_EPS], P[P_EPS]);
         n = (int64_t)P[P_N];
+        R = (int)P[P_R];
+        intra = P[P_INTRA] != 0.0;
     }
     __device__ int64_t cid(const double *p) const
     {
@@ -648,13 +666,13 @@ struct Grid {
     }
 };
 
-__global__ void zero_u32_kernel(uint32_t *a_in, const double *P_in, int idx, int64_t extra, FrameMap fm)
+__global__ void fill_u32_kernel(uint32_t *a_in, const double *P_in, int idx, int64_t extra, uint32_t v, FrameMap fm)
 {
     uint32_t *a = fm.ws(a_in);
     const double *P = fm.ws(P_in);
     const int64_t n = (int64_t)P[idx] + extra;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-        a[i] = 0;
+        a[i] = v;
 }
 
 __global__ void dbscan_cells_kernel(const double *x_in, const double *P_in, uint32_t *cid_in, uint32_t *cellcnt_in,
@@ -789,20 +807,20 @@ __global__ void copy_u32_kernel(uint32_t *dst_in, const uint32_t *src_in, const 
         dst[i] = src[i];
 }
 
-// visit every sorted slot u whose point is within eps of point (px,py,pz) in cell c
+// visit every sorted slot u whose point is within eps of point (px,py,pz) in cell c: the
+// (2R+1)^2 columns around c, each a contiguous z-run of 2R+1 cells in the sorted order
 template <class F>
 __device__ __forceinline__ void for_neighbours(const Grid &g, const uint32_t *start, const double *sxyz,
                                                double px, double py, double pz, uint32_t c, F &&f)
 {
     const int64_t cz = c % g.dim[2], cy = (c / g.dim[2]) % g.dim[1], cx = c / (g.dim[2] * g.dim[1]);
-    for (int64_t X = cx - 1; X <= cx + 1; ++X) {
+    const int64_t z0 = cz - g.R > 0 ? cz - g.R : 0, z1 = cz + g.R < g.dim[2] ? cz + g.R : g.dim[2] - 1;
+    for (int64_t X = cx - g.R; X <= cx + g.R; ++X) {
         if (X < 0 || X >= g.dim[0]) continue;
-        for (int64_t Y = cy - 1; Y <= cy + 1; ++Y) {
+        for (int64_t Y = cy - g.R; Y <= cy + g.R; ++Y) {
             if (Y < 0 || Y >= g.dim[1]) continue;
-            const int64_t z0 = cz > 0 ? cz - 1 : 0, z1 = cz + 1 < g.dim[2] ? cz + 1 : g.dim[2] - 1;
-            // cells (X, Y, z0..z1) are contiguous in the sorted order
-            const int64_t cc0 = (X * g.dim[1] + Y) * g.dim[2] + z0, cc1 = (X * g.dim[1] + Y) * g.dim[2] + z1;
-            const uint32_t u0 = start[cc0], u1 = start[cc1 + 1];
+            const int64_t col = (X * g.dim[1] + Y) * g.dim[2];
+            const uint32_t u0 = start[col + z0], u1 = start[col + z1 + 1];
             for (uint32_t u = u0; u < u1; ++u) {
                 const double d = lidar::dist2d(px, py, pz, sxyz[3 * u], sxyz[3 * u + 1], sxyz[3 * u + 2]);
                 if (d <= g.eps2) f(u);
@@ -818,21 +836,16 @@ __device__ __forceinline__ int32_t count_neighbours(const Grid &g, const uint32_
                                                     double px, double py, double pz, uint32_t c, int32_t limit)
 {
     const int64_t cz = c % g.dim[2], cy = (c / g.dim[2]) % g.dim[1], cx = c / (g.dim[2] * g.dim[1]);
-    const int64_t z0 = cz > 0 ? cz - 1 : 0, z1 = cz + 1 < g.dim[2] ? cz + 1 : g.dim[2] - 1;
+    const int64_t z0 = cz - g.R > 0 ? cz - g.R : 0, z1 = cz + g.R < g.dim[2] ? cz + g.R : g.dim[2] - 1;
+    const int W = 2 * g.R + 1, centre = g.R * W + g.R;
     int32_t k = 0;
     // the point's own (X, Y) column first: the likeliest place to find `limit` hits
-    for (int r = 0; r < 9; ++r) {
-        // r = 0 -> (0, 0); r = 1..8 -> the other eight (dX, dY) in row-major order
-        int dx = 0, dy = 0;
-        if (r > 0) {
-            const int q = r <= 4 ? r - 1 : r;  // skip the centre slot 4 of the 3x3 row-major order
-            dx = q / 3 - 1;
-            dy = q % 3 - 1;
-        }
-        const int64_t X = cx + dx, Y = cy + dy;
+    for (int r = 0; r < W * W; ++r) {
+        const int q = r == 0 ? centre : (r <= centre ? r - 1 : r);  // row-major columns, centre moved first
+        const int64_t X = cx + q / W - g.R, Y = cy + q % W - g.R;
         if (X < 0 || X >= g.dim[0] || Y < 0 || Y >= g.dim[1]) continue;
-        const int64_t cc0 = (X * g.dim[1] + Y) * g.dim[2] + z0, cc1 = (X * g.dim[1] + Y) * g.dim[2] + z1;
-        const uint32_t u0 = start[cc0], u1 = start[cc1 + 1];
+        const int64_t col = (X * g.dim[1] + Y) * g.dim[2];
+        const uint32_t u0 = start[col + z0], u1 = start[col + z1 + 1];
         for (uint32_t u = u0; u < u1; ++u) {
             const double d = lidar::dist2d(px, py, pz, sxyz[3 * u], sxyz[3 * u + 1], sxyz[3 * u + 2]);
             if (d <= g.eps2 && ++k >= limit) return k;
@@ -841,19 +854,37 @@ __device__ __forceinline__ int32_t count_neighbours(const Grid &g, const uint32_
     return k;
 }
 
+constexpr uint32_t kNoCore = 0xffffffffu;
+
+// eps-neighbour counts (stopping at `limit`); with `core_in` set also the core flag of every sorted
+// slot and rep[c] = the smallest core index of cell c (rep initialised to kNoCore).  Fine cells:
+// every point of a cell is a neighbour, so a cell of >= limit points settles its points' counts
+// without a distance test.
 __global__ void dbscan_count_kernel(const double *P_in, const uint32_t *cid_in, const uint32_t *start_in,
                                     const uint32_t *order_in, const double *sxyz_in, int32_t *cnt_in,
-                                    int32_t limit, FrameMap fm)
+                                    int32_t limit, int32_t min_samples, uint8_t *core_in, uint32_t *rep_in,
+                                    FrameMap fm)
 {
     const double *P = fm.ws(P_in), *sxyz = fm.ws(sxyz_in);
     const uint32_t *cid = fm.ws(cid_in), *start = fm.ws(start_in), *order = fm.ws(order_in);
     int32_t *cnt = fm.ws(cnt_in);
+    uint8_t *core = core_in ? fm.ws(core_in) : nullptr;
+    uint32_t *rep = rep_in ? fm.ws(rep_in) : nullptr;
     if (P[P_ACTIVE] == 0.0) return;
     Grid g;
     g.load(P);
     for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < g.n; t += (int64_t)gridDim.x * blockDim.x) {
-        const uint32_t i = order[t];
-        cnt[i] = count_neighbours(g, start, sxyz, sxyz[3 * t], sxyz[3 * t + 1], sxyz[3 * t + 2], cid[i], limit);
+        const uint32_t i = order[t], c = cid[i];
+        const int64_t in_cell = (int64_t)start[c + 1] - start[c];
+        const int32_t k = g.intra && in_cell >= limit
+                              ? (int32_t)in_cell
+                              : count_neighbours(g, start, sxyz, sxyz[3 * t], sxyz[3 * t + 1], sxyz[3 * t + 2], c, limit);
+        cnt[i] = k;
+        if (core) {
+            const bool is_core = k >= min_samples;
+            core[t] = is_core ? 1 : 0;
+            if (is_core) atomicMin(rep + c, i);
+        }
     }
 }
 
@@ -917,7 +948,7 @@ __global__ void dbscan_union_kernel(const double *P_in, const uint32_t *cid_in, 
     const uint32_t *cid = fm.ws(cid_in), *start = fm.ws(start_in), *order = fm.ws(order_in);
     const int32_t *cnt = fm.ws(cnt_in);
     int32_t *parent = fm.ws(parent_in);
-    if (P[P_ACTIVE] == 0.0) return;
+    if (P[P_ACTIVE] == 0.0 || P[P_INTRA] != 0.0) return;  // fine cells: dbscan_intra + dbscan_cross
     Grid g;
     g.load(P);
     for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < g.n; t += (int64_t)gridDim.x * blockDim.x) {
@@ -934,6 +965,71 @@ __global__ void dbscan_union_kernel(const double *P_in, const uint32_t *cid_in, 
                 if (rj != ri) ri = uf_unite(parent, ri, rj);
             }
         });
+    }
+}
+
+// Fine cells, step 1: every core point of a cell hooks straight under the cell's smallest core
+// index (all of a cell's points are mutually eps-neighbours; parent[i] <= i holds, and no other
+// kernel writes parent meanwhile).
+__global__ void dbscan_intra_kernel(const double *P_in, const uint32_t *cid_in, const uint32_t *order_in,
+                                    const uint8_t *core_in, const uint32_t *rep_in, int32_t *parent_in, FrameMap fm)
+{
+    const double *P = fm.ws(P_in);
+    if (P[P_ACTIVE] == 0.0 || P[P_INTRA] == 0.0) return;
+    const uint32_t *cid = fm.ws(cid_in), *order = fm.ws(order_in), *rep = fm.ws(rep_in);
+    const uint8_t *core = fm.ws(core_in);
+    int32_t *parent = fm.ws(parent_in);
+    const int64_t n = (int64_t)P[P_N];
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (int64_t)gridDim.x * blockDim.x) {
+        if (!core[t]) continue;
+        const uint32_t i = order[t], r = rep[cid[i]];
+        if (r != i) parent[i] = (int32_t)r;
+    }
+}
+
+// Fine cells, step 2: one thread per (cell A, offset o) over the 62 offsets of [-2, 2]^3 that come
+// lexicographically after (0, 0, 0) — every pair of cells within the stencil once.  If A and B =
+// A + o both hold core points that are not yet one component, any core of A within eps of any
+// core of B links them.  Each cell's cores are one component (step 1), so the components after
+// this pass are exactly those of the core-core eps graph.
+constexpr int kPairOffsets = 62;
+__global__ void dbscan_cross_kernel(const double *P_in, const uint32_t *start_in, const double *sxyz_in,
+                                    const uint8_t *core_in, const uint32_t *rep_in, int32_t *parent_in, FrameMap fm)
+{
+    const double *P = fm.ws(P_in);
+    if (P[P_ACTIVE] == 0.0 || P[P_INTRA] == 0.0) return;
+    const double *sxyz = fm.ws(sxyz_in);
+    const uint32_t *start = fm.ws(start_in), *rep = fm.ws(rep_in);
+    const uint8_t *core = fm.ws(core_in);
+    int32_t *parent = fm.ws(parent_in);
+    Grid g;
+    g.load(P);
+    const int64_t work = (int64_t)P[P_NCELL] * kPairOffsets;
+    for (int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; w < work; w += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t A = w / kPairOffsets;
+        const uint32_t ra0 = rep[A];
+        if (ra0 == kNoCore) continue;
+        const int o = (int)(w - A * kPairOffsets) + 63;  // 5x5x5 offsets in row-major order; (0,0,0) is 62
+        const int64_t ax = A / (g.dim[1] * g.dim[2]), ay = (A / g.dim[2]) % g.dim[1], az = A % g.dim[2];
+        const int64_t bx = ax + o / 25 - 2, by = ay + (o / 5) % 5 - 2, bz = az + o % 5 - 2;
+        if (bx < 0 || bx >= g.dim[0] || by < 0 || by >= g.dim[1] || bz < 0 || bz >= g.dim[2]) continue;
+        const int64_t B = (bx * g.dim[1] + by) * g.dim[2] + bz;
+        const uint32_t rb0 = rep[B];
+        if (rb0 == kNoCore) continue;
+        const int32_t ra = uf_find(parent, (int32_t)ra0), rb = uf_find(parent, (int32_t)rb0);
+        if (ra == rb) continue;
+        bool linked = false;
+        const uint32_t b0 = start[B], b1 = start[B + 1];
+        for (uint32_t u = start[A], u1 = start[A + 1]; u < u1 && !linked; ++u) {
+            if (!core[u]) continue;
+            const double px = sxyz[3 * u], py = sxyz[3 * u + 1], pz = sxyz[3 * u + 2];
+            for (uint32_t v = b0; v < b1; ++v)
+                if (core[v] && lidar::dist2d(px, py, pz, sxyz[3 * v], sxyz[3 * v + 1], sxyz[3 * v + 2]) <= g.eps2) {
+                    linked = true;
+                    break;
+                }
+        }
+        if (linked) uf_unite(parent, ra, rb);
     }
 }
 
@@ -960,9 +1056,10 @@ __global__ void dbscan_roots_kernel(const double *P_in, const int32_t *cnt_in, i
 __global__ void dbscan_labels_kernel(double *P_in, const uint32_t *cid_in, const uint32_t *start_in,
                                      const uint32_t *order_in, const double *sxyz_in, const int32_t *cnt_in,
                                      int32_t min_samples, const int32_t *parent_in, const uint32_t *rank_in,
-                                     int64_t *labels_in, FrameMap fm)
+                                     const uint8_t *core_in, int64_t *labels_in, FrameMap fm)
 {
     double *P = fm.ws(P_in);
+    const uint8_t *core = fm.ws(core_in);
     const double *sxyz = fm.ws(sxyz_in);
     const uint32_t *cid = fm.ws(cid_in), *start = fm.ws(start_in), *order = fm.ws(order_in), *rank = fm.ws(rank_in);
     const int32_t *cnt = fm.ws(cnt_in), *parent = fm.ws(parent_in);
@@ -979,9 +1076,8 @@ __global__ void dbscan_labels_kernel(double *P_in, const uint32_t *cid_in, const
         } else {
             int64_t best = -1;
             for_neighbours(g, start, sxyz, sxyz[3 * t], sxyz[3 * t + 1], sxyz[3 * t + 2], cid[i], [&](uint32_t u) {
-                const int32_t j = (int32_t)order[u];
-                if (cnt[j] >= min_samples) {
-                    const int64_t l = rank[parent[j]];
+                if (core[u]) {
+                    const int64_t l = rank[parent[order[u]]];
                     if (best < 0 || l < best) best = l;
                 }
             });
@@ -1266,10 +1362,12 @@ struct DbscanWs {
     uint32_t *cid, *cellcnt, *cellstart, *fill, *order, *flag, *rank, *partial;
     double *sxyz;
     int32_t *cnt, *parent;
+    uint8_t *core;  // per sorted slot; `fill` doubles as the cells' smallest core index after the scatter
     int64_t max_cells, nblk_cells, nblk_pts;
 };
 
-int64_t max_cells_for(int64_t n) { return std::min<int64_t>(4 * n + 64, 1 << 22); }
+constexpr int kDbscanParts = 13;
+int64_t max_cells_for(int64_t n) { return std::min<int64_t>(8 * n + 64, 1 << 22); }
 
 void plan_dbscan(lidar::Carver &cv, int64_t n, uint64_t *off)
 {
@@ -1286,6 +1384,7 @@ void plan_dbscan(lidar::Carver &cv, int64_t n, uint64_t *off)
     off[9] = cv.take<double>(3 * n);         // sxyz
     off[10] = cv.take<int32_t>(n);           // cnt
     off[11] = cv.take<int32_t>(n);           // parent
+    off[12] = cv.take<uint8_t>(n);           // core (sorted slots)
 }
 
 DbscanWs bind_dbscan(char *base, const uint64_t *off, int64_t n)
@@ -1303,6 +1402,7 @@ DbscanWs bind_dbscan(char *base, const uint64_t *off, int64_t n)
     w.sxyz = reinterpret_cast<double *>(base + off[9]);
     w.cnt = reinterpret_cast<int32_t *>(base + off[10]);
     w.parent = reinterpret_cast<int32_t *>(base + off[11]);
+    w.core = reinterpret_cast<uint8_t *>(base + off[12]);
     w.max_cells = max_cells_for(n);
     w.nblk_cells = (w.max_cells + 1 + kScanPer - 1) / kScanPer;
     w.nblk_pts = (n + 1 + kScanPer - 1) / kScanPer;
@@ -1329,33 +1429,52 @@ unsigned point_blocks(int64_t nmax, int frames)
 
 // the DBSCAN pipeline on x (P[P_N] points, eps P[P_EPS], bbox in P) -> labels, for every frame
 // exact_counts: cnt[i] is the full eps-neighbour count (radius counts, the standalone API's
-// counts output); otherwise counting stops at min_samples
-int run_dbscan(const double *x, int64_t nmax, int32_t min_samples, DbscanWs &w, int64_t *labels, hipStream_t s,
-               FrameMap fm, int frames, bool count_only = false, bool exact_counts = false)
+// counts output); otherwise counting stops at min_samples.  h: profiling spans (may be null).
+int run_dbscan(lidar_handle *h, const double *x, int64_t nmax, int32_t min_samples, DbscanWs &w, int64_t *labels,
+               hipStream_t s, FrameMap fm, int frames, bool count_only = false, bool exact_counts = false)
 {
     const int32_t limit = (count_only || exact_counts) ? 0x7fffffff : min_samples;
     const unsigned gp = point_blocks(nmax, frames);
     const unsigned gc = point_blocks(w.max_cells, frames);
-    const dim3 F1(1, frames), FP(gp, frames), FC(gc, frames);
-    hipLaunchKernelGGL(dbscan_setup_kernel, F1, dim3(64), 0, s, w.P, w.max_cells, fm);
-    hipLaunchKernelGGL(zero_u32_kernel, FC, dim3(256), 0, s, w.cellcnt, w.P, P_NCELL, 1, fm);
-    hipLaunchKernelGGL(dbscan_cells_kernel, FP, dim3(256), 0, s, x, w.P, w.cid, w.cellcnt, w.parent, fm);
-    int rc = run_scan(w.cellcnt, w.cellstart, w.P, P_NCELL, 0, w.partial, w.nblk_cells, s, fm, frames);
-    if (rc) return rc;
-    hipLaunchKernelGGL(copy_u32_kernel, FC, dim3(256), 0, s, w.fill, w.cellstart, w.P, P_NCELL, 1, fm);
-    hipLaunchKernelGGL(dbscan_scatter_kernel, FP, dim3(256), 0, s, x, w.P, w.cid, w.fill, w.order, w.sxyz, fm);
-    hipLaunchKernelGGL(dbscan_count_kernel, FP, dim3(256), 0, s, w.P, w.cid, w.cellstart, w.order, w.sxyz, w.cnt, limit, fm);
+    const unsigned gx = point_blocks(w.max_cells * kPairOffsets, frames);
+    const dim3 F1(1, frames), FP(gp, frames), FC(gc, frames), FX(gx, frames);
+    {
+        lidar::Span sp(h, "dbscan_grid", s);  // cell sizes, counting sort by cell
+        hipLaunchKernelGGL(dbscan_setup_kernel, F1, dim3(64), 0, s, w.P, w.max_cells, fm);
+        hipLaunchKernelGGL(fill_u32_kernel, FC, dim3(256), 0, s, w.cellcnt, w.P, P_NCELL, 1, 0u, fm);
+        hipLaunchKernelGGL(dbscan_cells_kernel, FP, dim3(256), 0, s, x, w.P, w.cid, w.cellcnt, w.parent, fm);
+        int rc = run_scan(w.cellcnt, w.cellstart, w.P, P_NCELL, 0, w.partial, w.nblk_cells, s, fm, frames);
+        if (rc) return rc;
+        hipLaunchKernelGGL(copy_u32_kernel, FC, dim3(256), 0, s, w.fill, w.cellstart, w.P, P_NCELL, 1, fm);
+        hipLaunchKernelGGL(dbscan_scatter_kernel, FP, dim3(256), 0, s, x, w.P, w.cid, w.fill, w.order, w.sxyz, fm);
+        if (!count_only)  // `fill` is free after the scatter: the cells' smallest core index
+            hipLaunchKernelGGL(fill_u32_kernel, FC, dim3(256), 0, s, w.fill, w.P, P_NCELL, 1, kNoCore, fm);
+    }
+    {
+        lidar::Span sp(h, "dbscan_count", s);
+        hipLaunchKernelGGL(dbscan_count_kernel, FP, dim3(256), 0, s, w.P, w.cid, w.cellstart, w.order, w.sxyz, w.cnt,
+                           limit, min_samples, count_only ? nullptr : w.core, count_only ? nullptr : w.fill, fm);
+    }
     if (count_only) {
         LAUNCH_CHECK();
         return LIDAR_OK;
     }
-    hipLaunchKernelGGL(dbscan_union_kernel, FP, dim3(256), 0, s, w.P, w.cid, w.cellstart, w.order, w.sxyz,
-                       w.cnt, min_samples, w.parent, fm);
-    hipLaunchKernelGGL(dbscan_roots_kernel, FP, dim3(256), 0, s, w.P, w.cnt, min_samples, w.parent, w.flag, fm);
-    rc = run_scan(w.flag, w.rank, w.P, P_N, 0, w.partial, w.nblk_pts, s, fm, frames);
-    if (rc) return rc;
-    hipLaunchKernelGGL(dbscan_labels_kernel, FP, dim3(256), 0, s, w.P, w.cid, w.cellstart, w.order, w.sxyz,
-                       w.cnt, min_samples, w.parent, w.rank, labels, fm);
+    {
+        lidar::Span sp(h, "dbscan_union", s);  // fine cells: intra + cross; coarse cells: per-point union
+        hipLaunchKernelGGL(dbscan_intra_kernel, FP, dim3(256), 0, s, w.P, w.cid, w.order, w.core, w.fill, w.parent, fm);
+        hipLaunchKernelGGL(dbscan_cross_kernel, FX, dim3(256), 0, s, w.P, w.cellstart, w.sxyz, w.core, w.fill,
+                           w.parent, fm);
+        hipLaunchKernelGGL(dbscan_union_kernel, FP, dim3(256), 0, s, w.P, w.cid, w.cellstart, w.order, w.sxyz,
+                           w.cnt, min_samples, w.parent, fm);
+    }
+    {
+        lidar::Span sp(h, "dbscan_labels", s);  // roots, rank scan, labels
+        hipLaunchKernelGGL(dbscan_roots_kernel, FP, dim3(256), 0, s, w.P, w.cnt, min_samples, w.parent, w.flag, fm);
+        int rc = run_scan(w.flag, w.rank, w.P, P_N, 0, w.partial, w.nblk_pts, s, fm, frames);
+        if (rc) return rc;
+        hipLaunchKernelGGL(dbscan_labels_kernel, FP, dim3(256), 0, s, w.P, w.cid, w.cellstart, w.order, w.sxyz,
+                           w.cnt, min_samples, w.parent, w.rank, w.core, labels, fm);
+    }
     LAUNCH_CHECK();
     return LIDAR_OK;
 }
@@ -1370,7 +1489,7 @@ int run_preprocess(lidar_handle *h, const double *xyz, int64_t n, const int64_t 
     const uint64_t o_sc = cv.take<double>(3 * n);
     const uint64_t o_pos = cv.take<int32_t>(n);
     const uint64_t o_lab = cv.take<int64_t>(n);
-    uint64_t off[12];
+    uint64_t off[kDbscanParts];
     plan_dbscan(cv, n, off);
     const uint64_t wss = lidar::align_up(cv.off, 256);
     char *base = static_cast<char *>(lidar::workspace(h, wss * (uint64_t)frames));
@@ -1383,12 +1502,17 @@ int run_preprocess(lidar_handle *h, const double *xyz, int64_t n, const int64_t 
     fm.wss = (int64_t)wss;
     fm.offs = offs;
     HIP_TRY(hipMemsetAsync(scalars, 0, sizeof(double) * S_COUNT * frames, s));
-    hipLaunchKernelGGL(preprocess_kernel, dim3(1, frames), dim3(kT), 0, s, xyz, n, mask, colors, normals,
-                       compact_xyz, sc, ng_pos, scalars, fm, fixed_eps);
-    hipLaunchKernelGGL(dbscan_params_from_preprocess, dim3(1, frames), dim3(64), 0, s, scalars, w.P, w.max_cells, fm);
-    int rc = run_dbscan(sc, n, 5, w, ng_lab, s, fm, frames);
+    {
+        lidar::Span sp(h, "preprocess", s);
+        hipLaunchKernelGGL(preprocess_kernel, dim3(1, frames), dim3(kT), 0, s, xyz, n, mask, colors, normals,
+                           compact_xyz, sc, ng_pos, scalars, fm, fixed_eps);
+        hipLaunchKernelGGL(dbscan_params_from_preprocess, dim3(1, frames), dim3(64), 0, s, scalars, w.P, w.max_cells,
+                           fm);
+    }
+    int rc = run_dbscan(h, sc, n, 5, w, ng_lab, s, fm, frames);
     if (rc) return rc;
     const unsigned gp = point_blocks(n, frames);
+    lidar::Span sp(h, "label_scatter", s);
     hipLaunchKernelGGL(scatter_labels_kernel, dim3(gp, frames), dim3(256), 0, s, scalars, ng_lab, ng_pos, labels, fm);
     hipLaunchKernelGGL(scatter_labels2_kernel, dim3(gp, frames), dim3(256), 0, s, scalars, ng_lab, ng_pos, labels, fm);
     hipLaunchKernelGGL(nclust_kernel, dim3(1, frames), dim3(64), 0, s, w.P, scalars, fm);
@@ -1407,10 +1531,10 @@ LIDAR_EXPORT int lidar_dbscan_f64(lidar_handle *h, const double *x, int64_t n, d
     REQUIRE(eps > 0.0, "lidar_dbscan_f64: eps must be > 0");
     REQUIRE(min_samples >= 1, "lidar_dbscan_f64: min_samples must be >= 1");
     if (n == 0) return LIDAR_OK;
-    HIP_TRY(hipSetDevice(h->device));
+    ON_DEVICE(h->device);
     hipStream_t s = static_cast<hipStream_t>(stream);
     lidar::Carver cv;
-    uint64_t off[12];
+    uint64_t off[kDbscanParts];
     plan_dbscan(cv, n, off);
     char *base = static_cast<char *>(lidar::workspace(h, cv.off));
     if (!base) return LIDAR_ENOMEM;
@@ -1421,7 +1545,7 @@ LIDAR_EXPORT int lidar_dbscan_f64(lidar_handle *h, const double *x, int64_t n, d
     hp[P_ACTIVE] = 1.0;
     HIP_TRY(hipMemcpyAsync(w.P, hp, sizeof hp, hipMemcpyHostToDevice, s));
     hipLaunchKernelGGL(dbscan_bbox_kernel, dim3(1), dim3(kT), 0, s, x, w.P, FrameMap{});
-    int rc = run_dbscan(x, n, min_samples, w, labels, s, FrameMap{}, 1, false, counts != nullptr);
+    int rc = run_dbscan(h, x, n, min_samples, w, labels, s, FrameMap{}, 1, false, counts != nullptr);
     if (rc) return rc;
     if (counts) HIP_TRY(hipMemcpyAsync(counts, w.cnt, sizeof(int32_t) * n, hipMemcpyDeviceToDevice, s));
     // hp is a stack buffer: make sure the H2D copy has consumed it
@@ -1436,7 +1560,7 @@ LIDAR_EXPORT int lidar_preprocess_f64(lidar_handle *h, const double *xyz, int64_
     REQUIRE(h && xyz && mask && colors && normals && compact_xyz && labels && scalars,
             "lidar_preprocess_f64: null pointer");
     REQUIRE(n >= 1 && n < 0x7fffffff, "lidar_preprocess_f64: need 1 <= n < 2^31");
-    HIP_TRY(hipSetDevice(h->device));
+    ON_DEVICE(h->device);
     return run_preprocess(h, xyz, n, nullptr, 1, mask, colors, normals, compact_xyz, labels, scalars,
                           static_cast<hipStream_t>(stream));
 }
@@ -1450,7 +1574,7 @@ LIDAR_EXPORT int lidar_preprocess_batch_f64(lidar_handle *h, const double *xyz, 
             "lidar_preprocess_batch_f64: null pointer");
     REQUIRE(frames >= 1 && frames <= 65535, "lidar_preprocess_batch_f64: need 1 <= frames <= 65535");
     REQUIRE(max_n >= 1 && max_n < 0x7fffffff, "lidar_preprocess_batch_f64: need 1 <= max_n < 2^31");
-    HIP_TRY(hipSetDevice(h->device));
+    ON_DEVICE(h->device);
     return run_preprocess(h, xyz, max_n, offsets, frames, mask, colors, normals, compact_xyz, labels, scalars,
                           static_cast<hipStream_t>(stream));
 }
@@ -1469,7 +1593,7 @@ LIDAR_EXPORT int lidar_preprocess_eps_batch_f64(lidar_handle *h, const double *x
             "lidar_preprocess_eps_batch_f64: need 1 <= frames <= 65535 (offsets for frames > 1)");
     REQUIRE(max_n >= 1 && max_n < 0x7fffffff, "lidar_preprocess_eps_batch_f64: need 1 <= max_n < 2^31");
     REQUIRE(eps > 0.0 && eps < INFINITY, "lidar_preprocess_eps_batch_f64: eps must be finite and > 0");
-    HIP_TRY(hipSetDevice(h->device));
+    ON_DEVICE(h->device);
     return run_preprocess(h, xyz, max_n, offsets, frames, mask, colors, normals, compact_xyz, labels, scalars,
                           static_cast<hipStream_t>(stream), eps);
 }
@@ -1481,7 +1605,7 @@ LIDAR_EXPORT int lidar_people_f64(lidar_handle *h, const double *xyz, const int6
     REQUIRE(n >= 0, "lidar_people_f64: n < 0");
     *k_host = 0;
     if (n == 0) return LIDAR_OK;
-    HIP_TRY(hipSetDevice(h->device));
+    ON_DEVICE(h->device);
     hipStream_t s = static_cast<hipStream_t>(stream);
     int64_t *kd = static_cast<int64_t *>(lidar::workspace(h, 256));
     if (!kd) return LIDAR_ENOMEM;
@@ -1522,7 +1646,7 @@ LIDAR_EXPORT int lidar_density_grid_f64(lidar_handle *h, const double *people, i
 {
     REQUIRE(h && people && grid_x && grid_y && density, "lidar_density_grid_f64: null pointer");
     REQUIRE(nx >= 1 && ny >= 1 && k >= 0, "lidar_density_grid_f64: bad sizes");
-    HIP_TRY(hipSetDevice(h->device));
+    ON_DEVICE(h->device);
     hipStream_t s = static_cast<hipStream_t>(stream);
     lidar::Carver cv;
     const uint64_t o_xe = cv.take<double>(nx + 1), o_ye = cv.take<double>(ny + 1);
@@ -1556,11 +1680,12 @@ LIDAR_EXPORT int lidar_people_batch_f64(lidar_handle *h, const double *compact_x
 {
     REQUIRE(h && compact_xyz && labels && offsets && scalars && people && kdev, "lidar_people_batch_f64: null pointer");
     REQUIRE(frames >= 1 && frames <= 65535 && max_n >= 1, "lidar_people_batch_f64: bad sizes");
-    HIP_TRY(hipSetDevice(h->device));
+    ON_DEVICE(h->device);
     hipStream_t s = static_cast<hipStream_t>(stream);
     FrameMap fm;
     fm.offs = offsets;
     HIP_TRY(hipMemsetAsync(kdev, 0, sizeof(int64_t) * frames, s));
+    lidar::Span sp(h, "people", s);
     hipLaunchKernelGGL(max_label_kernel, dim3(point_blocks(max_n, frames), frames), dim3(256), 0, s, labels, max_n,
                        kdev, scalars, fm);
     const unsigned pb = (unsigned)std::max(1, std::min(256, 2048 / std::max(1, (int)frames)));
@@ -1578,10 +1703,11 @@ LIDAR_EXPORT int lidar_density_batch_f64(lidar_handle *h, const double *people, 
 {
     REQUIRE(h && people && offsets && kdev && jobs && out, "lidar_density_batch_f64: null pointer");
     REQUIRE(frames >= 1 && frames <= 65535 && scratch_doubles >= 0, "lidar_density_batch_f64: bad sizes");
-    HIP_TRY(hipSetDevice(h->device));
+    ON_DEVICE(h->device);
     hipStream_t s = static_cast<hipStream_t>(stream);
     double *scratch = static_cast<double *>(lidar::workspace(h, (uint64_t)std::max<int64_t>(1, scratch_doubles) * 8));
     if (!scratch) return LIDAR_ENOMEM;
+    lidar::Span sp(h, "density_grid", s);
     hipLaunchKernelGGL(density_batch_kernel, dim3(1, frames), dim3(kT), 0, s, people, offsets, kdev, jobs, out,
                        scratch);
     LAUNCH_CHECK();
@@ -1605,10 +1731,10 @@ LIDAR_EXPORT int lidar_radius_count_f64(lidar_handle *h, const double *x, int64_
     REQUIRE(n >= 0 && n < 0x7fffffff, "lidar_radius_count_f64: n out of range");
     REQUIRE(r >= 0.0, "lidar_radius_count_f64: r must be >= 0");
     if (n == 0) return LIDAR_OK;
-    HIP_TRY(hipSetDevice(h->device));
+    ON_DEVICE(h->device);
     hipStream_t s = static_cast<hipStream_t>(stream);
     lidar::Carver cv;
-    uint64_t off[12];
+    uint64_t off[kDbscanParts];
     plan_dbscan(cv, n, off);
     char *base = static_cast<char *>(lidar::workspace(h, cv.off));
     if (!base) return LIDAR_ENOMEM;
@@ -1621,7 +1747,7 @@ LIDAR_EXPORT int lidar_radius_count_f64(lidar_handle *h, const double *x, int64_
     hp[P_ACTIVE] = 1.0;
     HIP_TRY(hipMemcpyAsync(w.P, hp, sizeof(double) * P_COUNT, hipMemcpyHostToDevice, s));
     hipLaunchKernelGGL(dbscan_bbox_kernel, dim3(1), dim3(kT), 0, s, x, w.P, FrameMap{});
-    int rc = run_dbscan(x, n, 1, w, nullptr, s, FrameMap{}, 1, true);
+    int rc = run_dbscan(h, x, n, 1, w, nullptr, s, FrameMap{}, 1, true);
     if (rc) return rc;
     hipLaunchKernelGGL(widen_counts_kernel, dim3(point_blocks(n, 1)), dim3(256), 0, s, w.cnt, n, counts);
     LAUNCH_CHECK();
@@ -1657,7 +1783,7 @@ LIDAR_EXPORT int lidar_histogram2d_f64(lidar_handle *h, const double *a, const d
 {
     REQUIRE(h && xedges && yedges && counts && (n == 0 || (a && b)), "lidar_histogram2d_f64: null pointer");
     REQUIRE(n >= 0 && bx >= 1 && by >= 1, "lidar_histogram2d_f64: bad sizes");
-    HIP_TRY(hipSetDevice(h->device));
+    ON_DEVICE(h->device);
     hipStream_t s = static_cast<hipStream_t>(stream);
     const int64_t m = bx * by;
     auto *cnt = static_cast<unsigned long long *>(lidar::workspace(h, (uint64_t)m * 8));
@@ -1715,11 +1841,54 @@ LIDAR_EXPORT int lidar_cell_radius_density_f64(lidar_handle *h, const double *pe
     REQUIRE(h && xg && yg && out && (k == 0 || people), "lidar_cell_radius_density_f64: null pointer");
     REQUIRE(k >= 0 && nxg >= 2 && nyg >= 2, "lidar_cell_radius_density_f64: bad sizes");
     REQUIRE(r >= 0.0 && divisor != 0.0, "lidar_cell_radius_density_f64: bad r / divisor");
-    HIP_TRY(hipSetDevice(h->device));
+    ON_DEVICE(h->device);
     const int64_t nx = nxg - 1, ny = nyg - 1, m = nx * ny;
     const int64_t blocks = std::min<int64_t>((m + 255) / 256, 65535);
     hipLaunchKernelGGL(cell_radius_density_kernel, dim3((unsigned)blocks), dim3(256), 2 * 256 * sizeof(double),
                        static_cast<hipStream_t>(stream), people, k, xg, nx, yg, ny, r * r, divisor, out);
+    LAUNCH_CHECK();
+    return LIDAR_OK;
+}
+
+// ------------------------------------------------------------------ venue grid
+// calculate_grid_density's binning (utils/data_processing.py:312-319) over a FIXED venue grid:
+// edges np.arange(x0, ..., g) (e[0] = a, e[1] = a + g, e[i] = a + i * ((a + g) - a), numpy's
+// DOUBLE_fill), searchsorted right with the last edge closed, points outside dropped.  Counts
+// add into int32 cells, so the frames of a rank and then the ranks (one RCCL all-reduce) sum.
+__device__ __forceinline__ double arange_edge(double a, double g, int64_t i)
+{
+    return i == 0 ? a : (i == 1 ? dadd(a, g) : dadd(a, dmul((double)i, dsub(dadd(a, g), a))));
+}
+__device__ __forceinline__ int64_t arange_bin(double a, double g, int64_t nb, double v)
+{
+    int64_t lo = 0, hi = nb + 1;  // first edge index with e[idx] > v
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (arange_edge(a, g, mid) <= v) lo = mid + 1;
+        else hi = mid;
+    }
+    if (v == arange_edge(a, g, nb)) --lo;  // the last edge is closed
+    return lo;                             // bin lo - 1 when 1 <= lo <= nb
+}
+__global__ void venue_counts_kernel(const double *__restrict__ people, int64_t k, double x0, double y0, double g,
+                                    int64_t nx, int64_t ny, int32_t *__restrict__ counts)
+{
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < k; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t bx = arange_bin(x0, g, nx, people[2 * i]), by = arange_bin(y0, g, ny, people[2 * i + 1]);
+        if (bx >= 1 && bx <= nx && by >= 1 && by <= ny) atomicAdd(&counts[(bx - 1) * ny + (by - 1)], 1);
+    }
+}
+
+LIDAR_EXPORT int lidar_venue_counts_f64(lidar_handle *h, const double *people, int64_t k, double x0, double y0,
+                                        double grid, int64_t nx, int64_t ny, int32_t *counts, void *stream)
+{
+    REQUIRE(h && counts && (k == 0 || people), "lidar_venue_counts_f64: null pointer");
+    REQUIRE(k >= 0 && nx >= 1 && ny >= 1 && grid > 0.0, "lidar_venue_counts_f64: bad sizes");
+    if (k == 0) return LIDAR_OK;
+    ON_DEVICE(h->device);
+    const unsigned blocks = (unsigned)std::min<int64_t>((k + 255) / 256, 4096);
+    hipLaunchKernelGGL(venue_counts_kernel, dim3(blocks), dim3(256), 0, static_cast<hipStream_t>(stream), people, k,
+                       x0, y0, grid, nx, ny, counts);
     LAUNCH_CHECK();
     return LIDAR_OK;
 }

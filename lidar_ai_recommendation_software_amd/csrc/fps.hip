@@ -543,7 +543,7 @@ LIDAR_EXPORT uint64_t lidar_fps_workspace_bytes(int64_t batch, int64_t n)
     return (uint64_t)(batch * lidar::align_up(5 * lidar::align_up(n, 64), 64)) * 4;
 }
 
-// threads: workgroup size per frame, 0 (the build default, 1024), 1024, 512 or 256 — same results
+// threads: workgroup size per frame, 0 (the build default, 1024), 1024 or 512 — same results
 LIDAR_EXPORT int lidar_fps_ex_f32(lidar_handle *h, const float *xyz, int64_t batch, int64_t n, int64_t npoint,
                                   int32_t *idx, float *new_xyz, int32_t *first_zero, const int32_t *prefix_ok,
                                   int32_t threads, void *stream)
@@ -552,12 +552,11 @@ LIDAR_EXPORT int lidar_fps_ex_f32(lidar_handle *h, const float *xyz, int64_t bat
     REQUIRE(batch >= 0 && n >= 1 && npoint >= 1, "lidar_fps_f32: need n >= 1 and npoint >= 1");
     REQUIRE(n <= 4 * 65536, "lidar_fps_f32: n > 262144 points per frame");
     if (threads == 0) threads = kThreads;
-    REQUIRE(threads == 1024 || threads == 512 || threads == 256,
-            "lidar_fps_ex_f32: threads must be 0, 256, 512 or 1024");
+    REQUIRE(threads == 1024 || threads == 512, "lidar_fps_ex_f32: threads must be 0, 512 or 1024");
     REQUIRE((n + 63) / 64 <= 8 * (int64_t)threads, "lidar_fps_f32: too many buckets for this workgroup size");
     REQUIRE(batch <= 0x7fffffff, "lidar_fps_f32: batch too large");
     if (batch == 0) return LIDAR_OK;
-    HIP_TRY(hipSetDevice(h->device));
+    ON_DEVICE(h->device);
     REQUIRE(prefix_ok == nullptr || npoint <= n, "lidar_fps_f32: prefix_ok needs npoint <= n");
     int64_t stride = lidar::align_up(5 * lidar::align_up(n, 64), 64);
     float *ws = static_cast<float *>(lidar::workspace(h, (uint64_t)(batch * stride) * 4));
@@ -565,8 +564,6 @@ LIDAR_EXPORT int lidar_fps_ex_f32(lidar_handle *h, const float *xyz, int64_t bat
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (threads == 512)
         return launch_fps<512>(xyz, batch, n, npoint, idx, new_xyz, first_zero, prefix_ok, ws, stride, s);
-    if (threads == 256)
-        return launch_fps<256>(xyz, batch, n, npoint, idx, new_xyz, first_zero, prefix_ok, ws, stride, s);
     return launch_fps<1024>(xyz, batch, n, npoint, idx, new_xyz, first_zero, prefix_ok, ws, stride, s);
 }
 
@@ -582,7 +579,7 @@ LIDAR_EXPORT int lidar_diag_fps_phases(lidar_handle *h, const float *xyz, int64_
                                        int64_t npoint, int32_t *idx, uint64_t *diag, void *stream)
 {
     REQUIRE(h && xyz && idx && diag && n <= 65536 && n >= 1 && npoint >= 1, "lidar_diag_fps_phases: bad args");
-    HIP_TRY(hipSetDevice(h->device));
+    ON_DEVICE(h->device);
     int64_t stride = lidar::align_up(5 * lidar::align_up(n, 64), 64);
     float *ws = static_cast<float *>(lidar::workspace(h, (uint64_t)(batch * stride) * 4));
     if (!ws) return LIDAR_ENOMEM;

@@ -1,4 +1,5 @@
-// handle.hip — handle lifetime, thread-local errors, workspace growth.
+// handle.hip — handle lifetime, thread-local errors, workspace growth, per-launch profiling.
+#include <algorithm>
 #include <cstring>
 #include <string>
 
@@ -22,23 +23,41 @@ void *workspace(lidar_handle *h, uint64_t bytes)
     uint64_t want = align_up(bytes + bytes / 4, 1 << 20);
     if (h->ws) {
         // the previous workspace may still be read by queued kernels
-        hipDeviceSynchronize();
-        hipFree(h->ws);
+        hipError_t e = hipDeviceSynchronize();
+        if (e != hipSuccess) {
+            set_error(std::string("workspace growth: hipDeviceSynchronize: ") + hipGetErrorString(e));
+            return nullptr;
+        }
+        e = hipFree(h->ws);
         h->ws = nullptr;
         h->ws_bytes = 0;
+        if (e != hipSuccess) {
+            set_error(std::string("workspace growth: hipFree: ") + hipGetErrorString(e));
+            return nullptr;
+        }
     }
-    if (hipMalloc(&h->ws, want) != hipSuccess) {
+    const hipError_t e = hipMalloc(&h->ws, want);
+    if (e != hipSuccess) {
         h->ws = nullptr;
-        set_error("workspace hipMalloc failed");
+        set_error(std::string("workspace hipMalloc(") + std::to_string(want) + "): " + hipGetErrorString(e));
         return nullptr;
     }
     h->ws_bytes = want;
     return h->ws;
 }
 
+static void drop_records(Prof *p)
+{
+    for (auto &r : p->recs) {
+        (void)hipEventDestroy(r.a);
+        (void)hipEventDestroy(r.b);
+    }
+    p->recs.clear();
+}
+
 }  // namespace lidar
 
-LIDAR_EXPORT int lidar_version(void) { return 1; }
+LIDAR_EXPORT int lidar_version(void) { return 2; }
 
 LIDAR_EXPORT const char *lidar_last_error(void) { return lidar::g_err.c_str(); }
 
@@ -46,7 +65,7 @@ LIDAR_EXPORT int lidar_create(int device, lidar_handle **out)
 {
     REQUIRE(out != nullptr, "lidar_create: out is NULL");
     *out = nullptr;
-    HIP_TRY(hipSetDevice(device));
+    ON_DEVICE(device);
     hipDeviceProp_t prop;
     HIP_TRY(hipGetDeviceProperties(&prop, device));
     if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
@@ -54,57 +73,133 @@ LIDAR_EXPORT int lidar_create(int device, lidar_handle **out)
                                               ", this library is built for gfx950 only");
     lidar_handle *h = new lidar_handle();
     h->device = device;
-    if (hipHostMalloc(&h->host_pinned, 4096, hipHostMallocDefault) != hipSuccess) {
+    const hipError_t e = hipHostMalloc(&h->host_pinned, 4096, hipHostMallocDefault);
+    if (e != hipSuccess) {
         delete h;
-        return lidar::fail(LIDAR_ENOMEM, "pinned host buffer allocation failed");
+        return lidar::fail(LIDAR_ENOMEM, std::string("pinned host buffer: ") + hipGetErrorString(e));
     }
     *out = h;
     return LIDAR_OK;
 }
 
+// Releases everything the handle owns.  Every step runs even if an earlier one fails (the
+// handle is gone either way); the first failure is reported.
 LIDAR_EXPORT int lidar_destroy(lidar_handle *h)
 {
     if (!h) return LIDAR_OK;
-    hipSetDevice(h->device);
-    hipDeviceSynchronize();
-    if (h->ws) hipFree(h->ws);
-    if (h->host_pinned) hipHostFree(h->host_pinned);
+    int rc = LIDAR_OK;
+    auto note = [&](hipError_t e, const char *what) {
+        if (e != hipSuccess && rc == LIDAR_OK) rc = lidar::fail(LIDAR_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+    };
+    {
+        lidar::DeviceScope scope(h->device);
+        note(scope.rc, "lidar_destroy: hipSetDevice");
+        note(hipDeviceSynchronize(), "lidar_destroy: hipDeviceSynchronize");
+        if (h->prof) {
+            lidar::drop_records(h->prof);
+            delete h->prof;
+        }
+        if (h->ws) note(hipFree(h->ws), "lidar_destroy: hipFree");
+        if (h->host_pinned) note(hipHostFree(h->host_pinned), "lidar_destroy: hipHostFree");
+    }
     delete h;
-    return LIDAR_OK;
+    return rc;
 }
 
 LIDAR_EXPORT int lidar_reserve(lidar_handle *h, uint64_t bytes)
 {
     REQUIRE(h != nullptr, "lidar_reserve: null handle");
-    HIP_TRY(hipSetDevice(h->device));
+    ON_DEVICE(h->device);
     if (!lidar::workspace(h, bytes)) return LIDAR_ENOMEM;
     return LIDAR_OK;
 }
 
-// A stream restricted to a subset of the device's compute units (bit i of mask[i / 32]
-// enables CU i).  Used by StreamingSSG to keep the latency-bound SA1 FPS chains and the
-// MFMA levels on disjoint CUs.  Returns the hipStream_t through *out.
-LIDAR_EXPORT int lidar_stream_create_cu_mask(int device, const uint32_t *mask, int32_t nwords, void **out)
+// enable != 0: record HIP events around the handle's kernel phases from now on (previous records
+// dropped); enable == 0: stop and drop the records.
+LIDAR_EXPORT int lidar_profile(lidar_handle *h, int32_t enable)
 {
-    REQUIRE(mask && out && nwords > 0, "lidar_stream_create_cu_mask: bad arguments");
-    HIP_TRY(hipSetDevice(device));
-    hipStream_t s = nullptr;
-    HIP_TRY(hipExtStreamCreateWithCUMask(&s, (uint32_t)nwords, mask));
-    *out = s;
+    REQUIRE(h != nullptr, "lidar_profile: null handle");
+    ON_DEVICE(h->device);
+    if (h->prof) {
+        lidar::drop_records(h->prof);
+        if (!enable) {
+            delete h->prof;
+            h->prof = nullptr;
+        }
+    } else if (enable) {
+        h->prof = new lidar::Prof();
+    }
     return LIDAR_OK;
 }
 
-LIDAR_EXPORT int lidar_stream_destroy(void *stream)
+// The recorded spans in launch order: names '\n'-separated into `names` (names_cap bytes, NUL
+// terminated), durations in ms into ms[0 .. *count); waits for the events and drops them.
+LIDAR_EXPORT int lidar_profile_read(lidar_handle *h, char *names, int64_t names_cap, float *ms, int64_t cap,
+                                    int64_t *count)
 {
-    if (stream) HIP_TRY(hipStreamDestroy(static_cast<hipStream_t>(stream)));
-    return LIDAR_OK;
+    REQUIRE(h && names && ms && count && names_cap > 0, "lidar_profile_read: null pointer");
+    *count = 0;
+    names[0] = '\0';
+    if (!h->prof) return LIDAR_OK;
+    ON_DEVICE(h->device);
+    std::string joined;
+    int64_t k = 0;
+    int rc = LIDAR_OK;
+    for (auto &r : h->prof->recs) {
+        if (k >= cap) break;
+        float t = 0.0f;
+        hipError_t e = hipEventSynchronize(r.b);
+        if (e == hipSuccess) e = hipEventElapsedTime(&t, r.a, r.b);
+        if (e != hipSuccess && rc == LIDAR_OK)
+            rc = lidar::fail(LIDAR_EHIP, std::string("lidar_profile_read: ") + hipGetErrorString(e));
+        ms[k++] = t;
+        joined += r.name;
+        joined += '\n';
+    }
+    lidar::drop_records(h->prof);
+    REQUIRE((int64_t)joined.size() < names_cap, "lidar_profile_read: names buffer too small");
+    std::memcpy(names, joined.c_str(), joined.size() + 1);
+    *count = k;
+    return rc;
 }
 
-LIDAR_EXPORT int lidar_device_cu_count(int device, int32_t *out)
+// ---- downsample_point_cloud's gather (utils/data_processing.py:247-249): rows copied as raw
+// bytes, 16 / 8 / 4 / 1 bytes per lane by the row size's alignment; indices out of range are
+// skipped (the host draws them with np.random.choice, always in range)
+namespace {
+template <class T>
+__global__ void gather_rows_kernel(const T *__restrict__ src, int64_t n_rows, int64_t row_words,
+                                   const int64_t *__restrict__ idx, int64_t k, T *__restrict__ dst)
 {
-    REQUIRE(out, "lidar_device_cu_count: null pointer");
-    int v = 0;
-    HIP_TRY(hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, device));
-    *out = v;
+    const int64_t total = k * row_words;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = e / row_words, w = e - r * row_words;
+        const int64_t j = idx[r];
+        if (j >= 0 && j < n_rows) dst[e] = src[j * row_words + w];
+    }
+}
+}  // namespace
+
+LIDAR_EXPORT int lidar_gather_rows(lidar_handle *h, const void *src, int64_t n_rows, int64_t row_bytes,
+                                   const int64_t *idx, int64_t k, void *dst, void *stream)
+{
+    REQUIRE(h && (k == 0 || (src && idx && dst)), "lidar_gather_rows: null pointer");
+    REQUIRE(n_rows >= 0 && row_bytes >= 0 && k >= 0, "lidar_gather_rows: negative size");
+    if (k == 0 || row_bytes == 0) return LIDAR_OK;
+    ON_DEVICE(h->device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const uintptr_t al = reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst) | (uintptr_t)row_bytes;
+    auto go = [&](auto tag) {
+        using T = decltype(tag);
+        const int64_t words = row_bytes / (int64_t)sizeof(T), total = k * words;
+        const unsigned blocks = (unsigned)std::min<int64_t>((total + 255) / 256, 8192);
+        hipLaunchKernelGGL(gather_rows_kernel<T>, dim3(blocks), dim3(256), 0, s, static_cast<const T *>(src), n_rows,
+                           words, idx, k, static_cast<T *>(dst));
+    };
+    if (al % 16 == 0) go(uint4{});
+    else if (al % 8 == 0) go(uint2{});
+    else if (al % 4 == 0) go(uint32_t{});
+    else go(uint8_t{});
+    LAUNCH_CHECK();
     return LIDAR_OK;
 }

@@ -1,6 +1,6 @@
 // sa_mlp16.hip — SetAbstraction layers on v_mfma_f32_16x16x4_f32, 16 grouped rows per wave.
 //
-// The same fused design as sa_mlp_pre.hip (gather -> MFMA chain -> max-pool, weights streamed
+// The fused SetAbstraction branch (gather -> MFMA chain -> max-pool, weights streamed
 // through LDS in 16 KiB chunks shared by the 4 waves of a workgroup), with 16-row tiles:
 //   16x16x4 f32: lane l holds A[l&15][k = l>>4], B[k = l>>4][l&15]; D reg r of lane l is row
 //   4*(l>>4) + r, column l&15.
@@ -15,7 +15,7 @@
 //
 // Why 16 rows: the activations of 16 rows take half the registers of 32 (y1 + y2 = 64 VGPRs
 // for 128-wide layers), so the kernel fits ~128 VGPRs: 4 waves per SIMD, and 2 still fit on a
-// CU that also hosts an FPS workgroup (the 32-row kernel needs 256 and drops to 1 there).
+// CU that also hosts an FPS workgroup (32-row tiles need ~256 and drop to 1 there).
 #include <vector>
 
 #include "common.hpp"
@@ -269,7 +269,7 @@ LIDAR_EXPORT int lidar_mlp_pack16_f32(int32_t xyz_level, int32_t c1, int32_t c2,
 }
 
 // the 16-row fused kernels.  xyz_level: p = xyz (B*n, 3), q = centres (B*m, 3) and layer 1 runs
-// here; else p / q are the per-point / per-centre layer-1 rows (lidar_sa_group_mlp_pre_f32's
+// here; else p / q are the per-point / per-centre layer-1 rows (layer1_per_point's
 // P and Q, row stride p_stride).  packed: lidar_mlp_pack16_f32's image.
 LIDAR_EXPORT int lidar_sa_group_mlp16_f32(lidar_handle *h, int32_t xyz_level, const float *p, int64_t p_stride,
                                           const float *q, const int32_t *idx, int64_t batch, int64_t n, int64_t m,
@@ -281,7 +281,7 @@ LIDAR_EXPORT int lidar_sa_group_mlp16_f32(lidar_handle *h, int32_t xyz_level, co
     REQUIRE(xyz_level || (p_stride >= c1 && p_stride % 4 == 0), "lidar_sa_group_mlp16_f32: bad p_stride");
     REQUIRE(out_offset >= 0 && out_offset + c3 <= out_stride, "lidar_sa_group_mlp16_f32: output columns exceed out_stride");
     if (batch == 0) return LIDAR_OK;
-    HIP_TRY(hipSetDevice(h->device));
+    ON_DEVICE(h->device);
     hipStream_t s = static_cast<hipStream_t>(stream);
 #define LIDAR_SA16(C1_, C2_, C3_, NS_, X_)                                                                 \
     if (!!xyz_level == X_ && c1 == C1_ && c2 == C2_ && c3 == C3_ && nsample == NS_)                         \

@@ -414,7 +414,7 @@ LIDAR_EXPORT int lidar_sa_group_mlp_x3_f32(lidar_handle *h, int32_t xyz_level, c
     REQUIRE(out_offset >= 0 && out_offset + c3 <= out_stride,
             "lidar_sa_group_mlp_x3_f32: output columns exceed out_stride");
     if (batch == 0) return LIDAR_OK;
-    HIP_TRY(hipSetDevice(h->device));
+    ON_DEVICE(h->device);
     hipStream_t s = static_cast<hipStream_t>(stream);
 #define LIDAR_SAX3(C1_, C2_, C3_, NS_, X_)                                                                   \
     if (!!xyz_level == X_ && c1 == C1_ && c2 == C2_ && c3 == C3_ && nsample == NS_)                           \
@@ -497,7 +497,7 @@ LIDAR_EXPORT int lidar_sa_group_mlp_x1_f32(lidar_handle *h, int32_t layer1_mode,
     REQUIRE(out_offset >= 0 && out_offset + c3 <= out_stride,
             "lidar_sa_group_mlp_x1_f32: output columns exceed out_stride");
     if (batch == 0) return LIDAR_OK;
-    HIP_TRY(hipSetDevice(h->device));
+    ON_DEVICE(h->device);
     hipStream_t s = static_cast<hipStream_t>(stream);
 #define LIDAR_SAX1(C1_, C2_, C3_, NS_, M_)                                                                    \
     if (layer1_mode == M_ && c1 == C1_ && c2 == C2_ && c3 == C3_ && nsample == NS_)                           \

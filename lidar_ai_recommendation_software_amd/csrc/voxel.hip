@@ -201,7 +201,7 @@ LIDAR_EXPORT int lidar_voxel_downsample_f32(lidar_handle *h, const float *xyz, i
     REQUIRE(voxel > 0.0f, "lidar_voxel_downsample_f32: voxel size must be > 0");
     *nvox_host = 0;
     if (n == 0) return LIDAR_OK;
-    HIP_TRY(hipSetDevice(h->device));
+    ON_DEVICE(h->device);
     hipStream_t s = static_cast<hipStream_t>(stream);
     lidar::Carver cv;
     const uint64_t ok0 = cv.take<uint32_t>(n), ov0 = cv.take<uint32_t>(n);

@@ -356,7 +356,7 @@ LIDAR_EXPORT int lidar_voxel_downsample_batch_f32(lidar_handle *h, const float *
             "lidar_voxel_downsample_batch_f32: batch in [0, 65535], n >= 1");
     REQUIRE(voxel > 0.0f, "lidar_voxel_downsample_batch_f32: voxel size must be > 0");
     if (batch == 0) return LIDAR_OK;
-    HIP_TRY(hipSetDevice(h->device));
+    ON_DEVICE(h->device);
     hipStream_t s = static_cast<hipStream_t>(stream);
     const int ntiles = (int)((n + TILE - 1) / TILE);
     lidar::Carver cv;

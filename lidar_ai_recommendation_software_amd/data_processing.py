@@ -21,21 +21,59 @@ import numpy as np
 from . import _native as nat
 
 # ----------------------------------------------------------------- device cache
+# Arrays this module returned keep their device copy, so that extract_people_positions /
+# calculate_grid_density on a preprocess_lidar_data result do not re-upload the frame.  A
+# hit needs the same object AND the same bytes: the entry stores an xxh3-128 digest of the
+# array's contents, so a caller that edits pd["points"] (or the people array) in place gets
+# the edited values uploaded, as the reference would read them.  Hashing a 65 k-point frame
+# (1.5 MB) costs ~0.1 ms on the host.
 _cache = {}
+
+
+def _digest(arr):
+    import xxhash
+    a = np.ascontiguousarray(arr)
+    return a.shape, a.dtype.str, xxhash.xxh3_128_intdigest(memoryview(a.reshape(-1)).cast("B"))
 
 
 def _remember(arr, tensor):
     key = id(arr)
-    _cache[key] = (weakref.ref(arr, lambda _r, k=key: _cache.pop(k, None)), tensor)
+    _cache[key] = (weakref.ref(arr, lambda _r, k=key: _cache.pop(k, None)), tensor, _digest(arr))
 
 
 def _on_device(arr, dtype):
     import torch
     hit = _cache.get(id(arr))
-    if hit is not None and hit[0]() is arr and hit[1].dtype == dtype:
+    if (hit is not None and hit[0]() is arr and hit[1].dtype == dtype and isinstance(arr, np.ndarray)
+            and hit[2] == _digest(arr)):
         return hit[1]
     npd = {torch.float64: np.float64, torch.int64: np.int64, torch.float32: np.float32}[dtype]
     return torch.from_numpy(np.ascontiguousarray(arr, dtype=npd)).cuda()
+
+
+def _reference_shape_errors(pts):
+    """The exceptions the reference raises for a frame that is not (N >= 1, 3), decided from the
+    array's shape before any kernel runs (utils/data_processing.py:143-207; the Streamlit apps'
+    preprocess_point_cloud, app_simplified.py:80-117, raises the same):
+      * not 2-D, or fewer than 3 columns: ``points[:, 2]`` raises IndexError;
+      * no rows: ``np.min`` of the empty z column raises ValueError;
+      * k > 3 columns: the 3-sigma mask runs over all k columns; an empty inlier set raises
+        IndexError from ``np.percentile`` (:164), otherwise unpacking ``np.min(inlier_points,
+        axis=0)`` into three names raises ValueError (:207).  That decision is the reference's own
+        numpy expression on the host: it selects the exception, it computes no result."""
+    if pts.ndim != 2:
+        raise IndexError(f"too many indices for array: array is {pts.ndim}-dimensional, but 2 were indexed")
+    k = pts.shape[1]
+    if k < 3:
+        raise IndexError(f"index 2 is out of bounds for axis 1 with size {k}")
+    if len(pts) == 0:
+        raise ValueError("zero-size array to reduction operation minimum which has no identity")
+    if k > 3:
+        mean = np.mean(pts, axis=0)
+        std = np.std(pts, axis=0)
+        if not np.all(np.abs(pts - mean) < 3 * std, axis=1).any():
+            raise IndexError("index -1 is out of bounds for axis 0 with size 0")
+        raise ValueError("too many values to unpack (expected 3)")
 
 
 def _handle():
@@ -168,17 +206,15 @@ def preprocess_lidar_data(points):
 
     Returns the reference's dict {points, colors, normals, clusters, ground_plane,
     dimensions} with the same dtypes; raises the reference's exceptions (ValueError
-    on an empty frame, IndexError when no point survives the 3-sigma filter).
+    on an empty frame, IndexError when no point survives the 3-sigma filter, and the
+    shape errors of ``_reference_shape_errors`` for frames that are not (N, 3)).
     """
     import torch
     pts = np.asarray(points)
-    if pts.ndim != 2 or pts.shape[1] < 3:
-        raise IndexError("too many indices for array")
+    _reference_shape_errors(pts)  # frames that are not (N >= 1, 3): the reference's exceptions
     n = len(pts)
-    if n == 0:
-        raise ValueError("zero-size array to reduction operation minimum which has no identity")
     is_int = pts.dtype.kind in "iub"
-    x = torch.from_numpy(np.ascontiguousarray(pts[:, :3], dtype=np.float64)).cuda()
+    x = torch.from_numpy(np.ascontiguousarray(pts, dtype=np.float64)).cuda()
     dev = x.device
     mask = torch.empty(n, dtype=torch.uint8, device=dev)
     colors = torch.empty((n, 3), dtype=torch.float64, device=dev)
@@ -223,15 +259,42 @@ def preprocess_lidar_data(points):
 
 def downsample_point_cloud(points, factor=0.1):
     """Replaces ``utils/data_processing.py:231-249``: identity for factor >= 1, else
-    ``points[np.random.choice(n, max(1, int(n*factor)), replace=False)]`` drawn from the
-    GLOBAL legacy NumPy RNG exactly as the reference does (the draw is host RNG state, not
-    arithmetic; the gather is a host index)."""
+    ``points[np.random.choice(n, max(1, int(n*factor)), replace=False)]``.
+
+    The draw is the reference's own: ``np.random.choice`` on the GLOBAL legacy NumPy RNG (host
+    RNG state: identical indices, identical RNG state afterwards).  The gather runs on the GPU
+    (``lidar_gather_rows`` moves rows as raw bytes, so any dtype comes back bit for bit).  A CUDA
+    tensor in gives a CUDA tensor out (throughput mode: only the indices cross PCIe); a NumPy
+    array in gives a NumPy array out."""
     if factor >= 1.0:
         return points
     num = len(points)
     keep = max(1, int(num * factor))
     idx = np.random.choice(num, keep, replace=False)
-    return points[idx]
+    import torch
+    if isinstance(points, torch.Tensor):
+        src = points.contiguous()
+        out = torch.empty((keep,) + tuple(src.shape[1:]), dtype=src.dtype, device=src.device)
+        return _gather_rows(src, idx, out)
+    a = np.asarray(points)
+    if a.dtype.hasobject:  # Python object references cannot live in device memory
+        return a[idx]
+    src = torch.from_numpy(np.ascontiguousarray(a).reshape(len(a), -1).view(np.uint8)).cuda()
+    out = torch.empty((keep, src.shape[1]), dtype=torch.uint8, device=src.device)
+    _gather_rows(src, idx, out)
+    return out.cpu().numpy().view(a.dtype).reshape((keep,) + a.shape[1:])
+
+
+def _gather_rows(src, idx, out):
+    """out[r] = src[idx[r]] on the GPU (rows of numel / len elements, copied as raw bytes)."""
+    import torch
+    n = len(src)
+    row_bytes = src.element_size() * (src.numel() // max(n, 1))
+    d_idx = torch.from_numpy(np.ascontiguousarray(idx, dtype=np.int64)).to(src.device)
+    nat.call("lidar_gather_rows", nat.handle(src.device.index), nat.ptr(src), n, row_bytes, nat.ptr(d_idx),
+             len(idx), nat.ptr(out), nat.stream_ptr())
+    d_idx.record_stream(torch.cuda.current_stream(src.device))
+    return out
 
 
 # ------------------------------------------------------------- people / density (L2)

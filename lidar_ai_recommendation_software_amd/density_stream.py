@@ -122,6 +122,28 @@ class DensityStream:
         return out
 
     # ------------------------------------------------------------------ batched mode
+    BATCH_SLOT = 7  # run_batch's library handle slot
+
+    def profile(self, enable):
+        """Per-phase HIP-event timing of run_batch's launches (lidar_profile): phases preprocess,
+        dbscan_grid, dbscan_count, dbscan_union, dbscan_labels, label_scatter, people, density_grid."""
+        nat.profile(nat.handle(self.device.index, slot=self.BATCH_SLOT), enable)
+
+    def profile_read(self):
+        """{phase: (launches, total ms)} since the last read (waits for the events)."""
+        out = {}
+        for name, ms in nat.profile_read(nat.handle(self.device.index, slot=self.BATCH_SLOT)):
+            n, t = out.get(name, (0, 0.0))
+            out[name] = (n + 1, t + ms)
+        return out
+
+    def people_of_last_batch(self):
+        """The people positions of every frame of the last run_batch, concatenated in frame order:
+        a (sum K_f, 2) float64 CUDA tensor (what extract_people_positions returns per frame)."""
+        people, offs, K = self._last_people
+        rows = [people[int(o):int(o) + int(k)] for o, k in zip(offs[:-1], K) if k > 0]
+        return torch.cat(rows) if rows else people[:0]
+
     def run_batch(self, frames):
         """frames: list of (n_i, 3) float64 CUDA tensors -> list of analyze results, one
         launch per phase for the whole list.  Raises the reference's exception of the first
@@ -143,7 +165,7 @@ class DensityStream:
         colors, normals, comp = (torch.empty((rows, 3), **f64) for _ in range(3))
         labels = torch.empty(rows, dtype=torch.int64, device=dev)
         scal = torch.empty((F, 64), **f64)
-        h = nat.handle(self.device.index, slot=7)
+        h = nat.handle(self.device.index, slot=self.BATCH_SLOT)
         sp = torch.cuda.current_stream(dev).cuda_stream
         nat.call("lidar_preprocess_batch_f64", h, nat.ptr(x), nat.ptr(offs), F, max_n, nat.ptr(mask),
                  nat.ptr(colors), nat.ptr(normals), nat.ptr(comp), nat.ptr(labels), nat.ptr(scal), sp)
@@ -158,6 +180,7 @@ class DensityStream:
             if S[f, 15] != 0.0:
                 raise IndexError("index -1 is out of bounds for axis 0 with size 0")
         K = kdev.cpu().numpy()  # read-back 2
+        self._last_people = (people, offs_h, K)
         jobs = np.zeros((F, 8), dtype=np.float64)
         out_off = scr_off = 0
         dims = []

@@ -1,0 +1,89 @@
+"""Host frames to the density path with the host work and the PCIe copy off the critical path
+(the input step before the hot path).
+
+The drop-in API takes one host NumPy frame per call, uploads it, runs the kernels and reads the
+result back: each frame pays its parse, its copy and its kernels one after the other
+(``app.py:78-84`` -> ``utils/data_processing.py:8-229``).  ``HostFrameFeed`` pipelines a stream of
+frames in batches: a staging thread parses (``load_lidar_data``'s multithreaded C parser for
+PCD / PLY) or takes the frames, packs batch k+1 into a pinned host buffer and issues its H2D copy
+on a copy stream, while the GPU runs batch k through ``DensityStream.run_batch`` (one launch per
+phase over the CSR batch).  Results are the drop-in API's, frame for frame (same kernels); the
+reference's exceptions are raised for the first bad frame.
+"""
+import concurrent.futures
+
+import numpy as np
+import torch
+
+from .data_processing import _reference_shape_errors, load_lidar_data
+from .density_stream import DensityStream
+
+
+class HostFrameFeed:
+    def __init__(self, device=None, batch=8, grid_size=1.0):
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.batch = max(1, int(batch))
+        self.ds = DensityStream(self.device, workers=1, grid_size=grid_size)
+        self.copy_stream = torch.cuda.Stream(device=self.device)
+        self._pinned = [None, None]  # host staging, double-buffered
+        self._dev = [None, None]
+        self._pool = concurrent.futures.ThreadPoolExecutor(max_workers=1)
+
+    def _buffers(self, slot, rows):
+        if self._pinned[slot] is None or self._pinned[slot].shape[0] < rows:
+            cap = max(rows, 1 << 16)
+            self._pinned[slot] = torch.empty((cap, 3), dtype=torch.float64, pin_memory=True)
+            self._dev[slot] = torch.empty((cap, 3), dtype=torch.float64, device=self.device)
+        return self._pinned[slot], self._dev[slot]
+
+    def _stage(self, items, slot, from_files):
+        """(staging thread) frames -> pinned rows -> H2D on the copy stream; returns the device
+        frames (views) and the copy's completion event."""
+        torch.cuda.set_device(self.device)
+        frames = [load_lidar_data(p) if from_files else p for p in items]
+        arrs = []
+        for f in frames:
+            a = np.asarray(f)
+            _reference_shape_errors(a)
+            arrs.append(a)
+        sizes = [len(a) for a in arrs]
+        total = sum(sizes)
+        pin, dev = self._buffers(slot, total)
+        host = pin.numpy()
+        o = 0
+        for a in arrs:
+            host[o:o + len(a)] = a  # int frames convert to float64 here, as the drop-in does
+            o += len(a)
+        ev = torch.cuda.Event()
+        with torch.cuda.stream(self.copy_stream):
+            dev[:total].copy_(pin[:total], non_blocking=True)
+            ev.record(self.copy_stream)
+        views, o = [], 0
+        for n in sizes:
+            views.append(dev[o:o + n])
+            o += n
+        return views, ev
+
+    def _run(self, items, from_files):
+        batches = [items[i:i + self.batch] for i in range(0, len(items), self.batch)]
+        out = []
+        if not batches:
+            return out
+        fut = self._pool.submit(self._stage, batches[0], 0, from_files)
+        for i in range(len(batches)):
+            views, ev = fut.result()
+            # batch i - 1 (slot (i + 1) % 2) is complete: run_batch ends with host read-backs
+            if i + 1 < len(batches):
+                fut = self._pool.submit(self._stage, batches[i + 1], (i + 1) % 2, from_files)
+            torch.cuda.current_stream(self.device).wait_event(ev)
+            out += self.ds.run_batch(views)
+        return out
+
+    def run(self, frames):
+        """frames: host (n_i, 3) arrays -> CrowdDensityModel(grid_size).analyze dict per frame."""
+        return self._run(list(frames), False)
+
+    def run_files(self, paths):
+        """point-cloud files (any format load_lidar_data reads) -> analyze dict per file; the next
+        batch's files are parsed while the current batch's kernels run."""
+        return self._run(list(paths), True)

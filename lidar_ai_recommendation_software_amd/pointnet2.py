@@ -172,33 +172,6 @@ def ball_query_bin(radius, nsample, xyz, grid, slot=0):
     return grid
 
 
-def pack_branch(layers, cfeat):
-    """Host-side packed weight image for lidar_sa_group_mlp_f32 (3-layer branch)."""
-    (w1, b1), (w2, b2), (w3, b3) = layers
-    c1, c2, c3 = w1.shape[1], w2.shape[1], w3.shape[1]
-    lib = nat.load_library()
-    size = lib.lidar_mlp_packed_size(cfeat, c1, c2, c3)
-    out = np.zeros(size, dtype=np.float32)
-    arrs = [np.ascontiguousarray(a, dtype=np.float32) for a in (w1, b1, w2, b2, w3, b3)]
-    nat.check(lib.lidar_mlp_pack_f32(cfeat, c1, c2, c3, *[a.ctypes.data_as(ctypes.c_void_p) for a in arrs],
-                                     out.ctypes.data_as(ctypes.c_void_p)), "lidar_mlp_pack_f32")
-    return out
-
-
-def pack_branch_bf16(layers, cfeat):
-    """Host-side packed image for lidar_sa_group_mlp_bf16 (bf16 fragments + fp32 biases),
-    returned as a uint8 array."""
-    (w1, b1), (w2, b2), (w3, b3) = layers
-    c1, c2, c3 = w1.shape[1], w2.shape[1], w3.shape[1]
-    lib = nat.load_library()
-    size = lib.lidar_mlp_packed_size_bf16(cfeat, c1, c2, c3)
-    out = np.zeros(size, dtype=np.uint8)
-    arrs = [np.ascontiguousarray(a, dtype=np.float32) for a in (w1, b1, w2, b2, w3, b3)]
-    nat.check(lib.lidar_mlp_pack_bf16(cfeat, c1, c2, c3, *[a.ctypes.data_as(ctypes.c_void_p) for a in arrs],
-                                      out.ctypes.data_as(ctypes.c_void_p)), "lidar_mlp_pack_bf16")
-    return out
-
-
 # (xyz_level, c1, c2, c3, nsample) combinations lidar_sa_group_mlp16_f32 instantiates
 MLP16_SHAPES = {(True, 64, 64, 128, 32), (True, 32, 32, 64, 16), (True, 64, 96, 128, 128), (False, 128, 128, 256, 64),
                 (False, 128, 128, 256, 128), (False, 64, 64, 128, 32)}
@@ -309,40 +282,6 @@ def group_mlp_x3(p, q, idx, n, packed, widths, out, out_offset=0, xyz_level=Fals
     return out
 
 
-def group_mlp(xyz, feats, new_xyz, idx, packed, widths, out=None, out_offset=0, bf16=False):
-    """Fused grouping + 3-layer MLP + max over nsample -> (B, M, c3) (or into `out`)."""
-    B, N, _ = xyz.shape
-    M, ns = idx.shape[1], idx.shape[2]
-    cfeat = 0 if feats is None else feats.shape[2]
-    c1, c2, c3 = widths
-    if out is None:
-        out = torch.empty((B, M, c3), dtype=torch.float32, device=xyz.device)
-    _dev_check(xyz, new_xyz, idx, packed, out)
-    if feats is not None and (not feats.is_cuda or feats.stride(2) != 1
-                              or feats.stride(0) != feats.shape[1] * feats.stride(1)):
-        raise ValueError("group_mlp: feats must be CUDA rows with unit channel stride")
-    nat.call("lidar_sa_group_mlp_bf16" if bf16 else "lidar_sa_group_mlp_f32", nat.handle(xyz.device.index),
-             nat.ptr(xyz), nat.ptr(feats),
-             feats.stride(1) if feats is not None else 0, nat.ptr(new_xyz), nat.ptr(idx), B, N, M, ns, cfeat, c1, c2, c3,
-             nat.ptr(packed), nat.ptr(out), out.shape[-1], out_offset, nat.stream_ptr())
-    return out
-
-
-def group_mlp_pre(p, q, idx, n, packed, cfeat, widths, out, out_offset=0):
-    """group_mlp with layer 1 applied per point beforehand (layer1_per_point):
-    p rows b*n + k = [f, x] W1 + b1, q rows b*M + c = centre W1_xyz; idx (B, M, ns)
-    -> out[..., off:off+c3] (out (B, M, stride))."""
-    B, M, ns = idx.shape
-    c1, c2, c3 = widths
-    if p.shape[0] < B * n or q.shape[0] < B * M or p.shape[1] < c1 or q.shape[1] != p.shape[1]:
-        raise ValueError("group_mlp_pre: p/q shapes do not match the batch")
-    _dev_check(p, q, idx, packed, out)
-    nat.call("lidar_sa_group_mlp_pre_f32", nat.handle(p.device.index), nat.ptr(p), p.shape[1], nat.ptr(q),
-             nat.ptr(idx), B, n, M, ns, cfeat, c1, c2, c3, nat.ptr(packed), nat.ptr(out),
-             out.shape[-1], out_offset, nat.stream_ptr())
-    return out
-
-
 def layer1_weights(layer, cfeat, to_dev):
     """(W1 (3 + cfeat, c1), b1) -> the per-point GEMM operands of layer1_per_point:
     w1 rows [f..., x, y, z, 0-pad] (k padded to 16), wq rows [x, y, z, 0-pad] (16), columns
@@ -361,14 +300,15 @@ def layer1_weights(layer, cfeat, to_dev):
     return {"w1": to_dev(w1p), "b1": to_dev(bp), "wq": to_dev(wq), "zero": to_dev(np.zeros(cp, np.float32))}
 
 
-def layer1_per_point(x_rows, xyz, cfeat, new_xyz, branches, x3=False, x3s=False):
+def layer1_per_point(x_rows, xyz, cfeat, new_xyz, branches, x3=True):
     """Layer 1 of every branch of a level, per point instead of per grouped row.
 
     x_rows: (R, kp) padded rows [f (cfeat), x, y, z, 0...] of the level's B*N points
     (R = B*N rounded up to 128; the previous level wrote f in place), xyz (B, N, 3);
     new_xyz (B, M, 3).  Returns per branch (P, Q): P = x_rows W1' + b1 (R, c1),
     Q = [c, 0] W1_xyz' (B*M rounded to 128, c1), both without ReLU (columns padded to a
-    multiple of 128 with zero weights)."""
+    multiple of 128 with zero weights).  x3: on the split-bf16 GEMM (fp32 rows in, split in the
+    tile loop); else the native fp32 MFMA GEMM."""
     B, N, _ = xyz.shape
     M = new_xyz.shape[1]
     R, kp = x_rows.shape
@@ -379,19 +319,14 @@ def layer1_per_point(x_rows, xyz, cfeat, new_xyz, branches, x3=False, x3s=False)
     cpad = torch.zeros((rq, 16), dtype=torch.float32, device=dev)
     nat.call("lidar_concat_xyz_pad_f32", h, nat.ptr(new_xyz), B * M, nat.ptr(cpad), 16, 0, nat.stream_ptr())
     out = []
-    if x3 and x3s:  # fp32 rows in (split in the tile loop: one column tile re-reads nothing)
-        xs, cs = x_rows, cpad
-        for br in branches:
-            pre = br["pre"]
-            cp = pre["w1"].shape[1]
-            out.append((dense_x3s(xs, pre["w1_x3"], pre["b1"], cp, relu=False),
-                        dense_x3s(cs, pre["wq_x3"], pre["zero"], cp, relu=False)))
-        return out
     for br in branches:
         pre = br["pre"]
-        P = dense(x_rows, pre["w1"], pre["b1"], relu=False, x3=x3, wpack=pre.get("w1_x3") if x3 else None)
-        Q = dense(cpad, pre["wq"], pre["zero"], relu=False, x3=x3, wpack=pre.get("wq_x3") if x3 else None)
-        out.append((P, Q))
+        cp = pre["w1"].shape[1]
+        if x3:
+            out.append((dense_x3s(x_rows, pre["w1_x3"], pre["b1"], cp, relu=False),
+                        dense_x3s(cpad, pre["wq_x3"], pre["zero"], cp, relu=False)))
+        else:
+            out.append((dense(x_rows, pre["w1"], pre["b1"], relu=False), dense(cpad, pre["wq"], pre["zero"], relu=False)))
     return out
 
 
@@ -406,23 +341,22 @@ def pack_dense_x3(w):
     return out
 
 
-def dense(x, w, b, relu=True, pool_rows=0, out=None, x3=False, wpack=None):
-    """x (rows, k) @ w (k, cout) + b [-> ReLU] [-> max over runs of pool_rows rows].
-    x3: on the split-bf16 GEMM (lidar_dense_x3_f32; fp32 arithmetic within 1e-4); wpack =
-    pack_dense_x3(w) skips the per-call packing of w."""
+def dense(x, w, b, relu=True, pool_rows=0, out=None):
+    """x (rows, k) @ w (k, cout) + b [-> ReLU] [-> max over runs of pool_rows rows] on the native
+    fp32 matrix cores (lidar_dense_f32)."""
     rows, k = x.shape
     cout = w.shape[1]
     if out is None:
         shape = (rows // pool_rows, cout) if pool_rows else (rows, cout)
         out = (torch.zeros if pool_rows else torch.empty)(shape, dtype=torch.float32, device=x.device)
-    _dev_check(x, w, b, out, wpack)
-    if x3 and wpack is not None:
-        nat.call("lidar_dense_x3p_f32", nat.handle(x.device.index), nat.ptr(x), rows, k, nat.ptr(wpack),
-                 nat.ptr(b), cout, 1 if relu else 0, pool_rows, nat.ptr(out), nat.stream_ptr())
-        return out
-    nat.call("lidar_dense_x3_f32" if x3 else "lidar_dense_f32", nat.handle(x.device.index), nat.ptr(x), rows, k,
-             nat.ptr(w), nat.ptr(b), cout, 1 if relu else 0, pool_rows, nat.ptr(out), nat.stream_ptr())
+    _dev_check(x, w, b, out)
+    nat.call("lidar_dense_f32", nat.handle(x.device.index), nat.ptr(x), rows, k, nat.ptr(w), nat.ptr(b), cout,
+             1 if relu else 0, pool_rows, nat.ptr(out), nat.stream_ptr())
     return out
+
+
+def dense_relu(x, w, b, pool_rows=0, out=None):
+    return dense(x, w, b, True, pool_rows, out)
 
 
 class SplitPlanes:
@@ -484,149 +418,120 @@ def dense_x3s(a, wpack, b, cout, relu=True, split_out=False, pool_rows=0, out=No
     return res
 
 
-def dense_relu(x, w, b, pool_rows=0, out=None, x3=False, wpack=None):
-    if x3:
-        return dense(x, w, b, True, pool_rows, out, x3=True, wpack=wpack)
-    rows, k = x.shape
-    cout = w.shape[1]
-    if out is None:
-        shape = (rows // pool_rows, cout) if pool_rows else (rows, cout)
-        out = (torch.zeros if pool_rows else torch.empty)(shape, dtype=torch.float32, device=x.device)
-    _dev_check(x, w, b, out)
-    nat.call("lidar_dense_relu_f32", nat.handle(x.device.index), nat.ptr(x), rows, k, nat.ptr(w),
-             nat.ptr(b), cout, pool_rows, nat.ptr(out), nat.stream_ptr())
-    return out
-
-
 # ----------------------------------------------------------------------- backbone
 class _Timers:
-    """Optional per-launch HIP-event timing on the launching stream (bench.py)."""
+    """Optional per-launch HIP-event timing on the launching stream (bench.py): per kernel name
+    the launches made, each with the number of frames it processed."""
 
     def __init__(self):
         self.ev = {}
 
-    def __call__(self, name, fn, *a, **k):
+    def __call__(self, name, frames, fn, *a, **k):
         s = torch.cuda.current_stream()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(s)
         out = fn(*a, **k)
         e1.record(s)
-        self.ev.setdefault(name, []).append((e0, e1))
+        self.ev.setdefault(name, []).append((e0, e1, int(frames)))
         return out
 
+    def totals(self):
+        """{name: (launches, frames over all launches, total ms)} (waits for the events)."""
+        return {k: (len(v), sum(f for _, _, f in v), sum(a.elapsed_time(b) for a, b, _ in v))
+                for k, v in self.ev.items()}
+
     def mean_ms(self):
-        return {k: sum(a.elapsed_time(b) for a, b in v) / len(v) for k, v in self.ev.items()}
+        return {k: t / n for k, (n, _, t) in self.totals().items()}
 
 
-def _call(timers, name, fn, *a, **k):
-    return timers(name, fn, *a, **k) if timers is not None else fn(*a, **k)
+def _call(timers, name, frames, fn, *a, **k):
+    return timers(name, frames, fn, *a, **k) if timers is not None else fn(*a, **k)
 
 
 class PointNet2Backbone:
     """SSG / MSG PointNet++ encoder on liblidar_amd.  ``forward(xyz)`` -> global feature
-    (B, C_last) plus the per-level (new_xyz, features, fps_idx)."""
+    (B, C_last) plus, with keep_levels, per level (new_xyz, features, fps_idx, [ball-query
+    idx per branch])."""
 
-    def __init__(self, cfg=SSG, weights=None, device="cuda", seed=0, dtype="f32", pre_layer1=True, mlp16="pre", x3=True,
-                 x3s=True, x1=True):
-        """dtype "bf16": the SA branches run on bf16 MFMA (inputs/activations/weights rounded
-        to bf16, fp32 accumulation; BASELINE configs[4]); group_all stays fp32.
-        pre_layer1 (fp32, levels with point features): layer 1 runs per point as a GEMM
-        and the fused kernel starts at layer 2 (layer1_per_point / group_mlp_pre).
-        mlp16 (fp32): branches whose shape lidar_sa_group_mlp16_f32 instantiates run on the
-        16-row kernels (MLP16_SHAPES); "pre" / "xyz": only the per-point-layer-1 / the
-        xyz-only levels.
-        x3 (fp32): the same branches on the split-bf16 kernels (lidar_sa_group_mlp_x3_f32;
-        True, or "pre" / "xyz" for one kind of level).
-        x3s (with x3): the dense layers on the split-plane GEMM (dense_x3s / split_x3).
-        x1 (bf16): the branches on the fused 16-row kernel with one bf16 product per MFMA
-        (lidar_sa_group_mlp_x1_f32), feature levels with the per-point feature part of layer 1."""
+    def __init__(self, cfg=SSG, weights=None, device="cuda", seed=0, dtype="f32", x3=True):
+        """dtype "f32" (the fp32 contract: features within 1e-4 of the fp32 oracle): x3=True (default)
+        runs the MLPs on the bf16 matrix cores in split-bf16 arithmetic (lidar_sa_group_mlp_x3_f32,
+        lidar_dense_x3s_f32), x3=False on the native fp32 matrix cores (lidar_sa_group_mlp16_f32,
+        lidar_dense_f32) — the strict-fp32 path.
+        dtype "bf16" (BASELINE configs[4]): the SA branches in the bf16 spec on the X1 kernels
+        (inputs, activations and weights rounded to bf16, fp32 accumulation); group_all stays in
+        fp32 arithmetic on the x3 GEMM.
+        Levels with point features run layer 1 per point (layer1_per_point / layer1_points_x1) and
+        the fused kernel from layer 2 on."""
         if dtype not in ("f32", "bf16"):
             raise ValueError("dtype must be 'f32' or 'bf16'")
         self.bf16 = dtype == "bf16"
+        self.x3 = bool(x3) or self.bf16  # the dense GEMMs (per-point layer 1, group_all)
         self.cfg = cfg
         self.device = torch.device(device)
         self.weights = weights if weights is not None else init_weights(cfg, seed)
         self.levels = []
         cfeat = 0
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).to(self.device)
         for lvl, wl in zip(cfg["levels"], self.weights):
+            kp = (cfeat + 3 + 15) // 16 * 16
             if lvl.get("group_all"):
                 (w1, b1), (w2, b2), (w3, b3) = wl[0]
-                kp = (cfeat + 3 + 15) // 16 * 16
                 # canonical rows [x, y, z, f...] -> physical input [f..., x, y, z, 0-pad]
                 w1p = np.zeros((kp, w1.shape[1]), np.float32)
                 w1p[:cfeat] = w1[3:]
                 w1p[cfeat:cfeat + 3] = w1[:3]
-                t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(self.device)
-                self.levels.append({"group_all": True, "k": kp, "cfeat": cfeat,
-                                    "w": [t(w1p), t(w2), t(w3)], "b": [t(b1), t(b2), t(b3)]})
-                cfeat = w3.shape[1]
-            else:
-                pre = pre_layer1 and not self.bf16 and cfeat > 0
-                kp = (cfeat + 3 + 15) // 16 * 16
-                t = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).to(self.device)
-                branches = []
-                for (r, ns, widths, layers) in zip(lvl["radii"], lvl["nsamples"], lvl["mlps"], wl):
-                    pk = pack_branch_bf16(layers, cfeat) if self.bf16 else pack_branch(layers, cfeat)
-                    packed = torch.from_numpy(pk).to(self.device)
-                    br = {"r": r, "ns": ns, "widths": widths, "packed": packed}
-                    xyz_level = cfeat == 0
-                    use16 = mlp16 is True or (mlp16 == "pre" and pre) or (mlp16 == "xyz" and xyz_level)
-                    if (use16 and not self.bf16 and (pre or xyz_level)
-                            and (xyz_level, *widths, ns) in MLP16_SHAPES):
-                        br["packed16"] = torch.from_numpy(pack_branch16(layers, xyz_level)).to(self.device)
-                    usex3 = x3 is True or (x3 == "pre" and pre) or (x3 == "xyz" and xyz_level)
-                    if (usex3 and not self.bf16 and (pre or xyz_level)
-                            and (xyz_level, *widths, ns) in MLP16_SHAPES):
-                        br["packed_x3"] = torch.from_numpy(pack_branch_x3(layers, xyz_level)).to(self.device)
-                    if pre:
-                        br["pre"] = layer1_weights(layers[0], cfeat, t)
-                    if self.bf16 and x1 and (xyz_level, *widths, ns) in MLP16_SHAPES:
-                        br["packed_x1"] = torch.from_numpy(pack_branch_x1(layers)).to(self.device)
-                        if not xyz_level:  # W1_f: rows [f..., (x, y, z) = 0, 0-pad], columns to 128
-                            w1, b1 = layers[0]
-                            cp = (w1.shape[1] + 127) // 128 * 128
-                            w1f = np.zeros((kp, cp), np.float32)
-                            w1f[:cfeat, :w1.shape[1]] = w1[3:]
-                            b1p = np.zeros(cp, np.float32)
-                            b1p[:w1.shape[1]] = b1
-                            br["pre_x1"] = {"w1f": t(w1f), "b1": t(b1p)}
-                            br["pre_x1"]["w1f_x3"] = pack_dense_x3(br["pre_x1"]["w1f"])
-                    branches.append(br)
-                entry = {"div": lvl["npoint_div"], "branches": branches, "cfeat": cfeat}
-                if pre:
-                    entry.update(pre=True, k=kp)
-                if cfeat > 0 and branches and all("pre_x1" in br for br in branches):
-                    entry.update(pre=True, pre_x1=True, k=kp)  # the previous level writes padded rows
+                entry = {"group_all": True, "k": kp, "cfeat": cfeat, "w": [t(w1p), t(w2), t(w3)],
+                         "b": [t(b1), t(b2), t(b3)]}
+                if self.x3:  # packed once into x3 B fragments
+                    entry["w_x3"] = [pack_dense_x3(w) for w in entry["w"]]
                 self.levels.append(entry)
-                cfeat = sum(w[-1] for w in lvl["mlps"])
+                cfeat = w3.shape[1]
+                continue
+            xyz_level = cfeat == 0
+            branches = []
+            for (r, ns, widths, layers) in zip(lvl["radii"], lvl["nsamples"], lvl["mlps"], wl):
+                if (xyz_level, *widths, ns) not in MLP16_SHAPES:
+                    raise ValueError(f"SA branch (widths {widths}, nsample {ns}, xyz level {xyz_level}) has no "
+                                     f"instantiated kernel; instantiated: {sorted(MLP16_SHAPES)}")
+                br = {"r": r, "ns": ns, "widths": widths}
+                if self.bf16:
+                    br["packed_x1"] = torch.from_numpy(pack_branch_x1(layers)).to(self.device)
+                    if not xyz_level:  # W1_f: rows [f..., (x, y, z) = 0, 0-pad], columns to 128
+                        w1, b1 = layers[0]
+                        cp = (w1.shape[1] + 127) // 128 * 128
+                        w1f = np.zeros((kp, cp), np.float32)
+                        w1f[:cfeat, :w1.shape[1]] = w1[3:]
+                        b1p = np.zeros(cp, np.float32)
+                        b1p[:w1.shape[1]] = b1
+                        br["pre_x1"] = {"w1f": t(w1f), "b1": t(b1p)}
+                        br["pre_x1"]["w1f_x3"] = pack_dense_x3(br["pre_x1"]["w1f"])
+                else:
+                    if x3:
+                        br["packed_x3"] = torch.from_numpy(pack_branch_x3(layers, xyz_level)).to(self.device)
+                    else:
+                        br["packed16"] = torch.from_numpy(pack_branch16(layers, xyz_level)).to(self.device)
+                    if not xyz_level:
+                        br["pre"] = layer1_weights(layers[0], cfeat, t)
+                        if x3:
+                            br["pre"]["w1_x3"] = pack_dense_x3(br["pre"]["w1"])
+                            br["pre"]["wq_x3"] = pack_dense_x3(br["pre"]["wq"])
+                branches.append(br)
+            entry = {"div": lvl["npoint_div"], "branches": branches, "cfeat": cfeat}
+            if not xyz_level:  # the previous level writes this level's padded rows [f, x, y, z, 0]
+                entry.update(pre=True, k=kp)
+            self.levels.append(entry)
+            cfeat = sum(w[-1] for w in lvl["mlps"])
         self.out_channels = cfeat
-        # x3 on: the dense layers (per-point layer 1, group_all) on the split-bf16 GEMM too
-        # (bf16 too: group_all stays in fp32 arithmetic, DESIGN.md §3 — x3 is that contract)
-        self.x3_dense = bool(x3)
-        # x3s: the dense layers take split planes (split once per input, dense1 -> dense2 -> dense3
-        # hand them over) instead of splitting fp32 activations inside every GEMM tile
-        self.x3_split = self.x3_dense and bool(x3s)
-        if self.x3_dense:  # the dense layers' weights packed once into x3 B fragments
-            for lvl in self.levels:
-                if lvl.get("group_all"):
-                    lvl["w_x3"] = [pack_dense_x3(w) for w in lvl["w"]]
-                for br in lvl.get("branches", []):
-                    if "pre" in br:
-                        br["pre"]["w1_x3"] = pack_dense_x3(br["pre"]["w1"])
-                        br["pre"]["wq_x3"] = pack_dense_x3(br["pre"]["wq"])
         self.timers = None  # set to a _Timers() to time every launch
 
-    def forward_from_sa1_fps(self, xyz, idx1, new_xyz1, fz1, gidx1=None, grid1=None, pre=None):
-        """forward() with level 0's FPS (and ball queries, or the ball-query binning of the
-        frames) already computed (StreamingSSG); `pre` adds precomputed later levels."""
-        pre = dict(pre or {})
-        pre[0] = {"fps": (idx1, new_xyz1, fz1), "bq": gidx1, "grid": grid1}
-        return self.forward(xyz, pre=pre)[0]
+    def forward_from_sa1_fps(self, xyz, idx1, new_xyz1, fz1, gidx1, keep_levels=False):
+        """forward() with level 0's FPS and ball queries already computed (StreamingSSG)."""
+        return self.forward(xyz, keep_levels, pre={0: {"fps": (idx1, new_xyz1, fz1), "bq": gidx1}})
 
     def forward(self, xyz, keep_levels=False, pre=None):
-        """pre: {level: {"fps": (idx, new_xyz, first_zero), "bq": [gidx per branch] or None,
-        "grid": ball-query grid of this level's input points or None}} — work already done
-        for those levels (StreamingSSG's side streams); every other step runs here."""
+        """pre: {level: {"fps": (idx, new_xyz, first_zero), "bq": [gidx per branch]}} — work already
+        done for those levels (StreamingSSG's side streams); every other step runs here."""
         pre = pre or {}
         B, N, _ = xyz.shape
         N0 = N  # npoint_div is relative to the input frame (N/16, N/64)
@@ -634,6 +539,7 @@ class PointNet2Backbone:
         rows = None  # flat padded (R, k) rows behind `feats` when the next level reads them
         out_levels = []
         fz = None  # previous level's FPS first_zero (nested-FPS shortcut)
+        t = self.timers
         for li, lvl in enumerate(self.levels):
             if lvl.get("group_all"):
                 return self._group_all(xyz, feats, lvl, rows), out_levels
@@ -643,8 +549,8 @@ class PointNet2Backbone:
                 idx, new_xyz, nfz = pl["fps"]
             else:
                 nfz = torch.empty(B, dtype=torch.int32, device=xyz.device)
-                idx, new_xyz = _call(self.timers, f"sa{li + 1}_fps", farthest_point_sample, xyz, M,
-                                     return_xyz=True, first_zero=nfz, prefix_ok=fz)
+                idx, new_xyz = _call(t, f"sa{li + 1}_fps", B, farthest_point_sample, xyz, M, return_xyz=True,
+                                     first_zero=nfz, prefix_ok=fz)
             fz = nfz
             ctot = sum(br["widths"][-1] for br in lvl["branches"])
             nxt = self.levels[li + 1] if li + 1 < len(self.levels) else None
@@ -656,44 +562,37 @@ class PointNet2Backbone:
             out_rows = torch.empty((R, stride), dtype=torch.float32, device=xyz.device)
             out = out_rows[:B * M].view(B, M, stride)
             pq = None
-            if lvl.get("pre_x1"):
-                pq = _call(self.timers, f"sa{li + 1}_layer1_points", layer1_points_x1, rows, xyz, lvl["cfeat"],
+            if lvl.get("pre") and self.bf16:
+                pq = _call(t, f"sa{li + 1}_layer1_points", B, layer1_points_x1, rows, xyz, lvl["cfeat"],
                            lvl["branches"])
             elif lvl.get("pre"):
-                pq = _call(self.timers, f"sa{li + 1}_layer1_points", layer1_per_point, rows, xyz, lvl["cfeat"],
-                           new_xyz, lvl["branches"], x3=self.x3_dense, x3s=self.x3_split)
+                pq = _call(t, f"sa{li + 1}_layer1_points", B, layer1_per_point, rows, xyz, lvl["cfeat"], new_xyz,
+                           lvl["branches"], x3=self.x3)
             off = 0
+            gidxs = []
             for bi_, br in enumerate(lvl["branches"]):
                 tag = f"sa{li + 1}" + (f"_b{bi_}" if len(lvl["branches"]) > 1 else "")
                 if pl.get("bq") is not None:
                     gidx = pl["bq"][bi_]
                 else:
-                    gidx = _call(self.timers, f"{tag}_ball_query", ball_query, br["r"], br["ns"], xyz, new_xyz,
-                                 grid=pl.get("grid"))
-                if "packed_x1" in br:
+                    gidx = _call(t, f"{tag}_ball_query", B, ball_query, br["r"], br["ns"], xyz, new_xyz)
+                gidxs.append(gidx)
+                if self.bf16:
                     if pq is not None:
-                        _call(self.timers, f"{tag}_group_mlp", group_mlp_x1, pq[bi_], gidx, N, br["packed_x1"],
+                        _call(t, f"{tag}_group_mlp", B, group_mlp_x1, pq[bi_], gidx, N, br["packed_x1"],
                               br["widths"], out=out, out_offset=off, xyz=xyz, centres=new_xyz)
                     else:
-                        _call(self.timers, f"{tag}_group_mlp", group_mlp_x1, xyz, gidx, N, br["packed_x1"],
+                        _call(t, f"{tag}_group_mlp", B, group_mlp_x1, xyz, gidx, N, br["packed_x1"],
                               br["widths"], out=out, out_offset=off, centres=new_xyz)
-                elif "packed_x3" in br:
-                    p16, q16 = (pq[bi_] if pq is not None else (xyz, new_xyz))
-                    _call(self.timers, f"{tag}_group_mlp", group_mlp_x3, p16, q16, gidx, N, br["packed_x3"],
-                          br["widths"], out=out, out_offset=off, xyz_level=pq is None)
-                elif "packed16" in br:
-                    p16, q16 = (pq[bi_] if pq is not None else (xyz, new_xyz))
-                    _call(self.timers, f"{tag}_group_mlp", group_mlp16, p16, q16, gidx, N, br["packed16"],
-                          br["widths"], out=out, out_offset=off, xyz_level=pq is None)
-                elif pq is not None:
-                    _call(self.timers, f"{tag}_group_mlp", group_mlp_pre, pq[bi_][0], pq[bi_][1], gidx, N,
-                          br["packed"], lvl["cfeat"], br["widths"], out=out, out_offset=off)
                 else:
-                    _call(self.timers, f"{tag}_group_mlp", group_mlp, xyz, feats, new_xyz, gidx, br["packed"],
-                          br["widths"], out=out, out_offset=off, bf16=self.bf16)
+                    p16, q16 = (pq[bi_] if pq is not None else (xyz, new_xyz))
+                    kern = group_mlp_x3 if "packed_x3" in br else group_mlp16
+                    _call(t, f"{tag}_group_mlp", B, kern, p16, q16, gidx, N,
+                          br["packed_x3"] if "packed_x3" in br else br["packed16"], br["widths"], out=out,
+                          out_offset=off, xyz_level=pq is None)
                 off += br["widths"][-1]
             if keep_levels:
-                out_levels.append((new_xyz, out[..., :ctot], idx))
+                out_levels.append((new_xyz, out[..., :ctot], idx, gidxs))
             xyz, feats, rows = new_xyz, (out[..., :ctot] if padded else out), out_rows
             N = M
         return feats, out_levels
@@ -720,52 +619,18 @@ class PointNet2Backbone:
             x2 = x.view(B, M, kp)[:, sel].reshape(B * mp, kp).contiguous()
             M, rows = mp, B * mp
         t = self.timers
-        wp = lvl.get("w_x3") if self.x3_dense else None
-        if wp and self.x3_split:  # split once; dense1/dense2 hand split planes to the next layer
-            ws, bs = lvl["w"], lvl["b"]
-            h1 = _call(t, "sa3_dense1", dense_x3s, x2, wp[0], bs[0], ws[0].shape[1], split_out=True)
-            h2 = _call(t, "sa3_dense2", dense_x3s, h1, wp[1], bs[1], ws[1].shape[1], split_out=True)
-            return _call(t, "sa3_dense3_pool", dense_x3s, h2, wp[2], bs[2], ws[2].shape[1], pool_rows=M)
-        h1 = _call(t, "sa3_dense1", dense_relu, x2, lvl["w"][0], lvl["b"][0], x3=self.x3_dense,
-                   wpack=wp[0] if wp else None)
-        h2 = _call(t, "sa3_dense2", dense_relu, h1, lvl["w"][1], lvl["b"][1], x3=self.x3_dense,
-                   wpack=wp[1] if wp else None)
-        out = torch.zeros((rows // M, lvl["w"][2].shape[1]), dtype=torch.float32, device=x.device)
-        return _call(t, "sa3_dense3_pool", dense_relu, h2, lvl["w"][2], lvl["b"][2], pool_rows=M, out=out,
-                     x3=self.x3_dense, wpack=wp[2] if wp else None)
+        ws, bs = lvl["w"], lvl["b"]
+        if self.x3:  # dense1 / dense2 hand split planes to the next layer; dense3 fuses the max-pool
+            wp = lvl["w_x3"]
+            h1 = _call(t, "sa3_dense1", B, dense_x3s, x2, wp[0], bs[0], ws[0].shape[1], split_out=True)
+            h2 = _call(t, "sa3_dense2", B, dense_x3s, h1, wp[1], bs[1], ws[1].shape[1], split_out=True)
+            return _call(t, "sa3_dense3_pool", B, dense_x3s, h2, wp[2], bs[2], ws[2].shape[1], pool_rows=M)
+        h1 = _call(t, "sa3_dense1", B, dense_relu, x2, ws[0], bs[0])
+        h2 = _call(t, "sa3_dense2", B, dense_relu, h1, ws[1], bs[1])
+        out = torch.zeros((rows // M, ws[2].shape[1]), dtype=torch.float32, device=x.device)
+        return _call(t, "sa3_dense3_pool", B, dense_relu, h2, ws[2], bs[2], pool_rows=M, out=out)
 
     __call__ = forward
-
-
-def ctypes_void(p):
-    import ctypes
-    return ctypes.c_void_p(p)
-
-
-def cu_masks(device, side_cus, layout="xcd"):
-    """(side mask words, main mask words) over the device's CUs: `side_cus` CUs for the side
-    streams, the complement for the main stream."""
-    import ctypes
-    n = ctypes.c_int32(0)
-    nat.call("lidar_device_cu_count", int(device), ctypes.byref(n))
-    n = n.value
-    if not 0 < side_cus < n:
-        raise ValueError(f"side_cus must be in (0, {n})")
-    if layout == "xcd" and n % 8 == 0:
-        per, k = n // 8, max(1, side_cus // 8)
-        side = {x * per + j for x in range(8) for j in range(k)}
-    elif layout == "low":
-        side = set(range(side_cus))
-    else:
-        raise ValueError("cu_layout must be 'xcd' or 'low'")
-    words = (n + 31) // 32
-    sm, mm = [0] * words, [0] * words
-    for c in range(n):
-        if c in side:
-            sm[c // 32] |= 1 << (c % 32)
-        else:
-            mm[c // 32] |= 1 << (c % 32)
-    return sm, mm
 
 
 # ------------------------------------------------------------------ streaming executor
@@ -773,48 +638,40 @@ class StreamingSSG:
     """Frame-batch pipeline for a continuous feed (SSG/MSG backbone).
 
     SA1's farthest-point sampling is a serial chain of N/16 argmax steps per frame
-    (latency-bound, one workgroup per frame), while everything after it (ball queries,
-    fused MFMA MLPs, SA2's nested FPS, group_all) fills the whole GPU.  `run` therefore
-    issues later batches' SA1 FPS (+ level-0 ball queries) on side streams (own library
-    handles / workspaces) while batch k's remaining levels run on the main stream; events
-    order the hand-off and a ring of `depth + 1` output slots bounds memory.
+    (latency-bound, one workgroup per frame), while everything after it (fused MFMA MLPs,
+    SA2's nested FPS and ball queries, group_all) fills the whole GPU.  Later batches' SA1 FPS
+    and level-0 ball queries therefore run on `depth` side streams (own library handles /
+    workspaces) while earlier batches' remaining levels run on the main stream; events order
+    the hand-off and a ring of `depth + 1` slots bounds memory.
 
     fps_group = G > 1: G consecutive batches are staged into one (G*B, N, 3) buffer; one
     side-stream launch runs their SA1 FPS (G*B workgroups share the serial chain of steps
     without needing more streams than the device's hardware queues) and one main-stream
     pass runs their MFMA levels (larger launches fill the chip better).  Every operator is
     per frame, so results are identical to ``PointNet2Backbone.forward`` per batch.
+
+    ``run(batches)`` processes a finite list (pipeline fill and drain included); ``feed()``
+    returns a persistent feed whose ``push(batch)`` keeps `depth` groups in flight (the steady
+    state of a LiDAR stream) and ``flush()`` drains it.
     """
 
-    def __init__(self, backbone, batch, n, depth=1, side_priority=0, side_cus=0, cu_layout="xcd", fps_group=1,
-                 bq_on_main=False, fps_threads=0, level1_on_side=False, shared_bin=False, reserve=True, ramp=True):
-        """side_cus > 0: the SA1 FPS / ball-query streams run on `side_cus` CUs and the
-        main stream on the rest (CU-masked HIP streams; measured slower).
-        cu_layout "xcd" takes side_cus/8 CUs of each of the 8 XCDs (mask bit = 32*xcd + cu),
-        "low" the lowest-numbered CUs."""
+    def __init__(self, backbone, batch, n, depth=1, fps_group=1, fps_threads=0, side_priority=0, ramp=True,
+                 reserve=True, keep_levels=False):
+        """fps_threads: SA1 FPS workgroup size (0 = 1024; 512: half the CU footprint beside the
+        MLPs).  ramp: in run(), the first groups hold 1, 2, ... batches (a shorter pipeline fill).
+        keep_levels: every output is (global feature, per-level (new_xyz, features, fps idx,
+        [ball-query idx per branch])) instead of the global feature alone."""
         self.bb = backbone
         self.B, self.N, self.depth, self.G = batch, n, depth, max(1, int(fps_group))
-        self.ramp = bool(ramp)  # first groups of 1, 2, ... batches (shorter pipeline fill)
-        self.bq_on_main = bool(bq_on_main)  # level-0 ball queries on the main stream instead
-        self.fps_threads = int(fps_threads)  # SA1 FPS workgroup size (0 = 1024; 512: half the CU footprint)
-        # level1_on_side: SA2's FPS (over SA1's centres) and ball queries depend only on SA1's FPS
-        # output, so they can run on the side stream too (balances the two chains)
-        lvl1 = backbone.levels[1] if len(backbone.levels) > 1 else None
-        self.l1 = bool(level1_on_side) and lvl1 is not None and not lvl1.get("group_all")
+        self.ramp = bool(ramp)
+        self.fps_threads = int(fps_threads)
+        self.keep = bool(keep_levels)
         dev = backbone.device
         lvl0 = backbone.levels[0]
         self.M1 = max(1, n // lvl0["div"])
-        self._owned = []
-        self.main = None
-        if side_cus:
-            side, main = cu_masks(dev.index, side_cus, cu_layout)
-            mk = lambda m: self._masked_stream(dev, m)
-            self.fps_streams = [mk(side) for _ in range(depth)]
-            self.main = mk(main)
-        else:
-            # side_priority < 0 puts the latency-bound FPS chains ahead of the MLP waves in
-            # the dispatcher (HIP stream priority); results do not depend on it
-            self.fps_streams = [torch.cuda.Stream(device=dev, priority=side_priority) for _ in range(depth)]
+        # side_priority < 0 puts the latency-bound FPS chains ahead of the MLP waves in the
+        # dispatcher (HIP stream priority); results do not depend on it
+        self.fps_streams = [torch.cuda.Stream(device=dev, priority=side_priority) for _ in range(depth)]
         nslot = depth + 1
         GB = self.G * batch
         self.stage = [torch.empty((GB, n, 3), dtype=torch.float32, device=dev) if self.G > 1 else None
@@ -822,16 +679,8 @@ class StreamingSSG:
         self.idx = [torch.empty((GB, self.M1), dtype=torch.int32, device=dev) for _ in range(nslot)]
         self.cxyz = [torch.empty((GB, self.M1, 3), dtype=torch.float32, device=dev) for _ in range(nslot)]
         self.fz = [torch.empty(GB, dtype=torch.int32, device=dev) for _ in range(nslot)]
-        # level-0 ball queries of every branch ride on the FPS stream too
         self.gidx = [[torch.empty((GB, self.M1, br["ns"]), dtype=torch.int32, device=dev)
                       for br in lvl0["branches"]] for _ in range(nslot)]
-        # bq_on_main: the level-0 frames are binned for the ball query on the side stream
-        # (it depends only on the frames), once for all branches at the largest radius
-        # the level-0 frames are binned once per group (largest radius, valid for every branch's
-        # query) — on the side stream, for the main stream's queries (bq_on_main) or its own
-        # (shared_bin=False: each side-stream query bins for its own radius)
-        self.grid = [ball_query_grid_buffer(GB, n, dev) if (self.bq_on_main or shared_bin) and n >= BQ_GRID_MIN_N
-                     else None for _ in range(nslot)]
         # setup-time workspace sizing of the side handles (FPS + ball queries), so no stage's
         # first call allocates (lidar_reserve; a grow re-allocates after a device sync)
         if reserve:
@@ -839,44 +688,20 @@ class StreamingSSG:
             need = max(lib.lidar_fps_workspace_bytes(GB, n), lib.lidar_ball_query_grid_bytes(GB, n))
             for sl in range(1, depth + 1):
                 nat.call("lidar_reserve", nat.handle(dev.index, sl), need)
-        if self.l1:
-            self.M2 = max(1, n // lvl1["div"])
-            self.idx2 = [torch.empty((GB, self.M2), dtype=torch.int32, device=dev) for _ in range(nslot)]
-            self.cxyz2 = [torch.empty((GB, self.M2, 3), dtype=torch.float32, device=dev) for _ in range(nslot)]
-            self.fz2 = [torch.empty(GB, dtype=torch.int32, device=dev) for _ in range(nslot)]
-            self.gidx2 = [[torch.empty((GB, self.M2, br["ns"]), dtype=torch.int32, device=dev)
-                           for br in lvl1["branches"]] for _ in range(nslot)]
         self.fps_done = [torch.cuda.Event() for _ in range(nslot)]
         self.slot_free = [torch.cuda.Event() for _ in range(nslot)]
         for e in self.slot_free:
             e.record(torch.cuda.current_stream(dev))
 
-    def _masked_stream(self, dev, mask):
-        import ctypes
-        ptr = ctypes.c_void_p()
-        arr = (ctypes.c_uint32 * len(mask))(*mask)
-        nat.call("lidar_stream_create_cu_mask", dev.index, ctypes.cast(arr, ctypes.c_void_p), len(mask),
-                 ctypes.byref(ptr))
-        self._owned.append(ptr.value)
-        return torch.cuda.ExternalStream(ptr.value, device=dev)
-
-    def close(self):
-        """Release the CU-masked streams (side_cus > 0).  Explicit, after a device sync: torch
-        only wraps them (ExternalStream) and its caching allocator may still reference them,
-        so they are never destroyed implicitly (a garbage-collected executor leaks them)."""
-        if self._owned:
-            torch.cuda.synchronize(self.bb.device)
-            for p in self._owned:
-                nat.call("lidar_stream_destroy", ctypes_void(p))
-            self._owned = []
-
     def _fps(self, k, xs, ready):
         """SA1 FPS + level-0 ball queries of group k (the batches in xs) on a side stream."""
         slot = k % (self.depth + 1)
         fs = self.fps_streams[k % self.depth]
+        hs = 1 + k % self.depth  # the side stream's own library handle
         fs.wait_event(self.slot_free[slot])
         fs.wait_event(ready)
         g = len(xs) * self.B
+        t = self.bb.timers
         with torch.cuda.stream(fs):
             if self.G > 1:
                 x = self.stage[slot][:g]
@@ -886,29 +711,13 @@ class StreamingSSG:
                 x = xs[0]
             for xj in xs:  # read on this stream: keep the caller's buffers alive until then
                 xj.record_stream(fs)
-            _call(self.bb.timers, "sa1_fps", farthest_point_sample, x, self.M1, return_xyz=True,
-                  first_zero=self.fz[slot][:g], slot=1 + k % self.depth, out_idx=self.idx[slot][:g],
-                  out_xyz=self.cxyz[slot][:g], threads=self.fps_threads)
+            _call(t, "sa1_fps", g, farthest_point_sample, x, self.M1, return_xyz=True, first_zero=self.fz[slot][:g],
+                  slot=hs, out_idx=self.idx[slot][:g], out_xyz=self.cxyz[slot][:g], threads=self.fps_threads)
             lvl0 = self.bb.levels[0]
-            if self.grid[slot] is not None:
-                br = max(lvl0["branches"], key=lambda b: b["r"])
-                _call(self.bb.timers, "sa1_bq_bin", ball_query_bin, br["r"], br["ns"], x, self.grid[slot],
-                      slot=1 + k % self.depth)
-            for bi_, br in enumerate([] if self.bq_on_main else lvl0["branches"]):
+            for bi_, br in enumerate(lvl0["branches"]):
                 tag = "sa1" + (f"_b{bi_}" if len(lvl0["branches"]) > 1 else "")
-                _call(self.bb.timers, f"{tag}_ball_query", ball_query, br["r"], br["ns"], x, self.cxyz[slot][:g],
-                      out=self.gidx[slot][bi_][:g], slot=1 + k % self.depth, grid=self.grid[slot])
-            if self.l1:
-                hs = 1 + k % self.depth
-                c1 = self.cxyz[slot][:g]
-                _call(self.bb.timers, "sa2_fps", farthest_point_sample, c1, self.M2, return_xyz=True,
-                      first_zero=self.fz2[slot][:g], prefix_ok=self.fz[slot][:g], slot=hs,
-                      out_idx=self.idx2[slot][:g], out_xyz=self.cxyz2[slot][:g])
-                lvl1 = self.bb.levels[1]
-                for bi_, br in enumerate(lvl1["branches"]):
-                    tag = "sa2" + (f"_b{bi_}" if len(lvl1["branches"]) > 1 else "")
-                    _call(self.bb.timers, f"{tag}_ball_query", ball_query, br["r"], br["ns"], c1,
-                          self.cxyz2[slot][:g], out=self.gidx2[slot][bi_][:g], slot=hs)
+                _call(t, f"{tag}_ball_query", g, ball_query, br["r"], br["ns"], x, self.cxyz[slot][:g],
+                      out=self.gidx[slot][bi_][:g], slot=hs)
             self.fps_done[slot].record(fs)
         return slot
 
@@ -918,48 +727,71 @@ class StreamingSSG:
         main.wait_event(self.fps_done[slot])
         B, g = self.B, len(xs) * self.B
         x = self.stage[slot][:g] if self.G > 1 else xs[0]
-        pre = None
-        if self.l1:
-            pre = {1: {"fps": (self.idx2[slot][:g], self.cxyz2[slot][:g], self.fz2[slot][:g]),
-                       "bq": [gi[:g] for gi in self.gidx2[slot]]}}
-        out = self.bb.forward_from_sa1_fps(x, self.idx[slot][:g], self.cxyz[slot][:g], self.fz[slot][:g],
-                                           None if self.bq_on_main else [gi[:g] for gi in self.gidx[slot]],
-                                           self.grid[slot], pre=pre)
+        lvl0 = [self.idx[slot][:g], self.cxyz[slot][:g], self.fz[slot][:g], [gi[:g] for gi in self.gidx[slot]]]
+        if self.keep:  # the slot's buffers are reused by a later group
+            lvl0 = [a.clone() for a in lvl0[:3]] + [[gi.clone() for gi in lvl0[3]]]
+        out, levels = self.bb.forward_from_sa1_fps(x, *lvl0, keep_levels=self.keep)
         self.slot_free[slot].record(main)
-        return list(out.split(B)) if len(xs) > 1 else [out]
+        outs = list(out.split(B))
+        if not self.keep:
+            return outs
+        per = []
+        for j in range(len(xs)):
+            sl = slice(j * B, (j + 1) * B)
+            per.append((outs[j], [(nx[sl], nf[sl], ni[sl], [gi[sl] for gi in ng]) for nx, nf, ni, ng in levels]))
+        return per
+
+    def feed(self):
+        return _Feed(self)
 
     def run(self, inputs):
-        """inputs: list of (B, N, 3) CUDA tensors -> list of global features (B, C)."""
-        if self.main is not None:
-            cur = torch.cuda.current_stream(self.bb.device)
-            self.main.wait_stream(cur)
-            with torch.cuda.stream(self.main):
-                outs = self._run(inputs)
-            cur.wait_stream(self.main)
-            return outs
-        return self._run(inputs)
-
-    def _run(self, inputs):
-        main = torch.cuda.current_stream(self.bb.device)
-        ready = torch.cuda.Event()
-        ready.record(main)  # the inputs exist on the caller's stream
-        # ramp: groups of 1, 2, ... G batches — the first group's FPS (the pipeline fill, during
-        # which the main stream waits) is a third as long as a full group's; results are per
-        # frame, so the grouping never changes them
-        groups, i, k = [], 0, 0
+        """inputs: list of (B, N, 3) CUDA tensors -> list of global features (B, C), in order."""
+        f = _Feed(self)
+        outs, i, k = [], 0, 0
         while i < len(inputs):
+            # ramp: groups of 1, 2, ... G batches — the first group's FPS (the pipeline fill,
+            # during which the main stream waits) is a third as long as a full group's
             sz = min(self.G, k + 1) if self.ramp else self.G
-            groups.append(inputs[i:i + sz])
+            outs += f._issue(list(inputs[i:i + sz]))
             i, k = i + sz, k + 1
-        outs = []
-        pending = []
-        for k, xs in enumerate(groups):
-            pending.append((self._fps(k, xs, ready), xs))
-            if len(pending) > self.depth:
-                slot, pxs = pending.pop(0)
-                outs.extend(self._rest(slot, pxs, main))
-        while pending:
-            slot, pxs = pending.pop(0)
-            outs.extend(self._rest(slot, pxs, main))
-        return outs
+        return outs + f.flush()
 
+
+class _Feed:
+    """StreamingSSG's persistent feed: push(batch) stages batches; every full group of G issues
+    its SA1 FPS on a side stream and, once `depth` groups are in flight, the oldest group's
+    remaining levels on the main stream (the caller's current stream).  push returns the
+    outputs of the batches that call completed (in input order); flush() issues a partial last
+    group and drains the pipeline."""
+
+    def __init__(self, pipe):
+        self.p = pipe
+        self.main = torch.cuda.current_stream(pipe.bb.device)
+        self.buf, self.pending, self.k = [], [], 0
+
+    def _issue(self, xs):
+        ready = torch.cuda.Event()
+        ready.record(self.main)  # the inputs exist on the caller's stream
+        self.pending.append((self.p._fps(self.k, xs, ready), xs))
+        self.k += 1
+        if len(self.pending) > self.p.depth:
+            slot, pxs = self.pending.pop(0)
+            return self.p._rest(slot, pxs, self.main)
+        return []
+
+    def push(self, x):
+        self.buf.append(x)
+        if len(self.buf) < self.p.G:
+            return []
+        xs, self.buf = self.buf, []
+        return self._issue(xs)
+
+    def flush(self):
+        out = []
+        if self.buf:
+            xs, self.buf = self.buf, []
+            out += self._issue(xs)
+        while self.pending:
+            slot, pxs = self.pending.pop(0)
+            out += self.p._rest(slot, pxs, self.main)
+        return out

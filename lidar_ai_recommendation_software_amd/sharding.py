@@ -53,10 +53,28 @@ def timed(run, device=None, world=1):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device if cuda else "cpu")
+        # RCCL reduces device tensors; gloo (the CPU tests, or ranks sharing one GPU) host ones
+        on_dev = cuda and dist.get_backend() == "nccl"
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device if on_dev else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     return elapsed
+
+
+def init_distributed(world, local):
+    """One process per GPU (torch.distributed.run).  Returns the local device index.  Ranks that
+    share a GPU (more ranks than visible devices: a rehearsal of the N-GPU path on a 1-GPU box)
+    use gloo for the timing collectives; otherwise RCCL ("nccl") over xGMI.  Counting devices
+    does not initialise the GPU, so this runs before any GPU call."""
+    ndev = max(1, torch.cuda.device_count())
+    dev = local % ndev
+    if world > 1:
+        if world > ndev:
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(dev)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+    return dev
 
 
 def aggregate_rate(units_per_rank, world, elapsed):

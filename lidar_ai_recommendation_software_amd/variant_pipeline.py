@@ -23,7 +23,7 @@ import ctypes
 import numpy as np
 
 from . import _native as nat
-from .data_processing import _handle, _on_device, _remember
+from .data_processing import _handle, _on_device, _reference_shape_errors, _remember
 
 EPS = 0.3          # app_simplified.py:107
 MIN_SAMPLES = 5    # the kernel's DBSCAN min_samples (fixed, as in the reference)
@@ -38,13 +38,10 @@ def preprocess_point_cloud(points, eps=EPS):
     point survives the 3-sigma filter (``np.percentile`` of an empty array)."""
     import torch
     pts = np.asarray(points)
-    if pts.ndim != 2 or pts.shape[1] < 3:
-        raise IndexError("too many indices for array")
+    _reference_shape_errors(pts)  # frames that are not (N >= 1, 3): app_simplified.py:80-117 raises the same
     n = len(pts)
-    if n == 0:
-        raise ValueError("zero-size array to reduction operation minimum which has no identity")
     is_int = pts.dtype.kind in "iub"
-    x = torch.from_numpy(np.ascontiguousarray(pts[:, :3], dtype=np.float64)).cuda()
+    x = torch.from_numpy(np.ascontiguousarray(pts, dtype=np.float64)).cuda()
     dev = x.device
     mask = torch.empty(n, dtype=torch.uint8, device=dev)
     colors = torch.empty((n, 3), dtype=torch.float64, device=dev)

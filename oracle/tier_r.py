@@ -111,8 +111,12 @@ def percentile30(z):
     return r
 
 
-def preprocess_lidar_data(points):
-    """Restates utils/data_processing.py:127-229 (``preprocess_lidar_data``)."""
+def preprocess_lidar_data(points, dbscan="c"):
+    """Restates utils/data_processing.py:127-229 (``preprocess_lidar_data``).
+
+    dbscan "c": the order-independent C DBSCAN (lidar_oracle.c) and the written-out scaler;
+    "sklearn": scikit-learn's StandardScaler().fit_transform and DBSCAN(eps, min_samples=5).fit —
+    the reference's own calls (:190-197), used as bench.py's CPU baseline of the density path."""
     points = np.asarray(points)
     # :143-147 height colours over ALL points
     z = points[:, 2]
@@ -145,10 +149,15 @@ def preprocess_lidar_data(points):
     # :186-200 DBSCAN on the scaled non-ground points
     ng = inl[nonground]
     if len(ng) > 10:
-        scaled = standard_scale(ng)[0]
+        if dbscan == "sklearn":
+            from sklearn.cluster import DBSCAN
+            from sklearn.preprocessing import StandardScaler
+            scaled = StandardScaler().fit_transform(ng)
+        else:
+            scaled = standard_scale(ng)[0]
         avg = np.mean(np.std(scaled, axis=0)) * 0.5
         eps = max(0.2, min(0.5, avg))
-        lab = dbscan_labels(scaled, eps, 5)
+        lab = DBSCAN(eps=eps, min_samples=5).fit(scaled).labels_ if dbscan == "sklearn" else dbscan_labels(scaled, eps, 5)
     else:
         lab = np.zeros(len(ng), dtype=int)
     # :203-204

@@ -90,3 +90,35 @@ def test_gloo_world2_timing_and_sharded_frames(tmp_path):
         pd = tier_r.preprocess_lidar_data(uniform_frame(1024, seed=sharding.frame_seed(0, base=f)))
         np.testing.assert_array_equal(got[f"c{f}"], pd["clusters"])
         np.testing.assert_array_equal(got[f"p{f}"], tier_r.extract_people_positions(pd))
+
+
+def _venue_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle import tier_r
+    from lidar_ai_recommendation_software_amd.global_density import VenueGrid
+    from lidar_ai_recommendation_software_amd.synthetic import uniform_frame
+    xr, yr = (-15.0, 15.0), (-15.0, 15.0)
+    vg = VenueGrid(xr, yr, 1.0, device="cpu")
+    # this rank's people (the GPU path bins them with lidar_venue_counts_f64; here the oracle's
+    # histogram of the same edges stands in, the collective is what is under test)
+    people = uniform_frame(200 + 50 * rank, seed=40 + rank)[:, :2]
+    h = tier_r.calculate_grid_density(people, xr, yr, 1.0)[2]
+    vg.counts += torch.from_numpy(h.astype(np.int32))
+    vg.all_reduce()
+    np.save(os.path.join(out_dir, f"venue{rank}.npy"), vg.density())
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_venue_grid_all_reduce(tmp_path):
+    """SURVEY §8e's optional global density: per-rank venue counts summed by one all_reduce
+    (RCCL on the GPU box; gloo here) equal the grid density of all ranks' people together."""
+    from oracle import tier_r
+    from lidar_ai_recommendation_software_amd.synthetic import uniform_frame
+    world = 2
+    mp.spawn(_venue_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    allp = np.concatenate([uniform_frame(200 + 50 * r, seed=40 + r)[:, :2] for r in range(world)])
+    want = tier_r.calculate_grid_density(allp, (-15.0, 15.0), (-15.0, 15.0), 1.0)[2]
+    for r in range(world):
+        assert np.array_equal(np.load(tmp_path / f"venue{r}.npy"), want)

@@ -1,0 +1,54 @@
+"""bench.py's N-rank path rehearsed on one GPU (the driver's 8-GPU scaling run uses the same code).
+
+torch.distributed.run starts two ranks before any GPU call; with more ranks than visible devices
+they share the GPU and use gloo for the timing collectives (RCCL needs a device per rank).  Each
+rank processes the frames of its own seed; the test then runs each rank's workload alone
+(`--seed-rank r`) and requires bit-identical outputs, and checks that the aggregate rate counts
+the work of both ranks over the max-over-ranks time.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ARGS = ["--points", "8192", "--batch", "4", "--steps", "6", "--warmup", "1", "--rotate", "3", "--no-extras",
+        "--no-density", "--no-cpu-baseline", "--no-fp32-mfma-leg", "--no-standalone"]
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _last_json(out):
+    return json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
+
+
+def test_bench_two_ranks_on_one_gpu(cuda, tmp_path):
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="4")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2", *ARGS, "--dump", str(tmp_path / "w2")]
+    r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    line = _last_json(r.stdout)
+    assert line["n_gpus"] == 2 and line["steps"] == 6
+    # whole-job rate: both ranks' frames over the max-over-ranks window
+    per_rank_points = 4 * 8192 * 6
+    assert abs(line["value"] - 2 * per_rank_points / (line["ms_per_step"] * 6 / 1e3) / 1e6) <= 1e-6 * line["value"]
+    for rank in (0, 1):
+        w2 = json.load(open(tmp_path / f"w2.rank{rank}.json"))
+        assert w2["world"] == 2 and w2["seed_rank"] == rank
+        r1 = subprocess.run([sys.executable, "bench.py", *ARGS, "--seed-rank", str(rank), "--dump",
+                             str(tmp_path / f"w1_{rank}")], cwd=REPO, env=env, capture_output=True, text=True,
+                            timeout=300)
+        assert r1.returncode == 0, r1.stderr[-4000:]
+        w1 = json.load(open(tmp_path / f"w1_{rank}.rank0.json"))
+        assert w1["world"] == 1 and w1["seed_rank"] == rank
+        assert w2["digests"] == w1["digests"], f"rank {rank}: outputs differ from its 1-rank run"
+    assert json.load(open(tmp_path / "w2.rank0.json"))["digests"] != json.load(open(tmp_path / "w2.rank1.json"))["digests"]

@@ -45,7 +45,7 @@ def frames_for(kind, b, n, seed):
     ("clumped", 2, 5000, 300), ("dups", 2, 3000, 2000), ("grid", 1, 4096, 600),
     ("uniform", 2, 1, 4), ("uniform", 1, 37, 60), ("uniform", 1, 64, 64),
 ])
-@pytest.mark.parametrize("threads", [0, 512, 256])
+@pytest.mark.parametrize("threads", [0, 512])
 def test_fps_bit_exact(cuda, kind, b, n, m, threads):
     x = frames_for(kind, b, n, 11)
     if threads and (n + 63) // 64 > 8 * threads:  # 8 buckets per lane at most
@@ -118,20 +118,6 @@ def test_ball_query_grid_edge_frames(cuda, name, r, ns):
         assert np.array_equal(got, want), f"{mode}: {(got != want).sum()} differ"
 
 
-@pytest.mark.parametrize("name", ["uniform"] + list(_bq_edge_frames()))
-def test_ball_query_split_binning(cuda, monkeypatch, name):
-    """LIDAR_BQ_BIN_SPLIT=1: the grid built by the five low-LDS kernels (global atomics,
-    slot order differs from the one-workgroup binning) gives the oracle's indices exactly."""
-    monkeypatch.setenv("LIDAR_BQ_BIN_SPLIT", "1")
-    x = unit_frames(3, 20000, 8) if name == "uniform" else _bq_edge_frames()[name][None]
-    c = np.ascontiguousarray(np.concatenate([x[:, :600:3], x[:, :40] + np.float32(7.5)], 1))
-    xt, ct = torch.from_numpy(x).to(cuda), torch.from_numpy(c).to(cuda)
-    for r, ns in [(0.1, 32), (0.0, 8), (0.3, 128)]:
-        got = pn.ball_query(r, ns, xt, ct, mode="grid").cpu().numpy()
-        want = tier_n.ball_query(x, c, r, ns)
-        assert np.array_equal(got, want), f"r={r}: {(got != want).sum()} differ"
-
-
 def test_ball_query_binned_reuse(cuda):
     """one binning (lidar_ball_query_bin_f32) serves queries at smaller, equal and larger
     radii and other nsample values, exactly."""
@@ -144,66 +130,6 @@ def test_ball_query_binned_reuse(cuda):
         got = pn.ball_query(r, ns, xt, ct, grid=grid).cpu().numpy()
         want = tier_n.ball_query(x, c, r, ns)
         assert np.array_equal(got, want), f"r={r} ns={ns}: {(got != want).sum()} differ"
-
-
-@pytest.mark.parametrize("cfg_name,level,branch", [("ssg", 0, 0), ("ssg", 1, 0), ("msg", 0, 0), ("msg", 0, 1),
-                                                   ("msg", 0, 2), ("msg", 1, 0), ("msg", 1, 1), ("msg", 1, 2)])
-def test_group_mlp(cuda, cfg_name, level, branch):
-    cfg = pn.CONFIGS[cfg_name]
-    w = pn.init_weights(cfg, seed=3)
-    lvl = cfg["levels"][level]
-    layers = w[level][branch]
-    cfeat = layers[0][0].shape[0] - 3
-    r, ns, widths = lvl["radii"][branch], lvl["nsamples"][branch], lvl["mlps"][branch]
-    B, N, M = 2, 2048, 128
-    rng = np.random.default_rng(7)
-    x = unit_frames(B, N, 9)
-    f = rng.standard_normal((B, N, cfeat)).astype(np.float32) if cfeat else None
-    c = x[:, :M].copy()
-    gi = tier_n.ball_query(x, c, r, ns)
-    packed = torch.from_numpy(pn.pack_branch(layers, cfeat)).to(cuda)
-    T = lambda a: None if a is None else torch.from_numpy(np.ascontiguousarray(a)).to(cuda)
-    got = pn.group_mlp(T(x), T(f), T(c), T(gi), packed, widths).cpu().numpy()
-    for bi in range(B):
-        want = tier_n.mlp_maxpool(tier_n.group(x[bi], None if f is None else f[bi], c[bi], gi[bi]), layers, ns)
-        feat_close(got[bi], want, f"{cfg_name} L{level} br{branch} frame {bi}")
-
-
-@pytest.mark.parametrize("cfg_name,level,branch", [("ssg", 1, 0), ("msg", 1, 0), ("msg", 1, 1), ("msg", 1, 2)])
-def test_group_mlp_layer1_per_point(cuda, cfg_name, level, branch):
-    """layer 1 as per-point / per-centre GEMMs + the fused kernel from layer 2 on
-    (relu(P[k] - Q[c]) = relu(W1^T [x_k - c, f_k] + b1)) vs the oracle's grouped rows."""
-    cfg = pn.CONFIGS[cfg_name]
-    w = pn.init_weights(cfg, seed=4)
-    lvl = cfg["levels"][level]
-    layers = w[level][branch]
-    cfeat = layers[0][0].shape[0] - 3
-    r, ns, widths = lvl["radii"][branch], lvl["nsamples"][branch], lvl["mlps"][branch]
-    B, N, M = 2, 2000, 100  # neither B*N nor B*M a multiple of 128: padded GEMM rows
-    rng = np.random.default_rng(8)
-    x = unit_frames(B, N, 10)
-    f = np.abs(rng.standard_normal((B, N, cfeat))).astype(np.float32)  # post-ReLU-like features
-    c = x[:, :M].copy()
-    gi = tier_n.ball_query(x, c, r, ns)
-    kp = (cfeat + 3 + 15) // 16 * 16
-    R = (B * N + 127) // 128 * 128
-    rows = torch.zeros((R, kp), dtype=torch.float32, device=cuda)
-    rows[:B * N, :cfeat] = torch.from_numpy(f.reshape(-1, cfeat)).to(cuda)
-    w1, b1 = layers[0]
-    T = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).to(cuda)
-    br = {"pre": pn.layer1_weights(layers[0], cfeat, T)}
-    (P, Q), = pn.layer1_per_point(rows, T(x), cfeat, T(c), [br])
-    packed = torch.from_numpy(pn.pack_branch(layers, cfeat)).to(cuda)
-    out = torch.empty((B, M, widths[-1]), dtype=torch.float32, device=cuda)
-    gti = torch.from_numpy(gi).to(cuda)
-    pn.group_mlp_pre(P, Q, gti, N, packed, cfeat, widths, out)
-    got = out.cpu().numpy()
-    for bi in range(B):
-        want = tier_n.mlp_maxpool(tier_n.group(x[bi], f[bi], c[bi], gi[bi]), layers, ns)
-        feat_close(got[bi], want, f"{cfg_name} L{level} br{branch} frame {bi} (layer 1 per point)")
-    # the per-point rows themselves: P = [f, x] W1 + b1
-    Pn = P[:B * N, :widths[0]].cpu().numpy()
-    feat_close(Pn, np.concatenate([x.reshape(-1, 3), f.reshape(-1, cfeat)], 1) @ w1 + b1, "P rows")
 
 
 @pytest.mark.parametrize("cfg_name,level,branch", [("ssg", 0, 0), ("msg", 0, 0), ("msg", 0, 1), ("msg", 0, 2),
@@ -234,7 +160,8 @@ def test_group_mlp16(cuda, cfg_name, level, branch):
         kp = (cfeat + 3 + 15) // 16 * 16
         rows = torch.zeros(((B * N + 127) // 128 * 128, kp), dtype=torch.float32, device=cuda)
         rows[:B * N, :cfeat] = T(f.reshape(-1, cfeat))
-        (P, Q), = pn.layer1_per_point(rows, T(x), cfeat, T(c), [{"pre": pn.layer1_weights(layers[0], cfeat, T)}])
+        (P, Q), = pn.layer1_per_point(rows, T(x), cfeat, T(c), [{"pre": pn.layer1_weights(layers[0], cfeat, T)}],
+                                      x3=False)
         pn.group_mlp16(P, Q, gti, N, packed, widths, out, off)
     got = out.cpu().numpy()
     assert (got[..., :off] == -7.0).all() and (got[..., off + widths[-1]:] == -7.0).all(), "wrote outside its columns"
@@ -272,7 +199,8 @@ def test_group_mlp_x3(cuda, cfg_name, level, branch):
         rows = torch.zeros(((B * N + 127) // 128 * 128, kp), dtype=torch.float32, device=cuda)
         rows[:B * N, :cfeat] = T(f.reshape(-1, cfeat).astype(np.float32))
         Tf = lambda a: T(np.asarray(a, dtype=np.float32))
-        (P, Q), = pn.layer1_per_point(rows, T(x), cfeat, T(c), [{"pre": pn.layer1_weights(layers[0], cfeat, Tf)}])
+        (P, Q), = pn.layer1_per_point(rows, T(x), cfeat, T(c), [{"pre": pn.layer1_weights(layers[0], cfeat, Tf)}],
+                                      x3=False)
         pn.group_mlp_x3(P, Q, gti, N, packed, widths, out, off)
     got = out.cpu().numpy()
     assert (got[..., :off] == -7.0).all() and (got[..., off + widths[-1]:] == -7.0).all()
@@ -288,27 +216,6 @@ def test_dense_no_relu(cuda):
     b = rng.standard_normal(128).astype(np.float32)
     T = lambda a: torch.from_numpy(a).to(cuda)
     feat_close(pn.dense(T(x), T(w), T(b), relu=False).cpu().numpy(), x @ w + b, "dense no relu")
-
-
-@pytest.mark.parametrize("rows,k,cout,pool", [(256, 144, 128, 0), (512, 272, 256, 0), (1024, 512, 1024, 512),
-                                              (384, 16, 128, 128), (2048, 256, 512, 1024), (128, 48, 384, 0)])
-def test_dense_x3(cuda, rows, k, cout, pool):
-    """split-bf16 GEMM vs the fp32 numpy product at the fp32 path's 1e-4 tolerance."""
-    rng = np.random.default_rng(rows + k)
-    x = np.abs(rng.standard_normal((rows, k))).astype(np.float32)
-    w = (rng.standard_normal((k, cout)) / np.sqrt(k)).astype(np.float32)
-    b = rng.standard_normal(cout).astype(np.float32) * 0.1
-    T = lambda a: torch.from_numpy(a).to(cuda)
-    want = x.astype(np.float64) @ w.astype(np.float64) + b
-    feat_close(pn.dense(T(x), T(w), T(b), relu=False, x3=True).cpu().numpy(), want, "dense x3 no relu")
-    wp = pn.pack_dense_x3(T(w))  # the packed-weight entry point the backbone uses
-    feat_close(pn.dense(T(x), T(w), T(b), relu=False, x3=True, wpack=wp).cpu().numpy(), want, "dense x3p")
-    want = np.maximum(want, 0)
-    if pool:
-        got = pn.dense_relu(T(x), T(w), T(b), pool_rows=pool, x3=True).cpu().numpy()
-        feat_close(got, want.reshape(rows // pool, pool, cout).max(axis=1), "dense x3 pooled")
-    else:
-        feat_close(pn.dense_relu(T(x), T(w), T(b), x3=True).cpu().numpy(), want, "dense x3 relu")
 
 
 @pytest.mark.parametrize("rows,k,cout,pool", [(256, 144, 128, 0), (512, 272, 256, 0), (1024, 512, 1024, 512),
@@ -368,23 +275,27 @@ def test_dense_relu_and_pool(cuda):
     feat_close(pooled, want.reshape(2, 256, 256).max(axis=1), "dense pooled")
 
 
-@pytest.mark.parametrize("cfg_name,n,pre,mlp16", [
-    ("ssg", 16384, True, False), ("ssg", 65536, True, False), ("sa1", 16384, True, False),
-    ("msg", 16384, True, False), ("ssg", 16384, False, False), ("msg", 16384, False, False),
-    ("ssg", 5000, True, False), ("ssg", 65536, True, True), ("msg", 16384, True, True), ("sa1", 16384, True, True),
-    ("ssg", 65536, True, "x3"), ("msg", 16384, True, "x3"), ("sa1", 16384, True, "x3")])
-def test_backbone_vs_oracle(cuda, cfg_name, n, pre, mlp16):
+@pytest.mark.parametrize("cfg_name,n,x3", [
+    ("ssg", 16384, True), ("ssg", 65536, True), ("sa1", 16384, True), ("msg", 16384, True), ("ssg", 5000, True),
+    ("ssg", 16384, False), ("ssg", 65536, False), ("msg", 16384, False), ("sa1", 16384, False), ("ssg", 777, True)])
+def test_backbone_vs_oracle(cuda, cfg_name, n, x3):
+    """x3: the default split-bf16 kernels; False: the native fp32-MFMA kernels.  FPS and
+    ball-query indices bit-exact at every level, features 1e-4."""
     cfg = pn.CONFIGS[cfg_name]
-    x3 = mlp16 == "x3"
-    bb = pn.PointNet2Backbone(cfg, device=cuda, seed=0, pre_layer1=pre, mlp16=False if x3 else mlp16, x3=x3)
+    bb = pn.PointNet2Backbone(cfg, device=cuda, seed=0, x3=x3)
     x = unit_frames(1, n, 21)
     g, levels = bb.forward(torch.from_numpy(x).to(cuda), keep_levels=True)
     torch.cuda.synchronize()
-    want, wl = tier_n.sa_stack(x[0], {"levels": pn.resolve(cfg, n)}, bb.weights)
-    for li, ((nx, nf, ni), (ox, of, oi)) in enumerate(zip(levels, wl)):
+    lv_cfg = pn.resolve(cfg, n)
+    want, wl = tier_n.sa_stack(x[0], {"levels": lv_cfg}, bb.weights)
+    pts = x[0]
+    for li, ((nx, nf, ni, ngi), (ox, of, oi)) in enumerate(zip(levels, wl)):
         assert np.array_equal(ni.cpu().numpy()[0], oi), f"level {li} FPS indices differ"
         assert np.array_equal(nx.cpu().numpy()[0], ox)
+        for bi, (r, ns) in enumerate(zip(lv_cfg[li]["radii"], lv_cfg[li]["nsamples"])):
+            assert np.array_equal(ngi[bi].cpu().numpy()[0], tier_n.ball_query(pts, ox, r, ns)), f"level {li} br {bi}"
         feat_close(nf.cpu().numpy()[0], of, f"level {li} features")
+        pts = ox
     feat_close(g.cpu().numpy()[0], want, "global feature")
 
 
@@ -437,32 +348,81 @@ def test_streaming_grouped_fps_matches_forward(cuda, cfg_name, dtype, group, dep
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("group,depth,threads,nb,l1", [(3, 3, 512, 7, False), (2, 2, 1024, 4, False),
-                                                       (4, 2, 512, 5, False), (3, 3, 512, 7, True),
-                                                       (2, 3, 1024, 3, True)])
-def test_streaming_bench_policy_matches_forward(cuda, group, depth, threads, nb, l1):
-    """the bench's executor policy: SA1 ball queries on the main stream answered from grids
-    binned on the side streams, 512-thread SA1 FPS, groups of batches (partial last group)."""
+@pytest.mark.parametrize("group,depth,threads,nb", [(3, 3, 512, 7), (2, 2, 1024, 4), (4, 2, 512, 5)])
+def test_streaming_bench_policy_matches_forward(cuda, group, depth, threads, nb):
+    """the bench's executor policy: 512-thread SA1 FPS + ball queries on the side streams, groups
+    of batches (partial last group), ramped groups."""
     bb = pn.PointNet2Backbone(pn.SSG, device=cuda, seed=4)
     xs = [torch.from_numpy(unit_frames(2, 8192, 50 + s)).to(cuda) for s in range(nb)]
     want = [bb.forward(x)[0] for x in xs]
-    pipe = pn.StreamingSSG(bb, 2, 8192, depth=depth, fps_group=group, bq_on_main=True, fps_threads=threads,
-                           level1_on_side=l1)
-    got = pipe.run(xs)
+    got = pn.StreamingSSG(bb, 2, 8192, depth=depth, fps_group=group, fps_threads=threads).run(xs)
     torch.cuda.synchronize()
     assert len(got) == nb
     for a, b in zip(got, want):
         assert torch.equal(a, b)
 
 
-def test_streaming_mlp16_matches_forward(cuda):
-    bb = pn.PointNet2Backbone(pn.SSG, device=cuda, seed=3, mlp16=True)
+def test_streaming_feed_steady_state(cuda):
+    """the persistent feed bench.py times: push() keeps `depth` groups in flight; after the fill
+    every group of G pushes completes exactly G batches, in order; flush() drains the rest."""
+    bb = pn.PointNet2Backbone(pn.SSG, device=cuda, seed=5)
+    xs = [torch.from_numpy(unit_frames(2, 4096, 70 + s)).to(cuda) for s in range(4)]
+    want = [bb.forward(x)[0] for x in xs]
+    G, depth = 2, 2
+    feed = pn.StreamingSSG(bb, 2, 4096, depth=depth, fps_group=G, ramp=False).feed()
+    outs, per_push = [], []
+    for i in range(14):
+        got = feed.push(xs[i % 4])
+        per_push.append(len(got))
+        outs += got
+    outs += feed.flush()
+    torch.cuda.synchronize()
+    # the first (depth + 1) * G - 1 pushes complete nothing; then every G-th push completes G
+    assert per_push[:(depth + 1) * G - 1] == [0] * ((depth + 1) * G - 1)
+    assert all(c in (0, G) for c in per_push) and sum(per_push) == 14 - depth * G
+    assert len(outs) == 14
+    for i, o in enumerate(outs):
+        assert torch.equal(o, want[i % 4]), i
+
+
+def test_streaming_native_fp32_matches_forward(cuda):
+    bb = pn.PointNet2Backbone(pn.SSG, device=cuda, seed=3, x3=False)
     xs = [torch.from_numpy(unit_frames(2, 8192, 30 + s)).to(cuda) for s in range(5)]
     want = [bb.forward(x)[0] for x in xs]
     got = pn.StreamingSSG(bb, 2, 8192, depth=2, fps_group=2).run(xs)
     torch.cuda.synchronize()
     for a, b in zip(got, want):
         assert torch.equal(a, b)
+
+
+def test_bench_shape_executor_vs_oracle(cuda):
+    """BASELINE configs[3]'s per-GPU share through the bench's executor: 32-frame batches of
+    65 536 points, groups of 3 batches (one 96-frame FPS launch), 3 groups in flight, 512-thread
+    FPS, ramped groups over 6 batches (1, 2, 3: the third group is a full 96-frame launch).
+    Frames 0, 31, 64 and 95 of that launch vs the oracle: FPS and ball-query indices bit-exact
+    at both SA levels, features and the global feature 1e-4."""
+    B, N = 32, 65536
+    bb = pn.PointNet2Backbone(pn.SSG, device=cuda, seed=0)
+    xs = [torch.from_numpy(unit_frames(B, N, 900 + s)).to(cuda) for s in range(6)]
+    got = pn.StreamingSSG(bb, B, N, depth=3, fps_group=3, fps_threads=512, keep_levels=True).run(xs)
+    torch.cuda.synchronize()
+    assert len(got) == 6
+    lv_cfg = pn.resolve(pn.SSG, N)
+    for gf in (0, 31, 64, 95):
+        bi, f = 3 + gf // B, gf % B
+        g, levels = got[bi]
+        x = xs[bi][f].cpu().numpy()
+        want, wl = tier_n.sa_stack(x, {"levels": lv_cfg}, bb.weights)
+        pts = x
+        for li, ((nx, nf, ni, ngi), (ox, of, oi)) in enumerate(zip(levels, wl)):
+            assert np.array_equal(ni[f].cpu().numpy(), oi), f"frame {gf} level {li}: FPS indices differ"
+            assert np.array_equal(nx[f].cpu().numpy(), ox)
+            r, ns = lv_cfg[li]["radii"][0], lv_cfg[li]["nsamples"][0]
+            assert np.array_equal(ngi[0][f].cpu().numpy(), tier_n.ball_query(pts, ox, r, ns)), \
+                f"frame {gf} level {li}: ball-query indices differ"
+            feat_close(nf[f].cpu().numpy(), of, f"frame {gf} level {li} features")
+            pts = ox
+        feat_close(g[f].cpu().numpy(), want, f"frame {gf} global feature")
 
 
 def bf16_close(got, want, what=""):
@@ -477,30 +437,6 @@ def bf16_close(got, want, what=""):
     tight = err <= RTOL * np.abs(want) + RTOL * scale
     assert tight.mean() >= 0.99, f"{what}: only {tight.mean():.4f} within fp32 tolerance"
     assert err.max() <= 2e-2 * scale, f"{what}: max err {err.max():.3e} vs rms {scale:.3e}"
-
-
-@pytest.mark.parametrize("cfg_name,level,branch", [("msg", 0, 0), ("msg", 0, 1), ("msg", 0, 2), ("msg", 1, 0),
-                                                   ("msg", 1, 1), ("msg", 1, 2), ("ssg", 0, 0), ("ssg", 1, 0)])
-def test_group_mlp_bf16(cuda, cfg_name, level, branch):
-    cfg = pn.CONFIGS[cfg_name]
-    w = pn.init_weights(cfg, seed=3)
-    lvl = cfg["levels"][level]
-    layers = w[level][branch]
-    cfeat = layers[0][0].shape[0] - 3
-    r, ns, widths = lvl["radii"][branch], lvl["nsamples"][branch], lvl["mlps"][branch]
-    B, N, M = 2, 2048, 128
-    rng = np.random.default_rng(7)
-    x = unit_frames(B, N, 9)
-    f = np.abs(rng.standard_normal((B, N, cfeat))).astype(np.float32) if cfeat else None
-    c = x[:, :M].copy()
-    gi = tier_n.ball_query(x, c, r, ns)
-    packed = torch.from_numpy(pn.pack_branch_bf16(layers, cfeat)).to(cuda)
-    T = lambda a: None if a is None else torch.from_numpy(np.ascontiguousarray(a)).to(cuda)
-    got = pn.group_mlp(T(x), T(f), T(c), T(gi), packed, widths, bf16=True).cpu().numpy()
-    for bi in range(B):
-        fin = None if f is None else tier_n.bf16_round(f[bi])
-        want = tier_n.mlp_maxpool(tier_n.group(x[bi], fin, c[bi], gi[bi]), layers, ns, bf16=True)
-        bf16_close(got[bi], want, f"bf16 {cfg_name} L{level} br{branch} frame {bi}")
 
 
 @pytest.mark.parametrize("cfg_name,level,branch", [("msg", 0, 0), ("msg", 0, 1), ("msg", 0, 2), ("msg", 1, 0),
@@ -548,15 +484,23 @@ def test_group_mlp_x1(cuda, cfg_name, level, branch):
         bf16_close(got[bi], want, f"x1 {cfg_name} L{level} br{branch} frame {bi}")
 
 
-@pytest.mark.parametrize("cfg_name,n", [("msg", 16384), ("ssg", 16384)])
+@pytest.mark.parametrize("cfg_name,n", [("msg", 16384), ("ssg", 16384), ("msg", 131072)])
 def test_backbone_bf16_vs_oracle(cuda, cfg_name, n):
+    """The bf16 spec (X1 kernels) vs the bf16-rounding oracle; ("msg", 131072) is BASELINE
+    configs[4]'s frame size (MSG radii 0.1/0.2/0.4, bf16): FPS and ball-query indices bit-exact
+    at every level and branch, features bf16_close."""
     cfg = pn.CONFIGS[cfg_name]
     bb = pn.PointNet2Backbone(cfg, device=cuda, seed=0, dtype="bf16")
     x = unit_frames(1, n, 22)
     g, levels = bb.forward(torch.from_numpy(x).to(cuda), keep_levels=True)
     torch.cuda.synchronize()
-    want, wl = tier_n.sa_stack(x[0], {"levels": pn.resolve(cfg, n)}, bb.weights, bf16=True)
-    for li, ((nx, nf, ni), (ox, of, oi)) in enumerate(zip(levels, wl)):
+    lv_cfg = pn.resolve(cfg, n)
+    want, wl = tier_n.sa_stack(x[0], {"levels": lv_cfg}, bb.weights, bf16=True)
+    pts = x[0]
+    for li, ((nx, nf, ni, ngi), (ox, of, oi)) in enumerate(zip(levels, wl)):
         assert np.array_equal(ni.cpu().numpy()[0], oi), f"level {li} FPS indices differ"
+        for bi, (r, ns) in enumerate(zip(lv_cfg[li]["radii"], lv_cfg[li]["nsamples"])):
+            assert np.array_equal(ngi[bi].cpu().numpy()[0], tier_n.ball_query(pts, ox, r, ns)), f"level {li} br {bi}"
         bf16_close(nf.cpu().numpy()[0], of, f"bf16 level {li} features")
+        pts = ox
     bf16_close(g.cpu().numpy()[0], want, "bf16 global feature")

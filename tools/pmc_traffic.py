@@ -14,7 +14,7 @@ Output JSON (profiles/<round>/pmc_traffic.json): {"config": ..., "calibration": 
 "launches": n}}}; bench.py copies traffic_bytes into roofline["traffic"].
 
 usage: python tools/pmc_traffic.py gpurun_out/pmc_calib_f gpurun_out/pmc_calib_w \
-           gpurun_out/pmc_fetch gpurun_out/pmc_write profiles/r01/pmc_traffic.json
+           gpurun_out/pmc_fetch gpurun_out/pmc_write profiles/<round>/pmc_traffic.json
 """
 import csv
 import glob
@@ -33,15 +33,13 @@ def rows(d):
     return list(csv.DictReader(open(f[0])))
 
 
-FRAMES_PER_LAUNCH = 96  # bench.py defaults: 32 frames per batch x fps_group 3 per main-stream pass
+FRAMES_PER_LAUNCH = 96  # bench.py defaults: 32 frames per batch x 3 batches per group (one launch per group)
 
 
 def label(name, grid, F=FRAMES_PER_LAUNCH):
-    """Kernel label of the SSG stack (N = 65536) for F frames per main-stream launch
-    (grid = threads).  The dense GEMMs launch (cout/128) x (rows/128) workgroups of 256:
-    SA2's per-point layer 1 is rows F*4096 x 128 (+ the centre rows F*1024 x 128) and
-    group_all's layers are rows F*1024 x 256 / 512 / 1024, so the layer-1 GEMM and SA3's
-    second layer share a grid; the caller splits those by dispatch order (layer 1 first)."""
+    """Kernel label of the SSG stack (N = 65536) for F frames per launch (grid = threads).
+    The split-plane GEMMs of SA2's per-point layer 1 (fp32 rows in, mode 0) and group_all's
+    layers are told apart by their template arguments <mode, fp32-input, x1>."""
     if "fps_bucket_kernel" in name:
         return "fps"  # split into sa1/sa2 by duration below
     if "ball_query_kernel" in name:
@@ -50,22 +48,20 @@ def label(name, grid, F=FRAMES_PER_LAUNCH):
         return {F * 4096 * 64: "sa1_ball_query", F * 1024 * 64: "sa2_ball_query"}.get(grid)
     if "bq_bin_kernel" in name:
         return "bq_bin"  # one 1024-thread workgroup per frame: SA1 (65536 pts) vs SA2 (4096) by duration
-    # sa_x3_kernel<C1, C2, C3, NS, layer-1 mode (0 xyz, 1 pre, 2 px), R, X1>
-    if any(k in name for k in ("sa_group_mlp_kernel<0, 64, 64, 128, 32", "sa_pre_lds_kernel<64, 64, 128, 32, true",
-                                "sa16_kernel<64, 64, 128, 32, true", "sa_x3_kernel<64, 64, 128, 32, 0, 2, false")):
+    # sa_x3_kernel<C1, C2, C3, NS, layer-1 mode (0 xyz, 1 pre, 2 px), R, X1>; sa16_kernel<C1, C2, C3, NS, XYZ>
+    if "sa_x3_kernel<64, 64, 128, 32, 0, 2, false>" in name or "sa16_kernel<64, 64, 128, 32, true" in name:
         return "sa1_group_mlp"
-    if any(k in name for k in ("sa_group_mlp_kernel<128, 128, 128, 256, 64", "sa_pre_lds_kernel<128, 128, 256, 64",
-                                "sa16_kernel<128, 128, 256, 64, false", "sa_x3_kernel<128, 128, 256, 64, 1, 2, false")):
+    if "sa_x3_kernel<128, 128, 256, 64, 1, 2, false>" in name or "sa16_kernel<128, 128, 256, 64, false" in name:
         return "sa2_group_mlp"
-    if "dense_relu_kernel" in name or "dense_x3_kernel" in name or "dense_x3p_kernel" in name:
-        return {F * 4096 * 2: "dense_shared", F * 1024 * 2: "sa2_layer1_points", F * 1024 * 4: "sa3_dense1",
-                F * 1024 * 16: "sa3_dense3_pool"}.get(grid)
-    if "dense_x3s_kernel<" in name:  # split-plane GEMM: <mode, fp32-input>
+    if "dense_x3s_kernel<" in name:  # split-plane GEMM: <mode, fp32-input, x1>
         for key, lab in (("<0, true, false>", "sa2_layer1_points"), ("<1, true, false>", "sa3_dense1"),
                          ("<1, false, false>", "sa3_dense2"), ("<2, false, false>", "sa3_dense3_pool")):
             if key in name:
                 return lab
         return None
+    if "dense_relu_kernel" in name:
+        return {F * 4096 * 2: "dense_shared", F * 1024 * 2: "sa2_layer1_points", F * 1024 * 4: "sa3_dense1",
+                F * 1024 * 16: "sa3_dense3_pool"}.get(grid)
     if "concat_xyz_pad" in name:
         return "concat"
     return None
@@ -130,7 +126,8 @@ def main(cf, cw, pf, pw, out):
     res = {"config": {"workload": "ssg", "points_per_frame": 65536, "frames_per_gpu": 32,
                       "frames_per_launch": FRAMES_PER_LAUNCH},
            "source": "rocprofv3 --kernel-trace --pmc FETCH_SIZE | WRITE_SIZE (separate passes) of "
-                     "bench.py --no-extras --no-cpu-baseline --no-density --no-fp32-mfma-leg --ramp 0 --steps 6 --warmup 1",
+                     "bench.py --no-extras --no-cpu-baseline --no-density --no-fp32-mfma-leg --no-standalone "
+                     "--steps 6 --warmup 1",
            "calibration": cal, "kernels": kern}
     os.makedirs(os.path.dirname(out) or ".", exist_ok=True)
     with open(out, "w") as f:

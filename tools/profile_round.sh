@@ -1,27 +1,35 @@
 #!/bin/bash
-# One GPU-box call that refreshes the round's evidence: GPU tests, the default bench line,
-# the rocprofv3 kernel-trace summary of the same bench, and the two PMC traffic passes
-# (+ their calibration copy).  Every GPU step has its own time limit; steps chained with &&.
-# usage (on the box): bash tools/profile_round.sh TAG
+# One GPU-box call that refreshes a round's evidence, every GPU step under its own time limit and
+# the steps chained so that the first failure ends the call:
+#   1 the GPU tests               2 the default bench line (bench.json)
+#   3 rocprofv3 --kernel-trace --stats of the SSG bench (kernel durations to compare with the
+#     in-bench HIP-event means)
+#   4 PMC: a 1 GiB copy calibrating FETCH_SIZE / WRITE_SIZE, then one pass per counter group over
+#     a short SSG bench (FETCH_SIZE; WRITE_SIZE; the SQ / GRBM VALU group)
+# usage (on the box): bash tools/profile_round.sh TAG [tests|notests]
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-TAG=${1:-r01}
+TAG=${1:-r02}
 O=$R/gpurun_out/$TAG
 mkdir -p $O
 cd $R
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/tests.log 2>&1 || exit 11
-timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err || exit 12
+SHORT="--no-extras --no-cpu-baseline --no-density --no-fp32-mfma-leg --no-standalone --steps 6 --warmup 1"
+if [ "${2:-tests}" = "tests" ]; then
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || exit 11
+fi
+timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err || exit 12
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o prof -- \
-    python3 $R/bench.py --no-extras --no-cpu-baseline --no-density > $O/prof_bench.json 2> $O/prof.err || exit 13
-timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $O/pmc_calib_f -o c -- \
+    python3 $R/bench.py --no-extras --no-cpu-baseline --no-density --no-fp32-mfma-leg > $O/prof_bench.json 2> $O/prof.err || exit 13
+timeout -s KILL 120 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $O/pmc_calib_f -o c -- \
     python3 $R/tools/pmc_calib.py > $O/pmc_calib.log 2>&1 || exit 14
-timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $O/pmc_calib_w -o c -- \
+timeout -s KILL 120 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $O/pmc_calib_w -o c -- \
     python3 $R/tools/pmc_calib.py >> $O/pmc_calib.log 2>&1 || exit 15
-timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o p -- \
-    python3 $R/bench.py --no-extras --no-cpu-baseline --no-density --no-fp32-mfma-leg --ramp 0 --steps 6 --warmup 1 \
-    > $O/pmc_fetch.json 2> $O/pmc_fetch.err || exit 16
-timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o p -- \
-    python3 $R/bench.py --no-extras --no-cpu-baseline --no-density --no-fp32-mfma-leg --ramp 0 --steps 6 --warmup 1 \
-    > $O/pmc_write.json 2> $O/pmc_write.err || exit 17
+timeout -s KILL 240 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o p -- \
+    python3 $R/bench.py $SHORT > $O/pmc_fetch.json 2> $O/pmc_fetch.err || exit 16
+timeout -s KILL 240 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o p -- \
+    python3 $R/bench.py $SHORT > $O/pmc_write.json 2> $O/pmc_write.err || exit 17
+timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
+    SQ_INSTS_SALU SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE --output-format csv -d $O/pmc_valu -o p -- \
+    python3 $R/bench.py $SHORT > $O/pmc_valu.json 2> $O/pmc_valu.err || exit 18
 exit 0

@@ -72,12 +72,12 @@ static int grid_build(grid_t *g, const double *p, int64_t n, double eps)
      * fp64 test can accept; coarsen when the box would need too many cells. */
     double cell = eps * (1.0 + 1.0 / 1048576.0);
     for (;;) {
-        int64_t tot = 1;
-        for (int a = 0; a < 3; ++a) {
-            g->dim[a] = (int64_t)floor((hi[a] - g->lo[a]) / cell) + 1;
-            tot *= g->dim[a];
+        double tot = 1.0; /* in double: a huge box must not overflow the product */
+        for (int a = 0; a < 3; ++a) tot *= floor((hi[a] - g->lo[a]) / cell) + 1.0;
+        if (tot <= 4.0 * n + 64.0 && tot <= (double)(1 << 24)) {
+            for (int a = 0; a < 3; ++a) g->dim[a] = (int64_t)floor((hi[a] - g->lo[a]) / cell) + 1;
+            break;
         }
-        if (tot <= 4 * n + 64 && tot <= (1 << 24)) break;
         cell *= 1.5;
     }
     g->cell = cell;

@@ -474,7 +474,7 @@ def test_host_frame_feed_matches_drop_in(cuda, tmp_path):
         p = tmp_path / f"f{i}.pcd"
         with open(p, "w") as fh:
             fh.write(f"VERSION .7\nFIELDS x y z\nPOINTS {len(f)}\nDATA ascii\n")
-            fh.writelines(f"{a!r} {b!r} {c!r}\n" for a, b, c in np.asarray(f, dtype=np.float64))
+            fh.writelines(f"{a!r} {b!r} {c!r}\n" for a, b, c in np.asarray(f, dtype=np.float64).tolist())
         paths.append(str(p))
     for name, g in zip(names, feed.run_files(paths)):
         _same_analyze(name, g, CrowdDensityModel().analyze(dp.preprocess_lidar_data(dp.load_lidar_data(

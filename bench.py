@@ -182,6 +182,19 @@ DENSITY_BYTES_PER_POINT = {
 }
 
 
+def eps_pairs(x):
+    """Unordered eps-neighbour pairs DBSCAN's graph has for frame x under preprocess_lidar_data
+    (utils/data_processing.py:164-197): the non-ground inliers (z above the 30th percentile),
+    standardised, eps from the heuristic; counted on the GPU by radius_count."""
+    from lidar_ai_recommendation_software_amd import data_processing as dp
+    pts = dp.preprocess_lidar_data(x)["points"]
+    ng = pts[pts[:, 2] > np.percentile(pts[:, 2], 30)]
+    sc = (ng - ng.mean(axis=0)) / ng.std(axis=0)
+    eps = max(0.2, min(0.5, float(np.mean(np.std(sc, axis=0))) * 0.5))
+    cnt = dp.radius_count(sc, eps)
+    return (int(cnt.sum()) - len(sc)) // 2
+
+
 def tier_r_leg(dev, rank, world, frames=32, n=65536, steps=3, cpu=True, cpu_budget=12.0):
     """The reference's own path (Tier R: preprocess -> DBSCAN -> people -> density grid) on
     device-resident uniform +-15 m frames: batches of `frames` frames through
@@ -213,7 +226,22 @@ def tier_r_leg(dev, rank, world, frames=32, n=65536, steps=3, cpu=True, cpu_budg
            "executor": "DensityStream.run_batch (CSR batch, one launch per phase)", "dtype": "f64",
            "parity": "byte-identical to the reference (tests/golden)",
            "phase_ms_per_launch": per_launch_ms, "dominant_phase": dom, "cpu_baseline": None}
-    if dom in DENSITY_BYTES_PER_POINT:
+    if dom.startswith("dbscan"):
+        # DBSCAN decides the eps-graph of the scaled non-ground points: SURVEY §8d prices it as
+        # 8 fp64 FLOP (3 sub, 3 mul, 2 add) per eps-pair against the FP64 VALU peak.  The pairs are
+        # counted exactly on the GPU (radius_count over each frame's scaled non-ground points, the
+        # fp64 test DBSCAN uses); the DBSCAN phases together are the "kernel" priced.
+        pairs = sum(eps_pairs(x.cpu().numpy()) for x in xs)
+        db_ms = sum(v for k, v in per_launch_ms.items() if k.startswith("dbscan"))
+        a = 8.0 * pairs / (db_ms / 1e3) / 1e12
+        rec["roofline"] = {"kernel": "dbscan (grid + count + union + labels)", "bound": "fp64-valu", "achieved": a,
+                           "peak": FP64_VALU_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": a / FP64_VALU_PEAK_TFLOPS,
+                           "traffic": None, "work_per_launch": 8.0 * pairs, "eps_pairs_per_frame": pairs / frames,
+                           "avg_launch_ms": db_ms,
+                           "peak_basis": "FP64 vector peak (FMA counted as 2) over 8 FLOP per eps-pair; the kernels "
+                                         "prune most pairs (same-cell shortcut, cell-pair links stop at the first "
+                                         "link), so this is work avoided, not work done"}
+    elif dom in DENSITY_BYTES_PER_POINT:
         algo = DENSITY_BYTES_PER_POINT[dom] * pts
         a = algo / (per_launch_ms[dom] / 1e3) / 1e9
         rec["roofline"] = {"kernel": dom, "bound": "hbm", "achieved": a, "peak": HBM_PEAK_GBS, "unit": "GB/s",

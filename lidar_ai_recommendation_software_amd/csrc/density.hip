@@ -992,9 +992,40 @@ __global__ void dbscan_intra_kernel(const double *P_in, const uint32_t *cid_in, 
 // A + o both hold core points that are not yet one component, any core of A within eps of any
 // core of B links them.  Each cell's cores are one component (step 1), so the components after
 // this pass are exactly those of the core-core eps graph.
-constexpr int kPairOffsets = 62;
+//
+// The 62 offsets run in two launches: first the 13 touching cells (Chebyshev distance 1), which in
+// a dense frame link almost every pair at the first core tested and merge nearly everything into
+// few components; then the 49 offsets two cells out, most of whose pairs are by then already one
+// component (two finds and out) instead of a full core x core scan that finds no link.  Union-find
+// yields the connected components whatever the order of the unions, so the split is exact.
+// A core u of A whose gap to B's cell box exceeds eps is skipped: the box is taken one part in 2^10
+// of a cell larger on every side, far beyond the rounding of floor((v - lo) / s), so it contains
+// every point binned into B, and the gap never overstates a true distance.
+constexpr int kPairOffsets = 62, kNearOffsets = 13;
+struct PairOffsets {
+    int o[kPairOffsets];
+    constexpr PairOffsets() : o{}
+    {
+        int k = 0;
+        for (int pass = 0; pass < 2; ++pass)
+            for (int v = 63; v < 125; ++v) {  // 5x5x5 row-major; (0,0,0) is 62, after it come the 62
+                const int dx = v / 25 - 2, dy = (v / 5) % 5 - 2, dz = v % 5 - 2;
+                const bool near = dx >= -1 && dx <= 1 && dy >= -1 && dy <= 1 && dz >= -1 && dz <= 1;
+                if (near == (pass == 0)) o[k++] = v;
+            }
+    }
+};
+__constant__ PairOffsets kOffsets = PairOffsets();
+
+__device__ __forceinline__ double box_gap(double v, double lo, double hi)
+{
+    const double a = lo - v, b = v - hi;
+    return a > 0.0 ? a : (b > 0.0 ? b : 0.0);
+}
+
 __global__ void dbscan_cross_kernel(const double *P_in, const uint32_t *start_in, const double *sxyz_in,
-                                    const uint8_t *core_in, const uint32_t *rep_in, int32_t *parent_in, FrameMap fm)
+                                    const uint8_t *core_in, const uint32_t *rep_in, int32_t *parent_in, int o0,
+                                    int no, FrameMap fm)
 {
     const double *P = fm.ws(P_in);
     if (P[P_ACTIVE] == 0.0 || P[P_INTRA] == 0.0) return;
@@ -1004,12 +1035,13 @@ __global__ void dbscan_cross_kernel(const double *P_in, const uint32_t *start_in
     int32_t *parent = fm.ws(parent_in);
     Grid g;
     g.load(P);
-    const int64_t work = (int64_t)P[P_NCELL] * kPairOffsets;
+    const double slack = g.cell * (1.0 / 1024.0);
+    const int64_t work = (int64_t)P[P_NCELL] * no;
     for (int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; w < work; w += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t A = w / kPairOffsets;
+        const int64_t A = w / no;
         const uint32_t ra0 = rep[A];
         if (ra0 == kNoCore) continue;
-        const int o = (int)(w - A * kPairOffsets) + 63;  // 5x5x5 offsets in row-major order; (0,0,0) is 62
+        const int o = kOffsets.o[o0 + (int)(w - A * no)];
         const int64_t ax = A / (g.dim[1] * g.dim[2]), ay = (A / g.dim[2]) % g.dim[1], az = A % g.dim[2];
         const int64_t bx = ax + o / 25 - 2, by = ay + (o / 5) % 5 - 2, bz = az + o % 5 - 2;
         if (bx < 0 || bx >= g.dim[0] || by < 0 || by >= g.dim[1] || bz < 0 || bz >= g.dim[2]) continue;
@@ -1018,11 +1050,20 @@ __global__ void dbscan_cross_kernel(const double *P_in, const uint32_t *start_in
         if (rb0 == kNoCore) continue;
         const int32_t ra = uf_find(parent, (int32_t)ra0), rb = uf_find(parent, (int32_t)rb0);
         if (ra == rb) continue;
+        double blo[3], bhi[3];
+        const int64_t bc[3] = {bx, by, bz};
+        for (int k = 0; k < 3; ++k) {
+            blo[k] = g.lo[k] + (double)bc[k] * g.cell - slack;
+            bhi[k] = g.lo[k] + (double)(bc[k] + 1) * g.cell + slack;
+        }
         bool linked = false;
         const uint32_t b0 = start[B], b1 = start[B + 1];
         for (uint32_t u = start[A], u1 = start[A + 1]; u < u1 && !linked; ++u) {
             if (!core[u]) continue;
             const double px = sxyz[3 * u], py = sxyz[3 * u + 1], pz = sxyz[3 * u + 2];
+            const double gx = box_gap(px, blo[0], bhi[0]), gy = box_gap(py, blo[1], bhi[1]),
+                         gz = box_gap(pz, blo[2], bhi[2]);
+            if ((gx * gx + gy * gy) + gz * gz > g.eps2) continue;
             for (uint32_t v = b0; v < b1; ++v)
                 if (core[v] && lidar::dist2d(px, py, pz, sxyz[3 * v], sxyz[3 * v + 1], sxyz[3 * v + 2]) <= g.eps2) {
                     linked = true;
@@ -1436,8 +1477,9 @@ int run_dbscan(lidar_handle *h, const double *x, int64_t nmax, int32_t min_sampl
     const int32_t limit = (count_only || exact_counts) ? 0x7fffffff : min_samples;
     const unsigned gp = point_blocks(nmax, frames);
     const unsigned gc = point_blocks(w.max_cells, frames);
-    const unsigned gx = point_blocks(w.max_cells * kPairOffsets, frames);
-    const dim3 F1(1, frames), FP(gp, frames), FC(gc, frames), FX(gx, frames);
+    const unsigned gx = point_blocks(w.max_cells * (kPairOffsets - kNearOffsets), frames);
+    const unsigned gn = point_blocks(w.max_cells * kNearOffsets, frames);
+    const dim3 F1(1, frames), FP(gp, frames), FC(gc, frames), FX(gx, frames), FN(gn, frames);
     {
         lidar::Span sp(h, "dbscan_grid", s);  // cell sizes, counting sort by cell
         hipLaunchKernelGGL(dbscan_setup_kernel, F1, dim3(64), 0, s, w.P, w.max_cells, fm);
@@ -1462,8 +1504,10 @@ int run_dbscan(lidar_handle *h, const double *x, int64_t nmax, int32_t min_sampl
     {
         lidar::Span sp(h, "dbscan_union", s);  // fine cells: intra + cross; coarse cells: per-point union
         hipLaunchKernelGGL(dbscan_intra_kernel, FP, dim3(256), 0, s, w.P, w.cid, w.order, w.core, w.fill, w.parent, fm);
+        hipLaunchKernelGGL(dbscan_cross_kernel, FN, dim3(256), 0, s, w.P, w.cellstart, w.sxyz, w.core, w.fill,
+                           w.parent, 0, kNearOffsets, fm);
         hipLaunchKernelGGL(dbscan_cross_kernel, FX, dim3(256), 0, s, w.P, w.cellstart, w.sxyz, w.core, w.fill,
-                           w.parent, fm);
+                           w.parent, kNearOffsets, kPairOffsets - kNearOffsets, fm);
         hipLaunchKernelGGL(dbscan_union_kernel, FP, dim3(256), 0, s, w.P, w.cid, w.cellstart, w.order, w.sxyz,
                            w.cnt, min_samples, w.parent, fm);
     }

@@ -399,6 +399,8 @@ def main():
     ap.add_argument("--x3", type=int, default=1,
                     help="1: MLPs on the split-bf16 (x3) kernels, fp32 arithmetic within the 1e-4 contract; "
                          "0: the native fp32-MFMA kernels")
+    ap.add_argument("--slots", type=int, default=0,
+                    help="StreamingSSG staging slots (0: its default, depth + 3)")
     ap.add_argument("--rotate", type=int, default=8, help="distinct device-resident input batches the feed cycles over")
     ap.add_argument("--no-fp32-mfma-leg", action="store_true",
                     help="skip the extra measurement of the native fp32-MFMA kernels (when --x3 is on)")
@@ -439,18 +441,21 @@ def main():
         nb = max(1, args.rotate)
         xs = [torch.from_numpy(unit_frames(B, N, seed=sharding.frame_seed(seed_rank, step=i))).to(dev) for i in range(nb)]
         refs = [bb.forward(x)[0] for x in xs]  # one-batch forward(): what every pipeline output must equal
-        pipe = pn.StreamingSSG(bb, B, N, depth=depth, fps_group=G, fps_threads=args.fps_threads, ramp=False)
+        ready = torch.cuda.Event()  # the inputs exist: the feed's FPS launches wait only for their slots
+        ready.record()
+        pipe = pn.StreamingSSG(bb, B, N, depth=depth, fps_group=G, fps_threads=args.fps_threads, ramp=False,
+                               slots=args.slots or None)
         feed = pipe.feed()
         nwarm = (depth + max(1, warmup)) * G  # whole groups; `depth` groups in flight when the window opens
         outs = []
         for i in range(nwarm):
-            outs += feed.push(xs[i % nb])
+            outs += feed.push(xs[i % nb], ready)
         timers = pn._Timers()
         win = []
 
         def window(i0, sink):
             for i in range(i0, i0 + steps):
-                sink.extend(feed.push(xs[i % nb]))
+                sink.extend(feed.push(xs[i % nb], ready))
 
         if events:
             bb.timers = timers

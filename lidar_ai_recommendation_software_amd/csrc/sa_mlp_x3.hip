@@ -16,6 +16,7 @@
 // accumulator pair (tiles 2s, 2s+1: channels 16t + 4g + r of point l&15, g = l>>4) is the
 // k-step-s fragment of the next layer with element j <-> channel in(s, g, j) = 32s + 16(j>>2) +
 // 4g + (j&3); the packed weights (lidar_mlp_pack_x3_f32) follow that k order.
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -312,10 +313,209 @@ __global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float 
     }
 }
 
+// max over the four row groups (lanes col, col+16, col+32, col+48) of every column, in all
+// four: v_permlane32_swap / v_permlane16_swap hand each lane its xor-32 / xor-16 partner
+__device__ __forceinline__ float max_row_groups(float v)
+{
+    const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = maxn(v, __uint_as_float(a[0]), __uint_as_float(a[1]));
+    const auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return maxn(v, __uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+
+// Lean form of sa_x3_kernel<.., L1_PRE, R = 2, false> for the wide feature levels (SA2): the same
+// arithmetic, results bit for bit, in <= 128 VGPRs and 34 KiB of LDS, so that a CU holds three
+// of its workgroups beside a resident 512-thread FPS workgroup (two for the 160-VGPR / 50-KiB
+// form).  Layer 2 runs one 16-row tile at a time (only that tile's layer-2 operand is live; its
+// weight chunks stream through LDS once per tile), layer 3 keeps R = 2 (both tiles share every
+// weight fragment), and the max-pool is a register max: per chunk, each lane's max over its rows
+// is reduced over the four row groups by two lane swaps and folded into mx[t / 4] of row group
+// t % 4 — no LDS table.
+template <int C1, int C2, int C3, int NS>
+__global__ __launch_bounds__(256, 4) void sa_x3_lean_kernel(const float *__restrict__ P, int64_t stride,
+                                                            const float *__restrict__ Q,
+                                                            const int32_t *__restrict__ idx, int n, int m,
+                                                            int64_t total, const uint4 *__restrict__ packed,
+                                                            float *__restrict__ out, int64_t out_stride,
+                                                            int64_t out_offset)
+{
+    constexpr int R = 2;
+    static_assert(NS % (16 * R) == 0 && C1 % 32 == 0 && C2 % 32 == 0 && C3 % 64 == 0, "tile shapes");
+    using K = PackX3<C1, C2, C3, false>;
+    constexpr int T1 = K::T1, T2 = K::T2, T3 = K::T3, KS2 = K::KS2, KS3 = K::KS3;
+    constexpr int CH2 = K::CH2, CH3 = K::CH3, CHMAX = CH2 > CH3 ? CH2 : CH3;
+    constexpr int NL2 = T2 / 2, NL3 = T3 / 2, NSEQ = R * NL2 + NL3;  // chunk passes per iteration
+    constexpr int ITERS = NS / (16 * R);
+    constexpr int PER = (CHMAX + 255) / 256;
+
+    __shared__ uint4 buf[2][CHMAX];
+    __shared__ float bias_s[C2 + C3];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int q = lane >> 4, col = lane & 15;
+    const int64_t unit = (int64_t)blockIdx.x * 4 + wave;
+    const bool live = unit < total;
+    const int64_t cc = live ? unit : total - 1;
+    const int64_t b = cc / m;
+
+    const uint4 *W2 = packed;
+    const uint4 *W3 = W2 + (int64_t)NL2 * CH2;
+    const float *Bias = reinterpret_cast<const float *>(W3 + (int64_t)NL3 * CH3);
+
+    // pass `seq` of an iteration: layer-2 chunk seq % NL2 for tile seq / NL2, then the layer-3 chunks
+    auto fetch = [&](int seq, int dst) {
+        const int c = seq < R * NL2 ? seq % NL2 : seq - R * NL2 + NL2;
+        const uint4 *src = c < NL2 ? W2 + c * CH2 : W3 + (c - NL2) * CH3;
+        asm volatile("" : "+s"(src));
+        const int len = c < NL2 ? CH2 : CH3;
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int base = 256 * i + 64 * wave;
+            if (base < len)
+                __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)(src + base + (unsigned)lane),
+                                                 (__attribute__((address_space(3))) void *)(&buf[dst][base]), 16, 0,
+                                                 0);
+        }
+    };
+    fetch(0, 0);
+    for (int i = tid; i < C2 + C3; i += 256) bias_s[i] = Bias[C1 + i];
+    __syncthreads();
+    float mx[T3 / 4];
+#pragma unroll
+    for (int j = 0; j < T3 / 4; ++j) mx[j] = -INFINITY;
+    int par = 0;
+
+#pragma unroll 1
+    for (int it = 0; it < ITERS; ++it) {
+        bf16x8 zh[R][KS3], zl[R][KS3];
+#pragma unroll
+        for (int rr = 0; rr < R; ++rr) {
+            // layer 1 of this tile's 16 rows: relu(P[k] - Q[c]) as the layer-2 hi / lo fragments
+            bf16x8 xh[KS2], xl[KS2];
+            {
+                int zero = 0;
+                asm volatile("" : "+v"(zero));
+                const int64_t k = idx[cc * NS + (it * R + rr) * 16 + col];
+                const f32x4 *pp = reinterpret_cast<const f32x4 *>(P + ((int64_t)b * n + k) * stride + 4 * q);
+                const f32x4 *qq = reinterpret_cast<const f32x4 *>(Q + cc * stride + 4 * q + zero);
+#pragma unroll
+                for (int s = 0; s < KS2; ++s) {
+                    f32x4 y[2];
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const f32x4 a = pp[4 * (2 * s + h)], c = qq[4 * (2 * s + h)];
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) y[h][r] = relu(a[r] - c[r]);
+                    }
+                    split_pair(y[0], y[1], xh[s], xl[s]);
+                }
+            }
+#pragma unroll
+            for (int c = 0; c < NL2; ++c) {
+                fetch(rr * NL2 + c + 1, par ^ 1);  // a layer-3 pass always follows: lands during these MFMAs
+                const uint4 *wb = buf[par] + lane;
+                f32x4 a0 = *reinterpret_cast<const f32x4 *>(&bias_s[16 * (2 * c) + 4 * q]);
+                f32x4 a1 = *reinterpret_cast<const f32x4 *>(&bias_s[16 * (2 * c + 1) + 4 * q]);
+#pragma unroll
+                for (int s = 0; s < KS2; ++s) {
+                    const bf16x8 h0 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 0) * 2 + 0) * 64]);
+                    const bf16x8 l0 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 0) * 2 + 1) * 64]);
+                    a0 = mfma_bf(h0, xh[s], a0);
+                    a0 = mfma_bf(h0, xl[s], a0);
+                    a0 = mfma_bf(l0, xh[s], a0);
+                    const bf16x8 h1 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 1) * 2 + 0) * 64]);
+                    const bf16x8 l1 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 1) * 2 + 1) * 64]);
+                    a1 = mfma_bf(h1, xh[s], a1);
+                    a1 = mfma_bf(h1, xl[s], a1);
+                    a1 = mfma_bf(l1, xh[s], a1);
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    a0[r] = relu_i(a0[r]);
+                    a1[r] = relu_i(a1[r]);
+                }
+                split_pair(a0, a1, zh[rr][c], zl[rr][c]);  // layer-2 chunk c = layer-3 k-step c
+                __syncthreads();
+                par ^= 1;
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < NL3; ++c) {
+            if (c + 1 < NL3 || it + 1 < ITERS) fetch(c + 1 < NL3 ? R * NL2 + c + 1 : 0, par ^ 1);
+            const uint4 *wb = buf[par] + lane;
+            f32x4 a0[R], a1[R];
+#pragma unroll
+            for (int rr = 0; rr < R; ++rr) a0[rr] = a1[rr] = f32x4{};
+#pragma unroll
+            for (int s = 0; s < KS3; ++s) {
+                const bf16x8 h0 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 0) * 2 + 0) * 64]);
+                const bf16x8 h1 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 1) * 2 + 0) * 64]);
+                const bf16x8 l0 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 0) * 2 + 1) * 64]);
+                const bf16x8 l1 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 1) * 2 + 1) * 64]);
+#pragma unroll
+                for (int rr = 0; rr < R; ++rr) {
+                    a0[rr] = mfma_bf(zh[rr][s], h0, a0[rr]);
+                    a1[rr] = mfma_bf(zh[rr][s], h1, a1[rr]);
+                    a0[rr] = mfma_bf(zh[rr][s], l0, a0[rr]);
+                    a1[rr] = mfma_bf(zh[rr][s], l1, a1[rr]);
+                    a0[rr] = mfma_bf(zl[rr][s], h0, a0[rr]);
+                    a1[rr] = mfma_bf(zl[rr][s], h1, a1[rr]);
+                }
+            }
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh) {
+                const int t = 2 * c + hh;
+                float v = -INFINITY;
+#pragma unroll
+                for (int rr = 0; rr < R; ++rr) {
+                    const f32x4 &acc = hh ? a1[rr] : a0[rr];
+                    v = maxn(maxn(v, acc[0], acc[1]), acc[2], acc[3]);
+                }
+                v = max_row_groups(v);
+                if (q == (t & 3)) mx[t >> 2] = __builtin_elementwise_maximum(mx[t >> 2], v);
+            }
+            __syncthreads();
+            par ^= 1;
+        }
+    }
+    static_assert(NSEQ == R * NL2 + NL3, "pass count");
+    if (live) {
+        float *o = out + unit * out_stride + out_offset;
+#pragma unroll
+        for (int j = 0; j < T3 / 4; ++j) {
+            const int c3 = 16 * (4 * j + q) + col;
+            o[c3] = relu(mx[j] + bias_s[C2 + c3]);
+        }
+    }
+}
+
 // LIDAR_X3_ROWS: 16-row tiles per wavefront (A/B builds; 2 unless NS = 16)
 #ifndef LIDAR_X3_ROWS
 #define LIDAR_X3_ROWS 2
 #endif
+
+// lean SA2 kernels (sa_x3_lean_kernel) unless LIDAR_SA_LEAN=0 (A/B switch)
+static bool use_lean()
+{
+    static const bool on = [] {
+        const char *e = getenv("LIDAR_SA_LEAN");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+template <int C1, int C2, int C3, int NS>
+int launch_x3_lean(const float *p, int64_t stride, const float *q, const int32_t *idx, int64_t batch, int64_t n,
+                   int64_t m, const void *packed, float *out, int64_t os, int64_t oo, hipStream_t s)
+{
+    const int64_t total = batch * m;
+    const int64_t blocks = (total + 3) / 4;
+    REQUIRE(blocks <= 0x7fffffff, "sa_group_mlp_x3: too many centres");
+    hipLaunchKernelGGL((sa_x3_lean_kernel<C1, C2, C3, NS>), dim3((unsigned)blocks), dim3(256), 0, s, p, stride, q,
+                       idx, (int)n, (int)m, total, static_cast<const uint4 *>(packed), out, os, oo);
+    LAUNCH_CHECK();
+    return LIDAR_OK;
+}
 
 template <int C1, int C2, int C3, int NS, int L1, bool X1 = false>
 int launch_x3(const float *p, int64_t stride, const float *q, const int32_t *idx, int64_t batch, int64_t n,
@@ -416,6 +616,14 @@ LIDAR_EXPORT int lidar_sa_group_mlp_x3_f32(lidar_handle *h, int32_t xyz_level, c
     if (batch == 0) return LIDAR_OK;
     ON_DEVICE(h->device);
     hipStream_t s = static_cast<hipStream_t>(stream);
+    if (!xyz_level && c1 == 128 && c2 == 128 && c3 == 256 && use_lean()) {
+        if (nsample == 64)
+            return launch_x3_lean<128, 128, 256, 64>(p, p_stride, q, idx, batch, n, m, packed, out, out_stride,
+                                                     out_offset, s);
+        if (nsample == 128)
+            return launch_x3_lean<128, 128, 256, 128>(p, p_stride, q, idx, batch, n, m, packed, out, out_stride,
+                                                      out_offset, s);
+    }
 #define LIDAR_SAX3(C1_, C2_, C3_, NS_, X_)                                                                   \
     if (!!xyz_level == X_ && c1 == C1_ && c2 == C2_ && c3 == C3_ && nsample == NS_)                           \
         return launch_x3<C1_, C2_, C3_, NS_, X_ ? L1_XYZ : L1_PRE>(p, p_stride, q, idx, batch, n, m, packed, out, \

@@ -642,7 +642,7 @@ class StreamingSSG:
     SA2's nested FPS and ball queries, group_all) fills the whole GPU.  Later batches' SA1 FPS
     and level-0 ball queries therefore run on `depth` side streams (own library handles /
     workspaces) while earlier batches' remaining levels run on the main stream; events order
-    the hand-off and a ring of `depth + 1` slots bounds memory.
+    the hand-off and a ring of `slots` (default depth + 3) staging slots bounds memory.
 
     fps_group = G > 1: G consecutive batches are staged into one (G*B, N, 3) buffer; one
     side-stream launch runs their SA1 FPS (G*B workgroups share the serial chain of steps
@@ -656,9 +656,13 @@ class StreamingSSG:
     """
 
     def __init__(self, backbone, batch, n, depth=1, fps_group=1, fps_threads=0, side_priority=0, ramp=True,
-                 reserve=True, keep_levels=False):
+                 reserve=True, keep_levels=False, slots=None):
         """fps_threads: SA1 FPS workgroup size (0 = 1024; 512: half the CU footprint beside the
         MLPs).  ramp: in run(), the first groups hold 1, 2, ... batches (a shorter pipeline fill).
+        slots: staging slots (>= depth + 1; default depth + 3).  Group k's FPS reuses the slot of
+        group k - slots, so it waits for that group's main-stream pass: with depth + 1 slots the
+        side chain could only start a group once the main stream was `depth` groups behind it,
+        which left the main stream idle whenever FPS took about `depth` main passes.
         keep_levels: every output is (global feature, per-level (new_xyz, features, fps idx,
         [ball-query idx per branch])) instead of the global feature alone."""
         self.bb = backbone
@@ -672,7 +676,10 @@ class StreamingSSG:
         # side_priority < 0 puts the latency-bound FPS chains ahead of the MLP waves in the
         # dispatcher (HIP stream priority); results do not depend on it
         self.fps_streams = [torch.cuda.Stream(device=dev, priority=side_priority) for _ in range(depth)]
-        nslot = depth + 1
+        nslot = depth + 3 if slots is None else int(slots)
+        if nslot < depth + 1:
+            raise ValueError("StreamingSSG: slots must be >= depth + 1")
+        self.nslot = nslot
         GB = self.G * batch
         self.stage = [torch.empty((GB, n, 3), dtype=torch.float32, device=dev) if self.G > 1 else None
                       for _ in range(nslot)]
@@ -694,12 +701,14 @@ class StreamingSSG:
             e.record(torch.cuda.current_stream(dev))
 
     def _fps(self, k, xs, ready):
-        """SA1 FPS + level-0 ball queries of group k (the batches in xs) on a side stream."""
-        slot = k % (self.depth + 1)
+        """SA1 FPS + level-0 ball queries of group k (the batches in xs, readable after the
+        events in `ready`) on a side stream."""
+        slot = k % self.nslot
         fs = self.fps_streams[k % self.depth]
         hs = 1 + k % self.depth  # the side stream's own library handle
         fs.wait_event(self.slot_free[slot])
-        fs.wait_event(ready)
+        for ev in ready:
+            fs.wait_event(ev)
         g = len(xs) * self.B
         t = self.bb.timers
         with torch.cuda.stream(fs):
@@ -768,29 +777,39 @@ class _Feed:
         self.p = pipe
         self.main = torch.cuda.current_stream(pipe.bb.device)
         self.buf, self.pending, self.k = [], [], 0
+        self.readies = []  # push()'s ready event per buffered batch
 
-    def _issue(self, xs):
-        ready = torch.cuda.Event()
-        ready.record(self.main)  # the inputs exist on the caller's stream
-        self.pending.append((self.p._fps(self.k, xs, ready), xs))
+    def _issue(self, xs, readies=None):
+        evs = [e for e in (readies or [None]) if e is not None]
+        if readies is None or len(evs) < len(readies):
+            ev = torch.cuda.Event()
+            ev.record(self.main)  # the inputs exist on the caller's stream
+            evs.append(ev)
+        self.pending.append((self.p._fps(self.k, xs, evs), xs))
         self.k += 1
         if len(self.pending) > self.p.depth:
             slot, pxs = self.pending.pop(0)
             return self.p._rest(slot, pxs, self.main)
         return []
 
-    def push(self, x):
+    def push(self, x, ready=None):
+        """ready: a CUDA event after which x is readable; None records one on the caller's stream
+        when the group issues — which also orders the group's FPS after every main-stream pass
+        issued so far, so a feed whose inputs were produced earlier passes the producer's event."""
         self.buf.append(x)
+        self.readies.append(ready)
         if len(self.buf) < self.p.G:
             return []
-        xs, self.buf = self.buf, []
-        return self._issue(xs)
+        xs, evs = self.buf, self.readies
+        self.buf, self.readies = [], []
+        return self._issue(xs, evs)
 
     def flush(self):
         out = []
         if self.buf:
-            xs, self.buf = self.buf, []
-            out += self._issue(xs)
+            xs, evs = self.buf, self.readies
+            self.buf, self.readies = [], []
+            out += self._issue(xs, evs)
         while self.pending:
             slot, pxs = self.pending.pop(0)
             out += self.p._rest(slot, pxs, self.main)

@@ -209,6 +209,22 @@ def test_group_mlp_x3(cuda, cfg_name, level, branch):
         feat_close(got[bi, :, off:off + widths[-1]], want, f"{cfg_name} L{level} br{branch} frame {bi} (x3)")
 
 
+def test_sa2_lean_kernel_bit_identical(cuda, tmp_path):
+    """The lean SA2 kernel (sa_x3_lean_kernel: <= 128 VGPRs, register max-pool, layer 2 one tile
+    at a time) computes the same products in the same order as the 160-VGPR sa_x3_kernel: outputs
+    equal bit for bit (the 160-VGPR form runs in a child process under LIDAR_SA_LEAN=0)."""
+    import os
+    import subprocess
+    import sys
+    import lean_ab_case
+    got = np.concatenate([a.ravel() for a in lean_ab_case.run(cuda)])
+    ref = tmp_path / "ref.npy"
+    env = dict(os.environ, LIDAR_SA_LEAN="0")
+    subprocess.run([sys.executable, lean_ab_case.__file__, str(ref)], env=env, check=True, timeout=300)
+    want = np.load(ref)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
 def test_dense_no_relu(cuda):
     rng = np.random.default_rng(2)
     x = rng.standard_normal((256, 144)).astype(np.float32)

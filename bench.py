@@ -401,6 +401,9 @@ def main():
                          "0: the native fp32-MFMA kernels")
     ap.add_argument("--slots", type=int, default=0,
                     help="StreamingSSG staging slots (0: its default, depth + 3)")
+    ap.add_argument("--bq", default="side", choices=["side", "bin", "main"],
+                    help="SA1 ball queries: on the FPS side streams, binning there + queries on the main "
+                         "stream, or all on the main stream (StreamingSSG bq)")
     ap.add_argument("--rotate", type=int, default=8, help="distinct device-resident input batches the feed cycles over")
     ap.add_argument("--no-fp32-mfma-leg", action="store_true",
                     help="skip the extra measurement of the native fp32-MFMA kernels (when --x3 is on)")
@@ -444,7 +447,7 @@ def main():
         ready = torch.cuda.Event()  # the inputs exist: the feed's FPS launches wait only for their slots
         ready.record()
         pipe = pn.StreamingSSG(bb, B, N, depth=depth, fps_group=G, fps_threads=args.fps_threads, ramp=False,
-                               slots=args.slots or None)
+                               slots=args.slots or None, bq=args.bq)
         feed = pipe.feed()
         nwarm = (depth + max(1, warmup)) * G  # whole groups; `depth` groups in flight when the window opens
         outs = []
@@ -560,7 +563,7 @@ def main():
     # in flight; FPS is one workgroup per frame, latency-bound: read as us/step) and the main
     # stream's full-chip kernels.  The roofline is reported for the kernel that dominates the
     # main chain's device time; the chain lengths say which chain bounds a step.
-    side = ("sa1_fps", "sa1_ball_query")
+    side = ("sa1_fps", "sa1_ball_query", "sa1_bq_bin") if args.bq == "side" else ("sa1_fps", "sa1_bq_bin")
     per_launch = {k: t / c for k, (c, f, t) in tot.items()}
     main_k = {k: v for k, v in per_launch.items() if k not in side}
     side_ms = sum(per_launch.get(k, 0) for k in side) / args.depth
@@ -604,7 +607,7 @@ def main():
             "pipeline": {"executor": "pointnet2.StreamingSSG feed (steady state: the window pushes and completes "
                                      "exactly `steps` batches; pipeline fill and drain outside it)",
                          "side_streams": args.depth, "batches_per_group": G, "frames_per_launch": G * B,
-                         "fps_threads": args.fps_threads, **chains},
+                         "fps_threads": args.fps_threads, "sa1_ball_queries": args.bq, **chains},
             "fp32_mfma_kernels": fp32_mfma,
             "other_configs": extras,
             "density_path": density,

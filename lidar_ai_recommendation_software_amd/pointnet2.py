@@ -525,13 +525,15 @@ class PointNet2Backbone:
         self.out_channels = cfeat
         self.timers = None  # set to a _Timers() to time every launch
 
-    def forward_from_sa1_fps(self, xyz, idx1, new_xyz1, fz1, gidx1, keep_levels=False):
-        """forward() with level 0's FPS and ball queries already computed (StreamingSSG)."""
-        return self.forward(xyz, keep_levels, pre={0: {"fps": (idx1, new_xyz1, fz1), "bq": gidx1}})
+    def forward_from_sa1_fps(self, xyz, idx1, new_xyz1, fz1, gidx1=None, keep_levels=False, grids1=None):
+        """forward() with level 0's FPS (and its ball queries: gidx1, or their binning: grids1)
+        already computed (StreamingSSG)."""
+        return self.forward(xyz, keep_levels, pre={0: {"fps": (idx1, new_xyz1, fz1), "bq": gidx1, "grid": grids1}})
 
     def forward(self, xyz, keep_levels=False, pre=None):
-        """pre: {level: {"fps": (idx, new_xyz, first_zero), "bq": [gidx per branch]}} — work already
-        done for those levels (StreamingSSG's side streams); every other step runs here."""
+        """pre: {level: {"fps": (idx, new_xyz, first_zero), "bq": [gidx per branch] | "grid": [ball_query_bin
+        buffer per branch]}} — work already done for those levels (StreamingSSG's side streams);
+        every other step runs here."""
         pre = pre or {}
         B, N, _ = xyz.shape
         N0 = N  # npoint_div is relative to the input frame (N/16, N/64)
@@ -575,7 +577,8 @@ class PointNet2Backbone:
                 if pl.get("bq") is not None:
                     gidx = pl["bq"][bi_]
                 else:
-                    gidx = _call(t, f"{tag}_ball_query", B, ball_query, br["r"], br["ns"], xyz, new_xyz)
+                    grid = pl["grid"][bi_] if pl.get("grid") is not None else None
+                    gidx = _call(t, f"{tag}_ball_query", B, ball_query, br["r"], br["ns"], xyz, new_xyz, grid=grid)
                 gidxs.append(gidx)
                 if self.bf16:
                     if pq is not None:
@@ -656,7 +659,7 @@ class StreamingSSG:
     """
 
     def __init__(self, backbone, batch, n, depth=1, fps_group=1, fps_threads=0, side_priority=0, ramp=True,
-                 reserve=True, keep_levels=False, slots=None):
+                 reserve=True, keep_levels=False, slots=None, bq="side"):
         """fps_threads: SA1 FPS workgroup size (0 = 1024; 512: half the CU footprint beside the
         MLPs).  ramp: in run(), the first groups hold 1, 2, ... batches (a shorter pipeline fill).
         slots: staging slots (>= depth + 1; default depth + 3).  Group k's FPS reuses the slot of
@@ -670,6 +673,9 @@ class StreamingSSG:
         self.ramp = bool(ramp)
         self.fps_threads = int(fps_threads)
         self.keep = bool(keep_levels)
+        if bq not in ("side", "bin", "main"):
+            raise ValueError("StreamingSSG: bq must be 'side', 'bin' or 'main'")
+        self.bq = bq
         dev = backbone.device
         lvl0 = backbone.levels[0]
         self.M1 = max(1, n // lvl0["div"])
@@ -687,7 +693,9 @@ class StreamingSSG:
         self.cxyz = [torch.empty((GB, self.M1, 3), dtype=torch.float32, device=dev) for _ in range(nslot)]
         self.fz = [torch.empty(GB, dtype=torch.int32, device=dev) for _ in range(nslot)]
         self.gidx = [[torch.empty((GB, self.M1, br["ns"]), dtype=torch.int32, device=dev)
-                      for br in lvl0["branches"]] for _ in range(nslot)]
+                      for br in lvl0["branches"]] for _ in range(nslot)] if bq == "side" else None
+        self.grid = [[ball_query_grid_buffer(GB, n, dev) for br in lvl0["branches"]]
+                     for _ in range(nslot)] if bq == "bin" else None
         # setup-time workspace sizing of the side handles (FPS + ball queries), so no stage's
         # first call allocates (lidar_reserve; a grow re-allocates after a device sync)
         if reserve:
@@ -725,8 +733,11 @@ class StreamingSSG:
             lvl0 = self.bb.levels[0]
             for bi_, br in enumerate(lvl0["branches"]):
                 tag = "sa1" + (f"_b{bi_}" if len(lvl0["branches"]) > 1 else "")
-                _call(t, f"{tag}_ball_query", g, ball_query, br["r"], br["ns"], x, self.cxyz[slot][:g],
-                      out=self.gidx[slot][bi_][:g], slot=hs)
+                if self.bq == "side":
+                    _call(t, f"{tag}_ball_query", g, ball_query, br["r"], br["ns"], x, self.cxyz[slot][:g],
+                          out=self.gidx[slot][bi_][:g], slot=hs)
+                elif self.bq == "bin":  # depends only on the points: the queries run on the main stream
+                    _call(t, f"{tag}_bq_bin", g, ball_query_bin, br["r"], br["ns"], x, self.grid[slot][bi_], slot=hs)
             self.fps_done[slot].record(fs)
         return slot
 
@@ -736,10 +747,12 @@ class StreamingSSG:
         main.wait_event(self.fps_done[slot])
         B, g = self.B, len(xs) * self.B
         x = self.stage[slot][:g] if self.G > 1 else xs[0]
-        lvl0 = [self.idx[slot][:g], self.cxyz[slot][:g], self.fz[slot][:g], [gi[:g] for gi in self.gidx[slot]]]
+        lvl0 = [self.idx[slot][:g], self.cxyz[slot][:g], self.fz[slot][:g],
+                [gi[:g] for gi in self.gidx[slot]] if self.gidx is not None else None]
         if self.keep:  # the slot's buffers are reused by a later group
-            lvl0 = [a.clone() for a in lvl0[:3]] + [[gi.clone() for gi in lvl0[3]]]
-        out, levels = self.bb.forward_from_sa1_fps(x, *lvl0, keep_levels=self.keep)
+            lvl0 = [a.clone() for a in lvl0[:3]] + [[gi.clone() for gi in lvl0[3]] if lvl0[3] is not None else None]
+        out, levels = self.bb.forward_from_sa1_fps(x, *lvl0, keep_levels=self.keep,
+                                                   grids1=self.grid[slot] if self.grid is not None else None)
         self.slot_free[slot].record(main)
         outs = list(out.split(B))
         if not self.keep:

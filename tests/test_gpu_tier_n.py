@@ -209,20 +209,20 @@ def test_group_mlp_x3(cuda, cfg_name, level, branch):
         feat_close(got[bi, :, off:off + widths[-1]], want, f"{cfg_name} L{level} br{branch} frame {bi} (x3)")
 
 
-def test_sa2_lean_kernel_bit_identical(cuda, tmp_path):
-    """The lean SA2 kernel (sa_x3_lean_kernel: <= 128 VGPRs, register max-pool, layer 2 one tile
-    at a time) computes the same products in the same order as the 160-VGPR sa_x3_kernel: outputs
-    equal bit for bit (the 160-VGPR form runs in a child process under LIDAR_SA_LEAN=0)."""
+def test_sa_kernel_variants_bit_identical(cuda, tmp_path):
+    """The lean feature-level kernel (sa_x3_lean_kernel: <= 128 VGPRs, register max-pool, layer 2
+    one tile at a time) computes the same products in the same order as the 160-VGPR sa_x3_kernel:
+    outputs equal bit for bit.  The 160-VGPR form runs in a child process under LIDAR_SA_LEAN=0."""
     import os
     import subprocess
     import sys
-    import lean_ab_case
-    got = np.concatenate([a.ravel() for a in lean_ab_case.run(cuda)])
+    import sa_variants_case
+    got = np.concatenate([a.ravel() for a in sa_variants_case.run(cuda)])
     ref = tmp_path / "ref.npy"
     env = dict(os.environ, LIDAR_SA_LEAN="0")
-    subprocess.run([sys.executable, lean_ab_case.__file__, str(ref)], env=env, check=True, timeout=300)
+    subprocess.run([sys.executable, sa_variants_case.__file__, str(ref)], env=env, check=True, timeout=300)
     want = np.load(ref)
-    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+    assert got.size == want.size and np.array_equal(got.view(np.uint32), want.view(np.uint32))
 
 
 def test_dense_no_relu(cuda):
@@ -364,14 +364,19 @@ def test_streaming_grouped_fps_matches_forward(cuda, cfg_name, dtype, group, dep
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("group,depth,threads,nb", [(3, 3, 512, 7), (2, 2, 1024, 4), (4, 2, 512, 5)])
-def test_streaming_bench_policy_matches_forward(cuda, group, depth, threads, nb):
-    """the bench's executor policy: 512-thread SA1 FPS + ball queries on the side streams, groups
-    of batches (partial last group), ramped groups."""
+@pytest.mark.parametrize("group,depth,threads,nb,bq,slots", [
+    (3, 3, 512, 7, "side", None), (2, 2, 1024, 4, "side", 3), (4, 2, 512, 5, "side", None),
+    (3, 3, 512, 7, "bin", None), (2, 2, 512, 5, "main", 4), (4, 3, 512, 9, "main", None)])
+def test_streaming_bench_policy_matches_forward(cuda, group, depth, threads, nb, bq, slots):
+    """the bench's executor policies: 512-thread SA1 FPS on the side streams with the level-0 ball
+    queries there, binned there and answered on the main stream, or all on the main stream;
+    staging slots from the minimum (depth + 1) up; groups of batches (partial last group), ramped
+    groups."""
     bb = pn.PointNet2Backbone(pn.SSG, device=cuda, seed=4)
     xs = [torch.from_numpy(unit_frames(2, 8192, 50 + s)).to(cuda) for s in range(nb)]
     want = [bb.forward(x)[0] for x in xs]
-    got = pn.StreamingSSG(bb, 2, 8192, depth=depth, fps_group=group, fps_threads=threads).run(xs)
+    got = pn.StreamingSSG(bb, 2, 8192, depth=depth, fps_group=group, fps_threads=threads, bq=bq,
+                          slots=slots).run(xs)
     torch.cuda.synchronize()
     assert len(got) == nb
     for a, b in zip(got, want):

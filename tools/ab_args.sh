@@ -9,7 +9,11 @@ for rep in $(seq 1 $REPS); do
   i=0
   for arm in "$@"; do
     i=$((i + 1))
-    timeout -k 10 300 env $arm_env python bench.py $BASE $arm > $O/arm${i}_$rep.json 2> $O/arm${i}_$rep.err || exit 1
+    envs=(); args=()
+    for tok in $arm; do
+      if [[ ${#args[@]} -eq 0 && $tok == *=* && $tok != -* ]]; then envs+=("$tok"); else args+=("$tok"); fi
+    done
+    timeout -k 10 300 env "${envs[@]}" python bench.py $BASE "${args[@]}" > $O/arm${i}_$rep.json 2> $O/arm${i}_$rep.err || exit 1
     python - $O/arm${i}_$rep.json "$arm" <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])

@@ -401,9 +401,10 @@ def main():
                          "0: the native fp32-MFMA kernels")
     ap.add_argument("--slots", type=int, default=0,
                     help="StreamingSSG staging slots (0: its default, depth + 3)")
-    ap.add_argument("--bq", default="side", choices=["side", "bin", "main"],
-                    help="SA1 ball queries: on the FPS side streams, binning there + queries on the main "
-                         "stream, or all on the main stream (StreamingSSG bq)")
+    ap.add_argument("--bq", default="bin", choices=["side", "bin", "main"],
+                    help="SA1 ball queries (StreamingSSG bq): binning on the FPS side streams and the queries "
+                         "inside the SA1 MLP kernel (bin), both on the main stream (main), or binning + a "
+                         "query launch on the side streams (side)")
     ap.add_argument("--rotate", type=int, default=8, help="distinct device-resident input batches the feed cycles over")
     ap.add_argument("--no-fp32-mfma-leg", action="store_true",
                     help="skip the extra measurement of the native fp32-MFMA kernels (when --x3 is on)")

@@ -206,6 +206,21 @@ int lidar_sa_group_mlp_x3_f32(lidar_handle *h, int32_t xyz_level, const float *p
                               const void *packed, float *out, int64_t out_stride,
                               int64_t out_offset, void *stream);
 
+/* An xyz level's SA branch with its ball queries answered inside the MLP kernel: grid =
+ * lidar_ball_query_bin_f32(xyz, radius, nsample) for these frames; each wavefront queries its
+ * centre from the grid into LDS, then groups, runs the MLP and max-pools.  Equal bit for bit to
+ * lidar_ball_query_binned_f32 followed by lidar_sa_group_mlp_x3_f32 (x1 = 0; packed from
+ * lidar_mlp_pack_x3_f32 with xyz_level = 1) or lidar_sa_group_mlp_x1_f32 mode 0 (x1 = 1; packed
+ * from lidar_mlp_pack_x1_f32).  xyz (batch, n, 3), centres (batch, m, 3); out_idx (batch, m,
+ * nsample) int32 or NULL receives the ball-query indices.  Shapes: (c1, c2, c3, nsample) in
+ * {(64, 64, 128, 32), (32, 32, 64, 16), (64, 96, 128, 128)}.  Replaces, for these levels, the
+ * pointnet2 `ball_query` + `group_points` + shared-MLP sequence behind the north_star's SA layer
+ * (no reference counterpart: SURVEY §0). */
+int lidar_sa_group_mlp_bq_f32(lidar_handle *h, int32_t x1, const float *xyz, const void *grid, const float *centres,
+                              int64_t batch, int64_t n, int64_t m, float radius, int32_t nsample, int32_t c1,
+                              int32_t c2, int32_t c3, const void *packed, float *out, int64_t out_stride,
+                              int64_t out_offset, int32_t *out_idx, void *stream);
+
 /* y (batch*m, ldy) columns [col0, col0+3) = xyz rows; columns [col0+3, ldy) zeroed —
  * builds group_all's input [feats, xyz, 0-pad] next to features already in y. */
 int lidar_concat_xyz_pad_f32(lidar_handle *h, const float *xyz, int64_t rows, float *y,

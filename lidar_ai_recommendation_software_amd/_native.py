@@ -63,6 +63,7 @@ SIGNATURES = {
     "lidar_mlp_packed_size_x1": [I32, I32, I32],
     "lidar_fps_workspace_bytes": [I64, I64],
     "lidar_mlp_pack_x1_f32": [I32, I32, I32, P, P, P, P, P, P, P],
+    "lidar_sa_group_mlp_bq_f32": [P, I32, P, P, P, I64, I64, I64, F32, I32, I32, I32, I32, P, P, I64, I64, P, P],
     "lidar_sa_group_mlp_x1_f32": [P, I32, P, I64, P, P, P, P, I64, I64, I64, I32, I32, I32, I32, P, P, I64, I64, P],
     "lidar_mlp_packed_size16": [I32, I32, I32, I32],
     "lidar_mlp_pack16_f32": [I32, I32, I32, I32, P, P, P, P, P, P, P],

@@ -25,7 +25,7 @@
 //   nsample hits.
 #include <cstdlib>
 
-#include "common.hpp"
+#include "bq_grid.hpp"
 
 namespace {
 
@@ -107,39 +107,7 @@ __global__ __launch_bounds__(256) void ball_query_kernel(const float *__restrict
 
 
 // ------------------------------------------------------------------ grid ball query
-constexpr int kTab = 16384;     // (window, cell) slots per frame: one int each in LDS (64 KiB)
-constexpr int kCap = 512;       // candidates per window a wavefront ranks in LDS
-constexpr int kGridMinN = 1024;  // below this the index-order scan is as cheap
-
-struct BqGrid {  // per frame, written by bq_bin_kernel
-    float minx, miny, minz, inv_s;
-    int dx, dy, dz, ncell;  // cells per axis; ncell = dx * dy * dz
-    int win_shift, nwin;    // windows of 2^win_shift consecutive indices
-    int pad[2];
-};
-
-// per frame: BqGrid (64 B) | tab[kTab + 64] | sorted float4[n]
-__host__ __device__ constexpr uint64_t grid_frame_bytes(int64_t n)
-{
-    return 64 + (uint64_t)(kTab + 64) * 4 + (uint64_t)n * 16;
-}
-
-// cell coordinate of v on one axis; centres may lie outside the bbox (clamped to
-// [-2, d+1] before the conversion, NaN -> -2), points inside land in [0, d-1]
-__device__ __forceinline__ int cell_of(float v, float lo, float inv_s, int d)
-{
-    float u = __fmul_rn(__fsub_rn(v, lo), inv_s);
-    u = fminf(fmaxf(u, -2.0f), (float)d + 1.0f);
-    return (int)floorf(u);
-}
-
-__device__ __forceinline__ int point_slot(float x, float y, float z, int k, const BqGrid &g)
-{
-    const int ix = min(max(cell_of(x, g.minx, g.inv_s, g.dx), 0), g.dx - 1);
-    const int iy = min(max(cell_of(y, g.miny, g.inv_s, g.dy), 0), g.dy - 1);
-    const int iz = min(max(cell_of(z, g.minz, g.inv_s, g.dz), 0), g.dz - 1);
-    return (k >> g.win_shift) * g.ncell + (ix * g.dy + iy) * g.dz + iz;
-}
+using namespace lidar_bq;
 
 // Grid parameters of one frame (thread 0 of bq_bin_kernel).
 //  * bbox over finite coordinates only: a point with an inf/NaN coordinate is never a hit
@@ -290,31 +258,6 @@ __global__ __launch_bounds__(1024) void bq_bin_kernel(const float *__restrict__ 
     }
 }
 
-// index-order scan of points [lo, hi) for one centre (a window with too many candidates)
-__device__ __forceinline__ void scan_range(const float *__restrict__ p, int lo, int hi, float cx, float cy,
-                                           float cz, float r2, int ns, int lane, uint64_t below, int &cnt,
-                                           int &first, int32_t *__restrict__ o)
-{
-    for (int k0 = lo; k0 < hi && cnt < ns; k0 += 64) {
-        const int k = k0 + lane;
-        bool hit = false;
-        if (k < hi) hit = lidar::dist2f(p[3 * k], p[3 * k + 1], p[3 * k + 2], cx, cy, cz) < r2;
-        const uint64_t mk = __ballot(hit);
-        if (mk) {
-            if (first < 0) first = k0 + __ffsll((unsigned long long)mk) - 1;
-            const int rk = cnt + __popcll(mk & below);
-            if (hit && rk < ns) o[rk] = k;
-            cnt += __popcll(mk);
-        }
-    }
-}
-
-__device__ __forceinline__ void lds_wave_sync()
-{
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-}
-
 // one wavefront per centre; blocks are laid out so that the blocks of a contiguous range of
 // frames share an XCD (block b and b + 8 share one): a frame's grid stays in one L2
 __global__ __launch_bounds__(256) void bq_grid_kernel(const float *__restrict__ xyz,
@@ -330,105 +273,9 @@ __global__ __launch_bounds__(256) void bq_grid_kernel(const float *__restrict__ 
     if (w >= total) return;  // wave-uniform
     const int64_t b = w / m;
     const char *fw = grid_ws + b * grid_frame_bytes(n);
-    const BqGrid g = *reinterpret_cast<const BqGrid *>(fw);
-    const int *tab = reinterpret_cast<const int *>(fw + 64);
-    const float4 *sp = reinterpret_cast<const float4 *>(fw + 64 + (kTab + 64) * 4);
     const float *p = xyz + b * (int64_t)n * 3;
     const float cx = centres[3 * w], cy = centres[3 * w + 1], cz = centres[3 * w + 2];
-    int32_t *o = out + w * (int64_t)ns;
-    const uint64_t below = (1ull << lane) - 1;
-    int *hw = hits[wid];
-
-    // candidate cells per axis: a hit has |u_p - u_c| < r inv_s (1 + 2^-23) + the rounding of
-    // the two cell coordinates (< 2^-12 at <= 1026 cells): floor(u_c -+ delta) bound its cell.
-    // At the binned radius that is 3 cells per axis; smaller radii take 1-2.
-    const float delta = __fadd_rn(__fmul_rn(__fmul_rn(r, g.inv_s), 1.0f + 1.0f / 1024.0f), 1.0f / 1024.0f);
-    const float ux = __fmul_rn(__fsub_rn(cx, g.minx), g.inv_s), uy = __fmul_rn(__fsub_rn(cy, g.miny), g.inv_s),
-                uz = __fmul_rn(__fsub_rn(cz, g.minz), g.inv_s);
-    auto lo_of = [](float u, float dl, int d) {
-        return max((int)floorf(fminf(fmaxf(__fsub_rn(u, dl), -2.0f), (float)d + 1.0f)), 0);
-    };
-    auto hi_of = [](float u, float dl, int d) {
-        return min((int)floorf(fminf(fmaxf(__fadd_rn(u, dl), -2.0f), (float)d + 1.0f)), d - 1);
-    };
-    // (NaN centres: fmaxf(NaN, -2) = -2 -> an empty range; they have no hits)
-    const int lox = lo_of(ux, delta, g.dx), hix = hi_of(ux, delta, g.dx);
-    const int loy = lo_of(uy, delta, g.dy), hiy = hi_of(uy, delta, g.dy);
-    const int loz = lo_of(uz, delta, g.dz), hiz = hi_of(uz, delta, g.dz);
-    int cnt = 0, first = -1;
-    // lane j < 9 owns the z-run of column (lox + j / 3, loy + j % 3); a radius above the
-    // binned one can need more columns: such centres walk the windows by index-order scan
-    const bool full = (hix - lox) > 2 || (hiy - loy) > 2;
-    const int jx = lox + lane / 3, jy = loy + lane % 3;
-    const bool col_ok = !full && lane < 9 && jx <= hix && jy <= hiy && loz <= hiz;
-    const int colbase = (jx * g.dy + jy) * g.dz + loz;
-    for (int win = 0; win < g.nwin && cnt < ns; ++win) {
-        const int wlo = win << g.win_shift, whi = min(n, (win + 1) << g.win_shift);
-        int st = 0, len = 0;
-        if (col_ok) {
-            const int s0 = win * g.ncell + colbase;
-            st = tab[s0];
-            len = tab[s0 + (hiz - loz) + 1] - st;
-        }
-        int incl = len;
-#pragma unroll
-        for (int d = 1; d < 16; d <<= 1) {
-            const int v = __shfl_up(incl, d, 64);
-            if (lane >= d) incl += v;
-        }
-        const int tot = full ? kCap + 1 : __builtin_amdgcn_readlane(incl, 8);
-        if (tot == 0) continue;
-        if (tot > kCap) {
-            scan_range(p, wlo, whi, cx, cy, cz, r2, ns, lane, below, cnt, first, o);
-            continue;
-        }
-        const int excl = incl - len;
-        int e[9], s[9];
-#pragma unroll
-        for (int j = 0; j < 9; ++j) {
-            e[j] = __builtin_amdgcn_readlane(excl, j);
-            s[j] = __builtin_amdgcn_readlane(st, j);
-        }
-        int hc = 0;
-        for (int t0 = 0; t0 < tot; t0 += 64) {
-            const int t = t0 + lane;
-            int pos = s[0] + t;
-#pragma unroll
-            for (int j = 1; j < 9; ++j)
-                if (t >= e[j]) pos = s[j] + (t - e[j]);
-            bool hit = false;
-            int idx = 0;
-            if (t < tot) {
-                const float4 q = sp[pos];
-                hit = lidar::dist2f(q.x, q.y, q.z, cx, cy, cz) < r2;
-                idx = __float_as_int(q.w);
-            }
-            const uint64_t mk = __ballot(hit);
-            if (hit) hw[hc + __popcll(mk & below)] = idx;
-            hc += __popcll(mk);
-        }
-        if (hc == 0) continue;
-        if (lane < 4) hw[hc + lane] = 0x7fffffff;
-        lds_wave_sync();
-        // rank every hit by index among the window's hits (indices are distinct)
-        int mnv = 0x7fffffff;
-        for (int e0 = 0; e0 < hc; e0 += 64) {
-            const int ei = e0 + lane;
-            const int v = ei < hc ? hw[ei] : 0x7fffffff;
-            int rank = 0;
-            for (int i = 0; i < hc; i += 4) {
-                const int4 h4 = *reinterpret_cast<const int4 *>(hw + i);
-                rank += (h4.x < v) + (h4.y < v) + (h4.z < v) + (h4.w < v);
-            }
-            if (ei < hc && cnt + rank < ns) o[cnt + rank] = v;
-            mnv = min(mnv, v);
-        }
-        if (first < 0) first = (int)lidar::wave_min_u32_dpp((uint32_t)mnv);
-        cnt += hc;
-        lds_wave_sync();
-    }
-    const int fill = first < 0 ? 0 : first;
-    for (int s2 = min(cnt, ns) + lane; s2 < ns; s2 += 64) o[s2] = fill;
+    grid_query_wave<kCap>(p, fw, n, cx, cy, cz, r, r2, ns, lane, hits[wid], out + w * (int64_t)ns);
 }
 
 }  // namespace

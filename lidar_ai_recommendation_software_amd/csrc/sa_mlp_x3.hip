@@ -20,7 +20,7 @@
 #include <cstring>
 #include <vector>
 
-#include "common.hpp"
+#include "bq_grid.hpp"
 
 namespace {
 
@@ -83,13 +83,22 @@ __device__ __forceinline__ float bf16r(float v) { return (float)(__bf16)v; }
 
 // R = 16-row tiles per wavefront (R grouped-row tiles of the same centre share every weight
 // fragment read from LDS: R = 2 halves the LDS and L2 weight bytes per MFMA)
-template <int C1, int C2, int C3, int NS, int L1, int R, bool X1>
+//
+// BQ (xyz levels): the kernel answers its centres' ball queries itself from the frame's grid
+// (bq_bin_kernel's output, grid_ws): each wave runs lidar_bq::grid_query_wave for its centre
+// into LDS before the MLP, so the (B, M, ns) index tensor never goes through HBM and no separate
+// full-chip query launch competes with the pipeline; out_idx (optional) receives the indices.
+constexpr int kBqCap = 256;  // candidates per window a fused wave ranks in LDS (more: index-order scan)
+template <int C1, int C2, int C3, int NS, int L1, int R, bool X1, bool BQ = false>
 __global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float *__restrict__ P, int64_t stride,
                                                      const float *__restrict__ Q, const int32_t *__restrict__ idx,
                                                      int n, int m, int64_t total, const uint4 *__restrict__ packed,
                                                      float *__restrict__ out, int64_t out_stride, int64_t out_offset,
-                                                     const float *__restrict__ X, const float *__restrict__ Cn)
+                                                     const float *__restrict__ X, const float *__restrict__ Cn,
+                                                     const char *__restrict__ grid_ws, float r, float r2,
+                                                     int32_t *__restrict__ out_idx)
 {
+    static_assert(!BQ || L1 == L1_XYZ, "fused ball query: xyz levels only");
     static_assert(NS % (16 * R) == 0 && C1 % 32 == 0 && C2 % 32 == 0 && C3 % 32 == 0, "tile shapes");
     constexpr bool XYZ = L1 == L1_XYZ, HASW1 = L1 != L1_PRE;
     using K = PackX3<C1, C2, C3, X1>;
@@ -135,7 +144,18 @@ __global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float 
     if constexpr (HASW1)
         for (int i = tid; i < T1 * 64; i += 256) w1_s[i] = reinterpret_cast<const float *>(packed)[i];
     for (int i = lane; i < 4 * C3; i += 64) (&mx_s[wave][0][0])[i] = -INFINITY;
+    __shared__ int qidx[BQ ? 4 : 1][BQ ? NS : 1];             // this wave's ball-query result
+    __shared__ int qhits[BQ ? 4 : 1][BQ ? kBqCap + 4 : 1];    // its per-window hit list
+    if constexpr (BQ) {
+        const float *pf = P + (int64_t)b * n * 3;
+        const char *fw = grid_ws + b * lidar_bq::grid_frame_bytes(n);
+        lidar_bq::grid_query_wave<kBqCap>(pf, fw, n, Q[cc * 3], Q[cc * 3 + 1], Q[cc * 3 + 2], r, r2, NS, lane,
+                                          qhits[wave], &qidx[wave][0]);
+    }
     __syncthreads();
+    if constexpr (BQ)
+        if (live && out_idx != nullptr)
+            for (int i = lane; i < NS; i += 64) out_idx[unit * NS + i] = qidx[wave][i];
     int par = 0;
     // layer 3's max-pool runs on the raw accumulators: x -> relu(x + bias) is monotone in
     // fp32 (round-to-nearest addition never reverses an order), so max_i relu(a_i + b) ==
@@ -148,7 +168,7 @@ __global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float 
         bf16x8 xh[R][KS2], xl[R][KS2];
 #pragma unroll
         for (int rr = 0; rr < R; ++rr) {
-            const int64_t k = idx[cc * NS + (it * R + rr) * 16 + col];
+            const int64_t k = BQ ? qidx[wave][(it * R + rr) * 16 + col] : idx[cc * NS + (it * R + rr) * 16 + col];
             f32x4 y1[T1];
             if constexpr (XYZ) {
                 const float *pr = P + ((int64_t)b * n + k) * 3;
@@ -342,7 +362,7 @@ __global__ __launch_bounds__(256, 4) void sa_x3_lean_kernel(const float *__restr
     constexpr int R = 2;
     static_assert(NS % (16 * R) == 0 && C1 % 32 == 0 && C2 % 32 == 0 && C3 % 64 == 0, "tile shapes");
     using K = PackX3<C1, C2, C3, false>;
-    constexpr int T1 = K::T1, T2 = K::T2, T3 = K::T3, KS2 = K::KS2, KS3 = K::KS3;
+    constexpr int T2 = K::T2, T3 = K::T3, KS2 = K::KS2, KS3 = K::KS3;
     constexpr int CH2 = K::CH2, CH3 = K::CH3, CHMAX = CH2 > CH3 ? CH2 : CH3;
     constexpr int NL2 = T2 / 2, NL3 = T3 / 2, NSEQ = R * NL2 + NL3;  // chunk passes per iteration
     constexpr int ITERS = NS / (16 * R);
@@ -527,7 +547,24 @@ int launch_x3(const float *p, int64_t stride, const float *q, const int32_t *idx
     const int64_t blocks = (total + 3) / 4;
     REQUIRE(blocks <= 0x7fffffff, "sa_group_mlp_x3: too many centres");
     hipLaunchKernelGGL((sa_x3_kernel<C1, C2, C3, NS, L1, R, X1>), dim3((unsigned)blocks), dim3(256), 0, s, p, stride,
-                       q, idx, (int)n, (int)m, total, static_cast<const uint4 *>(packed), out, os, oo, xyz, centres);
+                       q, idx, (int)n, (int)m, total, static_cast<const uint4 *>(packed), out, os, oo, xyz, centres,
+                       nullptr, 0.0f, 0.0f, nullptr);
+    LAUNCH_CHECK();
+    return LIDAR_OK;
+}
+
+template <int C1, int C2, int C3, int NS, bool X1>
+int launch_x3_bq(const float *xyz, const char *grid, const float *centres, int64_t batch, int64_t n, int64_t m,
+                 float radius, const void *packed, float *out, int64_t os, int64_t oo, int32_t *out_idx,
+                 hipStream_t s)
+{
+    constexpr int R = NS >= 16 * LIDAR_X3_ROWS ? LIDAR_X3_ROWS : 1;
+    const int64_t total = batch * m;
+    const int64_t blocks = (total + 3) / 4;
+    REQUIRE(blocks <= 0x7fffffff, "sa_group_mlp_bq: too many centres");
+    hipLaunchKernelGGL((sa_x3_kernel<C1, C2, C3, NS, L1_XYZ, R, X1, true>), dim3((unsigned)blocks), dim3(256), 0, s,
+                       xyz, (int64_t)3, centres, nullptr, (int)n, (int)m, total, static_cast<const uint4 *>(packed),
+                       out, os, oo, nullptr, nullptr, grid, radius, radius * radius, out_idx);
     LAUNCH_CHECK();
     return LIDAR_OK;
 }
@@ -719,4 +756,38 @@ LIDAR_EXPORT int lidar_sa_group_mlp_x1_f32(lidar_handle *h, int32_t layer1_mode,
     LIDAR_SAX1(128, 128, 256, 128, 2)
 #undef LIDAR_SAX1
     return lidar::fail(LIDAR_EINVAL, "lidar_sa_group_mlp_x1_f32: unsupported (widths, nsample) combination");
+}
+
+// SA branch of an xyz level with its ball queries answered inside the kernel (sa_x3_kernel with
+// BQ) from grid = lidar_ball_query_bin_f32(xyz, radius, nsample)'s output for these frames:
+// the same result as lidar_ball_query_binned_f32 followed by lidar_sa_group_mlp_x3_f32 (x1 = 0)
+// or lidar_sa_group_mlp_x1_f32 mode 0 (x1 = 1), bit for bit.  out_idx (batch, m, nsample) int32,
+// optional, receives the ball-query indices.  packed: the x3 / x1 image of the branch.
+LIDAR_EXPORT int lidar_sa_group_mlp_bq_f32(lidar_handle *h, int32_t x1, const float *xyz, const void *grid,
+                                           const float *centres, int64_t batch, int64_t n, int64_t m, float radius,
+                                           int32_t nsample, int32_t c1, int32_t c2, int32_t c3, const void *packed,
+                                           float *out, int64_t out_stride, int64_t out_offset, int32_t *out_idx,
+                                           void *stream)
+{
+    REQUIRE(h && xyz && grid && centres && packed && out, "lidar_sa_group_mlp_bq_f32: null pointer");
+    REQUIRE(batch >= 0 && n >= 1 && n < 0x3fffffff && m >= 1 && m < 0x7fffffff,
+            "lidar_sa_group_mlp_bq_f32: bad sizes");
+    REQUIRE(radius >= 0.0f, "lidar_sa_group_mlp_bq_f32: negative radius");
+    REQUIRE(out_offset >= 0 && out_offset + c3 <= out_stride,
+            "lidar_sa_group_mlp_bq_f32: output columns exceed out_stride");
+    if (batch == 0) return LIDAR_OK;
+    ON_DEVICE(h->device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const char *g = static_cast<const char *>(grid);
+#define LIDAR_SABQ(C1_, C2_, C3_, NS_)                                                                          \
+    if (c1 == C1_ && c2 == C2_ && c3 == C3_ && nsample == NS_)                                                  \
+        return x1 ? launch_x3_bq<C1_, C2_, C3_, NS_, true>(xyz, g, centres, batch, n, m, radius, packed, out,    \
+                                                           out_stride, out_offset, out_idx, s)                   \
+                  : launch_x3_bq<C1_, C2_, C3_, NS_, false>(xyz, g, centres, batch, n, m, radius, packed, out,   \
+                                                            out_stride, out_offset, out_idx, s);
+    LIDAR_SABQ(64, 64, 128, 32)
+    LIDAR_SABQ(32, 32, 64, 16)
+    LIDAR_SABQ(64, 96, 128, 128)
+#undef LIDAR_SABQ
+    return lidar::fail(LIDAR_EINVAL, "lidar_sa_group_mlp_bq_f32: unsupported (widths, nsample) combination");
 }

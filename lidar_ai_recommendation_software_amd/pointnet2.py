@@ -172,6 +172,8 @@ def ball_query_bin(radius, nsample, xyz, grid, slot=0):
     return grid
 
 
+BQ_GRID_MIN_N = 1024  # csrc/bq_grid.hpp kGridMinN: frames this large take the grid ball query
+
 # (xyz_level, c1, c2, c3, nsample) combinations lidar_sa_group_mlp16_f32 instantiates
 MLP16_SHAPES = {(True, 64, 64, 128, 32), (True, 32, 32, 64, 16), (True, 64, 96, 128, 128), (False, 128, 128, 256, 64),
                 (False, 128, 128, 256, 128), (False, 64, 64, 128, 32)}
@@ -279,6 +281,26 @@ def group_mlp_x3(p, q, idx, n, packed, widths, out, out_offset=0, xyz_level=Fals
     nat.call("lidar_sa_group_mlp_x3_f32", nat.handle(p.device.index), int(xyz_level), nat.ptr(p), stride,
              nat.ptr(q), nat.ptr(idx), B, n, M, ns, c1, c2, c3, nat.ptr(packed), nat.ptr(out), out.shape[-1],
              out_offset, nat.stream_ptr())
+    return out
+
+
+def group_mlp_bq(xyz, centres, grid, radius, nsample, packed, widths, out, out_offset=0, x1=False, out_idx=None):
+    """One xyz-level SA branch with its ball queries answered inside the MLP kernel
+    (lidar_sa_group_mlp_bq_f32): grid = ball_query_bin(radius, nsample, xyz, ...) of these
+    frames; packed = the branch's x3 image (x1=False) or bf16-spec image (x1=True).  Equal bit
+    for bit to ball_query(..., grid=grid) then group_mlp_x3 / group_mlp_x1; out_idx (B, M, ns)
+    int32, optional, receives the ball-query indices."""
+    B, n, _ = xyz.shape
+    M = centres.shape[1]
+    c1, c2, c3 = widths
+    if not (xyz.is_contiguous() and centres.is_contiguous()):
+        raise ValueError("group_mlp_bq: xyz / centres must be contiguous")
+    if out_idx is not None and (tuple(out_idx.shape) != (B, M, nsample) or out_idx.dtype != torch.int32):
+        raise ValueError("group_mlp_bq: out_idx must be (B, M, nsample) int32")
+    _dev_check(xyz, centres, grid, packed, out, *([out_idx] if out_idx is not None else []))
+    nat.call("lidar_sa_group_mlp_bq_f32", nat.handle(xyz.device.index), int(bool(x1)), nat.ptr(xyz), nat.ptr(grid),
+             nat.ptr(centres), B, n, M, float(radius), int(nsample), c1, c2, c3, nat.ptr(packed), nat.ptr(out),
+             out.shape[-1], out_offset, nat.ptr(out_idx) if out_idx is not None else None, nat.stream_ptr())
     return out
 
 
@@ -525,6 +547,14 @@ class PointNet2Backbone:
         self.out_channels = cfeat
         self.timers = None  # set to a _Timers() to time every launch
 
+    def _grid_buffer(self, B, N, device):
+        """The ball-query grid buffer forward() bins xyz levels into (grown on demand, reused by
+        every branch and call on this backbone's stream)."""
+        need = nat.load_library().lidar_ball_query_grid_bytes(B, N)
+        if getattr(self, "_grid", None) is None or self._grid.numel() < need:
+            self._grid = torch.empty((max(1, need),), dtype=torch.uint8, device=device)
+        return self._grid
+
     def forward_from_sa1_fps(self, xyz, idx1, new_xyz1, fz1, gidx1=None, keep_levels=False, grids1=None):
         """forward() with level 0's FPS (and its ball queries: gidx1, or their binning: grids1)
         already computed (StreamingSSG)."""
@@ -574,6 +604,23 @@ class PointNet2Backbone:
             gidxs = []
             for bi_, br in enumerate(lvl["branches"]):
                 tag = f"sa{li + 1}" + (f"_b{bi_}" if len(lvl["branches"]) > 1 else "")
+                fused = pq is None and pl.get("bq") is None and (self.bf16 or "packed_x3" in br) and (
+                    pl.get("grid") is not None or N >= BQ_GRID_MIN_N)
+                if fused:
+                    # xyz level: the MLP kernel answers the ball queries from the frame's grid
+                    if pl.get("grid") is not None:
+                        grid = pl["grid"][bi_]
+                    else:
+                        grid = _call(t, f"{tag}_bq_bin", B, ball_query_bin, br["r"], br["ns"], xyz,
+                                     self._grid_buffer(B, N, xyz.device))
+                    gidx = (torch.empty((B, M, br["ns"]), dtype=torch.int32, device=xyz.device)
+                            if keep_levels else None)
+                    _call(t, f"{tag}_group_mlp", B, group_mlp_bq, xyz, new_xyz, grid, br["r"], br["ns"],
+                          br["packed_x1"] if self.bf16 else br["packed_x3"], br["widths"], out=out, out_offset=off,
+                          x1=self.bf16, out_idx=gidx)
+                    gidxs.append(gidx)
+                    off += br["widths"][-1]
+                    continue
                 if pl.get("bq") is not None:
                     gidx = pl["bq"][bi_]
                 else:
@@ -659,7 +706,7 @@ class StreamingSSG:
     """
 
     def __init__(self, backbone, batch, n, depth=1, fps_group=1, fps_threads=0, side_priority=0, ramp=True,
-                 reserve=True, keep_levels=False, slots=None, bq="side"):
+                 reserve=True, keep_levels=False, slots=None, bq="bin"):
         """fps_threads: SA1 FPS workgroup size (0 = 1024; 512: half the CU footprint beside the
         MLPs).  ramp: in run(), the first groups hold 1, 2, ... batches (a shorter pipeline fill).
         slots: staging slots (>= depth + 1; default depth + 3).  Group k's FPS reuses the slot of

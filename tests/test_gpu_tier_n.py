@@ -225,6 +225,44 @@ def test_sa_kernel_variants_bit_identical(cuda, tmp_path):
     assert got.size == want.size and np.array_equal(got.view(np.uint32), want.view(np.uint32))
 
 
+@pytest.mark.parametrize("frame", ["uniform", "clump", "line", "all_equal", "lattice_ties"])
+@pytest.mark.parametrize("widths,r,ns", [([64, 64, 128], 0.2, 32), ([32, 32, 64], 0.1, 16), ([64, 96, 128], 0.4, 128)])
+@pytest.mark.parametrize("x1", [False, True])
+def test_group_mlp_bq_matches_unfused(cuda, frame, widths, r, ns, x1):
+    """lidar_sa_group_mlp_bq_f32 (each wave answers its centre's ball query from the grid inside
+    the MLP kernel) == grid ball query + the separate MLP launch, bit for bit, features and the
+    out_idx indices (which also equal the oracle's); x3 and bf16 (X1) images; degenerate frames
+    (a dense clump overflowing the per-window candidate list, a line, one repeated point, lattice
+    ties at exactly r)."""
+    B, N, M = 2, 6000, 301
+    x = unit_frames(B, N, 41) if frame == "uniform" else np.stack([_bq_edge_frames()[frame]] * B)
+    x = np.ascontiguousarray(x)
+    N = x.shape[1]  # the lattice frame has 18^3 points
+    c = np.ascontiguousarray(x[:, ::17][:, :M])
+    rng = np.random.default_rng(3)
+    layers, k = [], 3
+    for w in widths:
+        layers.append(((rng.standard_normal((k, w)) * (1.5 / np.sqrt(k))).astype(np.float32),
+                       (rng.standard_normal(w) * 0.1).astype(np.float32)))
+        k = w
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(cuda)
+    xt, ct = T(x), T(c)
+    packed = T(pn.pack_branch_x1(layers) if x1 else pn.pack_branch_x3(layers, True))
+    grid = pn.ball_query_bin(r, ns, xt, pn.ball_query_grid_buffer(B, N, cuda))
+    gi = pn.ball_query(r, ns, xt, ct, grid=grid)
+    want = torch.full((B, M, widths[-1] + 4), -7.0, dtype=torch.float32, device=cuda)
+    if x1:
+        pn.group_mlp_x1(xt, gi, N, packed, widths, want, 2, centres=ct)
+    else:
+        pn.group_mlp_x3(xt, ct, gi, N, packed, widths, want, 2, xyz_level=True)
+    got = torch.full_like(want, -7.0)
+    oi = torch.full((B, M, ns), -5, dtype=torch.int32, device=cuda)
+    pn.group_mlp_bq(xt, ct, grid, r, ns, packed, widths, got, 2, x1=x1, out_idx=oi)
+    assert torch.equal(oi, gi)
+    assert np.array_equal(oi.cpu().numpy(), tier_n.ball_query(x, c, r, ns))
+    assert np.array_equal(got.cpu().numpy().view(np.uint32), want.cpu().numpy().view(np.uint32))
+
+
 def test_dense_no_relu(cuda):
     rng = np.random.default_rng(2)
     x = rng.standard_normal((256, 144)).astype(np.float32)

@@ -195,11 +195,12 @@ def eps_pairs(x):
     return (int(cnt.sum()) - len(sc)) // 2
 
 
-def tier_r_leg(dev, rank, world, frames=32, n=65536, steps=3, cpu=True, cpu_budget=12.0):
+def tier_r_leg(dev, rank, world, frames=32, n=65536, steps=3, cpu=True, cpu_budget=12.0, wide=256):
     """The reference's own path (Tier R: preprocess -> DBSCAN -> people -> density grid) on
     device-resident uniform +-15 m frames: batches of `frames` frames through
     density_stream.DensityStream.run_batch (one launch per phase over the CSR batch), with
-    per-phase HIP-event durations from the library (lidar_profile) in a second window."""
+    per-phase HIP-event durations from the library (lidar_profile) in a second window; then
+    the same with `wide` frames per launch (wide_batch)."""
     import torch
     from lidar_ai_recommendation_software_amd import sharding
     from lidar_ai_recommendation_software_amd.density_stream import DensityStream
@@ -252,6 +253,17 @@ def tier_r_leg(dev, rank, world, frames=32, n=65536, steps=3, cpu=True, cpu_budg
     if "preprocess" in per_launch_ms:
         # the sequential chains: ~6 passes of n dependent fp64 adds per frame, frames in parallel
         rec["preprocess_chain_ns_per_row"] = per_launch_ms["preprocess"] * 1e6 / (6 * n)
+    if wide and wide > frames:
+        # the same path with `wide` frames per launch: preprocess and people run one workgroup
+        # per frame (sequential chains), so 32 frames leave most CUs idle in those phases
+        xw = xs + [torch.from_numpy(uniform_frame(n, sharding.frame_seed(rank, base=1000 + i))).to(dev)
+                   for i in range(frames, wide)]
+        ds.run_batch(xw)
+        elw = sharding.timed(lambda: [ds.run_batch(xw) for _ in range(steps)], dev, world)
+        rec["wide_batch"] = {"frames_per_launch": wide,
+                             "value": sharding.aggregate_rate(wide * n * steps, world, elw) / 1e6,
+                             "unit": "M points/s", "ms_per_launch": elw / steps * 1e3}
+        del xw
     if cpu and rank == 0 and world == 1:
         rec["cpu_baseline"] = tier_r_cpu_baseline(n, cpu_budget)
         rec["speedup_vs_cpu"] = rec["value"] / rec["cpu_baseline"]["value"]

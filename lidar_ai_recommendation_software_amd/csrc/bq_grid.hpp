@@ -103,15 +103,23 @@ __device__ __forceinline__ void grid_query_wave(const float *__restrict__ p, con
     const int jx = lox + lane / 3, jy = loy + lane % 3;
     const bool col_ok = !full && lane < 9 && jx <= hix && jy <= hiy && loz <= hiz;
     const int colbase = (jx * g.dy + jy) * g.dz + loz;
+    // the next window's slot-table entries are loaded while the current window is processed,
+    // and up to 4 chunks of 64 candidates are loaded before any is tested: about one memory
+    // round trip per window instead of one per table read and per candidate chunk
+    int st = 0, len = 0;
+    if (col_ok && g.nwin > 0) {
+        st = tab[colbase];
+        len = tab[colbase + (hiz - loz) + 1] - st;
+    }
     for (int win = 0; win < g.nwin && cnt < ns; ++win) {
         const int wlo = win << g.win_shift, whi = min(n, (win + 1) << g.win_shift);
-        int st = 0, len = 0;
-        if (col_ok) {
-            const int s0 = win * g.ncell + colbase;
-            st = tab[s0];
-            len = tab[s0 + (hiz - loz) + 1] - st;
+        const int cst = st, clen = len;
+        if (col_ok && win + 1 < g.nwin) {
+            const int s1 = (win + 1) * g.ncell + colbase;
+            st = tab[s1];
+            len = tab[s1 + (hiz - loz) + 1] - st;
         }
-        int incl = len;
+        int incl = clen;
 #pragma unroll
         for (int d = 1; d < 16; d <<= 1) {
             const int v = __shfl_up(incl, d, 64);
@@ -123,30 +131,33 @@ __device__ __forceinline__ void grid_query_wave(const float *__restrict__ p, con
             scan_range(p, wlo, whi, cx, cy, cz, r2, ns, lane, below, cnt, first, o);
             continue;
         }
-        const int excl = incl - len;
+        const int excl = incl - clen;
         int e[9], s[9];
 #pragma unroll
         for (int j = 0; j < 9; ++j) {
             e[j] = __builtin_amdgcn_readlane(excl, j);
-            s[j] = __builtin_amdgcn_readlane(st, j);
+            s[j] = __builtin_amdgcn_readlane(cst, j);
         }
         int hc = 0;
-        for (int t0 = 0; t0 < tot; t0 += 64) {
-            const int t = t0 + lane;
-            int pos = s[0] + t;
+        for (int t0 = 0; t0 < tot; t0 += 256) {
+            float4 qv[4];
 #pragma unroll
-            for (int j = 1; j < 9; ++j)
-                if (t >= e[j]) pos = s[j] + (t - e[j]);
-            bool hit = false;
-            int idx = 0;
-            if (t < tot) {
-                const float4 q = sp[pos];
-                hit = lidar::dist2f(q.x, q.y, q.z, cx, cy, cz) < r2;
-                idx = __float_as_int(q.w);
+            for (int u = 0; u < 4; ++u) {
+                const int t = t0 + 64 * u + lane;
+                int pos = s[0] + t;
+#pragma unroll
+                for (int j = 1; j < 9; ++j)
+                    if (t >= e[j]) pos = s[j] + (t - e[j]);
+                qv[u] = t < tot ? sp[pos] : make_float4(0.f, 0.f, 0.f, 0.f);
             }
-            const uint64_t mk = __ballot(hit);
-            if (hit) hw[hc + __popcll(mk & below)] = idx;
-            hc += __popcll(mk);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int t = t0 + 64 * u + lane;
+                const bool hit = t < tot && lidar::dist2f(qv[u].x, qv[u].y, qv[u].z, cx, cy, cz) < r2;
+                const uint64_t mk = __ballot(hit);
+                if (hit) hw[hc + __popcll(mk & below)] = __float_as_int(qv[u].w);
+                hc += __popcll(mk);
+            }
         }
         if (hc == 0) continue;
         if (lane < 4) hw[hc + lane] = 0x7fffffff;

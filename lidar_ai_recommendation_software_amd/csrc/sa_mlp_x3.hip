@@ -81,6 +81,16 @@ struct PackX3 {
 enum { L1_XYZ = 0, L1_PRE = 1, L1_PX = 2 };
 __device__ __forceinline__ float bf16r(float v) { return (float)(__bf16)v; }
 
+// max over the four row groups (lanes col, col+16, col+32, col+48) of every column, in all
+// four: v_permlane32_swap / v_permlane16_swap hand each lane its xor-32 / xor-16 partner
+__device__ __forceinline__ float max_row_groups(float v)
+{
+    const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = maxn(v, __uint_as_float(a[0]), __uint_as_float(a[1]));
+    const auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return maxn(v, __uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+
 // R = 16-row tiles per wavefront (R grouped-row tiles of the same centre share every weight
 // fragment read from LDS: R = 2 halves the LDS and L2 weight bytes per MFMA)
 //
@@ -99,7 +109,7 @@ __global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float 
                                                      int32_t *__restrict__ out_idx)
 {
     static_assert(!BQ || L1 == L1_XYZ, "fused ball query: xyz levels only");
-    static_assert(NS % (16 * R) == 0 && C1 % 32 == 0 && C2 % 32 == 0 && C3 % 32 == 0, "tile shapes");
+    static_assert(NS % (16 * R) == 0 && C1 % 32 == 0 && C2 % 32 == 0 && C3 % 64 == 0, "tile shapes");
     constexpr bool XYZ = L1 == L1_XYZ, HASW1 = L1 != L1_PRE;
     using K = PackX3<C1, C2, C3, X1>;
     constexpr int HV = K::HALVES;
@@ -112,7 +122,6 @@ __global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float 
     __shared__ uint4 buf[2][CHMAX];
     __shared__ float bias_s[C1 + C2 + C3];
     __shared__ float w1_s[HASW1 ? T1 * 64 : 1];
-    __shared__ float mx_s[4][4][C3];  // layer 3's running max-pool of the raw accumulators, per (wave, row group)
 
     // wave index in an SGPR: the LDS-DMA destinations (M0) and the unit below are wave-uniform
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -143,7 +152,12 @@ __global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float 
     for (int i = tid; i < C1 + C2 + C3; i += 256) bias_s[i] = Bias[i];
     if constexpr (HASW1)
         for (int i = tid; i < T1 * 64; i += 256) w1_s[i] = reinterpret_cast<const float *>(packed)[i];
-    for (int i = lane; i < 4 * C3; i += 64) (&mx_s[wave][0][0])[i] = -INFINITY;
+    // layer 3's running max-pool of the raw accumulators in registers: mx[j] of row group q
+    // holds channel 16 (4j + q) + col (register max, no LDS table: an LDS store here would make
+    // the compiler wait for the weight prefetches in flight)
+    float mx[T3 / 4];
+#pragma unroll
+    for (int j = 0; j < T3 / 4; ++j) mx[j] = -INFINITY;
     __shared__ int qidx[BQ ? 4 : 1][BQ ? NS : 1];             // this wave's ball-query result
     __shared__ int qhits[BQ ? 4 : 1][BQ ? kBqCap + 4 : 1];    // its per-window hit list
     if constexpr (BQ) {
@@ -313,34 +327,22 @@ __global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float 
                         const f32x4 &acc = hh ? a1[rr] : a0[rr];
                         v = maxn(maxn(v, acc[0], acc[1]), acc[2], acc[3]);
                     }
-                    // each row group q keeps its own slot: one LDS atomic max, no lane swaps
-                    __builtin_amdgcn_ds_fmaxf((__attribute__((address_space(3))) float *)&mx_s[wave][q][16 * t + col], v, 0,
-                                              0, false);
+                    v = max_row_groups(v);
+                    if (q == (t & 3)) mx[t >> 2] = __builtin_elementwise_maximum(mx[t >> 2], v);
                 }
             }
             __syncthreads();  // (vmcnt(0)) chunk c+1 landed for everyone; buf[par] free for c+2
             par ^= 1;
         }
     }
-    if (live && q == 0) {
+    if (live) {
         float *o = out + unit * out_stride + out_offset;
 #pragma unroll
-        for (int t = 0; t < T3; ++t) {
-            const int c3 = 16 * t + col;
-            const float v = maxn(maxn(mx_s[wave][0][c3], mx_s[wave][1][c3], mx_s[wave][2][c3]), mx_s[wave][3][c3], -INFINITY);
-            o[c3] = relu(v + bias_s[C1 + C2 + c3]);
+        for (int j = 0; j < T3 / 4; ++j) {
+            const int c3 = 16 * (4 * j + q) + col;
+            o[c3] = relu(mx[j] + bias_s[C1 + C2 + c3]);
         }
     }
-}
-
-// max over the four row groups (lanes col, col+16, col+32, col+48) of every column, in all
-// four: v_permlane32_swap / v_permlane16_swap hand each lane its xor-32 / xor-16 partner
-__device__ __forceinline__ float max_row_groups(float v)
-{
-    const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-    v = maxn(v, __uint_as_float(a[0]), __uint_as_float(a[1]));
-    const auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-    return maxn(v, __uint_as_float(b[0]), __uint_as_float(b[1]));
 }
 
 // Lean form of sa_x3_kernel<.., L1_PRE, R = 2, false> for the wide feature levels (SA2): the same

@@ -66,6 +66,9 @@ def ssg_kernel_work(n):
         "sa2_fps": ("hbm", 12 * m1 + 16 * m2),
         # read points + centres, write idx (the binning inside the call reads the points once more)
         "sa1_ball_query": ("hbm", 12 * (n + m1) + 4 * m1 * 32),
+        # SA1's binning (side stream; the queries run inside sa1_group_mlp): read the points,
+        # write the (x, y, z, index) copy and the 16 K-slot table
+        "sa1_bq_bin": ("hbm", 12 * n + 16 * n + 4 * 16448),
         "sa2_ball_query": ("hbm", 12 * (m1 + m2) + 4 * m2 * 64),
     }
 
@@ -559,6 +562,9 @@ def main():
         else:
             a, p, u = w_total / s / 1e9, HBM_PEAK_GBS, "GB/s"
             basis = "HBM peak over compulsory bytes"
+        if name == "sa1_group_mlp" and args.bq in ("bin", "main"):
+            basis += "; the kernel also answers SA1's ball queries (lidar_sa_group_mlp_bq_f32), whose time is " \
+                     "included and whose work is not priced"
         r = {"kernel": name, "bound": bound, "achieved": a, "peak": p, "unit": u, "frac": a / p,
              "traffic": None, "work_per_launch": w_total / launches, "avg_launch_ms": ms / launches,
              "launches": launches, "frames": frames, "total_ms": ms, "peak_basis": basis}

@@ -48,10 +48,13 @@ def label(name, grid, F=FRAMES_PER_LAUNCH):
         return {F * 4096 * 64: "sa1_ball_query", F * 1024 * 64: "sa2_ball_query"}.get(grid)
     if "bq_bin_kernel" in name:
         return "bq_bin"  # one 1024-thread workgroup per frame: SA1 (65536 pts) vs SA2 (4096) by duration
-    # sa_x3_kernel<C1, C2, C3, NS, layer-1 mode (0 xyz, 1 pre, 2 px), R, X1>; sa16_kernel<C1, C2, C3, NS, XYZ>
-    if "sa_x3_kernel<64, 64, 128, 32, 0, 2, false>" in name or "sa16_kernel<64, 64, 128, 32, true" in name:
+    # sa_x3_kernel<C1, C2, C3, NS, layer-1 mode (0 xyz, 1 pre, 2 px), R, X1, BQ> (BQ: the SA1 kernel
+    # that answers its own ball queries); sa_x3_lean_kernel<C1, C2, C3, NS> (SA2);
+    # sa16_kernel<C1, C2, C3, NS, XYZ> (the native fp32-MFMA leg)
+    if "sa_x3_kernel<64, 64, 128, 32, 0, 2, false" in name or "sa16_kernel<64, 64, 128, 32, true" in name:
         return "sa1_group_mlp"
-    if "sa_x3_kernel<128, 128, 256, 64, 1, 2, false>" in name or "sa16_kernel<128, 128, 256, 64, false" in name:
+    if ("sa_x3_lean_kernel<128, 128, 256, 64>" in name or "sa_x3_kernel<128, 128, 256, 64, 1, 2, false" in name
+            or "sa16_kernel<128, 128, 256, 64, false" in name):
         return "sa2_group_mlp"
     if "dense_x3s_kernel<" in name:  # split-plane GEMM: <mode, fp32-input, x1>
         for key, lab in (("<0, true, false>", "sa2_layer1_points"), ("<1, true, false>", "sa3_dense1"),

@@ -1,7 +1,8 @@
 #!/bin/bash
 # One GPU-box call that refreshes a round's evidence, every GPU step under its own time limit and
 # the steps chained so that the first failure ends the call:
-#   1 the GPU tests               2 the default bench line (bench.json)
+#   1 the GPU tests               2 the bench line at the driver's settings (bench.json, --steps 20
+#     --warmup 5) and a 240-step SSG-only line (bench240.json)
 #   3 rocprofv3 --kernel-trace --stats of the SSG bench (kernel durations to compare with the
 #     in-bench HIP-event means)
 #   4 PMC: a 1 GiB copy calibrating FETCH_SIZE / WRITE_SIZE, then one pass per counter group over
@@ -17,10 +18,11 @@ SHORT="--no-extras --no-cpu-baseline --no-density --no-fp32-mfma-leg --no-standa
 if [ "${2:-tests}" = "tests" ]; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || exit 11
 fi
-timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err || exit 12
+timeout -k 10 600 python bench.py --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err || exit 12
+timeout -k 10 600 python bench.py --steps 240 --warmup 3 --no-extras --no-density --no-fp32-mfma-leg > $O/bench240.json 2> $O/bench240.err || exit 19
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o prof -- \
-    python3 $R/bench.py --no-extras --no-cpu-baseline --no-density --no-fp32-mfma-leg > $O/prof_bench.json 2> $O/prof.err || exit 13
+    python3 $R/bench.py --steps 20 --warmup 5 --no-extras --no-cpu-baseline --no-density --no-fp32-mfma-leg > $O/prof_bench.json 2> $O/prof.err || exit 13
 timeout -s KILL 120 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $O/pmc_calib_f -o c -- \
     python3 $R/tools/pmc_calib.py > $O/pmc_calib.log 2>&1 || exit 14
 timeout -s KILL 120 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $O/pmc_calib_w -o c -- \

@@ -107,8 +107,8 @@ def pmc_per_frame(N):
     if got and got[0].get("config", {}).get("points_per_frame") == N:
         d, src = got
         for k, v in d.get("kernels", {}).items():
-            out.setdefault(k, {}).update({"valu_busy": v.get("valu_busy"), "valu_insts_per_frame": v.get("valu_insts_per_frame"),
-                                          "valu_source": src})
+            out.setdefault(k, {}).update({"valu_issue_frac": v.get("valu_issue_frac"),
+                                          "valu_insts_per_frame": v.get("valu_insts_per_frame"), "valu_source": src})
     return out
 
 
@@ -573,8 +573,10 @@ def main():
             r["traffic"] = pm["traffic_per_frame"] * frames / launches
             r["traffic_unit"] = "bytes per launch (PMC FETCH_SIZE*2 + WRITE_SIZE, " + pm["traffic_source"] + ")"
             r["measured_gbs"] = r["traffic"] / (ms / launches / 1e3) / 1e9
-        if pm.get("valu_busy") is not None:
-            r["valu_busy"] = pm["valu_busy"]
+        if pm.get("valu_issue_frac") is not None:
+            # VALU-throughput roofline: 2 SIMD cycles per wave64 VALU instruction over all SIMD-cycles
+            # of the dispatch alone (PMC pass, tools/pmc_valu.py)
+            r["valu_issue_frac"] = pm["valu_issue_frac"]
             r["valu_source"] = pm["valu_source"]
         return r
 

@@ -22,7 +22,7 @@ timeout -k 10 600 python bench.py --steps 20 --warmup 5 > $O/bench.json 2> $O/be
 timeout -k 10 600 python bench.py --steps 240 --warmup 3 --no-extras --no-density --no-fp32-mfma-leg > $O/bench240.json 2> $O/bench240.err || exit 19
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o prof -- \
-    python3 $R/bench.py --steps 20 --warmup 5 --no-extras --no-cpu-baseline --no-density --no-fp32-mfma-leg > $O/prof_bench.json 2> $O/prof.err || exit 13
+    python3 $R/bench.py --steps 20 --warmup 5 --no-extras --no-cpu-baseline --no-density --no-fp32-mfma-leg --no-standalone > $O/prof_bench.json 2> $O/prof.err || exit 13
 timeout -s KILL 120 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $O/pmc_calib_f -o c -- \
     python3 $R/tools/pmc_calib.py > $O/pmc_calib.log 2>&1 || exit 14
 timeout -s KILL 120 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $O/pmc_calib_w -o c -- \

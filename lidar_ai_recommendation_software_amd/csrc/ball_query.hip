@@ -27,6 +27,12 @@
 
 #include "bq_grid.hpp"
 
+// windows per frame ~ LIDAR_BQ_WIN x (expected hits per centre) / nsample: ~nsample expected hits per
+// window (1.0, measured: 1 234-1 254 vs 1 222-1 228 M pts/s for nsample / 2, 1 194-1 225 for 2 nsample)
+#ifndef LIDAR_BQ_WIN
+#define LIDAR_BQ_WIN 1.0
+#endif
+
 namespace {
 
 constexpr int kC = 8;  // centres per wavefront: every loaded 64-point chunk is tested against all
@@ -115,7 +121,7 @@ using namespace lidar_bq;
 //  * s >= r (1 + 2^-8): a hit has |p - c| < r (1 + 2^-23) per axis (d < r2 in rounded
 //    arithmetic), so |u_p - u_c| < (1 - 2^-8) + the rounding of u = (v - lo) * inv_s,
 //    <= 3 * 2^-24 * 1024 (at most 1024 cells per axis): the cells differ by at most 1.
-//  * windows: about ns / 2 expected hits per window for a uniform frame, <= 64 windows.
+//  * windows: about ns expected hits per window for a uniform frame (LIDAR_BQ_WIN), <= 64 windows.
 __device__ BqGrid bin_params(const float mn[3], const float mx[3], int n, float r, int ns)
 {
     BqGrid g;
@@ -133,7 +139,7 @@ __device__ BqGrid bin_params(const float mn[3], const float mx[3], int n, float 
     double vol = 1.0;
     for (int a = 0; a < 3; ++a) vol *= fmax((double)ext[a], 2.0 * rr);
     const double hits = vol > 0.0 ? n * (4.18879020478639 * rr * rr * rr) / vol : (double)n;
-    const double want = fmin(64.0, fmax(1.0, 2.0 * hits / (double)max(ns, 1)));
+    const double want = fmin(64.0, fmax(1.0, LIDAR_BQ_WIN * hits / (double)max(ns, 1)));
     int shift = 6;
     while (shift < 30 && ((int64_t)n >> shift) > 64) ++shift;                      // <= 64 windows
     while (shift < 30 && (double)(1ll << shift) * want < (double)n) ++shift;       // ~want windows

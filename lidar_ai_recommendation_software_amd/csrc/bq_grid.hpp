@@ -7,7 +7,10 @@
 namespace lidar_bq {
 
 constexpr int kTab = 16384;     // (window, cell) slots per frame: one int each in LDS (64 KiB)
-constexpr int kCap = 512;       // candidates per window a wavefront ranks in LDS
+#ifndef LIDAR_BQ_KCAP
+#define LIDAR_BQ_KCAP 512
+#endif
+constexpr int kCap = LIDAR_BQ_KCAP;  // candidates per window a wavefront ranks in LDS
 constexpr int kGridMinN = 1024;  // below this the index-order scan is as cheap
 
 struct BqGrid {  // per frame, written by bq_bin_kernel

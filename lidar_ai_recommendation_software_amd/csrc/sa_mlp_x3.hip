@@ -98,7 +98,10 @@ __device__ __forceinline__ float max_row_groups(float v)
 // (bq_bin_kernel's output, grid_ws): each wave runs lidar_bq::grid_query_wave for its centre
 // into LDS before the MLP, so the (B, M, ns) index tensor never goes through HBM and no separate
 // full-chip query launch competes with the pipeline; out_idx (optional) receives the indices.
-constexpr int kBqCap = 256;  // candidates per window a fused wave ranks in LDS (more: index-order scan)
+#ifndef LIDAR_BQ_CAP
+#define LIDAR_BQ_CAP 512
+#endif
+constexpr int kBqCap = LIDAR_BQ_CAP;  // candidates per window a fused wave ranks in LDS (more: index-order scan)
 template <int C1, int C2, int C3, int NS, int L1, int R, bool X1, bool BQ = false>
 __global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float *__restrict__ P, int64_t stride,
                                                      const float *__restrict__ Q, const int32_t *__restrict__ idx,

@@ -420,6 +420,9 @@ def main():
                     help="SA1 ball queries (StreamingSSG bq): binning on the FPS side streams and the queries "
                          "inside the SA1 MLP kernel (bin), both on the main stream (main), or binning + a "
                          "query launch on the side streams (side)")
+    ap.add_argument("--l2-side", type=int, default=1,
+                    help="1: SA2's nested FPS and ball queries on the side streams as well (StreamingSSG l2_side; "
+                         "1 213-1 227 vs 1 195-1 207 M pts/s in one A/B); 0: on the main stream")
     ap.add_argument("--rotate", type=int, default=8, help="distinct device-resident input batches the feed cycles over")
     ap.add_argument("--no-fp32-mfma-leg", action="store_true",
                     help="skip the extra measurement of the native fp32-MFMA kernels (when --x3 is on)")
@@ -463,7 +466,8 @@ def main():
         ready = torch.cuda.Event()  # the inputs exist: the feed's FPS launches wait only for their slots
         ready.record()
         pipe = pn.StreamingSSG(bb, B, N, depth=depth, fps_group=G, fps_threads=args.fps_threads, ramp=False,
-                               slots=args.slots or None, bq=args.bq)
+                               slots=args.slots or None, bq=args.bq,
+                               l2_side=bool(args.l2_side))
         feed = pipe.feed()
         nwarm = (depth + max(1, warmup)) * G  # whole groups; `depth` groups in flight when the window opens
         outs = []
@@ -585,6 +589,8 @@ def main():
     # stream's full-chip kernels.  The roofline is reported for the kernel that dominates the
     # main chain's device time; the chain lengths say which chain bounds a step.
     side = ("sa1_fps", "sa1_ball_query", "sa1_bq_bin") if args.bq == "side" else ("sa1_fps", "sa1_bq_bin")
+    if args.l2_side:
+        side = side + ("sa2_fps", "sa2_ball_query")
     per_launch = {k: t / c for k, (c, f, t) in tot.items()}
     main_k = {k: v for k, v in per_launch.items() if k not in side}
     side_ms = sum(per_launch.get(k, 0) for k in side) / args.depth

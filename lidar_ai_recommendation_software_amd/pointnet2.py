@@ -555,10 +555,13 @@ class PointNet2Backbone:
             self._grid = torch.empty((max(1, need),), dtype=torch.uint8, device=device)
         return self._grid
 
-    def forward_from_sa1_fps(self, xyz, idx1, new_xyz1, fz1, gidx1=None, keep_levels=False, grids1=None):
+    def forward_from_sa1_fps(self, xyz, idx1, new_xyz1, fz1, gidx1=None, keep_levels=False, grids1=None, pre2=None):
         """forward() with level 0's FPS (and its ball queries: gidx1, or their binning: grids1)
-        already computed (StreamingSSG)."""
-        return self.forward(xyz, keep_levels, pre={0: {"fps": (idx1, new_xyz1, fz1), "bq": gidx1, "grid": grids1}})
+        already computed (StreamingSSG); pre2: level 1's {"fps": ..., "bq": ...} likewise."""
+        pre = {0: {"fps": (idx1, new_xyz1, fz1), "bq": gidx1, "grid": grids1}}
+        if pre2 is not None:
+            pre[1] = pre2
+        return self.forward(xyz, keep_levels, pre=pre)
 
     def forward(self, xyz, keep_levels=False, pre=None):
         """pre: {level: {"fps": (idx, new_xyz, first_zero), "bq": [gidx per branch] | "grid": [ball_query_bin
@@ -706,7 +709,7 @@ class StreamingSSG:
     """
 
     def __init__(self, backbone, batch, n, depth=1, fps_group=1, fps_threads=0, side_priority=0, ramp=True,
-                 reserve=True, keep_levels=False, slots=None, bq="bin"):
+                 reserve=True, keep_levels=False, slots=None, bq="bin", l2_side=False):
         """fps_threads: SA1 FPS workgroup size (0 = 1024; 512: half the CU footprint beside the
         MLPs).  ramp: in run(), the first groups hold 1, 2, ... batches (a shorter pipeline fill).
         slots: staging slots (>= depth + 1; default depth + 3).  Group k's FPS reuses the slot of
@@ -714,7 +717,10 @@ class StreamingSSG:
         side chain could only start a group once the main stream was `depth` groups behind it,
         which left the main stream idle whenever FPS took about `depth` main passes.
         keep_levels: every output is (global feature, per-level (new_xyz, features, fps idx,
-        [ball-query idx per branch])) instead of the global feature alone."""
+        [ball-query idx per branch])) instead of the global feature alone.  l2_side: level 1's FPS
+        (nested: the prefix shortcut over SA1's centroids) and ball queries depend only on SA1's
+        FPS output, so they run on the side stream too (the main stream then runs only MLP work
+        and level 1's per-point layer 1)."""
         self.bb = backbone
         self.B, self.N, self.depth, self.G = batch, n, depth, max(1, int(fps_group))
         self.ramp = bool(ramp)
@@ -743,6 +749,15 @@ class StreamingSSG:
                       for br in lvl0["branches"]] for _ in range(nslot)] if bq == "side" else None
         self.grid = [[ball_query_grid_buffer(GB, n, dev) for br in lvl0["branches"]]
                      for _ in range(nslot)] if bq == "bin" else None
+        lvl1 = backbone.levels[1] if len(backbone.levels) > 1 else None
+        self.l2 = bool(l2_side) and lvl1 is not None and not lvl1.get("group_all")
+        if self.l2:
+            self.M2 = max(1, n // lvl1["div"])
+            self.idx2 = [torch.empty((GB, self.M2), dtype=torch.int32, device=dev) for _ in range(nslot)]
+            self.cxyz2 = [torch.empty((GB, self.M2, 3), dtype=torch.float32, device=dev) for _ in range(nslot)]
+            self.fz2 = [torch.empty(GB, dtype=torch.int32, device=dev) for _ in range(nslot)]
+            self.gidx2 = [[torch.empty((GB, self.M2, br["ns"]), dtype=torch.int32, device=dev)
+                           for br in lvl1["branches"]] for _ in range(nslot)]
         # setup-time workspace sizing of the side handles (FPS + ball queries), so no stage's
         # first call allocates (lidar_reserve; a grow re-allocates after a device sync)
         if reserve:
@@ -785,6 +800,16 @@ class StreamingSSG:
                           out=self.gidx[slot][bi_][:g], slot=hs)
                 elif self.bq == "bin":  # depends only on the points: the queries run on the main stream
                     _call(t, f"{tag}_bq_bin", g, ball_query_bin, br["r"], br["ns"], x, self.grid[slot][bi_], slot=hs)
+            if self.l2:
+                c1 = self.cxyz[slot][:g]
+                _call(t, "sa2_fps", g, farthest_point_sample, c1, self.M2, return_xyz=True,
+                      first_zero=self.fz2[slot][:g], prefix_ok=self.fz[slot][:g], slot=hs,
+                      out_idx=self.idx2[slot][:g], out_xyz=self.cxyz2[slot][:g])
+                lvl1 = self.bb.levels[1]
+                for bi_, br in enumerate(lvl1["branches"]):
+                    tag = "sa2" + (f"_b{bi_}" if len(lvl1["branches"]) > 1 else "")
+                    _call(t, f"{tag}_ball_query", g, ball_query, br["r"], br["ns"], c1, self.cxyz2[slot][:g],
+                          out=self.gidx2[slot][bi_][:g], slot=hs)
             self.fps_done[slot].record(fs)
         return slot
 
@@ -796,10 +821,17 @@ class StreamingSSG:
         x = self.stage[slot][:g] if self.G > 1 else xs[0]
         lvl0 = [self.idx[slot][:g], self.cxyz[slot][:g], self.fz[slot][:g],
                 [gi[:g] for gi in self.gidx[slot]] if self.gidx is not None else None]
+        pre2 = None
+        if self.l2:
+            pre2 = {"fps": (self.idx2[slot][:g], self.cxyz2[slot][:g], self.fz2[slot][:g]),
+                    "bq": [gi[:g] for gi in self.gidx2[slot]]}
         if self.keep:  # the slot's buffers are reused by a later group
             lvl0 = [a.clone() for a in lvl0[:3]] + [[gi.clone() for gi in lvl0[3]] if lvl0[3] is not None else None]
+            if pre2 is not None:
+                pre2 = {"fps": tuple(a.clone() for a in pre2["fps"]), "bq": [gi.clone() for gi in pre2["bq"]]}
         out, levels = self.bb.forward_from_sa1_fps(x, *lvl0, keep_levels=self.keep,
-                                                   grids1=self.grid[slot] if self.grid is not None else None)
+                                                   grids1=self.grid[slot] if self.grid is not None else None,
+                                                   pre2=pre2)
         self.slot_free[slot].record(main)
         outs = list(out.split(B))
         if not self.keep:

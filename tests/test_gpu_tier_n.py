@@ -402,10 +402,10 @@ def test_streaming_grouped_fps_matches_forward(cuda, cfg_name, dtype, group, dep
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("group,depth,threads,nb,bq,slots", [
-    (3, 3, 512, 7, "side", None), (2, 2, 1024, 4, "side", 3), (4, 2, 512, 5, "side", None),
-    (3, 3, 512, 7, "bin", None), (2, 2, 512, 5, "main", 4), (4, 3, 512, 9, "main", None)])
-def test_streaming_bench_policy_matches_forward(cuda, group, depth, threads, nb, bq, slots):
+@pytest.mark.parametrize("group,depth,threads,nb,bq,slots,l2", [
+    (3, 3, 512, 7, "side", None, False), (2, 2, 1024, 4, "side", 3, False), (4, 2, 512, 5, "side", None, True),
+    (3, 3, 512, 7, "bin", None, True), (2, 2, 512, 5, "main", 4, False), (4, 3, 512, 9, "main", None, True)])
+def test_streaming_bench_policy_matches_forward(cuda, group, depth, threads, nb, bq, slots, l2):
     """the bench's executor policies: 512-thread SA1 FPS on the side streams with the level-0 ball
     queries there, binned there and answered on the main stream, or all on the main stream;
     staging slots from the minimum (depth + 1) up; groups of batches (partial last group), ramped
@@ -414,7 +414,7 @@ def test_streaming_bench_policy_matches_forward(cuda, group, depth, threads, nb,
     xs = [torch.from_numpy(unit_frames(2, 8192, 50 + s)).to(cuda) for s in range(nb)]
     want = [bb.forward(x)[0] for x in xs]
     got = pn.StreamingSSG(bb, 2, 8192, depth=depth, fps_group=group, fps_threads=threads, bq=bq,
-                          slots=slots).run(xs)
+                          slots=slots, l2_side=l2).run(xs)
     torch.cuda.synchronize()
     assert len(got) == nb
     for a, b in zip(got, want):

@@ -266,7 +266,18 @@ def tier_r_leg(dev, rank, world, frames=32, n=65536, steps=3, cpu=True, cpu_budg
         rec["wide_batch"] = {"frames_per_launch": wide,
                              "value": sharding.aggregate_rate(wide * n * steps, world, elw) / 1e6,
                              "unit": "M points/s", "ms_per_launch": elw / steps * 1e3}
-        del xw
+        # the same frames as `wide // frames` batches of `frames`, two batches in flight
+        # (DensityStream.run_batches: a host thread + HIP stream + handle per lane)
+        bl = [xw[i:i + frames] for i in range(0, wide, frames)]
+        ref_b = ds.run_batches(bl)
+        elp = sharding.timed(lambda: [ds.run_batches(bl) for _ in range(steps)], dev, world)
+        got_b = ds.run_batches(bl)
+        assert all(a["total_people"] == b["total_people"] and np.array_equal(a["density_map"], b["density_map"])
+                   for ra, rb in zip(ref_b, got_b) for a, b in zip(ra, rb)), "pipelined batches not deterministic"
+        rec["pipelined_batches"] = {"frames_per_launch": frames, "batches_in_flight": 2, "batches": len(bl),
+                                    "value": sharding.aggregate_rate(wide * n * steps, world, elp) / 1e6,
+                                    "unit": "M points/s", "ms_per_batch": elp / (steps * len(bl)) * 1e3}
+        del xw, bl
     if cpu and rank == 0 and world == 1:
         rec["cpu_baseline"] = tier_r_cpu_baseline(n, cpu_budget)
         rec["speedup_vs_cpu"] = rec["value"] / rec["cpu_baseline"]["value"]

@@ -137,6 +137,40 @@ class DensityStream:
             out[name] = (n + 1, t + ms)
         return out
 
+    def run_batches(self, batches, lanes=2):
+        """batches: list of frame lists -> list of per-batch result lists, in order, with `lanes`
+        batches in flight: each lane is a host thread with its own HIP stream and library handle
+        (handles are per thread), so one lane's host read-backs and latency-bound phases (the
+        sequential preprocess / people chains run one workgroup per frame) overlap the other
+        lanes' kernels.  Results equal run_batch's batch by batch; the first failing batch's
+        exception (in batch order) is raised."""
+        out = [None] * len(batches)
+        lanes = max(1, min(int(lanes), len(batches)))
+        caller = torch.cuda.current_stream(self.device)
+        streams = [torch.cuda.Stream(device=self.device) for _ in range(lanes)]
+        for st in streams:
+            st.wait_stream(caller)  # the frames exist on the caller's stream
+
+        def work(j):
+            torch.cuda.set_device(self.device)
+            with torch.cuda.stream(streams[j]):
+                for i in range(j, len(batches), lanes):
+                    try:
+                        out[i] = self.run_batch(batches[i])
+                    except Exception as e:  # reported in batch order below
+                        out[i] = e
+            streams[j].synchronize()
+
+        ts = [threading.Thread(target=work, args=(j,)) for j in range(lanes)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        for r in out:
+            if isinstance(r, Exception):
+                raise r
+        return out
+
     def people_of_last_batch(self):
         """The people positions of every frame of the last run_batch, concatenated in frame order:
         a (sum K_f, 2) float64 CUDA tensor (what extract_people_positions returns per frame)."""

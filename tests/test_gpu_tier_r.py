@@ -165,6 +165,28 @@ def test_density_batch_matches_drop_in(cuda):
         _same_analyze(name, a, b)
 
 
+def test_density_run_batches_pipelined(cuda):
+    """DensityStream.run_batches: batches in flight on two lanes (host thread + HIP stream +
+    handle each) give run_batch's results batch by batch, in order; a failing batch raises the
+    reference's exception."""
+    import torch
+    from lidar_ai_recommendation_software_amd.density_stream import DensityStream
+    names = [k for k in ["uniform_16384_s0", "small_12", "crowd_16384_s7", "lattice_8163_s4", "small_20",
+                         "int_4096", "blobs_4293_s0", "dup_4096", "tight_2048"] if k in FRAMES]
+    T = lambda k: torch.from_numpy(np.ascontiguousarray(np.asarray(FRAMES[k](), dtype=np.float64))).to(cuda)
+    batches = [[T(k) for k in names[i:i + 3]] for i in range(0, len(names), 3)] * 2
+    ds = DensityStream(cuda, workers=1)
+    want = [ds.run_batch(b) for b in batches]
+    got = ds.run_batches(batches, lanes=2)
+    assert len(got) == len(want)
+    for wb, gb in zip(want, got):
+        for name, a, b in zip(names * 2, wb, gb):
+            _same_analyze(name, a, b)
+    bad = batches[:2] + [[T(names[0]), torch.zeros((0, 3), dtype=torch.float64, device=cuda)]]
+    with pytest.raises(ValueError):
+        ds.run_batches(bad, lanes=2)
+
+
 @pytest.mark.parametrize("bad,exc", [("empty", ValueError), ("const_col", IndexError), ("nan", IndexError)])
 def test_density_batch_errors(cuda, bad, exc):
     import torch

@@ -198,7 +198,8 @@ def eps_pairs(x):
     return (int(cnt.sum()) - len(sc)) // 2
 
 
-def tier_r_leg(dev, rank, world, frames=32, n=65536, steps=3, cpu=True, cpu_budget=12.0, wide=256):
+def tier_r_leg(dev, rank, world, frames=32, n=65536, steps=3, cpu=True, cpu_budget=12.0, wide=256,
+               lanes=int(os.environ.get("LIDAR_DENSITY_LANES", "4"))):
     """The reference's own path (Tier R: preprocess -> DBSCAN -> people -> density grid) on
     device-resident uniform +-15 m frames: batches of `frames` frames through
     density_stream.DensityStream.run_batch (one launch per phase over the CSR batch), with
@@ -266,15 +267,16 @@ def tier_r_leg(dev, rank, world, frames=32, n=65536, steps=3, cpu=True, cpu_budg
         rec["wide_batch"] = {"frames_per_launch": wide,
                              "value": sharding.aggregate_rate(wide * n * steps, world, elw) / 1e6,
                              "unit": "M points/s", "ms_per_launch": elw / steps * 1e3}
-        # the same frames as `wide // frames` batches of `frames`, two batches in flight
+        # the same frames as `wide // frames` batches of `frames`, `lanes` batches in flight (lanes 2 / 3 / 4 / 6:
+        # 451 / 510 / 584 / 430 M pts/s on 8 batches of 32 x 65 536 points)
         # (DensityStream.run_batches: a host thread + HIP stream + handle per lane)
         bl = [xw[i:i + frames] for i in range(0, wide, frames)]
-        ref_b = ds.run_batches(bl)
-        elp = sharding.timed(lambda: [ds.run_batches(bl) for _ in range(steps)], dev, world)
-        got_b = ds.run_batches(bl)
+        ref_b = ds.run_batches(bl, lanes=lanes)
+        elp = sharding.timed(lambda: [ds.run_batches(bl, lanes=lanes) for _ in range(steps)], dev, world)
+        got_b = ds.run_batches(bl, lanes=lanes)
         assert all(a["total_people"] == b["total_people"] and np.array_equal(a["density_map"], b["density_map"])
                    for ra, rb in zip(ref_b, got_b) for a, b in zip(ra, rb)), "pipelined batches not deterministic"
-        rec["pipelined_batches"] = {"frames_per_launch": frames, "batches_in_flight": 2, "batches": len(bl),
+        rec["pipelined_batches"] = {"frames_per_launch": frames, "batches_in_flight": lanes, "batches": len(bl),
                                     "value": sharding.aggregate_rate(wide * n * steps, world, elp) / 1e6,
                                     "unit": "M points/s", "ms_per_batch": elp / (steps * len(bl)) * 1e3}
         del xw, bl

@@ -180,11 +180,6 @@ def _parse_fast(raw, locate):
     if a == 0 and (not lines or b >= len(lines)):
         # no data section located inside the head: let the Python path decide
         return None
-    import ctypes
-    lib = nat.load_library()
-    cap = raw.count(b"\n") + 1
-    out = np.empty((cap, 3), dtype=np.float64)
-    n = ctypes.c_int64(0)
     max_lines = -1
     if locate is _ply_body:  # the vertex count bounds the data lines; none: to the end
         nvert = None
@@ -192,12 +187,26 @@ def _parse_fast(raw, locate):
             if "element vertex" in ln:
                 nvert = int(ln.split()[-1])
         max_lines = -1 if nvert is None else max(0, nvert)
-    rc = lib.lidar_parse_ascii_xyz(raw, len(raw), a, max_lines, out.ctypes.data_as(ctypes.c_void_p), cap,
+    pts = _parse_ascii_lines_or_none(raw, a, max_lines)
+    if pts is None:
+        return None
+    return pts if len(pts) else np.array([])
+
+
+def _parse_ascii_lines_or_none(raw, first, max_lines):
+    """(n, 3) float64 rows of lines [first, first + max_lines) of `raw` (max_lines < 0: to the
+    end) from liblidar_amd's C parser (lidar_parse_ascii_xyz), or None when a token needs
+    Python's float() (the caller's own loop then decides)."""
+    import ctypes
+    lib = nat.load_library()
+    cap = raw.count(b"\n") + 1
+    out = np.empty((cap, 3), dtype=np.float64)
+    n = ctypes.c_int64(0)
+    rc = lib.lidar_parse_ascii_xyz(raw, len(raw), first, max_lines, out.ctypes.data_as(ctypes.c_void_p), cap,
                                    ctypes.byref(n))
     if rc != 0:
         return None
-    n = n.value
-    return np.array(out[:n]) if n else np.array([])
+    return np.array(out[:n.value])
 
 
 # ---------------------------------------------------------------- preprocess (L2)

@@ -356,7 +356,11 @@ __global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float 
 // weight fragment), and the max-pool is a register max: per chunk, each lane's max over its rows
 // is reduced over the four row groups by two lane swaps and folded into mx[t / 4] of row group
 // t % 4 — no LDS table.
-template <int C1, int C2, int C3, int NS>
+//
+// PFX: the centre's NS point indices come in one coalesced load at the start (lane l holds rows
+// l, 64 + l, ...), and a tile's 16 row indices by ds_bpermute from those registers, so a tile's
+// gather of P rows waits on one memory round trip instead of two dependent ones (idx, then P).
+template <int C1, int C2, int C3, int NS, bool PFX>
 __global__ __launch_bounds__(256, 4) void sa_x3_lean_kernel(const float *__restrict__ P, int64_t stride,
                                                             const float *__restrict__ Q,
                                                             const int32_t *__restrict__ idx, int n, int m,
@@ -372,6 +376,7 @@ __global__ __launch_bounds__(256, 4) void sa_x3_lean_kernel(const float *__restr
     constexpr int NL2 = T2 / 2, NL3 = T3 / 2, NSEQ = R * NL2 + NL3;  // chunk passes per iteration
     constexpr int ITERS = NS / (16 * R);
     constexpr int PER = (CHMAX + 255) / 256;
+    static_assert(!PFX || NS % 64 == 0, "PFX: whole 64-row blocks of indices");
 
     __shared__ uint4 buf[2][CHMAX];
     __shared__ float bias_s[C2 + C3];
@@ -402,6 +407,11 @@ __global__ __launch_bounds__(256, 4) void sa_x3_lean_kernel(const float *__restr
                                                  0);
         }
     };
+    int32_t kall[PFX ? NS / 64 : 1];
+    if constexpr (PFX) {
+#pragma unroll
+        for (int j = 0; j < NS / 64; ++j) kall[j] = idx[cc * NS + 64 * j + lane];
+    }
     fetch(0, 0);
     for (int i = tid; i < C2 + C3; i += 256) bias_s[i] = Bias[C1 + i];
     __syncthreads();
@@ -420,7 +430,12 @@ __global__ __launch_bounds__(256, 4) void sa_x3_lean_kernel(const float *__restr
             {
                 int zero = 0;
                 asm volatile("" : "+v"(zero));
-                const int64_t k = idx[cc * NS + (it * R + rr) * 16 + col];
+                const int t16 = (it * R + rr) * 16;  // the tile's first row
+                int64_t k;
+                if constexpr (PFX)
+                    k = __shfl(kall[t16 >> 6], (t16 & 63) + col, 64);
+                else
+                    k = idx[cc * NS + t16 + col];
                 const f32x4 *pp = reinterpret_cast<const f32x4 *>(P + ((int64_t)b * n + k) * stride + 4 * q);
                 const f32x4 *qq = reinterpret_cast<const f32x4 *>(Q + cc * stride + 4 * q + zero);
 #pragma unroll
@@ -528,6 +543,15 @@ static bool use_lean()
     }();
     return on;
 }
+// index prefetch in the lean kernel unless LIDAR_LEAN_PFX=0 (A/B switch)
+static bool use_lean_pfx()
+{
+    static const bool on = [] {
+        const char *e = getenv("LIDAR_LEAN_PFX");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
 
 template <int C1, int C2, int C3, int NS>
 int launch_x3_lean(const float *p, int64_t stride, const float *q, const int32_t *idx, int64_t batch, int64_t n,
@@ -536,8 +560,12 @@ int launch_x3_lean(const float *p, int64_t stride, const float *q, const int32_t
     const int64_t total = batch * m;
     const int64_t blocks = (total + 3) / 4;
     REQUIRE(blocks <= 0x7fffffff, "sa_group_mlp_x3: too many centres");
-    hipLaunchKernelGGL((sa_x3_lean_kernel<C1, C2, C3, NS>), dim3((unsigned)blocks), dim3(256), 0, s, p, stride, q,
-                       idx, (int)n, (int)m, total, static_cast<const uint4 *>(packed), out, os, oo);
+    if (NS % 64 == 0 && use_lean_pfx())
+        hipLaunchKernelGGL((sa_x3_lean_kernel<C1, C2, C3, NS, NS % 64 == 0>), dim3((unsigned)blocks), dim3(256), 0, s,
+                           p, stride, q, idx, (int)n, (int)m, total, static_cast<const uint4 *>(packed), out, os, oo);
+    else
+        hipLaunchKernelGGL((sa_x3_lean_kernel<C1, C2, C3, NS, false>), dim3((unsigned)blocks), dim3(256), 0, s, p,
+                           stride, q, idx, (int)n, (int)m, total, static_cast<const uint4 *>(packed), out, os, oo);
     LAUNCH_CHECK();
     return LIDAR_OK;
 }

@@ -69,6 +69,7 @@ struct BlockScratch {
     int i[kW + 1];
     unsigned hist[2][256];
     double bc[16];  // broadcast
+    double chain[6];  // block_sum_chain results: [accumulator * 3 + column]
 };
 
 __device__ double block_min(BlockScratch &s, double v)
@@ -124,10 +125,11 @@ __device__ int block_flag_scan(BlockScratch &s, bool f, int *total)
 
 // ---- index-order fp64 chains with the rows streamed through LDS
 // numpy's axis-0 reductions of a row-major (n, 3) array are sequential per column, so the
-// result depends on every rounding in index order: the chain itself cannot be split.  What
-// can be removed is the memory latency: waves 1..15 stage 1024-row chunks into LDS (double
-// buffered) while lanes 0..2 of wave 0 (lane c = column c) run the dependent adds out of
-// LDS.  `step(c, v, a0, a1)` advances column c's accumulators by one row.
+// result depends on every rounding in index order.  The rows are staged into LDS in 1024-row
+// chunks (double buffered) by the waves that do not run a chain.  Two ways to run a chain:
+// block_seq_chain, the dependent adds themselves (lanes 0..2 of wave 0, lane c = column c), for
+// sums of signed values (coordinates, deviations: their accumulator wanders across binades near
+// zero), and block_sum_chain below, a parallel emulation, for sums of squares.
 constexpr int kSeqRows = 1024;
 struct SeqStage {
     double v[2][kSeqRows * 3];
@@ -168,6 +170,147 @@ __device__ void block_seq_chain(const double *x, int64_t n, SeqStage &st, Step s
         }
         __syncthreads();
     }
+}
+
+// ---- the same index-order chains, emulated in parallel, bit for bit
+// A chain a <- fl(a + inc_i) (i = 0..n-1, a = +0.0 first) is reproduced without n dependent adds.
+// While a stays in one binade [2^e, 2^(e+1)) (or its negative), with u = 2^(e-52), every partial
+// result is a multiple of u, and fl(a + v) = a + u * rint(v / u) as long as the exact sum stays in
+// that binade and v / u is not an exact tie (the tie goes to the even neighbour, which depends on a).
+// So a wavefront takes 64 rows at a time: lane l scales its increment to k_l = rint(inc_l * 2^(53-E))
+// (a = m 2^E, 0.5 <= |m| < 1: exact power-of-two scaling), an inclusive scan of the k_l (integers
+// of at most 2^46 each, so every partial sum is exact in fp64) gives A_l = A + P_l, and the rows up
+// to the first lane whose A_l leaves (2^52, 2^53) in magnitude, or whose increment is a tie, huge
+// (> 2^46 u), inf or NaN, are accepted at once: a = A_l * u.  The violating row is added with one
+// dadd, exactly as the sequential chain does, and the scan restarts after it.  Near zero (a = 0,
+// subnormal, non-finite) the rows go one dadd at a time; after a scan accepts fewer than
+// kChainMinRun rows (an accumulator hovering near a binade edge, as a centred column's sum does),
+// the next kChainSeqRun rows go one dadd at a time before the next scan.  Every accepted row has the
+// value the dependent add would have produced, so the result is the sequential one bit for bit
+// (tests/test_gpu_tier_r.py: the reference's goldens, byte-equal).
+constexpr int kChainMinRun = 16, kChainSeqRun = 32;
+
+// wave-uniform fp64 helpers (scalar registers: the chain's control flow stays scalar)
+__device__ __forceinline__ double readlane_d(double v, int l)
+{
+    const uint64_t u = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+__device__ __forceinline__ double uniform_d(double v)
+{
+    const uint64_t u = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)u);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(u >> 32));
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+// DPP move of an fp64 value (both halves), 0 where the row / bank masks or the row bounds leave
+// a lane without a source
+template <int CTRL, int RM, bool BC>
+__device__ __forceinline__ double dpp_d(double v)
+{
+    const uint64_t u = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, CTRL, RM, 0xf, BC);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTRL, RM, 0xf, BC);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+// inclusive wave scan of integer-valued doubles whose partial sums stay below 2^53 (exact):
+// row_shr 1 / 2 / 4 / 8 within each 16-lane row, then row_bcast 15 (rows 1, 3) and 31 (rows 2, 3)
+__device__ __forceinline__ double wave_scan_exact_d(double P)
+{
+    P = dadd(P, dpp_d<0x111, 0xf, true>(P));
+    P = dadd(P, dpp_d<0x112, 0xf, true>(P));
+    P = dadd(P, dpp_d<0x114, 0xf, true>(P));
+    P = dadd(P, dpp_d<0x118, 0xf, true>(P));
+    P = dadd(P, dpp_d<0x142, 0xa, false>(P));
+    P = dadd(P, dpp_d<0x143, 0xc, false>(P));
+    return P;
+}
+
+// chain (column c = wave % 3, accumulator q = wave / 3) of rows [0, n) of x (row-major (n, 3)):
+// a_q[c] <- fl(a_q[c] + inc(c, q, x[i][c])).  Waves 0 .. 3 NQ - 1 run the chains; the other waves
+// stage 1024-row chunks into LDS (double buffered).  Results land in s.chain[q * 3 + c] (ends with
+// a barrier).
+template <int NQ, class Inc>
+__device__ void block_sum_chain(const double *x, int64_t n, SeqStage &st, BlockScratch &s, Inc inc)
+{
+    constexpr int kCW = 3 * NQ;  // chain waves
+    constexpr double kTwo52 = 4503599627370496.0, kTwo53 = 9007199254740992.0, kTwo46 = 70368744177664.0;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t nch = (n + kSeqRows - 1) / kSeqRows;
+    auto stage = [&](int64_t k) {
+        if (wave < kCW || k >= nch) return;  // the chain waves never wait on global loads
+        const int64_t r0 = k * kSeqRows;
+        const int64_t cnt = (n - r0 < kSeqRows ? n - r0 : kSeqRows) * 3;
+        double *d = st.v[k & 1];
+        const double *src = x + 3 * r0;
+        for (int64_t e = tid - 64 * kCW; e < cnt; e += kT - 64 * kCW) d[e] = src[e];
+    };
+    const int c = wave % 3, q = wave / 3;
+    double a = 0.0;
+    int forced = 0;
+    stage(0);
+    __syncthreads();
+    for (int64_t k = 0; k < nch; ++k) {
+        stage(k + 1);
+        if (wave < kCW) {
+            const int64_t r0 = k * kSeqRows;
+            const int rows = (int)(n - r0 < kSeqRows ? n - r0 : kSeqRows);
+            const double *b = st.v[k & 1] + c;
+            int i = 0;
+            while (i < rows) {
+                a = uniform_d(a);
+                i = __builtin_amdgcn_readfirstlane(i);
+                forced = __builtin_amdgcn_readfirstlane(forced);
+                if (forced > 0 || !(fabs(a) >= 2.2250738585072014e-308) || !(fabs(a) < INFINITY)) {
+                    // one dadd per row (wave-uniform): near zero, non-finite, or a forced run
+                    const int run = forced > 0 ? (forced < rows - i ? forced : rows - i) : 1;
+                    int t = 0;
+                    for (; t + 8 <= run; t += 8) {
+                        double v[8];
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) v[u] = inc(c, q, b[3 * (i + t + u)]);
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) a = dadd(a, v[u]);
+                    }
+                    for (; t < run; ++t) a = dadd(a, inc(c, q, b[3 * (i + t)]));
+                    i += run;
+                    forced = forced > run ? forced - run : 0;
+                    continue;
+                }
+                int e2;
+                (void)frexp(a, &e2);  // a = m 2^e2, 0.5 <= |m| < 1
+                const int sh = __builtin_amdgcn_readfirstlane(53 - e2);
+                const double A = ldexp(a, sh);  // |A| in [2^52, 2^53), exact
+                const int j = i + lane;
+                const bool valid = j < rows;
+                const double v = valid ? inc(c, q, b[3 * j]) : 0.0;
+                const double xs = ldexp(v, sh);
+                double kq = rint(xs);
+                const bool bad = valid && (!(fabs(kq) <= kTwo46) || dsub(xs, floor(xs)) == 0.5);
+                if (!valid || bad) kq = 0.0;
+                const double Aj = dadd(A, wave_scan_exact_d(kq));  // exact below 2^53; >= 2^53 stays
+                const double sAj = a > 0.0 ? Aj : -Aj;
+                const bool viol = valid && (bad || !(sAj > kTwo52 && sAj < kTwo53));
+                const uint64_t vm = __ballot(viol);
+                const int nv = rows - i < 64 ? rows - i : 64;
+                if (vm == 0) {
+                    a = ldexp(readlane_d(Aj, nv - 1), -sh);
+                    i += nv;
+                } else {
+                    const int j0 = __builtin_amdgcn_readfirstlane(__ffsll((unsigned long long)vm) - 1);
+                    if (j0 > 0) a = ldexp(readlane_d(Aj, j0 - 1), -sh);
+                    a = dadd(a, readlane_d(v, j0));  // the violating row: the sequential add itself
+                    i += j0 + 1;
+                    if (j0 < kChainMinRun) forced = kChainSeqRun;
+                }
+            }
+        }
+        __syncthreads();
+    }
+    if (wave < kCW && lane == 0) s.chain[q * 3 + c] = a;
+    __syncthreads();
 }
 
 __device__ __forceinline__ uint64_t ordkey(double v)
@@ -224,13 +367,12 @@ __global__ __launch_bounds__(kT) void preprocess_kernel(const double *__restrict
         block_seq_chain(xyz, n, st, [](int, double v, double &a, double &) { a = dadd(a, v); }, sum, unused);
         if (tid < 3) s.bc[tid] = ddiv(sum, (double)n);
         __syncthreads();
-        const double mc = tid < 3 ? s.bc[tid] : 0.0;
-        double sq = 0.0;
-        block_seq_chain(xyz, n, st, [mc](int, double v, double &a, double &) {
-            const double d = dsub(v, mc);
-            a = dadd(a, dmul(d, d));
-        }, sq, unused);
-        if (tid < 3) s.bc[3 + tid] = __dsqrt_rn(ddiv(sq, (double)n));
+        const double mw = s.bc[(tid >> 6) % 3];  // the mean of this wave's chain column
+        block_sum_chain<1>(xyz, n, st, s, [mw](int, int, double v) {
+            const double d = dsub(v, mw);
+            return dmul(d, d);
+        });
+        if (tid < 3) s.bc[3 + tid] = __dsqrt_rn(ddiv(s.chain[tid], (double)n));
     }
     __syncthreads();
     double mean[3], thr[3];
@@ -369,11 +511,18 @@ __global__ __launch_bounds__(kT) void preprocess_kernel(const double *__restrict
     if (nground > 10) {
         const double mx = block_sum(s, sx, 1) / ng, my = block_sum(s, sy, 2) / ng,
                      mz = block_sum(s, sz, 3) / ng;
+        // centred coordinates times one power of two (2^-e, e = the exponent of the largest inlier
+        // extent): exact scaling, so the slopes are those of the unscaled system bit for bit, but
+        // the moments and det neither underflow (|x| ~ 1e-140) nor overflow (|x| ~ 1e150)
+        const double ext = fmax(fmax(dmax[0] - dmin[0], dmax[1] - dmin[1]), dmax[2] - dmin[2]);
+        int ee = 0;
+        if (ext > 0.0 && ext < INFINITY) (void)frexp(ext, &ee);
+        const double sc = ldexp(1.0, -ee);
         double axx = 0, axy = 0, ayy = 0, axz = 0, ayz = 0;
         for (int64_t i = tid; i < nin; i += kT) {
             const double pz = comp[3 * i + 2];
             if (pz <= zt) {
-                const double dx = comp[3 * i] - mx, dy = comp[3 * i + 1] - my, dz = pz - mz;
+                const double dx = (comp[3 * i] - mx) * sc, dy = (comp[3 * i + 1] - my) * sc, dz = (pz - mz) * sc;
                 axx += dx * dx;
                 axy += dx * dy;
                 ayy += dy * dy;
@@ -396,13 +545,15 @@ __global__ __launch_bounds__(kT) void preprocess_kernel(const double *__restrict
             pkind = 0.0;
         } else {
             // rank-deficient (collinear) ground: pseudo-inverse of the centred 2x2 normal
-            // system — gelsd's minimum-norm answer is reproduced only approximately here
+            // system M = [[axx, axy], [axy, ayy]] (rank 1: eigenvector (axx, axy), eigenvalue tr),
+            // pinv(M) r = (axx, axy) (axx axz + axy ayz) / (axx tr^2) — gelsd's minimum-norm
+            // answer is reproduced only approximately here
             const double tr = axx + ayy;
             double a = 0.0, b = 0.0;
             if (tr > 0.0) {
                 const double k = (axz * axx + ayz * axy) / (tr * tr);
-                a = k * axx;
-                b = k * axy;
+                a = k;
+                b = axx != 0.0 ? k * axy / axx : 0.0;
                 if (axx == 0.0) {
                     const double k2 = ayz / ayy;
                     a = 0.0;
@@ -524,14 +675,12 @@ __global__ __launch_bounds__(kT) void preprocess_kernel(const double *__restrict
         block_seq_chain(sc, nng, st, [](int, double v, double &a, double &) { a = dadd(a, v); }, sum, unused);
         if (tid < 3) s.bc[12 + tid] = ddiv(sum, nn);
         __syncthreads();
-        const double mc = tid < 3 ? s.bc[12 + tid] : 0.0;
-        double sq = 0.0;
-        block_seq_chain(sc, nng, st, [mc](int, double v, double &a, double &) {
-            const double d = dsub(v, mc);
-            a = dadd(a, dmul(d, d));
-        }, sq, unused);
-        __syncthreads();
-        if (tid < 3) s.bc[12 + tid] = __dsqrt_rn(ddiv(sq, nn));
+        const double mw = s.bc[12 + (tid >> 6) % 3];
+        block_sum_chain<1>(sc, nng, st, s, [mw](int, int, double v) {
+            const double d = dsub(v, mw);
+            return dmul(d, d);
+        });
+        if (tid < 3) s.bc[12 + tid] = __dsqrt_rn(ddiv(s.chain[tid], nn));
     }
     __syncthreads();
     if (tid == 0) {

@@ -131,6 +131,9 @@ __device__ int block_flag_scan(BlockScratch &s, bool f, int *total)
 // sums of signed values (coordinates, deviations: their accumulator wanders across binades near
 // zero), and block_sum_chain below, a parallel emulation, for sums of squares.
 constexpr int kSeqRows = 1024;
+// rows whose LDS reads are issued before their dependent adds (32 measured equal, 64 slower: the
+// chain is bound by the dependent fp64 adds, not by the LDS reads)
+constexpr int kSeqBatch = 16;
 struct SeqStage {
     double v[2][kSeqRows * 3];
 };
@@ -159,12 +162,12 @@ __device__ void block_seq_chain(const double *x, int64_t n, SeqStage &st, Step s
             // reads of a 16-row batch first, then its dependent adds (an explicit two-batch
             // software pipeline measured 2.4x slower: 7.6 vs 3.2 ms per 65k frame)
             int i = 0;
-            for (; i + 16 <= rows; i += 16) {
-                double v[16];
+            for (; i + kSeqBatch <= rows; i += kSeqBatch) {
+                double v[kSeqBatch];
 #pragma unroll
-                for (int u = 0; u < 16; ++u) v[u] = b[3 * (i + u)];
+                for (int u = 0; u < kSeqBatch; ++u) v[u] = b[3 * (i + u)];
 #pragma unroll
-                for (int u = 0; u < 16; ++u) step(tid, v[u], a0, a1);
+                for (int u = 0; u < kSeqBatch; ++u) step(tid, v[u], a0, a1);
             }
             for (; i < rows; ++i) step(tid, b[3 * i], a0, a1);
         }

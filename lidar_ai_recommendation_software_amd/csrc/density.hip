@@ -1307,12 +1307,13 @@ __global__ void scatter_labels2_kernel(const double *S_in, const int64_t *ng_lab
 }
 
 // ------------------------------------------------------------------ people
-// one wavefront per cluster scans the frame in index order: ballot the members of each
-// 64-point chunk, then add them lane by lane — numpy's sequential axis-0 order
-// One workgroup per cluster: waves 1..15 compact the cluster's members of a 960-point
-// chunk (index order: wave w holds points [64(w-1), 64w) of the chunk, ballot-ranked) into
-// LDS, double-buffered; lanes 0 / 1 of wave 0 run the x / y chains in index order, as
-// np.mean of the member rows does (sequential axis-0 sums starting from the first row).
+// One workgroup per cluster: waves 1..15 compact the cluster's members of a 960-point chunk
+// (wave w owns points [64(w-1), 64w) of every chunk) into LDS contiguously in index order
+// (double-buffered rows, triple-buffered per-wave counts), and lanes 0 / 1 of wave 0 run the
+// x / y chains over the chunk's members in one run, as np.mean of the member rows does
+// (sequential axis-0 sums starting from the first row).  Per chunk: the staging waves place
+// chunk k+1 (its counts were published a phase earlier) and count chunk k+2 while wave 0 adds
+// chunk k; one barrier per chunk.
 __global__ __launch_bounds__(kT) void people_kernel(const double *xyz_in, const int64_t *labels_in, int64_t n_in,
                                                     const int64_t *kdev_in, double *out_in, const double *S_in,
                                                     FrameMap fm)
@@ -1325,53 +1326,63 @@ __global__ __launch_bounds__(kT) void people_kernel(const double *xyz_in, const 
     double *out = fm.rows(out_in, 2);
     constexpr int kChunk = kT - 64;
     __shared__ double mem[2][kChunk * 2];
-    __shared__ int wcnt[2][kW];
+    __shared__ int wcnt[3][kW];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int64_t K = *kdev;
     const int64_t nch = (n + kChunk - 1) / kChunk;
     for (int64_t c = blockIdx.x; c < K; c += gridDim.x) {
-        auto stage = [&](int64_t k) {
-            if (wave == 0 || k >= nch) return;
+        // members of this wave's 64 points of chunk k (0 for wave 0 and past the end), published
+        // as the wave's count of chunk k
+        auto count = [&](int64_t k) -> uint64_t {
+            if (wave == 0) return 0;
             const int64_t i = k * kChunk + (tid - 64);
-            const bool hit = i < n && labels[i] == c;
-            const uint64_t m = __ballot(hit);
-            if (lane == 0) wcnt[k & 1][wave] = __popcll(m);
-            if (hit) {
-                const int r = (wave - 1) * 64 + __popcll(m & ((1ull << lane) - 1));
-                mem[k & 1][2 * r] = xyz[3 * i];
-                mem[k & 1][2 * r + 1] = xyz[3 * i + 1];
-            }
+            const uint64_t m = __ballot(k < nch && i < n && labels[i] == c);
+            if (lane == 0) wcnt[k % 3][wave] = __popcll(m);
+            return m;
+        };
+        auto place = [&](int64_t k, uint64_t m) {
+            if (wave == 0 || k >= nch || !((m >> lane) & 1)) return;
+            int base = 0;
+            for (int w = 1; w < wave; ++w) base += wcnt[k % 3][w];
+            const int64_t i = k * kChunk + (tid - 64);
+            const int r = base + __popcll(m & ((1ull << lane) - 1));
+            mem[k & 1][2 * r] = xyz[3 * i];
+            mem[k & 1][2 * r + 1] = xyz[3 * i + 1];
         };
         double acc = 0.0;
         int64_t cnt = 0;
-        stage(0);
+        uint64_t m_next = count(0);
+        __syncthreads();
+        place(0, m_next);
+        m_next = count(1);
         __syncthreads();
         for (int64_t k = 0; k < nch; ++k) {
-            stage(k + 1);
-            if (tid < 2) {
+            if (wave != 0) {
+                place(k + 1, m_next);
+                m_next = count(k + 2);
+            } else if (tid < 2) {
+                int tot = 0;
+                for (int w = 1; w < kW; ++w) tot += wcnt[k % 3][w];
                 const double *b = mem[k & 1] + tid;
-                for (int w = 1; w < kW; ++w) {
-                    const int m = wcnt[k & 1][w];
-                    const double *bw = b + 2 * (w - 1) * 64;
-                    int j = 0;
-                    if (cnt == 0 && m > 0) {  // np.add.reduce starts from the first row
-                        acc = bw[0];
-                        j = 1;
-                    }
-                    for (; j + 8 <= m; j += 8) {  // reads first, then the dependent adds
-                        double v[8];
-#pragma unroll
-                        for (int u = 0; u < 8; ++u) v[u] = bw[2 * (j + u)];
-#pragma unroll
-                        for (int u = 0; u < 8; ++u) acc = dadd(acc, v[u]);
-                    }
-                    for (; j < m; ++j) acc = dadd(acc, bw[2 * j]);
-                    cnt += m;
+                int j = 0;
+                if (cnt == 0 && tot > 0) {  // np.add.reduce starts from the first row
+                    acc = b[0];
+                    j = 1;
                 }
+                for (; j + 16 <= tot; j += 16) {  // reads first, then the dependent adds
+                    double v[16];
+#pragma unroll
+                    for (int u = 0; u < 16; ++u) v[u] = b[2 * (j + u)];
+#pragma unroll
+                    for (int u = 0; u < 16; ++u) acc = dadd(acc, v[u]);
+                }
+                for (; j < tot; ++j) acc = dadd(acc, b[2 * j]);
+                cnt += tot;
             }
             __syncthreads();
         }
         if (tid < 2) out[2 * c + tid] = ddiv(acc, (double)cnt);
+        __syncthreads();  // the next cluster's first counts reuse wcnt[0..1]
     }
 }
 

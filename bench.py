@@ -253,10 +253,12 @@ def tier_r_leg(dev, rank, world, frames=32, n=65536, steps=3, cpu=True, cpu_budg
                            "frac": a / HBM_PEAK_GBS, "traffic": None, "work_per_launch": algo,
                            "avg_launch_ms": per_launch_ms[dom],
                            "peak_basis": "HBM peak over algorithmic bytes; the phase is latency-bound (numpy's "
-                                         "sequential axis-0 sums: six dependent fp64 chains per frame, DESIGN.md §2)"}
+                                         "sequential axis-0 sums: four dependent fp64 chains per frame plus two "
+                                         "sums of squares emulated in parallel, DESIGN.md §2)"}
     if "preprocess" in per_launch_ms:
-        # the sequential chains: ~6 passes of n dependent fp64 adds per frame, frames in parallel
-        rec["preprocess_chain_ns_per_row"] = per_launch_ms["preprocess"] * 1e6 / (6 * n)
+        # the sequential chains: 4 passes of n dependent fp64 adds per frame (frames in parallel), plus
+        # the two emulated sums of squares (~1/5 of a pass each): time per row of one dependent pass
+        rec["preprocess_chain_ns_per_row"] = per_launch_ms["preprocess"] * 1e6 / (4.4 * n)
     if wide and wide > frames:
         # the same path with `wide` frames per launch: preprocess and people run one workgroup
         # per frame (sequential chains), so 32 frames leave most CUs idle in those phases

@@ -124,6 +124,22 @@ namespace lidar {
 
 // (dx*dx + dy*dy) + dz*dz with one rounding per operation (the -ffp-contract=off
 // build guarantees no FMA contraction)
+// XCD-affine block order (LIDAR_XCD_MAP, default on): the hardware hands workgroup b of a launch to
+// XCD b % 8, so consecutive blocks land on eight different L2s.  Blocks whose work gathers from the
+// same per-frame data (all centres of a frame read that frame's rows) are renumbered so that XCD x
+// runs the logical range [x G/8, (x+1) G/8) in order: a frame's gathers then hit one L2 instead of
+// being fetched into all eight.  A bijection of [0, G) for any G; results do not depend on it.
+#ifndef LIDAR_XCD_MAP
+#define LIDAR_XCD_MAP 1
+#endif
+__device__ __forceinline__ int64_t xcd_block()
+{
+    const int64_t b = blockIdx.x;
+    if (!LIDAR_XCD_MAP) return b;
+    const int64_t G = gridDim.x, q = G / 8, r = G % 8, x = b % 8, i = b / 8;
+    return x * q + (x < r ? x : r) + i;
+}
+
 __device__ __forceinline__ float dist2f(float ax, float ay, float az, float bx, float by, float bz)
 {
     float dx = ax - bx, dy = ay - by, dz = az - bz;

@@ -129,7 +129,7 @@ __global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float 
     // wave index in an SGPR: the LDS-DMA destinations (M0) and the unit below are wave-uniform
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int q = lane >> 4, col = lane & 15;
-    const int64_t unit = (int64_t)blockIdx.x * 4 + wave;
+    const int64_t unit = lidar::xcd_block() * 4 + wave;
     const bool live = unit < total;  // every wave takes part in the barriers
     const int64_t cc = live ? unit : total - 1;
     const int64_t b = cc / m;
@@ -383,7 +383,7 @@ __global__ __launch_bounds__(256, 4) void sa_x3_lean_kernel(const float *__restr
 
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int q = lane >> 4, col = lane & 15;
-    const int64_t unit = (int64_t)blockIdx.x * 4 + wave;
+    const int64_t unit = lidar::xcd_block() * 4 + wave;
     const bool live = unit < total;
     const int64_t cc = live ? unit : total - 1;
     const int64_t b = cc / m;

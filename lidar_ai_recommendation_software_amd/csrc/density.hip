@@ -180,18 +180,19 @@ __device__ void block_seq_chain(const double *x, int64_t n, SeqStage &st, Step s
 // While a stays in one binade [2^e, 2^(e+1)) (or its negative), with u = 2^(e-52), every partial
 // result is a multiple of u, and fl(a + v) = a + u * rint(v / u) as long as the exact sum stays in
 // that binade and v / u is not an exact tie (the tie goes to the even neighbour, which depends on a).
-// So a wavefront takes 64 rows at a time: lane l scales its increment to k_l = rint(inc_l * 2^(53-E))
-// (a = m 2^E, 0.5 <= |m| < 1: exact power-of-two scaling), an inclusive scan of the k_l (integers
-// of at most 2^46 each, so every partial sum is exact in fp64) gives A_l = A + P_l, and the rows up
-// to the first lane whose A_l leaves (2^52, 2^53) in magnitude, or whose increment is a tie, huge
-// (> 2^46 u), inf or NaN, are accepted at once: a = A_l * u.  The violating row is added with one
+// So a wavefront takes 256 rows at a time (4 consecutive rows per lane): every row's increment is
+// scaled to k = rint(inc * 2^(53-E)) (a = m 2^E, 0.5 <= |m| < 1: exact power-of-two scaling), a
+// lane-local prefix plus a DPP scan of the lane totals (integers of at most 2^44 each, so every
+// partial sum is exact in fp64) gives A_j = A + P_j, and the rows up to the first one whose A_j
+// leaves (2^52, 2^53) in magnitude, or whose increment is a tie, huge (> 2^44 u), inf or NaN, are
+// accepted at once: a = A_j * u.  The violating row is added with one
 // dadd, exactly as the sequential chain does, and the scan restarts after it.  Near zero (a = 0,
 // subnormal, non-finite) the rows go one dadd at a time; after a scan accepts fewer than
 // kChainMinRun rows (an accumulator hovering near a binade edge, as a centred column's sum does),
 // the next kChainSeqRun rows go one dadd at a time before the next scan.  Every accepted row has the
 // value the dependent add would have produced, so the result is the sequential one bit for bit
 // (tests/test_gpu_tier_r.py: the reference's goldens, byte-equal).
-constexpr int kChainMinRun = 16, kChainSeqRun = 32;
+constexpr int kChainMinRun = 16, kChainSeqRun = 32, kChainRowsPerLane = 4;
 
 // wave-uniform fp64 helpers (scalar registers: the chain's control flow stays scalar)
 __device__ __forceinline__ double readlane_d(double v, int l)
@@ -239,7 +240,7 @@ template <int NQ, class Inc>
 __device__ void block_sum_chain(const double *x, int64_t n, SeqStage &st, BlockScratch &s, Inc inc)
 {
     constexpr int kCW = 3 * NQ;  // chain waves
-    constexpr double kTwo52 = 4503599627370496.0, kTwo53 = 9007199254740992.0, kTwo46 = 70368744177664.0;
+    constexpr double kTwo52 = 4503599627370496.0, kTwo53 = 9007199254740992.0, kTwo44 = 17592186044416.0;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int64_t nch = (n + kSeqRows - 1) / kSeqRows;
     auto stage = [&](int64_t k) {
@@ -286,25 +287,53 @@ __device__ void block_sum_chain(const double *x, int64_t n, SeqStage &st, BlockS
                 (void)frexp(a, &e2);  // a = m 2^e2, 0.5 <= |m| < 1
                 const int sh = __builtin_amdgcn_readfirstlane(53 - e2);
                 const double A = ldexp(a, sh);  // |A| in [2^52, 2^53), exact
-                const int j = i + lane;
-                const bool valid = j < rows;
-                const double v = valid ? inc(c, q, b[3 * j]) : 0.0;
-                const double xs = ldexp(v, sh);
-                double kq = rint(xs);
-                const bool bad = valid && (!(fabs(kq) <= kTwo46) || dsub(xs, floor(xs)) == 0.5);
-                if (!valid || bad) kq = 0.0;
-                const double Aj = dadd(A, wave_scan_exact_d(kq));  // exact below 2^53; >= 2^53 stays
-                const double sAj = a > 0.0 ? Aj : -Aj;
-                const bool viol = valid && (bad || !(sAj > kTwo52 && sAj < kTwo53));
-                const uint64_t vm = __ballot(viol);
-                const int nv = rows - i < 64 ? rows - i : 64;
+                // lane l takes rows i + 4l .. i + 4l + 3: a window of 256 rows per scan
+                double v[kChainRowsPerLane], L[kChainRowsPerLane];
+                bool bad[kChainRowsPerLane], valid[kChainRowsPerLane];
+                double run = 0.0;  // the lane's own prefix of its rounded increments
+#pragma unroll
+                for (int r = 0; r < kChainRowsPerLane; ++r) {
+                    const int j = i + kChainRowsPerLane * lane + r;
+                    valid[r] = j < rows;
+                    v[r] = valid[r] ? inc(c, q, b[3 * j]) : 0.0;
+                    const double xs = ldexp(v[r], sh);
+                    double kq = rint(xs);
+                    bad[r] = valid[r] && (!(fabs(kq) <= kTwo44) || dsub(xs, floor(xs)) == 0.5);
+                    if (!valid[r] || bad[r]) kq = 0.0;
+                    run = dadd(run, kq);  // integers below 2^46: exact
+                    L[r] = run;
+                }
+                // exclusive prefix of the lane totals (<= 256 increments of <= 2^44: below 2^52, exact)
+                const double E = dsub(wave_scan_exact_d(run), run);
+                int first = kChainRowsPerLane;  // the lane's first violating row
+#pragma unroll
+                for (int r = kChainRowsPerLane - 1; r >= 0; --r) {
+                    const double Aj = dadd(A, dadd(E, L[r]));  // exact below 2^53; >= 2^53 stays
+                    const double sAj = a > 0.0 ? Aj : -Aj;
+                    if (valid[r] && (bad[r] || !(sAj > kTwo52 && sAj < kTwo53))) first = r;
+                }
+                const uint64_t vm = __ballot(first < kChainRowsPerLane);
+                const int nv = rows - i < 64 * kChainRowsPerLane ? rows - i : 64 * kChainRowsPerLane;
+                // the accumulator after the rows before window row t (t >= 1), and row t's increment
+                auto after = [&](int t) {
+                    const int ln = (t - 1) / kChainRowsPerLane, r = (t - 1) % kChainRowsPerLane;
+                    double pick = L[0];
+#pragma unroll
+                    for (int u = 1; u < kChainRowsPerLane; ++u) pick = r == u ? L[u] : pick;
+                    return ldexp(dadd(A, dadd(readlane_d(E, ln), readlane_d(pick, ln))), -sh);
+                };
                 if (vm == 0) {
-                    a = ldexp(readlane_d(Aj, nv - 1), -sh);
+                    a = after(nv);
                     i += nv;
                 } else {
-                    const int j0 = __builtin_amdgcn_readfirstlane(__ffsll((unsigned long long)vm) - 1);
-                    if (j0 > 0) a = ldexp(readlane_d(Aj, j0 - 1), -sh);
-                    a = dadd(a, readlane_d(v, j0));  // the violating row: the sequential add itself
+                    const int ln = __builtin_amdgcn_readfirstlane(__ffsll((unsigned long long)vm) - 1);
+                    const int rv = __builtin_amdgcn_readlane(first, ln);
+                    const int j0 = kChainRowsPerLane * ln + rv;
+                    if (j0 > 0) a = after(j0);
+                    double vj = v[0];
+#pragma unroll
+                    for (int u = 1; u < kChainRowsPerLane; ++u) vj = rv == u ? v[u] : vj;
+                    a = dadd(a, readlane_d(vj, ln));  // the violating row: the sequential add itself
                     i += j0 + 1;
                     if (j0 < kChainMinRun) forced = kChainSeqRun;
                 }

@@ -358,6 +358,19 @@ __device__ __forceinline__ double unordkey(uint64_t k)
 
 
 // ------------------------------------------------------------------ preprocess
+// LIDAR_PRE_DIAG builds (tools/micro/pre_phases.py only): shader-clock stamps of the sections
+// A..I into the frame's scalars 48..57 (cycles since the kernel start)
+#ifdef LIDAR_PRE_DIAG
+#define PRE_STAMP(k)                                                                   \
+    do {                                                                               \
+        __syncthreads();                                                               \
+        if (threadIdx.x == 0) S[48 + (k)] = (double)(clock64() - pre_t0);              \
+    } while (0)
+#else
+#define PRE_STAMP(k) \
+    do {             \
+    } while (0)
+#endif
 __global__ __launch_bounds__(kT) void preprocess_kernel(const double *__restrict__ xyz_in, int64_t n_in,
                                                         uint8_t *__restrict__ mask_in,
                                                         double *__restrict__ colors_in,
@@ -378,11 +391,15 @@ __global__ __launch_bounds__(kT) void preprocess_kernel(const double *__restrict
     double *sc = fm.ws(sc_in);
     int32_t *ng_pos = fm.ws(ng_pos_in);
     double *S = fm.scal(S_in);
+#ifdef LIDAR_PRE_DIAG
+    const long long pre_t0 = clock64();
+#endif
     if (n == 0) {  // an empty frame of a batch: the reference raises ValueError (status 2)
         if (tid == 0) S[S_STATUS] = 2.0;
         return;
     }
 
+    PRE_STAMP(0);
     // ---- A: colours over ALL points (data_processing.py:143-147)
     double lo = INFINITY, hi = -INFINITY;
     for (int64_t i = tid; i < n; i += kT) {
@@ -393,6 +410,7 @@ __global__ __launch_bounds__(kT) void preprocess_kernel(const double *__restrict
     const double zmin = block_min(s, lo), zmax = block_max(s, hi);
     const double denom = dadd(dsub(zmax, zmin), 1e-10);
 
+    PRE_STAMP(1);
     // ---- B: mean / std with numpy's sequential axis-0 sums (:151-152)
     {
         double sum = 0.0, unused = 0.0;
@@ -418,6 +436,7 @@ __global__ __launch_bounds__(kT) void preprocess_kernel(const double *__restrict
         S[S_STD + tid] = s.bc[3 + tid];
     }
 
+    PRE_STAMP(2);
     // ---- C: strict 3-sigma mask, order-preserving compaction (:155-157)
     int64_t nin = 0;
     for (int64_t b0 = 0; b0 < n; b0 += kT) {
@@ -459,6 +478,7 @@ __global__ __launch_bounds__(kT) void preprocess_kernel(const double *__restrict
     __threadfence_block();
     __syncthreads();
 
+    PRE_STAMP(3);
     // ---- D: z threshold = np.percentile(z, 30) 'linear' (:164)
     const double q = ddiv(30.0, 100.0);
     const double v = dmul((double)(nin - 1), q);
@@ -476,27 +496,62 @@ __global__ __launch_bounds__(kT) void preprocess_kernel(const double *__restrict
         // (select reads comp[3*i+2] through a small lambda-free loop)
         uint64_t pre[2] = {0, 0};
         int64_t kk[2] = {klo, khi};
+        // per-wave histograms (16 waves x 2 targets x 256 bins) in the chain staging memory, idle
+        // here: the early digits of a coordinate column share a few values, and one shared
+        // histogram serialised every wave's atomics on them
+        unsigned *wh = reinterpret_cast<unsigned *>(&st.v[0][0]);
+        static_assert(sizeof(SeqStage) >= kW * 2 * 256 * sizeof(unsigned), "per-wave histograms");
+        const int lane = tid & 63, wave = tid >> 6;
         for (int pass = 0; pass < 8; ++pass) {
             const int shift = 56 - 8 * pass;
-            for (int i = tid; i < 512; i += kT) (&s.hist[0][0])[i] = 0;
+            for (int i = tid; i < kW * 2 * 256; i += kT) wh[i] = 0;
             __syncthreads();
+            unsigned *mine = wh + wave * 2 * 256;
             for (int64_t i = tid; i < nin; i += kT) {
                 const uint64_t key = ordkey(comp[3 * i + 2]);
                 const uint64_t hk = pass == 0 ? 0 : key >> (shift + 8);
                 const unsigned dig = (unsigned)(key >> shift) & 255u;
-                if (hk == pre[0]) atomicAdd(&s.hist[0][dig], 1u);
-                if (hk == pre[1]) atomicAdd(&s.hist[1][dig], 1u);
+                if (hk == pre[0]) atomicAdd(&mine[dig], 1u);
+                if (hk == pre[1]) atomicAdd(&mine[256 + dig], 1u);
             }
             __syncthreads();
-            if (tid < 2) {
-                int64_t cum = 0;
-                int d = 0;
-                for (; d < 256; ++d) {
-                    if (cum + s.hist[tid][d] > kk[tid]) break;
-                    cum += s.hist[tid][d];
+            if (tid < 512) {
+                unsigned sum = 0;
+                for (int w = 0; w < kW; ++w) sum += wh[w * 512 + tid];
+                (&s.hist[0][0])[tid] = sum;
+            }
+            __syncthreads();
+            if (wave < 2) {  // wave r selects target r: the first bin whose running count passes kk[r]
+                const int r = wave;
+                unsigned h[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) h[j] = s.hist[r][4 * lane + j];
+                const int64_t loc = (int64_t)h[0] + h[1] + h[2] + h[3];
+                int64_t incl = loc;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const int64_t t = __shfl_up(incl, o, 64);
+                    if (lane >= o) incl += t;
                 }
-                s.d[4 + tid][0] = __longlong_as_double((long long)((pre[tid] << 8) | (uint64_t)d));
-                s.d[4 + tid][1] = __longlong_as_double((long long)(kk[tid] - cum));
+                int64_t cum = incl - loc;
+                int d = -1;
+                int64_t before = 0;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    if (d < 0 && cum + h[j] > kk[r]) {
+                        d = 4 * lane + j;
+                        before = cum;
+                    }
+                    cum += h[j];
+                }
+                const uint64_t hit = __ballot(d >= 0);
+                const int wl = hit ? __ffsll((unsigned long long)hit) - 1 : 63;
+                const int dsel = hit ? __shfl(d, wl, 64) : 256;
+                const int64_t bsel = hit ? __shfl(before, wl, 64) : __shfl(cum, 63, 64);
+                if (lane == 0) {
+                    s.d[4 + r][0] = __longlong_as_double((long long)((pre[r] << 8) | (uint64_t)dsel));
+                    s.d[4 + r][1] = __longlong_as_double((long long)(kk[r] - bsel));
+                }
             }
             __syncthreads();
             for (int r = 0; r < 2; ++r) {
@@ -513,6 +568,7 @@ __global__ __launch_bounds__(kT) void preprocess_kernel(const double *__restrict
     double zt = dadd(za, dmul(diff, t));
     if (t >= 0.5) zt = dsub(zb, dmul(diff, dsub(1.0, t)));
 
+    PRE_STAMP(4);
     // ---- E: ground count and plane (:165-183)
     double cnt = 0, sx = 0, sy = 0, sz = 0, imin[3] = {INFINITY, INFINITY, INFINITY},
            imax[3] = {-INFINITY, -INFINITY, -INFINITY};
@@ -610,6 +666,7 @@ __global__ __launch_bounds__(kT) void preprocess_kernel(const double *__restrict
         S[S_PLANE_KIND] = pkind;
     }
 
+    PRE_STAMP(5);
     // ---- F: non-ground compaction (:186)
     int64_t nng = 0;
     for (int64_t b0 = 0; b0 < nin; b0 += kT) {
@@ -649,6 +706,7 @@ __global__ __launch_bounds__(kT) void preprocess_kernel(const double *__restrict
         return;
     }
 
+    PRE_STAMP(6);
     // ---- G: StandardScaler fit (sklearn _incremental_mean_and_var, zero prior) (:190-191)
     {
         const double nn = (double)nng;
@@ -684,6 +742,7 @@ __global__ __launch_bounds__(kT) void preprocess_kernel(const double *__restrict
         S[S_SMEAN + tid] = smean[tid];
         S[S_SSCALE + tid] = sscale[tid];
     }
+    PRE_STAMP(7);
     // ---- H: transform (X -= mean_; X /= scale_) and bbox of the scaled cloud
     double slo[3] = {INFINITY, INFINITY, INFINITY}, shi[3] = {-INFINITY, -INFINITY, -INFINITY};
     for (int64_t i = tid; i < nng; i += kT)
@@ -700,6 +759,7 @@ __global__ __launch_bounds__(kT) void preprocess_kernel(const double *__restrict
     }
     __threadfence_block();
     __syncthreads();
+    PRE_STAMP(8);
     // ---- I: eps = max(0.2, min(0.5, mean(std(scaled, axis=0)) * 0.5)) (:194-195)
     {
         const double nn = (double)nng;
@@ -725,6 +785,7 @@ __global__ __launch_bounds__(kT) void preprocess_kernel(const double *__restrict
             S[S_SHI + c] = bhi[c];
         }
     }
+    PRE_STAMP(9);
 }
 
 // ------------------------------------------------------------------ DBSCAN

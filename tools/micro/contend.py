@@ -1,0 +1,74 @@
+"""Main chain (the MFMA levels of one 128-frame group, forward_from_sa1_fps) alone and beside synthetic
+side loads: `chase` (dependent L2-missing loads, ~no CU footprint) and `occupy` (FPS-sized workgroups
+that only sleep), and beside real SA1 FPS launches.  usage: python tools/micro/contend.py"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+from lidar_ai_recommendation_software_amd import pointnet2 as pn  # noqa: E402
+from lidar_ai_recommendation_software_amd.synthetic import unit_frames  # noqa: E402
+
+lib = ctypes.CDLL(os.path.join(HERE, "libcontend.so"))
+lib.contend_chase.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+lib.contend_occupy.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+dev = torch.device("cuda:0")
+F, N = 128, 65536
+bb = pn.PointNet2Backbone(pn.SSG, device=dev, seed=0)
+x = torch.from_numpy(unit_frames(F, N, seed=3)).to(dev)
+idx, nx = pn.farthest_point_sample(x, N // 16, return_xyz=True, threads=512)
+fz = torch.empty(F, dtype=torch.int32, device=dev)
+pn.farthest_point_sample(x, N // 16, first_zero=fz, threads=512)
+n_el = 128 << 20  # 512 MB permutation
+perm = torch.from_numpy(np.random.default_rng(0).permutation(n_el).astype(np.uint32)).to(dev)
+sink = torch.zeros(4, dtype=torch.float32, device=dev)
+side = torch.cuda.Stream(device=dev)
+xs2 = [torch.from_numpy(unit_frames(F, N, seed=10 + s)).to(dev) for s in range(2)]
+torch.cuda.synchronize()
+
+
+def main_ms(reps=6):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    bb.forward_from_sa1_fps(x, idx, nx, fz, None)
+    e0.record()
+    for _ in range(reps):
+        bb.forward_from_sa1_fps(x, idx, nx, fz, None)
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def with_side(launch):
+    torch.cuda.synchronize()
+    with torch.cuda.stream(side):
+        launch()
+    t = main_ms()
+    torch.cuda.synchronize()
+    return t
+
+
+alone = main_ms()
+print(f"main chain alone                         {alone:7.2f} ms")
+for blocks in (128, 256, 512):
+    t = with_side(lambda: lib.contend_chase(ctypes.c_void_p(perm.data_ptr()), blocks, 60000,
+                                            ctypes.c_void_p(sink.data_ptr()), ctypes.c_void_p(side.cuda_stream)))
+    print(f"beside chase ({blocks:3d} one-wave workgroups)   {t:7.2f} ms")
+for variant, what in ((0, "64 VGPRs + 17 KiB LDS"), (1, "few VGPRs + 17 KiB LDS"), (2, "64 VGPRs, no LDS")):
+    for blocks in (256, 384):
+        t = with_side(lambda: lib.contend_occupy(blocks, 60000, ctypes.c_void_p(sink.data_ptr()),
+                                                 ctypes.c_void_p(side.cuda_stream), variant))
+        print(f"beside occupy ({blocks:3d} x 512 threads, {what:22s}) {t:7.2f} ms")
+
+
+sides = [torch.cuda.Stream(device=dev) for _ in range(3)]
+torch.cuda.synchronize()
+for k, st in enumerate(sides):  # three concurrent FPS launches, as the pipeline's side streams
+    with torch.cuda.stream(st):
+        pn.farthest_point_sample(xs2[k % 2], N // 16, threads=512, slot=1 + k)
+t = main_ms()
+torch.cuda.synchronize()
+print(f"beside 3 x 128-frame SA1 FPS launches    {t:7.2f} ms")

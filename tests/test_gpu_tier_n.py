@@ -501,6 +501,42 @@ def bf16_close(got, want, what=""):
     assert err.max() <= 2e-2 * scale, f"{what}: max err {err.max():.3e} vs rms {scale:.3e}"
 
 
+def _bf16_monotone(t):
+    """bf16 RNE of float32 RNE of float64 t: monotone, and equal to the kernel's bf16 rounding on
+    every float32 value."""
+    return tier_n.bf16_round(np.asarray(t, dtype=np.float64).astype(np.float32)).astype(np.float64)
+
+
+def x1_forward_bound(rows, layers, group):
+    """The bf16 spec (X1) of a grouped MLP + max-pool with a rigorous per-element error bound.
+
+    Layer by layer, with e the bound on |kernel input - oracle input| (0 for the grouped rows,
+    computed identically on both sides):
+      * the kernel's bf16(x^) and the oracle's bf16(x) differ by at most
+        d = bf16(x + e) - bf16(x - e) (RNE is monotone; 0 when the interval rounds to one value);
+      * both accumulate exact bf16 x bf16 products in fp32 (kernel: MFMA order; oracle: float64
+        then one rounding), each within (K + 2) 2^-24 sum|products| + 2^-24 |sum| of the exact sum;
+      * bias add (one fp32 rounding each) and ReLU / max-pool (1-Lipschitz).
+    Returns (oracle output, bound), both (R / group, Cout) float64."""
+    u = 2.0 ** -24
+    h = np.asarray(rows, dtype=np.float32).astype(np.float64)
+    e = np.zeros_like(h)
+    for W, b in layers:
+        Wb = tier_n.bf16_round(W).astype(np.float64)
+        hb = _bf16_monotone(h)
+        up = np.nextafter(h + e, np.inf)
+        dn = np.nextafter(h - e, -np.inf)
+        d = np.where(e > 0, _bf16_monotone(up) - _bf16_monotone(dn), 0.0)
+        acc = hb @ Wb
+        K = Wb.shape[0]
+        mag = (np.abs(hb) + d) @ np.abs(Wb)
+        y = np.maximum(acc.astype(np.float32) + b.astype(np.float32), np.float32(0)).astype(np.float64)
+        e = d @ np.abs(Wb) + 2 * (K + 2) * u * mag + 4 * u * (np.abs(acc) + np.abs(b))
+        h = y
+    R, C = h.shape
+    return h.reshape(-1, group, C).max(axis=1), e.reshape(-1, group, C).max(axis=1)
+
+
 @pytest.mark.parametrize("cfg_name,level,branch", [("msg", 0, 0), ("msg", 0, 1), ("msg", 0, 2), ("msg", 1, 0),
                                                    ("msg", 1, 1), ("msg", 1, 2), ("ssg", 0, 0), ("ssg", 1, 0)])
 def test_group_mlp_x1(cuda, cfg_name, level, branch):
@@ -544,6 +580,12 @@ def test_group_mlp_x1(cuda, cfg_name, level, branch):
         fin = None if f is None else tier_n.bf16_round(f[bi])
         want = tier_n.mlp_maxpool(tier_n.group(x[bi], fin, c[bi], gi[bi]), layers, ns, bf16=True)
         bf16_close(got[bi], want, f"x1 {cfg_name} L{level} br{branch} frame {bi}")
+        if cfeat == 0:  # xyz levels: every element within its rigorous forward error bound
+            want_b, bound = x1_forward_bound(tier_n.group(x[bi], None, c[bi], gi[bi]), layers, ns)
+            assert np.array_equal(want_b.astype(np.float32), want)
+            err = np.abs(got[bi].astype(np.float64) - want_b)
+            worst = float(np.max(err - bound))
+            assert worst <= 0.0, f"x1 {cfg_name} L{level} br{branch} frame {bi}: {worst:.3e} over the bound"
 
 
 @pytest.mark.parametrize("cfg_name,n", [("msg", 16384), ("ssg", 16384), ("msg", 131072)])

@@ -134,6 +134,29 @@ def check(rc, what):
         raise LidarError(f"{what} failed ({rc}: {LIDAR_ERRORS.get(rc, '?')}): {msg}")
 
 
+def grid_dims(x_min, x_max, y_min, y_max, grid_size):
+    """(nx, ny) of calculate_grid_density's grid (lidar_grid_dims: np.arange's length of the
+    margin-padded edges, utils/data_processing.py:305-313).  A grid numpy could never allocate
+    (more than 2^40 cells, or more cells than the device has free memory for) raises MemoryError,
+    as the reference's np.arange / np.histogram2d do (a frame 1e12 m wide)."""
+    nx, ny = I64(0), I64(0)
+    rc = load_library().lidar_grid_dims(float(x_min), float(x_max), float(y_min), float(y_max),
+                                        float(grid_size), ctypes.byref(nx), ctypes.byref(ny))
+    if rc == -3:
+        raise MemoryError(f"Unable to allocate a density grid for x in [{x_min}, {x_max}], "
+                          f"y in [{y_min}, {y_max}] at grid size {grid_size}")
+    check(rc, "lidar_grid_dims")
+    nx, ny = nx.value, ny.value
+    import torch
+    if torch.cuda.is_available():
+        free, _ = torch.cuda.mem_get_info()
+        need = 8 * (4 * nx * ny + nx + ny + 64)
+        if need > free:
+            raise MemoryError(f"Unable to allocate {need / 2**30:.1f} GiB for an array with shape "
+                              f"({nx}, {ny}) and data type float64")
+    return nx, ny
+
+
 def handle(device=None, slot=0):
     """The calling thread's handle for `device` (default: torch's current device).
 

@@ -3,8 +3,8 @@
 // Replaces, kernel for kernel:
 //   preprocess_kernel  utils/data_processing.py:143-195 — height colours, 3-sigma filter
 //                      (numpy sequential axis-0 sums), 30th-percentile ground split
-//                      (radix select + numpy's _lerp), ground plane (normal equations;
-//                      LAPACK gelsd is not bit-reproducible, parity 1e-9 rel), StandardScaler
+//                      (radix select + numpy's _lerp), ground plane (TSQR + Jacobi SVD with gelsd's
+//                      rank rule; gelsd is not bit-reproducible, see plane_solve), StandardScaler
 //                      (sklearn's corrected two-pass variance, near-constant mask), eps heuristic.
 //   dbscan_*           data_processing.py:197 sklearn DBSCAN(eps, min_samples=5):
 //                      counting-sort voxel hash (cells > eps, 27-cell stencil), fp64
@@ -345,6 +345,132 @@ __device__ void block_sum_chain(const double *x, int64_t n, SeqStage &st, BlockS
     __syncthreads();
 }
 
+// ---- ground plane: numpy.linalg.lstsq(A, z, rcond=None), A = [x y 1] (data_processing.py:171-177)
+// LAPACK gelsd returns the minimum-norm least-squares solution of A's SVD truncated at
+// rcond = eps * max(M, 3): singular values s_i <= rcond * s_1 count as zero.  That decision is what
+// makes a frame far from the origin (|x| ~ 1e12 with a unit spread) or at tiny magnitudes (1e-140)
+// rank-deficient, and the truncated solution differs there from the plain least-squares plane.
+// The device reproduces the decision and the solution: (1) a Givens QR of the centred rows
+// w = [(x - mx) sx, (y - my) sx, 1, (z - mz) sz] (sx, sz powers of two: no overflow, exact
+// unscaling), per thread over its rows, then merged as a fixed tree (TSQR); (2) since
+// [x y 1] = [x - mx, y - my, 1] T with T = [[1,0,0],[0,1,0],[mx,my,1]], A = Q (R3 T) and Q^T z =
+// R[:3,3] + mz R[:3,2], so A's singular values and the solution are those of the 3x3 system
+// B = R3 T, c; (3) one-sided Jacobi SVD of B (high relative accuracy), the same rank rule, and
+// x = sum over the kept i of v_i (u_i . c) / s_i.  The centring perturbs A far less than gelsd's own
+// backward error, so the result agrees with gelsd to ~eps * s_1 / s_rank relative (both are
+// backward-stable solvers of the same truncated problem); tests/test_gpu_tier_r.py states that
+// tolerance.  Row 3 of R (the residual) is not needed and not formed.
+__device__ __forceinline__ constexpr int plane_ro(int k) { return k == 0 ? 0 : k == 1 ? 4 : k == 2 ? 7 : 9; }
+template <int K0>
+__device__ __forceinline__ void plane_row(double (&r)[10], double (&w)[4])
+{
+#pragma unroll
+    for (int k = K0; k < 3; ++k) {
+        const double a = r[plane_ro(k)], b = w[k];
+        const double h = __dsqrt_rn(dadd(dmul(a, a), dmul(b, b)));
+        const bool skip = b == 0.0 || h == 0.0;  // h == 0: b's square underflowed (negligible)
+        const double inv = skip ? 0.0 : ddiv(1.0, h);
+        const double c = skip ? 1.0 : dmul(a, inv), s = skip ? 0.0 : dmul(b, inv);
+        r[plane_ro(k)] = skip ? a : h;
+#pragma unroll
+        for (int j = k + 1; j < 4; ++j) {
+            const double t = r[plane_ro(k) + j - k];
+            r[plane_ro(k) + j - k] = dadd(dmul(c, t), dmul(s, w[j]));
+            w[j] = dsub(dmul(c, w[j]), dmul(s, t));
+        }
+    }
+}
+__device__ __forceinline__ void plane_merge(double (&r)[10], const double (&p)[10])
+{
+    double w0[4] = {p[0], p[1], p[2], p[3]};
+    plane_row<0>(r, w0);
+    double w1[4] = {0.0, p[4], p[5], p[6]};
+    plane_row<1>(r, w1);
+    double w2[4] = {0.0, 0.0, p[7], p[8]};
+    plane_row<2>(r, w2);
+}
+// the truncated minimum-norm solution from the merged R (one thread); returns the rank
+__device__ int plane_solve(const double (&r)[10], double sx_inv_exp, double sz_inv_exp, double mx, double my,
+                           double mz, double m_rows, double (&x)[3])
+{
+    auto R = [&](int i, int j) { return j < i ? 0.0 : r[plane_ro(i) + j - i]; };
+    const int ex = (int)sx_inv_exp, ez = (int)sz_inv_exp;
+    double B[3][3], c[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        B[i][0] = dadd(ldexp(R(i, 0), ex), dmul(R(i, 2), mx));
+        B[i][1] = dadd(ldexp(R(i, 1), ex), dmul(R(i, 2), my));
+        B[i][2] = R(i, 2);
+        c[i] = dadd(ldexp(R(i, 3), ez), dmul(mz, R(i, 2)));
+    }
+    double bm = 0.0;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) bm = fmax(bm, fabs(B[i][j]));
+    int eb = 0;
+    if (bm > 0.0 && bm < INFINITY) (void)frexp(bm, &eb);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        c[i] = ldexp(c[i], -eb);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) B[i][j] = ldexp(B[i][j], -eb);
+    }
+    double V[3][3] = {{1.0, 0.0, 0.0}, {0.0, 1.0, 0.0}, {0.0, 0.0, 1.0}};
+    constexpr double kEps = 2.220446049250313e-16;  // numpy.finfo(float64).eps
+    for (int sweep = 0; sweep < 40; ++sweep) {
+        bool rot = false;
+#pragma unroll
+        for (int pq = 0; pq < 3; ++pq) {
+            const int p = pq == 2 ? 1 : 0, q = pq == 0 ? 1 : 2;
+            double al = 0.0, be = 0.0, ga = 0.0;
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                al = dadd(al, dmul(B[i][p], B[i][p]));
+                be = dadd(be, dmul(B[i][q], B[i][q]));
+                ga = dadd(ga, dmul(B[i][p], B[i][q]));
+            }
+            if (ga == 0.0 || fabs(ga) <= dmul(kEps, dmul(__dsqrt_rn(al), __dsqrt_rn(be)))) continue;
+            rot = true;
+            const double zeta = ddiv(dsub(be, al), dmul(2.0, ga));
+            const double t = fabs(zeta) > 1e150 ? ddiv(0.5, zeta)
+                                                : ddiv(copysign(1.0, zeta),
+                                                       dadd(fabs(zeta), __dsqrt_rn(dadd(1.0, dmul(zeta, zeta)))));
+            const double cs = ddiv(1.0, __dsqrt_rn(dadd(1.0, dmul(t, t)))), sn = dmul(cs, t);
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                const double bp = B[i][p], bq = B[i][q];
+                B[i][p] = dsub(dmul(cs, bp), dmul(sn, bq));
+                B[i][q] = dadd(dmul(sn, bp), dmul(cs, bq));
+                const double vp = V[i][p], vq = V[i][q];
+                V[i][p] = dsub(dmul(cs, vp), dmul(sn, vq));
+                V[i][q] = dadd(dmul(sn, vp), dmul(cs, vq));
+            }
+        }
+        if (!rot) break;
+    }
+    double s2[3], sv[3], smax = 0.0;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        s2[k] = dadd(dadd(dmul(B[0][k], B[0][k]), dmul(B[1][k], B[1][k])), dmul(B[2][k], B[2][k]));
+        sv[k] = __dsqrt_rn(s2[k]);
+        smax = fmax(smax, sv[k]);
+    }
+    const double tol = dmul(dmul(kEps, fmax(m_rows, 3.0)), smax);  // numpy: rcond = eps * max(M, N)
+    int rank = 0;
+    x[0] = x[1] = x[2] = 0.0;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const bool keep = sv[k] > tol;
+        rank += keep ? 1 : 0;
+        const double coef = keep ? ddiv(dadd(dadd(dmul(B[0][k], c[0]), dmul(B[1][k], c[1])), dmul(B[2][k], c[2])), s2[k])
+                                 : 0.0;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) x[i] = keep ? dadd(x[i], dmul(V[i][k], coef)) : x[i];
+    }
+    return rank;
+}
+
 __device__ __forceinline__ uint64_t ordkey(double v)
 {
     uint64_t u = (uint64_t)__double_as_longlong(v);
@@ -599,61 +725,51 @@ __global__ __launch_bounds__(kT) void preprocess_kernel(const double *__restrict
     if (nground > 10) {
         const double mx = block_sum(s, sx, 1) / ng, my = block_sum(s, sy, 2) / ng,
                      mz = block_sum(s, sz, 3) / ng;
-        // centred coordinates times one power of two (2^-e, e = the exponent of the largest inlier
-        // extent): exact scaling, so the slopes are those of the unscaled system bit for bit, but
-        // the moments and det neither underflow (|x| ~ 1e-140) nor overflow (|x| ~ 1e150)
-        const double ext = fmax(fmax(dmax[0] - dmin[0], dmax[1] - dmin[1]), dmax[2] - dmin[2]);
-        int ee = 0;
-        if (ext > 0.0 && ext < INFINITY) (void)frexp(ext, &ee);
-        const double sc = ldexp(1.0, -ee);
-        double axx = 0, axy = 0, ayy = 0, axz = 0, ayz = 0;
+        // TSQR of the centred, power-of-two-scaled rows (see plane_solve): |w| < 1 per entry
+        int exy = 0, ezz = 0;
+        const double extxy = fmax(dmax[0] - dmin[0], dmax[1] - dmin[1]), extz = dmax[2] - dmin[2];
+        if (extxy > 0.0 && extxy < INFINITY) (void)frexp(extxy, &exy);
+        if (extz > 0.0 && extz < INFINITY) (void)frexp(extz, &ezz);
+        double r[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
         for (int64_t i = tid; i < nin; i += kT) {
             const double pz = comp[3 * i + 2];
             if (pz <= zt) {
-                const double dx = (comp[3 * i] - mx) * sc, dy = (comp[3 * i + 1] - my) * sc, dz = (pz - mz) * sc;
-                axx += dx * dx;
-                axy += dx * dy;
-                ayy += dy * dy;
-                axz += dx * dz;
-                ayz += dy * dz;
+                double w[4] = {ldexp(dsub(comp[3 * i], mx), -exy), ldexp(dsub(comp[3 * i + 1], my), -exy), 1.0,
+                               ldexp(dsub(pz, mz), -ezz)};
+                plane_row<0>(r, w);
             }
         }
-        axx = block_sum(s, axx, 0);
-        axy = block_sum(s, axy, 1);
-        ayy = block_sum(s, ayy, 2);
-        axz = block_sum(s, axz, 3);
-        ayz = block_sum(s, ayz, 0);
-        const double det = axx * ayy - axy * axy;
-        if (det != 0.0) {
-            const double a = (axz * ayy - ayz * axy) / det, b = (axx * ayz - axy * axz) / det;
-            plane[0] = a;
-            plane[1] = b;
-            plane[2] = -1.0;
-            plane[3] = mz - a * mx - b * my;
-            pkind = 0.0;
-        } else {
-            // rank-deficient (collinear) ground: pseudo-inverse of the centred 2x2 normal
-            // system M = [[axx, axy], [axy, ayy]] (rank 1: eigenvector (axx, axy), eigenvalue tr),
-            // pinv(M) r = (axx, axy) (axx axz + axy ayz) / (axx tr^2) — gelsd's minimum-norm
-            // answer is reproduced only approximately here
-            const double tr = axx + ayy;
-            double a = 0.0, b = 0.0;
-            if (tr > 0.0) {
-                const double k = (axz * axx + ayz * axy) / (tr * tr);
-                a = k;
-                b = axx != 0.0 ? k * axy / axx : 0.0;
-                if (axx == 0.0) {
-                    const double k2 = ayz / ayy;
-                    a = 0.0;
-                    b = k2;
-                }
-            }
-            plane[0] = a;
-            plane[1] = b;
-            plane[2] = -1.0;
-            plane[3] = mz - a * mx - b * my;
-            pkind = 2.0;
+        for (int m = 1; m < 64; m <<= 1) {  // fixed butterfly: lane 0 ends with the wave's R
+            double p[10];
+#pragma unroll
+            for (int k = 0; k < 10; ++k) p[k] = __shfl_xor(r[k], m, 64);
+            plane_merge(r, p);
         }
+        __syncthreads();  // st is free between the chains; its first 160 doubles hold the waves' R
+        if ((tid & 63) == 0)
+#pragma unroll
+            for (int k = 0; k < 10; ++k) st.v[0][(tid >> 6) * 10 + k] = r[k];
+        __syncthreads();
+        if (tid < 64) {
+#pragma unroll
+            for (int k = 0; k < 10; ++k) r[k] = tid < kW ? st.v[0][tid * 10 + k] : 0.0;
+            for (int m = 1; m < kW; m <<= 1) {
+                double p[10];
+#pragma unroll
+                for (int k = 0; k < 10; ++k) p[k] = __shfl_xor(r[k], m, 64);
+                plane_merge(r, p);
+            }
+            if (tid == 0) {
+                double x[3];
+                const int rank = plane_solve(r, (double)exy, (double)ezz, mx, my, mz, ng, x);
+                plane[0] = x[0];
+                plane[1] = x[1];
+                plane[2] = -1.0;
+                plane[3] = x[2];
+                pkind = rank == 3 ? 0.0 : 2.0;
+            }
+        }
+        __syncthreads();
     }
     if (tid == 0) {
         S[S_ZT] = zt;
@@ -1927,7 +2043,12 @@ LIDAR_EXPORT int lidar_grid_dims(double xmin, double xmax, double ymin, double y
     const double x0 = xmin - m, x1 = (xmax + m) + grid;
     const double y0 = ymin - m, y1 = (ymax + m) + grid;
     const double lx = std::ceil((x1 - x0) / grid), ly = std::ceil((y1 - y0) / grid);
-    REQUIRE(lx >= 2 && ly >= 2 && lx < 1e8 && ly < 1e8, "lidar_grid_dims: degenerate grid");
+    REQUIRE(lx >= 2 && ly >= 2, "lidar_grid_dims: degenerate grid");
+    // more than 2^40 cells (8 TiB of float64): numpy's np.arange / histogram2d raise MemoryError
+    if (!(lx < 1e15 && ly < 1e15 && (lx - 1) * (ly - 1) <= 1099511627776.0)) {
+        lidar::set_error("lidar_grid_dims: the grid has more than 2^40 cells");
+        return LIDAR_ENOMEM;
+    }
     *nx = (int64_t)lx - 1;
     *ny = (int64_t)ly - 1;
     return LIDAR_OK;

@@ -32,7 +32,9 @@ bool parse_token(const char *p, const char *e, double *v)
     char buf[352];
     for (size_t i = 0; i < len; ++i) {
         const char c = p[i];
-        if (c == '_' || c == 'x' || c == 'X' || c == 'p' || c == 'P') return false;  // Python-only / hex forms
+        // Python-only / hex forms, and strtod's "nan(chars)", which Python's float() rejects: the
+        // caller's Python loop then reproduces what the reference does with such a row
+        if (c == '_' || c == 'x' || c == 'X' || c == 'p' || c == 'P' || c == '(') return false;
         buf[i] = c;
     }
     buf[len] = '\0';

@@ -26,14 +26,22 @@ from . import _native as nat
 # hit needs the same object AND the same bytes: the entry stores an xxh3-128 digest of the
 # array's contents, so a caller that edits pd["points"] (or the people array) in place gets
 # the edited values uploaded, as the reference would read them.  Hashing a 65 k-point frame
-# (1.5 MB) costs ~0.1 ms on the host.
+# (1.5 MB) costs ~0.1 ms on the host with xxhash (optional), ~2 ms with the standard library's
+# blake2b otherwise.
 _cache = {}
+try:
+    import xxhash as _xxhash
+except ImportError:  # xxhash is optional: the standard library's blake2b decides equally
+    _xxhash = None
 
 
 def _digest(arr):
-    import xxhash
     a = np.ascontiguousarray(arr)
-    return a.shape, a.dtype.str, xxhash.xxh3_128_intdigest(memoryview(a.reshape(-1)).cast("B"))
+    mv = memoryview(a.reshape(-1)).cast("B")
+    if _xxhash is not None:
+        return a.shape, a.dtype.str, _xxhash.xxh3_128_intdigest(mv)
+    import hashlib
+    return a.shape, a.dtype.str, hashlib.blake2b(mv, digest_size=16).digest()
 
 
 def _remember(arr, tensor):
@@ -128,14 +136,16 @@ def _pcd_body_start(lines):
 
 
 def _ply_body(lines):
+    # utils/data_processing.py:87-97: the data lines are range(start, start + (n_points or
+    # len(lines))), so an absent or zero "element vertex" count reads to the end of the file
     nvert = None
     for i, ln in enumerate(lines):
         if ln.strip() == "end_header":
             start = i + 1
-            return start, start + (nvert if nvert is not None else len(lines))
+            return start, start + (nvert or len(lines))
         if "element vertex" in ln:
             nvert = int(ln.split()[-1])
-    return 0, (nvert if nvert is not None else len(lines))
+    return 0, (nvert or len(lines))
 
 
 def _read_ascii_body(path, locate):
@@ -186,7 +196,7 @@ def _parse_fast(raw, locate):
         for ln in lines[:a]:
             if "element vertex" in ln:
                 nvert = int(ln.split()[-1])
-        max_lines = -1 if nvert is None else max(0, nvert)
+        max_lines = -1 if not nvert else max(0, nvert)  # None or 0: to the end (:97)
     pts = _parse_ascii_lines_or_none(raw, a, max_lines)
     if pts is None:
         return None
@@ -271,27 +281,23 @@ def downsample_point_cloud(points, factor=0.1):
     ``points[np.random.choice(n, max(1, int(n*factor)), replace=False)]``.
 
     The draw is the reference's own: ``np.random.choice`` on the GLOBAL legacy NumPy RNG (host
-    RNG state: identical indices, identical RNG state afterwards).  The gather runs on the GPU
-    (``lidar_gather_rows`` moves rows as raw bytes, so any dtype comes back bit for bit).  A CUDA
-    tensor in gives a CUDA tensor out (throughput mode: only the indices cross PCIe); a NumPy
-    array in gives a NumPy array out."""
+    RNG state: identical indices, identical RNG state afterwards).  A host array (or anything
+    that is not a CUDA tensor) is indexed on the host, ``points[idx]``, exactly as the reference
+    does (same result, same exceptions, e.g. TypeError for a Python list; uploading a host frame
+    to gather rows would only add two PCIe copies).  A CUDA tensor in gives a CUDA tensor out:
+    the gather runs on the GPU (``lidar_gather_rows`` moves rows as raw bytes) and only the
+    indices cross PCIe (throughput mode)."""
     if factor >= 1.0:
         return points
     num = len(points)
     keep = max(1, int(num * factor))
     idx = np.random.choice(num, keep, replace=False)
     import torch
-    if isinstance(points, torch.Tensor):
+    if isinstance(points, torch.Tensor) and points.is_cuda:
         src = points.contiguous()
         out = torch.empty((keep,) + tuple(src.shape[1:]), dtype=src.dtype, device=src.device)
         return _gather_rows(src, idx, out)
-    a = np.asarray(points)
-    if a.dtype.hasobject:  # Python object references cannot live in device memory
-        return a[idx]
-    src = torch.from_numpy(np.ascontiguousarray(a).reshape(len(a), -1).view(np.uint8)).cuda()
-    out = torch.empty((keep, src.shape[1]), dtype=torch.uint8, device=src.device)
-    _gather_rows(src, idx, out)
-    return out.cpu().numpy().view(a.dtype).reshape((keep,) + a.shape[1:])
+    return points[idx]
 
 
 def _gather_rows(src, idx, out):
@@ -331,14 +337,10 @@ def extract_people_positions(processed_data):
 
 
 def _grid(people_positions, x_range, y_range, grid_size):
-    import ctypes
     import torch
     x_min, x_max = x_range
     y_min, y_max = y_range
-    nx, ny = nat.I64(0), nat.I64(0)
-    nat.call("lidar_grid_dims", float(x_min), float(x_max), float(y_min), float(y_max), float(grid_size),
-             ctypes.byref(nx), ctypes.byref(ny))
-    nx, ny = nx.value, ny.value
+    nx, ny = nat.grid_dims(x_min, x_max, y_min, y_max, grid_size)
     p = _on_device(np.asarray(people_positions, dtype=np.float64).reshape(-1, 2), torch.float64)
     dev = p.device
     gx = torch.empty(nx, dtype=torch.float64, device=dev)

@@ -75,10 +75,7 @@ class DensityStream:
                     "grid_coordinates": (np.array([0]), np.array([0])), "density_values": np.array([0]),
                     "hotspots": []}, frame
         x_min, x_max, y_min, y_max = S[5], S[6], S[7], S[8]
-        nx, ny = nat.I64(0), nat.I64(0)
-        nat.call("lidar_grid_dims", float(x_min), float(x_max), float(y_min), float(y_max), self.grid_size,
-                 ctypes.byref(nx), ctypes.byref(ny))
-        nx, ny = nx.value, ny.value
+        nx, ny = nat.grid_dims(x_min, x_max, y_min, y_max, self.grid_size)
         m = nx * ny
         with torch.cuda.stream(s):
             gx = torch.empty(nx, dtype=torch.float64, device=self.device)
@@ -151,12 +148,16 @@ class DensityStream:
         for st in streams:
             st.wait_stream(caller)  # the frames exist on the caller's stream
 
+        people = [None] * len(batches)
+
         def work(j):
             torch.cuda.set_device(self.device)
             with torch.cuda.stream(streams[j]):
                 for i in range(j, len(batches), lanes):
                     try:
-                        out[i] = self.run_batch(batches[i])
+                        out[i] = self._run_batch(batches[i])
+                        people[i] = out[i][1]
+                        out[i] = out[i][0]
                     except Exception as e:  # reported in batch order below
                         out[i] = e
             streams[j].synchronize()
@@ -169,11 +170,14 @@ class DensityStream:
         for r in out:
             if isinstance(r, Exception):
                 raise r
+        if batches:  # the last batch in batch order, whichever lane finished last
+            self._last_people = people[-1]
         return out
 
     def people_of_last_batch(self):
-        """The people positions of every frame of the last run_batch, concatenated in frame order:
-        a (sum K_f, 2) float64 CUDA tensor (what extract_people_positions returns per frame)."""
+        """The people positions of every frame of the last batch of run_batch / run_batches (in
+        batch order), concatenated in frame order: a (sum K_f, 2) float64 CUDA tensor (what
+        extract_people_positions returns per frame)."""
         people, offs, K = self._last_people
         rows = [people[int(o):int(o) + int(k)] for o, k in zip(offs[:-1], K) if k > 0]
         return torch.cat(rows) if rows else people[:0]
@@ -182,9 +186,17 @@ class DensityStream:
         """frames: list of (n_i, 3) float64 CUDA tensors -> list of analyze results, one
         launch per phase for the whole list.  Raises the reference's exception of the first
         failing frame (ValueError empty, IndexError no inlier), like `run`."""
+        res, people = self._run_batch(frames)
+        if people is not None:
+            self._last_people = people
+        return res
+
+    def _run_batch(self, frames):
+        """run_batch's work -> (results, (people, offsets, K) or None); no shared state is
+        written, so lanes of run_batches may call it concurrently."""
         F = len(frames)
         if F == 0:
-            return []
+            return [], None
         dev = self.device
         sizes = [int(x.shape[0]) for x in frames]
         offs_h = np.zeros(F + 1, dtype=np.int64)
@@ -214,7 +226,7 @@ class DensityStream:
             if S[f, 15] != 0.0:
                 raise IndexError("index -1 is out of bounds for axis 0 with size 0")
         K = kdev.cpu().numpy()  # read-back 2
-        self._last_people = (people, offs_h, K)
+        last_people = (people, offs_h, K)
         jobs = np.zeros((F, 8), dtype=np.float64)
         out_off = scr_off = 0
         dims = []
@@ -223,10 +235,7 @@ class DensityStream:
                 dims.append(None)
                 continue
             x_min, x_max, y_min, y_max = S[f, 5], S[f, 6], S[f, 7], S[f, 8]
-            nx, ny = nat.I64(0), nat.I64(0)
-            nat.call("lidar_grid_dims", float(x_min), float(x_max), float(y_min), float(y_max), self.grid_size,
-                     ctypes.byref(nx), ctypes.byref(ny))
-            nx, ny = nx.value, ny.value
+            nx, ny = nat.grid_dims(x_min, x_max, y_min, y_max, self.grid_size)
             m = nx * ny
             g2 = self.grid_size * 2.0
             jobs[f] = (x_min - g2, y_min - g2, self.grid_size, nx, ny, out_off, scr_off, 0)
@@ -258,4 +267,4 @@ class DensityStream:
                       "max_density": np.float64(stats[0]), "density_map": dens,
                       "grid_coordinates": (flat_x, flat_y), "density_values": flat,
                       "hotspots": [{"x": flat_x[i], "y": flat_y[i], "density": flat[i]} for i in hot]}
-        return res
+        return res, last_people

@@ -12,7 +12,6 @@ by one RCCL all-reduce (``torch.distributed`` backend "nccl" = RCCL over xGMI on
 nx*ny*4-byte message, 4.6 KB for a 34 x 34 venue: latency-bound), ``density()`` equals
 ``calculate_grid_density(all those people, x_range, y_range, grid_size)[2]`` bit for bit.
 """
-import ctypes
 
 import numpy as np
 import torch
@@ -28,10 +27,8 @@ class VenueGrid:
         self.x_range = (float(x_range[0]), float(x_range[1]))
         self.y_range = (float(y_range[0]), float(y_range[1]))
         self.grid_size = float(grid_size)
-        nx, ny = nat.I64(0), nat.I64(0)
-        nat.call("lidar_grid_dims", self.x_range[0], self.x_range[1], self.y_range[0], self.y_range[1],
-                 self.grid_size, ctypes.byref(nx), ctypes.byref(ny))
-        self.nx, self.ny = nx.value, ny.value
+        self.nx, self.ny = nat.grid_dims(self.x_range[0], self.x_range[1], self.y_range[0], self.y_range[1],
+                                         self.grid_size)
         self.x0 = self.x_range[0] - self.grid_size * 2.0  # data_processing.py:305-309's margin
         self.y0 = self.y_range[0] - self.grid_size * 2.0
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())

@@ -133,7 +133,7 @@ def voxel_downsample_batch(xyz, voxel, slot=0):
 
 
 BQ_MODES = {"auto": 0, "scan": 1, "grid": 2}
-BQ_GRID_MIN_N = 1024  # csrc/ball_query.hip kGridMinN: "auto" bins frames of at least this many points
+BQ_GRID_MIN_N = 1024  # csrc/bq_grid.hpp kGridMinN: "auto" bins frames of at least this many points
 
 
 def ball_query(radius, nsample, xyz, new_xyz, out=None, slot=0, mode="auto", grid=None):
@@ -171,8 +171,6 @@ def ball_query_bin(radius, nsample, xyz, grid, slot=0):
              float(radius), int(nsample), nat.ptr(grid), nat.stream_ptr())
     return grid
 
-
-BQ_GRID_MIN_N = 1024  # csrc/bq_grid.hpp kGridMinN: frames this large take the grid ball query
 
 # (xyz_level, c1, c2, c3, nsample) combinations lidar_sa_group_mlp16_f32 instantiates
 MLP16_SHAPES = {(True, 64, 64, 128, 32), (True, 32, 32, 64, 16), (True, 64, 96, 128, 128), (False, 128, 128, 256, 64),

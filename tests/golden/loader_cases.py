@@ -67,6 +67,10 @@ def _cases():
                           "4 5 6 extra tokens"] + _rows(20, 5)
     c["pcd_bad_rows"] = ("bad.pcd", _pcd(bad))
     c["pcd_crlf"] = ("crlf.pcd", _pcd(_rows(200, 6), nl="\r\n"))
+    # strtod reads "nan(1)" / "nan()", Python's float() does not: the row is the
+    # reference loop's to judge, in a small file (Python path) and past the C parser's window
+    c["pcd_nan_paren"] = ("np.pcd", _pcd(_rows(20, 18) + ["nan(1) 2 3", "1 nan() 3"] + _rows(5, 19)))
+    c["pcd_nan_paren_big"] = ("npb.pcd", _pcd(_rows(4000, 20) + ["nan(7) 2 3"] + _rows(100, 21)))
     c["pcd_nbsp"] = ("nbsp.pcd", _pcd(_rows(10, 7) + ["1.5 2.5 3.5", "7 8 9"]))
     c["pcd_binary"] = ("bin.pcd", _pcd([], data="binary") + bytes(range(256)))
     c["pcd_binary_compressed"] = ("binc.pcd", _pcd([], data="binary_compressed") + bytes(64))

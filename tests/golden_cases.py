@@ -4,7 +4,7 @@
 (captured by ``tests/golden/gen_tier_r.py``).  ``check_tier_r`` compares a
 ``(processed_data, people, analyze_result)`` triple — produced by the oracle or
 by the HIP path — against one case, byte for byte (the ground plane, which
-LAPACK's gelsd does not make bit-reproducible, to 1e-9 relative).
+LAPACK's gelsd does not make bit-reproducible, by ``check_plane``).
 """
 import hashlib
 import json
@@ -13,7 +13,8 @@ import os
 import numpy as np
 
 from lidar_ai_recommendation_software_amd.synthetic import (uniform_frame, crowd_frame,
-                                                        blob_frame, lattice_frame)
+                                                        blob_frame, lattice_frame,
+                                                        stress_frame, STRESS_KINDS)
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
@@ -46,6 +47,7 @@ FRAMES.update({
     "dup_4096": lambda: np.repeat(uniform_frame(1024, 4), 4, axis=0),
     "tight_2048": lambda: uniform_frame(2048, 9, -1.0, 1.0) * np.array([1.0, 1.0, 0.01]),
 })
+FRAMES.update({f"stress_{k}": (lambda k=k: stress_frame(k)) for k in STRESS_KINDS if k != "int_big"})
 ERROR_FRAMES = {
     "empty": lambda: np.zeros((0, 3)),
     "one": lambda: uniform_frame(1, 0),
@@ -69,7 +71,53 @@ def _same(name, got, want, what):
     assert g["sha256"] == want["sha256"], f"{name}.{what}: bytes differ"
 
 
-def check_tier_r(name, pd, people, res):
+PLANE_EPS = float(np.finfo(np.float64).eps)
+
+
+def plane_conditioning(inliers):
+    """(rank, kappa) of the reference's ground design ``[x y 1]`` (data_processing.py:164-175):
+    gelsd's rank at rcond = eps * max(M, 3), and kappa = s_1 / s_rank (None: fallback plane)."""
+    pts = np.asarray(inliers, dtype=np.float64)
+    z = pts[:, 2]
+    g = pts[z <= np.percentile(z, 30)]
+    if len(g) <= 10:
+        return None, None, None
+    a = np.column_stack((g[:, 0], g[:, 1], np.ones(len(g))))
+    s = np.linalg.svd(a, compute_uv=False)
+    rank = int(np.sum(s > PLANE_EPS * max(len(g), 3) * s[0]))
+    return rank, float(s[0] / s[rank - 1]), (a, g[:, 2])
+
+
+def check_plane(name, got, want, inliers):
+    """The ground plane vs the reference's ``lstsq(rcond=None)`` plane (data_processing.py:169-183).
+
+    gelsd is a backward-stable solver whose roundings are not reproducible, so the device (TSQR +
+    Jacobi SVD, density.hip plane_solve) and gelsd both sit within ~eps * kappa of the exact
+    (rank-truncated, minimum-norm) solution, kappa = s_1 / s_rank; ill-conditioned full-rank
+    designs add the least-squares kappa^2 tan(theta) term (measured <= 51 eps kappa on
+    ``stress_xy_line``, <= 4 elsewhere).  The contract: the same rank decision, every coefficient
+    within 1e-9 relative + 1024 eps kappa ||x||, and the residual norm within 1e-9 ||z|| (the
+    residual is well-conditioned).  Fallback planes ([0, 0, 1, -min z]) are exact.
+    """
+    got = np.asarray(got, dtype=np.float64)
+    want = np.asarray(want, dtype=np.float64)
+    rank, kappa, design = plane_conditioning(inliers)
+    if rank is None or want[2] != -1.0:
+        assert got.tobytes() == want.tobytes(), f"{name}.ground_plane (fallback): {got} != {want}"
+        return
+    assert got[2] == -1.0, f"{name}.ground_plane[2] = {got[2]}"
+    x, y = want[[0, 1, 3]], got[[0, 1, 3]]
+    tol = 1e-9 * np.abs(x) + 1024 * PLANE_EPS * kappa * np.linalg.norm(x)
+    assert np.all(np.abs(y - x) <= tol), f"{name}.ground_plane {got} vs {want} (rank {rank}, kappa {kappa:.3g})"
+    a, z = design
+    rx, ry = np.linalg.norm(a @ x - z), np.linalg.norm(a @ y - z)
+    assert abs(rx - ry) <= 1e-9 * np.linalg.norm(z), f"{name}.ground_plane residual {ry} vs {rx}"
+
+
+def check_tier_r(name, pd, people, analyze):
+    """`analyze` is a callable returning the analyze dict: where the reference's analyze raised
+    (``analyze_error``: a 1e12 m wide frame whose np.arange grid edges cannot be allocated), the
+    same exception type is required instead."""
     ent = META["cases"][name]
     key = f"{name}/clusters"
     if key in ARRAYS.files:
@@ -82,7 +130,7 @@ def check_tier_r(name, pd, people, res):
     gp = np.asarray(pd["ground_plane"])
     want_gp = np.array([float.fromhex(v) for v in ent["ground_plane"]])
     assert str(gp.dtype) == ent["ground_plane_dtype"]
-    np.testing.assert_allclose(gp, want_gp, rtol=1e-9, atol=1e-12, err_msg=f"{name}.ground_plane")
+    check_plane(name, gp, want_gp, pd["points"])
     d = pd["dimensions"]
     for k in ("x_range", "y_range", "z_range"):
         assert [float(v).hex() for v in d[k]] == ent["dims"][k], f"{name}.{k}"
@@ -90,6 +138,13 @@ def check_tier_r(name, pd, people, res):
         assert float(d[k]).hex() == ent["dims_scalar"][k], f"{name}.{k}"
     assert str(np.asarray(d["width"]).dtype) == ent["dims_dtype"]
     _same(name, people, ent["people"], "people")
+    if "analyze_error" in ent:
+        try:
+            analyze()
+        except MemoryError:
+            return
+        raise AssertionError(f"{name}: analyze must raise {ent['analyze_error']} as the reference does")
+    res = analyze()
     assert res["total_people"] == ent["total_people"]
     assert float(res["avg_density"]).hex() == ent["avg_density"]
     assert type(res["avg_density"]).__name__ == ent["avg_density_type"], f"{name}.avg_density type"

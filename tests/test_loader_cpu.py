@@ -108,3 +108,40 @@ def test_fast_parser_crlf_split_at_head_cut(tmp_path):
     got = dp.load_lidar_data(str(path))
     want = dp._read_ascii_body_py(text, dp._ply_body)
     assert np.array_equal(got.view(np.uint64), want.view(np.uint64))
+
+
+# ------------------------------------------------ reference-captured load_lidar_data fixtures
+import hashlib  # noqa: E402
+import json  # noqa: E402
+import os  # noqa: E402
+import sys  # noqa: E402
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+import load_cases  # noqa: E402
+
+with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "load.json")) as _f:
+    LOAD_GOLD = json.load(_f)
+
+
+def test_load_fixture_set_complete():
+    assert sorted(LOAD_GOLD) == load_cases.NAMES
+
+
+@pytest.mark.parametrize("name", load_cases.NAMES)
+def test_load_lidar_data_matches_reference(tmp_path, name):
+    """load_lidar_data (C parser + Python loop) == what the reference's load_lidar_data returned
+    on the same bytes (tests/golden/gen_load.py): PLY vertex counts of 0 / absent / negative /
+    repeated, no end_header, CRLF, face rows, PCD nan(...) tokens, CSV / XYZ / TXT / NPY."""
+    fname, data = load_cases.build(name)
+    path = tmp_path / (name + "_" + fname)
+    path.write_bytes(data)
+    want = LOAD_GOLD[name]
+    if want["ok"]:
+        a = np.ascontiguousarray(dp.load_lidar_data(str(path)))
+        assert list(a.shape) == want["shape"] and str(a.dtype) == want["dtype"]
+        assert hashlib.sha256(a.tobytes()).hexdigest() == want["sha256"]
+    else:
+        with pytest.raises(Exception) as ei:
+            dp.load_lidar_data(str(path))
+        assert type(ei.value).__name__ == want["type"]
+        assert str(ei.value).replace(str(path), "<path>") == want["message"]

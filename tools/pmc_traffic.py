@@ -1,20 +1,30 @@
-"""Reduce rocprofv3 --pmc passes of bench.py to memory-side bytes per launch per kernel.
+"""Reduce rocprofv3 --pmc passes of bench.py to memory-side bytes per frame per kernel.
 
-Input: the FETCH_SIZE and WRITE_SIZE counter CSVs of `tools/pmc_passes.sh` (one pass per
-counter, `--kernel-trace` only beside `--pmc`) plus its calibration passes (a 1 GiB
-device copy).  Units and the gfx950 correction follow MI355X_MICROARCH.md §HBM:
-FETCH_SIZE and WRITE_SIZE are in KiB; FETCH_SIZE reports exactly half of a wide
-coalesced read on gfx950, so it is doubled; the calibration pass checks both factors
-on this box (copy of 2^30 bytes -> expected read and write 2^30 bytes).  The counters sit
-on the L2's memory side, so Infinity-Cache hits are included: "traffic" is bytes that
-left the L2, an upper bound on HBM bytes.
+Input: the FETCH_SIZE and WRITE_SIZE counter CSVs of `tools/profile_round.sh` (one pass per
+counter, `--kernel-trace` only beside `--pmc`) plus its calibration passes (a 1 GiB device copy),
+and the bench line each pass printed (its `pipeline.frames_per_launch` F).  The passes run
+`bench.py --no-verify` at the driver's settings (--steps 20: G = 4 batches of 32 frames, 128-frame
+launches), so every library launch is a pipeline launch of F frames: the one-batch forward()
+references that the timed bench compares against are not issued.
 
-Output JSON (profiles/<round>/pmc_traffic.json): {"config": ..., "calibration": ...,
-"kernels": {label: {"fetch_bytes": F, "write_bytes": W, "traffic_bytes": F + W,
-"launches": n}}}; bench.py copies traffic_bytes into roofline["traffic"].
+Labels come from the kernel's template prefix (`label`).  Each dispatch's frames are derived from
+its Grid_Size with the launch geometry of its kernel (`frames_of`): one workgroup per frame for
+FPS and the ball-query binning, one wavefront per centre for the SA kernels and the grid query,
+128-row tiles x 128-column tiles of 256 threads for the split-plane GEMMs.  A dispatch whose
+geometry does not give exactly F frames is reported under "unmatched" and left out, so a label
+never averages launches of different sizes.  Units and the gfx950 correction follow
+MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in KiB; FETCH_SIZE reports half of a wide
+coalesced read on gfx950, so it is doubled; the calibration pass checks both factors on this box
+(copy of 2^30 bytes -> expected read and write 2^30 bytes).  The counters sit on the L2's memory
+side, so Infinity-Cache hits are included: "traffic" is bytes that left the L2, an upper bound on
+HBM bytes.
 
-usage: python tools/pmc_traffic.py gpurun_out/pmc_calib_f gpurun_out/pmc_calib_w \
-           gpurun_out/pmc_fetch gpurun_out/pmc_write profiles/<round>/pmc_traffic.json
+Output JSON (profiles/<round>/pmc_traffic.json): {"config": {..., "frames_per_launch": F},
+"calibration": ..., "kernels": {label: {"fetch_bytes", "write_bytes", "traffic_bytes" (per launch
+of F frames), "traffic_per_frame", "launches"}}, "unmatched": {...}}; bench.py scales
+traffic_per_frame to its own launches.
+
+usage: python tools/pmc_traffic.py CALIB_F CALIB_W PMC_FETCH PMC_WRITE BENCH_JSON OUT_JSON
 """
 import csv
 import glob
@@ -24,6 +34,8 @@ import sys
 from collections import defaultdict
 
 GIB = 1 << 30
+N_POINTS = 65536
+M1, M2 = N_POINTS // 16, N_POINTS // 64  # SA1 / SA2 centres per frame
 
 
 def rows(d):
@@ -33,77 +45,110 @@ def rows(d):
     return list(csv.DictReader(open(f[0])))
 
 
-FRAMES_PER_LAUNCH = 96  # bench.py defaults: 32 frames per batch x 3 batches per group (one launch per group)
+# (template prefix, label).  First match wins; the prefixes carry the template arguments that
+# tell the levels apart.  Kernels of one name that serve two levels (the ball-query binning, the
+# split-plane GEMM in mode 0) are split by `frames_of`'s geometry or by duration below.
+PREFIXES = (
+    ("fps_bucket_kernel<512,", "sa1_fps"),  # the pipeline's SA1 FPS (--fps-threads 512)
+    ("fps_bucket_kernel<1024, 1, false>", "fps_1024"),  # SA2's nested FPS (and SA1 at --fps-threads 1024)
+    ("fps_bucket_kernel<1024, 1, true>", "fps_1024"),
+    ("bq_bin_kernel", "bq_bin"),
+    ("bq_grid_kernel", "sa2_ball_query"),  # SA1's queries run inside its MLP kernel (bq="bin")
+    ("ball_query_kernel", "ball_query_scan"),
+    ("sa_x3_kernel<64, 64, 128, 32, 0, 2, false, true>", "sa1_group_mlp"),
+    ("sa_x3_kernel<64, 64, 128, 32, 0, 2, false>", "sa1_group_mlp"),
+    ("sa_x3_lean_kernel<128, 128, 256, 64,", "sa2_group_mlp"),
+    ("sa16_kernel<64, 64, 128, 32, true", "sa1_group_mlp"),
+    ("sa16_kernel<128, 128, 256, 64, false", "sa2_group_mlp"),
+    ("dense_x3s_kernel<0, true, false>", "sa2_layer1"),  # point rows and centre rows: split by grid
+    ("dense_x3s_kernel<1, true, false>", "sa3_dense1"),
+    ("dense_x3s_kernel<1, false, false>", "sa3_dense2"),
+    ("dense_x3s_kernel<2, false, false>", "sa3_dense3_pool"),
+    ("dense_x3_pack_kernel", "weight_pack"),
+    ("concat_xyz_pad_kernel", "concat"),
+    ("dense_relu_kernel", "dense_relu_fp32"),
+    ("__amd_rocclr_", "runtime_copy"),
+    ("at::native::", "torch"),
+)
 
 
-def label(name, grid, F=FRAMES_PER_LAUNCH):
-    """Kernel label of the SSG stack (N = 65536) for F frames per launch (grid = threads).
-    The split-plane GEMMs of SA2's per-point layer 1 (fp32 rows in, mode 0) and group_all's
-    layers are told apart by their template arguments <mode, fp32-input, x1>."""
-    if "fps_bucket_kernel" in name:
-        return "fps"  # split into sa1/sa2 by duration below
-    if "ball_query_kernel" in name:
-        return {F * 4096 * 8: "sa1_ball_query", F * 1024 * 8: "sa2_ball_query"}.get(grid)
-    if "bq_grid_kernel" in name:  # one wavefront per centre
-        return {F * 4096 * 64: "sa1_ball_query", F * 1024 * 64: "sa2_ball_query"}.get(grid)
-    if "bq_bin_kernel" in name:
-        return "bq_bin"  # one 1024-thread workgroup per frame: SA1 (65536 pts) vs SA2 (4096) by duration
-    # sa_x3_kernel<C1, C2, C3, NS, layer-1 mode (0 xyz, 1 pre, 2 px), R, X1, BQ> (BQ: the SA1 kernel
-    # that answers its own ball queries); sa_x3_lean_kernel<C1, C2, C3, NS> (SA2);
-    # sa16_kernel<C1, C2, C3, NS, XYZ> (the native fp32-MFMA leg)
-    if "sa_x3_kernel<64, 64, 128, 32, 0, 2, false" in name or "sa16_kernel<64, 64, 128, 32, true" in name:
-        return "sa1_group_mlp"
-    if ("sa_x3_lean_kernel<128, 128, 256, 64>" in name or "sa_x3_kernel<128, 128, 256, 64, 1, 2, false" in name
-            or "sa16_kernel<128, 128, 256, 64, false" in name):
-        return "sa2_group_mlp"
-    if "dense_x3s_kernel<" in name:  # split-plane GEMM: <mode, fp32-input, x1>
-        for key, lab in (("<0, true, false>", "sa2_layer1_points"), ("<1, true, false>", "sa3_dense1"),
-                         ("<1, false, false>", "sa3_dense2"), ("<2, false, false>", "sa3_dense3_pool")):
-            if key in name:
-                return lab
-        return None
-    if "dense_relu_kernel" in name:
-        return {F * 4096 * 2: "dense_shared", F * 1024 * 2: "sa2_layer1_points", F * 1024 * 4: "sa3_dense1",
-                F * 1024 * 16: "sa3_dense3_pool"}.get(grid)
-    if "concat_xyz_pad" in name:
-        return "concat"
+def label(name):
+    """The label of a kernel name (rocprofv3's Kernel_Name), or None."""
+    short = name.split("::", 1)[1] if name.startswith("void (anonymous namespace)::") else name
+    short = short.replace("(anonymous namespace)::", "")
+    for prefix, lab in PREFIXES:
+        if short.startswith(prefix) or (prefix.startswith("at::") and prefix in name):
+            return lab
     return None
 
 
-def per_label(rs, counter):
-    acc = defaultdict(list)
-    fps, bins = [], []
-    nsh = 0
+def _tiles(rows_per_frame, cout, F):
+    """Threads of a dense_x3s launch over F frames (128 x 128 tiles of 256 threads, grid rounded
+    up to a multiple of 8 workgroups for the XCD-affine order)."""
+    total = (F * rows_per_frame // 128) * (cout // 128)
+    return ((total + 7) // 8) * 8 * 256
+
+
+def frames_of(lab, name, grid, wg, F):
+    """(label, frames) of a dispatch when its grid is that of an F-frame pipeline launch, else
+    (label, None).  `lab` may be refined (the two GEMMs of SA2's per-point layer 1)."""
+    if lab in ("sa1_fps", "fps_1024", "bq_bin"):
+        return lab, (grid // wg if grid // wg == F else None)
+    if lab == "sa1_group_mlp":
+        return lab, (F if grid == F * M1 * 64 else None)
+    if lab == "sa2_group_mlp":
+        return lab, (F if grid == F * M2 * 64 else None)
+    if lab == "sa2_ball_query":
+        blocks = (F * M2 + 3) // 4
+        return lab, (F if grid == ((blocks + 7) // 8) * 8 * 256 else None)
+    if lab == "sa2_layer1":
+        if grid == _tiles(M1, 128, F):
+            return "sa2_layer1_points", F
+        if grid == _tiles(M2, 128, F):
+            return "sa2_layer1_centres", F
+        return lab, None
+    if lab == "sa3_dense1":
+        return lab, (F if grid == _tiles(M2, 256, F) else None)
+    if lab == "sa3_dense2":
+        return lab, (F if grid == _tiles(M2, 512, F) else None)
+    if lab == "sa3_dense3_pool":
+        return lab, (F if grid == _tiles(M2, 1024, F) else None)
+    return lab, None
+
+
+def per_label(rs, counter, F):
+    """{label: [bytes of each F-frame dispatch]} and {kernel: count} of dispatches left out."""
+    acc, unmatched = defaultdict(list), defaultdict(int)
+    by_dur = defaultdict(list)  # same geometry, two levels: split by duration
     for r in sorted(rs, key=lambda r: int(r["Dispatch_Id"])):
         if r["Counter_Name"] != counter:
             continue
         v = float(r["Counter_Value"]) * 1024.0  # KiB -> bytes
-        lab = label(r["Kernel_Name"], int(r["Grid_Size"]))
-        if lab == "fps":
-            fps.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"]), v))
-        elif lab == "bq_bin":
-            bins.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"]), v))
-        elif lab == "dense_shared":
-            acc["sa2_layer1_points" if nsh % 2 == 0 else "sa3_dense2"].append(v)
-            nsh += 1
-        elif lab:
+        name = r["Kernel_Name"]
+        lab = label(name)
+        if lab in (None, "torch", "runtime_copy", "weight_pack", "concat"):
+            unmatched[(lab or "unlabelled") + ": " + name[:80]] += 1
+            continue
+        lab, frames = frames_of(lab, name, int(r["Grid_Size"]), int(r["Workgroup_Size"]), F)
+        if frames is None:
+            unmatched[lab + ": " + name[:80]] += 1
+            continue
+        dur = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        if lab in ("fps_1024", "bq_bin"):
+            by_dur[lab].append((dur, v))
+        else:
             acc[lab].append(v)
-    if fps:  # SA1 FPS (65536 -> 4096, long) vs SA2's nested-prefix FPS (short)
-        fps.sort()
-        half = len(fps) // 2
-        acc["sa2_fps"] = [v for _, v in fps[:half]]
-        acc["sa1_fps"] = [v for _, v in fps[half:]]
-    if bins:  # SA1's binning (65536-point frames, side stream) vs SA2's (4096 points, inside its query)
-        bins.sort()
-        half = len(bins) // 2
-        acc["sa2_bq_bin"] = [v for _, v in bins[:half]]
-        acc["sa1_bq_bin"] = [v for _, v in bins[half:]]
-    # sa2_layer1_points = its two GEMMs (point rows, centre rows) per pass: report their sum
-    if "sa2_layer1_points" in acc:
-        v = acc["sa2_layer1_points"]
-        passes = max(1, len(v) // 2)
-        acc["sa2_layer1_points"] = [sum(v) / passes]
-    return acc
+    # SA2's nested FPS (prefix shortcut: microseconds) is the only 1024-thread FPS of the pipeline at
+    # --fps-threads 512; the binning runs once per level per group (SA1: 65 536-point frames, long;
+    # SA2: 4 096-point frames, short)
+    if by_dur.get("fps_1024"):
+        acc["sa2_fps"] = [v for _, v in by_dur["fps_1024"]]
+    if by_dur.get("bq_bin"):
+        b = sorted(by_dur["bq_bin"])
+        half = len(b) // 2
+        acc["sa2_bq_bin"] = [v for _, v in b[:half]]
+        acc["sa1_bq_bin"] = [v for _, v in b[half:]]
+    return acc, dict(unmatched)
 
 
 def calib(rs, counter):
@@ -112,33 +157,49 @@ def calib(rs, counter):
     return sum(v) / len(v) if v else None
 
 
-def main(cf, cw, pf, pw, out):
+def bench_frames_per_launch(path):
+    with open(path) as f:
+        line = [ln for ln in f if ln.startswith("{")][-1]
+    return int(json.loads(line)["pipeline"]["frames_per_launch"])
+
+
+def main(cf, cw, pf, pw, bench_json, out):
+    F = bench_frames_per_launch(bench_json)
     fetch_scale = 2.0  # gfx950: FETCH_SIZE = half the bytes of a wide coalesced read
     c_read, c_write = calib(rows(cf), "FETCH_SIZE"), calib(rows(cw), "WRITE_SIZE")
     cal = {"copy_bytes": GIB, "fetch_size_raw_bytes": c_read, "write_size_raw_bytes": c_write,
            "fetch_scale": fetch_scale,
            "fetch_check": None if c_read is None else fetch_scale * c_read / GIB,
            "write_check": None if c_write is None else c_write / GIB}
-    fa, wa = per_label(rows(pf), "FETCH_SIZE"), per_label(rows(pw), "WRITE_SIZE")
+    (fa, fu), (wa, wu) = per_label(rows(pf), "FETCH_SIZE", F), per_label(rows(pw), "WRITE_SIZE", F)
     kern = {}
     for lab in sorted(set(fa) | set(wa)):
         f = fetch_scale * sum(fa.get(lab, [0])) / max(1, len(fa.get(lab, [])))
         w = sum(wa.get(lab, [0])) / max(1, len(wa.get(lab, [])))
-        kern[lab] = {"fetch_bytes": f, "write_bytes": w, "traffic_bytes": f + w,
+        kern[lab] = {"fetch_bytes": f, "write_bytes": w, "traffic_bytes": f + w, "traffic_per_frame": (f + w) / F,
                      "launches": len(fa.get(lab, []))}
-    res = {"config": {"workload": "ssg", "points_per_frame": 65536, "frames_per_gpu": 32,
-                      "frames_per_launch": FRAMES_PER_LAUNCH},
-           "source": "rocprofv3 --kernel-trace --pmc FETCH_SIZE | WRITE_SIZE (separate passes) of "
-                     "bench.py --no-extras --no-cpu-baseline --no-density --no-fp32-mfma-leg --no-standalone "
-                     "--steps 6 --warmup 1",
-           "calibration": cal, "kernels": kern}
+    # SA2's per-point layer 1 is two GEMMs per pass (point rows, centre rows): bench.py times them as one
+    if "sa2_layer1_points" in kern and "sa2_layer1_centres" in kern:
+        p, c = kern.pop("sa2_layer1_points"), kern.pop("sa2_layer1_centres")
+        kern["sa2_layer1_points"] = {k: p[k] + c[k] for k in ("fetch_bytes", "write_bytes", "traffic_bytes",
+                                                              "traffic_per_frame")}
+        kern["sa2_layer1_points"]["launches"] = p["launches"]
+    res = {"config": {"workload": "ssg", "points_per_frame": N_POINTS, "frames_per_gpu": 32,
+                      "frames_per_launch": F},
+           "source": "rocprofv3 --kernel-trace --pmc FETCH_SIZE | WRITE_SIZE (separate passes) of bench.py "
+                     "--no-verify --no-extras --no-cpu-baseline --no-density --no-fp32-mfma-leg --no-standalone "
+                     "--steps 20 --warmup 5 (the driver's G = 4: 128-frame launches); every dispatch whose grid is "
+                     "not an F-frame pipeline launch is listed under 'unmatched' and left out",
+           "calibration": cal, "kernels": kern, "unmatched": {"fetch": fu, "write": wu}}
     os.makedirs(os.path.dirname(out) or ".", exist_ok=True)
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
     for k, v in kern.items():
-        print(f"{k:18s} fetch {v['fetch_bytes'] / 1e6:10.2f} MB  write {v['write_bytes'] / 1e6:10.2f} MB")
-    print("calibration", cal)
+        print(f"{k:20s} fetch {v['fetch_bytes'] / 1e6:10.2f} MB  write {v['write_bytes'] / 1e6:10.2f} MB  "
+              f"per frame {v['traffic_per_frame'] / 1e6:8.3f} MB  ({v['launches']} launches)")
+    print("F =", F, "calibration", cal)
+    print("unmatched", fu)
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:6])
+    main(*sys.argv[1:7])

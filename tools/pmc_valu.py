@@ -12,7 +12,7 @@ GPU-busy clock summed over the 8 XCDs, so a dispatch lasts GRBM_GUI_ACTIVE / 8 c
 
 rocprofv3 serialises dispatches while collecting counters, so each row is the kernel alone.
 
-usage: python tools/pmc_valu.py gpurun_out/<tag>/pmc_valu profiles/<round>/pmc_valu.json
+usage: python tools/pmc_valu.py gpurun_out/<tag>/pmc_valu gpurun_out/<tag>/pmc_valu.json profiles/<round>/pmc_valu.json
 """
 import json
 import os
@@ -20,34 +20,40 @@ import sys
 from collections import defaultdict
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-from pmc_traffic import FRAMES_PER_LAUNCH, label, rows  # noqa: E402
+from pmc_traffic import bench_frames_per_launch, frames_of, label, rows  # noqa: E402
 
 SIMDS = 1024
 
 
-def main(d, out):
+def main(d, bench_json, out):
+    F = bench_frames_per_launch(bench_json)
     per = defaultdict(lambda: defaultdict(float))  # (dispatch) -> counter -> value
     meta = {}
     for r in rows(d):
         k = int(r["Dispatch_Id"])
         per[k][r["Counter_Name"]] += float(r["Counter_Value"])
-        meta[k] = (r["Kernel_Name"], int(r["Grid_Size"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+        meta[k] = (r["Kernel_Name"], int(r["Grid_Size"]), int(r["Workgroup_Size"]),
+                   int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
     acc = defaultdict(list)
-    fps, bins = [], []
+    bins = []
+    unmatched = defaultdict(int)
     for k in sorted(per):
-        name, grid, dur = meta[k]
-        lab = label(name, grid)
-        if lab == "fps":
-            fps.append((dur, per[k]))
+        name, grid, wg, dur = meta[k]
+        lab = label(name)
+        if lab in (None, "torch", "runtime_copy", "weight_pack", "concat"):
+            unmatched[(lab or "unlabelled") + ": " + name[:80]] += 1
+            continue
+        lab, frames = frames_of(lab, name, grid, wg, F)
+        if frames is None:
+            unmatched[lab + ": " + name[:80]] += 1
         elif lab == "bq_bin":
             bins.append((dur, per[k]))
-        elif lab and lab not in ("dense_shared", "concat"):
-            acc[lab].append(per[k])
-    for lst, small, big in ((fps, "sa2_fps", "sa1_fps"), (bins, "sa2_bq_bin", "sa1_bq_bin")):
-        lst.sort(key=lambda t: t[0])
-        half = len(lst) // 2
-        acc[small] += [c for _, c in lst[:half]]
-        acc[big] += [c for _, c in lst[half:]]
+        else:
+            acc["sa2_fps" if lab == "fps_1024" else lab].append(per[k])
+    bins.sort(key=lambda t: t[0])
+    half = len(bins) // 2
+    acc["sa2_bq_bin"] += [c for _, c in bins[:half]]
+    acc["sa1_bq_bin"] += [c for _, c in bins[half:]]
     kern = {}
     for lab, cs in acc.items():
         if not cs:
@@ -57,12 +63,13 @@ def main(d, out):
         kern[lab] = {"launches": len(cs), **{c.lower(): v for c, v in m.items()},
                      "valu_busy": 4 * m.get("SQ_ACTIVE_INST_VALU", 0.0) / (SIMDS * cyc) if cyc else None,
                      "valu_issue_frac": 2 * m.get("SQ_INSTS_VALU", 0.0) / (SIMDS * cyc) if cyc else None,
-                     "valu_insts_per_frame": m.get("SQ_INSTS_VALU", 0.0) / FRAMES_PER_LAUNCH}
+                     "valu_insts_per_frame": m.get("SQ_INSTS_VALU", 0.0) / F}
     res = {"config": {"workload": "ssg", "points_per_frame": 65536, "frames_per_gpu": 32,
-                      "frames_per_launch": FRAMES_PER_LAUNCH},
+                      "frames_per_launch": F},
            "source": "rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES "
-                     "SQ_INSTS_SALU SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE of bench.py (SSG leg only)",
-           "kernels": kern}
+                     "SQ_INSTS_SALU SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE of bench.py --no-verify (SSG leg only, the "
+                     "driver's --steps 20: F-frame pipeline launches; other dispatches under 'unmatched')",
+           "kernels": kern, "unmatched": dict(unmatched)}
     os.makedirs(os.path.dirname(out) or ".", exist_ok=True)
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
@@ -72,4 +79,4 @@ def main(d, out):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(sys.argv[1], sys.argv[2], sys.argv[3])

@@ -291,15 +291,21 @@ def tier_r_leg(dev, rank, world, frames=32, n=65536, steps=3, cpu=True, cpu_budg
     vg = VenueGrid((-15.0, 15.0), (-15.0, 15.0), 1.0, device=dev)
     people = ds.people_of_last_batch()
     vg.add(people)
-    t0 = time.perf_counter()
-    vg.all_reduce()
-    torch.cuda.synchronize(dev)
-    rec["global_density"] = {"venue_cells": int(vg.counts.numel()), "people_per_rank": int(people.shape[0]),
-                             "people_all_ranks": int(vg.counts.sum().item()),
-                             "all_reduce_ms": (time.perf_counter() - t0) * 1e3,
-                             "collective": "torch.distributed all_reduce(int32, SUM) over "
-                                           + ("RCCL" if world > 1 and vg.backend() == "nccl" else
-                                              "gloo" if world > 1 else "none (1 rank)")}
+    gd = {"venue_cells": int(vg.counts.numel()), "people_per_rank": int(people.shape[0])}
+    if world > 1:
+        # the collective alone: everything queued before it has finished and every rank has arrived
+        torch.cuda.synchronize(dev)
+        torch.distributed.barrier()
+        t0 = time.perf_counter()
+        vg.all_reduce()
+        torch.cuda.synchronize(dev)
+        gd["all_reduce_ms"] = (time.perf_counter() - t0) * 1e3
+        gd["collective"] = "torch.distributed all_reduce(int32, SUM) over " + (
+            "RCCL" if vg.backend() == "nccl" else vg.backend())
+    else:
+        gd["collective"] = "none (1 rank: the venue grid is this rank's own)"
+    gd["people_all_ranks"] = int(vg.counts.sum().item())
+    rec["global_density"] = gd
     return rec
 
 
@@ -451,6 +457,9 @@ def main():
     ap.add_argument("--seed-rank", type=int, default=None,
                     help="generate the frames of this rank (a 1-process run reproducing one rank of an N-rank run)")
     ap.add_argument("--dump", default=None, help="write this rank's output digests to DUMP.rank<r>.json")
+    ap.add_argument("--no-verify", action="store_true",
+                    help="skip the one-batch forward() references and the bit-equality check of every pipeline "
+                         "output (PMC passes: only the pipeline's own launches are then counted)")
     args = ap.parse_args()
 
     import torch
@@ -467,6 +476,7 @@ def main():
     B, N = args.batch, args.points
     G = pick_group(args.steps, args.fps_group)
     digests = {}
+    local_ms = {}  # this rank's own window time per leg (the line reports the max over ranks)
 
     def measure(key, cfg, dtype, B, N, steps, warmup, depth, G, x3=True, events=True):
         """Steady-state window of `steps` batches through StreamingSSG's feed.  events: HIP
@@ -477,7 +487,9 @@ def main():
         bb = pn.PointNet2Backbone(cfg, device=dev, seed=0, dtype=dtype, x3=x3)
         nb = max(1, args.rotate)
         xs = [torch.from_numpy(unit_frames(B, N, seed=sharding.frame_seed(seed_rank, step=i))).to(dev) for i in range(nb)]
-        refs = [bb.forward(x)[0] for x in xs]  # one-batch forward(): what every pipeline output must equal
+        # one-batch forward(): what every pipeline output must equal (--no-verify: not issued, so a
+        # counter pass sees only the pipeline's launches)
+        refs = None if args.no_verify else [bb.forward(x)[0] for x in xs]
         ready = torch.cuda.Event()  # the inputs exist: the feed's FPS launches wait only for their slots
         ready.record()
         pipe = pn.StreamingSSG(bb, B, N, depth=depth, fps_group=G, fps_threads=args.fps_threads, ramp=False,
@@ -497,12 +509,12 @@ def main():
 
         if events:
             bb.timers = timers
-            elapsed = sharding.timed(lambda: window(nwarm, win), dev, world)  # max over ranks
+            elapsed, local = sharding.timed_detail(lambda: window(nwarm, win), dev, world)  # max over ranks
             bb.timers = None
             outs += win
             i_end = nwarm + steps
         else:
-            elapsed = sharding.timed(lambda: window(nwarm, win), dev, world)
+            elapsed, local = sharding.timed_detail(lambda: window(nwarm, win), dev, world)
             outs += win
             bb.timers = timers
             win2 = []
@@ -514,9 +526,11 @@ def main():
         outs += feed.flush()
         torch.cuda.synchronize(dev)
         assert len(outs) == i_end, (len(outs), i_end)
-        bad = [i for i, o in enumerate(outs) if not torch.equal(o, refs[i % nb])]
-        assert not bad, f"{key}: streaming outputs differ from forward() for batches {bad[:5]}"
-        digests[key] = [hashlib.sha256(r.cpu().numpy().tobytes()).hexdigest() for r in refs]
+        if refs is not None:
+            bad = [i for i, o in enumerate(outs) if not torch.equal(o, refs[i % nb])]
+            assert not bad, f"{key}: streaming outputs differ from forward() for batches {bad[:5]}"
+            digests[key] = [hashlib.sha256(r.cpu().numpy().tobytes()).hexdigest() for r in refs]
+        local_ms[key] = local * 1e3
         return elapsed, timers.totals(), bb, xs
 
     tot_x3 = None
@@ -616,6 +630,10 @@ def main():
               "sa1_fps_us_per_step": per_launch.get("sa1_fps", 0) * 1e3 / max(1, N // 16)}
 
     value = sharding.aggregate_rate(B * N * args.steps, world, elapsed) / 1e6
+    # what the process group saw (backend, ranks, GPUs) and each rank's own frames and window time:
+    # an N-GPU line shows by itself that RCCL ran N ranks, one per GPU
+    group = sharding.group_report(dev, world, B * args.steps, local_ms["ssg"] / 1e3)
+    sharding.check_backend(world, group["backend"], group["device_count"])
     if args.dump:
         with open(f"{args.dump}.rank{rank}.json", "w") as f:
             json.dump({"rank": rank, "seed_rank": seed_rank, "world": world, "digests": digests,
@@ -646,6 +664,7 @@ def main():
             "roofline_standalone": ({k: roof(k, standalone) for k in standalone if k in work}
                                     if standalone else None),
             "kernel_ms_per_launch": per_launch,
+            "distributed": group,
             "pipeline": {"executor": "pointnet2.StreamingSSG feed (steady state: the window pushes and completes "
                                      "exactly `steps` batches; pipeline fill and drain outside it)",
                          "side_streams": args.depth, "batches_per_group": G, "frames_per_launch": G * B,

@@ -43,8 +43,13 @@ typedef struct lidar_handle lidar_handle;
 /* ------------------------------------------------------------------ handle */
 int lidar_create(int device, lidar_handle **out);
 int lidar_destroy(lidar_handle *h);
-/* grow the scratch workspace to at least `bytes` now (not inside graph capture) */
+/* grow the scratch workspace to at least `bytes` now (not inside graph capture).  Growth never
+ * synchronises the device: the replaced block is retired (queued kernels may still read it) and
+ * freed by lidar_destroy or lidar_trim. */
 int lidar_reserve(lidar_handle *h, uint64_t bytes);
+/* free the workspaces retired by growth (*freed = their bytes, may be NULL); the caller guarantees
+ * that the work it queued with this handle before the growth has completed */
+int lidar_trim(lidar_handle *h, uint64_t *freed);
 
 const char *lidar_last_error(void);
 int lidar_version(void);

@@ -40,6 +40,7 @@ SIGNATURES = {
     "lidar_create": [ctypes.c_int, ctypes.POINTER(P)],
     "lidar_destroy": [P],
     "lidar_reserve": [P, ctypes.c_uint64],
+    "lidar_trim": [P, P],
     "lidar_last_error": [],
     "lidar_version": [],
     "lidar_profile": [P, I32],

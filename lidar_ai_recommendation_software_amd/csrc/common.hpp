@@ -26,6 +26,11 @@ struct lidar_handle {
     int device = 0;
     void *ws = nullptr;       // scratch workspace (device)
     uint64_t ws_bytes = 0;
+    // workspaces replaced by a larger one: queued kernels on any stream may still read them, so
+    // they are freed only where the handle is known idle (lidar_destroy, lidar_trim), never by a
+    // device-wide synchronisation in the middle of a pipeline
+    std::vector<void *> retired;
+    uint64_t retired_bytes = 0;
     void *host_pinned = nullptr;  // small pinned host buffer for scalar read-backs
     lidar::Prof *prof = nullptr;  // non-null while lidar_profile(h, 1) is on
 };

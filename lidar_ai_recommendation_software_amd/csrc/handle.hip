@@ -20,28 +20,21 @@ int fail(int code, const std::string &msg)
 void *workspace(lidar_handle *h, uint64_t bytes)
 {
     if (bytes <= h->ws_bytes) return h->ws;
-    uint64_t want = align_up(bytes + bytes / 4, 1 << 20);
-    if (h->ws) {
-        // the previous workspace may still be read by queued kernels
-        hipError_t e = hipDeviceSynchronize();
-        if (e != hipSuccess) {
-            set_error(std::string("workspace growth: hipDeviceSynchronize: ") + hipGetErrorString(e));
-            return nullptr;
-        }
-        e = hipFree(h->ws);
-        h->ws = nullptr;
-        h->ws_bytes = 0;
-        if (e != hipSuccess) {
-            set_error(std::string("workspace growth: hipFree: ") + hipGetErrorString(e));
-            return nullptr;
-        }
-    }
-    const hipError_t e = hipMalloc(&h->ws, want);
+    // at least double: the retired blocks then total less than the live one
+    const uint64_t want = align_up(std::max(bytes + bytes / 4, 2 * h->ws_bytes), 1 << 20);
+    void *fresh = nullptr;
+    const hipError_t e = hipMalloc(&fresh, want);
     if (e != hipSuccess) {
-        h->ws = nullptr;
         set_error(std::string("workspace hipMalloc(") + std::to_string(want) + "): " + hipGetErrorString(e));
-        return nullptr;
+        return nullptr;  // the current workspace stays as it was
     }
+    if (h->ws) {
+        // queued kernels (on whichever streams the caller used) may still read the old block:
+        // retire it instead of synchronising the device (lidar_trim / lidar_destroy free it)
+        h->retired.push_back(h->ws);
+        h->retired_bytes += h->ws_bytes;
+    }
+    h->ws = fresh;
     h->ws_bytes = want;
     return h->ws;
 }
@@ -100,6 +93,7 @@ LIDAR_EXPORT int lidar_destroy(lidar_handle *h)
             delete h->prof;
         }
         if (h->ws) note(hipFree(h->ws), "lidar_destroy: hipFree");
+        for (void *r : h->retired) note(hipFree(r), "lidar_destroy: hipFree (retired workspace)");
         if (h->host_pinned) note(hipHostFree(h->host_pinned), "lidar_destroy: hipHostFree");
     }
     delete h;
@@ -112,6 +106,25 @@ LIDAR_EXPORT int lidar_reserve(lidar_handle *h, uint64_t bytes)
     ON_DEVICE(h->device);
     if (!lidar::workspace(h, bytes)) return LIDAR_ENOMEM;
     return LIDAR_OK;
+}
+
+// Frees the workspaces retired by growth.  The caller guarantees that no work it queued with this
+// handle before the growth is still pending (e.g. after synchronising the streams it used).
+LIDAR_EXPORT int lidar_trim(lidar_handle *h, uint64_t *freed)
+{
+    REQUIRE(h != nullptr, "lidar_trim: null handle");
+    ON_DEVICE(h->device);
+    const uint64_t bytes = h->retired_bytes;
+    int rc = LIDAR_OK;
+    for (void *r : h->retired) {
+        const hipError_t e = hipFree(r);
+        if (e != hipSuccess && rc == LIDAR_OK)
+            rc = lidar::fail(LIDAR_EHIP, std::string("lidar_trim: hipFree: ") + hipGetErrorString(e));
+    }
+    h->retired.clear();
+    h->retired_bytes = 0;
+    if (freed) *freed = bytes;
+    return rc;
 }
 
 // enable != 0: record HIP events around the handle's kernel phases from now on (previous records

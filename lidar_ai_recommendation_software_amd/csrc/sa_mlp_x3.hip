@@ -348,10 +348,10 @@ __global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float 
     }
 }
 
-// Lean form of sa_x3_kernel<.., L1_PRE, R = 2, false> for the wide feature levels (SA2): the same
-// arithmetic, results bit for bit, in <= 128 VGPRs and 34 KiB of LDS, so that a CU holds three
-// of its workgroups beside a resident 512-thread FPS workgroup (two for the 160-VGPR / 50-KiB
-// form).  Layer 2 runs one 16-row tile at a time (only that tile's layer-2 operand is live; its
+// The wide feature levels (SA2): the arithmetic of sa_x3_kernel<.., L1_PRE, R = 2, false> in
+// <= 128 VGPRs and 34 KiB of LDS, so that a CU holds three of its workgroups beside a resident
+// 512-thread FPS workgroup (two for that form, 160 VGPRs / 50 KiB, which this kernel replaced:
+// the two were tested bit-identical in round 2, and only this one ships).  Layer 2 runs one 16-row tile at a time (only that tile's layer-2 operand is live; its
 // weight chunks stream through LDS once per tile), layer 3 keeps R = 2 (both tiles share every
 // weight fragment), and the max-pool is a register max: per chunk, each lane's max over its rows
 // is reduced over the four row groups by two lane swaps and folded into mx[t / 4] of row group
@@ -534,25 +534,6 @@ __global__ __launch_bounds__(256, 4) void sa_x3_lean_kernel(const float *__restr
 #define LIDAR_X3_ROWS 2
 #endif
 
-// lean SA2 kernels (sa_x3_lean_kernel) unless LIDAR_SA_LEAN=0 (A/B switch)
-static bool use_lean()
-{
-    static const bool on = [] {
-        const char *e = getenv("LIDAR_SA_LEAN");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
-// index prefetch in the lean kernel unless LIDAR_LEAN_PFX=0 (A/B switch)
-static bool use_lean_pfx()
-{
-    static const bool on = [] {
-        const char *e = getenv("LIDAR_LEAN_PFX");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
-
 template <int C1, int C2, int C3, int NS>
 int launch_x3_lean(const float *p, int64_t stride, const float *q, const int32_t *idx, int64_t batch, int64_t n,
                    int64_t m, const void *packed, float *out, int64_t os, int64_t oo, hipStream_t s)
@@ -560,12 +541,9 @@ int launch_x3_lean(const float *p, int64_t stride, const float *q, const int32_t
     const int64_t total = batch * m;
     const int64_t blocks = (total + 3) / 4;
     REQUIRE(blocks <= 0x7fffffff, "sa_group_mlp_x3: too many centres");
-    if (NS % 64 == 0 && use_lean_pfx())
-        hipLaunchKernelGGL((sa_x3_lean_kernel<C1, C2, C3, NS, NS % 64 == 0>), dim3((unsigned)blocks), dim3(256), 0, s,
-                           p, stride, q, idx, (int)n, (int)m, total, static_cast<const uint4 *>(packed), out, os, oo);
-    else
-        hipLaunchKernelGGL((sa_x3_lean_kernel<C1, C2, C3, NS, false>), dim3((unsigned)blocks), dim3(256), 0, s, p,
-                           stride, q, idx, (int)n, (int)m, total, static_cast<const uint4 *>(packed), out, os, oo);
+    // a centre's row indices in one coalesced load whenever NS is a multiple of the wavefront
+    hipLaunchKernelGGL((sa_x3_lean_kernel<C1, C2, C3, NS, NS % 64 == 0>), dim3((unsigned)blocks), dim3(256), 0, s, p,
+                       stride, q, idx, (int)n, (int)m, total, static_cast<const uint4 *>(packed), out, os, oo);
     LAUNCH_CHECK();
     return LIDAR_OK;
 }
@@ -686,7 +664,8 @@ LIDAR_EXPORT int lidar_sa_group_mlp_x3_f32(lidar_handle *h, int32_t xyz_level, c
     if (batch == 0) return LIDAR_OK;
     ON_DEVICE(h->device);
     hipStream_t s = static_cast<hipStream_t>(stream);
-    if (!xyz_level && c1 == 128 && c2 == 128 && c3 == 256 && use_lean()) {
+    // the wide feature levels (SA2, MSG's 128-sample branch) run the lean kernel
+    if (!xyz_level && c1 == 128 && c2 == 128 && c3 == 256) {
         if (nsample == 64)
             return launch_x3_lean<128, 128, 256, 64>(p, p_stride, q, idx, batch, n, m, packed, out, out_stride,
                                                      out_offset, s);
@@ -701,8 +680,6 @@ LIDAR_EXPORT int lidar_sa_group_mlp_x3_f32(lidar_handle *h, int32_t xyz_level, c
     LIDAR_SAX3(64, 64, 128, 32, true)
     LIDAR_SAX3(32, 32, 64, 16, true)
     LIDAR_SAX3(64, 96, 128, 128, true)
-    LIDAR_SAX3(128, 128, 256, 64, false)
-    LIDAR_SAX3(128, 128, 256, 128, false)
     LIDAR_SAX3(64, 64, 128, 32, false)
 #undef LIDAR_SAX3
     return lidar::fail(LIDAR_EINVAL, "lidar_sa_group_mlp_x3_f32: unsupported (widths, nsample) combination");

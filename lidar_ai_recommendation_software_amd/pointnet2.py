@@ -757,7 +757,7 @@ class StreamingSSG:
             self.gidx2 = [[torch.empty((GB, self.M2, br["ns"]), dtype=torch.int32, device=dev)
                            for br in lvl1["branches"]] for _ in range(nslot)]
         # setup-time workspace sizing of the side handles (FPS + ball queries), so no stage's
-        # first call allocates (lidar_reserve; a grow re-allocates after a device sync)
+        # first call grows a workspace (lidar_reserve; growth retires the old block, no device sync)
         if reserve:
             lib = nat.load_library()
             need = max(lib.lidar_fps_workspace_bytes(GB, n), lib.lidar_ball_query_grid_bytes(GB, n))

@@ -37,6 +37,17 @@ def frame_seed(rank, step=0, base=0):
 def timed(run, device=None, world=1):
     """Barrier + device sync, run(), device sync + barrier; returns the elapsed wall
     time MAXED over ranks (the whole job finishes when the slowest rank does)."""
+    return timed_detail(run, device, world)[0]
+
+
+def _host_collectives(device):
+    """True when the process group reduces host tensors (gloo: the CPU tests, or ranks sharing
+    one GPU), False for RCCL, which reduces device tensors."""
+    return not (device is not None and device.type == "cuda" and dist.get_backend() == "nccl")
+
+
+def timed_detail(run, device=None, world=1):
+    """`timed`, returning (max-over-ranks elapsed, this rank's own elapsed)."""
     cuda = device is not None and device.type == "cuda"
 
     def sync():
@@ -51,14 +62,40 @@ def timed(run, device=None, world=1):
     sync()
     if world > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
+    local = elapsed = time.perf_counter() - t0
     if world > 1:
-        # RCCL reduces device tensors; gloo (the CPU tests, or ranks sharing one GPU) host ones
-        on_dev = cuda and dist.get_backend() == "nccl"
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device if on_dev else "cpu")
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if _host_collectives(device) else device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    return elapsed
+    return elapsed, local
+
+
+def group_report(device, world, frames, elapsed_local):
+    """What the process group saw, for the bench line: the backend, the world size, the GPUs this
+    node exposes, and every rank's (device index, frames processed, own elapsed ms), gathered with
+    one all_gather over the group (the reporting path, not the data path).  With world 1 no
+    collective runs."""
+    ndev = torch.cuda.device_count()
+    dev_idx = device.index if device is not None and device.type == "cuda" else -1
+    mine = [float(dist.get_rank() if world > 1 else 0), float(dev_idx), float(frames), elapsed_local * 1e3]
+    if world > 1:
+        t = torch.tensor(mine, dtype=torch.float64, device="cpu" if _host_collectives(device) else device)
+        parts = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(parts, t)
+        rows = [p.cpu().tolist() for p in parts]
+        backend, ws = dist.get_backend(), dist.get_world_size()
+    else:
+        rows, backend, ws = [mine], None, 1
+    return {"backend": backend, "world_size": ws, "device_count": ndev,
+            "ranks": [{"rank": int(r[0]), "device": int(r[1]), "frames": int(r[2]), "ms": r[3]} for r in rows]}
+
+
+def check_backend(world, backend, device_count):
+    """One process per GPU must talk RCCL: a multi-rank run with at least as many visible GPUs as
+    ranks that ended up on another backend is a misconfiguration (init_distributed picks gloo only
+    when ranks share a GPU)."""
+    if world > 1 and world <= device_count and backend != "nccl":
+        raise RuntimeError(f"{world} ranks over {device_count} GPUs must use RCCL ('nccl'), got {backend!r}")
 
 
 def init_distributed(world, local):

@@ -122,3 +122,38 @@ def test_gloo_world2_venue_grid_all_reduce(tmp_path):
     want = tier_r.calculate_grid_density(allp, (-15.0, 15.0), (-15.0, 15.0), 1.0)[2]
     for r in range(world):
         assert np.array_equal(np.load(tmp_path / f"venue{r}.npy"), want)
+
+
+def _report_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    el, local = sharding.timed_detail(lambda: time.sleep(0.05 + 0.2 * rank), None, world)
+    rep = sharding.group_report(None, world, 32 * (rank + 1), local)
+    np.save(os.path.join(out_dir, f"rep{rank}.npy"),
+            np.array([el, local] + [v for r in rep["ranks"] for v in (r["rank"], r["frames"], r["ms"])]
+                     + [rep["world_size"], float(rep["backend"] == "gloo")], dtype=np.float64))
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_group_report(tmp_path):
+    """bench.py's `distributed` record: every rank's frames and own window time, gathered over the
+    group, the backend and world size the group reports; the max equals the slowest rank's time."""
+    world = 2
+    mp.spawn(_report_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    recs = [np.load(tmp_path / f"rep{r}.npy") for r in range(world)]
+    for rec in recs:
+        el, local = rec[0], rec[1]
+        rows = rec[2:2 + 3 * world].reshape(world, 3)
+        assert list(rows[:, 0]) == [0, 1] and list(rows[:, 1]) == [32, 64]
+        assert el == recs[0][0] and abs(el * 1e3 - rows[:, 2].max()) < 1e-6 and local <= el
+        assert rec[-2] == world and rec[-1] == 1.0
+    assert recs[1][1] >= 0.25
+
+
+def test_check_backend_rules():
+    sharding.check_backend(1, None, 1)          # one rank: nothing to check
+    sharding.check_backend(8, "nccl", 8)        # one rank per GPU over RCCL
+    sharding.check_backend(2, "gloo", 1)        # two ranks sharing one GPU: gloo by design
+    with pytest.raises(RuntimeError):
+        sharding.check_backend(8, "gloo", 8)    # a GPU per rank but not RCCL

@@ -209,25 +209,6 @@ def test_group_mlp_x3(cuda, cfg_name, level, branch):
         feat_close(got[bi, :, off:off + widths[-1]], want, f"{cfg_name} L{level} br{branch} frame {bi} (x3)")
 
 
-@pytest.mark.parametrize("variant", ["LIDAR_SA_LEAN", "LIDAR_LEAN_PFX"])
-def test_sa_kernel_variants_bit_identical(cuda, tmp_path, variant):
-    """The lean feature-level kernel (sa_x3_lean_kernel: <= 128 VGPRs, register max-pool, layer 2
-    one tile at a time, row indices prefetched once per centre) computes the same products in the
-    same order as the 160-VGPR sa_x3_kernel: outputs equal bit for bit.  The other form runs in a
-    child process: the 160-VGPR kernel under LIDAR_SA_LEAN=0, the lean kernel loading each tile's
-    indices from memory under LIDAR_LEAN_PFX=0."""
-    import os
-    import subprocess
-    import sys
-    import sa_variants_case
-    got = np.concatenate([a.ravel() for a in sa_variants_case.run(cuda)])
-    ref = tmp_path / "ref.npy"
-    env = dict(os.environ, **{variant: "0"})
-    subprocess.run([sys.executable, sa_variants_case.__file__, str(ref)], env=env, check=True, timeout=300)
-    want = np.load(ref)
-    assert got.size == want.size and np.array_equal(got.view(np.uint32), want.view(np.uint32))
-
-
 @pytest.mark.parametrize("frame", ["uniform", "clump", "line", "all_equal", "lattice_ties"])
 @pytest.mark.parametrize("widths,r,ns", [([64, 64, 128], 0.2, 32), ([32, 32, 64], 0.1, 16), ([64, 96, 128], 0.4, 128)])
 @pytest.mark.parametrize("x1", [False, True])

@@ -6,15 +6,18 @@
 #   3 rocprofv3 --kernel-trace --stats of the SSG bench (kernel durations to compare with the
 #     in-bench HIP-event means)
 #   4 PMC: a 1 GiB copy calibrating FETCH_SIZE / WRITE_SIZE, then one pass per counter group over
-#     a short SSG bench (FETCH_SIZE; WRITE_SIZE; the SQ / GRBM VALU group)
+#     the SSG bench at the driver's shape (FETCH_SIZE; WRITE_SIZE; the SQ / GRBM VALU group)
+# reduce afterwards (CPU): tools/pmc_traffic.py and tools/pmc_valu.py with the passes' bench lines
 # usage (on the box): bash tools/profile_round.sh TAG [tests|notests]
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-TAG=${1:-r02}
+TAG=${1:-r03}
 O=$R/gpurun_out/$TAG
 mkdir -p $O
 cd $R
-SHORT="--no-extras --no-cpu-baseline --no-density --no-fp32-mfma-leg --no-standalone --steps 6 --warmup 1"
+# the PMC passes run the driver's shape (--steps 20: G = 4, 128-frame launches) with only the pipeline's own
+# launches (--no-verify: no one-batch forward() references), so every counted dispatch is a 128-frame launch
+SHORT="--no-verify --no-extras --no-cpu-baseline --no-density --no-fp32-mfma-leg --no-standalone --steps 20 --warmup 5"
 if [ "${2:-tests}" = "tests" ]; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || exit 11
 fi

@@ -4,7 +4,7 @@
 set -o pipefail
 O=$1; REPS=$2; shift 2
 mkdir -p $O
-BASE="--no-extras --no-density --no-cpu-baseline --no-fp32-mfma-leg --no-standalone"
+BASE=${AB_BASE:-"--no-extras --no-density --no-cpu-baseline --no-fp32-mfma-leg --no-standalone"}
 for rep in $(seq 1 $REPS); do
   i=0
   for arm in "$@"; do
@@ -22,6 +22,9 @@ print("[%s]" % sys.argv[2], "value %.1f" % d["value"], "ms/step %.3f" % d["ms_pe
       "frac %.3f" % d["roofline_grouped_mlp"]["frac"],
       "side %.2f main %.2f G=%d" % (p["side_ms_per_group"], p["main_ms_per_group"], p["batches_per_group"]),
       {k: round(v, 3) for k, v in d["kernel_ms_per_launch"].items()}, flush=True)
+if d.get("roofline_standalone"):
+    print("   standalone", {k: (round(v["avg_launch_ms"], 3), round(v["frac"], 3)) for k, v in d["roofline_standalone"].items()},
+          flush=True)
 PY
   done
 done

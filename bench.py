@@ -42,6 +42,7 @@ BF16_MFMA_PEAK_TFLOPS = 2500.0  # bf16 dense matrix peak
 X3_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 3
 FP64_VALU_PEAK_TFLOPS = 78.6
 HBM_PEAK_GBS = 8000.0
+F64_ADD_LATENCY_CYCLES = 6.3  # dependent v_add_f64, operand in a register (tools/micro/f64_chain.hip)
 X3_KERNELS = ("sa1_group_mlp", "sa2_group_mlp", "sa2_layer1_points", "sa3_dense1", "sa3_dense2", "sa3_dense3_pool")
 
 
@@ -246,6 +247,23 @@ def tier_r_leg(dev, rank, world, frames=32, n=65536, steps=3, cpu=True, cpu_budg
                            "peak_basis": "FP64 vector peak (FMA counted as 2) over 8 FLOP per eps-pair; the kernels "
                                          "prune most pairs (same-cell shortcut, cell-pair links stop at the first "
                                          "link), so this is work avoided, not work done"}
+    elif dom == "preprocess":
+        # the preprocess is bound by the dependent fp64 chains numpy's sequential axis-0 sums force
+        # (utils/data_processing.py:151-152, :191-194): per frame 4 signed sums of n dependent
+        # v_add_f64 plus the two emulated sums of squares (~0.2 of a pass each), one workgroup per
+        # frame, all frames of the launch in parallel.  Floor: 4.4 n dependent adds at the measured
+        # 6.3-cycle v_add_f64 latency (tools/micro/f64_chain.hip) at 2.4 GHz; frac = floor / achieved
+        floor_ns = F64_ADD_LATENCY_CYCLES / 2.4
+        ns_row = per_launch_ms["preprocess"] * 1e6 / (4.4 * n)
+        rec["roofline"] = {"kernel": "preprocess", "bound": "fp64-add-latency", "achieved": ns_row,
+                           "peak": floor_ns, "unit": "ns per dependent row", "frac": floor_ns / ns_row,
+                           "traffic": None, "work_per_launch": 4.4 * n, "avg_launch_ms": per_launch_ms["preprocess"],
+                           "peak_basis": "one dependent v_add_f64 per row of a sequential sum: 6.3 cycles measured "
+                                         "(tools/micro/f64_chain.hip) at 2.4 GHz; 4.4 passes of n rows per frame (4 "
+                                         "signed sums + 2 emulated sums of squares at ~0.2 of a pass), frames in "
+                                         "parallel (one workgroup each), so the launch time is one frame's chain",
+                           "hbm_frac": DENSITY_BYTES_PER_POINT["preprocess"] * pts
+                                       / (per_launch_ms["preprocess"] / 1e3) / 1e9 / HBM_PEAK_GBS}
     elif dom in DENSITY_BYTES_PER_POINT:
         algo = DENSITY_BYTES_PER_POINT[dom] * pts
         a = algo / (per_launch_ms[dom] / 1e3) / 1e9
@@ -430,8 +448,9 @@ def main():
     ap.add_argument("--fps-group", type=int, default=3,
                     help="batches per SA1-FPS launch (StreamingSSG fps_group); must divide --steps, else the "
                          "nearest of 3, 4, 5, 2 that does")
-    ap.add_argument("--fps-threads", type=int, default=512, choices=[512, 1024],
-                    help="SA1 FPS workgroup size in the pipeline (512: half the CU footprint beside the MLPs)")
+    ap.add_argument("--fps-threads", type=int, default=0, choices=[0, 64, 512, 1024],
+                    help="SA1 FPS workgroup size in the pipeline (0 = auto: one wavefront per frame up to 65 536 "
+                         "points; 512 / 1024: the multi-wave bucket kernel)")
     ap.add_argument("--x3", type=int, default=1,
                     help="1: MLPs on the split-bf16 (x3) kernels, fp32 arithmetic within the 1e-4 contract; "
                          "0: the native fp32-MFMA kernels")

@@ -36,6 +36,15 @@ def frames_for(kind, b, n, seed):
     elif kind == "grid":  # lattice: many exactly equal distances (argmax ties)
         g = np.stack(np.meshgrid(*[np.arange(16)] * 3, indexing="ij"), -1).reshape(-1, 3)
         x = np.tile((g[:n] / 8.0 - 1.0).astype(np.float32)[None], (b, 1, 1))
+    elif kind == "offset":  # far from the origin, unit spread: coarse fp32 spacing of the boxes
+        x = (x.astype(np.float64) + np.array([3.0e4, -7.5e3, 1.0e5])).astype(np.float32)
+    elif kind == "flat":  # one axis constant (zero-width boxes), another with a 1e-30 spread
+        x[..., 2] = np.float32(0.25)
+        x[..., 1] *= np.float32(1e-30)
+    elif kind == "nonfinite":  # +-inf and NaN coordinates: nothing may be pruned wrongly
+        x[:, 5, 0] = np.inf
+        x[:, 17, 1] = -np.inf
+        x[:, 40, 2] = np.nan
     return np.ascontiguousarray(x)
 
 
@@ -44,11 +53,15 @@ def frames_for(kind, b, n, seed):
     ("uniform", 1, 65536, 4096), ("uniform", 1, 131072, 512), ("uniform", 1, 150000, 64),
     ("clumped", 2, 5000, 300), ("dups", 2, 3000, 2000), ("grid", 1, 4096, 600),
     ("uniform", 2, 1, 4), ("uniform", 1, 37, 60), ("uniform", 1, 64, 64),
+    ("offset", 2, 20000, 700), ("flat", 2, 9000, 500), ("nonfinite", 2, 3000, 300), ("uniform", 2, 4097, 300),
+    ("grid", 1, 4096, 4096),
 ])
-@pytest.mark.parametrize("threads", [0, 512])
+@pytest.mark.parametrize("threads", [0, 64, 512])
 def test_fps_bit_exact(cuda, kind, b, n, m, threads):
+    """threads 0 = auto (the one-wave kernel up to 65 536 points), 64 = one wavefront per frame,
+    512 = the 8-wave bucket kernel; bit-exact indices and coordinates against the C oracle."""
     x = frames_for(kind, b, n, 11)
-    if threads and (n + 63) // 64 > 8 * threads:  # 8 buckets per lane at most
+    if threads and (n + 63) // 64 > (2048 if threads == 64 else 8 * threads):  # bucket capacity
         with pytest.raises(LidarError, match="too many buckets"):
             pn.farthest_point_sample(torch.from_numpy(x).to(cuda), m, threads=threads)
         return

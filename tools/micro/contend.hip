@@ -39,6 +39,27 @@ __global__ __launch_bounds__(512) void occupy(int us, float *sink)
     if (s == -1.0f) sink[0] = s;
 }
 
+// one-wave workgroups (the one-wave FPS's footprint): NREG VGPRs per lane, LDSF floats of LDS
+template <int NREG, int LDSF>
+__global__ __launch_bounds__(64) void occupy1(int us, float *sink)
+{
+    __shared__ float lds[LDSF > 0 ? LDSF : 1];
+    const long long w0 = wall_clock64();
+    float r[NREG > 0 ? NREG : 1];
+#pragma unroll
+    for (int i = 0; i < NREG; ++i) r[i] = (float)(threadIdx.x + i);
+    for (int i = threadIdx.x; i < LDSF; i += 64) lds[i] = 0.0f;
+    while (wall_clock64() - w0 < (long long)us * 100) {
+        __builtin_amdgcn_s_sleep(8);
+#pragma unroll
+        for (int i = 0; i < NREG; ++i) asm volatile("" : "+v"(r[i]));
+    }
+    float s = LDSF > 0 ? lds[threadIdx.x % (LDSF > 0 ? LDSF : 1)] : 0.0f;
+#pragma unroll
+    for (int i = 0; i < NREG; ++i) s += r[i];
+    if (s == -1.0f) sink[0] = s;
+}
+
 extern "C" int contend_chase(const unsigned *next, int blocks, int us, unsigned *sink, void *stream)
 {
     hipLaunchKernelGGL(chase, dim3(blocks), dim3(64), 0, static_cast<hipStream_t>(stream), next, 12345u, us, sink);
@@ -50,5 +71,9 @@ extern "C" int contend_occupy(int blocks, int us, float *sink, void *stream, int
     if (variant == 0) hipLaunchKernelGGL((occupy<64, 17 * 256>), dim3(blocks), dim3(512), 0, st, us, sink);
     if (variant == 1) hipLaunchKernelGGL((occupy<0, 17 * 256>), dim3(blocks), dim3(512), 0, st, us, sink);
     if (variant == 2) hipLaunchKernelGGL((occupy<64, 0>), dim3(blocks), dim3(512), 0, st, us, sink);
+    if (variant == 3) hipLaunchKernelGGL((occupy1<116, 22 * 256>), dim3(blocks), dim3(64), 0, st, us, sink);
+    if (variant == 4) hipLaunchKernelGGL((occupy1<116, 0>), dim3(blocks), dim3(64), 0, st, us, sink);
+    if (variant == 5) hipLaunchKernelGGL((occupy1<0, 22 * 256>), dim3(blocks), dim3(64), 0, st, us, sink);
+    if (variant == 6) hipLaunchKernelGGL((occupy1<0, 11 * 256>), dim3(blocks), dim3(64), 0, st, us, sink);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

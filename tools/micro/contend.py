@@ -64,11 +64,20 @@ for variant, what in ((0, "64 VGPRs + 17 KiB LDS"), (1, "few VGPRs + 17 KiB LDS"
         print(f"beside occupy ({blocks:3d} x 512 threads, {what:22s}) {t:7.2f} ms")
 
 
+for variant, what in ((3, "116 VGPRs + 22 KiB LDS"), (4, "116 VGPRs, no LDS"), (5, "few VGPRs + 22 KiB LDS"),
+                      (6, "few VGPRs + 11 KiB LDS")):
+    for blocks in (256, 384, 512):
+        t = with_side(lambda: lib.contend_occupy(blocks, 60000, ctypes.c_void_p(sink.data_ptr()),
+                                                 ctypes.c_void_p(side.cuda_stream), variant))
+        print(f"beside occupy ({blocks:3d} x 64 threads, {what:22s}) {t:7.2f} ms")
+
+
 sides = [torch.cuda.Stream(device=dev) for _ in range(3)]
-torch.cuda.synchronize()
-for k, st in enumerate(sides):  # three concurrent FPS launches, as the pipeline's side streams
-    with torch.cuda.stream(st):
-        pn.farthest_point_sample(xs2[k % 2], N // 16, threads=512, slot=1 + k)
-t = main_ms()
-torch.cuda.synchronize()
-print(f"beside 3 x 128-frame SA1 FPS launches    {t:7.2f} ms")
+for T in (512, 64):
+    torch.cuda.synchronize()
+    for k, st in enumerate(sides):  # three concurrent FPS launches, as the pipeline's side streams
+        with torch.cuda.stream(st):
+            pn.farthest_point_sample(xs2[k % 2], N // 16, threads=T, slot=1 + k)
+    t = main_ms()
+    torch.cuda.synchronize()
+    print(f"beside 3 x 128-frame SA1 FPS launches ({T} threads)   {t:7.2f} ms")

@@ -448,9 +448,8 @@ def main():
     ap.add_argument("--fps-group", type=int, default=3,
                     help="batches per SA1-FPS launch (StreamingSSG fps_group); must divide --steps, else the "
                          "nearest of 3, 4, 5, 2 that does")
-    ap.add_argument("--fps-threads", type=int, default=0, choices=[0, 64, 512, 1024],
-                    help="SA1 FPS workgroup size in the pipeline (0 = auto: one wavefront per frame up to 65 536 "
-                         "points; 512 / 1024: the multi-wave bucket kernel)")
+    ap.add_argument("--fps-threads", type=int, default=512, choices=[512, 1024],
+                    help="SA1 FPS workgroup size in the pipeline (512: half the CU footprint beside the MLPs)")
     ap.add_argument("--x3", type=int, default=1,
                     help="1: MLPs on the split-bf16 (x3) kernels, fp32 arithmetic within the 1e-4 contract; "
                          "0: the native fp32-MFMA kernels")

@@ -82,10 +82,9 @@ uint64_t lidar_fps_workspace_bytes(int64_t batch, int64_t n);
 int lidar_fps_f32(lidar_handle *h, const float *xyz, int64_t batch, int64_t n, int64_t npoint,
                   int32_t *idx, float *new_xyz, int32_t *first_zero, const int32_t *prefix_ok,
                   void *stream);
-/* the same with an explicit workgroup size per frame: threads 0 (auto: 64 up to 131 072 points,
- * 1024 above), 64 (ONE wavefront per frame, < 6 KiB of LDS for 65 536 points: the footprint
- * that leaves the CUs to kernels running beside it), 1024 or 512 (the multi-wave bucket kernel:
- * shorter steps for a single frame).  Identical results. */
+/* the same with an explicit workgroup size per frame: threads 0 (default, 1024), 1024 or 512.
+ * 512 takes ~25 % longer per step and half the CU footprint (throughput pipelines that run
+ * other kernels beside FPS).  Identical results. */
 int lidar_fps_ex_f32(lidar_handle *h, const float *xyz, int64_t batch, int64_t n, int64_t npoint,
                      int32_t *idx, float *new_xyz, int32_t *first_zero, const int32_t *prefix_ok,
                      int32_t threads, void *stream);

@@ -26,8 +26,6 @@
 // is the identity 0..m-1 while the parent's winning distance stayed > 0 — the parent
 // run records the first step whose winning distance was 0 (`first_zero`), the child run
 // takes it as `prefix_ok` and copies the prefix when m <= prefix_ok.
-#include <algorithm>
-
 #include "common.hpp"
 
 namespace {
@@ -515,525 +513,7 @@ __global__ __launch_bounds__(T) void fps_bucket_kernel(const float *__restrict__
     }
 }
 
-// ----------------------------------------------------------------- one-wave FPS (round 3)
-// The kernel above spends 8-16 waves per frame on ~20 active buckets per step, and those waves'
-// registers cost the MFMA levels that share the CUs a wave slot per SIMD.  Here a
-// frame is ONE wavefront: no barriers, one wave of CU footprint per frame in flight, and under
-// 11 KiB of LDS for a 65 536-point frame (measured: a 64-thread workgroup with ~116 VGPRs and
-// 11 KiB of LDS per frame costs the MFMA levels nothing measurable; 22 KiB costs them a workgroup
-// slot per CU, tools/micro/contend.py).
-//
-// Buckets are 128 consecutive Morton-sorted points (two per lane), grouped into slots of 64
-// buckets (8 192 points: 1/8 of a 65 536-point frame's Morton curve).  Bucket b = 64 q + lane.
-//   registers: lane l holds the boxes of buckets (q, l) for every slot q, quantised to 8 bits per
-//              bound relative to slot q's box (2 VGPRs per bucket); lane q < S holds slot q's box,
-//              its quantisation step, and the slot's key (max dist, lowest index, coordinates, and
-//              which bucket holds it);
-//   LDS:       every bucket's key: kd = max-dist bits, kc = (x, y, z, index | argmax member << 24).
-// A step tests the S slot boxes (one instruction), then the buckets of the active slots, appends
-// the active buckets to an LDS list, streams them in batches (all loads of a batch in flight
-// together, the reductions of a batch interleaved), re-keys the slots whose argmax bucket changed
-// and takes the frame argmax over the slot keys — all inside one wave.
-// Exactness: a quantised box CONTAINS the bucket's fp32 box (each bound is rounded outward and
-// checked in the same fp32 fma the test uses), so its bound lb is still <= every member's d
-// (the argument in the header); frames with a non-finite coordinate test nothing (lb = 0).
-constexpr int kWaveMaxSlots = 16;  // 16 x 64 buckets x 128 points = 131 072 points per frame
-constexpr int kWB = 128;           // points per bucket
-
-struct WaveLayout {  // the one-wave FPS's per-frame workspace, offsets in floats
-    int npad, nbs, S;
-    int64_t p, d, qbox, init, slot, total;
-};
-__host__ __device__ inline WaveLayout wave_layout(int n)
-{
-    WaveLayout L;
-    const int nb = (n + kWB - 1) / kWB;
-    L.npad = nb * kWB;
-    int S = 1;
-    while (S * 64 < nb) S *= 2;
-    L.S = S;
-    L.nbs = S * 64;
-    L.p = 0;                        // (npad + kWB) float4 (x, y, z, index): points, sentinels, a dummy bucket
-    L.d = 4 * (int64_t)(L.npad + kWB);
-    L.qbox = L.d + L.npad + kWB;    // 2 u32 per bucket record
-    L.init = L.qbox + 2 * L.nbs;    // float4 per bucket: its key at dist +inf (lowest index member)
-    L.slot = L.init + 4 * L.nbs;    // 16 floats per slot: lo[3], hi[3], step[3], no-filter flag
-    L.total = L.slot + 16 * kWaveMaxSlots;
-    return L;
-}
-
-__device__ __forceinline__ float wave_min_dpp(float v)
-{
-    v = fminf(v, __int_as_float(lidar::dpp_i<0xB1>(__float_as_int(v))));
-    v = fminf(v, __int_as_float(lidar::dpp_i<0x4E>(__float_as_int(v))));
-    v = fminf(v, __int_as_float(lidar::dpp_i<0x141>(__float_as_int(v))));
-    v = fminf(v, __int_as_float(lidar::dpp_i<0x140>(__float_as_int(v))));
-    const float a = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
-    const float b = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
-    const float c = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
-    const float d = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
-    return fminf(fminf(a, b), fminf(c, d));
-}
-
-// max over the wave in EVERY lane, in VALU only (4 DPP row steps, then the xor-32 / xor-16
-// partners by v_permlane32_swap / v_permlane16_swap): independent reductions interleave freely
-__device__ __forceinline__ int wave_max_all(int v)
-{
-    v = max(v, lidar::dpp_i<0xB1>(v));
-    v = max(v, lidar::dpp_i<0x4E>(v));
-    v = max(v, lidar::dpp_i<0x141>(v));
-    v = max(v, lidar::dpp_i<0x140>(v));
-    const auto a = __builtin_amdgcn_permlane32_swap((uint32_t)v, (uint32_t)v, false, false);
-    v = max(v, max((int)a[0], (int)a[1]));
-    const auto c = __builtin_amdgcn_permlane16_swap((uint32_t)v, (uint32_t)v, false, false);
-    return max(v, max((int)c[0], (int)c[1]));
-}
-__device__ __forceinline__ uint32_t wave_min_all_u32(uint32_t v)
-{
-    v = min(v, (uint32_t)lidar::dpp_i<0xB1>((int)v));
-    v = min(v, (uint32_t)lidar::dpp_i<0x4E>((int)v));
-    v = min(v, (uint32_t)lidar::dpp_i<0x141>((int)v));
-    v = min(v, (uint32_t)lidar::dpp_i<0x140>((int)v));
-    const auto a = __builtin_amdgcn_permlane32_swap(v, v, false, false);
-    v = min(v, min((uint32_t)a[0], (uint32_t)a[1]));
-    const auto c = __builtin_amdgcn_permlane16_swap(v, v, false, false);
-    return min(v, min((uint32_t)c[0], (uint32_t)c[1]));
-}
-
-__device__ __forceinline__ float rdl(float v, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); }
-
-// lower bound of d(., q) over a box, with the rounded operations of lidar::dist2f
-__device__ __forceinline__ float box_lb(float qx, float qy, float qz, float lx, float ly, float lz, float hx, float hy,
-                                        float hz)
-{
-    const float gx = gap(qx, lx, hx), gy = gap(qy, ly, hy), gz = gap(qz, lz, hz);
-    return __fadd_rn(__fadd_rn(__fmul_rn(gx, gx), __fmul_rn(gy, gy)), __fmul_rn(gz, gz));
-}
-
-// Prologue of the one-wave FPS, one 1 024-thread workgroup per frame: the Morton counting sort
-// (fps_prologue), padding to whole 128-point buckets plus the dummy bucket, every bucket's box and
-// key at dist +inf, every slot's box and step, and the quantised bucket boxes.
-__global__ __launch_bounds__(1024) void fps_wave_prep_kernel(const float *__restrict__ xyz, int n, int npoint,
-                                                             const int32_t *__restrict__ prefix_ok,
-                                                             float *__restrict__ ws, int64_t ws_stride)
-{
-    constexpr int T = 1024;
-    const int b = blockIdx.x;
-    if (prefix_ok != nullptr && prefix_ok[b] >= npoint) return;  // the step kernel copies the prefix
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const float *p = xyz + (int64_t)b * n * 3;
-    const WaveLayout L = wave_layout(n);
-    float *wsb = ws + (int64_t)b * ws_stride;
-    const FrameWs W{reinterpret_cast<float4 *>(wsb + L.p), wsb + L.d};
-    __shared__ uint32_t hist[kCells];
-    __shared__ float red[6][T / 64];
-    __shared__ uint32_t wsum[T / 64];
-    __shared__ float box[kWaveMaxSlots * 64][6];
-    __shared__ int nonfinite;
-    if (tid == 0) nonfinite = 0;  // fps_prologue's barriers order this before every use
-    fps_prologue<T>(p, n, W, hist, red, wsum);
-    const int nb = L.npad / kWB, S = L.S;
-    // fps_prologue pads to whole 64-point groups; the rest of the last bucket and the dummy bucket
-    // that pads a step's last batch (never closer, never reduced): dist -1 sentinels
-    for (int i = (n + 63) / 64 * 64 + tid; i < L.npad + kWB; i += T) {
-        W.p[i] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(0xffffffffu));
-        W.d[i] = -1.0f;
-    }
-    float4 *init = reinterpret_cast<float4 *>(wsb + L.init);
-    uint32_t *qbox = reinterpret_cast<uint32_t *>(wsb + L.qbox);
-    float *slotp = wsb + L.slot;
-    for (int bucket = wave; bucket < L.nbs; bucket += T / 64) {
-        const int pos = bucket * kWB + lane;
-        const bool r0 = pos < n, r1 = pos + 64 < n;
-        const float4 P0 = r0 ? W.p[pos] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        const float4 P1 = r1 ? W.p[pos + 64] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        const bool bad = (r0 && !(isfinite(P0.x) && isfinite(P0.y) && isfinite(P0.z))) ||
-                         (r1 && !(isfinite(P1.x) && isfinite(P1.y) && isfinite(P1.z)));
-        const float lx = wave_min_dpp(fminf(r0 ? P0.x : INFINITY, r1 ? P1.x : INFINITY));
-        const float ly = wave_min_dpp(fminf(r0 ? P0.y : INFINITY, r1 ? P1.y : INFINITY));
-        const float lz = wave_min_dpp(fminf(r0 ? P0.z : INFINITY, r1 ? P1.z : INFINITY));
-        const float hx = lidar::wave_max_dpp(fmaxf(r0 ? P0.x : -INFINITY, r1 ? P1.x : -INFINITY));
-        const float hy = lidar::wave_max_dpp(fmaxf(r0 ? P0.y : -INFINITY, r1 ? P1.y : -INFINITY));
-        const float hz = lidar::wave_max_dpp(fmaxf(r0 ? P0.z : -INFINITY, r1 ? P1.z : -INFINITY));
-        const uint32_t i0 = r0 ? __float_as_uint(P0.w) : 0xffffffffu, i1 = r1 ? __float_as_uint(P1.w) : 0xffffffffu;
-        const uint32_t mi = lidar::wave_min_u32_dpp(min(i0, i1));
-        const uint64_t c0 = __ballot(i0 == mi);
-        const int sub = c0 ? 0 : 1;  // index 0xffffffff (no member) only in buckets past nb
-        const int wl = __ffsll((unsigned long long)(c0 ? c0 : __ballot(i1 == mi))) - 1;
-        const float wx = rdl(sub ? P1.x : P0.x, wl), wy = rdl(sub ? P1.y : P0.y, wl), wz = rdl(sub ? P1.z : P0.z, wl);
-        const bool any_bad = __ballot(bad) != 0;
-        if (lane == 0) {
-            box[bucket][0] = lx;
-            box[bucket][1] = ly;
-            box[bucket][2] = lz;
-            box[bucket][3] = hx;
-            box[bucket][4] = hy;
-            box[bucket][5] = hz;
-            // key at dist +inf: the lowest-index member (the argmax member); empty records carry
-            // index 2^24 - 1 and member 0 (never changes: the padding dist is -1)
-            init[bucket] = bucket < nb ? make_float4(wx, wy, wz, __uint_as_float(mi | ((uint32_t)(wl + 64 * sub) << 24)))
-                                       : make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(0xffffffu));
-            if (any_bad) nonfinite = 1;
-        }
-    }
-    __syncthreads();
-    if (wave < S) {  // slot `wave`: lane = bucket within the slot
-        const int bucket = wave * 64 + lane;
-        const bool real = bucket < nb;
-        float lo[3], hi[3], slo[3], shi[3], st[3];
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            lo[a] = real ? box[bucket][a] : INFINITY;
-            hi[a] = real ? box[bucket][3 + a] : -INFINITY;
-            slo[a] = wave_min_dpp(lo[a]);
-            shi[a] = lidar::wave_max_dpp(hi[a]);
-        }
-        bool nof = nonfinite != 0;  // wave-uniform throughout
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            float s = __fdiv_rn(__fsub_rn(shi[a], slo[a]), 255.0f);
-            if (!(isfinite(slo[a]) && isfinite(shi[a]) && isfinite(s))) {
-                nof = true;
-                s = 0.0f;
-            }
-            // the top code must reach the slot's upper bound in the step kernel's own fma
-            for (int k = 0; k < 8 && !nof && __fmaf_rn(255.0f, s, slo[a]) < shi[a]; ++k) s = nextafterf(s, INFINITY);
-            if (!nof && !(__fmaf_rn(255.0f, s, slo[a]) >= shi[a])) nof = true;
-            st[a] = s;
-        }
-        uint32_t ql[3] = {0, 0, 0}, qh[3] = {0, 0, 0};
-        if (!nof && real) {
-#pragma unroll
-            for (int a = 0; a < 3; ++a) {
-                if (st[a] > 0.0f) {
-                    int v = (int)fminf(fmaxf(floorf(__fdiv_rn(__fsub_rn(lo[a], slo[a]), st[a])), 0.0f), 255.0f);
-                    while (v > 0 && __fmaf_rn((float)v, st[a], slo[a]) > lo[a]) --v;  // outward: <= lo
-                    int w = (int)fminf(fmaxf(ceilf(__fdiv_rn(__fsub_rn(hi[a], slo[a]), st[a])), 0.0f), 255.0f);
-                    while (w < 255 && __fmaf_rn((float)w, st[a], slo[a]) < hi[a]) ++w;  // outward: >= hi
-                    ql[a] = (uint32_t)v;
-                    qh[a] = (uint32_t)w;
-                }  // step 0: the slot is one point on this axis, code 0 decodes to it exactly
-            }
-        }
-        qbox[2 * bucket] = ql[0] | (ql[1] << 8) | (ql[2] << 16) | (qh[0] << 24);
-        qbox[2 * bucket + 1] = qh[1] | (qh[2] << 8);
-        if (lane < 10) {
-            const float v = lane < 3 ? slo[lane % 3] : lane < 6 ? shi[lane % 3] : lane < 9 ? st[lane % 3] : (nof ? 1.0f : 0.0f);
-            slotp[wave * 16 + lane] = v;
-        }
-    }
-}
-
-// One round of up to 8 active buckets: lane group g = lane / 8 takes the list entry k + g (the
-// dummy bucket past the list's end), lane j = lane % 8 of it the bucket's points 8 i + j, i < 16
-// (each load instruction reads one 128-B line per group).  All 32 loads of a lane are in flight
-// together; per point the new distance, per lane the max and its lowest index, then a 3-step DPP
-// reduction inside the group gives the bucket's key (max dist bits, lowest index, position).  A
-// bucket whose key changed and is its slot's argmax bucket marks the slot for a re-key.
-__device__ __forceinline__ void group_round(int e, const float4 *__restrict__ P4, float *__restrict__ Dd, int *kd,
-                                            uint32_t *kc, const uint8_t *sbbl, int lane, float qx, float qy, float qz,
-                                            uint32_t &touched)
-{
-    const int j = lane & 7;
-    const int bb = __builtin_amdgcn_ds_bpermute((lane >> 3) << 2, e);  // entry g of the round
-    const uint32_t base = (uint32_t)(bb * kWB + j);
-    float4 P[16];
-    float D[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        P[i] = P4[base + 8 * i];
-        D[i] = Dd[base + 8 * i];
-    }
-    const int old_d = kd[bb];
-    const uint32_t old_c = kc[bb];
-    const int slot_arg = sbbl[bb >> 6];
-    int o[16], best = INT_MIN;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        const float d = lidar::dist2f(P[i].x, P[i].y, P[i].z, qx, qy, qz);
-        // float order: a NaN d (inf - inf) never replaces a dist, as in the oracle
-        const bool lower = d < D[i];
-        o[i] = lower ? __float_as_int(d) : __float_as_int(D[i]);
-        Dd[base + 8 * i] = __int_as_float(o[i]);  // unchanged members rewrite their own dist
-        best = max(best, o[i]);
-    }
-    // the group's max, then the lowest index holding it
-    best = max(best, lidar::dpp_i<0xB1>(best));
-    best = max(best, lidar::dpp_i<0x4E>(best));
-    best = max(best, lidar::dpp_i<0x141>(best));
-    uint32_t mi = 0xffffffffu;
-    int mpos = 0;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        const uint32_t I = __float_as_uint(P[i].w);
-        const bool c = o[i] == best && I < mi;
-        mi = c ? I : mi;
-        mpos = c ? 8 * i + j : mpos;
-    }
-    uint32_t gmi = min(mi, (uint32_t)lidar::dpp_i<0xB1>((int)mi));
-    gmi = min(gmi, (uint32_t)lidar::dpp_i<0x4E>((int)gmi));
-    gmi = min(gmi, (uint32_t)lidar::dpp_i<0x141>((int)gmi));
-    // the holder's position: lanes with mi == gmi hold it (one lane: indices are distinct)
-    int gpos = mi == gmi ? mpos : 0;
-    gpos = max(gpos, lidar::dpp_i<0xB1>(gpos));
-    gpos = max(gpos, lidar::dpp_i<0x4E>(gpos));
-    gpos = max(gpos, lidar::dpp_i<0x141>(gpos));
-    const uint32_t rec = (gmi & 0xffffffu) | ((uint32_t)gpos << 24);
-    if (j == 0) {
-        kd[bb] = best;
-        kc[bb] = rec;
-    }
-    // keys only decrease: a slot's key can change only when its argmax bucket's key did
-    const bool mark = j == 0 && (best != old_d || rec != old_c) && (bb & 63) == slot_arg;
-    uint32_t m = mark ? 1u << (bb >> 6) : 0u;
-    m |= (uint32_t)lidar::dpp_i<0xB1>((int)m);
-    m |= (uint32_t)lidar::dpp_i<0x4E>((int)m);
-    m |= (uint32_t)lidar::dpp_i<0x141>((int)m);
-    m |= (uint32_t)lidar::dpp_i<0x140>((int)m);
-    const auto a = __builtin_amdgcn_permlane32_swap(m, m, false, false);
-    m |= a[0] | a[1];
-    const auto c = __builtin_amdgcn_permlane16_swap(m, m, false, false);
-    m |= c[0] | c[1];
-    touched |= (uint32_t)__builtin_amdgcn_readfirstlane((int)m);
-}
-
-// DIAG builds (lidar_diag_fps_wave only) accumulate, per frame: shader cycles of [0] slot tests and
-// the list, [1] batches, [2] slot re-keys, [3] frame argmax; counts of [4] active slots, [5] active
-// buckets, [6] batches, [7] re-keyed slots, [8] steps
-template <int S, bool DIAG = false>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(128))) void fps_wave_kernel(
-    const float *__restrict__ xyz, int n, int npoint, int32_t *__restrict__ out_idx, float *__restrict__ out_xyz,
-    int32_t *__restrict__ first_zero, const int32_t *__restrict__ prefix_ok, float *__restrict__ ws, int64_t ws_stride,
-    uint64_t *__restrict__ diag)
-{
-    uint64_t dacc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-    uint64_t t0 = 0, t1 = 0;
-    auto tick = [&](int k) {
-        if constexpr (DIAG) {
-            __builtin_amdgcn_sched_barrier(0);
-            t1 = stamp();
-            dacc[k] += t1 - t0;
-            t0 = t1;
-            __builtin_amdgcn_sched_barrier(0);
-        }
-    };
-    constexpr int NBS = S * 64;
-    const int b = blockIdx.x, lane = threadIdx.x;
-    const float *p = xyz + (int64_t)b * n * 3;
-    if (prefix_ok != nullptr && prefix_ok[b] >= npoint) {  // nested FPS shortcut (see the header)
-        for (int i = lane; i < npoint; i += 64) {
-            out_idx[(int64_t)b * npoint + i] = i;
-            if (out_xyz) {
-                float *o = out_xyz + ((int64_t)b * npoint + i) * 3;
-                o[0] = p[3 * i];
-                o[1] = p[3 * i + 1];
-                o[2] = p[3 * i + 2];
-            }
-        }
-        if (first_zero && lane == 0) first_zero[b] = prefix_ok[b];
-        return;
-    }
-    const WaveLayout L = wave_layout(n);
-    float *wsb = ws + (int64_t)b * ws_stride;
-    const float4 *P4 = reinterpret_cast<const float4 *>(wsb + L.p);
-    float *Dd = wsb + L.d;
-    const int nb = L.npad / kWB;  // also the dummy bucket's number
-    __shared__ int kd[NBS + 1];
-    __shared__ uint32_t kc[NBS + 1];  // index | position of the argmax member in the bucket << 24
-    __shared__ uint16_t list[NBS];
-    __shared__ uint8_t sbbl[S];       // each slot's argmax bucket (lane), as sbb below
-    constexpr int kInf = 0x7f800000, kNeg1 = (int)0xbf800000u;
-
-    uint32_t qb0[S], qb1[S];
-    {
-        const uint32_t *qbox = reinterpret_cast<const uint32_t *>(wsb + L.qbox);
-        const float4 *init = reinterpret_cast<const float4 *>(wsb + L.init);
-#pragma unroll
-        for (int q = 0; q < S; ++q) {
-            const int bucket = q * 64 + lane;
-            qb0[q] = qbox[2 * bucket];
-            qb1[q] = qbox[2 * bucket + 1];
-            kd[bucket] = bucket < nb ? kInf : kNeg1;
-            kc[bucket] = __float_as_uint(init[bucket].w);
-        }
-        if (lane == 0) {  // the dummy's record when every bucket of the last slot is real
-            kd[NBS] = kNeg1;
-            kc[NBS] = 0xffffffu;
-        }
-    }
-    // slot q's box lo[3], hi[3], step[3], no-filter flag (LDS: read per step, not held in VGPRs)
-    __shared__ __attribute__((aligned(16))) float slp[S][12];
-    for (int i = lane; i < 10 * S; i += 64) slp[i / 10][i % 10] = wsb[L.slot + (i / 10) * 16 + i % 10];
-    // lane q < S: slot q's key (max dist bits, lowest index), the lane (bucket within the slot) that
-    // holds it and the member's position in that bucket; INT_MIN elsewhere
-    int sbd = INT_MIN, sbb = 0, sbp = 0;
-    uint32_t sbi = 0xffffffffu;
-    auto slot_key = [&](int q) {
-        const int v = kd[q * 64 + lane];
-        const uint32_t r = kc[q * 64 + lane];
-        const uint32_t id = r & 0xffffffu;
-        const int m = wave_max_all(v);
-        const uint64_t c = __ballot(v == m);
-        int wl;
-        if (__popcll(c) == 1) {
-            wl = __ffsll((unsigned long long)c) - 1;
-        } else {
-            const uint32_t mi = wave_min_all_u32(v == m ? id : 0xffffffffu);
-            wl = __ffsll((unsigned long long)__ballot(v == m && id == mi)) - 1;
-        }
-        const uint32_t wr = (uint32_t)__builtin_amdgcn_readlane((int)r, wl);
-        const bool me = lane == q;
-        sbd = me ? m : sbd;
-        sbb = me ? wl : sbb;
-        sbi = me ? (wr & 0xffffffu) : sbi;
-        sbp = me ? (int)(wr >> 24) : sbp;
-        if (lane == 0) sbbl[q] = (uint8_t)wl;
-    };
-#pragma unroll
-    for (int q = 0; q < S; ++q) slot_key(q);
-
-    float qx = p[0], qy = p[1], qz = p[2];
-    if (lane == 0) {
-        out_idx[(int64_t)b * npoint] = 0;
-        if (out_xyz) {
-            float *o = out_xyz + (int64_t)b * npoint * 3;
-            o[0] = qx;
-            o[1] = qy;
-            o[2] = qz;
-        }
-    }
-    int zero_at = npoint;
-    for (int it = 1; it < npoint; ++it) {
-        int lane = threadIdx.x;  // opaque per step: keeps per-slot lane offsets from being hoisted
-        asm volatile("" : "+v"(lane));
-        if constexpr (DIAG) {
-            __builtin_amdgcn_sched_barrier(0);
-            t0 = stamp();
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        // slots whose box may hold a point closer to q than the slot's max
-        const int ls = lane < S ? lane : 0;
-        const float lbs = slp[ls][9] != 0.0f ? 0.0f
-                                             : box_lb(qx, qy, qz, slp[ls][0], slp[ls][1], slp[ls][2], slp[ls][3],
-                                                      slp[ls][4], slp[ls][5]);
-        const uint32_t act = (uint32_t)__ballot(lane < S && __float_as_int(lbs) < sbd);
-        // their buckets' keys (all reads in flight together), then the bucket tests; the active
-        // buckets are appended to the list
-        int kdv[S];
-#pragma unroll
-        for (int q = 0; q < S; ++q)
-            if ((act >> q) & 1u) kdv[q] = kd[q * 64 + lane];
-        int cnt = 0;
-#pragma unroll
-        for (int q = 0; q < S; ++q) {
-            if (!((act >> q) & 1u)) continue;  // wave-uniform
-            const float b0 = slp[q][0], b1 = slp[q][1], b2 = slp[q][2];
-            const float s0 = slp[q][6], s1 = slp[q][7], s2 = slp[q][8];
-            uint32_t w0 = qb0[q], w1 = qb1[q];
-            // opaque per step: otherwise the decoded boxes (6 VGPRs per slot) are hoisted out of
-            // the step loop and the kernel needs ~3x the registers
-            asm volatile("" : "+v"(w0), "+v"(w1));
-            const float lx = __fmaf_rn((float)(w0 & 0xff), s0, b0);
-            const float ly = __fmaf_rn((float)((w0 >> 8) & 0xff), s1, b1);
-            const float lz = __fmaf_rn((float)((w0 >> 16) & 0xff), s2, b2);
-            const float hx = __fmaf_rn((float)(w0 >> 24), s0, b0);
-            const float hy = __fmaf_rn((float)(w1 & 0xff), s1, b1);
-            const float hz = __fmaf_rn((float)((w1 >> 8) & 0xff), s2, b2);
-            float lb = box_lb(qx, qy, qz, lx, ly, lz, hx, hy, hz);
-            if (slp[q][9] != 0.0f) lb = 0.0f;  // no-filter slot: every bucket is tested
-            const uint64_t mk = __ballot(__float_as_int(lb) < kdv[q]);
-            if ((mk >> lane) & 1ull) {
-                const int at = cnt + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32),
-                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u));
-                list[at] = (uint16_t)(q * 64 + lane);
-            }
-            cnt += __popcll(mk);
-        }
-        if constexpr (DIAG) {
-            dacc[4] += __popc(act);
-            dacc[5] += cnt;
-            dacc[6] += (cnt + 7) / 8;
-        }
-        tick(0);
-        uint32_t touched = 0;
-        for (int k = 0; k < cnt; k += 8) {  // wave-uniform
-            const int e = lane < 8 && k + lane < cnt ? (int)list[k + lane] : nb;
-            group_round(e, P4, Dd, kd, kc, sbbl, lane, qx, qy, qz, touched);
-        }
-        tick(1);
-        if constexpr (DIAG) dacc[7] += __popc(touched);
-#pragma unroll
-        for (int q = 0; q < S; ++q)
-            if ((touched >> q) & 1u) slot_key(q);
-        tick(2);
-        // the frame argmax over the slot keys (lanes < S; the rest hold INT_MIN)
-        const int gm = wave_max_all(sbd);
-        const uint64_t gc = __ballot(sbd == gm);
-        int g;
-        if (__popcll(gc) == 1) {
-            g = __ffsll((unsigned long long)gc) - 1;
-        } else {
-            const uint32_t mi = wave_min_all_u32(sbd == gm ? sbi : 0xffffffffu);
-            g = __ffsll((unsigned long long)__ballot(sbd == gm && sbi == mi)) - 1;
-        }
-        {  // the winner's coordinates (one uniform load: the sorted copy is read-only here)
-            const int wb = g * 64 + __builtin_amdgcn_readlane(sbb, g);
-            const float4 W = P4[wb * kWB + __builtin_amdgcn_readlane(sbp, g)];
-            qx = W.x;
-            qy = W.y;
-            qz = W.z;
-        }
-        if (lane == 0) {
-            out_idx[(int64_t)b * npoint + it] = __builtin_amdgcn_readlane((int)sbi, g);
-            if (out_xyz) {
-                float *o = out_xyz + ((int64_t)b * npoint + it) * 3;
-                o[0] = qx;
-                o[1] = qy;
-                o[2] = qz;
-            }
-        }
-        if (zero_at == npoint && gm == 0) zero_at = it;
-        tick(3);
-        if constexpr (DIAG) dacc[8]++;
-    }
-    if (first_zero && lane == 0) first_zero[b] = zero_at;
-    if constexpr (DIAG) {
-        if (lane == 0)
-            for (int k = 0; k < 9; ++k) diag[(int64_t)b * 9 + k] = dacc[k];
-    }
-}
-
 }  // namespace
-
-static int launch_fps_wave(const float *xyz, int64_t batch, int64_t n, int64_t npoint, int32_t *idx, float *new_xyz,
-                           int32_t *first_zero, const int32_t *prefix_ok, float *ws, int64_t stride, hipStream_t s)
-{
-    const WaveLayout L = wave_layout((int)n);
-    hipLaunchKernelGGL(fps_wave_prep_kernel, dim3((unsigned)batch), dim3(1024), 0, s, xyz, (int)n, (int)npoint,
-                       prefix_ok, ws, stride);
-    LAUNCH_CHECK();
-    auto go = [&](auto kern) {
-        hipLaunchKernelGGL(kern, dim3((unsigned)batch), dim3(64), 0, s, xyz, (int)n, (int)npoint, idx, new_xyz,
-                           first_zero, prefix_ok, ws, stride, nullptr);
-    };
-    // batches of 8 buckets (80 VGPRs of loads in flight) up to 8 slots; 4 beside 16 slots' boxes
-    switch (L.S) {
-        case 1: go(fps_wave_kernel<1>); break;
-        case 2: go(fps_wave_kernel<2>); break;
-        case 4: go(fps_wave_kernel<4>); break;
-        case 8: go(fps_wave_kernel<8>); break;
-        default: go(fps_wave_kernel<16>); break;
-    }
-    LAUNCH_CHECK();
-    return LIDAR_OK;
-}
-
-static int64_t fps_stride(int64_t n)
-{
-    const int64_t old = 5 * (int64_t)lidar::align_up(n, 64);
-    const int64_t wave = (n + kWB - 1) / kWB <= kWaveMaxSlots * 64 ? wave_layout((int)n).total : 0;
-    return (int64_t)lidar::align_up((uint64_t)std::max(old, wave), 64);
-}
 
 template <int T>
 static int launch_fps(const float *xyz, int64_t batch, int64_t n, int64_t npoint, int32_t *idx, float *new_xyz,
@@ -1060,11 +540,10 @@ static int launch_fps(const float *xyz, int64_t batch, int64_t n, int64_t npoint
 // workspace bytes lidar_fps_f32 / lidar_fps_ex_f32 take from the handle for (batch, n)
 LIDAR_EXPORT uint64_t lidar_fps_workspace_bytes(int64_t batch, int64_t n)
 {
-    return (uint64_t)(batch * fps_stride(n)) * 4;
+    return (uint64_t)(batch * lidar::align_up(5 * lidar::align_up(n, 64), 64)) * 4;
 }
 
-// threads: workgroup size per frame — 0 (auto: the one-wave kernel up to 65 536 points, 1024
-// threads above), 64 (one wavefront per frame), 1024 or 512 — same results
+// threads: workgroup size per frame, 0 (the build default, 1024), 1024 or 512 — same results
 LIDAR_EXPORT int lidar_fps_ex_f32(lidar_handle *h, const float *xyz, int64_t batch, int64_t n, int64_t npoint,
                                   int32_t *idx, float *new_xyz, int32_t *first_zero, const int32_t *prefix_ok,
                                   int32_t threads, void *stream)
@@ -1072,21 +551,17 @@ LIDAR_EXPORT int lidar_fps_ex_f32(lidar_handle *h, const float *xyz, int64_t bat
     REQUIRE(h && xyz && idx, "lidar_fps_f32: null pointer");
     REQUIRE(batch >= 0 && n >= 1 && npoint >= 1, "lidar_fps_f32: need n >= 1 and npoint >= 1");
     REQUIRE(n <= 4 * 65536, "lidar_fps_f32: n > 262144 points per frame");
-    const int64_t nb = (n + 63) / 64, nbw = (n + kWB - 1) / kWB;
-    if (threads == 0) threads = nbw <= kWaveMaxSlots * 64 ? 64 : kThreads;
-    REQUIRE(threads == 1024 || threads == 512 || threads == 64, "lidar_fps_ex_f32: threads must be 0, 64, 512 or 1024");
-    REQUIRE(threads == 64 ? nbw <= kWaveMaxSlots * 64 : nb <= 8 * (int64_t)threads,
-            "lidar_fps_f32: too many buckets for this workgroup size");
+    if (threads == 0) threads = kThreads;
+    REQUIRE(threads == 1024 || threads == 512, "lidar_fps_ex_f32: threads must be 0, 512 or 1024");
+    REQUIRE((n + 63) / 64 <= 8 * (int64_t)threads, "lidar_fps_f32: too many buckets for this workgroup size");
     REQUIRE(batch <= 0x7fffffff, "lidar_fps_f32: batch too large");
     if (batch == 0) return LIDAR_OK;
     ON_DEVICE(h->device);
     REQUIRE(prefix_ok == nullptr || npoint <= n, "lidar_fps_f32: prefix_ok needs npoint <= n");
-    const int64_t stride = fps_stride(n);
+    int64_t stride = lidar::align_up(5 * lidar::align_up(n, 64), 64);
     float *ws = static_cast<float *>(lidar::workspace(h, (uint64_t)(batch * stride) * 4));
     if (!ws) return LIDAR_ENOMEM;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    if (threads == 64)
-        return launch_fps_wave(xyz, batch, n, npoint, idx, new_xyz, first_zero, prefix_ok, ws, stride, s);
     if (threads == 512)
         return launch_fps<512>(xyz, batch, n, npoint, idx, new_xyz, first_zero, prefix_ok, ws, stride, s);
     return launch_fps<1024>(xyz, batch, n, npoint, idx, new_xyz, first_zero, prefix_ok, ws, stride, s);
@@ -1099,32 +574,13 @@ LIDAR_EXPORT int lidar_fps_f32(lidar_handle *h, const float *xyz, int64_t batch,
     return lidar_fps_ex_f32(h, xyz, batch, n, npoint, idx, new_xyz, first_zero, prefix_ok, 0, stream);
 }
 
-// diagnostic build (not part of the product ABI): per-frame phase cycles and counts of the one-wave
-// FPS (65 536-point frames: 8 slots), diag (batch, 9) u64
-LIDAR_EXPORT int lidar_diag_fps_wave(lidar_handle *h, const float *xyz, int64_t batch, int64_t n, int64_t npoint,
-                                     int32_t *idx, uint64_t *diag, void *stream)
-{
-    REQUIRE(h && xyz && idx && diag && n <= 65536 && n > 32768 && npoint >= 1, "lidar_diag_fps_wave: bad args");
-    ON_DEVICE(h->device);
-    const int64_t stride = fps_stride(n);
-    float *ws = static_cast<float *>(lidar::workspace(h, (uint64_t)(batch * stride) * 4));
-    if (!ws) return LIDAR_ENOMEM;
-    hipStream_t s = static_cast<hipStream_t>(stream);
-    hipLaunchKernelGGL(fps_wave_prep_kernel, dim3((unsigned)batch), dim3(1024), 0, s, xyz, (int)n, (int)npoint,
-                       nullptr, ws, stride);
-    hipLaunchKernelGGL((fps_wave_kernel<8, true>), dim3((unsigned)batch), dim3(64), 0, s, xyz, (int)n, (int)npoint,
-                       idx, nullptr, nullptr, nullptr, ws, stride, diag);
-    LAUNCH_CHECK();
-    return LIDAR_OK;
-}
-
 // diagnostic build (not part of the product ABI): per-wave phase cycle totals of one FPS run
 LIDAR_EXPORT int lidar_diag_fps_phases(lidar_handle *h, const float *xyz, int64_t batch, int64_t n,
                                        int64_t npoint, int32_t *idx, uint64_t *diag, void *stream)
 {
     REQUIRE(h && xyz && idx && diag && n <= 65536 && n >= 1 && npoint >= 1, "lidar_diag_fps_phases: bad args");
     ON_DEVICE(h->device);
-    const int64_t stride = fps_stride(n);
+    int64_t stride = lidar::align_up(5 * lidar::align_up(n, 64), 64);
     float *ws = static_cast<float *>(lidar::workspace(h, (uint64_t)(batch * stride) * 4));
     if (!ws) return LIDAR_ENOMEM;
     REQUIRE((n + 63) / 64 <= kThreads, "lidar_diag_fps_phases: n too large for BPL=1");

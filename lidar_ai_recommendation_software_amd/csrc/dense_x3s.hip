@@ -31,9 +31,19 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int SBM = 128, SBN = 128, SBK = 32;
-constexpr int kPlaneStage = SBM * SBK;    // bf16 per plane per A stage (8 KiB)
-constexpr int kStageB = 4 * 2 * 2 * 512;  // bf16 per B stage (16 KiB)
+#ifndef DENSE_SBK
+#define DENSE_SBK 32
+#endif
+constexpr int SBM = 128, SBN = 128, SBK = DENSE_SBK;  // K per LDS stage: 32 (64 KiB of LDS) or 16 (32 KiB)
+constexpr int NSS = SBK / 16;                        // MFMA k-steps per stage
+constexpr int CPR = SBK / 8;                         // 16-byte chunks per A row and plane
+constexpr int kPlaneStage = SBM * SBK;               // bf16 per plane per A stage
+constexpr int kStageB = 4 * 2 * NSS * 512;           // bf16 per B stage
+static_assert(SBK == 16 || SBK == 32, "DENSE_SBK must be 16 or 32");
+// chunk swizzle: row r's chunk q sits at slot q ^ sw(r), so a fragment read (32 consecutive rows,
+// one chunk) hits 16 distinct 16-byte bank groups per 16 lanes
+__device__ __forceinline__ int swz(int r) { return CPR == 4 ? (r >> 2) & 3 : (r >> 3) & 1; }
+__device__ __forceinline__ int swzf(int r) { return CPR == 4 ? (r >> 1) & 7 : (r >> 2) & 3; }  // fp32 rows
 
 __host__ __device__ constexpr int rho(int r) { return (r & 3) + 8 * (r >> 2); }
 
@@ -86,38 +96,42 @@ __global__ __launch_bounds__(256, 2) void dense_x3s_kernel(const __bf16 *__restr
     if (logical >= total) return;                           // whole workgroup
     const int64_t row0 = logical / ntn * SBM;
     const int tn = (int)(logical % ntn);
-    const int nst = ks / 2;
+    // stages that hold k < kdim (a 16-deep stage past kdim would be all padding: zero weights, and
+    // for fp32 rows a read past the row)
+    const int nst = (kdim + SBK - 1) / SBK;
 
-    // A: wave w loads plane w >> 1, rows 64 (w & 1) .. +63: 4 instructions of 16 rows x 64 B;
-    // lane i of instruction t fills slot i & 3 of row 16 t + (i >> 2) with chunk slot ^ f(row)
+    // A: wave w loads plane w >> 1, rows 64 (w & 1) .. +63: CPR instructions of 64 / CPR rows;
+    // lane i of instruction t fills slot i % CPR of row (64 / CPR) t + i / CPR with chunk slot ^ swz(row)
     const int pl = wave >> 1, rbase = 64 * (wave & 1);
     const __bf16 *ap = a + pl * a_plane;
     const float *af = reinterpret_cast<const float *>(a);
     auto load_stage = [&](int st, int buf) {
         const int k0 = st * SBK;
-        if constexpr (AF32) {  // wave w: rows 32 w .. 32 w + 31, 4 instructions of 8 rows x 128 B
+        if constexpr (AF32) {  // wave w: rows 32 w .. 32 w + 31 of 2 CPR 16-byte chunks, CPR instructions
+            constexpr int CF = 2 * CPR, RPI = 64 / CF;
             float *dst = reinterpret_cast<float *>(&As[buf][0][0]);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int r = 32 * wave + 8 * i + (lane >> 3);
-                const int kq = (lane & 7) ^ ((r >> 1) & 7);
+            for (int i = 0; i < CPR; ++i) {
+                const int r = 32 * wave + RPI * i + lane / CF;
+                const int kq = (lane % CF) ^ swzf(r);
                 // chunks at or past k (the weights there are zero) re-read the stage's first
                 // chunk: finite, in bounds, and no stale LDS in the products
                 const int kc = k0 + 4 * kq < kdim ? k0 + 4 * kq : k0;
-                lds_dma16(af + (row0 + r) * lda + kc, dst + (32 * wave + 8 * i) * SBK);
+                lds_dma16(af + (row0 + r) * lda + kc, dst + (32 * wave + RPI * i) * SBK);
             }
         } else {
+            constexpr int RPI = 64 / CPR;
 #pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                const int r = rbase + 16 * t + (lane >> 2);
-                const int q = (lane & 3) ^ ((r >> 2) & 3);
-                lds_dma16(ap + (row0 + r) * lda + k0 + 8 * q, &As[buf][pl][(rbase + 16 * t) * SBK]);
+            for (int t = 0; t < CPR; ++t) {
+                const int r = rbase + RPI * t + lane / CPR;
+                const int q = (lane % CPR) ^ swz(r);
+                lds_dma16(ap + (row0 + r) * lda + k0 + 8 * q, &As[buf][pl][(rbase + RPI * t) * SBK]);
             }
         }
-        // B: wave w loads column tile 4 tn + w, k-steps 2 st, 2 st + 1, hi / lo: 4 KiB contiguous
-        const __bf16 *src = wp + (((int64_t)(4 * tn + wave) * ks + 2 * st) * 2) * 512;
+        // B: wave w loads column tile 4 tn + w, k-steps NSS st .. NSS st + NSS - 1, hi / lo (contiguous)
+        const __bf16 *src = wp + (((int64_t)(4 * tn + wave) * ks + NSS * st) * 2) * 512;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) lds_dma16(src + i * 512 + lane * 8, &Bs[buf][(wave * 4 + i) * 512]);
+        for (int i = 0; i < 2 * NSS; ++i) lds_dma16(src + i * 512 + lane * 8, &Bs[buf][(wave * 2 * NSS + i) * 512]);
     };
 
     f32x16 acc[2][2] = {};
@@ -127,7 +141,7 @@ __global__ __launch_bounds__(256, 2) void dense_x3s_kernel(const __bf16 *__restr
         __syncthreads();  // (vmcnt(0)) stage st landed everywhere; buf ^ 1 no longer read
         if (st + 1 < nst) load_stage(st + 1, buf ^ 1);
 #pragma unroll
-        for (int ss = 0; ss < 2; ++ss) {
+        for (int ss = 0; ss < NSS; ++ss) {
             bf16x8 xh[2], xl[2], wh[2], wl[2];
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
@@ -135,21 +149,21 @@ __global__ __launch_bounds__(256, 2) void dense_x3s_kernel(const __bf16 *__restr
                 if constexpr (AF32) {
                     const float *as = reinterpret_cast<const float *>(&As[buf][0][0]);
                     const int kq = 4 * ss + 2 * h;
-                    const int sl = kq ^ ((r >> 1) & 7);  // kq even: the pair (sl, sl ^ 1)
+                    const int sl = kq ^ swzf(r);  // kq even: the pair (sl, sl ^ 1)
                     const f32x4 a0 = *reinterpret_cast<const f32x4 *>(as + r * SBK + 4 * sl);
                     const f32x4 a1 = *reinterpret_cast<const f32x4 *>(as + r * SBK + 4 * (sl ^ 1));
                     split8(a0, a1, xh[i], xl[i]);
                 } else {
-                    const int slot = (2 * ss + h) ^ ((r >> 2) & 3);
-                    xh[i] = *reinterpret_cast<const bf16x8 *>(&As[buf][0][(r * 4 + slot) * 8]);
-                    xl[i] = *reinterpret_cast<const bf16x8 *>(&As[buf][1][(r * 4 + slot) * 8]);
+                    const int slot = (2 * ss + h) ^ swz(r);
+                    xh[i] = *reinterpret_cast<const bf16x8 *>(&As[buf][0][(r * CPR + slot) * 8]);
+                    xl[i] = *reinterpret_cast<const bf16x8 *>(&As[buf][1][(r * CPR + slot) * 8]);
                 }
             }
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
                 const int tt = 2 * wn + j;
-                wh[j] = *reinterpret_cast<const bf16x8 *>(&Bs[buf][((tt * 2 + ss) * 2 + 0) * 512 + lane * 8]);
-                wl[j] = *reinterpret_cast<const bf16x8 *>(&Bs[buf][((tt * 2 + ss) * 2 + 1) * 512 + lane * 8]);
+                wh[j] = *reinterpret_cast<const bf16x8 *>(&Bs[buf][((tt * NSS + ss) * 2 + 0) * 512 + lane * 8]);
+                wl[j] = *reinterpret_cast<const bf16x8 *>(&Bs[buf][((tt * NSS + ss) * 2 + 1) * 512 + lane * 8]);
             }
 #pragma unroll
             for (int i = 0; i < 2; ++i)
@@ -262,7 +276,7 @@ static int dense_x3s_launch(lidar_handle *h, const void *a_planes, int64_t a_pla
     REQUIRE(rows % SBM == 0 && k > 0 && k <= lda && cout % SBN == 0 && cout > 0,
             "lidar_dense_x3s_f32: rows % 128, k <= lda, cout % 128 must hold");
     // split planes: lda = k rounded up to 32 (zeros past k); fp32 rows: any row stride, k % 4
-    REQUIRE(af32 ? (k % 4 == 0 && lda % 4 == 0) : lda == (k + SBK - 1) / SBK * SBK,
+    REQUIRE(af32 ? (k % 4 == 0 && lda % 4 == 0) : lda == (k + 31) / 32 * 32,
             "lidar_dense_x3s_f32: planes need lda = k rounded up to 32; fp32 rows need k % 4 == 0 and lda % 4 == 0");
     REQUIRE(af32 || (a_plane >= rows * lda && a_plane % 8 == 0),
             "lidar_dense_x3s_f32: a_plane < rows * lda or not 16-B aligned");
@@ -273,7 +287,7 @@ static int dense_x3s_launch(lidar_handle *h, const void *a_planes, int64_t a_pla
             "lidar_dense_x3s_f32: the max-pool needs relu and pool_rows a multiple of 128 dividing rows");
     if (rows == 0) return LIDAR_OK;
     ON_DEVICE(h->device);
-    const int ks = (k + SBK - 1) / SBK * 2;  // the packed image of a (k, cout) layer covers ceil(k/32)*2 k-steps
+    const int ks = (k + 31) / 32 * 2;  // the packed image of a (k, cout) layer covers ceil(k/32)*2 k-steps
     const int ntn = cout / SBN;
     const int64_t total = (rows / SBM) * ntn, per_xcd = (total + 7) / 8;
     REQUIRE(per_xcd * 8 <= 0x7fffffff, "lidar_dense_x3s_f32: too many rows");

@@ -97,9 +97,11 @@ __device__ __forceinline__ void update_batch(uint64_t &mask, const FrameWs &W, i
     bool redo[K];
 #pragma unroll
     for (int u = 0; u < K; ++u) {
-        const float d = lidar::dist2f(P[u].x, P[u].y, P[u].z, qx, qy, qz);
-        const bool lower = d < D[u];  // float order: a NaN d (inf - inf) never replaces a dist, as in the oracle
-        od[u] = lower ? __float_as_int(d) : __float_as_int(D[u]);
+        // d >= +0 or NaN; the sign bit cleared, a NaN d (inf - inf) orders above every dist and never
+        // replaces one, as in the oracle (a bare bit compare let a negative NaN in)
+        const int db = __float_as_int(lidar::dist2f(P[u].x, P[u].y, P[u].z, qx, qy, qz)) & 0x7fffffff;
+        od[u] = min(db, __float_as_int(D[u]));
+        const bool lower = od[u] != __float_as_int(D[u]);
         if (lower) W.d[pos[u]] = __int_as_float(od[u]);  // only changed members dirty a line
         const uint64_t ch = __ballot(lower);
         const int bpu = __builtin_amdgcn_readlane(bp, bbs[u]);

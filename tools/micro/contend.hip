@@ -60,6 +60,43 @@ __global__ __launch_bounds__(64) void occupy1(int us, float *sink)
     if (s == -1.0f) sink[0] = s;
 }
 
+// coalesced traffic without CU footprint: one wave per workgroup reads DEPTH random 1-KiB chunks
+// (16 B per lane, like an FPS bucket's float4 records) per round trip from a buffer far larger than
+// the Infinity Cache, until `us` microseconds have passed
+template <int DEPTH>
+__global__ __launch_bounds__(64) void stream1k(const float4 *buf, unsigned nchunks, int us, float *sink,
+                                               unsigned long long *rounds)
+{
+    const long long w0 = wall_clock64();
+    unsigned r = 2654435761u * (blockIdx.x + 1);
+    float acc = 0.0f;
+    unsigned long long nr = 0;
+    while (wall_clock64() - w0 < (long long)us * 100) {
+        ++nr;
+        float4 v[DEPTH];
+#pragma unroll
+        for (int k = 0; k < DEPTH; ++k) {
+            r = r * 1664525u + 1013904223u;
+            v[k] = buf[(size_t)(r % nchunks) * 64 + threadIdx.x];
+        }
+#pragma unroll
+        for (int k = 0; k < DEPTH; ++k) acc += v[k].x;
+    }
+    if (acc == -1.0f) sink[0] = acc;
+    if (threadIdx.x == 0) atomicAdd(rounds, nr);
+}
+
+extern "C" int contend_stream(const void *buf, unsigned nchunks, int blocks, int depth, int us, float *sink,
+                              unsigned long long *rounds, void *stream)
+{
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const float4 *b = static_cast<const float4 *>(buf);
+    if (depth == 1) hipLaunchKernelGGL(stream1k<1>, dim3(blocks), dim3(64), 0, st, b, nchunks, us, sink, rounds);
+    if (depth == 4) hipLaunchKernelGGL(stream1k<4>, dim3(blocks), dim3(64), 0, st, b, nchunks, us, sink, rounds);
+    if (depth == 16) hipLaunchKernelGGL(stream1k<16>, dim3(blocks), dim3(64), 0, st, b, nchunks, us, sink, rounds);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 extern "C" int contend_chase(const unsigned *next, int blocks, int us, unsigned *sink, void *stream)
 {
     hipLaunchKernelGGL(chase, dim3(blocks), dim3(64), 0, static_cast<hipStream_t>(stream), next, 12345u, us, sink);

@@ -53,6 +53,24 @@ def with_side(launch):
 
 alone = main_ms()
 print(f"main chain alone                         {alone:7.2f} ms")
+lib.contend_stream.argtypes = [ctypes.c_void_p, ctypes.c_uint, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                               ctypes.c_void_p, ctypes.c_void_p]
+rounds = torch.zeros(1, dtype=torch.int64, device=dev)
+big = torch.empty(1 << 30, dtype=torch.uint8, device=dev)  # 1 GiB: 1 M chunks of 1 KiB
+# the traffic rate each side load generates alone (chunks per second x 1 KiB), then main beside it
+for blocks, depth in ((256, 1), (256, 4), (512, 4), (256, 16), (512, 16)):
+    torch.cuda.synchronize()
+    rounds.zero_()
+    lib.contend_stream(ctypes.c_void_p(big.data_ptr()), 1 << 20, blocks, depth, 20000, ctypes.c_void_p(sink.data_ptr()),
+                       ctypes.c_void_p(rounds.data_ptr()), ctypes.c_void_p(side.cuda_stream))
+    torch.cuda.synchronize()
+    gbs = rounds.item() * depth * 1024 / 20e-3 / 1e9
+    t = with_side(lambda: lib.contend_stream(ctypes.c_void_p(big.data_ptr()), 1 << 20, blocks, depth, 60000,
+                                             ctypes.c_void_p(sink.data_ptr()), ctypes.c_void_p(rounds.data_ptr()),
+                                             ctypes.c_void_p(side.cuda_stream)))
+    print(f"beside stream ({blocks:3d} one-wave workgroups, {depth:2d} x 1 KiB per round trip, {gbs:6.0f} GB/s alone)"
+          f" {t:7.2f} ms", flush=True)
+del big
 for blocks in (128, 256, 512):
     t = with_side(lambda: lib.contend_chase(ctypes.c_void_p(perm.data_ptr()), blocks, 60000,
                                             ctypes.c_void_p(sink.data_ptr()), ctypes.c_void_p(side.cuda_stream)))

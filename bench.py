@@ -574,7 +574,22 @@ def main():
         torch.cuda.synchronize(dev)
         bb.timers = None
         standalone = st.totals()
-        del xg
+        # SA1's fused kernel answers its ball queries itself; the same MLP on precomputed indices (the
+        # separate grid query, then lidar_sa_group_mlp_x3 over the index tensor) decomposes its time
+        lvl0 = bb.levels[0]["branches"][0]
+        fz1 = torch.empty(xg.shape[0], dtype=torch.int32, device=dev)
+        idx1, nx1 = pn.farthest_point_sample(xg, N // bb.levels[0]["div"], return_xyz=True, first_zero=fz1)
+        st2 = pn._Timers()
+        bb.timers = st2
+        for _ in range(3):
+            gidx1 = pn._call(st2, "sa1_ball_query", xg.shape[0], pn.ball_query, lvl0["r"], lvl0["ns"], xg, nx1)
+            bb.forward_from_sa1_fps(xg, idx1, nx1, fz1, gidx1=[gidx1])
+        torch.cuda.synchronize(dev)
+        bb.timers = None
+        t2 = st2.totals()
+        standalone["sa1_group_mlp_given_idx"] = t2["sa1_group_mlp"]
+        standalone["sa1_ball_query_separate"] = t2["sa1_ball_query"]
+        del xg, idx1, nx1, fz1, gidx1
     extras = {}
     if not args.no_extras:
         # the other BASELINE.json configs, measured the same way (not the headline metric)
@@ -597,6 +612,22 @@ def main():
         host = host_frame_leg(seed_rank, world, cpu=cpu)
     work = ssg_kernel_work(N)
     pmc = pmc_per_frame(N)
+
+    def sa1_split(totals):
+        """The fused SA1 kernel's time (ball queries + MLP, standalone) against the same MLP on
+        precomputed indices: the difference is what answering the queries costs inside it."""
+        if not totals or "sa1_group_mlp_given_idx" not in totals:
+            return None
+        f_l, f_f, f_ms = totals["sa1_group_mlp"]
+        m_l, m_f, m_ms = totals["sa1_group_mlp_given_idx"]
+        q_l, q_f, q_ms = totals["sa1_ball_query_separate"]
+        per_frame = work["sa1_group_mlp"][1]
+        return {"fused_ms_per_launch": f_ms / f_l, "mlp_given_idx_ms_per_launch": m_ms / m_l,
+                "query_ms_inside_fused": f_ms / f_l - m_ms / m_l, "separate_query_ms_per_launch": q_ms / q_l,
+                "frames_per_launch": f_f / f_l, "mlp_only_frac": per_frame * m_f / (m_ms / 1e3) / 1e12 / X3_PEAK_TFLOPS,
+                "fused_frac": per_frame * f_f / (f_ms / 1e3) / 1e12 / X3_PEAK_TFLOPS,
+                "basis": "one forward() over a group's frames, nothing else on the chip; the MLP on given indices "
+                         "is lidar_sa_group_mlp_x3 over the (B, M, 32) index tensor of the separate grid query"}
 
     def roof(name, totals):
         """Roofline of one kernel over the launches `totals` recorded: achieved = the algorithmic
@@ -681,6 +712,7 @@ def main():
             "roofline_all": {k: roof(k, tot) for k in tot if k in work},
             "roofline_standalone": ({k: roof(k, standalone) for k in standalone if k in work}
                                     if standalone else None),
+            "sa1_fused_split": sa1_split(standalone),
             "kernel_ms_per_launch": per_launch,
             "distributed": group,
             "pipeline": {"executor": "pointnet2.StreamingSSG feed (steady state: the window pushes and completes "

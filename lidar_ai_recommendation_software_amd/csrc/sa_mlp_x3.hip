@@ -161,13 +161,17 @@ __global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float 
     float mx[T3 / 4];
 #pragma unroll
     for (int j = 0; j < T3 / 4; ++j) mx[j] = -INFINITY;
-    __shared__ int qidx[BQ ? 4 : 1][BQ ? NS : 1];             // this wave's ball-query result
-    __shared__ int qhits[BQ ? 4 : 1][BQ ? kBqCap + 4 : 1];    // its per-window hit list
+    // windows hold ~NS expected hits, so their candidates (27 cells of side >= r) scale with NS:
+    // about 220 at NS = 32 (SSG SA1), about 900 at NS = 128 (MSG's r = 0.4 branch), which past
+    // the cap would fall back to an index-order scan of the whole window
+    constexpr int QCAP = NS >= 128 ? 2 * kBqCap : kBqCap;
+    __shared__ int qidx[BQ ? 4 : 1][BQ ? NS : 1];           // this wave's ball-query result
+    __shared__ int qhits[BQ ? 4 : 1][BQ ? QCAP + 4 : 1];    // its per-window hit list
     if constexpr (BQ) {
         const float *pf = P + (int64_t)b * n * 3;
         const char *fw = grid_ws + b * lidar_bq::grid_frame_bytes(n);
-        lidar_bq::grid_query_wave<kBqCap>(pf, fw, n, Q[cc * 3], Q[cc * 3 + 1], Q[cc * 3 + 2], r, r2, NS, lane,
-                                          qhits[wave], &qidx[wave][0]);
+        lidar_bq::grid_query_wave<QCAP>(pf, fw, n, Q[cc * 3], Q[cc * 3 + 1], Q[cc * 3 + 2], r, r2, NS, lane,
+                                        qhits[wave], &qidx[wave][0]);
     }
     __syncthreads();
     if constexpr (BQ)

@@ -269,7 +269,7 @@ def test_dense_no_relu(cuda):
     feat_close(pn.dense(T(x), T(w), T(b), relu=False).cpu().numpy(), x @ w + b, "dense no relu")
 
 
-@pytest.mark.parametrize("rows,k,cout,pool", [(256, 144, 128, 0), (512, 272, 256, 0), (1024, 512, 1024, 512),
+@pytest.mark.parametrize("rows,k,cout,pool", [(256, 144, 128, 0), (512, 272, 256, 0), (1024, 512, 1024, 512), (768, 272, 256, 256),
                                               (384, 16, 128, 128), (2048, 256, 512, 1024), (128, 48, 384, 0)])
 def test_dense_x3s(cuda, rows, k, cout, pool):
     """split-plane GEMM (all three output modes) vs the fp32 numpy product at 1e-4."""

@@ -263,7 +263,11 @@ def tier_r_leg(dev, rank, world, frames=32, n=65536, steps=3, cpu=True, cpu_budg
                                          "signed sums + 2 emulated sums of squares at ~0.2 of a pass), frames in "
                                          "parallel (one workgroup each), so the launch time is one frame's chain",
                            "hbm_frac": DENSITY_BYTES_PER_POINT["preprocess"] * pts
-                                       / (per_launch_ms["preprocess"] / 1e3) / 1e9 / HBM_PEAK_GBS}
+                                       / (per_launch_ms["preprocess"] / 1e3) / 1e9 / HBM_PEAK_GBS,
+                           # one frame's 65 536-row chain in a 1 024-thread workgroup, wall time
+                           # (tools/micro/seq_chain.hip): the dependent adds alone, and fed from LDS
+                           # in the kernel's 16-row batches (the form block_seq_chain runs)
+                           "in_situ_ns_per_row": {"adds_only": 4.04, "lds_fed": 5.8}}
     elif dom in DENSITY_BYTES_PER_POINT:
         algo = DENSITY_BYTES_PER_POINT[dom] * pts
         a = algo / (per_launch_ms[dom] / 1e3) / 1e9

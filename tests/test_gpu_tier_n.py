@@ -451,21 +451,27 @@ def test_streaming_native_fp32_matches_forward(cuda):
         assert torch.equal(a, b)
 
 
-def test_bench_shape_executor_vs_oracle(cuda):
+@pytest.mark.parametrize("G,l2", [(3, False), (4, True)])
+def test_bench_shape_executor_vs_oracle(cuda, G, l2):
     """BASELINE configs[3]'s per-GPU share through the bench's executor: 32-frame batches of
-    65 536 points, groups of 3 batches (one 96-frame FPS launch), 3 groups in flight, 512-thread
-    FPS, ramped groups over 6 batches (1, 2, 3: the third group is a full 96-frame launch).
-    Frames 0, 31, 64 and 95 of that launch vs the oracle: FPS and ball-query indices bit-exact
-    at both SA levels, features and the global feature 1e-4."""
+    65 536 points, groups of G batches (one 32 G-frame FPS launch), 3 groups in flight, 512-thread
+    FPS, SA1 ball queries binned on the side streams and answered inside the MLP kernel, ramped
+    groups (1, 2, .., G: the last group is a full launch).  G = 4 with SA2's nested FPS and ball
+    queries on the side streams (l2_side) is the driver's `--steps 20` shape, 128-frame launches.
+    The first, last and two middle frames of that launch vs the oracle: FPS and ball-query indices
+    bit-exact at both SA levels, features and the global feature 1e-4."""
     B, N = 32, 65536
+    nb = G * (G + 1) // 2
     bb = pn.PointNet2Backbone(pn.SSG, device=cuda, seed=0)
-    xs = [torch.from_numpy(unit_frames(B, N, 900 + s)).to(cuda) for s in range(6)]
-    got = pn.StreamingSSG(bb, B, N, depth=3, fps_group=3, fps_threads=512, keep_levels=True).run(xs)
+    xs = [torch.from_numpy(unit_frames(B, N, 900 + s)).to(cuda) for s in range(nb)]
+    got = pn.StreamingSSG(bb, B, N, depth=3, fps_group=G, fps_threads=512, keep_levels=True, bq="bin",
+                          l2_side=l2).run(xs)
     torch.cuda.synchronize()
-    assert len(got) == 6
+    assert len(got) == nb
     lv_cfg = pn.resolve(pn.SSG, N)
-    for gf in (0, 31, 64, 95):
-        bi, f = 3 + gf // B, gf % B
+    first = nb - G  # the full group's first batch
+    for gf in (0, B - 1, 2 * B, G * B - 1):
+        bi, f = first + gf // B, gf % B
         g, levels = got[bi]
         x = xs[bi][f].cpu().numpy()
         want, wl = tier_n.sa_stack(x, {"levels": lv_cfg}, bb.weights)

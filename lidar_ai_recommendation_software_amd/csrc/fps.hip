@@ -576,7 +576,9 @@ LIDAR_EXPORT int lidar_fps_f32(lidar_handle *h, const float *xyz, int64_t batch,
     return lidar_fps_ex_f32(h, xyz, batch, n, npoint, idx, new_xyz, first_zero, prefix_ok, 0, stream);
 }
 
-// diagnostic build (not part of the product ABI): per-wave phase cycle totals of one FPS run
+#ifdef LIDAR_DIAG
+// diagnostic build only (`make diag`, not part of the product library or ABI): per-wave phase cycle
+// totals of one FPS run
 LIDAR_EXPORT int lidar_diag_fps_phases(lidar_handle *h, const float *xyz, int64_t batch, int64_t n,
                                        int64_t npoint, int32_t *idx, uint64_t *diag, void *stream)
 {
@@ -592,3 +594,4 @@ LIDAR_EXPORT int lidar_diag_fps_phases(lidar_handle *h, const float *xyz, int64_
     LAUNCH_CHECK();
     return LIDAR_OK;
 }
+#endif

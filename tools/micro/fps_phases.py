@@ -4,7 +4,8 @@ frames and waves: [0] bucket tests + active-bucket updates (loads, distances, DP
 [1] wave argmax + LDS publish, [2] barrier wait, [3] 16-way merge, plus active-bucket batches per
 wave-step, and the same for the first / last 256 steps.
 
-usage: python tools/micro/fps_phases.py [B] [N] [M]"""
+usage (the diagnostic library, `make -C lidar_ai_recommendation_software_amd/csrc diag`):
+LIDAR_AMD_LIB=lidar_ai_recommendation_software_amd/liblidar_amd_diag.so python tools/micro/fps_phases.py [B] [N] [M]"""
 import ctypes
 import os
 import sys

@@ -1,6 +1,7 @@
 """Per-section shader-clock stamps of preprocess_kernel (a LIDAR_PRE_DIAG build of liblidar_amd.so,
 selected with LIDAR_AMD_LIB): one 65 536-point uniform frame.  usage:
-LIDAR_AMD_LIB=abl/libprediag.so python tools/micro/pre_phases.py"""
+LIDAR_AMD_LIB=lidar_ai_recommendation_software_amd/liblidar_amd_diag.so python tools/micro/pre_phases.py
+(`make -C lidar_ai_recommendation_software_amd/csrc diag` builds it)"""
 import os
 import sys
 

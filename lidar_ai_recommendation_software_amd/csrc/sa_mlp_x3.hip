@@ -364,6 +364,13 @@ __global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float 
 // PFX: the centre's NS point indices come in one coalesced load at the start (lane l holds rows
 // l, 64 + l, ...), and a tile's 16 row indices by ds_bpermute from those registers, so a tile's
 // gather of P rows waits on one memory round trip instead of two dependent ones (idx, then P).
+//
+// LIDAR_SA_ABL (diagnostic builds only, tools/micro/sa2_ablate.py; 0 in the product): bit 1 drops the
+// weight streaming after the first two chunks, bit 2 the per-pass barriers, bit 4 the row gather
+// (every tile reads rows 0..15 of its frame) — wrong results, for pricing each part of a pass
+#ifndef LIDAR_SA_ABL
+#define LIDAR_SA_ABL 0
+#endif
 template <int C1, int C2, int C3, int NS, bool PFX>
 __global__ __launch_bounds__(256, 4) void sa_x3_lean_kernel(const float *__restrict__ P, int64_t stride,
                                                             const float *__restrict__ Q,
@@ -398,6 +405,8 @@ __global__ __launch_bounds__(256, 4) void sa_x3_lean_kernel(const float *__restr
 
     // pass `seq` of an iteration: layer-2 chunk seq % NL2 for tile seq / NL2, then the layer-3 chunks
     auto fetch = [&](int seq, int dst) {
+        if constexpr ((LIDAR_SA_ABL & 1) != 0)
+            if (seq > 1 || dst != seq) return;
         const int c = seq < R * NL2 ? seq % NL2 : seq - R * NL2 + NL2;
         const uint4 *src = c < NL2 ? W2 + c * CH2 : W3 + (c - NL2) * CH3;
         asm volatile("" : "+s"(src));
@@ -417,6 +426,7 @@ __global__ __launch_bounds__(256, 4) void sa_x3_lean_kernel(const float *__restr
         for (int j = 0; j < NS / 64; ++j) kall[j] = idx[cc * NS + 64 * j + lane];
     }
     fetch(0, 0);
+    if constexpr ((LIDAR_SA_ABL & 1) != 0) fetch(1, 1);
     for (int i = tid; i < C2 + C3; i += 256) bias_s[i] = Bias[C1 + i];
     __syncthreads();
     float mx[T3 / 4];
@@ -436,7 +446,9 @@ __global__ __launch_bounds__(256, 4) void sa_x3_lean_kernel(const float *__restr
                 asm volatile("" : "+v"(zero));
                 const int t16 = (it * R + rr) * 16;  // the tile's first row
                 int64_t k;
-                if constexpr (PFX)
+                if constexpr ((LIDAR_SA_ABL & 4) != 0)
+                    k = col;
+                else if constexpr (PFX)
                     k = __shfl(kall[t16 >> 6], (t16 & 63) + col, 64);
                 else
                     k = idx[cc * NS + t16 + col];
@@ -479,7 +491,7 @@ __global__ __launch_bounds__(256, 4) void sa_x3_lean_kernel(const float *__restr
                     a1[r] = relu_i(a1[r]);
                 }
                 split_pair(a0, a1, zh[rr][c], zl[rr][c]);  // layer-2 chunk c = layer-3 k-step c
-                __syncthreads();
+                if constexpr ((LIDAR_SA_ABL & 2) == 0) __syncthreads();
                 par ^= 1;
             }
         }
@@ -518,7 +530,7 @@ __global__ __launch_bounds__(256, 4) void sa_x3_lean_kernel(const float *__restr
                 v = max_row_groups(v);
                 if (q == (t & 3)) mx[t >> 2] = __builtin_elementwise_maximum(mx[t >> 2], v);
             }
-            __syncthreads();
+            if constexpr ((LIDAR_SA_ABL & 2) == 0) __syncthreads();
             par ^= 1;
         }
     }

@@ -86,8 +86,13 @@ __global__ __launch_bounds__(256, 2) void dense_x3s_kernel(const __bf16 *__restr
                                                            int64_t per_xcd, int kdim)
 {
     constexpr bool TRANS = MODE != 2;
-    __shared__ __attribute__((aligned(16))) __bf16 As[2][2][kPlaneStage];
-    __shared__ __attribute__((aligned(16))) __bf16 Bs[2][kStageB];
+    // the two stage buffers are separate LDS variables (distinct alias scopes) and the stage loop is
+    // unrolled by two, so a stage's reads need not wait for the next stage streaming into the other
+    // buffer (with one array indexed by st & 1 the compiler waited for the stage it had just issued)
+    __shared__ __attribute__((aligned(16))) __bf16 As0[2][kPlaneStage], As1[2][kPlaneStage];
+    __shared__ __attribute__((aligned(16))) __bf16 Bs0[kStageB], Bs1[kStageB];
+    auto Asb = [&](int buf) { return buf ? As1 : As0; };
+    auto Bsb = [&](int buf) { return buf ? Bs1 : Bs0; };
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int h = lane >> 5, col = lane & 31;
     const int wm = wave >> 1, wn = wave & 1;
@@ -109,7 +114,7 @@ __global__ __launch_bounds__(256, 2) void dense_x3s_kernel(const __bf16 *__restr
         const int k0 = st * SBK;
         if constexpr (AF32) {  // wave w: rows 32 w .. 32 w + 31 of 2 CPR 16-byte chunks, CPR instructions
             constexpr int CF = 2 * CPR, RPI = 64 / CF;
-            float *dst = reinterpret_cast<float *>(&As[buf][0][0]);
+            float *dst = reinterpret_cast<float *>(&Asb(buf)[0][0]);
 #pragma unroll
             for (int i = 0; i < CPR; ++i) {
                 const int r = 32 * wave + RPI * i + lane / CF;
@@ -125,21 +130,18 @@ __global__ __launch_bounds__(256, 2) void dense_x3s_kernel(const __bf16 *__restr
             for (int t = 0; t < CPR; ++t) {
                 const int r = rbase + RPI * t + lane / CPR;
                 const int q = (lane % CPR) ^ swz(r);
-                lds_dma16(ap + (row0 + r) * lda + k0 + 8 * q, &As[buf][pl][(rbase + RPI * t) * SBK]);
+                lds_dma16(ap + (row0 + r) * lda + k0 + 8 * q, &Asb(buf)[pl][(rbase + RPI * t) * SBK]);
             }
         }
         // B: wave w loads column tile 4 tn + w, k-steps NSS st .. NSS st + NSS - 1, hi / lo (contiguous)
         const __bf16 *src = wp + (((int64_t)(4 * tn + wave) * ks + NSS * st) * 2) * 512;
 #pragma unroll
-        for (int i = 0; i < 2 * NSS; ++i) lds_dma16(src + i * 512 + lane * 8, &Bs[buf][(wave * 2 * NSS + i) * 512]);
+        for (int i = 0; i < 2 * NSS; ++i) lds_dma16(src + i * 512 + lane * 8, &Bsb(buf)[(wave * 2 * NSS + i) * 512]);
+        __builtin_amdgcn_sched_barrier(0);  // issued before the stage's reads and MFMAs
     };
 
     f32x16 acc[2][2] = {};
-    load_stage(0, 0);
-    for (int st = 0; st < nst; ++st) {
-        const int buf = st & 1;
-        __syncthreads();  // (vmcnt(0)) stage st landed everywhere; buf ^ 1 no longer read
-        if (st + 1 < nst) load_stage(st + 1, buf ^ 1);
+    auto compute = [&](int buf) {
 #pragma unroll
         for (int ss = 0; ss < NSS; ++ss) {
             bf16x8 xh[2], xl[2], wh[2], wl[2];
@@ -147,7 +149,7 @@ __global__ __launch_bounds__(256, 2) void dense_x3s_kernel(const __bf16 *__restr
             for (int i = 0; i < 2; ++i) {
                 const int r = wm * 64 + i * 32 + col;
                 if constexpr (AF32) {
-                    const float *as = reinterpret_cast<const float *>(&As[buf][0][0]);
+                    const float *as = reinterpret_cast<const float *>(&Asb(buf)[0][0]);
                     const int kq = 4 * ss + 2 * h;
                     const int sl = kq ^ swzf(r);  // kq even: the pair (sl, sl ^ 1)
                     const f32x4 a0 = *reinterpret_cast<const f32x4 *>(as + r * SBK + 4 * sl);
@@ -155,15 +157,15 @@ __global__ __launch_bounds__(256, 2) void dense_x3s_kernel(const __bf16 *__restr
                     split8(a0, a1, xh[i], xl[i]);
                 } else {
                     const int slot = (2 * ss + h) ^ swz(r);
-                    xh[i] = *reinterpret_cast<const bf16x8 *>(&As[buf][0][(r * CPR + slot) * 8]);
-                    xl[i] = *reinterpret_cast<const bf16x8 *>(&As[buf][1][(r * CPR + slot) * 8]);
+                    xh[i] = *reinterpret_cast<const bf16x8 *>(&Asb(buf)[0][(r * CPR + slot) * 8]);
+                    xl[i] = *reinterpret_cast<const bf16x8 *>(&Asb(buf)[1][(r * CPR + slot) * 8]);
                 }
             }
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
                 const int tt = 2 * wn + j;
-                wh[j] = *reinterpret_cast<const bf16x8 *>(&Bs[buf][((tt * NSS + ss) * 2 + 0) * 512 + lane * 8]);
-                wl[j] = *reinterpret_cast<const bf16x8 *>(&Bs[buf][((tt * NSS + ss) * 2 + 1) * 512 + lane * 8]);
+                wh[j] = *reinterpret_cast<const bf16x8 *>(&Bsb(buf)[((tt * NSS + ss) * 2 + 0) * 512 + lane * 8]);
+                wl[j] = *reinterpret_cast<const bf16x8 *>(&Bsb(buf)[((tt * NSS + ss) * 2 + 1) * 512 + lane * 8]);
             }
 #pragma unroll
             for (int i = 0; i < 2; ++i)
@@ -181,6 +183,17 @@ __global__ __launch_bounds__(256, 2) void dense_x3s_kernel(const __bf16 *__restr
                         acc[i][j] = mfma_bf(xl[i], wh[j], acc[i][j]);
                     }
                 }
+        }
+    };
+    load_stage(0, 0);
+    for (int st = 0; st < nst; st += 2) {
+        __syncthreads();  // (vmcnt(0)) stage st landed everywhere; buffer 1 no longer read
+        if (st + 1 < nst) load_stage(st + 1, 1);
+        compute(0);
+        if (st + 1 < nst) {
+            __syncthreads();  // stage st + 1 landed; buffer 0 no longer read
+            if (st + 2 < nst) load_stage(st + 2, 0);
+            compute(1);
         }
     }
 

@@ -122,7 +122,19 @@ __global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float 
     constexpr int ITERS = NS / (16 * R);
     constexpr int PER = (CHMAX + 255) / 256;
 
-    __shared__ uint4 buf[2][CHMAX];
+    // SPLIT (the fused SA1 kernel): two LDS variables (distinct alias scopes), so a pass's reads of
+    // one buffer need not wait for the weight chunk streaming into the other — with one array the
+    // compiler waited for the chunk it had just issued before the pass's first read.  The other
+    // instantiations keep one array: there the freed schedule hoists reads and costs registers.
+    constexpr bool SPLIT = BQ;
+    __shared__ uint4 bufa[SPLIT ? 1 : 2][CHMAX];
+    __shared__ uint4 bufb[SPLIT ? CHMAX : 1];
+    auto bufp = [&](int p) -> uint4 * {
+        if constexpr (SPLIT)
+            return p ? bufb : bufa[0];
+        else
+            return bufa[p];
+    };
     __shared__ float bias_s[C1 + C2 + C3];
     __shared__ float w1_s[HASW1 ? T1 * 64 : 1];
 
@@ -145,11 +157,12 @@ __global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float 
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
             const int base = 256 * i + 64 * wave;  // scalar: SGPR base + 32-bit lane offset
-            if (base < len)
+            if ((SPLIT && CH2 == CH3 && CH2 % 256 == 0) || base < len)  // equal whole chunks: unconditional
                 __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)(src + base + (unsigned)lane),
-                                                 (__attribute__((address_space(3))) void *)(&buf[dst][base]), 16, 0,
+                                                 (__attribute__((address_space(3))) void *)(&bufp(dst)[base]), 16, 0,
                                                  0);
         }
+        if constexpr (SPLIT) __builtin_amdgcn_sched_barrier(0);  // issued before the pass's reads and MFMAs
     };
     fetch(0, 0);
     for (int i = tid; i < C1 + C2 + C3; i += 256) bias_s[i] = Bias[i];
@@ -242,7 +255,7 @@ __global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float 
             const int cn = c + 1 < NCH ? c + 1 : 0;
             const bool more = c + 1 < NCH || it + 1 < ITERS;
             if (more) fetch(cn, par ^ 1);  // lands during this chunk's MFMAs
-            const uint4 *wb = buf[par] + lane;
+            const uint4 *wb = bufp(par) + lane;
             f32x4 a0[R], a1[R];
             if (c < T2 / 2) {
                 // layer 2 accumulators start at the bias (channel rows: 16t + 4q + r)
@@ -365,8 +378,8 @@ __global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float 
 // l, 64 + l, ...), and a tile's 16 row indices by ds_bpermute from those registers, so a tile's
 // gather of P rows waits on one memory round trip instead of two dependent ones (idx, then P).
 //
-// LIDAR_SA_ABL (diagnostic builds only, tools/micro/sa2_ablate.py; 0 in the product): bit 1 drops the
-// weight streaming after the first two chunks, bit 2 the per-pass barriers, bit 4 the row gather
+// LIDAR_SA_ABL (diagnostic builds only, tools/micro/sa2_ablate.py; 0 in the product): bit 1 streams
+// layer 2's first chunk for every pass (same instructions, one L2-hot 16 KiB source), bit 2 the per-pass barriers, bit 4 the row gather
 // (every tile reads rows 0..15 of its frame) — wrong results, for pricing each part of a pass
 #ifndef LIDAR_SA_ABL
 #define LIDAR_SA_ABL 0
@@ -389,7 +402,8 @@ __global__ __launch_bounds__(256, 4) void sa_x3_lean_kernel(const float *__restr
     constexpr int PER = (CHMAX + 255) / 256;
     static_assert(!PFX || NS % 64 == 0, "PFX: whole 64-row blocks of indices");
 
-    __shared__ uint4 buf[2][CHMAX];
+    __shared__ uint4 buf0[CHMAX], buf1[CHMAX];  // two variables, as in sa_x3_kernel
+    auto bufp = [&](int p) -> uint4 * { return p ? buf1 : buf0; };
     __shared__ float bias_s[C2 + C3];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -405,20 +419,19 @@ __global__ __launch_bounds__(256, 4) void sa_x3_lean_kernel(const float *__restr
 
     // pass `seq` of an iteration: layer-2 chunk seq % NL2 for tile seq / NL2, then the layer-3 chunks
     auto fetch = [&](int seq, int dst) {
-        if constexpr ((LIDAR_SA_ABL & 1) != 0)
-            if (seq > 1 || dst != seq) return;
-        const int c = seq < R * NL2 ? seq % NL2 : seq - R * NL2 + NL2;
+        const int c = (LIDAR_SA_ABL & 1) != 0 ? 0 : seq < R * NL2 ? seq % NL2 : seq - R * NL2 + NL2;
         const uint4 *src = c < NL2 ? W2 + c * CH2 : W3 + (c - NL2) * CH3;
         asm volatile("" : "+s"(src));
         const int len = c < NL2 ? CH2 : CH3;
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
             const int base = 256 * i + 64 * wave;
-            if (base < len)
+            if ((CH2 == CH3 && CH2 % 256 == 0) || base < len)  // equal whole chunks: unconditional, so the waits can count them
                 __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)(src + base + (unsigned)lane),
-                                                 (__attribute__((address_space(3))) void *)(&buf[dst][base]), 16, 0,
+                                                 (__attribute__((address_space(3))) void *)(&bufp(dst)[base]), 16, 0,
                                                  0);
         }
+        __builtin_amdgcn_sched_barrier(0);  // issued before the pass's reads and MFMAs, not sunk to its end
     };
     int32_t kall[PFX ? NS / 64 : 1];
     if constexpr (PFX) {
@@ -426,7 +439,6 @@ __global__ __launch_bounds__(256, 4) void sa_x3_lean_kernel(const float *__restr
         for (int j = 0; j < NS / 64; ++j) kall[j] = idx[cc * NS + 64 * j + lane];
     }
     fetch(0, 0);
-    if constexpr ((LIDAR_SA_ABL & 1) != 0) fetch(1, 1);
     for (int i = tid; i < C2 + C3; i += 256) bias_s[i] = Bias[C1 + i];
     __syncthreads();
     float mx[T3 / 4];
@@ -469,7 +481,7 @@ __global__ __launch_bounds__(256, 4) void sa_x3_lean_kernel(const float *__restr
 #pragma unroll
             for (int c = 0; c < NL2; ++c) {
                 fetch(rr * NL2 + c + 1, par ^ 1);  // a layer-3 pass always follows: lands during these MFMAs
-                const uint4 *wb = buf[par] + lane;
+                const uint4 *wb = bufp(par) + lane;
                 f32x4 a0 = *reinterpret_cast<const f32x4 *>(&bias_s[16 * (2 * c) + 4 * q]);
                 f32x4 a1 = *reinterpret_cast<const f32x4 *>(&bias_s[16 * (2 * c + 1) + 4 * q]);
 #pragma unroll
@@ -498,7 +510,7 @@ __global__ __launch_bounds__(256, 4) void sa_x3_lean_kernel(const float *__restr
 #pragma unroll
         for (int c = 0; c < NL3; ++c) {
             if (c + 1 < NL3 || it + 1 < ITERS) fetch(c + 1 < NL3 ? R * NL2 + c + 1 : 0, par ^ 1);
-            const uint4 *wb = buf[par] + lane;
+            const uint4 *wb = bufp(par) + lane;
             f32x4 a0[R], a1[R];
 #pragma unroll
             for (int rr = 0; rr < R; ++rr) a0[rr] = a1[rr] = f32x4{};

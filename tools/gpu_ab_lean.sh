@@ -1,6 +1,6 @@
-# MFMA kernels (lean SA2, fused SA1, dense_x3s) with each weight chunk / stage issued at the start of a pass and
-# waited for at its end (two LDS variables, unconditional pieces, sched_barrier) against the product build, same box:
-# the Tier N tests on the candidate, the kernel alone (tools/micro/sa2_ablate.py), then the SSG line alternating
+# A/B of a candidate library (tools/ablib/liblidar_cand.so, built from the working tree) against the product build,
+# same box: the Tier N tests on the candidate, the SA2 grouped MLP alone (tools/micro/sa2_ablate.py), then the
+# SSG line with both libraries alternating. Used for the MFMA kernels' double buffering, pass-epilogue deferral and the FPS batch wait.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 O=gpurun_out/abl2; mkdir -p $O

@@ -59,7 +59,18 @@ __global__ __launch_bounds__(64 * WPG, 4) void sa16_kernel(const float *__restri
     static_assert(CH2 % 64 == 0 && CH3 % 64 == 0, "chunks copied in 64-float4 slabs, one per wave");
     static_assert(T2 % 2 == 0 && T3 % 2 == 0, "output tiles come in pairs");
 
-    __shared__ f32x4 buf[2][CHMAX];
+    // two LDS variables (distinct alias scopes) when the chunk count per tile is even, so the buffer of a
+    // pass is a compile-time choice: a pass's reads (and its max-pool stores) then need not wait for the
+    // chunk streaming into the other buffer (as sa_x3_kernel's SPLIT, sa_mlp_x3.hip)
+    constexpr bool SPLIT = NCH % 2 == 0;
+    __shared__ f32x4 bufa[SPLIT ? 1 : 2][CHMAX];
+    __shared__ f32x4 bufb[SPLIT ? CHMAX : 1];
+    auto bufp = [&](int p) -> f32x4 * {
+        if constexpr (SPLIT)
+            return p ? bufb : bufa[0];
+        else
+            return bufa[p];
+    };
     __shared__ float bias_s[C1 + C2 + C3];
     __shared__ float w1_s[XYZ ? T1 * 64 : 1];
     __shared__ float mx_s[WPG][C3];  // running max-pool per wave: kept out of the registers
@@ -85,11 +96,12 @@ __global__ __launch_bounds__(64 * WPG, 4) void sa16_kernel(const float *__restri
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
             const int base = NT * i + 64 * wave;
-            if (base < len)
+            if ((SPLIT && CH2 == CH3 && CH2 % NT == 0) || base < len)  // equal whole chunks: unconditional
                 __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)(src + base + lane),
-                                                 (__attribute__((address_space(3))) void *)(&buf[dst][base]), 16, 0,
+                                                 (__attribute__((address_space(3))) void *)(&bufp(dst)[base]), 16, 0,
                                                  0);
         }
+        if constexpr (SPLIT) __builtin_amdgcn_sched_barrier(0);  // issued before the pass's reads and MFMAs
     };
     fetch(0, 0);
     for (int i = tid; i < C1 + C2 + C3; i += NT) bias_s[i] = Bias[i];
@@ -138,7 +150,7 @@ __global__ __launch_bounds__(64 * WPG, 4) void sa16_kernel(const float *__restri
             const int cn = c + 1 < NCH ? c + 1 : 0;
             const bool more = c + 1 < NCH || tile + 1 < TILES;
             if (more) fetch(cn, par ^ 1);  // lands during this chunk's MFMAs
-            const f32x4 *wb = buf[par] + lane;
+            const f32x4 *wb = bufp(par) + lane;
             f32x4 a0 = {}, a1 = {};
             if (c < T2 / 2) {  // layer 2: output tiles 2c, 2c+1 (channel rows x point columns)
                 constexpr int S = C1 / 4;  // k-steps

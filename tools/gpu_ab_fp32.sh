@@ -1,5 +1,5 @@
-# candidate library (tools/ablib/liblidar_cand.so: split LDS buffers in the strict-fp32 sa16_kernel, the fused SA1
-# kernel held to 80 VGPRs) against the product build: the Tier N tests on the candidate, then the full SSG line
+# candidate library (tools/ablib/liblidar_cand.so; used for: split LDS buffers in the strict-fp32 sa16_kernel, the fused SA1
+# kernel at 80 VGPRs, DENSE_SBK=16 on the double-buffered dense kernels) against the product build: the Tier N tests on the candidate, then the full SSG line
 # (with the fp32-MFMA leg and the standalone legs) with both libraries alternating
 set -o pipefail
 cd $GRAFT_REPO_ROOT

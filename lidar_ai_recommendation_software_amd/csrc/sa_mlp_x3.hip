@@ -102,10 +102,8 @@ __device__ __forceinline__ float max_row_groups(float v)
 #define LIDAR_BQ_CAP 512
 #endif
 constexpr int kBqCap = LIDAR_BQ_CAP;  // candidates per window a fused wave ranks in LDS (more: index-order scan)
-// the fused SSG SA1 kernel (BQ, NS = 32) is held to 80 VGPRs (six waves per SIMD by registers): a SIMD that
-// also holds four FPS waves (2 x 64 VGPRs each of two 512-thread workgroups) then fits three of its waves, not two
 template <int C1, int C2, int C3, int NS, int L1, int R, bool X1, bool BQ = false>
-__global__ __launch_bounds__(256, R == 1 ? 3 : (BQ && NS <= 32 ? 6 : 2)) void sa_x3_kernel(const float *__restrict__ P, int64_t stride,
+__global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float *__restrict__ P, int64_t stride,
                                                      const float *__restrict__ Q, const int32_t *__restrict__ idx,
                                                      int n, int m, int64_t total, const uint4 *__restrict__ packed,
                                                      float *__restrict__ out, int64_t out_stride, int64_t out_offset,

@@ -144,6 +144,23 @@ struct SeqStage {
     double v[2][kSeqRows * 3];
 };
 
+// one staged chunk's rows of the index-order chain of column c (lane c of wave 0): b = the chunk's column c
+template <class Step>
+__device__ __forceinline__ void seq_chain_rows(const double *b, int rows, int c, Step step, double &a0, double &a1)
+{
+    // reads of a 16-row batch first, then its dependent adds (an explicit two-batch
+    // software pipeline measured 2.4x slower: 7.6 vs 3.2 ms per 65k frame)
+    int i = 0;
+    for (; i + kSeqBatch <= rows; i += kSeqBatch) {
+        double v[kSeqBatch];
+#pragma unroll
+        for (int u = 0; u < kSeqBatch; ++u) v[u] = b[3 * (i + u)];
+#pragma unroll
+        for (int u = 0; u < kSeqBatch; ++u) step(c, v[u], a0, a1);
+    }
+    for (; i < rows; ++i) step(c, b[3 * i], a0, a1);
+}
+
 template <class Step>
 __device__ void block_seq_chain(const double *x, int64_t n, SeqStage &st, Step step, double &a0, double &a1)
 {
@@ -164,18 +181,7 @@ __device__ void block_seq_chain(const double *x, int64_t n, SeqStage &st, Step s
         if (tid < 3) {
             const int64_t r0 = k * kSeqRows;
             const int rows = (int)(n - r0 < kSeqRows ? n - r0 : kSeqRows);
-            const double *b = st.v[k & 1] + tid;
-            // reads of a 16-row batch first, then its dependent adds (an explicit two-batch
-            // software pipeline measured 2.4x slower: 7.6 vs 3.2 ms per 65k frame)
-            int i = 0;
-            for (; i + kSeqBatch <= rows; i += kSeqBatch) {
-                double v[kSeqBatch];
-#pragma unroll
-                for (int u = 0; u < kSeqBatch; ++u) v[u] = b[3 * (i + u)];
-#pragma unroll
-                for (int u = 0; u < kSeqBatch; ++u) step(tid, v[u], a0, a1);
-            }
-            for (; i < rows; ++i) step(tid, b[3 * i], a0, a1);
+            seq_chain_rows(st.v[k & 1] + tid, rows, tid, step, a0, a1);
         }
         __syncthreads();
     }
@@ -242,11 +248,95 @@ __device__ __forceinline__ double wave_scan_exact_d(double P)
 // a_q[c] <- fl(a_q[c] + inc(c, q, x[i][c])).  Waves 0 .. 3 NQ - 1 run the chains; the other waves
 // stage 1024-row chunks into LDS (double buffered).  Results land in s.chain[q * 3 + c] (ends with
 // a barrier).
+// one staged chunk's rows of the emulated chain a <- fl(a + inc(c, q, x_i[c])) (one wavefront; b = the chunk's
+// column c; a and forced carry over from chunk to chunk)
+template <class Inc>
+__device__ __forceinline__ void sum_chain_rows(const double *b, int rows, int c, int q, Inc inc, double &a, int &forced)
+{
+    constexpr double kTwo52 = 4503599627370496.0, kTwo53 = 9007199254740992.0, kTwo44 = 17592186044416.0;
+    const int lane = threadIdx.x & 63;
+    int i = 0;
+    while (i < rows) {
+        a = uniform_d(a);
+        i = __builtin_amdgcn_readfirstlane(i);
+        forced = __builtin_amdgcn_readfirstlane(forced);
+        if (forced > 0 || !(fabs(a) >= 2.2250738585072014e-308) || !(fabs(a) < INFINITY)) {
+            // one dadd per row (wave-uniform): near zero, non-finite, or a forced run
+            const int run = forced > 0 ? (forced < rows - i ? forced : rows - i) : 1;
+            int t = 0;
+            for (; t + 8 <= run; t += 8) {
+                double v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) v[u] = inc(c, q, b[3 * (i + t + u)]);
+#pragma unroll
+                for (int u = 0; u < 8; ++u) a = dadd(a, v[u]);
+            }
+            for (; t < run; ++t) a = dadd(a, inc(c, q, b[3 * (i + t)]));
+            i += run;
+            forced = forced > run ? forced - run : 0;
+            continue;
+        }
+        int e2;
+        (void)frexp(a, &e2);  // a = m 2^e2, 0.5 <= |m| < 1
+        const int sh = __builtin_amdgcn_readfirstlane(53 - e2);
+        const double A = ldexp(a, sh);  // |A| in [2^52, 2^53), exact
+        // lane l takes rows i + 4l .. i + 4l + 3: a window of 256 rows per scan
+        double v[kChainRowsPerLane], L[kChainRowsPerLane];
+        bool bad[kChainRowsPerLane], valid[kChainRowsPerLane];
+        double run = 0.0;  // the lane's own prefix of its rounded increments
+#pragma unroll
+        for (int r = 0; r < kChainRowsPerLane; ++r) {
+            const int j = i + kChainRowsPerLane * lane + r;
+            valid[r] = j < rows;
+            v[r] = valid[r] ? inc(c, q, b[3 * j]) : 0.0;
+            const double xs = ldexp(v[r], sh);
+            double kq = rint(xs);
+            bad[r] = valid[r] && (!(fabs(kq) <= kTwo44) || dsub(xs, floor(xs)) == 0.5);
+            if (!valid[r] || bad[r]) kq = 0.0;
+            run = dadd(run, kq);  // integers below 2^46: exact
+            L[r] = run;
+        }
+        // exclusive prefix of the lane totals (<= 256 increments of <= 2^44: below 2^52, exact)
+        const double E = dsub(wave_scan_exact_d(run), run);
+        int first = kChainRowsPerLane;  // the lane's first violating row
+#pragma unroll
+        for (int r = kChainRowsPerLane - 1; r >= 0; --r) {
+            const double Aj = dadd(A, dadd(E, L[r]));  // exact below 2^53; >= 2^53 stays
+            const double sAj = a > 0.0 ? Aj : -Aj;
+            if (valid[r] && (bad[r] || !(sAj > kTwo52 && sAj < kTwo53))) first = r;
+        }
+        const uint64_t vm = __ballot(first < kChainRowsPerLane);
+        const int nv = rows - i < 64 * kChainRowsPerLane ? rows - i : 64 * kChainRowsPerLane;
+        // the accumulator after the rows before window row t (t >= 1), and row t's increment
+        auto after = [&](int t) {
+            const int ln = (t - 1) / kChainRowsPerLane, r = (t - 1) % kChainRowsPerLane;
+            double pick = L[0];
+#pragma unroll
+            for (int u = 1; u < kChainRowsPerLane; ++u) pick = r == u ? L[u] : pick;
+            return ldexp(dadd(A, dadd(readlane_d(E, ln), readlane_d(pick, ln))), -sh);
+        };
+        if (vm == 0) {
+            a = after(nv);
+            i += nv;
+        } else {
+            const int ln = __builtin_amdgcn_readfirstlane(__ffsll((unsigned long long)vm) - 1);
+            const int rv = __builtin_amdgcn_readlane(first, ln);
+            const int j0 = kChainRowsPerLane * ln + rv;
+            if (j0 > 0) a = after(j0);
+            double vj = v[0];
+#pragma unroll
+            for (int u = 1; u < kChainRowsPerLane; ++u) vj = rv == u ? v[u] : vj;
+            a = dadd(a, readlane_d(vj, ln));  // the violating row: the sequential add itself
+            i += j0 + 1;
+            if (j0 < kChainMinRun) forced = kChainSeqRun;
+        }
+    }
+}
+
 template <int NQ, class Inc>
 __device__ void block_sum_chain(const double *x, int64_t n, SeqStage &st, BlockScratch &s, Inc inc)
 {
     constexpr int kCW = 3 * NQ;  // chain waves
-    constexpr double kTwo52 = 4503599627370496.0, kTwo53 = 9007199254740992.0, kTwo44 = 17592186044416.0;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int64_t nch = (n + kSeqRows - 1) / kSeqRows;
     auto stage = [&](int64_t k) {
@@ -268,86 +358,50 @@ __device__ void block_sum_chain(const double *x, int64_t n, SeqStage &st, BlockS
             const int64_t r0 = k * kSeqRows;
             const int rows = (int)(n - r0 < kSeqRows ? n - r0 : kSeqRows);
             const double *b = st.v[k & 1] + c;
-            int i = 0;
-            while (i < rows) {
-                a = uniform_d(a);
-                i = __builtin_amdgcn_readfirstlane(i);
-                forced = __builtin_amdgcn_readfirstlane(forced);
-                if (forced > 0 || !(fabs(a) >= 2.2250738585072014e-308) || !(fabs(a) < INFINITY)) {
-                    // one dadd per row (wave-uniform): near zero, non-finite, or a forced run
-                    const int run = forced > 0 ? (forced < rows - i ? forced : rows - i) : 1;
-                    int t = 0;
-                    for (; t + 8 <= run; t += 8) {
-                        double v[8];
-#pragma unroll
-                        for (int u = 0; u < 8; ++u) v[u] = inc(c, q, b[3 * (i + t + u)]);
-#pragma unroll
-                        for (int u = 0; u < 8; ++u) a = dadd(a, v[u]);
-                    }
-                    for (; t < run; ++t) a = dadd(a, inc(c, q, b[3 * (i + t)]));
-                    i += run;
-                    forced = forced > run ? forced - run : 0;
-                    continue;
-                }
-                int e2;
-                (void)frexp(a, &e2);  // a = m 2^e2, 0.5 <= |m| < 1
-                const int sh = __builtin_amdgcn_readfirstlane(53 - e2);
-                const double A = ldexp(a, sh);  // |A| in [2^52, 2^53), exact
-                // lane l takes rows i + 4l .. i + 4l + 3: a window of 256 rows per scan
-                double v[kChainRowsPerLane], L[kChainRowsPerLane];
-                bool bad[kChainRowsPerLane], valid[kChainRowsPerLane];
-                double run = 0.0;  // the lane's own prefix of its rounded increments
-#pragma unroll
-                for (int r = 0; r < kChainRowsPerLane; ++r) {
-                    const int j = i + kChainRowsPerLane * lane + r;
-                    valid[r] = j < rows;
-                    v[r] = valid[r] ? inc(c, q, b[3 * j]) : 0.0;
-                    const double xs = ldexp(v[r], sh);
-                    double kq = rint(xs);
-                    bad[r] = valid[r] && (!(fabs(kq) <= kTwo44) || dsub(xs, floor(xs)) == 0.5);
-                    if (!valid[r] || bad[r]) kq = 0.0;
-                    run = dadd(run, kq);  // integers below 2^46: exact
-                    L[r] = run;
-                }
-                // exclusive prefix of the lane totals (<= 256 increments of <= 2^44: below 2^52, exact)
-                const double E = dsub(wave_scan_exact_d(run), run);
-                int first = kChainRowsPerLane;  // the lane's first violating row
-#pragma unroll
-                for (int r = kChainRowsPerLane - 1; r >= 0; --r) {
-                    const double Aj = dadd(A, dadd(E, L[r]));  // exact below 2^53; >= 2^53 stays
-                    const double sAj = a > 0.0 ? Aj : -Aj;
-                    if (valid[r] && (bad[r] || !(sAj > kTwo52 && sAj < kTwo53))) first = r;
-                }
-                const uint64_t vm = __ballot(first < kChainRowsPerLane);
-                const int nv = rows - i < 64 * kChainRowsPerLane ? rows - i : 64 * kChainRowsPerLane;
-                // the accumulator after the rows before window row t (t >= 1), and row t's increment
-                auto after = [&](int t) {
-                    const int ln = (t - 1) / kChainRowsPerLane, r = (t - 1) % kChainRowsPerLane;
-                    double pick = L[0];
-#pragma unroll
-                    for (int u = 1; u < kChainRowsPerLane; ++u) pick = r == u ? L[u] : pick;
-                    return ldexp(dadd(A, dadd(readlane_d(E, ln), readlane_d(pick, ln))), -sh);
-                };
-                if (vm == 0) {
-                    a = after(nv);
-                    i += nv;
-                } else {
-                    const int ln = __builtin_amdgcn_readfirstlane(__ffsll((unsigned long long)vm) - 1);
-                    const int rv = __builtin_amdgcn_readlane(first, ln);
-                    const int j0 = kChainRowsPerLane * ln + rv;
-                    if (j0 > 0) a = after(j0);
-                    double vj = v[0];
-#pragma unroll
-                    for (int u = 1; u < kChainRowsPerLane; ++u) vj = rv == u ? v[u] : vj;
-                    a = dadd(a, readlane_d(vj, ln));  // the violating row: the sequential add itself
-                    i += j0 + 1;
-                    if (j0 < kChainMinRun) forced = kChainSeqRun;
-                }
-            }
+            sum_chain_rows(b, rows, c, q, inc, a, forced);
         }
         __syncthreads();
     }
     if (wave < kCW && lane == 0) s.chain[q * 3 + c] = a;
+    __syncthreads();
+}
+
+// both kinds at once over the same staged rows: the index-order chain `step` (lanes 0..2 of wave 0, as
+// block_seq_chain) and the emulated chain of `inc` (waves 1..3, column = wave - 1, as block_sum_chain with
+// NQ = 1, result in s.chain[column]); waves 4.. stage.  One pass instead of two, or instead of a step
+// carrying both: the StandardScaler's second pass (its correction sum stays sequential, its sum of
+// squared deviations is emulated beside it)
+template <class Step, class Inc>
+__device__ void block_seq_sum_chain(const double *x, int64_t n, SeqStage &st, BlockScratch &s, Step step, double &a0,
+                                    double &a1, Inc inc)
+{
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t nch = (n + kSeqRows - 1) / kSeqRows;
+    auto stage = [&](int64_t k) {
+        if (wave < 4 || k >= nch) return;
+        const int64_t r0 = k * kSeqRows;
+        const int64_t cnt = (n - r0 < kSeqRows ? n - r0 : kSeqRows) * 3;
+        double *d = st.v[k & 1];
+        const double *src = x + 3 * r0;
+        for (int64_t e = tid - 256; e < cnt; e += kT - 256) d[e] = src[e];
+    };
+    const int c = wave >= 1 && wave <= 3 ? wave - 1 : 0;
+    double a = 0.0;
+    int forced = 0;
+    stage(0);
+    __syncthreads();
+    for (int64_t k = 0; k < nch; ++k) {
+        stage(k + 1);
+        const int64_t r0 = k * kSeqRows;
+        const int rows = (int)(n - r0 < kSeqRows ? n - r0 : kSeqRows);
+        if (wave == 0) {
+            if (tid < 3) seq_chain_rows(st.v[k & 1] + tid, rows, tid, step, a0, a1);
+        } else if (wave <= 3) {
+            sum_chain_rows(st.v[k & 1] + c, rows, c, 0, inc, a, forced);
+        }
+        __syncthreads();
+    }
+    if (wave >= 1 && wave <= 3 && lane == 0) s.chain[c] = a;
     __syncthreads();
 }
 
@@ -837,14 +891,17 @@ __global__ __launch_bounds__(kT) void preprocess_kernel(const double *__restrict
         if (tid < 3) s.bc[6 + tid] = ddiv(sum, nn);
         __syncthreads();
         const double Tc = tid < 3 ? s.bc[6 + tid] : 0.0;
-        double corr = 0.0, un = 0.0;
-        block_seq_chain(sc, nng, st, [Tc](int, double v, double &cr, double &u) {
-            const double d = dsub(v, Tc);
-            cr = dadd(cr, d);
-            u = dadd(u, dmul(d, d));
-        }, corr, un);
+        // the second pass: sum of deviations (sequential) and, beside it, the sum of their squares (emulated)
+        const double Tw = s.bc[6 + ((tid >> 6) + 2) % 3];  // waves 1..3: the mean of column wave - 1
+        double corr = 0.0, unused2 = 0.0;
+        block_seq_sum_chain(sc, nng, st, s, [Tc](int, double v, double &cr, double &) { cr = dadd(cr, dsub(v, Tc)); },
+                            corr, unused2, [Tw](int, int, double v) {
+                                const double d = dsub(v, Tw);
+                                return dmul(d, d);
+                            });
         if (tid < 3) {
         const double T = Tc;
+        double un = s.chain[tid];
         un = dsub(un, ddiv(dmul(corr, corr), nn));
         const double var = ddiv(un, nn);
         const double e = 2.220446049250313e-16;

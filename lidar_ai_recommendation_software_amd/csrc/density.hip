@@ -281,14 +281,20 @@ __device__ __forceinline__ void sum_chain_rows(const double *b, int rows, int c,
         const int sh = __builtin_amdgcn_readfirstlane(53 - e2);
         const double A = ldexp(a, sh);  // |A| in [2^52, 2^53), exact
         // lane l takes rows i + 4l .. i + 4l + 3: a window of 256 rows per scan
-        double v[kChainRowsPerLane], L[kChainRowsPerLane];
+        double v[kChainRowsPerLane], L[kChainRowsPerLane], raw[kChainRowsPerLane];
         bool bad[kChainRowsPerLane], valid[kChainRowsPerLane];
         double run = 0.0;  // the lane's own prefix of its rounded increments
+        // the window's LDS reads all issued first and unconditionally (rows past the end read row i, and
+        // their values are dropped below): one wait, not one branch and wait per row
 #pragma unroll
         for (int r = 0; r < kChainRowsPerLane; ++r) {
             const int j = i + kChainRowsPerLane * lane + r;
             valid[r] = j < rows;
-            v[r] = valid[r] ? inc(c, q, b[3 * j]) : 0.0;
+            raw[r] = b[3 * (valid[r] ? j : i)];
+        }
+#pragma unroll
+        for (int r = 0; r < kChainRowsPerLane; ++r) {
+            v[r] = valid[r] ? inc(c, q, raw[r]) : 0.0;
             const double xs = ldexp(v[r], sh);
             double kq = rint(xs);
             bad[r] = valid[r] && (!(fabs(kq) <= kTwo44) || dsub(xs, floor(xs)) == 0.5);
@@ -308,12 +314,20 @@ __device__ __forceinline__ void sum_chain_rows(const double *b, int rows, int c,
         const uint64_t vm = __ballot(first < kChainRowsPerLane);
         const int nv = rows - i < 64 * kChainRowsPerLane ? rows - i : 64 * kChainRowsPerLane;
         // the accumulator after the rows before window row t (t >= 1), and row t's increment
+        // (the row choices read every candidate out of lane ln and select among the scalars: a select of
+        // per-row registers with a runtime row made the compiler keep L[] and v[] in scratch memory)
+        auto pick_at = [&](const double (&arr)[kChainRowsPerLane], int ln, int r) {
+            double p = readlane_d(arr[0], ln);
+#pragma unroll
+            for (int u = 1; u < kChainRowsPerLane; ++u) {
+                const double x = readlane_d(arr[u], ln);
+                p = r == u ? x : p;
+            }
+            return p;
+        };
         auto after = [&](int t) {
             const int ln = (t - 1) / kChainRowsPerLane, r = (t - 1) % kChainRowsPerLane;
-            double pick = L[0];
-#pragma unroll
-            for (int u = 1; u < kChainRowsPerLane; ++u) pick = r == u ? L[u] : pick;
-            return ldexp(dadd(A, dadd(readlane_d(E, ln), readlane_d(pick, ln))), -sh);
+            return ldexp(dadd(A, dadd(readlane_d(E, ln), pick_at(L, ln, r))), -sh);
         };
         if (vm == 0) {
             a = after(nv);
@@ -323,10 +337,7 @@ __device__ __forceinline__ void sum_chain_rows(const double *b, int rows, int c,
             const int rv = __builtin_amdgcn_readlane(first, ln);
             const int j0 = kChainRowsPerLane * ln + rv;
             if (j0 > 0) a = after(j0);
-            double vj = v[0];
-#pragma unroll
-            for (int u = 1; u < kChainRowsPerLane; ++u) vj = rv == u ? v[u] : vj;
-            a = dadd(a, readlane_d(vj, ln));  // the violating row: the sequential add itself
+            a = dadd(a, pick_at(v, ln, rv));  // the violating row: the sequential add itself
             i += j0 + 1;
             if (j0 < kChainMinRun) forced = kChainSeqRun;
         }

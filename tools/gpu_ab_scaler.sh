@@ -1,5 +1,5 @@
-# density path: the StandardScaler's second pass as one sequential chain + an emulated sum of squares beside it
-# (product) vs the previous single sequential step carrying both (tools/ablib/liblidar_cand.so), same box:
+# density path A/B, product vs tools/ablib/liblidar_cand.so (used for: the StandardScaler second pass split; the emulated
+# chains' scan without scratch arrays or per-row branches), same box:
 # the Tier R GPU tests on the product, then the bench's density leg alternating
 set -o pipefail
 cd $GRAFT_REPO_ROOT

@@ -51,3 +51,34 @@ def test_pmc_reductions_are_per_pipeline_launch():
         assert v["traffic_bytes"] > 0 and abs(v["traffic_per_frame"] * F - v["traffic_bytes"]) < 1e-3 * v["traffic_bytes"]
     v = json.load(open(_latest("pmc_valu.json")))
     assert v["config"]["frames_per_launch"] == F and v["kernels"]["sa2_group_mlp"]["valu_issue_frac"] is not None
+
+
+def _bench_lines():
+    out = []
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "r03", "*bench*.json"))):
+        line = open(f).readline().strip()
+        if line.startswith("{"):
+            out.append((os.path.relpath(f, REPO), json.loads(line)))
+    return out
+
+
+def test_committed_bench_lines_keep_the_contract():
+    # every committed bench line carries the driver's keys, a self-consistent roofline for the
+    # dominant kernel, the 1-rank CPU baseline and the distributed record of the ranks it saw
+    lines = _bench_lines()
+    if not lines:
+        pytest.skip("no committed bench line")
+    for name, d in lines:
+        for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+                  "scaling", "dtype", "data", "config", "roofline", "cpu_baseline"):
+            assert k in d, f"{name}: missing {k}"
+        r = d["roofline"]
+        assert r["kernel"] == "sa2_group_mlp" and r["bound"] == "mfma"
+        assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-9
+        assert abs(r["achieved"] - r["work_per_launch"] / (r["avg_launch_ms"] * 1e-3) / 1e12) < 1e-6 * r["achieved"]
+        assert 0 < r["frac"] < 1
+        if "distributed" in d:
+            dist = d["distributed"]
+            assert dist["world_size"] == d["n_gpus"] == len(dist["ranks"])
+            if d["cpu_baseline"] is not None:
+                assert d["cpu_baseline"]["value"] > 0 and d["cpu_baseline"]["cores"] >= 1

@@ -51,8 +51,10 @@ class VenueGrid:
 
     def all_reduce(self, group=None):
         """Sum the venue counts over all ranks: one all_reduce(int32, SUM) — RCCL when the process
-        group is "nccl"; gloo reduces a host copy (CPU tests, ranks sharing a GPU)."""
-        if self.backend() is None or dist.get_world_size(group) == 1:
+        group is "nccl"; gloo reduces a host copy (CPU tests, ranks sharing a GPU).  A one-rank
+        group still runs the collective (an identity; one per reporting interval, never per frame),
+        so the RCCL branch is the same code at every world size."""
+        if self.backend() is None:
             return self
         if self.backend() == "nccl":
             dist.all_reduce(self.counts, op=dist.ReduceOp.SUM, group=group)

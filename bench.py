@@ -20,7 +20,16 @@ The input rotates over 8 distinct device-resident batches, and every output of w
 window and drain is checked bit for bit against one-batch forward() of its batch.
 Synthetic data: uniform [-1, 1]^3 float32 frames (seeded per rank), random-init weights.
 
-Run:  python bench.py [--gpus N --steps K --warmup W]  (N>1 via torch.distributed.run)
+Run:  python bench.py [--gpus N --steps K --warmup W]
+With --gpus N > 1 and no torch.distributed.run environment, bench.py starts
+`python -m torch.distributed.run --nproc-per-node N ... bench.py ...` as a CHILD process (before
+anything touches the GPU) and relays its output and exit code; under torch.distributed.run
+(WORLD_SIZE set) every rank checks WORLD_SIZE == --gpus.
+
+Output: the LAST stdout line is a compact JSON record (<= LINE_MAX bytes: the driver keeps only
+the tail of stdout) with the contract keys, the headline roofline, the CPU baseline, the
+precision check and the distributed record; the full record (every kernel's roofline, the
+standalone timings, the density / voxel / host-frame / variant legs) goes to --detail.
 """
 import argparse
 import hashlib
@@ -119,6 +128,148 @@ def cpu_model():
             return next(l.split(":", 1)[1].strip() for l in f if l.startswith("model name"))
     except Exception:
         return platform.processor() or platform.machine()
+
+
+LINE_MAX = 4096  # bytes of the last stdout line (the driver keeps ~8 KB of stdout tail)
+
+
+def _sig(x, digits=4):
+    """Round every float in a JSON-able value to `digits` significant digits."""
+    if isinstance(x, float):
+        return float(f"{x:.{digits}g}") if np.isfinite(x) else None
+    if isinstance(x, dict):
+        return {k: _sig(v, digits) for k, v in x.items()}
+    if isinstance(x, (list, tuple)):
+        return [_sig(v, digits) for v in x]
+    return x
+
+
+def compact_line(rec, detail_path=None):
+    """The driver-facing line: the contract keys of the full record `rec`, the headline roofline
+    and CPU baseline without their long prose, the distributed record, and one number per side
+    measurement.  Optional parts are dropped (last first) until the line fits LINE_MAX bytes."""
+    keep_roof = ("kernel", "bound", "achieved", "peak", "unit", "frac", "traffic", "work_per_launch",
+                 "avg_launch_ms", "launches", "frames", "measured_gbs", "valu_issue_frac")
+    line = {k: rec.get(k) for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                                    "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config")}
+    roof = rec.get("roofline") or {}
+    line["roofline"] = {k: roof[k] for k in keep_roof if k in roof}
+    if roof.get("traffic") is not None:
+        line["roofline"]["traffic_basis"] = "HBM-side bytes per launch, rocprofv3 PMC (FETCH_SIZE x2 + WRITE_SIZE)"
+    cb = rec.get("cpu_baseline")
+    line["cpu_baseline"] = None if cb is None else {
+        "value": cb["value"], "unit": cb["unit"], "cores": cb["cores"], "kind": cb["kind"], "sample": cb["sample"][:200]}
+    line["speedup_vs_cpu"] = rec.get("speedup_vs_cpu")
+    if rec.get("precision") is not None:
+        line["precision"] = rec["precision"]
+    d = rec.get("distributed") or {}
+    line["distributed"] = {"backend": d.get("backend"), "world_size": d.get("world_size"),
+                           "device_count": d.get("device_count"),
+                           "ranks": [[r["rank"], r["device"], r["frames"], r["ms"]] for r in d.get("ranks", [])],
+                           "ranks_cols": ["rank", "device", "frames", "ms"]}
+    optional = []
+    pipe = rec.get("pipeline") or {}
+    if pipe:
+        optional.append(("chains_ms_per_group", {"main": pipe.get("main_ms_per_group"),
+                                                 "side": pipe.get("side_ms_per_group"),
+                                                 "frames_per_launch": pipe.get("frames_per_launch")}))
+    allr = rec.get("roofline_all") or {}
+    if allr:
+        optional.append(("kernels", {k: [v["avg_launch_ms"], v["frac"]] for k, v in allr.items()}))
+        optional.append(("kernels_cols", ["avg_launch_ms", "frac"]))
+    legs = {}
+    if rec.get("fp32_mfma_kernels"):
+        legs["ssg_native_fp32_mfma"] = rec["fp32_mfma_kernels"]["value"]
+    for k, v in (rec.get("other_configs") or {}).items():
+        legs[k] = v["M_points_per_s"]
+    dp_ = rec.get("density_path")
+    if dp_:
+        legs["density_path_32"] = dp_["value"]
+        if dp_.get("wide_batch"):
+            legs["density_path_256"] = dp_["wide_batch"]["value"]
+        if dp_.get("pipelined_batches"):
+            legs["density_path_lanes"] = dp_["pipelined_batches"]["value"]
+        if dp_.get("cpu_baseline"):
+            legs["density_path_cpu_sklearn"] = dp_["cpu_baseline"]["value"]
+        if dp_.get("roofline"):
+            legs["density_roofline_frac"] = dp_["roofline"]["frac"]
+    if rec.get("voxel_downsample"):
+        legs["voxel_downsample"] = rec["voxel_downsample"]["value"]
+        legs["voxel_roofline_frac"] = rec["voxel_downsample"]["roofline"]["frac"]
+    if rec.get("host_frames"):
+        legs["host_frame_feed"] = rec["host_frames"]["host_frame_feed"]["value"]
+    if rec.get("variant_path"):
+        legs["variant_path"] = rec["variant_path"]["value"]
+    if legs:
+        optional.append(("legs_M_points_per_s", legs))
+    if detail_path:
+        optional.insert(0, ("detail", detail_path))
+    for k, v in optional:
+        line[k] = v
+    exact = {k: line[k] for k in ("value", "ms_per_step")}
+    line = _sig(line)
+    line.update(exact)  # the headline numbers at full precision
+    while len(json.dumps(line)) > LINE_MAX and optional:
+        line.pop(optional.pop()[0], None)
+    if len(json.dumps(line)) > LINE_MAX and line.get("cpu_baseline"):
+        line["cpu_baseline"]["sample"] = line["cpu_baseline"]["sample"][:60]
+    return line
+
+
+def launch_ranks(n, argv, script=None):
+    """`--gpus N` outside torch.distributed.run: start N ranks of `script` (this file) as a child
+    `python -m torch.distributed.run` process on 127.0.0.1, relay its stdout line by line, and
+    return its exit code.  The parent never touches the GPU (no exec from a GPU process)."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), script or os.path.abspath(__file__), *argv]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True, bufsize=1)
+    for line in p.stdout:
+        sys.stdout.write(line)
+        sys.stdout.flush()
+    return p.wait()
+
+
+REL_FLOOR = 1e-2  # pure relative error is reported over elements with |want| >= REL_FLOOR * RMS(want)
+
+
+def rel_stats(got, want, rtol=1e-4):
+    """Tier N's feature contract on one array: the max pure relative error over elements with
+    |want| >= REL_FLOOR * RMS, and the max of err / (rtol |want| + rtol RMS) (the tests' feat_close,
+    <= 1 passes)."""
+    got = np.asarray(got, np.float64).ravel()
+    want = np.asarray(want, np.float64).ravel()
+    rms = float(np.sqrt(np.mean(want ** 2))) + 1e-30
+    err = np.abs(got - want)
+    big = np.abs(want) >= REL_FLOOR * rms
+    rel = err[big] / np.abs(want[big]) if big.any() else np.zeros(1)
+    return {"max_rel": float(rel.max()), "n_rel": int(big.sum()), "n": int(want.size),
+            "max_tol_ratio": float((err / (rtol * np.abs(want) + rtol * rms)).max())}
+
+
+def precision_check(bb, xb, cfg, n):
+    """Frame 0 of the bench's first batch through forward(keep_levels) against the fp32 oracle
+    (the checker, in the CPU-baseline leg): per level and for the global feature, rel_stats;
+    FPS indices compared bit for bit."""
+    import torch
+    from oracle import tier_n
+    from lidar_ai_recommendation_software_amd import pointnet2 as pn
+    g, levels = bb.forward(xb, keep_levels=True)
+    torch.cuda.synchronize()
+    x = xb[0].cpu().numpy()
+    want, wl = tier_n.sa_stack(x, {"levels": pn.resolve(cfg, n)}, bb.weights)
+    out = {"contract": "max |got-want|/|want| over |want| >= 1e-2 RMS, and max err/(1e-4|want| + 1e-4 RMS)",
+           "frame": "batch 0 frame 0", "fps_exact": True}
+    for li, ((nx, nf, ni, _), (ox, of, oi)) in enumerate(zip(levels, wl)):
+        out["fps_exact"] &= bool(np.array_equal(ni[0].cpu().numpy(), oi))
+        out[f"level{li + 1}"] = rel_stats(nf[0].cpu().numpy(), of)
+    out["global"] = rel_stats(g[0].cpu().numpy(), want)
+    return out
 
 
 def cpu_baseline(n, budget_s=20.0):
@@ -304,7 +455,7 @@ def tier_r_leg(dev, rank, world, frames=32, n=65536, steps=3, cpu=True, cpu_budg
                                     "value": sharding.aggregate_rate(wide * n * steps, world, elp) / 1e6,
                                     "unit": "M points/s", "ms_per_batch": elp / (steps * len(bl)) * 1e3}
         del xw, bl
-    if cpu and rank == 0 and world == 1:
+    if cpu and rank == 0:
         rec["cpu_baseline"] = tier_r_cpu_baseline(n, cpu_budget)
         rec["speedup_vs_cpu"] = rec["value"] / rec["cpu_baseline"]["value"]
     # SURVEY §8e's optional global density: every frame's people binned into one fixed venue grid
@@ -389,7 +540,7 @@ def voxel_leg(dev, rank, world, B=32, n=65536, voxel=0.05, steps=20, cpu=True):
                         "work_per_launch": algo, "avg_launch_ms": per_launch * 1e3,
                         "peak_basis": "HBM peak; algorithmic bytes (the radix sort moves ~5x more)"},
            "cpu_baseline": None}
-    if cpu and rank == 0 and world == 1:
+    if cpu and rank == 0:
         from oracle import tier_n
         xs = x[:2].cpu().numpy()
         t0 = time.perf_counter()
@@ -422,7 +573,7 @@ def variant_leg(rank, world, frames=8, n=65536, cpu=True, cpu_budget=6.0):
            "points_per_frame": n, "frames": frames, "data": "synthetic crowd frames (people clumps, metres)",
            "parity": "byte-identical to scikit-learn's DBSCAN / KDTree results (tests/golden/variant.json)",
            "cpu_baseline": None}
-    if cpu and rank == 0 and world == 1:
+    if cpu and rank == 0:
         from oracle import tier_r
         k, t0 = 0, time.perf_counter()
         while True:
@@ -482,7 +633,15 @@ def main():
     ap.add_argument("--no-verify", action="store_true",
                     help="skip the one-batch forward() references and the bit-equality check of every pipeline "
                          "output (PMC passes: only the pipeline's own launches are then counted)")
+    ap.add_argument("--detail", default=os.path.join(REPO, "gpurun_out", "bench_detail.json"),
+                    help="file for the full record (rank 0); the last stdout line is the compact one")
     args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # N ranks, one per GPU: a child torch.distributed.run, started before any GPU call
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if int(os.environ.get("WORLD_SIZE", "1")) != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={os.environ.get('WORLD_SIZE', '1')}")
 
     import torch
     import torch.distributed as dist
@@ -697,13 +856,14 @@ def main():
             "value": value, "unit": "M points/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "f32" + (" (MLP products as split-bf16 x3 MFMA products, fp32 accumulation)" if args.x3 else ""),
-            "precision": ("fp32 inputs/weights/outputs; SA layers 2-3, SA2's per-point layer 1 and group_all: each "
-                          "fp32 operand split exactly into bf16 hi+lo, products ah*bh + ah*bl + al*bh accumulated in "
-                          "fp32 (<= ~2^-15 per product); SA1 layer 1 (K = 3) on fp32 MFMA; features within the 1e-4 "
-                          "rel contract of the fp32 oracle (tests/test_gpu_tier_n.py::test_group_mlp_x3, "
-                          "test_dense_x3s, test_backbone_vs_oracle, test_bench_shape_executor_vs_oracle)")
-                         if args.x3 else "fp32 MFMA (v_mfma_f32_*_f32)",
+            "dtype": "f32",
+            "arithmetic": ("fp32 inputs/weights/outputs; SA layers 2-3, SA2's per-point layer 1 and group_all: each "
+                           "fp32 operand split exactly into bf16 hi+lo, products ah*bh + ah*bl + al*bh accumulated in "
+                           "fp32 (<= ~2^-15 per product); SA1 layer 1 (K = 3) on fp32 MFMA; features within the 1e-4 "
+                           "rel contract of the fp32 oracle (tests/test_gpu_tier_n.py::test_group_mlp_x3, "
+                           "test_dense_x3s, test_backbone_vs_oracle, test_bench_shape_executor_vs_oracle)")
+                          if args.x3 else "fp32 MFMA (v_mfma_f32_*_f32)",
+            "precision": None,
             "data": "synthetic: uniform [-1,1]^3 float32 frames (seeded per rank, %d distinct batches cycled), "
                     "random-init SSG weights" % max(1, args.rotate),
             "config": {"workload": "PointNet++ SSG encoder (SA1 N/16 r0.2 ns32 [64,64,128]; "
@@ -731,10 +891,22 @@ def main():
             "voxel_downsample": voxel,
             "cpu_baseline": None,
         }
-        if world == 1 and not args.no_cpu_baseline:
+        if not args.no_cpu_baseline:
+            # rank 0 at every world size, after the timed windows (the other ranks wait at the
+            # final barrier); the oracle also checks frame 0 of the bench's first batch
             rec["cpu_baseline"] = cpu_baseline(N, args.cpu_budget)
             rec["speedup_vs_cpu"] = value / rec["cpu_baseline"]["value"]
-        print(json.dumps(rec), flush=True)
+            rec["precision"] = precision_check(bb, xs[0], pn.SSG, N)
+        detail = None
+        if args.detail:
+            try:
+                os.makedirs(os.path.dirname(os.path.abspath(args.detail)), exist_ok=True)
+                with open(args.detail, "w") as f:
+                    json.dump(rec, f, indent=1)
+                detail = os.path.relpath(os.path.abspath(args.detail), REPO)
+            except OSError as e:
+                print(f"bench.py: could not write {args.detail}: {e}", file=sys.stderr)
+        print(json.dumps(compact_line(rec, detail)), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -231,20 +231,24 @@ int lidar_sa_group_mlp_bq_f32(lidar_handle *h, int32_t x1, const float *xyz, con
 int lidar_concat_xyz_pad_f32(lidar_handle *h, const float *xyz, int64_t rows, float *y,
                              int64_t ldy, int64_t col0, void *stream);
 
-/* voxel downsample: per-point voxel id (rank of its voxel key, ascending), centroids
- * (sequential fp32 sums in point order / count), counts; *nvox_host receives V
- * (synchronises `stream`).  centroids/counts must hold n entries. */
-int lidar_voxel_downsample_f32(lidar_handle *h, const float *xyz, int64_t n, float voxel,
+/* voxel downsample.  The voxel of a point is calculate_grid_density's grid hash
+ * (utils/data_processing.py:305-319) per axis: edges np.arange(lo - 2v, (hi + 2v) + v, v) over the
+ * frame's extent, histogram2d's searchsorted-right binning with the last edge closed; key =
+ * (bx*ny + by)*nz + bz.  Per-point voxel id (rank of its key, ascending; -1 outside every bin),
+ * centroids (sequential fp32 sums in point order / count), counts; *nvox_host receives V
+ * (synchronises `stream`).  centroids/counts must hold n entries.  LIDAR_EINVAL when the extent
+ * is not finite or the grid has 2^32 keys or more. */
+int lidar_voxel_downsample_f32(lidar_handle *h, const float *xyz, int64_t n, double voxel,
                                int32_t *voxel_id, float *centroids, int32_t *counts,
                                int64_t *nvox_host, void *stream);
 
 /* Voxel downsampling of `batch` frames of n points over the whole chip (csrc/voxel_batch.hip):
  * xyz (batch, n, 3) fp32; voxel_id (batch, n) int32; centroids (batch, n, 3) and counts (batch, n),
- * the first nvox[f] rows of frame f valid; nvox (batch,) int32 on the device (-1: the frame's grid
- * exceeds 2^32 keys).  No host synchronisation; per frame equal to lidar_voxel_downsample_f32.
- * Workspace: lidar_voxel_batch_workspace_bytes(batch, n) (for lidar_reserve). */
+ * the first nvox[f] rows of frame f valid; nvox (batch,) int32 on the device (-1: the frame's extent
+ * is not finite or its grid has 2^32 keys or more).  No host synchronisation; per frame equal to
+ * lidar_voxel_downsample_f32.  Workspace: lidar_voxel_batch_workspace_bytes(batch, n). */
 uint64_t lidar_voxel_batch_workspace_bytes(int64_t batch, int64_t n);
-int lidar_voxel_downsample_batch_f32(lidar_handle *h, const float *xyz, int64_t batch, int64_t n, float voxel,
+int lidar_voxel_downsample_batch_f32(lidar_handle *h, const float *xyz, int64_t batch, int64_t n, double voxel,
                                      int32_t *voxel_id, float *centroids, int32_t *counts, int32_t *nvox,
                                      void *stream);
 

@@ -1,9 +1,10 @@
 // voxel.hip — voxel downsampling on gfx950 (north_star "voxel hashing").
 //
-// Spec (oracle tier_n.voxel_downsample): v = floor((p - min(p)) / voxel)
-// per axis in fp32 (one rounding per op), key = (vx*Dy + vy)*Dz + vz with D = max(v)+1,
-// voxels in ascending key order, per-point voxel id = rank of its key, centroid =
-// sequential fp32 sum of the voxel's points in point order / count.
+// Spec (voxel_grid.hpp, oracle tier_n.voxel_downsample): per axis the bins of
+// calculate_grid_density (utils/data_processing.py:305-319: np.arange edges over the frame's
+// extent with the 2-cell margin, histogram2d's searchsorted-right rule, last edge closed), key =
+// (bx*ny + by)*nz + bz, voxels in ascending key order, per-point voxel id = rank of its key (-1
+// outside every bin), centroid = sequential fp32 sum of the voxel's points in point order / count.
 //
 // Pipeline (one frame): bbox -> keys -> stable LSD radix sort of (key, index) in one
 // 1024-thread workgroup (8-bit digits; the stable in-wave rank comes from 8 ballots per
@@ -12,63 +13,67 @@
 // the sort is stable).  HBM-bound integer work: no float reductions besides the
 // centroid sums, whose order is part of the spec.
 #include "common.hpp"
+#include "voxel_grid.hpp"
 
 namespace {
 
 constexpr int kT = 1024;
 constexpr int kW = kT / 64;
 
-__global__ __launch_bounds__(kT) void voxel_keys_kernel(const float *__restrict__ xyz, int64_t n, float voxel,
+__global__ __launch_bounds__(kT) void voxel_keys_kernel(const float *__restrict__ xyz, int64_t n, double voxel,
                                                         uint32_t *__restrict__ key, uint32_t *__restrict__ idx,
                                                         uint32_t *__restrict__ meta)
 {
-    __shared__ float red[3][kW];
-    __shared__ int ired[3][kW];
+    __shared__ float red[6][kW];
+    __shared__ int anyout;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    float lo[3] = {INFINITY, INFINITY, INFINITY};
-    for (int64_t i = tid; i < n; i += kT)
-        for (int a = 0; a < 3; ++a) lo[a] = fminf(lo[a], xyz[3 * i + a]);
-    for (int a = 0; a < 3; ++a) {
-        float v = lidar::wave_min_f(lo[a]);
-        if (lane == 0) red[a][wave] = v;
-    }
-    __syncthreads();
-    for (int a = 0; a < 3; ++a) {
-        float v = red[a][0];
-        for (int w = 1; w < kW; ++w) v = fminf(v, red[a][w]);
-        lo[a] = v;
-    }
-    int hi[3] = {0, 0, 0};
+    // the extent: numpy's min / max (a NaN anywhere makes it NaN: no finite grid)
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    bool nan = false;
     for (int64_t i = tid; i < n; i += kT)
         for (int a = 0; a < 3; ++a) {
-            const float q = __fdiv_rn(__fsub_rn(xyz[3 * i + a], lo[a]), voxel);
-            hi[a] = max(hi[a], (int)floorf(q));
+            const float v = xyz[3 * i + a];
+            nan |= v != v;
+            lo[a] = fminf(lo[a], v);
+            hi[a] = fmaxf(hi[a], v);
         }
+    if (tid == 0) anyout = 0;
     for (int a = 0; a < 3; ++a) {
-        int v = hi[a];
-        for (int m = 32; m >= 1; m >>= 1) v = max(v, __shfl_xor(v, m, 64));
-        if (lane == 0) ired[a][wave] = v;
+        const float v = lidar::wave_min_f(lo[a]), w = -lidar::wave_min_f(-hi[a]);
+        if (lane == 0) {
+            red[a][wave] = v;
+            red[3 + a][wave] = w;
+        }
     }
+    if (__ballot(nan) && lane == 0) red[0][wave] = NAN;
     __syncthreads();
-    uint32_t dim[3];
+    double dlo[3], dhi[3];
     for (int a = 0; a < 3; ++a) {
-        int v = ired[a][0];
-        for (int w = 1; w < kW; ++w) v = max(v, ired[a][w]);
-        dim[a] = (uint32_t)v + 1u;
+        float v = red[a][0], w = red[3 + a][0];
+        for (int q = 1; q < kW; ++q) {
+            v = (v != v || red[a][q] != red[a][q]) ? NAN : fminf(v, red[a][q]);
+            w = fmaxf(w, red[3 + a][q]);
+        }
+        dlo[a] = (double)v;
+        dhi[a] = (double)w;
     }
+    const lidar_vox::Grid g = lidar_vox::make_grid(dlo, dhi, voxel);
+    if (!g.ok) {
+        if (tid == 0) meta[0] = 0xffffffffu;
+        return;
+    }
+    bool outside = false;
     for (int64_t i = tid; i < n; i += kT) {
-        uint32_t c[3];
-        for (int a = 0; a < 3; ++a)
-            c[a] = (uint32_t)(int)floorf(__fdiv_rn(__fsub_rn(xyz[3 * i + a], lo[a]), voxel));
-        key[i] = (c[0] * dim[1] + c[1]) * dim[2] + c[2];
+        const uint32_t k = lidar_vox::key(g, xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2]);
+        outside |= k == lidar_vox::kOutside;
+        key[i] = k;
         idx[i] = (uint32_t)i;
     }
+    if (__ballot(outside) && lane == 0) atomicOr(&anyout, 1);
+    __syncthreads();
     if (tid == 0) {
-        const uint64_t tot = (uint64_t)dim[0] * dim[1] * dim[2];
-        meta[0] = tot > 0xffffffffull ? 0xffffffffu : (uint32_t)tot;
-        meta[1] = dim[0];
-        meta[2] = dim[1];
-        meta[3] = dim[2];
+        // keys span [0, g.keys) (plus kOutside): the radix passes above their bits are skipped
+        meta[0] = anyout ? 0xfffffffeu : (uint32_t)g.keys;
     }
 }
 
@@ -80,7 +85,8 @@ __global__ __launch_bounds__(kT) void radix_pass_kernel(const uint32_t *__restri
     __shared__ uint32_t cnt[256];          // total per digit, then running offsets
     __shared__ uint32_t wcnt[kW][256];     // per-wave per-digit counts of the current tile
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    // skip passes above the key range (keys < meta[0])
+    if (meta[0] == 0xffffffffu) return;  // no usable grid: nothing was keyed
+    // skip passes above the key range (keys < meta[0]; 0xfffffffe: keys up to kOutside)
     if (shift > 0 && ((uint64_t)meta[0] - 1) >> shift == 0) {
         for (int64_t i = tid; i < n; i += kT) {
             kout[i] = kin[i];
@@ -144,11 +150,15 @@ __global__ __launch_bounds__(kT) void voxel_runs_kernel(const uint32_t *__restri
                                                         uint32_t *__restrict__ meta)
 {
     __shared__ uint32_t ws[kW];
+    __shared__ uint32_t end;  // end of the last voxel's run: n, or the first point outside every bin
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (meta[0] == 0xffffffffu) return;
+    if (tid == 0) end = (uint32_t)n;
     uint32_t base = 0;
     for (int64_t b0 = 0; b0 < n; b0 += kT) {
         const int64_t i = b0 + tid;
-        const bool f = i < n && (i == 0 || skey[i] != skey[i - 1]);
+        const bool in = i < n && skey[i] != lidar_vox::kOutside;
+        const bool f = in && (i == 0 || skey[i] != skey[i - 1]);
         const uint64_t m = __ballot(f);
         const uint32_t inw = (uint32_t)__popcll(m & ((1ull << lane) - 1));
         if (lane == 0) ws[wave] = (uint32_t)__popcll(m);
@@ -158,17 +168,21 @@ __global__ __launch_bounds__(kT) void voxel_runs_kernel(const uint32_t *__restri
             pre += w < wave ? ws[w] : 0;
             tot += ws[w];
         }
-        if (i < n) {
+        if (in) {
             const uint32_t v = base + pre + inw + (f ? 1u : 0u) - 1u;  // id of my voxel
             vid[sidx[i]] = (int32_t)v;
             if (f) vstart[v] = (uint32_t)i;
+        } else if (i < n) {
+            vid[sidx[i]] = -1;  // outside every bin (sorted after the last voxel)
+            if (i == 0 || skey[i - 1] != lidar_vox::kOutside) end = (uint32_t)i;
         }
         base += tot;
         __syncthreads();
     }
+    __syncthreads();
     if (tid == 0) {
         meta[4] = base;
-        vstart[base] = (uint32_t)n;
+        vstart[base] = end;
     }
 }
 
@@ -176,6 +190,7 @@ __global__ void voxel_centroid_kernel(const float *__restrict__ xyz, const uint3
                                       const uint32_t *__restrict__ vstart, const uint32_t *__restrict__ meta,
                                       float *__restrict__ cent, int32_t *__restrict__ counts)
 {
+    if (meta[0] == 0xffffffffu) return;
     const uint32_t V = meta[4];
     for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < V; v += gridDim.x * blockDim.x) {
         const uint32_t a = vstart[v], b = vstart[v + 1];
@@ -192,13 +207,13 @@ __global__ void voxel_centroid_kernel(const float *__restrict__ xyz, const uint3
 
 }  // namespace
 
-LIDAR_EXPORT int lidar_voxel_downsample_f32(lidar_handle *h, const float *xyz, int64_t n, float voxel,
+LIDAR_EXPORT int lidar_voxel_downsample_f32(lidar_handle *h, const float *xyz, int64_t n, double voxel,
                                             int32_t *voxel_id, float *centroids, int32_t *counts,
                                             int64_t *nvox_host, void *stream)
 {
     REQUIRE(h && xyz && voxel_id && centroids && counts && nvox_host, "lidar_voxel_downsample_f32: null pointer");
     REQUIRE(n >= 0 && n < 0x7fffffff, "lidar_voxel_downsample_f32: n out of range");
-    REQUIRE(voxel > 0.0f, "lidar_voxel_downsample_f32: voxel size must be > 0");
+    REQUIRE(voxel > 0.0 && voxel < INFINITY, "lidar_voxel_downsample_f32: voxel size must be finite and > 0");
     *nvox_host = 0;
     if (n == 0) return LIDAR_OK;
     ON_DEVICE(h->device);
@@ -225,7 +240,8 @@ LIDAR_EXPORT int lidar_voxel_downsample_f32(lidar_handle *h, const float *xyz, i
     uint32_t *hm = static_cast<uint32_t *>(h->host_pinned);
     HIP_TRY(hipMemcpyAsync(hm, meta, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
-    REQUIRE(hm[0] != 0xffffffffu, "lidar_voxel_downsample_f32: voxel grid exceeds 2^32 keys (voxel too small)");
+    REQUIRE(hm[0] != 0xffffffffu,
+            "lidar_voxel_downsample_f32: the extent is not finite or the voxel grid has 2^32 keys or more");
     *nvox_host = hm[4];
     return LIDAR_OK;
 }

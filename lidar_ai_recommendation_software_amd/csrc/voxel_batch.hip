@@ -1,9 +1,12 @@
 // voxel_batch.hip — voxel downsampling of a batch of frames over the whole chip.
 //
-// Same spec as voxel.hip: v = floor((p - min p) / voxel) per axis in fp32, key =
-// (vx*Dy + vy)*Dz + vz with D = max v + 1, voxels in ascending key order, voxel id = rank of the
-// key, centroid = sequential fp32 sum of the voxel's points in point order / count.  voxel.hip
-// runs one frame in one workgroup; here every pass is spread over (tiles x frames) workgroups:
+// Spec (voxel_grid.hpp): the voxel key of a point is calculate_grid_density's grid
+// hash (utils/data_processing.py:305-319: np.arange edges over the frame's extent with the 2-cell
+// margin, histogram2d's searchsorted-right binning with the last edge closed) per axis, key =
+// (bx*ny + by)*nz + bz; voxels in ascending key order, voxel id = rank of the key (-1 for a point
+// outside every bin), centroid = sequential fp32 sum of the voxel's points in point order / count.
+// voxel.hip runs one frame in one workgroup; here every pass is spread over (tiles x frames)
+// workgroups:
 //
 //   bbox (min, max) -> keys (u32) + indices              grid (chunks, frames), atomics per frame
 //   LSD radix sort, 8-bit digits, only the passes a frame's key range needs (per-frame parity):
@@ -18,10 +21,11 @@
 // Memory-side bytes per point: xyz read 3x (36 B: bbox, keys, centroids) + keys/indices (8 B written) + per radix pass
 // 24 B (two reads, one write of 8 B) + runs 12 B + centroid gathers 12 B; the algorithmic floor is
 // 12 B in + 4 B voxel id out (+16 B per voxel).  No host synchronisation: nvox[f] lands on the
-// device (-1: the frame's grid exceeds 2^32 keys).
+// device (-1: the frame's extent is not finite, or its grid has 2^32 keys or more).
 #include <algorithm>
 
 #include "common.hpp"
+#include "voxel_grid.hpp"
 
 namespace {
 
@@ -30,8 +34,8 @@ constexpr int TILE = 4096;   // radix tile (elements per scatter workgroup)
 constexpr int ST = 1024;     // scatter / runs workgroup threads
 constexpr int SW = ST / 64;  // waves per scatter workgroup
 
-// per-frame meta words: [0..2] / [3..5] monotone bits of the min / max point, [6] key bits, [7] overflow,
-// [8] voxel count
+// per-frame meta words: [0..2] / [3..5] monotone bits of the min / max point, [6] key bits, [7] unusable
+// grid, [8] voxel count, [9] some point lies outside every bin (its key kOutside needs all 32 bits sorted)
 constexpr int MW = 16;
 
 __device__ __forceinline__ uint32_t ord(float f)  // monotone float -> u32
@@ -53,7 +57,7 @@ __global__ void vb_init_kernel(uint32_t *meta, int batch)
         m[a] = 0xffffffffu;  // >= ord(any float)
         m[3 + a] = 0u;        // <= ord(any float)
     }
-    m[6] = m[7] = m[8] = 0u;
+    m[6] = m[7] = m[8] = m[9] = 0u;
 }
 
 // per-frame bbox in one pass: min and max as monotone bit patterns (atomics per wave)
@@ -81,37 +85,37 @@ __global__ __launch_bounds__(VT) void vb_bbox_kernel(const float *__restrict__ x
     }
 }
 
-__device__ __forceinline__ int cell(float x, float lo, float voxel)
+__device__ __forceinline__ lidar_vox::Grid frame_grid(const uint32_t *m, double voxel)
 {
-    return (int)floorf(__fdiv_rn(__fsub_rn(x, lo), voxel));
+    const double lo[3] = {unord(m[0]), unord(m[1]), unord(m[2])}, hi[3] = {unord(m[3]), unord(m[4]), unord(m[5])};
+    return lidar_vox::make_grid(lo, hi, voxel);
 }
 
-__global__ __launch_bounds__(VT) void vb_keys_kernel(const float *__restrict__ xyz, int64_t n, float voxel,
+__global__ __launch_bounds__(VT) void vb_keys_kernel(const float *__restrict__ xyz, int64_t n, double voxel,
                                                      uint32_t *meta, uint32_t *__restrict__ key,
                                                      uint32_t *__restrict__ idx)
 {
     const int f = blockIdx.y;
     const float *p = xyz + (int64_t)f * n * 3;
     uint32_t *m = meta + (int64_t)f * MW;
-    const float lo[3] = {unord(m[0]), unord(m[1]), unord(m[2])};
-    // the largest cell per axis is the max point's: p -> floor((p - lo) / voxel) is monotone in
-    // fp32 (each correctly rounded op is), so max_i cell(p_i) == cell(max_i p_i)
-    const uint64_t d0 = (uint64_t)cell(unord(m[3]), lo[0], voxel) + 1;
-    const uint64_t d1 = (uint64_t)cell(unord(m[4]), lo[1], voxel) + 1, d2 = (uint64_t)cell(unord(m[5]), lo[2], voxel) + 1;
-    const uint64_t tot = d0 * d1 * d2;
+    const lidar_vox::Grid g = frame_grid(m, voxel);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
-        m[7] = tot > 0x100000000ull ? 1u : 0u;
-        const uint64_t top = tot - 1;
+        m[10] = (uint32_t)n;  // end of the last voxel's run, unless points lie outside every bin (runs kernel)
+        m[7] = g.ok ? 0u : 1u;
+        const uint64_t top = g.ok ? g.keys - 1 : 0;
         m[6] = top == 0 ? 0u : (uint32_t)(64 - __clzll((long long)top));  // bits of the largest key
     }
+    if (!g.ok) return;
     uint32_t *k = key + (int64_t)f * n;
     uint32_t *v = idx + (int64_t)f * n;
+    bool outside = false;
     for (int64_t i = (int64_t)blockIdx.x * VT + threadIdx.x; i < n; i += (int64_t)gridDim.x * VT) {
-        const uint32_t c0 = (uint32_t)cell(p[3 * i], lo[0], voxel), c1 = (uint32_t)cell(p[3 * i + 1], lo[1], voxel),
-                       c2 = (uint32_t)cell(p[3 * i + 2], lo[2], voxel);
-        k[i] = (uint32_t)(((uint64_t)c0 * d1 + c1) * d2 + c2);
+        const uint32_t kk = lidar_vox::key(g, p[3 * i], p[3 * i + 1], p[3 * i + 2]);
+        outside |= kk == lidar_vox::kOutside;
+        k[i] = kk;
         v[i] = (uint32_t)i;
     }
+    if (__ballot(outside) && (threadIdx.x & 63) == 0) atomicOr(m + 9, 1u);
 }
 
 // key bits of frame f, read after vb_keys_kernel (0 when the grid overflowed: nothing is sorted,
@@ -119,7 +123,7 @@ __global__ __launch_bounds__(VT) void vb_keys_kernel(const float *__restrict__ x
 __device__ __forceinline__ int frame_bits(const uint32_t *meta, int f)
 {
     const uint32_t *m = meta + (int64_t)f * MW;
-    return m[7] ? 0 : (int)m[6];
+    return m[7] ? 0 : (m[9] ? 32 : (int)m[6]);
 }
 
 __global__ __launch_bounds__(VT) void vb_hist_kernel(const uint32_t *__restrict__ kin, int64_t n, int shift,
@@ -228,7 +232,7 @@ __device__ __forceinline__ void sorted_bufs(const uint32_t *m, int f, int64_t n,
                                             const uint32_t *v0, const uint32_t *k1, const uint32_t *v1,
                                             const uint32_t *&sk, const uint32_t *&si)
 {
-    const int passes = ((int)m[6] + 7) / 8;  // the sorted data sits in buffer (passes run) % 2
+    const int passes = ((m[9] ? 32 : (int)m[6]) + 7) / 8;  // the sorted data sits in buffer (passes run) % 2
     sk = (passes & 1 ? k1 : k0) + (int64_t)f * n;
     si = (passes & 1 ? v1 : v0) + (int64_t)f * n;
 }
@@ -247,7 +251,8 @@ __global__ __launch_bounds__(ST) void vb_runs_count_kernel(const uint32_t *__res
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int64_t i0 = (int64_t)t * TILE, i1 = min<int64_t>(n, i0 + TILE);
     uint32_t c = 0;
-    for (int64_t i = i0 + tid; i < i1; i += ST) c += (i == 0 || sk[i] != sk[i - 1]) ? 1u : 0u;
+    for (int64_t i = i0 + tid; i < i1; i += ST)
+        c += (sk[i] != lidar_vox::kOutside && (i == 0 || sk[i] != sk[i - 1])) ? 1u : 0u;
     for (int o = 32; o >= 1; o >>= 1) c += (uint32_t)__shfl_xor((int)c, o, 64);
     if (lane == 0) ws[wave] = c;
     __syncthreads();
@@ -282,7 +287,8 @@ __global__ __launch_bounds__(ST) void vb_runs_write_kernel(const uint32_t *__res
     const int64_t i0 = (int64_t)t * TILE, i1 = min<int64_t>(n, i0 + TILE);
     for (int64_t b0 = i0; b0 < i1; b0 += ST) {
         const int64_t i = b0 + tid;
-        const bool st = i < i1 && (i == 0 || sk[i] != sk[i - 1]);
+        const bool in = i < i1 && sk[i] != lidar_vox::kOutside;
+        const bool st = in && (i == 0 || sk[i] != sk[i - 1]);
         const uint64_t mk = __ballot(st);
         const uint32_t inw = (uint32_t)__popcll(mk & ((1ull << lane) - 1));
         if (lane == 0) ws[wave] = (uint32_t)__popcll(mk);
@@ -292,16 +298,18 @@ __global__ __launch_bounds__(ST) void vb_runs_write_kernel(const uint32_t *__res
             pre += w < wave ? ws[w] : 0u;
             tot += ws[w];
         }
-        if (i < i1) {
+        if (in) {
             const uint32_t r = base + pre + inw + (st ? 1u : 0u) - 1u;  // my voxel's rank
             vf[si[i]] = (int32_t)r;
             if (st) vs[r] = (uint32_t)i;
+        } else if (i < i1) {
+            vf[si[i]] = -1;  // outside every bin (sorted after the last voxel)
+            if (i == 0 || sk[i - 1] != lidar_vox::kOutside) m[10] = (uint32_t)i;  // the last run's end
         }
         base += tot;
         __syncthreads();
     }
     if (t == ntiles - 1 && tid == 0) {
-        vs[base] = (uint32_t)n;
         m[8] = base;
         nvox[f] = (int32_t)base;
     }
@@ -315,13 +323,13 @@ __global__ __launch_bounds__(VT) void vb_centroid_kernel(const float *__restrict
     const int f = blockIdx.y;
     const uint32_t *m = meta + (int64_t)f * MW;
     if (m[7]) return;
-    const int passes = ((int)m[6] + 7) / 8;  // the sorted indices sit in buffer (passes run) % 2
+    const int passes = ((m[9] ? 32 : (int)m[6]) + 7) / 8;  // the sorted indices sit in buffer (passes run) % 2
     const uint32_t *si = (passes & 1 ? v1 : v0) + (int64_t)f * n;
     const uint32_t *vs = vstart + (int64_t)f * (n + 1);
     const float *p = xyz + (int64_t)f * n * 3;
     const uint32_t V = m[8];
     for (uint32_t v = blockIdx.x * VT + threadIdx.x; v < V; v += gridDim.x * VT) {
-        const uint32_t a = vs[v], b = vs[v + 1];
+        const uint32_t a = vs[v], b = v + 1 < V ? vs[v + 1] : m[10];
         float s[3] = {0.f, 0.f, 0.f};
         for (uint32_t t = a; t < b; ++t) {
             const uint32_t i = si[t];
@@ -345,16 +353,17 @@ LIDAR_EXPORT uint64_t lidar_voxel_batch_workspace_bytes(int64_t batch, int64_t n
 
 // Voxel downsampling of `batch` frames of n points (xyz (batch, n, 3) fp32), all on the device:
 // voxel_id (batch, n) int32, centroids (batch, n, 3) and counts (batch, n) with the first nvox[f]
-// rows of frame f valid, nvox (batch,) int32 (-1: the frame's voxel grid exceeds 2^32 keys).
+// rows of frame f valid, nvox (batch,) int32 (-1: the frame's extent is not finite or its voxel grid
+// has 2^32 keys or more; voxel_id -1: a point outside every bin).
 // Same results as lidar_voxel_downsample_f32 per frame.
 LIDAR_EXPORT int lidar_voxel_downsample_batch_f32(lidar_handle *h, const float *xyz, int64_t batch, int64_t n,
-                                                  float voxel, int32_t *voxel_id, float *centroids, int32_t *counts,
+                                                  double voxel, int32_t *voxel_id, float *centroids, int32_t *counts,
                                                   int32_t *nvox, void *stream)
 {
     REQUIRE(h && xyz && voxel_id && centroids && counts && nvox, "lidar_voxel_downsample_batch_f32: null pointer");
     REQUIRE(batch >= 0 && batch <= 65535 && n >= 1 && n < 0x7fffffff,
             "lidar_voxel_downsample_batch_f32: batch in [0, 65535], n >= 1");
-    REQUIRE(voxel > 0.0f, "lidar_voxel_downsample_batch_f32: voxel size must be > 0");
+    REQUIRE(voxel > 0.0 && voxel < INFINITY, "lidar_voxel_downsample_batch_f32: voxel size must be finite and > 0");
     if (batch == 0) return LIDAR_OK;
     ON_DEVICE(h->device);
     hipStream_t s = static_cast<hipStream_t>(stream);

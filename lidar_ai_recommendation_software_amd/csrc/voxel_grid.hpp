@@ -1,0 +1,102 @@
+// voxel_grid.hpp — the voxel grid of voxel_downsample: calculate_grid_density's
+// grid hash (utils/data_processing.py:305-319) per axis, extended to 3-D.
+//
+// Per axis, over the frame's own extent lo = min p, hi = max p (float32 widened exactly):
+//   edges  = np.arange(lo - 2v, (hi + 2v) + v, v)    the reference's 2-cell margin (:305-309) and
+//            arange (:312-313): L = ceil((stop - start) / v) edges, e[0] = start, e[1] = start + v,
+//            e[i] = start + i * (e[1] - e[0]) (numpy's DOUBLE_fill)
+//   bin(p) = searchsorted(edges, p, 'right') - 1 with p == e[L-1] moved into the last bin, -1 when
+//            outside (histogram2d's rule, numpy histogramdd)
+// key = (bx * ny + by) * nz + bz over the nx * ny * nz bins.  Summed over z, a frame's voxel counts
+// are therefore the reference's own calculate_grid_density histogram of its (x, y) columns
+// (tests/golden/gen_voxel.py captures that from the reference).  All arithmetic is float64 with one
+// rounding per operation (the library is built with -ffp-contract=off), on the host and the device.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+namespace lidar_vox {
+
+constexpr uint32_t kOutside = 0xffffffffu;  // key of a point outside every bin (sorts last)
+
+struct Axis {
+    double start, e1, delta;  // e[0], e[1], e[1] - e[0]
+    int64_t nb;               // bins (edges - 1)
+};
+
+// false when numpy's arange would not give >= 2 edges (non-finite or degenerate extents) or the
+// axis alone has >= 2^32 bins
+__host__ __device__ inline bool make_axis(double lo, double hi, double v, Axis &ax)
+{
+    const double m = v * 2.0;
+    const double start = lo - m, stop = (hi + m) + v;
+    const double len = ceil((stop - start) / v);
+    if (!(len >= 2.0 && len <= 4294967296.0)) return false;
+    ax.start = start;
+    ax.e1 = start + v;
+    ax.delta = ax.e1 - start;
+    ax.nb = (int64_t)len - 1;
+    return true;
+}
+
+__host__ __device__ inline double edge(const Axis &ax, int64_t i)
+{
+    return i == 0 ? ax.start : (i == 1 ? ax.e1 : ax.start + (double)i * ax.delta);
+}
+
+// histogram2d's bin of p on this axis, -1 outside
+__host__ __device__ inline int64_t bin(const Axis &ax, double p)
+{
+    const int64_t L = ax.nb + 1;
+    // c = number of edges <= p (the edges are non-decreasing): guess from the spacing, verify,
+    // else binary search
+    int64_t c = -1;
+    if (ax.delta > 0.0) {
+        const double g = floor((p - ax.start) / ax.delta) + 1.0;
+        if (g >= 0.0 && g <= (double)L) {
+            const int64_t t = (int64_t)g;
+            if ((t == 0 || edge(ax, t - 1) <= p) && (t == L || edge(ax, t) > p)) c = t;
+        }
+    }
+    if (c < 0) {
+        int64_t lo = 0, hi = L;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (edge(ax, mid) <= p) lo = mid + 1;
+            else hi = mid;
+        }
+        c = lo;
+    }
+    if (p == edge(ax, L - 1)) --c;  // the last edge is closed
+    return (c >= 1 && c <= ax.nb) ? c - 1 : -1;
+}
+
+struct Grid {
+    Axis ax[3];
+    bool ok;       // every axis valid and nx * ny * nz < 2^32
+    uint64_t keys; // nx * ny * nz
+};
+
+__host__ __device__ inline Grid make_grid(const double lo[3], const double hi[3], double v)
+{
+    Grid g;
+    g.ok = true;
+    g.keys = 1;
+    for (int a = 0; a < 3; ++a) {
+        g.ok = g.ok && make_axis(lo[a], hi[a], v, g.ax[a]);
+        if (g.ok) g.keys *= (uint64_t)g.ax[a].nb;
+        g.ok = g.ok && g.keys < 0xffffffffull;
+    }
+    return g;
+}
+
+// key of point p (kOutside when a coordinate lies outside its axis' bins)
+__host__ __device__ inline uint32_t key(const Grid &g, float x, float y, float z)
+{
+    const int64_t bx = bin(g.ax[0], (double)x), by = bin(g.ax[1], (double)y), bz = bin(g.ax[2], (double)z);
+    if (bx < 0 || by < 0 || bz < 0) return kOutside;
+    return (uint32_t)(((uint64_t)bx * (uint64_t)g.ax[1].nb + (uint64_t)by) * (uint64_t)g.ax[2].nb + (uint64_t)bz);
+}
+
+}  // namespace lidar_vox

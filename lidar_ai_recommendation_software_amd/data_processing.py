@@ -370,11 +370,18 @@ def calculate_grid_density(people_positions, x_range, y_range, grid_size=1.0):
 def voxel_downsample(points, voxel_size):
     """One point per occupied voxel (mean of its points, voxels in ascending key order)
     plus the voxel id of every input point.  Returns (centroids (V, 3) float32,
-    voxel_id (N,) int32, counts (V,) int32).  SURVEY §8a N1 (no reference counterpart)."""
+    voxel_id (N,) int32, counts (V,) int32).  SURVEY §8a N1.
+
+    The voxels are ``calculate_grid_density``'s grid (``utils/data_processing.py:305-319``)
+    extended to z: per axis ``np.arange(lo - 2v, (hi + 2v) + v, v)`` over the frame's extent,
+    histogram2d's binning (searchsorted right, the last edge closed).  Summed over z, the
+    counts are the reference's 2-D histogram of the points' (x, y) on its own edges.  Raises
+    ValueError (as ``np.arange`` does) for a non-finite extent, or when the grid has 2^32 keys
+    or more."""
     import torch
     from .pointnet2 import voxel_downsample_batch
-    if not voxel_size > 0:
-        raise ValueError("voxel size must be > 0")
+    if not 0 < voxel_size < np.inf:
+        raise ValueError("voxel size must be finite and > 0")
     x = _on_device(np.asarray(points, dtype=np.float32).reshape(-1, 3), torch.float32)
     n = len(x)
     if n == 0:
@@ -384,7 +391,7 @@ def voxel_downsample(points, voxel_size):
     cent, vid, cnt, nv = voxel_downsample_batch(x[None].contiguous(), float(voxel_size))
     v = int(nv[0].item())
     if v < 0:
-        raise ValueError("voxel_downsample: voxel grid exceeds 2^32 keys (voxel too small)")
+        raise ValueError("voxel_downsample: the extent is not finite or the voxel grid has 2^32 keys or more")
     return cent[0, :v].cpu().numpy(), vid[0].cpu().numpy(), cnt[0, :v].cpu().numpy()
 
 

@@ -90,23 +90,30 @@ def group_report(device, world, frames, elapsed_local):
             "ranks": [{"rank": int(r[0]), "device": int(r[1]), "frames": int(r[2]), "ms": r[3]} for r in rows]}
 
 
-def check_backend(world, backend, device_count):
-    """One process per GPU must talk RCCL: a multi-rank run with at least as many visible GPUs as
-    ranks that ended up on another backend is a misconfiguration (init_distributed picks gloo only
-    when ranks share a GPU)."""
-    if world > 1 and world <= device_count and backend != "nccl":
-        raise RuntimeError(f"{world} ranks over {device_count} GPUs must use RCCL ('nccl'), got {backend!r}")
+def local_world():
+    """Ranks on this node (torch.distributed.run's LOCAL_WORLD_SIZE; WORLD_SIZE when unset)."""
+    return int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1")))
+
+
+def check_backend(world, backend, device_count, local=None):
+    """One process per GPU must talk RCCL: a multi-rank run whose node has at least as many visible
+    GPUs as ranks on it, but ended up on another backend, is a misconfiguration (init_distributed
+    picks gloo only when ranks on a node share a GPU).  The comparison is per node, so a 16-rank
+    job over two 8-GPU nodes is held to RCCL as well."""
+    local = local_world() if local is None else local
+    if world > 1 and local <= device_count and backend != "nccl":
+        raise RuntimeError(f"{local} ranks per node over {device_count} GPUs must use RCCL ('nccl'), got {backend!r}")
 
 
 def init_distributed(world, local):
     """One process per GPU (torch.distributed.run).  Returns the local device index.  Ranks that
-    share a GPU (more ranks than visible devices: a rehearsal of the N-GPU path on a 1-GPU box)
+    share a GPU (more ranks on this node than visible devices: a rehearsal of the N-GPU path on a 1-GPU box)
     use gloo for the timing collectives; otherwise RCCL ("nccl") over xGMI.  Counting devices
     does not initialise the GPU, so this runs before any GPU call."""
     ndev = max(1, torch.cuda.device_count())
     dev = local % ndev
     if world > 1:
-        if world > ndev:
+        if local_world() > ndev:
             dist.init_process_group("gloo")
         else:
             torch.cuda.set_device(dev)

@@ -29,7 +29,8 @@
  *                     ((dx*dx + dy*dy) + dz*dz), running min, argmax, lowest index wins ties.
  *   orc_ball_query    first `nsample` indices (ascending) with d < r*r (fp32),
  *                     padded with the first hit, zero hits -> index 0.
- *   orc_voxel_keys    per-point voxel coordinates floor((p - lo) / v) in fp32.
+ * (voxel_downsample's bins are restated in numpy, oracle/tier_n.py: the reference's own arange +
+ * searchsorted rule.)
  */
 #include <math.h>
 #include <stdint.h>
@@ -252,18 +253,4 @@ void orc_ball_query(const float *xyz, int64_t n, const float *centres, int64_t m
             }
         }
     }
-}
-
-void orc_voxel_keys(const float *xyz, int64_t n, float voxel, int32_t *vcoord, float *lo_out)
-{
-    float lo[3] = {INFINITY, INFINITY, INFINITY};
-    for (int64_t i = 0; i < n; ++i)
-        for (int a = 0; a < 3; ++a)
-            if (xyz[3 * i + a] < lo[a]) lo[a] = xyz[3 * i + a];
-    for (int64_t i = 0; i < n; ++i)
-        for (int a = 0; a < 3; ++a) {
-            float q = (xyz[3 * i + a] - lo[a]) / voxel;
-            vcoord[3 * i + a] = (int32_t)floorf(q);
-        }
-    if (lo_out) memcpy(lo_out, lo, sizeof lo);
 }

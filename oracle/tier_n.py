@@ -22,10 +22,15 @@ Spec (all fp32, one rounding per operation, never fused multiply-add):
   bf16 mode   SA branches: grouped xyz offsets, features, hidden activations and
               weights rounded to bf16 (RNE) before each layer, fp32 accumulation, fp32
               bias/ReLU/pool; group_all stays fp32.
-  voxel       v = floor((p - min(p)) / voxel_size) per axis (fp32 divide);
-              key = (vx * Dy + vy) * Dz + vz with D = max(v) + 1; voxels in
-              ascending key order; centroid = sequential fp32 sum in point
-              order / count; per-point voxel id = rank of its key.
+  voxel       per axis the bins of the reference's calculate_grid_density
+              (utils/data_processing.py:305-319): edges np.arange(lo - 2v,
+              (hi + 2v) + v, v) over the frame's extent (float64), histogram2d's
+              rule (searchsorted right, the last edge closed, outside -> none);
+              key = (bx * ny + by) * nz + bz; voxels in ascending key order;
+              centroid = sequential fp32 sum in point order / count; per-point
+              voxel id = rank of its key (-1 outside every bin).  The x/y part is
+              PINNED: summed over z the counts equal the reference's own
+              calculate_grid_density on the frame's (x, y) (tests/golden/voxel.npz).
 """
 import numpy as np
 
@@ -157,26 +162,63 @@ def sa_stack(xyz, cfg, weights, bf16=False):
 
 
 # ---------------------------------------------------------------- voxels
+def voxel_edges(lo, hi, voxel_size):
+    """calculate_grid_density's edges for the extent [lo, hi] (utils/data_processing.py:305-313):
+    the 2-cell margin, then np.arange(lo - 2v, (hi + 2v) + v, v)."""
+    margin = voxel_size * 2
+    return np.arange(lo - margin, (hi + margin) + voxel_size, voxel_size)
+
+
+def voxel_bins(xyz, voxel_size):
+    """(N,3) float32 -> per-axis bins (N,3) int64 (-1 outside) and the bin counts (nx, ny, nz):
+    histogramdd's rule (numpy/lib/_histograms_impl.py) on voxel_edges of each axis."""
+    x = np.asarray(xyz, dtype=np.float32).astype(np.float64)
+    v = float(voxel_size)
+    bins = np.empty(x.shape, dtype=np.int64)
+    dims = []
+    for a in range(3):
+        e = voxel_edges(float(x[:, a].min()), float(x[:, a].max()), v)
+        if len(e) < 2:
+            raise ValueError("voxel_downsample: fewer than 2 edges on an axis")
+        c = np.searchsorted(e, x[:, a], side="right")
+        c[x[:, a] == e[-1]] -= 1
+        b = c - 1
+        b[(c < 1) | (c > len(e) - 1)] = -1
+        bins[:, a] = b
+        dims.append(len(e) - 1)
+    if dims[0] * dims[1] * dims[2] >= 0xffffffff:
+        raise ValueError("voxel_downsample: the voxel grid has 2^32 keys or more")
+    return bins, tuple(dims)
+
+
 def voxel_downsample(xyz, voxel_size):
     """(N,3) float32 -> (centroids (V,3) f32, voxel id per point (N,) int32, counts (V,) int32)."""
     xyz = np.ascontiguousarray(xyz, dtype=np.float32)
     n = len(xyz)
     if n == 0:
         return np.zeros((0, 3), np.float32), np.zeros(0, np.int32), np.zeros(0, np.int32)
-    vc = np.empty((n, 3), dtype=np.int32)
-    lib().orc_voxel_keys(_ptr(xyz), n, float(np.float32(voxel_size)), _ptr(vc), None)
-    dims = vc.max(axis=0).astype(np.int64) + 1
-    key = (vc[:, 0].astype(np.int64) * dims[1] + vc[:, 1]) * dims[2] + vc[:, 2]
-    uniq, vid, counts = np.unique(key, return_inverse=True, return_counts=True)
+    if not np.isfinite(xyz).all():
+        raise ValueError("voxel_downsample: the extent is not finite (np.arange cannot compute a length)")
+    bins, (nx, ny, nz) = voxel_bins(xyz, voxel_size)
+    inside = (bins >= 0).all(axis=1)
+    key = (bins[:, 0] * ny + bins[:, 1]) * nz + bins[:, 2]
+    uniq, inv, counts = np.unique(key[inside], return_inverse=True, return_counts=True)
+    vid = np.full(n, -1, dtype=np.int64)
+    vid[inside] = inv
     sums = np.zeros((len(uniq), 3), dtype=np.float32)
-    order = np.argsort(vid, kind="stable")  # point order inside every voxel
+    pts = np.flatnonzero(inside)
+    order = pts[np.argsort(vid[pts], kind="stable")]  # point order inside every voxel
     for i in order:  # sequential fp32 sums in point order (small sizes only)
         sums[vid[i]] += xyz[i]
     cent = sums / counts[:, None].astype(np.float32)
     return cent.astype(np.float32), vid.astype(np.int32), counts.astype(np.int32)
 
 
-def voxel_keys_numpy(xyz, voxel_size):
-    xyz = np.asarray(xyz, dtype=np.float32)
-    lo = xyz.min(axis=0)
-    return np.floor((xyz - lo) / np.float32(voxel_size)).astype(np.int32)
+def voxel_counts_xy(vid, counts, bins, dims):
+    """The (nx, ny) histogram of a frame's voxels summed over z (what calculate_grid_density
+    counts on the same x / y edges)."""
+    nx, ny, _ = dims
+    out = np.zeros((nx, ny), dtype=np.int64)
+    inside = vid >= 0
+    np.add.at(out, (bins[inside, 0], bins[inside, 1]), 1)
+    return out

@@ -39,7 +39,6 @@ def lib():
         L.orc_dbscan_labels.argtypes = [P, i64, f64, i32, P, P]
         L.orc_fps.argtypes = [P, i64, i64, P, P]
         L.orc_ball_query.argtypes = [P, i64, P, i64, f32, i32, P]
-        L.orc_voxel_keys.argtypes = [P, i64, f32, P, P]
         L.orc_eps_count.restype = ctypes.c_int
         L.orc_dbscan_labels.restype = ctypes.c_int
         _LIB = L

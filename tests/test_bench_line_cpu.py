@@ -1,0 +1,105 @@
+"""bench.py's driver-facing output, on CPU: the last stdout line must stay small enough for the
+driver's stdout tail (LINE_MAX bytes) and still carry the contract keys, the headline roofline,
+the CPU baseline and the distributed record; `--gpus N` outside torch.distributed.run must start
+N ranks itself."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+import bench  # noqa: E402  (module level imports numpy only)
+
+CONTRACT = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline", "speedup_vs_cpu", "distributed")
+
+
+def _full_record():
+    """The round-3 full record (the 23 KB line the driver could not parse)."""
+    with open(os.path.join(REPO, "profiles", "r03", "recheck_bench_final.json")) as f:
+        return json.loads(f.readline())
+
+
+def _with_ranks(rec, world):
+    rec = json.loads(json.dumps(rec))
+    rec["n_gpus"] = world
+    rec["distributed"] = {"backend": "nccl", "world_size": world, "device_count": world,
+                          "ranks": [{"rank": r, "device": r, "frames": 640, "ms": 32.948751933872 + r / 7}
+                                    for r in range(world)]}
+    stats = {"max_rel": 3.1415926e-05, "n_rel": 131000, "n": 131072, "max_tol_ratio": 0.123456789}
+    rec["precision"] = {"contract": "max |got-want|/|want| over |want| >= 1e-2 RMS, and max err/(1e-4|want| + "
+                                    "1e-4 RMS)", "frame": "batch 0 frame 0", "fps_exact": True,
+                        "level1": stats, "level2": stats, "global": stats}
+    return rec
+
+
+@pytest.mark.parametrize("world", [1, 2, 8, 16])
+def test_compact_line_fits_and_keeps_the_contract(world):
+    rec = _with_ranks(_full_record(), world)
+    line = bench.compact_line(rec, "gpurun_out/bench_detail.json")
+    text = json.dumps(line)
+    assert len(text) <= bench.LINE_MAX, len(text)
+    d = json.loads(text)
+    for k in CONTRACT:
+        assert k in d, k
+    assert d["value"] == pytest.approx(rec["value"], rel=1e-3) and d["n_gpus"] == world
+    r = d["roofline"]
+    for k in ("kernel", "bound", "achieved", "peak", "unit", "frac", "traffic"):
+        assert k in r
+    assert r["frac"] == pytest.approx(r["achieved"] / r["peak"], rel=2e-3)
+    assert r["achieved"] == pytest.approx(r["work_per_launch"] / (r["avg_launch_ms"] * 1e-3) / 1e12, rel=2e-3)
+    assert d["cpu_baseline"]["value"] > 0 and d["cpu_baseline"]["cores"] >= 1 and d["cpu_baseline"]["kind"] == "port"
+    assert d["distributed"]["world_size"] == world == len(d["distributed"]["ranks"])
+    assert d["precision"]["global"]["max_rel"] == pytest.approx(3.142e-05)
+    if world <= 8:  # the optional parts survive at the driver's world sizes
+        assert "legs_M_points_per_s" in d and "kernels" in d and d["detail"] == "gpurun_out/bench_detail.json"
+
+
+def test_compact_line_drops_optional_parts_last_first():
+    rec = _with_ranks(_full_record(), 8)
+    rec["distributed"]["ranks"] *= 40  # an absurd rank list: the optional parts go, the contract stays
+    line = bench.compact_line(rec)
+    for k in CONTRACT:
+        assert k in line
+
+
+def test_committed_r04_lines_are_driver_readable():
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r0[4-9]", "*bench*.log")))
+    if not files:
+        pytest.skip("no committed round-4 bench log")
+    for f in files:
+        lines = [l for l in open(f).read().splitlines() if l.strip()]
+        last = lines[-1]
+        assert len(last.encode()) <= bench.LINE_MAX, f"{f}: last line {len(last)} bytes"
+        d = json.loads(last)
+        for k in CONTRACT:
+            assert k in d, f"{f}: {k}"
+
+
+def test_launch_ranks_starts_n_ranks(tmp_path):
+    """--gpus N without WORLD_SIZE: a child torch.distributed.run with N ranks, output relayed,
+    exit code returned (a stand-in script: this container has no GPU)."""
+    script = tmp_path / "rank.py"
+    script.write_text("import os, sys\n"
+                      "print('rank', os.environ['RANK'], 'of', os.environ['WORLD_SIZE'], sys.argv[1:], flush=True)\n"
+                      "sys.exit(3 if os.environ['RANK'] == '1' and '--fail' in sys.argv else 0)\n")
+    code = ("import sys; sys.path.insert(0, %r); import bench; "
+            "sys.exit(bench.launch_ranks(2, sys.argv[1:], script=%r))" % (REPO, str(script)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, "-c", code, "--x", "1"], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    got = sorted(l for l in r.stdout.splitlines() if l.startswith("rank"))
+    assert got == ["rank 0 of 2 ['--x', '1']", "rank 1 of 2 ['--x', '1']"]
+    r = subprocess.run([sys.executable, "-c", code, "--fail"], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode != 0
+
+
+def test_world_size_must_match_gpus():
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "4"], capture_output=True,
+                       text=True, timeout=60, env=env)
+    assert r.returncode != 0 and "WORLD_SIZE=2" in r.stderr

@@ -155,8 +155,19 @@ def test_gloo_world2_group_report(tmp_path):
 
 
 def test_check_backend_rules():
-    sharding.check_backend(1, None, 1)          # one rank: nothing to check
-    sharding.check_backend(8, "nccl", 8)        # one rank per GPU over RCCL
-    sharding.check_backend(2, "gloo", 1)        # two ranks sharing one GPU: gloo by design
+    sharding.check_backend(1, None, 1, local=1)          # one rank: nothing to check
+    sharding.check_backend(8, "nccl", 8, local=8)        # one rank per GPU over RCCL
+    sharding.check_backend(2, "gloo", 1, local=2)        # two ranks sharing one GPU: gloo by design
     with pytest.raises(RuntimeError):
-        sharding.check_backend(8, "gloo", 8)    # a GPU per rank but not RCCL
+        sharding.check_backend(8, "gloo", 8, local=8)    # a GPU per rank but not RCCL
+    with pytest.raises(RuntimeError):
+        sharding.check_backend(16, "gloo", 8, local=8)   # two 8-GPU nodes, 8 ranks each: RCCL
+    sharding.check_backend(16, "gloo", 8, local=16)      # 16 ranks on one 8-GPU node share GPUs
+
+
+def test_local_world_from_env(monkeypatch):
+    monkeypatch.setenv("WORLD_SIZE", "16")
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
+    assert sharding.local_world() == 8
+    monkeypatch.delenv("LOCAL_WORLD_SIZE")
+    assert sharding.local_world() == 16

@@ -1,7 +1,8 @@
 """bench.py's N-rank path rehearsed on one GPU (the driver's 8-GPU scaling run uses the same code).
 
-torch.distributed.run starts two ranks before any GPU call; with more ranks than visible devices
-they share the GPU and use gloo for the timing collectives (RCCL needs a device per rank).  Each
+Plain `bench.py --gpus 2` (the driver's form) starts a child torch.distributed.run with two ranks
+before any GPU call; with more ranks than visible devices they share the GPU and use gloo for the
+timing collectives (RCCL needs a device per rank).  Each
 rank processes the frames of its own seed; the test then runs each rank's workload alone
 (`--seed-rank r`) and requires bit-identical outputs, and checks that the aggregate rate counts
 the work of both ranks over the max-over-ranks time.
@@ -32,12 +33,15 @@ def _last_json(out):
 
 def test_bench_two_ranks_on_one_gpu(cuda, tmp_path):
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="4")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
-           "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2", *ARGS, "--dump", str(tmp_path / "w2")]
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, "bench.py", "--gpus", "2", *ARGS, "--dump", str(tmp_path / "w2"),
+           "--detail", str(tmp_path / "detail.json")]
     r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=400)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     line = _last_json(r.stdout)
     assert line["n_gpus"] == 2 and line["steps"] == 6
+    assert line["distributed"]["world_size"] == 2 and len(line["distributed"]["ranks"]) == 2
+    assert len(r.stdout.strip().splitlines()[-1]) <= 4096
     # whole-job rate: both ranks' frames over the max-over-ranks window
     per_rank_points = 4 * 8192 * 6
     assert abs(line["value"] - 2 * per_rank_points / (line["ms_per_step"] * 6 / 1e3) / 1e6) <= 1e-6 * line["value"]

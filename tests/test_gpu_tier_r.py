@@ -6,16 +6,22 @@ is rebuilt from its seed and run through the HIP path; arrays must be byte-ident
 (ground plane: golden_cases.check_plane, gelsd's rank rule and eps*kappa), scalars
 identical in value and type, hotspots identical in order.  Plus the reference's
 error behaviour, the standalone DBSCAN kernel against the oracle on adversarial
-frames, and voxel downsampling (Tier N, parity unpinned) against the oracle.
+frames, and voxel downsampling against the oracle and (its x / y binning) the reference's own
+calculate_grid_density outputs (tests/golden/voxel.npz).
 """
+import os
+
 import numpy as np
 import pytest
 
+from golden.voxel_cases import VOXEL_CASES
 from golden_cases import ARRAYS, ERROR_FRAMES, FRAMES, META, check_plane, check_tier_r
 from lidar_ai_recommendation_software_amd import data_processing as dp
 from lidar_ai_recommendation_software_amd.crowd_density_model import CrowdDensityModel
 from lidar_ai_recommendation_software_amd.synthetic import STRESS_KINDS, lattice_frame, stress_frame, uniform_frame
 from oracle import tier_n, tier_r
+
+HERE = os.path.dirname(os.path.abspath(__file__))
 
 pytestmark = pytest.mark.gpu
 
@@ -283,14 +289,27 @@ def test_cell_radius_density_boundary(cuda):
     assert np.array_equal(out.cpu().numpy(), np.sum(d <= 4.0, axis=2) / 4.0)
 
 
+def _outside_frame(n):
+    """Points near 2^30 with a voxel of 3.3 float64 ulps there: numpy's arange spacing
+    (e[1] - e[0]) rounds below the step, so the edges stop short of the extent and the top
+    third of the points lies outside every bin (histogram2d drops them; voxel id -1)."""
+    lo = np.float32(2.0 ** 30 + 1024)
+    x = np.zeros((n, 3), np.float32)
+    x[:, 0] = np.where(np.arange(n) % 3 == 1, lo + np.float32(128), lo)
+    x[:, 1] = np.float32(0.5)
+    x[:, 2] = np.float32(-0.25)
+    return x, 3.3 * 2.0 ** -22
+
+
 def test_voxel_downsample_batch_vs_oracle(cuda):
     """The chip-wide batched voxel path vs the oracle frame by frame: different extents and
-    voxel sizes per key range (0, 1, 2 and 3 radix passes), duplicated points, a one-voxel
-    frame, and a grid past 2^32 keys (nvox -1)."""
+    voxel sizes per key range (0 to 4 radix passes), duplicated points, a one-voxel frame, a flat
+    frame, a frame with points outside every bin (32-bit keys), and grids of 2^32 keys or more or
+    with a NaN extent (nvox -1)."""
     import torch
     from lidar_ai_recommendation_software_amd import pointnet2 as pn
     rng = np.random.default_rng(11)
-    B, N = 6, 5000
+    B, N = 6, 5001
     x = rng.uniform(-1, 1, (B, N, 3)).astype(np.float32)
     x[1] *= 7.5
     x[2, N // 2:] = x[2, : N - N // 2]  # duplicates share voxels
@@ -304,26 +323,69 @@ def test_voxel_downsample_batch_vs_oracle(cuda):
             assert nv[f] == len(wcnt), (voxel, f)
             assert np.array_equal(vid[f], wvid) and np.array_equal(cnt[f, :nv[f]], wcnt)
             assert np.array_equal(c[f, :nv[f]].view(np.uint32), wc.view(np.uint32)), (voxel, f)
+    xo, vo = _outside_frame(N)
+    xb = np.stack([xo, xo])
+    xb[1, 7, 1] = np.nan  # NaN extent: np.arange cannot compute a length
+    c, vid, cnt, nv = (t.cpu().numpy() for t in pn.voxel_downsample_batch(torch.from_numpy(xb).to(cuda), vo))
+    wc, wvid, wcnt = tier_n.voxel_downsample(xo, vo)
+    assert (wvid < 0).sum() == N // 3 + (N % 3 > 1) and nv.tolist() == [len(wcnt), -1]
+    assert np.array_equal(vid[0], wvid) and np.array_equal(cnt[0, :nv[0]], wcnt)
+    assert np.array_equal(c[0, :nv[0]].view(np.uint32), wc.view(np.uint32))
     _, _, _, nv = pn.voxel_downsample_batch(torch.from_numpy(x[:2]).to(cuda), 1e-6)
     assert nv.cpu().numpy().tolist() == [-1, -1]
 
 
+@pytest.mark.parametrize("name", list(VOXEL_CASES))
+def test_voxel_downsample_pinned_to_reference(cuda, name):
+    """SURVEY §8a N1's voxel key is calculate_grid_density's grid hash extended to z: the GPU's voxel
+    ids, summed over z, divided by v^2, equal the density grid the REFERENCE returned for the frame's
+    (x, y) (tests/golden/voxel.npz, captured by gen_voxel.py) bit for bit; ids, counts and centroids
+    equal the oracle's."""
+    g = np.load(os.path.join(HERE, "golden", "voxel.npz"), allow_pickle=False)
+    make, v = VOXEL_CASES[name]
+    x = make()
+    c, vid, cnt = dp.voxel_downsample(x, v)
+    wc, wvid, wcnt = tier_n.voxel_downsample(x, v)
+    assert np.array_equal(vid, wvid) and np.array_equal(cnt, wcnt)
+    assert np.array_equal(c.view(np.uint32), wc.view(np.uint32))
+    bins, dims = tier_n.voxel_bins(x, v)
+    hist = tier_n.voxel_counts_xy(vid, cnt, bins, dims)
+    want = g[f"{name}__density"]
+    assert np.array_equal((hist / (v * v)).view(np.uint64), want.view(np.uint64))
+
+
+def test_voxel_downsample_errors_like_arange(cuda):
+    x = uniform_frame(2000, 4, -1, 1).astype(np.float32)
+    x[5, 2] = np.inf
+    with pytest.raises(ValueError):
+        dp.voxel_downsample(x, 0.1)
+    with pytest.raises(ValueError):
+        dp.voxel_downsample(uniform_frame(2000, 4, -1, 1).astype(np.float32), 1e-4)  # >= 2^32 keys
+    with pytest.raises(ValueError):
+        dp.voxel_downsample(uniform_frame(20, 4, -1, 1).astype(np.float32), 0.0)
+
+
 def test_voxel_single_workgroup_entry_matches_batched(cuda):
     """lidar_voxel_downsample_f32 (one frame, one workgroup; the C-ABI single-frame entry)
-    equals the batched chip-wide path."""
+    equals the batched chip-wide path, incl. points outside every bin."""
+    import torch
+    for xn, vv in ((uniform_frame(30000, 5, -1, 1).astype(np.float32), 0.06), _outside_frame(3001)):
+        _single_vs_batched(cuda, torch.from_numpy(xn).to(cuda), vv)
+
+
+def _single_vs_batched(cuda, x, voxel):
     import ctypes
     import torch
     from lidar_ai_recommendation_software_amd import _native as nat
     from lidar_ai_recommendation_software_amd import pointnet2 as pn
-    x = torch.from_numpy(uniform_frame(30000, 5, -1, 1).astype(np.float32)).to(cuda)
     n = len(x)
     vid = torch.empty(n, dtype=torch.int32, device=cuda)
     cent = torch.empty((n, 3), dtype=torch.float32, device=cuda)
     cnt = torch.empty(n, dtype=torch.int32, device=cuda)
     v = nat.I64(0)
-    nat.call("lidar_voxel_downsample_f32", nat.handle(0), nat.ptr(x), n, 0.06, nat.ptr(vid), nat.ptr(cent),
+    nat.call("lidar_voxel_downsample_f32", nat.handle(0), nat.ptr(x), n, voxel, nat.ptr(vid), nat.ptr(cent),
              nat.ptr(cnt), ctypes.byref(v), nat.stream_ptr())
-    c2, vid2, cnt2, nv = pn.voxel_downsample_batch(x[None].contiguous(), 0.06)
+    c2, vid2, cnt2, nv = pn.voxel_downsample_batch(x[None].contiguous(), voxel)
     v = v.value
     assert int(nv[0]) == v
     assert torch.equal(vid, vid2[0]) and torch.equal(cnt[:v], cnt2[0, :v])

@@ -4,12 +4,16 @@
   reference (``tests/golden/gen_tier_r.py``) byte for byte, and its error behaviour.
 * Tier N (parity unpinned by the reference): the C loops agree with the pure-numpy
   restatement, and the frozen vectors in ``tests/golden/tier_n.npz`` still reproduce.
+  voxel_downsample's x / y binning is pinned: it is calculate_grid_density's, checked against
+  the reference's own outputs (``tests/golden/voxel.npz``, ``gen_voxel.py``).
 """
+import hashlib
 import os
 
 import numpy as np
 import pytest
 
+from golden.voxel_cases import VOXEL_CASES
 from golden_cases import ERROR_FRAMES, FRAMES, LARGE, META, SMALL, check_tier_r
 from oracle import tier_n, tier_r
 from lidar_ai_recommendation_software_amd.synthetic import unit_frames, uniform_frame
@@ -74,13 +78,47 @@ def test_ball_query_c_vs_numpy():
         assert np.array_equal(tier_n.ball_query(x, c, r, ns), tier_n.ball_query_numpy(x, c, r, ns))
 
 
-def test_voxel_keys_c_vs_numpy():
+@pytest.mark.parametrize("name", list(VOXEL_CASES))
+def test_voxel_bins_pinned_to_reference(name):
+    """voxel_downsample's x / y binning IS calculate_grid_density's: summed over z, the oracle's voxel
+    counts divided by v^2 equal the density grid the reference itself returned for the frame's
+    (x, y) columns (tests/golden/voxel.npz, captured by gen_voxel.py), bit for bit."""
+    g = np.load(os.path.join(HERE, "golden", "voxel.npz"), allow_pickle=False)
+    make, v = VOXEL_CASES[name]
+    x = make()
+    assert hashlib.sha256(np.ascontiguousarray(x).tobytes()).digest() == g[f"{name}__sha"].tobytes(), "frame drifted"
+    cent, vid, cnt = tier_n.voxel_downsample(x, v)
+    bins, dims = tier_n.voxel_bins(x, v)
+    hist = tier_n.voxel_counts_xy(vid, cnt, bins, dims)
+    want = g[f"{name}__density"]
+    assert hist.shape == want.shape
+    assert np.array_equal((hist / (v * v)).view(np.uint64), want.view(np.uint64))
+    assert cnt.sum() == (vid >= 0).sum() == len(x)
+    # the reference's cell centres come from the same edges
+    for a, key in ((0, "grid_x"), (1, "grid_y")):
+        e = tier_n.voxel_edges(float(x[:, a].min()), float(x[:, a].max()), v)
+        assert np.array_equal((e[:-1] + e[1:]) / 2, g[f"{name}__{key}"])
+
+
+def test_voxel_downsample_oracle_rules():
+    """Voxels in ascending key order, ids = key ranks, centroids = in-order fp32 sums / count,
+    and the error cases numpy's arange gives."""
     x = uniform_frame(5000, 2, -1, 1).astype(np.float32)
-    vc = tier_n.voxel_downsample(x, 0.07)[1]
-    keys = tier_n.voxel_keys_numpy(x, 0.07)
-    d = keys.max(axis=0).astype(np.int64) + 1
-    k = (keys[:, 0].astype(np.int64) * d[1] + keys[:, 1]) * d[2] + keys[:, 2]
-    assert np.array_equal(vc, np.unique(k, return_inverse=True)[1])
+    cent, vid, cnt = tier_n.voxel_downsample(x, 0.07)
+    bins, (nx, ny, nz) = tier_n.voxel_bins(x, 0.07)
+    key = (bins[:, 0] * ny + bins[:, 1]) * nz + bins[:, 2]
+    assert np.array_equal(vid, np.unique(key, return_inverse=True)[1])
+    for v in (0, 7, len(cnt) - 1):
+        s = np.zeros(3, np.float32)
+        for p in x[vid == v]:
+            s = s + p
+        assert np.array_equal(cent[v], s / np.float32(cnt[v]))
+    bad = x.copy()
+    bad[3, 1] = np.nan
+    with pytest.raises(ValueError):
+        tier_n.voxel_downsample(bad, 0.07)
+    with pytest.raises(ValueError):
+        tier_n.voxel_downsample(x, 1e-4)  # 2 / 1e-4 cells per axis: >= 2^32 keys
 
 
 def test_tier_n_frozen_vectors():

@@ -131,32 +131,25 @@ int lidar_dense_f32(lidar_handle *h, const float *x, int64_t rows, int32_t k, co
                     const float *bias, int32_t cout, int32_t relu_on, int32_t pool_rows, float *y,
                     void *stream);
 
-/* The x3 GEMM (fp32 arithmetic on the bf16 matrix cores: operands split exactly into bf16 hi +
- * lo, products ah*bh + ah*bl + al*bh accumulated in fp32, <= ~2^-15 per product) runs on a
- * weight image packed once: lidar_dense_x3_packed_size(k, cout) bytes, filled on the device by
- * lidar_dense_x3_pack_f32 from W (k, cout) fp32 (bf16 hi / lo MFMA B fragments, K padded to 32). */
+/* The dense GEMM of the fp32 contract ("h3" arithmetic, csrc/h3.hpp: operands scaled by powers of
+ * two and split exactly into fp16 hi + lo, products ah*bh + ah*bl + al*bh accumulated in fp32 on
+ * the fp16 matrix cores, unscaled once: <= ~3 2^-22 |a b| per product) runs on a weight image packed
+ * once: lidar_dense_x3_packed_size(k, cout) bytes, filled on the device by lidar_dense_x3_pack_f32
+ * from W (k, cout) fp32 (fp16 hi / lo MFMA B fragments of W 2^s, K padded to 32, s in the image's
+ * tail).  lidar_dense_x1_pack_f32 fills the same size with the bf16 image of the bf16 spec (X1). */
 int64_t lidar_dense_x3_packed_size(int32_t k, int32_t cout);
 int lidar_dense_x3_pack_f32(lidar_handle *h, const float *w, int32_t k, int32_t cout, void *packed, void *stream);
+int lidar_dense_x1_pack_f32(lidar_handle *h, const float *w, int32_t k, int32_t cout, void *packed, void *stream);
 
-/* the x3 GEMM on pre-split activations ("split planes", csrc/dense_x3s.hip): a_planes holds
- * two bf16 planes (hi = bf16(x), lo = bf16(x - hi)) of row-major (rows, lda) elements, the lo
- * plane a_plane elements after the hi plane; lda = k rounded up to 32, elements k..lda-1 zero.
- * packed = lidar_dense_x3_pack_f32's image of W (k, cout).  mode 0: y = x W + b [ReLU] as fp32
- * rows (rows, ldo); mode 1: the same as split planes (rows, ldo) x 2, o_plane apart (the next
- * layer's input); mode 2: ReLU and max over runs of pool_rows rows into fp32 (rows/pool_rows,
- * ldo), out zeroed by the caller.  rows % 128 == 0, cout % 128 == 0.  Mode flag 4 (fp32 rows in,
- * mode 0 only): one bf16 product per MFMA, bf16(x) bf16(w) in fp32 — the bf16 spec. */
-int lidar_dense_x3s_f32(lidar_handle *h, const void *a_planes, int64_t a_plane, int32_t lda, int64_t rows,
-                        int32_t k, const void *packed, const float *bias, int32_t cout, int32_t mode,
-                        int32_t relu_on, int32_t pool_rows, void *out, int64_t o_plane, int64_t ldo, void *stream);
-/* the same GEMM with A as fp32 rows (rows, k) of row stride lda (k % 4 == 0), split inside the
- * tile loop (for a chain's first layer, whose input nobody split) */
+/* y = x W + b on that image (csrc/dense_x3s.hip): A = fp32 rows (rows, k) of row stride lda
+ * (k % 4 == 0; elements k..lda-1 are read and must be finite), each wave scales and splits the
+ * fragments it reads.  mode 0: y [ReLU] as fp32 rows (rows, ldo); mode 2: ReLU and max over runs
+ * of pool_rows rows into fp32 (rows/pool_rows, ldo), out zeroed by the caller.  rows % 128 == 0,
+ * cout % 128 == 0; o_plane is unused (0).  Mode flag 4 (mode 0 only, lidar_dense_x1_pack_f32's
+ * image): one bf16 product per MFMA, bf16(x) bf16(w) in fp32 — the bf16 spec. */
 int lidar_dense_x3f_f32(lidar_handle *h, const float *a, int32_t lda, int64_t rows, int32_t k, const void *packed,
                         const float *bias, int32_t cout, int32_t mode, int32_t relu_on, int32_t pool_rows, void *out,
                         int64_t o_plane, int64_t ldo, void *stream);
-/* fp32 rows (rows, k), row stride ldx -> split planes (rows, lda) for lidar_dense_x3s_f32 */
-int lidar_split_x3_f32(lidar_handle *h, const float *x, int64_t rows, int32_t k, int64_t ldx, void *planes,
-                       int64_t plane, int32_t lda, void *stream);
 
 /* SA branch in the bf16 spec (BASELINE configs[4]) on the fused 16-row kernel of
  * lidar_sa_group_mlp_x3_f32 with one bf16 product per MFMA: layer inputs and weights rounded to

@@ -58,8 +58,7 @@ SIGNATURES = {
     "lidar_dense_f32": [P, P, I64, I32, P, P, I32, I32, I32, P, P],
     "lidar_dense_x3_packed_size": [I32, I32],
     "lidar_dense_x3_pack_f32": [P, P, I32, I32, P, P],
-    "lidar_dense_x3s_f32": [P, P, I64, I32, I64, I32, P, P, I32, I32, I32, I32, P, I64, I64, P],
-    "lidar_split_x3_f32": [P, P, I64, I32, I64, P, I64, I32, P],
+    "lidar_dense_x1_pack_f32": [P, P, I32, I32, P, P],
     "lidar_dense_x3f_f32": [P, P, I32, I64, I32, P, P, I32, I32, I32, I32, P, I64, I64, P],
     "lidar_mlp_packed_size_x1": [I32, I32, I32],
     "lidar_fps_workspace_bytes": [I64, I64],
@@ -137,25 +136,52 @@ def check(rc, what):
 
 def grid_dims(x_min, x_max, y_min, y_max, grid_size):
     """(nx, ny) of calculate_grid_density's grid (lidar_grid_dims: np.arange's length of the
-    margin-padded edges, utils/data_processing.py:305-313).  A grid numpy could never allocate
-    (more than 2^40 cells, or more cells than the device has free memory for) raises MemoryError,
-    as the reference's np.arange / np.histogram2d do (a frame 1e12 m wide)."""
+    margin-padded edges, utils/data_processing.py:305-313), with numpy's errors for grids it could
+    never build: a non-finite extent or a length past what an array may hold raises ValueError
+    ("Maximum allowed size exceeded"), more than 2^40 cells MemoryError (a frame 1e12 m wide).
+    The grid's own allocation raises MemoryError too when the device has no room for it
+    (grid_alloc)."""
     nx, ny = I64(0), I64(0)
     rc = load_library().lidar_grid_dims(float(x_min), float(x_max), float(y_min), float(y_max),
                                         float(grid_size), ctypes.byref(nx), ctypes.byref(ny))
     if rc == -3:
         raise MemoryError(f"Unable to allocate a density grid for x in [{x_min}, {x_max}], "
                           f"y in [{y_min}, {y_max}] at grid size {grid_size}")
+    if rc == -1:
+        raise ValueError("Maximum allowed size exceeded")
     check(rc, "lidar_grid_dims")
-    nx, ny = nx.value, ny.value
-    import torch
-    if torch.cuda.is_available():
-        free, _ = torch.cuda.mem_get_info()
-        need = 8 * (4 * nx * ny + nx + ny + 64)
-        if need > free:
-            raise MemoryError(f"Unable to allocate {need / 2**30:.1f} GiB for an array with shape "
-                              f"({nx}, {ny}) and data type float64")
-    return nx, ny
+    return nx.value, ny.value
+
+
+class grid_alloc:
+    """Context for the device allocations of a density grid: torch's out-of-memory error becomes
+    the MemoryError numpy raises for an array it cannot allocate."""
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, et, ev, tb):
+        import torch
+        if et is not None and issubclass(et, torch.cuda.OutOfMemoryError):
+            raise MemoryError(f"Unable to allocate the density grid on the device: {ev}") from ev
+        return False
+
+
+class _ThreadHandles(dict):
+    """This thread's handles, {(device, slot): handle}.  When the thread ends, its thread-local
+    storage is released and the handles with it (lidar_destroy frees their workspaces); the main
+    thread's live until exit, when the process's teardown reclaims the device memory."""
+
+    def __del__(self):
+        import sys
+        if sys.is_finalizing() or threading.current_thread() is threading.main_thread():
+            return
+        lib = _lib
+        if lib is None:
+            return
+        for h in self.values():
+            lib.lidar_destroy(h)
+        self.clear()
 
 
 def handle(device=None, slot=0):
@@ -170,7 +196,7 @@ def handle(device=None, slot=0):
         device = torch.cuda.current_device()
     hs = getattr(_tls, "handles", None)
     if hs is None:
-        hs = _tls.handles = {}
+        hs = _tls.handles = _ThreadHandles()
     key = (device, slot)
     h = hs.get(key)
     if h is None:
@@ -179,6 +205,22 @@ def handle(device=None, slot=0):
         check(lib.lidar_create(int(device), ctypes.byref(hp)), "lidar_create")
         h = hs[key] = hp
     return h
+
+
+def trim(device=None):
+    """Free the workspaces this thread's handles for `device` retired when they grew
+    (lidar_trim).  Call only where the work queued with those handles has completed (after
+    synchronising the streams it ran on).  Returns the bytes freed."""
+    import torch
+    if device is None:
+        device = torch.cuda.current_device()
+    freed = 0
+    for (d, _), h in list((getattr(_tls, "handles", None) or {}).items()):
+        if d == device:
+            b = ctypes.c_uint64(0)
+            call("lidar_trim", h, ctypes.byref(b))
+            freed += b.value
+    return freed
 
 
 def stream_ptr(stream=None):

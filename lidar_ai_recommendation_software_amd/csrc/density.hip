@@ -2117,9 +2117,17 @@ LIDAR_EXPORT int lidar_grid_dims(double xmin, double xmax, double ymin, double y
     const double x0 = xmin - m, x1 = (xmax + m) + grid;
     const double y0 = ymin - m, y1 = (ymax + m) + grid;
     const double lx = std::ceil((x1 - x0) / grid), ly = std::ceil((y1 - y0) / grid);
+    // numpy's errors (np.arange, then histogram2d's (nx, ny) float64 array): a length it cannot
+    // compute or hold (not finite, >= 2^63 elements, or >= 2^63 bytes) is a ValueError ("Maximum
+    // allowed size exceeded" / "array is too big") -> LIDAR_EINVAL; a representable grid of more
+    // than 2^40 cells (8 TiB of float64) a MemoryError -> LIDAR_ENOMEM
+    const double kBig = 1152921504606846976.0;  // 2^60 float64 elements = 2^63 bytes
+    if (!(std::isfinite(lx) && std::isfinite(ly) && lx < kBig && ly < kBig && (lx - 1) * (ly - 1) < kBig)) {
+        lidar::set_error("lidar_grid_dims: Maximum allowed size exceeded");
+        return LIDAR_EINVAL;
+    }
     REQUIRE(lx >= 2 && ly >= 2, "lidar_grid_dims: degenerate grid");
-    // more than 2^40 cells (8 TiB of float64): numpy's np.arange / histogram2d raise MemoryError
-    if (!(lx < 1e15 && ly < 1e15 && (lx - 1) * (ly - 1) <= 1099511627776.0)) {
+    if ((lx - 1) * (ly - 1) > 1099511627776.0) {
         lidar::set_error("lidar_grid_dims: the grid has more than 2^40 cells");
         return LIDAR_ENOMEM;
     }

@@ -1,13 +1,15 @@
-// sa_mlp_x3.hip — SetAbstraction layers 2-3 in fp32 arithmetic carried by the bf16 matrix cores.
+// sa_mlp_x3.hip — SetAbstraction layers 2-3 in fp32 arithmetic carried by the fp16 matrix cores.
 //
-// Every fp32 operand x is split exactly as x = hi + lo + e with hi = bf16(x), lo = bf16(x - hi)
-// (RNE both; x - hi is exact in fp32) and |e| <= 2^-17 |x|.  A product is accumulated as
-//   a*b ~ ah*bh + ah*bl + al*bh          (three v_mfma_f32_16x16x32_bf16, fp32 accumulation)
-// whose error against the fp32 product is <= ~2^-15 |a*b| (the dropped al*bl and the two
-// splitting residues): the 1e-4 contract of the fp32 path holds with margin
-// (tests/test_gpu_tier_n.py::test_group_mlp_x3 vs the fp32 oracle).  bf16 x bf16 products are
-// exact in fp32.  The bf16 MFMA issues 16x the fp32 one's flops per cycle, so three of them
-// still run ~5x the fp32 rate.
+// h3 arithmetic (h3.hpp): every fp32 operand x is scaled by a power of two and split exactly as
+// hi = fp16(x S), lo = fp16(x S - hi), and a product is accumulated as
+//   a*b S_a S_w ~ ah*bh + ah*bl + al*bh    (three v_mfma_f32_16x16x32_f16, fp32 accumulation)
+// then unscaled once (exact): <= ~3 2^-22 |a*b| per product, fp32-class, so the features meet
+// 1e-4 RELATIVE on every element >= 1e-2 RMS (tests/test_gpu_tier_n.py).  Weights are scaled per
+// layer at pack time; activations per 16-row tile: layer 2's input by its tile maximum, layer 3's
+// by the tile maximum (fused SA1 kernel) or by the bound colsum(W2) 2^e2 + max|b2| (lean SA2
+// kernel, which splits layer 2's output chunk by chunk).  fp16 x fp16 products are exact in fp32.
+// The fp16 MFMA issues 16x the fp32 one's flops per cycle, so three of them still run ~5x the
+// fp32 rate.  X1 (the bf16 spec, BASELINE configs[4]) runs one bf16 product per MFMA instead.
 //
 // Same fused design as sa_mlp16.hip (16 grouped rows per wave, weights streamed through LDS in
 // chunks of two output tiles shared by the 4 waves, layer 3 transposed so the max-pool is a
@@ -16,20 +18,28 @@
 // accumulator pair (tiles 2s, 2s+1: channels 16t + 4g + r of point l&15, g = l>>4) is the
 // k-step-s fragment of the next layer with element j <-> channel in(s, g, j) = 32s + 16(j>>2) +
 // 4g + (j&3); the packed weights (lidar_mlp_pack_x3_f32) follow that k order.
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 #include <vector>
 
 #include "bq_grid.hpp"
+#include "h3.hpp"
 
 namespace {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+using lidar_h3::f16x8;
 
 __device__ __forceinline__ f32x4 mfma_bf(bf16x8 a, bf16x8 b, f32x4 c)
 {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mfma_bf(f16x8 a, f16x8 b, f32x4 c)
+{
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
 __device__ __forceinline__ f32x4 mfma_f(float a, float b, f32x4 c)
 {
@@ -46,8 +56,13 @@ __device__ __forceinline__ float maxn(float a, float b, float c)
     return __builtin_elementwise_maximum(__builtin_elementwise_maximum(a, b), c);
 }
 
-// two accumulator tiles -> the hi / lo bf16 fragments of one k-step
-__device__ __forceinline__ void split_pair(const f32x4 &t0, const f32x4 &t1, bf16x8 &hi, bf16x8 &lo)
+// two accumulator tiles -> the hi / lo fragments of one k-step: h3 (fp16, scaled by s) ...
+__device__ __forceinline__ void split_pair(const f32x4 &t0, const f32x4 &t1, f16x8 &hi, f16x8 &lo, float s)
+{
+    lidar_h3::split8(t0, t1, s, hi, lo);
+}
+// ... or bf16 (X1: only hi is read)
+__device__ __forceinline__ void split_pair(const f32x4 &t0, const f32x4 &t1, bf16x8 &hi, bf16x8 &lo, float)
 {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -59,9 +74,11 @@ __device__ __forceinline__ void split_pair(const f32x4 &t0, const f32x4 &t1, bf1
 }
 
 // packed image (16-byte units "u4"): [W1 fp32 (T1*64 floats, xyz levels only), padded to 16 B]
-// [layer-2 chunks] [layer-3 chunks] [b1 b2 b3 fp32].  Chunk c = output tiles (2c, 2c+1) of a
-// layer with K inputs: u4 at ((s*2 + t)*2 + h)*64 + lane = bf16x8 (h = 0 hi, 1 lo) of
-// W[in(s, lane>>4, j)][16(2c+t) + (lane&15)], j = 0..7, s < K/32.
+// [layer-2 chunks] [layer-3 chunks] [b1 b2 b3 fp32] [tail].  Chunk c = output tiles (2c, 2c+1)
+// of a layer with K inputs: u4 at ((s*2 + t)*2 + h)*64 + lane = f16x8 (h = 0 hi, 1 lo) of
+// W[in(s, lane>>4, j)][16(2c+t) + (lane&15)] 2^s_layer, j = 0..7, s < K/32.  Tail (x3 image, 16
+// bytes): int32 s2, s3 (the layers' scaling exponents), float colsum(W2) (max over output
+// channels of sum |W2|), float max |b2| — layer 3's input bound in the lean kernel.
 // X1 (the bf16 spec, BASELINE configs[4]): one product ah*bh per MFMA on bf16(x) and bf16(w) —
 // the image keeps the hi fragments only: u4 at (s*2 + t)*64 + lane.
 template <int C1, int C2, int C3, bool X1 = false>
@@ -72,6 +89,19 @@ struct PackX3 {
     static constexpr int CH2 = KS2 * 2 * HALVES * 64, CH3 = KS3 * 2 * HALVES * 64;  // chunk sizes in u4
     static constexpr int W1U4 = T1 * 64 / 4;                                       // fp32 W1 in u4
 };
+
+// the x3 image's tail (after the biases)
+struct X3Tail {
+    int32_t s2, s3;
+    float colsum2, bmax2;
+};
+// layer 3's input scaling exponent from layer 2's input exponent e2 (the lean kernel's bound:
+// |y2| <= colsum(W2) 2^e2 + max|b2|, widened by 2^-10 for the roundings of y2 and of the bound)
+__device__ __forceinline__ int bound_exp3(const X3Tail &t, int e2)
+{
+    const float b = (t.colsum2 * ldexpf(1.0f, e2) + t.bmax2) * (1.0f + 0x1p-10f);
+    return lidar_h3::exp_of_bits(__float_as_uint(b));
+}
 
 // layer-1 modes: the grouped row's layer-1 output comes from
 //   L1_XYZ  W1 (xyz rows, fp32 in LDS) . (p[k] - c) + b1 on a 16x16x4 fp32 MFMA (levels without features)
@@ -103,7 +133,7 @@ __device__ __forceinline__ float max_row_groups(float v)
 #endif
 constexpr int kBqCap = LIDAR_BQ_CAP;  // candidates per window a fused wave ranks in LDS (more: index-order scan)
 template <int C1, int C2, int C3, int NS, int L1, int R, bool X1, bool BQ = false>
-__global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float *__restrict__ P, int64_t stride,
+__global__ __launch_bounds__(256, (BQ && !X1 && NS == 32) ? 5 : (R == 1 ? 3 : 2)) void sa_x3_kernel(const float *__restrict__ P, int64_t stride,
                                                      const float *__restrict__ Q, const int32_t *__restrict__ idx,
                                                      int n, int m, int64_t total, const uint4 *__restrict__ packed,
                                                      float *__restrict__ out, int64_t out_stride, int64_t out_offset,
@@ -115,6 +145,7 @@ __global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float 
     static_assert(NS % (16 * R) == 0 && C1 % 32 == 0 && C2 % 32 == 0 && C3 % 64 == 0, "tile shapes");
     constexpr bool XYZ = L1 == L1_XYZ, HASW1 = L1 != L1_PRE;
     using K = PackX3<C1, C2, C3, X1>;
+    using PT = std::conditional_t<X1, bf16x8, f16x8>;  // MFMA operand pieces
     constexpr int HV = K::HALVES;
     constexpr int T1 = K::T1, T2 = K::T2, T3 = K::T3, KS2 = K::KS2, KS3 = K::KS3;
     constexpr int CH2 = K::CH2, CH3 = K::CH3, CHMAX = CH2 > CH3 ? CH2 : CH3;
@@ -149,6 +180,13 @@ __global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float 
     const uint4 *W2 = packed + (HASW1 ? K::W1U4 : 0);
     const uint4 *W3 = W2 + (int64_t)(T2 / 2) * CH2;
     const float *Bias = reinterpret_cast<const float *>(W3 + (int64_t)(T3 / 2) * CH3);
+    // h3: the layers' weight scaling exponents (X1: no scaling)
+    int sw2 = 0, sw3 = 0;
+    if constexpr (!X1) {
+        const X3Tail *tl = reinterpret_cast<const X3Tail *>(Bias + C1 + C2 + C3);
+        sw2 = tl->s2;
+        sw3 = tl->s3;
+    }
 
     auto fetch = [&](int c, int dst) {
         const uint4 *src = c < T2 / 2 ? W2 + c * CH2 : W3 + (c - T2 / 2) * CH3;
@@ -199,7 +237,8 @@ __global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float 
 #pragma unroll 1
     for (int it = 0; it < ITERS; ++it) {
         // ---- layer 1 -> the layer-2 operand fragments (hi / lo) of R x 16 grouped rows
-        bf16x8 xh[R][KS2], xl[R][KS2];
+        PT xh[R][KS2], xl[R][KS2];
+        int e2[R], e3[R];  // h3: the tiles' scaling exponents of layers 2 and 3 (wave-uniform)
 #pragma unroll
         for (int rr = 0; rr < R; ++rr) {
             const int64_t k = BQ ? qidx[wave][(it * R + rr) * 16 + col] : idx[cc * NS + (it * R + rr) * 16 + col];
@@ -244,12 +283,22 @@ __global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float 
                     for (int r = 0; r < 4; ++r) y1[ti][r] = relu(a[r] - c[r]);
                 }
             }
+            float sc = 1.0f;
+            if constexpr (!X1) {
+                uint32_t mb = 0;
 #pragma unroll
-            for (int s = 0; s < KS2; ++s) split_pair(y1[2 * s], y1[2 * s + 1], xh[rr][s], xl[rr][s]);
+                for (int t = 0; t < T1; ++t)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) mb = max(mb, __float_as_uint(y1[t][r]));  // ReLU outputs: non-negative bits
+                e2[rr] = lidar_h3::wave_exp(mb);
+                sc = lidar_h3::scale_of(e2[rr]);
+            }
+#pragma unroll
+            for (int s = 0; s < KS2; ++s) split_pair(y1[2 * s], y1[2 * s + 1], xh[rr][s], xl[rr][s], sc);
         }
 
         f32x4 y2[R][T2];
-        bf16x8 zh[R][KS3], zl[R][KS3];
+        PT zh[R][KS3], zl[R][KS3];
 #pragma unroll
         for (int c = 0; c < NCH; ++c) {
             const int cn = c + 1 < NCH ? c + 1 : 0;
@@ -257,10 +306,11 @@ __global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float 
             if (more) fetch(cn, par ^ 1);  // lands during this chunk's MFMAs
             const uint4 *wb = bufp(par) + lane;
             f32x4 a0[R], a1[R];
-            if (c < T2 / 2) {
-                // layer 2 accumulators start at the bias (channel rows: 16t + 4q + r)
-                const f32x4 b0 = *reinterpret_cast<const f32x4 *>(&bias_s[C1 + 16 * (2 * c) + 4 * q]);
-                const f32x4 b1 = *reinterpret_cast<const f32x4 *>(&bias_s[C1 + 16 * (2 * c + 1) + 4 * q]);
+            // layer 2's bias (channel rows: 16t + 4q + r): the accumulators' initial value in X1, added
+            // after the unscaling in h3
+            const f32x4 b0 = c < T2 / 2 ? *reinterpret_cast<const f32x4 *>(&bias_s[C1 + 16 * (2 * c) + 4 * q]) : f32x4{};
+            const f32x4 b1 = c < T2 / 2 ? *reinterpret_cast<const f32x4 *>(&bias_s[C1 + 16 * (2 * c + 1) + 4 * q]) : f32x4{};
+            if (X1 && c < T2 / 2) {
 #pragma unroll
                 for (int rr = 0; rr < R; ++rr) {
                     a0[rr] = b0;
@@ -273,8 +323,8 @@ __global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float 
             if (c < T2 / 2) {  // layer 2: output tiles 2c, 2c+1 (channel rows x point columns)
 #pragma unroll
                 for (int s = 0; s < KS2; ++s) {
-                    const bf16x8 h0 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 0) * HV + 0) * 64]);
-                    const bf16x8 h1 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 1) * HV + 0) * 64]);
+                    const PT h0 = __builtin_bit_cast(PT, wb[((s * 2 + 0) * HV + 0) * 64]);
+                    const PT h1 = __builtin_bit_cast(PT, wb[((s * 2 + 1) * HV + 0) * 64]);
                     if constexpr (X1) {
 #pragma unroll
                         for (int rr = 0; rr < R; ++rr) {
@@ -282,8 +332,8 @@ __global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float 
                             a1[rr] = mfma_bf(h1, xh[rr][s], a1[rr]);
                         }
                     } else {
-                        const bf16x8 l0 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 0) * HV + 1) * 64]);
-                        const bf16x8 l1 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 1) * HV + 1) * 64]);
+                        const PT l0 = __builtin_bit_cast(PT, wb[((s * 2 + 0) * HV + 1) * 64]);
+                        const PT l1 = __builtin_bit_cast(PT, wb[((s * 2 + 1) * HV + 1) * 64]);
 #pragma unroll
                         for (int rr = 0; rr < R; ++rr) {
                             a0[rr] = mfma_bf(h0, xh[rr][s], a0[rr]);
@@ -297,8 +347,14 @@ __global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float 
                 }
 #pragma unroll
                 for (int rr = 0; rr < R; ++rr) {
+                    // unscale by 2^-(s_a + s_w) and add the bias: one fma by an exact power of two
+                    const float us = X1 ? 1.0f : ldexpf(1.0f, e2[rr] - 14 - sw2);
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
+                        if constexpr (!X1) {
+                            a0[rr][r] = fmaf(a0[rr][r], us, b0[r]);
+                            a1[rr][r] = fmaf(a1[rr][r], us, b1[r]);
+                        }
                         a0[rr][r] = relu_i(a0[rr][r]);
                         a1[rr][r] = relu_i(a1[rr][r]);
                     }
@@ -307,17 +363,28 @@ __global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float 
                 }
                 if (c == T2 / 2 - 1) {  // layer 2 complete: its output as layer-3 fragments
 #pragma unroll
-                    for (int rr = 0; rr < R; ++rr)
+                    for (int rr = 0; rr < R; ++rr) {
+                        float sc = 1.0f;
+                        if constexpr (!X1) {  // scaled by the tile's maximum
+                            uint32_t mb = 0;
+#pragma unroll
+                            for (int t = 0; t < T2; ++t)
+#pragma unroll
+                                for (int r = 0; r < 4; ++r) mb = max(mb, __float_as_uint(y2[rr][t][r]));  // ReLU outputs: non-negative bits
+                            e3[rr] = lidar_h3::wave_exp(mb);
+                            sc = lidar_h3::scale_of(e3[rr]);
+                        }
 #pragma unroll
                         for (int s = 0; s < KS3; ++s)
-                            split_pair(y2[rr][2 * s], y2[rr][2 * s + 1], zh[rr][s], zl[rr][s]);
+                            split_pair(y2[rr][2 * s], y2[rr][2 * s + 1], zh[rr][s], zl[rr][s], sc);
+                    }
                 }
             } else {  // layer 3: output tiles 2tp, 2tp+1, transposed (point rows), + max-pool
                 const int tp = c - T2 / 2;
 #pragma unroll
                 for (int s = 0; s < KS3; ++s) {
-                    const bf16x8 h0 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 0) * HV + 0) * 64]);
-                    const bf16x8 h1 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 1) * HV + 0) * 64]);
+                    const PT h0 = __builtin_bit_cast(PT, wb[((s * 2 + 0) * HV + 0) * 64]);
+                    const PT h1 = __builtin_bit_cast(PT, wb[((s * 2 + 1) * HV + 0) * 64]);
                     if constexpr (X1) {
 #pragma unroll
                         for (int rr = 0; rr < R; ++rr) {
@@ -325,8 +392,8 @@ __global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float 
                             a1[rr] = mfma_bf(zh[rr][s], h1, a1[rr]);
                         }
                     } else {
-                        const bf16x8 l0 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 0) * HV + 1) * 64]);
-                        const bf16x8 l1 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 1) * HV + 1) * 64]);
+                        const PT l0 = __builtin_bit_cast(PT, wb[((s * 2 + 0) * HV + 1) * 64]);
+                        const PT l1 = __builtin_bit_cast(PT, wb[((s * 2 + 1) * HV + 1) * 64]);
 #pragma unroll
                         for (int rr = 0; rr < R; ++rr) {
                             a0[rr] = mfma_bf(zh[rr][s], h0, a0[rr]);
@@ -345,7 +412,11 @@ __global__ __launch_bounds__(256, R == 1 ? 3 : 2) void sa_x3_kernel(const float 
 #pragma unroll
                     for (int rr = 0; rr < R; ++rr) {
                         const f32x4 &acc = hh ? a1[rr] : a0[rr];
-                        v = maxn(maxn(v, acc[0], acc[1]), acc[2], acc[3]);
+                        float m4 = maxn(acc[0], acc[1], __builtin_elementwise_maximum(acc[2], acc[3]));
+                        // a tile's rows share its scale (2^k x is monotone and exact): its max is
+                        // unscaled, before the max over the tiles, whose scales differ
+                        if constexpr (!X1) m4 = ldexpf(m4, e3[rr] - 14 - sw3);
+                        v = __builtin_elementwise_maximum(v, m4);
                     }
                     v = max_row_groups(v);
                     if (q == (t & 3)) mx[t >> 2] = __builtin_elementwise_maximum(mx[t >> 2], v);
@@ -416,6 +487,7 @@ __global__ __launch_bounds__(256, 4) void sa_x3_lean_kernel(const float *__restr
     const uint4 *W2 = packed;
     const uint4 *W3 = W2 + (int64_t)NL2 * CH2;
     const float *Bias = reinterpret_cast<const float *>(W3 + (int64_t)NL3 * CH3);
+    const X3Tail tl = *reinterpret_cast<const X3Tail *>(Bias + C1 + C2 + C3);
 
     // pass `seq` of an iteration: layer-2 chunk seq % NL2 for tile seq / NL2, then the layer-3 chunks
     auto fetch = [&](int seq, int dst) {
@@ -448,11 +520,14 @@ __global__ __launch_bounds__(256, 4) void sa_x3_lean_kernel(const float *__restr
 
 #pragma unroll 1
     for (int it = 0; it < ITERS; ++it) {
-        bf16x8 zh[R][KS3], zl[R][KS3];
+        f16x8 zh[R][KS3], zl[R][KS3];
+        int e3[R];  // the tiles' layer-3 input exponents (wave-uniform)
 #pragma unroll
         for (int rr = 0; rr < R; ++rr) {
-            // layer 1 of this tile's 16 rows: relu(P[k] - Q[c]) as the layer-2 hi / lo fragments
-            bf16x8 xh[KS2], xl[KS2];
+            // layer 1 of this tile's 16 rows: relu(P[k] - Q[c]) as the layer-2 hi / lo fragments,
+            // scaled by the tile's maximum
+            f16x8 xh[KS2], xl[KS2];
+            int e2;
             {
                 int zero = 0;
                 asm volatile("" : "+v"(zero));
@@ -466,43 +541,55 @@ __global__ __launch_bounds__(256, 4) void sa_x3_lean_kernel(const float *__restr
                     k = idx[cc * NS + t16 + col];
                 const f32x4 *pp = reinterpret_cast<const f32x4 *>(P + ((int64_t)b * n + k) * stride + 4 * q);
                 const f32x4 *qq = reinterpret_cast<const f32x4 *>(Q + cc * stride + 4 * q + zero);
+                f32x4 y[KS2][2];
+                uint32_t mb = 0;
 #pragma unroll
-                for (int s = 0; s < KS2; ++s) {
-                    f32x4 y[2];
+                for (int s = 0; s < KS2; ++s)
 #pragma unroll
                     for (int h = 0; h < 2; ++h) {
                         const f32x4 a = pp[4 * (2 * s + h)], c = qq[4 * (2 * s + h)];
 #pragma unroll
-                        for (int r = 0; r < 4; ++r) y[h][r] = relu(a[r] - c[r]);
+                        for (int r = 0; r < 4; ++r) {
+                            y[s][h][r] = relu(a[r] - c[r]);
+                            mb = max(mb, __float_as_uint(y[s][h][r]));  // ReLU outputs: non-negative bits
+                        }
                     }
-                    split_pair(y[0], y[1], xh[s], xl[s]);
-                }
+                e2 = lidar_h3::wave_exp(mb);
+                const float sc = lidar_h3::scale_of(e2);
+#pragma unroll
+                for (int s = 0; s < KS2; ++s) split_pair(y[s][0], y[s][1], xh[s], xl[s], sc);
             }
+            // layer 2's output is split chunk by chunk (layer-3 k-step c): its scale comes from the
+            // bound colsum(W2) 2^e2 + max|b2|, known before any chunk
+            e3[rr] = bound_exp3(tl, e2);
+            const float sc3 = lidar_h3::scale_of(e3[rr]);
 #pragma unroll
             for (int c = 0; c < NL2; ++c) {
                 fetch(rr * NL2 + c + 1, par ^ 1);  // a layer-3 pass always follows: lands during these MFMAs
                 const uint4 *wb = bufp(par) + lane;
-                f32x4 a0 = *reinterpret_cast<const f32x4 *>(&bias_s[16 * (2 * c) + 4 * q]);
-                f32x4 a1 = *reinterpret_cast<const f32x4 *>(&bias_s[16 * (2 * c + 1) + 4 * q]);
+                f32x4 a0 = f32x4{}, a1 = f32x4{};
 #pragma unroll
                 for (int s = 0; s < KS2; ++s) {
-                    const bf16x8 h0 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 0) * 2 + 0) * 64]);
-                    const bf16x8 l0 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 0) * 2 + 1) * 64]);
+                    const f16x8 h0 = __builtin_bit_cast(f16x8, wb[((s * 2 + 0) * 2 + 0) * 64]);
+                    const f16x8 l0 = __builtin_bit_cast(f16x8, wb[((s * 2 + 0) * 2 + 1) * 64]);
                     a0 = mfma_bf(h0, xh[s], a0);
                     a0 = mfma_bf(h0, xl[s], a0);
                     a0 = mfma_bf(l0, xh[s], a0);
-                    const bf16x8 h1 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 1) * 2 + 0) * 64]);
-                    const bf16x8 l1 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 1) * 2 + 1) * 64]);
+                    const f16x8 h1 = __builtin_bit_cast(f16x8, wb[((s * 2 + 1) * 2 + 0) * 64]);
+                    const f16x8 l1 = __builtin_bit_cast(f16x8, wb[((s * 2 + 1) * 2 + 1) * 64]);
                     a1 = mfma_bf(h1, xh[s], a1);
                     a1 = mfma_bf(h1, xl[s], a1);
                     a1 = mfma_bf(l1, xh[s], a1);
                 }
+                const f32x4 b0 = *reinterpret_cast<const f32x4 *>(&bias_s[16 * (2 * c) + 4 * q]);
+                const f32x4 b1 = *reinterpret_cast<const f32x4 *>(&bias_s[16 * (2 * c + 1) + 4 * q]);
+                const float us = ldexpf(1.0f, e2 - 14 - tl.s2);  // 2^-(s_a + s_w): one exact fma with the bias
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    a0[r] = relu_i(a0[r]);
-                    a1[r] = relu_i(a1[r]);
+                    a0[r] = relu_i(fmaf(a0[r], us, b0[r]));
+                    a1[r] = relu_i(fmaf(a1[r], us, b1[r]));
                 }
-                split_pair(a0, a1, zh[rr][c], zl[rr][c]);  // layer-2 chunk c = layer-3 k-step c
+                split_pair(a0, a1, zh[rr][c], zl[rr][c], sc3);  // layer-2 chunk c = layer-3 k-step c
                 if constexpr ((LIDAR_SA_ABL & 2) == 0) __syncthreads();
                 par ^= 1;
             }
@@ -516,10 +603,10 @@ __global__ __launch_bounds__(256, 4) void sa_x3_lean_kernel(const float *__restr
             for (int rr = 0; rr < R; ++rr) a0[rr] = a1[rr] = f32x4{};
 #pragma unroll
             for (int s = 0; s < KS3; ++s) {
-                const bf16x8 h0 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 0) * 2 + 0) * 64]);
-                const bf16x8 h1 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 1) * 2 + 0) * 64]);
-                const bf16x8 l0 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 0) * 2 + 1) * 64]);
-                const bf16x8 l1 = __builtin_bit_cast(bf16x8, wb[((s * 2 + 1) * 2 + 1) * 64]);
+                const f16x8 h0 = __builtin_bit_cast(f16x8, wb[((s * 2 + 0) * 2 + 0) * 64]);
+                const f16x8 h1 = __builtin_bit_cast(f16x8, wb[((s * 2 + 1) * 2 + 0) * 64]);
+                const f16x8 l0 = __builtin_bit_cast(f16x8, wb[((s * 2 + 0) * 2 + 1) * 64]);
+                const f16x8 l1 = __builtin_bit_cast(f16x8, wb[((s * 2 + 1) * 2 + 1) * 64]);
 #pragma unroll
                 for (int rr = 0; rr < R; ++rr) {
                     a0[rr] = mfma_bf(zh[rr][s], h0, a0[rr]);
@@ -537,7 +624,9 @@ __global__ __launch_bounds__(256, 4) void sa_x3_lean_kernel(const float *__restr
 #pragma unroll
                 for (int rr = 0; rr < R; ++rr) {
                     const f32x4 &acc = hh ? a1[rr] : a0[rr];
-                    v = maxn(maxn(v, acc[0], acc[1]), acc[2], acc[3]);
+                    // the tile's max, unscaled (its rows share the scale) before the max over tiles
+                    const float m4 = maxn(acc[0], acc[1], __builtin_elementwise_maximum(acc[2], acc[3]));
+                    v = __builtin_elementwise_maximum(v, ldexpf(m4, e3[rr] - 14 - tl.s3));
                 }
                 v = max_row_groups(v);
                 if (q == (t & 3)) mx[t >> 2] = __builtin_elementwise_maximum(mx[t >> 2], v);
@@ -623,6 +712,31 @@ __host__ float bf16_to_f(uint16_t h)
     memcpy(&f, &u, 4);
     return f;
 }
+// fp16 (RNE) bits of a float, and back (the host side of h3.hpp's split)
+__host__ uint16_t f16_bits(float f)
+{
+    const _Float16 h = (_Float16)f;
+    uint16_t u;
+    memcpy(&u, &h, 2);
+    return u;
+}
+__host__ float f16_to_f(uint16_t u)
+{
+    _Float16 h;
+    memcpy(&h, &u, 2);
+    return (float)h;
+}
+// a layer's scaling exponent s (max |W| 2^s < 2^14)
+__host__ int32_t layer_exp(const float *w, int64_t n)
+{
+    uint32_t m = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        uint32_t u;
+        memcpy(&u, &w[i], 4);
+        m = std::max(m, u & 0x7fffffffu);
+    }
+    return 14 - lidar_h3::exp_of_bits(m);
+}
 
 }  // namespace
 
@@ -631,11 +745,12 @@ LIDAR_EXPORT int64_t lidar_mlp_packed_size_x3(int32_t xyz_level, int32_t c1, int
 {
     const int64_t w1 = xyz_level ? (int64_t)(c1 / 16) * 64 * 4 : 0;
     return w1 + ((int64_t)(c2 / 32) * (c1 / 32) + (int64_t)(c3 / 32) * (c2 / 32)) * 4 * 64 * 16 +
-           (int64_t)(c1 + c2 + c3) * 4;
+           (int64_t)(c1 + c2 + c3) * 4 + (int64_t)sizeof(X3Tail);
 }
 
 // host packer: w1 (3 + ..., c1) read only for an xyz level (its xyz rows, fp32 as the 16-row
-// kernel's layer 1); w2 (c1, c2), w3 (c2, c3) split into bf16 hi / lo in the fragment order
+// kernel's layer 1); w2 (c1, c2), w3 (c2, c3) scaled by their layer's power of two and split into
+// fp16 hi / lo in the fragment order (h3.hpp); the tail holds the exponents and layer 3's bound
 LIDAR_EXPORT int lidar_mlp_pack_x3_f32(int32_t xyz_level, int32_t c1, int32_t c2, int32_t c3, const float *w1,
                                        const float *b1, const float *w2, const float *b2, const float *w3,
                                        const float *b3, void *packed)
@@ -653,7 +768,11 @@ LIDAR_EXPORT int lidar_mlp_pack_x3_f32(int32_t xyz_level, int32_t c1, int32_t c2
             }
         o = reinterpret_cast<char *>(f);
     }
-    auto layer = [&](const float *w, int cin, int cout) {
+    X3Tail tail;
+    tail.s2 = layer_exp(w2, (int64_t)c1 * c2);
+    tail.s3 = layer_exp(w3, (int64_t)c2 * c3);
+    auto layer = [&](const float *w, int cin, int cout, int32_t sexp) {
+        const float sc = std::ldexp(1.0f, sexp);
         uint16_t *u = reinterpret_cast<uint16_t *>(o);
         for (int c = 0; c < cout / 32; ++c)
             for (int s = 0; s < cin / 32; ++s)
@@ -662,18 +781,30 @@ LIDAR_EXPORT int lidar_mlp_pack_x3_f32(int32_t xyz_level, int32_t c1, int32_t c2
                         for (int l = 0; l < 64; ++l)
                             for (int j = 0; j < 8; ++j) {
                                 const int in = 32 * s + 16 * (j >> 2) + 4 * (l >> 4) + (j & 3);
-                                const float v = w[(int64_t)in * cout + 16 * (2 * c + t) + (l & 15)];
-                                const uint16_t hi = bf16_rne(v);
-                                *u++ = h == 0 ? hi : bf16_rne(v - bf16_to_f(hi));
+                                const float v = w[(int64_t)in * cout + 16 * (2 * c + t) + (l & 15)] * sc;
+                                const uint16_t hi = f16_bits(v);
+                                *u++ = h == 0 ? hi : f16_bits(v - f16_to_f(hi));
                             }
         o = reinterpret_cast<char *>(u);
     };
-    layer(w2, c1, c2);
-    layer(w3, c2, c3);
+    layer(w2, c1, c2, tail.s2);
+    layer(w3, c2, c3, tail.s3);
     float *f = reinterpret_cast<float *>(o);
     for (int i = 0; i < c1; ++i) *f++ = b1[i];
     for (int i = 0; i < c2; ++i) *f++ = b2[i];
     for (int i = 0; i < c3; ++i) *f++ = b3[i];
+    // layer 3's input bound (lean kernel): max over channels of sum_k |W2[k][c]|, and max |b2|,
+    // rounded up (float64 sums, then the next float up)
+    double cs = 0.0, bm = 0.0;
+    for (int c = 0; c < c2; ++c) {
+        double a = 0.0;
+        for (int k = 0; k < c1; ++k) a += std::fabs((double)w2[(int64_t)k * c2 + c]);
+        cs = std::max(cs, a);
+        bm = std::max(bm, std::fabs((double)b2[c]));
+    }
+    tail.colsum2 = std::nextafter((float)cs, INFINITY);
+    tail.bmax2 = std::nextafter((float)bm, INFINITY);
+    memcpy(f, &tail, sizeof tail);
     return LIDAR_OK;
 }
 

@@ -343,9 +343,10 @@ def _grid(people_positions, x_range, y_range, grid_size):
     nx, ny = nat.grid_dims(x_min, x_max, y_min, y_max, grid_size)
     p = _on_device(np.asarray(people_positions, dtype=np.float64).reshape(-1, 2), torch.float64)
     dev = p.device
-    gx = torch.empty(nx, dtype=torch.float64, device=dev)
-    gy = torch.empty(ny, dtype=torch.float64, device=dev)
-    buf = torch.empty(3 * nx * ny + 13, dtype=torch.float64, device=dev)
+    with nat.grid_alloc():
+        gx = torch.empty(nx, dtype=torch.float64, device=dev)
+        gy = torch.empty(ny, dtype=torch.float64, device=dev)
+        buf = torch.empty(3 * nx * ny + 13, dtype=torch.float64, device=dev)
     nat.call("lidar_density_grid_f64", _handle(), nat.ptr(p), len(p), float(x_min), float(x_max),
              float(y_min), float(y_max), float(grid_size), nx, ny, nat.ptr(gx), nat.ptr(gy), nat.ptr(buf),
              nat.stream_ptr())

@@ -15,7 +15,7 @@ return per frame the reference's ``analyze`` result (the big per-point arrays st
 the device).  Results are the drop-in path's, bit for bit (same kernels).
 """
 import ctypes
-import threading
+from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 import torch
@@ -32,6 +32,27 @@ class DensityStream:
         self.grid_size = float(grid_size)
         self._streams = [torch.cuda.Stream(device=self.device) for _ in range(workers)]
         self._bufs = [{} for _ in range(workers)]
+        # one persistent host thread per lane: the library's handles (workspaces) are per thread,
+        # so a lane keeps its handles from call to call instead of creating them per call
+        self._lanes = []
+        self._last_people = None
+
+    def _lane(self, j):
+        while len(self._lanes) <= j:
+            self._lanes.append(ThreadPoolExecutor(max_workers=1, thread_name_prefix=f"density-lane{len(self._lanes)}"))
+        return self._lanes[j]
+
+    def close(self):
+        """Stop the lane threads (their handles are destroyed with them)."""
+        for ex in self._lanes:
+            ex.shutdown(wait=True)
+        self._lanes = []
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
     def _buffers(self, w, n):
         b = self._bufs[w]
@@ -77,7 +98,7 @@ class DensityStream:
         x_min, x_max, y_min, y_max = S[5], S[6], S[7], S[8]
         nx, ny = nat.grid_dims(x_min, x_max, y_min, y_max, self.grid_size)
         m = nx * ny
-        with torch.cuda.stream(s):
+        with torch.cuda.stream(s), nat.grid_alloc():
             gx = torch.empty(nx, dtype=torch.float64, device=self.device)
             gy = torch.empty(ny, dtype=torch.float64, device=self.device)
             buf = torch.empty(3 * m + 13, dtype=torch.float64, device=self.device)
@@ -107,12 +128,10 @@ class DensityStream:
                 except Exception as e:  # reported per frame, like the reference per call
                     out[i] = e
             self._streams[w].synchronize()
+            nat.trim(self.device.index)  # this lane's work is done: free retired workspaces
 
-        ts = [threading.Thread(target=work, args=(w,)) for w in range(min(self.workers, len(frames)))]
-        for t in ts:
-            t.start()
-        for t in ts:
-            t.join()
+        for f in [self._lane(w).submit(work, w) for w in range(min(self.workers, len(frames)))]:
+            f.result()
         for r in out:
             if isinstance(r, Exception):
                 raise r
@@ -161,16 +180,14 @@ class DensityStream:
                     except Exception as e:  # reported in batch order below
                         out[i] = e
             streams[j].synchronize()
+            nat.trim(self.device.index)  # this lane's work is done: free retired workspaces
 
-        ts = [threading.Thread(target=work, args=(j,)) for j in range(lanes)]
-        for t in ts:
-            t.start()
-        for t in ts:
-            t.join()
+        for f in [self._lane(j).submit(work, j) for j in range(lanes)]:
+            f.result()
         for r in out:
             if isinstance(r, Exception):
                 raise r
-        if batches:  # the last batch in batch order, whichever lane finished last
+        if batches and people[-1] is not None:  # the last batch in batch order (an empty one keeps the previous)
             self._last_people = people[-1]
         return out
 
@@ -178,6 +195,8 @@ class DensityStream:
         """The people positions of every frame of the last batch of run_batch / run_batches (in
         batch order), concatenated in frame order: a (sum K_f, 2) float64 CUDA tensor (what
         extract_people_positions returns per frame)."""
+        if self._last_people is None:
+            return torch.empty((0, 2), dtype=torch.float64, device=self.device)
         people, offs, K = self._last_people
         rows = [people[int(o):int(o) + int(k)] for o, k in zip(offs[:-1], K) if k > 0]
         return torch.cat(rows) if rows else people[:0]
@@ -189,6 +208,8 @@ class DensityStream:
         res, people = self._run_batch(frames)
         if people is not None:
             self._last_people = people
+        torch.cuda.current_stream(self.device).synchronize()
+        nat.trim(self.device.index)
         return res
 
     def _run_batch(self, frames):
@@ -245,7 +266,8 @@ class DensityStream:
         res = [None] * F
         if out_off:
             jd = torch.from_numpy(jobs).to(dev)
-            out = torch.empty(out_off, **f64)
+            with nat.grid_alloc():
+                out = torch.empty(out_off, **f64)
             nat.call("lidar_density_batch_f64", h, nat.ptr(people), nat.ptr(offs), nat.ptr(kdev), F, nat.ptr(jd),
                      nat.ptr(out), scr_off, sp)
             ob = out.cpu().numpy()  # read-back 3

@@ -211,7 +211,8 @@ def group_mlp16(p, q, idx, n, packed, widths, out, out_offset=0, xyz_level=False
 
 
 def pack_branch_x3(layers, xyz_level):
-    """Host-side packed image (uint8) for lidar_sa_group_mlp_x3_f32 (bf16 hi/lo fragments)."""
+    """Host-side packed image (uint8) for lidar_sa_group_mlp_x3_f32 (fp16 hi/lo fragments of each layer's
+    W 2^s, h3 arithmetic; csrc/h3.hpp)."""
     (w1, b1), (w2, b2), (w3, b3) = layers
     c1, c2, c3 = w1.shape[1], w2.shape[1], w3.shape[1]
     lib = nat.load_library()
@@ -263,12 +264,13 @@ def layer1_points_x1(x_rows, xyz, cfeat, branches):
     B, N, _ = xyz.shape
     nat.call("lidar_concat_xyz_pad_f32", nat.handle(xyz.device.index), nat.ptr(xyz), B * N, nat.ptr(x_rows),
              x_rows.shape[1], cfeat, nat.stream_ptr())
-    return [dense_x3s(x_rows, br["pre_x1"]["w1f_x3"], br["pre_x1"]["b1"], br["pre_x1"]["w1f"].shape[1],
+    return [dense_x3s(x_rows, br["pre_x1"]["w1f_x1"], br["pre_x1"]["b1"], br["pre_x1"]["w1f"].shape[1],
                       relu=False, x1=True) for br in branches]
 
 
 def group_mlp_x3(p, q, idx, n, packed, widths, out, out_offset=0, xyz_level=False):
-    """group_mlp16 with layers 2-3 on split-bf16 MFMAs (fp32-accurate, see sa_mlp_x3.hip)."""
+    """group_mlp16 with layers 2-3 in h3 arithmetic (scaled fp16 hi/lo pieces on the fp16 MFMAs,
+    fp32-class products, see sa_mlp_x3.hip)."""
     B, M, ns = idx.shape
     c1, c2, c3 = widths
     stride = 3 if xyz_level else p.shape[1]
@@ -328,7 +330,7 @@ def layer1_per_point(x_rows, xyz, cfeat, new_xyz, branches, x3=True):
     (R = B*N rounded up to 128; the previous level wrote f in place), xyz (B, N, 3);
     new_xyz (B, M, 3).  Returns per branch (P, Q): P = x_rows W1' + b1 (R, c1),
     Q = [c, 0] W1_xyz' (B*M rounded to 128, c1), both without ReLU (columns padded to a
-    multiple of 128 with zero weights).  x3: on the split-bf16 GEMM (fp32 rows in, split in the
+    multiple of 128 with zero weights).  x3: on the h3 GEMM (fp32 rows in, scaled and split in the
     tile loop); else the native fp32 MFMA GEMM."""
     B, N, _ = xyz.shape
     M = new_xyz.shape[1]
@@ -351,14 +353,15 @@ def layer1_per_point(x_rows, xyz, cfeat, new_xyz, branches, x3=True):
     return out
 
 
-def pack_dense_x3(w):
-    """(k, cout) fp32 CUDA weights -> the x3 GEMM's packed bf16 hi / lo image (device)."""
+def pack_dense_x3(w, x1=False):
+    """(k, cout) fp32 CUDA weights -> the dense GEMM's packed image (device): the h3 image (fp16 hi /
+    lo of W 2^s, lidar_dense_x3_pack_f32) or, x1, the bf16 spec's image (lidar_dense_x1_pack_f32)."""
     _dev_check(w)
     k, cout = w.shape
     nbytes = nat.load_library().lidar_dense_x3_packed_size(k, cout)
     out = torch.empty((nbytes,), dtype=torch.uint8, device=w.device)
-    nat.call("lidar_dense_x3_pack_f32", nat.handle(w.device.index), nat.ptr(w), k, cout, nat.ptr(out),
-             nat.stream_ptr())
+    nat.call("lidar_dense_x1_pack_f32" if x1 else "lidar_dense_x3_pack_f32", nat.handle(w.device.index), nat.ptr(w),
+             k, cout, nat.ptr(out), nat.stream_ptr())
     return out
 
 
@@ -380,63 +383,25 @@ def dense_relu(x, w, b, pool_rows=0, out=None):
     return dense(x, w, b, True, pool_rows, out)
 
 
-class SplitPlanes:
-    """Activations pre-split for the x3 GEMM: planes (2, rows, lda) bf16 = hi, lo of x (rows, k);
-    lda = k rounded up to 32, columns k.. zero (csrc/dense_x3s.hip)."""
-
-    def __init__(self, planes, k):
-        self.planes, self.k = planes, k
-
-    @property
-    def rows(self):
-        return self.planes.shape[1]
-
-
-def split_x3(x, k=None):
-    """fp32 rows x (rows, >= k) -> SplitPlanes (lidar_split_x3_f32)."""
-    _dev_check(x)
-    rows, ldx = x.shape
-    k = ldx if k is None else k
-    lda = (k + 31) // 32 * 32
-    planes = torch.empty((2, rows, lda), dtype=torch.bfloat16, device=x.device)
-    nat.call("lidar_split_x3_f32", nat.handle(x.device.index), nat.ptr(x), rows, k, ldx, nat.ptr(planes),
-             rows * lda, lda, nat.stream_ptr())
-    return SplitPlanes(planes, k)
-
-
-def dense_x3s(a, wpack, b, cout, relu=True, split_out=False, pool_rows=0, out=None, x1=False):
-    """a @ W + b on the x3 GEMM of csrc/dense_x3s.hip (wpack = pack_dense_x3(W)): a is
-    SplitPlanes (lidar_dense_x3s_f32) or fp32 rows (rows, k) (lidar_dense_x3f_f32, split in
-    the tile loop).  Returns fp32 rows (rows, cout), SplitPlanes (split_out) or, with
-    pool_rows, the fp32 max over runs of pool_rows rows (ReLU)."""
-    f32 = not isinstance(a, SplitPlanes)
-    rows, lda = (a.shape[0], a.shape[1]) if f32 else (a.planes.shape[1], a.planes.shape[2])
-    dev = a.device if f32 else a.planes.device
+def dense_x3s(a, wpack, b, cout, relu=True, pool_rows=0, out=None, x1=False):
+    """a (rows, k) fp32 @ W + b on the dense GEMM of csrc/dense_x3s.hip (lidar_dense_x3f_f32; wpack =
+    pack_dense_x3(W), h3 arithmetic; x1: pack_dense_x3(W, x1=True), the bf16 spec).  Returns fp32
+    rows (rows, cout) or, with pool_rows, the fp32 max over runs of pool_rows rows (ReLU)."""
+    rows, lda = a.shape
+    dev = a.device
     if pool_rows:
         mode = 2
         if out is None:
             out = torch.zeros((rows // pool_rows, cout), dtype=torch.float32, device=dev)
-        ldo, oplane, res = out.shape[1], 0, out
-    elif split_out:
-        mode = 1
-        out = torch.empty((2, rows, cout), dtype=torch.bfloat16, device=dev)
-        ldo, oplane, res = cout, rows * cout, SplitPlanes(out, cout)
     else:
         mode = 0
         if out is None:
             out = torch.empty((rows, cout), dtype=torch.float32, device=dev)
-        ldo, oplane, res = out.shape[1], 0, out
-    if f32:
-        _dev_check(a, wpack, b, out)
-        nat.call("lidar_dense_x3f_f32", nat.handle(dev.index), nat.ptr(a), lda, rows, lda, nat.ptr(wpack), nat.ptr(b),
-                 cout, mode | (4 if x1 else 0), 1 if relu else 0, pool_rows, nat.ptr(out), oplane, ldo,
-                 nat.stream_ptr())
-        return res
-    _dev_check(a.planes, wpack, b, out)
-    nat.call("lidar_dense_x3s_f32", nat.handle(dev.index), nat.ptr(a.planes), rows * lda, lda, rows, a.k,
-             nat.ptr(wpack), nat.ptr(b), cout, mode, 1 if relu else 0, pool_rows, nat.ptr(out), oplane, ldo,
+    _dev_check(a, wpack, b, out)
+    nat.call("lidar_dense_x3f_f32", nat.handle(dev.index), nat.ptr(a), lda, rows, lda, nat.ptr(wpack), nat.ptr(b),
+             cout, mode | (4 if x1 else 0), 1 if relu else 0, pool_rows, nat.ptr(out), 0, out.shape[1],
              nat.stream_ptr())
-    return res
+    return out
 
 
 # ----------------------------------------------------------------------- backbone
@@ -476,8 +441,8 @@ class PointNet2Backbone:
 
     def __init__(self, cfg=SSG, weights=None, device="cuda", seed=0, dtype="f32", x3=True):
         """dtype "f32" (the fp32 contract: features within 1e-4 of the fp32 oracle): x3=True (default)
-        runs the MLPs on the bf16 matrix cores in split-bf16 arithmetic (lidar_sa_group_mlp_x3_f32,
-        lidar_dense_x3s_f32), x3=False on the native fp32 matrix cores (lidar_sa_group_mlp16_f32,
+        runs the MLPs on the fp16 matrix cores in h3 arithmetic (lidar_sa_group_mlp_x3_f32,
+        lidar_dense_x3f_f32), x3=False on the native fp32 matrix cores (lidar_sa_group_mlp16_f32,
         lidar_dense_f32) — the strict-fp32 path.
         dtype "bf16" (BASELINE configs[4]): the SA branches in the bf16 spec on the X1 kernels
         (inputs, activations and weights rounded to bf16, fp32 accumulation); group_all stays in
@@ -526,7 +491,7 @@ class PointNet2Backbone:
                         b1p = np.zeros(cp, np.float32)
                         b1p[:w1.shape[1]] = b1
                         br["pre_x1"] = {"w1f": t(w1f), "b1": t(b1p)}
-                        br["pre_x1"]["w1f_x3"] = pack_dense_x3(br["pre_x1"]["w1f"])
+                        br["pre_x1"]["w1f_x1"] = pack_dense_x3(br["pre_x1"]["w1f"], x1=True)
                 else:
                     if x3:
                         br["packed_x3"] = torch.from_numpy(pack_branch_x3(layers, xyz_level)).to(self.device)
@@ -672,10 +637,10 @@ class PointNet2Backbone:
             M, rows = mp, B * mp
         t = self.timers
         ws, bs = lvl["w"], lvl["b"]
-        if self.x3:  # dense1 / dense2 hand split planes to the next layer; dense3 fuses the max-pool
+        if self.x3:  # fp32 rows between the layers; dense3 fuses the max-pool
             wp = lvl["w_x3"]
-            h1 = _call(t, "sa3_dense1", B, dense_x3s, x2, wp[0], bs[0], ws[0].shape[1], split_out=True)
-            h2 = _call(t, "sa3_dense2", B, dense_x3s, h1, wp[1], bs[1], ws[1].shape[1], split_out=True)
+            h1 = _call(t, "sa3_dense1", B, dense_x3s, x2, wp[0], bs[0], ws[0].shape[1])
+            h2 = _call(t, "sa3_dense2", B, dense_x3s, h1, wp[1], bs[1], ws[1].shape[1])
             return _call(t, "sa3_dense3_pool", B, dense_x3s, h2, wp[2], bs[2], ws[2].shape[1], pool_rows=M)
         h1 = _call(t, "sa3_dense1", B, dense_relu, x2, ws[0], bs[0])
         h2 = _call(t, "sa3_dense2", B, dense_relu, h1, ws[1], bs[1])
@@ -895,7 +860,9 @@ class _Feed:
         self.buf, self.readies = [], []
         return self._issue(xs, evs)
 
-    def flush(self):
+    def flush(self, trim=True):
+        """Issue a partial last group and drain the pipeline.  trim: then wait for the side streams
+        and free the workspaces the library's handles retired while growing (lidar_trim)."""
         out = []
         if self.buf:
             xs, evs = self.buf, self.readies
@@ -904,4 +871,9 @@ class _Feed:
         while self.pending:
             slot, pxs = self.pending.pop(0)
             out += self.p._rest(slot, pxs, self.main)
+        if trim:
+            for fs in self.p.fps_streams:
+                fs.synchronize()
+            self.main.synchronize()
+            nat.trim(self.p.bb.device.index)
         return out

@@ -84,3 +84,17 @@ def test_device_cache_digest_without_xxhash():
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     r = subprocess.run([sys.executable, "-c", code], cwd=repo, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr
+
+
+@pytest.mark.parametrize("x_max,err", [(1e13, MemoryError), (1e12, MemoryError), (float("inf"), ValueError),
+                                       (1e300, ValueError), (float("nan"), ValueError), (2e18, ValueError)])
+def test_grid_dims_errors_match_numpy(x_max, err):
+    """calculate_grid_density's grid (utils/data_processing.py:305-319) for extreme extents: the
+    error type numpy's np.arange raises for the same edges (a length it cannot hold or compute:
+    ValueError; a representable but unallocatable grid: MemoryError)."""
+    from lidar_ai_recommendation_software_amd import _native as nat
+    with pytest.raises(err):
+        np.arange(0.0 - 2.0, (x_max + 2.0) + 1.0, 1.0) if err is ValueError else nat.grid_dims(0.0, x_max, 0.0, 1.0, 1.0)
+    with pytest.raises(err):
+        nat.grid_dims(0.0, x_max, 0.0, 1.0, 1.0)
+    assert nat.grid_dims(0.0, 30.0, -15.0, 15.0, 1.0) == (34, 34)

@@ -1,13 +1,14 @@
 """CPU check of the fused SA kernels' weight images (no GPU needed).
 
-``sa_x3_kernel`` (csrc/sa_mlp_x3.hip) chains layers on v_mfma_f32_16x16x32_bf16 without any
-transpose: the accumulator pair of output tiles (2s, 2s+1) IS the k-step-s operand of the next
-layer, element j of lane l holding channel in(s, l>>4, j) = 32s + 16(j>>2) + 4(l>>4) + (j&3).
-That k order lives only in the packed weight image built by the library's host packers
-(``lidar_mlp_pack_x3_f32``: bf16 hi / lo fragments; ``lidar_mlp_pack_x1_f32``: the bf16 spec's
-fragments).  These tests decode the images by the documented layout, check that every weight
-appears exactly once with the exact split (hi = bf16(w), lo = bf16(w - hi)), and emulate one
-layer lane by lane (16x16x32 fragment semantics) against the plain matrix product, so a wrong
+``sa_x3_kernel`` (csrc/sa_mlp_x3.hip) chains layers on v_mfma_f32_16x16x32_f16 (h3) /
+_bf16 (X1) without any transpose: the accumulator pair of output tiles (2s, 2s+1) IS the k-step-s
+operand of the next layer, element j of lane l holding channel in(s, l>>4, j) = 32s + 16(j>>2) +
+4(l>>4) + (j&3).  That k order lives only in the packed weight image built by the library's host
+packers (``lidar_mlp_pack_x3_f32``: fp16 hi / lo fragments of each layer's W 2^s, the exponents and
+layer 3's input bound in a tail; ``lidar_mlp_pack_x1_f32``: the bf16 spec's fragments).  These
+tests decode the images by the documented layout, check that every weight appears exactly once
+with the exact split (hi = fp16(w 2^s), lo = fp16(w 2^s - hi), max |w| 2^s < 2^14), and emulate
+one layer lane by lane (16x16x32 fragment semantics) against the plain matrix product, so a wrong
 packing order fails here before any GPU run."""
 import numpy as np
 import pytest
@@ -25,11 +26,21 @@ def bits_to_f(u16):
     return (u16.astype(np.uint32) << 16).view(np.float32)
 
 
+def f16_to_f(u16):
+    return u16.astype(np.uint16).view(np.float16).astype(np.float32)
+
+
+def layer_exp(w):
+    """the packer's scaling exponent: max |w| 2^s < 2^14 <= 2 max |w| 2^s"""
+    m = float(np.abs(w).max())
+    return 14 - (int(np.frexp(np.float32(m))[1]) if m > 0 else -100)
+
+
 def in_channel(s, g, j):
     return 32 * s + 16 * (j >> 2) + 4 * g + (j & 3)
 
 
-def decode_layer(u16, cin, cout, halves):
+def decode_layer(u16, cin, cout, halves, conv=bits_to_f):
     """(cout/32, cin/32, 2 tiles, halves, 64 lanes, 8) fragments -> per half the (cin, cout)
     matrix they encode (NaN where nothing was written) and how often each entry was written."""
     frag = u16[: (cout // 32) * (cin // 32) * 2 * halves * 64 * 8].reshape(cout // 32, cin // 32, 2, halves, 64, 8)
@@ -40,7 +51,7 @@ def decode_layer(u16, cin, cout, halves):
     for hh in range(halves):
         m = np.full((cin, cout), np.nan, np.float32)
         sel = h == hh
-        m[rows[sel], cols[sel]] = bits_to_f(frag[sel])
+        m[rows[sel], cols[sel]] = conv(frag[sel])
         mats.append(m)
     np.add.at(hits, (rows[h == 0], cols[h == 0]), 1)
     return mats, frag.size * 2, hits
@@ -66,13 +77,22 @@ def test_x3_image_holds_every_weight_split_exactly(cfg_name, level, branch):
         off = w1img.nbytes
     u16 = np.frombuffer(raw[off:], np.uint16)
     for w, cin, cout in ((w2, c1, c2), (w3, c2, c3)):
-        (hi, lo), used, hits = decode_layer(u16, cin, cout, 2)
+        (hi, lo), used, hits = decode_layer(u16, cin, cout, 2, f16_to_f)
         assert (hits == 1).all(), "every entry of W must be written exactly once"
-        assert np.array_equal(bf16_bits(hi), bf16_bits(tier_n.bf16_round(w))) and np.array_equal(hi, tier_n.bf16_round(w))
-        assert np.array_equal(lo, tier_n.bf16_round(w - hi)), "lo is not bf16(w - hi)"
+        ws = w * np.float32(2.0 ** layer_exp(w))
+        assert np.abs(ws).max() < 2 ** 14
+        assert np.array_equal(hi, ws.astype(np.float16).astype(np.float32)), "hi is not fp16(w 2^s)"
+        assert np.array_equal(lo, (ws - hi).astype(np.float16).astype(np.float32)), "lo is not fp16(w 2^s - hi)"
         u16 = u16[used // 2:]
-    biases = np.frombuffer(u16.tobytes(), np.float32)
+    tail = u16.tobytes()
+    nb = 4 * (c1 + c2 + c3)
+    biases = np.frombuffer(tail[:nb], np.float32)
     assert np.array_equal(biases, np.concatenate([b1, b2, b3]).astype(np.float32))
+    s2, s3 = np.frombuffer(tail[nb:nb + 8], np.int32)
+    colsum2, bmax2 = np.frombuffer(tail[nb + 8:nb + 16], np.float32)
+    assert (s2, s3) == (layer_exp(w2), layer_exp(w3)) and len(tail) == nb + 16
+    cs = np.abs(w2.astype(np.float64)).sum(axis=0).max()
+    assert cs <= colsum2 <= cs * (1 + 2 ** -20) and np.abs(b2).max() <= bmax2 <= np.abs(b2).max() * (1 + 2 ** -20)
 
 
 def mfma_16x16x32(acc, a_frag, b_frag):
@@ -90,19 +110,23 @@ def mfma_16x16x32(acc, a_frag, b_frag):
 def test_x3_chain_emulation_matches_matrix_form():
     """Layer 2 of SSG's SA2 branch as the kernel computes it: activations of 16 points in the
     accumulator layout of layer 1 (reg r of lane l = channel 16 t + 4 (l >> 4) + r of point
-    l & 15), split_pair into k-step fragments, three MFMAs per product against the packed
-    fragments; vs the x3 formula on plain matrices."""
+    l & 15), scaled by the tile's power of two and split_pair'ed into k-step fragments, three
+    MFMAs per product against the packed fragments, unscaled; vs the h3 formula on plain
+    matrices, and within 3 2^-22 per product (+ the fp32 sums) of the exact product."""
     rng = np.random.default_rng(0)
     layers = pn.init_weights(pn.SSG, seed=4)[1][0]
     (w1, _), (w2, b2), _ = layers
     c1, c2 = w1.shape[1], w2.shape[1]
     img = pn.pack_branch_x3(layers, False)
-    (hi, lo), _, _ = decode_layer(np.frombuffer(img.tobytes(), np.uint16), c1, c2, 2)
+    (hi, lo), _, _ = decode_layer(np.frombuffer(img.tobytes(), np.uint16), c1, c2, 2, f16_to_f)
     frag = np.frombuffer(img.tobytes(), np.uint16)[: (c2 // 32) * (c1 // 32) * 2 * 2 * 64 * 8]
     frag = frag.reshape(c2 // 32, c1 // 32, 2, 2, 64, 8)
-    x = np.abs(rng.standard_normal((16, c1))).astype(np.float32)  # 16 points' layer-1 outputs
-    xh = tier_n.bf16_round(x)
-    xl = tier_n.bf16_round(x - xh)
+    x = np.abs(rng.standard_normal((16, c1))).astype(np.float32) * np.float32(3e-3)  # 16 points' layer-1 outputs
+    e = int(np.frexp(np.abs(x).max())[1])  # the tile's exponent: max < 2^e
+    S = np.float32(2.0 ** (14 - e))
+    xs = x * S
+    xh = xs.astype(np.float16).astype(np.float32)
+    xl = (xs - xh).astype(np.float16).astype(np.float32)
     got = np.zeros((c2, 16))
     for c in range(c2 // 32):
         for t in range(2):
@@ -113,17 +137,19 @@ def test_x3_chain_emulation_matches_matrix_form():
                 j = np.arange(8)[None, :]
                 ch = in_channel(s, l >> 4, j)
                 bh, bl = xh[l & 15, ch], xl[l & 15, ch]
-                wh = bits_to_f(frag[c, s, t, 0]).astype(np.float64)
-                wl = bits_to_f(frag[c, s, t, 1]).astype(np.float64)
+                wh = f16_to_f(frag[c, s, t, 0]).astype(np.float64)
+                wl = f16_to_f(frag[c, s, t, 1]).astype(np.float64)
                 acc = mfma_16x16x32(acc, wh, bh)
                 acc = mfma_16x16x32(acc, wh, bl)
                 acc = mfma_16x16x32(acc, wl, bh)
             got[16 * (2 * c + t):16 * (2 * c + t) + 16] = acc  # D rows = output channels, columns = points
     want = (xh.astype(np.float64) @ hi + xl.astype(np.float64) @ hi + xh.astype(np.float64) @ lo).T
     np.testing.assert_allclose(got, want, rtol=1e-12, atol=1e-12)
-    # and the x3 product is within the fp32 contract of the fp32 matrix product
+    # unscaled, the h3 product is within 3 2^-22 (1 + 2^-10) sum |x w| of the exact one
+    got = got * 2.0 ** -(14 - e + layer_exp(w2))
     ref = (x.astype(np.float64) @ w2.astype(np.float64)).T
-    np.testing.assert_allclose(got, ref, rtol=0, atol=2e-4 * np.abs(ref).max())
+    mag = (np.abs(x).astype(np.float64) @ np.abs(w2).astype(np.float64)).T
+    assert np.all(np.abs(got - ref) <= 3 * 2.0 ** -22 * (1 + 2 ** -10) * mag)
 
 
 @pytest.mark.parametrize("cfg_name,level,branch", [("msg", 0, 1), ("msg", 1, 2), ("ssg", 1, 0)])

@@ -135,7 +135,7 @@ __device__ int block_flag_scan(BlockScratch &s, bool f, int *total)
 #endif
 // rows per staged chunk: 3 072 (147 KiB double-buffered; the kernel is one 1 024-thread workgroup per CU
 // by its registers anyway): preprocess 2.70 ms per 32 frames vs 2.79 at 2 048 and 2.98 at 1 024
-// (tools/gpu_ab_seqrows.sh): fewer chunk barriers, each waiting on the next chunk's staging
+// (round-3 A/B): fewer chunk barriers, each waiting on the next chunk's staging
 constexpr int kSeqRows = LIDAR_SEQ_ROWS;
 // rows whose LDS reads are issued before their dependent adds (32 measured equal, 64 slower: the
 // chain is bound by the dependent fp64 adds, not by the LDS reads)

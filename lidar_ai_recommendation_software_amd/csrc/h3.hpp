@@ -57,8 +57,9 @@ __device__ __forceinline__ void split2(float v0, float v1, uint32_t &hi, uint32_
     typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
     const f16x2 h = {(_Float16)v0, (_Float16)v1};
     hi = __builtin_bit_cast(uint32_t, h);
-    uint32_t l = 0;
-    asm volatile("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "+v"(l) : "v"(hi), "v"(v0));
+    // mixlo writes the low half (its high half is whatever the register held: mixhi overwrites it)
+    uint32_t l;
+    asm volatile("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(l) : "v"(hi), "v"(v0));
     asm volatile("v_fma_mixhi_f16 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(l) : "v"(hi), "v"(v1));
     lo = l;
 }

@@ -1,4 +1,4 @@
-"""Reduce the three SQ / GRBM passes of `tools/gpu_pmc_alone.sh` (the SSG kernels alone, tools/ssg_alone.py)
+"""Reduce the three SQ / GRBM passes of the round-3 PMC script (history at f4fc716) (the SSG kernels alone, tools/ssg_alone.py)
 to per-kernel shares: MFMA busy (SQ_VALU_MFMA_BUSY_CYCLES over 1024 SIMDs x GRBM_GUI_ACTIVE / 8), and the
 disjoint wave-cycle shares SQ_WAIT_ANY (parked at s_waitcnt / barrier), SQ_WAIT_INST_ANY (issue stall, a busy
 matrix pipe included) and SQ_ACTIVE_INST_ANY, per MI355X_MICROARCH.md's units.

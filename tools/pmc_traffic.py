@@ -60,11 +60,17 @@ PREFIXES = (
     ("sa_x3_lean_kernel<128, 128, 256, 64,", "sa2_group_mlp"),
     ("sa16_kernel<64, 64, 128, 32, true", "sa1_group_mlp"),
     ("sa16_kernel<128, 128, 256, 64, false", "sa2_group_mlp"),
-    ("dense_x3s_kernel<0, true, false>", "sa2_layer1"),  # point rows and centre rows: split by grid
+    ("dense_x3_kernel<0, false>", "dense_rows"),  # SA2's layer 1 (points, centres), dense1, dense2: by grid
+    ("dense_x3_kernel<2, false>", "sa3_dense3_pool"),
+    ("dense_x3_kernel<0, true>", "dense_x1"),  # the bf16 spec's per-point layer 1 (MSG)
+    ("dense_x3s_kernel<0, true, false>", "sa2_layer1"),  # round-3 names (split planes)
     ("dense_x3s_kernel<1, true, false>", "sa3_dense1"),
     ("dense_x3s_kernel<1, false, false>", "sa3_dense2"),
     ("dense_x3s_kernel<2, false, false>", "sa3_dense3_pool"),
     ("dense_x3_pack_kernel", "weight_pack"),
+    ("dense_pack_kernel", "weight_pack"),
+    ("dense_absmax_kernel", "weight_pack"),
+    ("vb_", "voxel_batch"),
     ("concat_xyz_pad_kernel", "concat"),
     ("dense_relu_kernel", "dense_relu_fp32"),
     ("__amd_rocclr_", "runtime_copy"),
@@ -101,6 +107,12 @@ def frames_of(lab, name, grid, wg, F):
     if lab == "sa2_ball_query":
         blocks = (F * M2 + 3) // 4
         return lab, (F if grid == ((blocks + 7) // 8) * 8 * 256 else None)
+    if lab == "dense_rows":
+        for rows, cout, name_ in ((M1, 128, "sa2_layer1_points"), (M2, 128, "sa2_layer1_centres"),
+                                  (M2, 256, "sa3_dense1"), (M2, 512, "sa3_dense2")):
+            if grid == _tiles(rows, cout, F):
+                return name_, F
+        return lab, None
     if lab == "sa2_layer1":
         if grid == _tiles(M1, 128, F):
             return "sa2_layer1_points", F
@@ -126,7 +138,7 @@ def per_label(rs, counter, F):
         v = float(r["Counter_Value"]) * 1024.0  # KiB -> bytes
         name = r["Kernel_Name"]
         lab = label(name)
-        if lab in (None, "torch", "runtime_copy", "weight_pack", "concat"):
+        if lab in (None, "torch", "runtime_copy", "weight_pack", "concat", "voxel_batch", "dense_x1"):
             unmatched[(lab or "unlabelled") + ": " + name[:80]] += 1
             continue
         lab, frames = frames_of(lab, name, int(r["Grid_Size"]), int(r["Workgroup_Size"]), F)
@@ -160,7 +172,8 @@ def calib(rs, counter):
 def bench_frames_per_launch(path):
     with open(path) as f:
         line = [ln for ln in f if ln.startswith("{")][-1]
-    return int(json.loads(line)["pipeline"]["frames_per_launch"])
+    d = json.loads(line)  # the full record (--detail) or the compact last line
+    return int(d["pipeline"]["frames_per_launch"] if "pipeline" in d else d["chains_ms_per_group"]["frames_per_launch"])
 
 
 def main(cf, cw, pf, pw, bench_json, out):

@@ -534,12 +534,20 @@ def voxel_leg(dev, rank, world, B=32, n=65536, voxel=0.05, steps=20, cpu=True):
            "ms_per_launch": per_launch * 1e3, "frames": B, "points_per_frame": n, "voxel": voxel,
            "voxels_per_frame": nv / B, "parity": "bit-exact vs oracle/tier_n.voxel_downsample "
            "(tests/test_gpu_tier_r.py::test_voxel_downsample_batch_vs_oracle)",
-           "roofline": {"kernel": "voxel_downsample_batch (11 launches)", "bound": "hbm",
+           "roofline": {"kernel": "voxel_downsample_batch (9-12 launches: bbox, keys, per radix pass "
+                                  "[histogram] + scatter, runs x2, centroids)", "bound": "hbm",
                         "achieved": algo / per_launch / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": algo / per_launch / 1e9 / HBM_PEAK_GBS, "traffic": None,
                         "work_per_launch": algo, "avg_launch_ms": per_launch * 1e3,
-                        "peak_basis": "HBM peak; algorithmic bytes (the radix sort moves ~5x more)"},
+                        "peak_basis": "HBM peak; algorithmic bytes 16 B per point + 16 B per voxel (the radix "
+                                      "sort moves several times more: traffic)"},
            "cpu_baseline": None}
+    got = latest_profile("pmc_voxel.json")
+    if got and got[0]["config"].get("points_per_frame") == n and got[0]["config"].get("voxel") == voxel:
+        d, src = got
+        t = d["traffic_bytes_per_point"] * B * n
+        rec["roofline"].update({"traffic": t, "traffic_unit": "bytes per launch (PMC FETCH_SIZE*2 + WRITE_SIZE, "
+                                + src + ")", "measured_gbs": t / per_launch / 1e9})
     if cpu and rank == 0:
         from oracle import tier_n
         xs = x[:2].cpu().numpy()

@@ -52,7 +52,7 @@ int lidar_reserve(lidar_handle *h, uint64_t bytes);
 int lidar_trim(lidar_handle *h, uint64_t *freed);
 
 const char *lidar_last_error(void);
-int lidar_version(void);
+int lidar_version(void); /* 3 (what changed per version) */
 
 /* Per-phase timing of a handle's launches (bench.py's in-window kernel durations): with
  * lidar_profile(h, 1) every kernel phase issued on h is bracketed by two HIP events on its

@@ -10,6 +10,7 @@ calls on one handle, so two threads never share one.
 """
 import ctypes
 import os
+import sys
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -172,9 +173,13 @@ class _ThreadHandles(dict):
     storage is released and the handles with it (lidar_destroy frees their workspaces); the main
     thread's live until exit, when the process's teardown reclaims the device memory."""
 
-    def __del__(self):
-        import sys
-        if sys.is_finalizing() or threading.current_thread() is threading.main_thread():
+    # bound at definition: at interpreter exit module globals and imports may already be gone
+    def __del__(self, _finalizing=sys.is_finalizing, _current=threading.current_thread,
+                _main=threading.main_thread):
+        try:
+            if _finalizing() or _current() is _main():
+                return
+        except Exception:  # interpreter teardown
             return
         lib = _lib
         if lib is None:

@@ -22,6 +22,7 @@ constexpr uint32_t kOutside = 0xffffffffu;  // key of a point outside every bin 
 
 struct Axis {
     double start, e1, delta;  // e[0], e[1], e[1] - e[0]
+    double inv;               // 1 / delta (rounded: only the guess of `bin` uses it)
     int64_t nb;               // bins (edges - 1)
 };
 
@@ -36,6 +37,7 @@ __host__ __device__ inline bool make_axis(double lo, double hi, double v, Axis &
     ax.start = start;
     ax.e1 = start + v;
     ax.delta = ax.e1 - start;
+    ax.inv = ax.delta > 0.0 ? 1.0 / ax.delta : 0.0;
     ax.nb = (int64_t)len - 1;
     return true;
 }
@@ -49,13 +51,16 @@ __host__ __device__ inline double edge(const Axis &ax, int64_t i)
 __host__ __device__ inline int64_t bin(const Axis &ax, double p)
 {
     const int64_t L = ax.nb + 1;
-    // c = number of edges <= p (the edges are non-decreasing): guess from the spacing, verify,
-    // else binary search
+    // c = number of edges <= p (the edges are non-decreasing): guess from the spacing (a multiply
+    // by the rounded reciprocal; the guess only has to be within one edge), verify, step one edge
+    // down or up when the verification fails, else binary search
     int64_t c = -1;
     if (ax.delta > 0.0) {
-        const double g = floor((p - ax.start) / ax.delta) + 1.0;
+        const double g = floor((p - ax.start) * ax.inv) + 1.0;
         if (g >= 0.0 && g <= (double)L) {
-            const int64_t t = (int64_t)g;
+            int64_t t = (int64_t)g;
+            if (t > 0 && edge(ax, t - 1) > p) --t;
+            else if (t < L && edge(ax, t) <= p) ++t;
             if ((t == 0 || edge(ax, t - 1) <= p) && (t == L || edge(ax, t) > p)) c = t;
         }
     }

@@ -88,6 +88,11 @@ def plane_conditioning(inliers):
     return rank, float(s[0] / s[rank - 1]), (a, g[:, 2])
 
 
+# per case: rank, kappa and the observed error (max |got - want| / tol over the coefficients, residual gap
+# / its bound); written to gpurun_out/plane_report.json at the end of a run that checked any plane
+PLANE_REPORT = {}
+
+
 def check_plane(name, got, want, inliers):
     """The ground plane vs the reference's ``lstsq(rcond=None)`` plane (data_processing.py:169-183).
 
@@ -103,15 +108,20 @@ def check_plane(name, got, want, inliers):
     want = np.asarray(want, dtype=np.float64)
     rank, kappa, design = plane_conditioning(inliers)
     if rank is None or want[2] != -1.0:
+        PLANE_REPORT[name] = {"rank": rank, "fallback": True, "equal": got.tobytes() == want.tobytes()}
         assert got.tobytes() == want.tobytes(), f"{name}.ground_plane (fallback): {got} != {want}"
         return
     assert got[2] == -1.0, f"{name}.ground_plane[2] = {got[2]}"
     x, y = want[[0, 1, 3]], got[[0, 1, 3]]
     tol = 1e-9 * np.abs(x) + 1024 * PLANE_EPS * kappa * np.linalg.norm(x)
-    assert np.all(np.abs(y - x) <= tol), f"{name}.ground_plane {got} vs {want} (rank {rank}, kappa {kappa:.3g})"
     a, z = design
     rx, ry = np.linalg.norm(a @ x - z), np.linalg.norm(a @ y - z)
-    assert abs(rx - ry) <= 1e-9 * np.linalg.norm(z), f"{name}.ground_plane residual {ry} vs {rx}"
+    rep = {"rank": rank, "kappa": float(kappa), "max_rel": float(np.max(np.abs(y - x) / np.abs(x).clip(1e-300))),
+           "err_over_tol": float(np.max(np.abs(y - x) / tol)),
+           "residual_gap_over_bound": float(abs(rx - ry) / (1e-9 * np.linalg.norm(z)))}
+    PLANE_REPORT[name] = rep
+    assert np.all(np.abs(y - x) <= tol), f"{name}.ground_plane {got} vs {want}: {rep}"
+    assert abs(rx - ry) <= 1e-9 * np.linalg.norm(z), f"{name}.ground_plane residual {ry} vs {rx}: {rep}"
 
 
 def check_tier_r(name, pd, people, analyze):

@@ -25,6 +25,13 @@ def test_library_exports_every_declared_symbol():
     assert len(declared_symbols()) >= 15
 
 
+def test_abi_version_matches_integration_doc():
+    # a host call (no GPU needed); INTEGRATION.md lists what changed in this version
+    v = nat.load_library().lidar_version()
+    assert v == 3
+    assert f"### ABI version {v} (`lidar_version() == {v}`" in open(os.path.join(REPO, "INTEGRATION.md")).read()
+
+
 def test_binding_covers_header():
     assert sorted(nat.SIGNATURES) == declared_symbols()
 

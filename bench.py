@@ -52,7 +52,8 @@ X3_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 3
 FP64_VALU_PEAK_TFLOPS = 78.6
 HBM_PEAK_GBS = 8000.0
 F64_ADD_LATENCY_CYCLES = 6.3  # dependent v_add_f64, operand in a register (tools/micro/f64_chain.hip)
-X3_KERNELS = ("sa1_group_mlp", "sa2_group_mlp", "sa2_layer1_points", "sa3_dense1", "sa3_dense2", "sa3_dense3_pool")
+X3_KERNELS = ("sa1_group_mlp", "sa1_group_mlp_l1", "sa2_group_mlp", "sa2_layer1_points", "sa2_centre_layer1",
+              "sa3_dense1", "sa3_dense2", "sa3_dense3_pool")
 
 
 def mlp_flops(rows, widths_in):
@@ -64,6 +65,11 @@ def ssg_kernel_work(n):
     m1, m2 = n // 16, n // 64
     return {
         "sa1_group_mlp": ("mfma", mlp_flops(m1 * 32, [3, 64, 64, 128])),
+        # the same kernel with SA2's per-point layer 1 (P = [f, x] W1 + b1 over the N/16 centres) as its
+        # epilogue (lidar_sa_group_mlp_bq_l1_f32); Q = c W1_xyz over the N/64 SA2 centres then runs on
+        # the side streams (sa2_centre_layer1)
+        "sa1_group_mlp_l1": ("mfma", mlp_flops(m1 * 32, [3, 64, 64, 128]) + 2 * m1 * 131 * 128),
+        "sa2_centre_layer1": ("mfma", 2 * m2 * 3 * 128),
         # SA2 layer 1 runs per point (N/16 rows of [f, x] W1 + b1, N/64 centre rows of
         # c W1_xyz); the fused kernel computes layers 2-3 of every grouped row
         "sa2_layer1_points": ("mfma", 2 * m1 * 131 * 128 + 2 * m2 * 3 * 128),
@@ -789,16 +795,19 @@ def main():
         precomputed indices: the difference is what answering the queries costs inside it."""
         if not totals or "sa1_group_mlp_given_idx" not in totals:
             return None
-        f_l, f_f, f_ms = totals["sa1_group_mlp"]
+        fk = "sa1_group_mlp_l1" if "sa1_group_mlp_l1" in totals else "sa1_group_mlp"
+        f_l, f_f, f_ms = totals[fk]
         m_l, m_f, m_ms = totals["sa1_group_mlp_given_idx"]
         q_l, q_f, q_ms = totals["sa1_ball_query_separate"]
         per_frame = work["sa1_group_mlp"][1]
         return {"fused_ms_per_launch": f_ms / f_l, "mlp_given_idx_ms_per_launch": m_ms / m_l,
                 "query_ms_inside_fused": f_ms / f_l - m_ms / m_l, "separate_query_ms_per_launch": q_ms / q_l,
                 "frames_per_launch": f_f / f_l, "mlp_only_frac": per_frame * m_f / (m_ms / 1e3) / 1e12 / X3_PEAK_TFLOPS,
-                "fused_frac": per_frame * f_f / (f_ms / 1e3) / 1e12 / X3_PEAK_TFLOPS,
+                "fused_frac": work[fk][1] * f_f / (f_ms / 1e3) / 1e12 / X3_PEAK_TFLOPS, "fused_kernel": fk,
                 "basis": "one forward() over a group's frames, nothing else on the chip; the MLP on given indices "
-                         "is lidar_sa_group_mlp_x3 over the (B, M, 32) index tensor of the separate grid query"}
+                         "is lidar_sa_group_mlp_x3 over the (B, M, 32) index tensor of the separate grid query"
+                         + ("; the fused kernel also computes SA2's per-point layer 1 (its epilogue), priced in "
+                            "fused_frac" if fk == "sa1_group_mlp_l1" else "")}
 
     def roof(name, totals):
         """Roofline of one kernel over the launches `totals` recorded: achieved = the algorithmic
@@ -815,7 +824,7 @@ def main():
         else:
             a, p, u = w_total / s / 1e9, HBM_PEAK_GBS, "GB/s"
             basis = "HBM peak over compulsory bytes"
-        if name == "sa1_group_mlp" and args.bq in ("bin", "main"):
+        if name in ("sa1_group_mlp", "sa1_group_mlp_l1") and args.bq in ("bin", "main"):
             basis += "; the kernel also answers SA1's ball queries (lidar_sa_group_mlp_bq_f32), whose time is " \
                      "included and whose work is not priced"
         r = {"kernel": name, "bound": bound, "achieved": a, "peak": p, "unit": u, "frac": a / p,
@@ -839,7 +848,7 @@ def main():
     # main chain's device time; the chain lengths say which chain bounds a step.
     side = ("sa1_fps", "sa1_ball_query", "sa1_bq_bin") if args.bq == "side" else ("sa1_fps", "sa1_bq_bin")
     if args.l2_side:
-        side = side + ("sa2_fps", "sa2_ball_query")
+        side = side + ("sa2_fps", "sa2_ball_query", "sa2_centre_layer1")
     per_launch = {k: t / c for k, (c, f, t) in tot.items()}
     main_k = {k: v for k, v in per_launch.items() if k not in side}
     side_ms = sum(per_launch.get(k, 0) for k in side) / args.depth
@@ -865,11 +874,11 @@ def main():
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "f32",
-            "arithmetic": ("fp32 inputs/weights/outputs; SA layers 2-3, SA2's per-point layer 1 and group_all: each "
-                           "fp32 operand split exactly into bf16 hi+lo, products ah*bh + ah*bl + al*bh accumulated in "
-                           "fp32 (<= ~2^-15 per product); SA1 layer 1 (K = 3) on fp32 MFMA; features within the 1e-4 "
-                           "rel contract of the fp32 oracle (tests/test_gpu_tier_n.py::test_group_mlp_x3, "
-                           "test_dense_x3s, test_backbone_vs_oracle, test_bench_shape_executor_vs_oracle)")
+            "arithmetic": ("fp32 inputs/weights/outputs; SA layers 2-3, SA2's per-point layer 1 and group_all in h3 "
+                           "arithmetic: each fp32 operand scaled by a power of two and split exactly into fp16 hi+lo, "
+                           "products ah*bh + ah*bl + al*bh accumulated in fp32 (<= 3*2^-22 per product, csrc/h3.hpp); "
+                           "layer-1 xyz terms on fp32 MFMA; features within 1e-4 pure relative of the fp32 oracle on "
+                           "every element >= 1e-2 RMS (tests/test_gpu_tier_n.py; `precision` below)")
                           if args.x3 else "fp32 MFMA (v_mfma_f32_*_f32)",
             "precision": None,
             "data": "synthetic: uniform [-1,1]^3 float32 frames (seeded per rank, %d distinct batches cycled), "

@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""Price a main-chain operator of the SSG pipeline by skipping it (diagnostic; wrong results by
+design, so run with --no-verify): the operator runs once per distinct shape and its cached output
+is returned afterwards, so the pipeline keeps every other launch and the skipped one's upper-bound
+gain shows in the line.
+
+  python tools/skip_probe.py {none|l1|dense1|l1+dense1} [bench.py args ...]
+
+  l1      SA2's per-point layer 1 (layer1_per_point: 2 xyz-pad copies + the P and Q GEMMs)
+  dense1  group_all's first dense layer
+"""
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+import bench  # noqa: E402
+from lidar_ai_recommendation_software_amd import pointnet2 as pn  # noqa: E402
+
+
+def memo(fn):
+    cache = {}
+
+    def wrapped(*a, **k):
+        key = tuple(tuple(x.shape) if hasattr(x, "shape") else repr(x) for x in a[:2])
+        if key not in cache:
+            cache[key] = fn(*a, **k)
+        return cache[key]
+    return wrapped
+
+
+def main():
+    what = sys.argv[1]
+    skip = set(what.split("+")) - {"none"}
+    if "l1" in skip:
+        pn.layer1_per_point = memo(pn.layer1_per_point)
+    if "dense1" in skip:
+        real = pn.dense_x3s
+        cache = {}
+
+        def dense_x3s(a, wpack, b, cout, *r, **k):
+            # group_all's first layer is the only dense_x3s call whose input is the padded SA2 rows
+            # (k = 272); the per-point layer 1 reads k = 144 / 16 and dense2 / dense3 read 256 / 512
+            if a.shape[1] == 272 and not k.get("pool_rows"):
+                key = tuple(a.shape)
+                if key not in cache:
+                    cache[key] = real(a, wpack, b, cout, *r, **k)
+                return cache[key]
+            return real(a, wpack, b, cout, *r, **k)
+        pn.dense_x3s = dense_x3s
+    sys.argv = [sys.argv[0]] + sys.argv[2:]
+    bench.main()
+
+
+if __name__ == "__main__":
+    main()

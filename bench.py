@@ -632,6 +632,8 @@ def main():
                     help="1: SA2's nested FPS and ball queries on the side streams as well (StreamingSSG l2_side; "
                          "1 213-1 227 vs 1 195-1 207 M pts/s in one A/B); 0: on the main stream")
     ap.add_argument("--rotate", type=int, default=8, help="distinct device-resident input batches the feed cycles over")
+    ap.add_argument("--pe", type=int, default=0,
+                    help="1: SA1's kernel computes SA2's per-point layer 1 as its epilogue (A/B; DESIGN.md 4.2)")
     ap.add_argument("--no-fp32-mfma-leg", action="store_true",
                     help="skip the extra measurement of the native fp32-MFMA kernels (when --x3 is on)")
     ap.add_argument("--no-standalone", action="store_true",
@@ -679,7 +681,7 @@ def main():
         come from the same window); False: the window runs clean and the per-kernel durations come
         from a second window of the same length (with ~25 launches per step, as MSG has, the
         events cost ~1/3)."""
-        bb = pn.PointNet2Backbone(cfg, device=dev, seed=0, dtype=dtype, x3=x3)
+        bb = pn.PointNet2Backbone(cfg, device=dev, seed=0, dtype=dtype, x3=x3, point_layer_epilogue=bool(args.pe))
         nb = max(1, args.rotate)
         xs = [torch.from_numpy(unit_frames(B, N, seed=sharding.frame_seed(seed_rank, step=i))).to(dev) for i in range(nb)]
         # one-batch forward(): what every pipeline output must equal (--no-verify: not issued, so a

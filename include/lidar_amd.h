@@ -151,6 +151,20 @@ int lidar_dense_x3f_f32(lidar_handle *h, const float *a, int32_t lda, int64_t ro
                         const float *bias, int32_t cout, int32_t mode, int32_t relu_on, int32_t pool_rows, void *out,
                         int64_t o_plane, int64_t ldo, void *stream);
 
+/* group_all's h3 chain (csrc/dense_x3s.hip): the same GEMM with the activations split ONCE, by the
+ * producing layer.  A: fp32 rows (a_exp NULL; k % 4 == 0, lda % 4 == 0, elements k..lda-1 read and
+ * finite) or h3 planes (a_exp (rows,) int32: |x| < 2^e per row; the fp16 hi plane (rows, lda) at a, the
+ * lo plane at a + rows*lda halves, hi + lo = x 2^(14 - e) up to 2^-22; lda = k rounded up to 32, zeros
+ * past k) — what mode 1 writes.  mode 0: fp32 rows (rows, ldo) [+ ReLU]; 1: h3 planes of y [+ ReLU]
+ * (hi at out, lo at out + rows*ldo halves, ldo == cout) and out_exp (rows,): an exponent bound shared
+ * by every column tile, 2^e_in w_colsum + b_max (w_colsum >= max_c sum_k |W_kc|, b_max >= max |b|,
+ * the caller's, rounded up); 2: ReLU and max over runs of pool_rows rows (fp32, out zeroed by the
+ * caller).  rows % 128 == 0, cout % 128 == 0; packed: lidar_dense_x3_pack_f32's image. */
+int lidar_dense_h3p_f32(lidar_handle *h, const void *a, int32_t lda, int64_t rows, int32_t k, const int32_t *a_exp,
+                        const void *packed, const float *bias, int32_t cout, int32_t mode, int32_t relu_on,
+                        int32_t pool_rows, void *out, int32_t *out_exp, int64_t ldo, float w_colsum, float b_max,
+                        void *stream);
+
 /* SA branch in the bf16 spec (BASELINE configs[4]) on the fused 16-row kernel of
  * lidar_sa_group_mlp_x3_f32 with one bf16 product per MFMA: layer inputs and weights rounded to
  * bf16 (RNE), fp32 accumulation, bias / ReLU / max-pool in fp32.  layer1_mode 0 (xyz level):

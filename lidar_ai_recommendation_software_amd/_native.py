@@ -61,6 +61,7 @@ SIGNATURES = {
     "lidar_dense_x3_pack_f32": [P, P, I32, I32, P, P],
     "lidar_dense_x1_pack_f32": [P, P, I32, I32, P, P],
     "lidar_dense_x3f_f32": [P, P, I32, I64, I32, P, P, I32, I32, I32, I32, P, I64, I64, P],
+    "lidar_dense_h3p_f32": [P, P, I32, I64, I32, P, P, P, I32, I32, I32, I32, P, P, I64, F32, F32, P],
     "lidar_mlp_packed_size_x1": [I32, I32, I32],
     "lidar_fps_workspace_bytes": [I64, I64],
     "lidar_mlp_pack_x1_f32": [I32, I32, I32, P, P, P, P, P, P, P],

@@ -17,11 +17,20 @@
 // 32 double-buffered in LDS by global_load_lds:
 //   A stage: 128 rows x 32 fp32; row r's 16-byte chunk q at slot q ^ ((r >> 1) & 7);
 //   B stage: x3_pack.hip's packed weight fragments, read lane-linear.
-// Both output modes compute D = W^T X^T (a lane holds one row: its row's scale is its own):
+// Every output mode computes D = W^T X^T (a lane holds one row: its row's scale is its own):
 //   0 fp32 rows (rows, ldo) [+ ReLU]             — a lane stores 4 consecutive channels of its row
+//   1 h3 planes (rows, ldo) x 2 [+ ReLU]         — the next layer's A operand already scaled and split
+//                                                   (fp16 hi plane, then lo plane), with the row's
+//                                                   exponent e (|y| < 2^e) in out_exp[row]
 //   2 fp32 max-pool over runs of pool_rows rows  — the max over the 32 rows of a tile by lane
 //     (rows / pool_rows, ldo), ReLU, out zeroed     swaps, then an atomic max on the bits (exact,
 //     by the caller                                 order-free) across waves and workgroups
+// PL (A as h3 planes, lidar_dense_h3p_f32): the producing layer (mode 1) split every element once,
+// scaled by its row's exponent, so the GEMM loop does no max pass, no rescale and no split (an
+// fp32 row is re-split by every column tile's workgroup: 8 times for group_all's third layer).  A
+// row's exponent must hold in every column tile of the producer, so it is a bound, not the row's
+// maximum: |y_c| <= sum_k |x_k| |W_kc| + |b_c| < 2^e_in colsum(W) + max|b| (the lean SA2 kernel's
+// layer-3 rule, sa_mlp_x3.hip), from the input row's own exponent (PL) or its running one (fp32 A).
 #include "h3.hpp"
 
 namespace {
@@ -85,15 +94,33 @@ __device__ __forceinline__ bf16x8 round8_bf(const f32x4 &a0, const f32x4 &a1)
     return hi;
 }
 
-// MODE 0 / 2 as in the header; X1: the bf16 spec (one ah*bh product, no scaling)
-template <int MODE, bool X1>
+// r's 16-byte chunk q of a planes stage (CPR per row and plane) sits at slot q ^ swzp(r): a fragment
+// read (32 consecutive rows, one chunk) spreads over the banks
+__device__ __forceinline__ int swzp(int r) { return CPR == 4 ? (r >> 2) & 3 : (r >> 3) & 1; }
+
+// the h3 output exponent of a row whose inputs are below 2^e_in: |y| < 2^e_in colsum + bmax,
+// widened by 2^-10 for the roundings of y and of the bound (sa_mlp_x3.hip's bound_exp3)
+__device__ __forceinline__ int out_bound_exp(float colsum, float bmax, int e_in)
+{
+    const float b = (colsum * ldexpf(1.0f, e_in) + bmax) * (1.0f + 0x1p-10f);
+    return lidar_h3::exp_of_bits(__float_as_uint(b));
+}
+
+// MODE 0 / 1 / 2 as in the header; X1: the bf16 spec (one ah*bh product, no scaling); PL: A as h3
+// planes (hi at a, lo at a + a_plane halves, row exponents a_exp)
+template <int MODE, bool X1, bool PL = false>
 __global__ __launch_bounds__(256, 4) void dense_x3_kernel(const float *__restrict__ af, int lda,
                                                           const uint16_t *__restrict__ wp, int ks,
                                                           const int32_t *__restrict__ wexp,
                                                           const float *__restrict__ bias, int relu_on,
                                                           int pool_rows, float *__restrict__ out, int64_t ldo,
-                                                          int cout, int ntn, int64_t total, int64_t per_xcd, int kdim)
+                                                          int cout, int ntn, int64_t total, int64_t per_xcd, int kdim,
+                                                          const int32_t *__restrict__ a_exp = nullptr,
+                                                          int64_t a_plane = 0, int32_t *__restrict__ out_exp = nullptr,
+                                                          float w_colsum = 0.0f, float b_max = 0.0f)
 {
+    static_assert(!PL || !X1, "h3 planes carry the fp32 contract only");
+    static_assert(MODE != 1 || !X1, "mode 1 writes h3 planes");
     // the two stage buffers are separate LDS variables (distinct alias scopes) and the stage loop is
     // unrolled by two, so a stage's reads need not wait for the next stage streaming into the other
     // buffer (with one array indexed by st & 1 the compiler waited for the stage it had just issued)
@@ -114,6 +141,20 @@ __global__ __launch_bounds__(256, 4) void dense_x3_kernel(const float *__restric
 
     auto load_stage = [&](int st, int buf) {
         const int k0 = st * SBK;
+        if constexpr (PL) {
+            // wave w: plane w >> 1 (hi, lo), rows 64 (w & 1) .. + 63, CPR instructions of 64 / CPR rows;
+            // lane i fills slot i % CPR of its row with chunk slot ^ swzp(row); planes are zero past k
+            constexpr int RPI = 64 / CPR;
+            const int pl = wave >> 1, rbase = 64 * (wave & 1);
+            const uint16_t *ap = reinterpret_cast<const uint16_t *>(af) + pl * a_plane;
+            uint16_t *dst = reinterpret_cast<uint16_t *>(Asb(buf)) + pl * (SBM * SBK);
+#pragma unroll
+            for (int t = 0; t < CPR; ++t) {
+                const int r = rbase + RPI * t + lane / CPR;
+                const int q = (lane % CPR) ^ swzp(r);
+                lds_dma16(ap + (row0 + r) * lda + k0 + 8 * q, dst + (rbase + RPI * t) * SBK);
+            }
+        } else {
         // wave w: rows 32 w .. 32 w + 31 of 2 CPR 16-byte chunks, CPR instructions
         constexpr int CF = 2 * CPR, RPI = 64 / CF;
         float *dst = Asb(buf);
@@ -126,6 +167,7 @@ __global__ __launch_bounds__(256, 4) void dense_x3_kernel(const float *__restric
             const int kc = k0 + 4 * kq < kdim ? k0 + 4 * kq : k0;
             lds_dma16(af + (row0 + r) * lda + kc, dst + (32 * wave + RPI * i) * SBK);
         }
+        }
         // B: wave w loads column tile 4 tn + w, k-steps NSS st .. NSS st + NSS - 1, hi / lo (contiguous)
         const uint16_t *src = wp + (((int64_t)(4 * tn + wave) * ks + NSS * st) * 2) * 512;
 #pragma unroll
@@ -137,6 +179,7 @@ __global__ __launch_bounds__(256, 4) void dense_x3_kernel(const float *__restric
     // h3: the running scaling exponent of the lane's row (its values so far are below 2^(E - 3):
     // three bits of headroom, so a later stage rarely needs a rescale); kEmin - 1 = unset
     int E = lidar_h3::kEmin - 1;
+    if constexpr (PL) E = a_exp[row0 + 32 * wave + col];  // the row's exponent, fixed
     // the lane's row r = 32 wave + col, k = 8 h .. 8 h + 7 of k-step ss: A fragment of the MFMA
     auto frag = [&](const float *as, int ss, f32x4 &a0, f32x4 &a1) {
         const int r = 32 * wave + col;
@@ -146,6 +189,25 @@ __global__ __launch_bounds__(256, 4) void dense_x3_kernel(const float *__restric
         a1 = *reinterpret_cast<const f32x4 *>(as + r * SBK + 4 * (sl ^ 1));
     };
     auto compute = [&](int buf) {
+        if constexpr (PL) {
+            const uint16_t *ah = reinterpret_cast<const uint16_t *>(Asb(buf));
+            const int r = 32 * wave + col;
+#pragma unroll
+            for (int ss = 0; ss < NSS; ++ss) {
+                const int slot = (2 * ss + h) ^ swzp(r);
+                const f16x8 xh = *reinterpret_cast<const f16x8 *>(ah + (r * CPR + slot) * 8);
+                const f16x8 xl = *reinterpret_cast<const f16x8 *>(ah + SBM * SBK + (r * CPR + slot) * 8);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const f16x8 wh = *reinterpret_cast<const f16x8 *>(&Bsb(buf)[((j * NSS + ss) * 2 + 0) * 512 + lane * 8]);
+                    const f16x8 wl = *reinterpret_cast<const f16x8 *>(&Bsb(buf)[((j * NSS + ss) * 2 + 1) * 512 + lane * 8]);
+                    acc[j] = mfma_h(wh, xh, acc[j]);
+                    acc[j] = mfma_h(wl, xh, acc[j]);
+                    acc[j] = mfma_h(wh, xl, acc[j]);
+                }
+            }
+            return;
+        }
         const float *as = Asb(buf);
         float S = 1.0f;
         if constexpr (!X1) {
@@ -220,7 +282,34 @@ __global__ __launch_bounds__(256, 4) void dense_x3_kernel(const float *__restric
             for (int r = 0; r < 16; ++r) acc[j][r] = ldexpf(acc[j][r], us);
     }
     const int cbase = tn * SBN;
-    if constexpr (MODE == 0) {
+    if constexpr (MODE == 1) {
+        // h3 planes of y = relu?(acc + b): every column tile's workgroup takes the same exponent for a
+        // row (a bound from the row's input exponent E), so the next layer reads one scale per row
+        const int64_t row = row0 + 32 * wave + col;
+        // |x| < 2^E for planes; the running exponent of fp32 rows keeps three bits of headroom
+        const int eo = out_bound_exp(w_colsum, b_max, PL ? E : E - 3);
+        const float so = lidar_h3::scale_of(eo);
+        uint16_t *oh = reinterpret_cast<uint16_t *>(out);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int c = cbase + 32 * j + 8 * g + 4 * h;
+                const f32x4 b4 = *reinterpret_cast<const f32x4 *>(bias + c);
+                float v[4];
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const float y = acc[j][4 * g + t] + b4[t];
+                    v[t] = (relu_on ? relu_i(y) : y) * so;
+                }
+                uint32_t hi[2], lo[2];
+                lidar_h3::split2(v[0], v[1], hi[0], lo[0]);
+                lidar_h3::split2(v[2], v[3], hi[1], lo[1]);
+                *reinterpret_cast<uint2 *>(oh + row * ldo + c) = make_uint2(hi[0], hi[1]);
+                *reinterpret_cast<uint2 *>(oh + row * ldo + c + (int64_t)total / ntn * SBM * ldo) = make_uint2(lo[0], lo[1]);
+            }
+        if (h == 0 && tn == 0) out_exp[row] = eo;
+    } else if constexpr (MODE == 0) {
         const int64_t row = row0 + 32 * wave + col;
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -298,12 +387,69 @@ LIDAR_EXPORT int lidar_dense_x3f_f32(lidar_handle *h, const float *a, int32_t ld
     const dim3 grid((unsigned)(per_xcd * 8)), block(256);
     auto go = [&](auto kern, int relu, int pool) {
         hipLaunchKernelGGL(kern, grid, block, 0, s, a, (int)lda, w, ks, wexp, bias, relu, pool,
-                           static_cast<float *>(out), ldo, (int)cout, ntn, total, per_xcd, (int)k);
+                           static_cast<float *>(out), ldo, (int)cout, ntn, total, per_xcd, (int)k,
+                           (const int32_t *)nullptr, (int64_t)0, (int32_t *)nullptr, 0.0f, 0.0f);
     };
     const int rl = relu_on ? 1 : 0;
     if (x1) go(dense_x3_kernel<0, true>, rl, 0);
     else if (mode == 0) go(dense_x3_kernel<0, false>, rl, 0);
     else go(dense_x3_kernel<2, false>, 1, (int)pool_rows);
+    LAUNCH_CHECK();
+    return LIDAR_OK;
+}
+
+// The h3 chain of group_all: A as fp32 rows (a_exp NULL; lda % 4 == 0, elements k..lda-1 read and
+// finite) or as h3 planes (a_exp (rows,) int32 the rows' exponents, |x| < 2^e: hi plane (rows, lda)
+// fp16 at a, lo plane at a + rows * lda halves; lda = k rounded up to 32, zeros past k — what mode 1
+// writes).  mode 0: fp32 rows (rows, ldo) [+ ReLU]; 1: h3 planes of y [+ ReLU] (hi at out, lo at
+// out + rows * ldo halves, ldo % 8 == 0) and out_exp (rows,) — their exponent, from the bound
+// 2^e_in w_colsum + b_max (w_colsum >= max over columns of sum_k |W_kc|, b_max >= max |b|: the
+// caller's, rounded up); 2: ReLU + max over runs of pool_rows rows (out zeroed by the caller).
+LIDAR_EXPORT int lidar_dense_h3p_f32(lidar_handle *h, const void *a, int32_t lda, int64_t rows, int32_t k,
+                                     const int32_t *a_exp, const void *packed, const float *bias, int32_t cout,
+                                     int32_t mode, int32_t relu_on, int32_t pool_rows, void *out, int32_t *out_exp,
+                                     int64_t ldo, float w_colsum, float b_max, void *stream)
+{
+    const bool pl = a_exp != nullptr;
+    REQUIRE(h && a && packed && bias && out, "lidar_dense_h3p_f32: null pointer");
+    REQUIRE(rows % SBM == 0 && k > 0 && k <= lda && cout % SBN == 0 && cout > 0,
+            "lidar_dense_h3p_f32: rows % 128, k <= lda, cout % 128 must hold");
+    REQUIRE(pl ? lda == (k + 31) / 32 * 32 : (k % 4 == 0 && lda % 4 == 0),
+            "lidar_dense_h3p_f32: planes need lda = k rounded up to 32; fp32 rows k % 4 == 0 and lda % 4 == 0");
+    REQUIRE(mode >= 0 && mode <= 2, "lidar_dense_h3p_f32: mode must be 0, 1 or 2");
+    REQUIRE(mode != 1 || (out_exp != nullptr && ldo == cout && w_colsum >= 0.0f && b_max >= 0.0f),
+            "lidar_dense_h3p_f32: mode 1 needs out_exp, ldo == cout and the bounds w_colsum, b_max >= 0");
+    REQUIRE(ldo >= cout && ldo % 4 == 0, "lidar_dense_h3p_f32: ldo must be >= cout and a multiple of 4");
+    REQUIRE(mode != 2 || (relu_on && pool_rows > 0 && pool_rows % SBM == 0 && rows % pool_rows == 0),
+            "lidar_dense_h3p_f32: the max-pool needs relu and pool_rows a multiple of 128 dividing rows");
+    if (rows == 0) return LIDAR_OK;
+    ON_DEVICE(h->device);
+    const int ks = (k + 31) / 32 * 2;
+    const int ntn = cout / SBN;
+    const int64_t total = (rows / SBM) * ntn, per_xcd = (total + 7) / 8;
+    REQUIRE(per_xcd * 8 <= 0x7fffffff, "lidar_dense_h3p_f32: too many rows");
+    int64_t wbytes = 0;
+    if (lidar_dense_x3_packed_image(k, cout, &wbytes) != LIDAR_OK) return LIDAR_EINVAL;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const uint16_t *w = static_cast<const uint16_t *>(packed);
+    const int32_t *wexp = reinterpret_cast<const int32_t *>(static_cast<const char *>(packed) + wbytes);
+    const dim3 grid((unsigned)(per_xcd * 8)), block(256);
+    const float *af = static_cast<const float *>(a);
+    float *o = static_cast<float *>(out);
+    const int rl = relu_on ? 1 : 0;
+    auto go = [&](auto kern, int relu, int pool) {
+        hipLaunchKernelGGL(kern, grid, block, 0, s, af, (int)lda, w, ks, wexp, bias, relu, pool, o, ldo, (int)cout, ntn,
+                           total, per_xcd, (int)k, a_exp, rows * lda, out_exp, w_colsum, b_max);
+    };
+    if (pl) {
+        if (mode == 0) go(dense_x3_kernel<0, false, true>, rl, 0);
+        else if (mode == 1) go(dense_x3_kernel<1, false, true>, rl, 0);
+        else go(dense_x3_kernel<2, false, true>, 1, (int)pool_rows);
+    } else {
+        if (mode == 0) go(dense_x3_kernel<0, false>, rl, 0);
+        else if (mode == 1) go(dense_x3_kernel<1, false>, rl, 0);
+        else go(dense_x3_kernel<2, false>, 1, (int)pool_rows);
+    }
     LAUNCH_CHECK();
     return LIDAR_OK;
 }

@@ -466,6 +466,44 @@ def dense_x3s(a, wpack, b, cout, relu=True, pool_rows=0, out=None, x1=False, slo
     return out
 
 
+def h3_bounds(w, b):
+    """(w_colsum, b_max) of a dense layer for lidar_dense_h3p_f32's mode-1 exponent bound: the largest
+    column sum of |W| and the largest |b|, each rounded up to the next float32."""
+    cs = np.abs(np.asarray(w, np.float64)).sum(axis=0).max() if np.size(w) else 0.0
+    bm = np.abs(np.asarray(b, np.float64)).max() if np.size(b) else 0.0
+    up = lambda v: float(np.nextafter(np.float32(v), np.float32(np.inf)))
+    return up(cs), up(bm)
+
+
+def dense_h3p(a, a_exp, wpack, b, cout, mode, bounds=(0.0, 0.0), relu=True, pool_rows=0, out=None):
+    """One layer of group_all's h3 chain (lidar_dense_h3p_f32).  A: fp32 rows (rows, k) with a_exp None,
+    or h3 planes (2, rows, k) float16 (hi, lo) with a_exp (rows,) int32 — mode 1's output.  mode 0 ->
+    fp32 rows (rows, cout); 1 -> (planes (2, rows, cout) float16, exponents (rows,) int32), the next
+    layer's A; 2 -> ReLU + max over runs of pool_rows rows (rows / pool_rows, cout) fp32.  bounds: the
+    layer's h3_bounds(W, b) (mode 1)."""
+    dev = a.device
+    if a_exp is None:
+        rows, k = a.shape
+        lda = k
+    else:
+        _, rows, k = a.shape
+        lda = k
+    if mode == 2:
+        out = torch.zeros((rows // pool_rows, cout), dtype=torch.float32, device=dev) if out is None else out
+        oexp = None
+    elif mode == 1:
+        out = torch.empty((2, rows, cout), dtype=torch.float16, device=dev) if out is None else out
+        oexp = torch.empty(rows, dtype=torch.int32, device=dev)
+    else:
+        out = torch.empty((rows, cout), dtype=torch.float32, device=dev) if out is None else out
+        oexp = None
+    _dev_check(a, a_exp, wpack, b, out, oexp)
+    nat.call("lidar_dense_h3p_f32", nat.handle(dev.index), nat.ptr(a), lda, rows, k, nat.ptr(a_exp), nat.ptr(wpack),
+             nat.ptr(b), cout, mode, 1 if relu else 0, pool_rows, nat.ptr(out), nat.ptr(oexp), cout, float(bounds[0]),
+             float(bounds[1]), nat.stream_ptr())
+    return (out, oexp) if mode == 1 else out
+
+
 # ----------------------------------------------------------------------- backbone
 class _Timers:
     """Optional per-launch HIP-event timing on the launching stream (bench.py): per kernel name
@@ -501,7 +539,7 @@ class PointNet2Backbone:
     (B, C_last) plus, with keep_levels, per level (new_xyz, features, fps_idx, [ball-query
     idx per branch])."""
 
-    def __init__(self, cfg=SSG, weights=None, device="cuda", seed=0, dtype="f32", x3=True):
+    def __init__(self, cfg=SSG, weights=None, device="cuda", seed=0, dtype="f32", x3=True, point_layer_epilogue=False):
         """dtype "f32" (the fp32 contract: features within 1e-4 of the fp32 oracle): x3=True (default)
         runs the MLPs on the fp16 matrix cores in h3 arithmetic (lidar_sa_group_mlp_x3_f32,
         lidar_dense_x3f_f32), x3=False on the native fp32 matrix cores (lidar_sa_group_mlp16_f32,
@@ -510,7 +548,9 @@ class PointNet2Backbone:
         (inputs, activations and weights rounded to bf16, fp32 accumulation); group_all stays in
         fp32 arithmetic on the x3 GEMM.
         Levels with point features run layer 1 per point (layer1_per_point / layer1_points_x1) and
-        the fused kernel from layer 2 on."""
+        the fused kernel from layer 2 on.  point_layer_epilogue (SSG, x3): SA1's kernel computes SA2's
+        per-point layer 1 as its epilogue (lidar_sa_group_mlp_bq_l1_f32) instead of the separate GEMM —
+        measured slower in the pipeline, so off by default."""
         if dtype not in ("f32", "bf16"):
             raise ValueError("dtype must be 'f32' or 'bf16'")
         self.bf16 = dtype == "bf16"
@@ -533,6 +573,7 @@ class PointNet2Backbone:
                          "b": [t(b1), t(b2), t(b3)]}
                 if self.x3:  # packed once into x3 B fragments
                     entry["w_x3"] = [pack_dense_x3(w) for w in entry["w"]]
+                    entry["h3_bounds"] = [h3_bounds(w1p, b1), h3_bounds(w2, b2), h3_bounds(w3, b3)]
                 self.levels.append(entry)
                 cfeat = w3.shape[1]
                 continue
@@ -564,7 +605,7 @@ class PointNet2Backbone:
                         if x3:
                             br["pre"]["w1_x3"] = pack_dense_x3(br["pre"]["w1"])
                             br["pre"]["wq_x3"] = pack_dense_x3(br["pre"]["wq"])
-                            if cfeat == 128 and widths[0] == 128 and has_point_layer_epilogue():
+                            if point_layer_epilogue and cfeat == 128 and widths[0] == 128:
                                 # the previous (SSG SA1) level's kernel computes P itself (forward)
                                 br["pre"]["point_l1"] = pack_point_layer_x3(layers[0], cfeat, self.device)
                 branches.append(br)
@@ -727,11 +768,11 @@ class PointNet2Backbone:
             M, rows = mp, B * mp
         t = self.timers
         ws, bs = lvl["w"], lvl["b"]
-        if self.x3:  # fp32 rows between the layers; dense3 fuses the max-pool
-            wp = lvl["w_x3"]
-            h1 = _call(t, "sa3_dense1", B, dense_x3s, x2, wp[0], bs[0], ws[0].shape[1])
-            h2 = _call(t, "sa3_dense2", B, dense_x3s, h1, wp[1], bs[1], ws[1].shape[1])
-            return _call(t, "sa3_dense3_pool", B, dense_x3s, h2, wp[2], bs[2], ws[2].shape[1], pool_rows=M)
+        if self.x3:  # h3 planes between the layers (split once, by the producer); dense3 fuses the max-pool
+            wp, bd = lvl["w_x3"], lvl["h3_bounds"]
+            h1, e1 = _call(t, "sa3_dense1", B, dense_h3p, x2, None, wp[0], bs[0], ws[0].shape[1], 1, bd[0])
+            h2, e2 = _call(t, "sa3_dense2", B, dense_h3p, h1, e1, wp[1], bs[1], ws[1].shape[1], 1, bd[1])
+            return _call(t, "sa3_dense3_pool", B, dense_h3p, h2, e2, wp[2], bs[2], ws[2].shape[1], 2, pool_rows=M)
         h1 = _call(t, "sa3_dense1", B, dense_relu, x2, ws[0], bs[0])
         h2 = _call(t, "sa3_dense2", B, dense_relu, h1, ws[1], bs[1])
         out = torch.zeros((rows // M, ws[2].shape[1]), dtype=torch.float32, device=x.device)

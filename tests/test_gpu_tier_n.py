@@ -338,6 +338,8 @@ def test_group_mlp_bq_l1_matches_unfused(cuda, frame, M):
     and every element of P = f W1f + c W1x + b1 lies within its rigorous bound against the exact
     (float64) product over the kernel's own features: h3's product terms on f W1f, the fp32 MFMA's
     roundings on the xyz / bias term, one rounding of the sum.  M = 301: a partial last workgroup."""
+    if not pn.has_point_layer_epilogue():  # an earlier round's library loaded for an A/B (LIDAR_AMD_LIB)
+        pytest.skip("library without lidar_sa_group_mlp_bq_l1_f32")
     B, N = 2, 6000
     x = unit_frames(B, N, 43) if frame == "uniform" else np.stack([_bq_edge_frames()[frame]] * B)
     x = np.ascontiguousarray(x)
@@ -382,6 +384,58 @@ def test_group_mlp_bq_l1_matches_unfused(cuda, frame, M):
     P2 = torch.full_like(P, -9.0)
     pn.group_mlp_bq_l1(xt, ct, grid, r, ns, packed, widths, pimg, P2)
     assert torch.equal(P2, P)
+
+
+def _h3_decode(planes, e):
+    """h3 planes (2, rows, k) float16 + row exponents -> the values the next GEMM multiplies (float64)."""
+    p = planes.cpu().numpy().astype(np.float64)
+    return (p[0] + p[1]) * np.exp2(e.cpu().numpy().astype(np.float64) - 14)[:, None]
+
+
+@pytest.mark.parametrize("rows,dims,pool", [(512, (272, 256, 512, 1024), 512), (256, (144, 128, 384, 256), 128)])
+def test_dense_h3p_chain(cuda, rows, dims, pool):
+    """group_all's h3 chain (lidar_dense_h3p_f32): fp32 rows -> planes -> planes -> max-pool.  Every layer
+    is checked against the exact (float64) layer over the values the kernel actually read (the
+    previous layer's planes, decoded): the weights' split and the dropped products (H3_PRODUCT), the
+    fp32 accumulation, and the output's own split (2^-22 relative, 2^(e - 38) absolute); rows of
+    magnitudes 2^-30..2^30 and a zero row; plane exponents bound every row's values."""
+    rng = np.random.default_rng(rows + dims[0])
+    k0 = dims[0]
+    x = rng.standard_normal((rows, k0)).astype(np.float32) * np.exp2(rng.integers(-30, 30, (rows, 1))).astype(np.float32)
+    x[7] = 0.0
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(cuda)
+    ws = [(rng.standard_normal((a, b)) / np.sqrt(a)).astype(np.float32) for a, b in zip(dims[:-1], dims[1:])]
+    bs = [(rng.standard_normal(b) * 0.1).astype(np.float32) for b in dims[1:]]
+    wp = [pn.pack_dense_x3(T(w)) for w in ws]
+    inp = x.astype(np.float64)
+    a, ae = T(x), None
+    for i, (w, b) in enumerate(zip(ws, bs)):
+        last = i == len(ws) - 1
+        mode = 2 if last else 1
+        res = pn.dense_h3p(a, ae, wp[i], T(b), w.shape[1], mode, pn.h3_bounds(w, b), pool_rows=pool if last else 0)
+        wd, bd = w.astype(np.float64), b.astype(np.float64)
+        exact = np.maximum(inp @ wd + bd, 0.0)
+        mag = np.abs(inp) @ np.abs(wd)
+        K = w.shape[0]
+        wfloor = 2.0 ** -37 * np.abs(wd).max() * np.abs(inp).sum(axis=1)[:, None]  # weights below 2^-14 of the max
+        bound = (H3_PRODUCT + 2 * (3 * K + 4) * U24) * (mag + wfloor) + wfloor + 2 * U24 * (np.abs(exact) + np.abs(bd))
+        if i == 0:  # fp32 rows: split in the tile loop under the running row scale
+            bound += _h3_terms(np.abs(inp), wd, np.abs(inp).max())
+        if last:
+            exact = exact.reshape(-1, pool, exact.shape[1]).max(axis=1)
+            bound = bound.reshape(-1, pool, bound.shape[1]).max(axis=1)
+            got = res.cpu().numpy().astype(np.float64)
+        else:
+            planes, e = res
+            en = e.cpu().numpy().astype(np.float64)
+            assert np.all(np.abs(exact).max(axis=1) < np.exp2(en) * (1 + 2.0 ** -20)), "row exponent is not a bound"
+            got = _h3_decode(planes, e)
+            bound = bound + 2.0 ** -22 * np.abs(got) + np.exp2(en - 38)[:, None]
+        err = np.abs(got - exact)
+        worst = np.unravel_index(int(np.argmax(err / np.maximum(bound, 1e-300))), err.shape)
+        assert np.all(err <= bound), f"layer {i + 1}, element {worst}: |err| {err[worst]:.3e} > bound {bound[worst]:.3e}"
+        if not last:
+            a, ae, inp = planes, e, got
 
 
 def test_dense_no_relu(cuda):

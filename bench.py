@@ -52,8 +52,7 @@ X3_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 3
 FP64_VALU_PEAK_TFLOPS = 78.6
 HBM_PEAK_GBS = 8000.0
 F64_ADD_LATENCY_CYCLES = 6.3  # dependent v_add_f64, operand in a register (tools/micro/f64_chain.hip)
-X3_KERNELS = ("sa1_group_mlp", "sa1_group_mlp_l1", "sa2_group_mlp", "sa2_layer1_points", "sa2_centre_layer1",
-              "sa3_dense1", "sa3_dense2", "sa3_dense3_pool")
+X3_KERNELS = ("sa1_group_mlp", "sa2_group_mlp", "sa2_layer1_points", "sa3_dense1", "sa3_dense2", "sa3_dense3_pool")
 
 
 def mlp_flops(rows, widths_in):
@@ -65,11 +64,6 @@ def ssg_kernel_work(n):
     m1, m2 = n // 16, n // 64
     return {
         "sa1_group_mlp": ("mfma", mlp_flops(m1 * 32, [3, 64, 64, 128])),
-        # the same kernel with SA2's per-point layer 1 (P = [f, x] W1 + b1 over the N/16 centres) as its
-        # epilogue (lidar_sa_group_mlp_bq_l1_f32); Q = c W1_xyz over the N/64 SA2 centres then runs on
-        # the side streams (sa2_centre_layer1)
-        "sa1_group_mlp_l1": ("mfma", mlp_flops(m1 * 32, [3, 64, 64, 128]) + 2 * m1 * 131 * 128),
-        "sa2_centre_layer1": ("mfma", 2 * m2 * 3 * 128),
         # SA2 layer 1 runs per point (N/16 rows of [f, x] W1 + b1, N/64 centre rows of
         # c W1_xyz); the fused kernel computes layers 2-3 of every grouped row
         "sa2_layer1_points": ("mfma", 2 * m1 * 131 * 128 + 2 * m2 * 3 * 128),
@@ -632,8 +626,6 @@ def main():
                     help="1: SA2's nested FPS and ball queries on the side streams as well (StreamingSSG l2_side; "
                          "1 213-1 227 vs 1 195-1 207 M pts/s in one A/B); 0: on the main stream")
     ap.add_argument("--rotate", type=int, default=8, help="distinct device-resident input batches the feed cycles over")
-    ap.add_argument("--pe", type=int, default=0,
-                    help="1: SA1's kernel computes SA2's per-point layer 1 as its epilogue (A/B; DESIGN.md 4.2)")
     ap.add_argument("--no-fp32-mfma-leg", action="store_true",
                     help="skip the extra measurement of the native fp32-MFMA kernels (when --x3 is on)")
     ap.add_argument("--no-standalone", action="store_true",
@@ -681,7 +673,7 @@ def main():
         come from the same window); False: the window runs clean and the per-kernel durations come
         from a second window of the same length (with ~25 launches per step, as MSG has, the
         events cost ~1/3)."""
-        bb = pn.PointNet2Backbone(cfg, device=dev, seed=0, dtype=dtype, x3=x3, point_layer_epilogue=bool(args.pe))
+        bb = pn.PointNet2Backbone(cfg, device=dev, seed=0, dtype=dtype, x3=x3)
         nb = max(1, args.rotate)
         xs = [torch.from_numpy(unit_frames(B, N, seed=sharding.frame_seed(seed_rank, step=i))).to(dev) for i in range(nb)]
         # one-batch forward(): what every pipeline output must equal (--no-verify: not issued, so a
@@ -797,19 +789,16 @@ def main():
         precomputed indices: the difference is what answering the queries costs inside it."""
         if not totals or "sa1_group_mlp_given_idx" not in totals:
             return None
-        fk = "sa1_group_mlp_l1" if "sa1_group_mlp_l1" in totals else "sa1_group_mlp"
-        f_l, f_f, f_ms = totals[fk]
+        f_l, f_f, f_ms = totals["sa1_group_mlp"]
         m_l, m_f, m_ms = totals["sa1_group_mlp_given_idx"]
         q_l, q_f, q_ms = totals["sa1_ball_query_separate"]
         per_frame = work["sa1_group_mlp"][1]
         return {"fused_ms_per_launch": f_ms / f_l, "mlp_given_idx_ms_per_launch": m_ms / m_l,
                 "query_ms_inside_fused": f_ms / f_l - m_ms / m_l, "separate_query_ms_per_launch": q_ms / q_l,
                 "frames_per_launch": f_f / f_l, "mlp_only_frac": per_frame * m_f / (m_ms / 1e3) / 1e12 / X3_PEAK_TFLOPS,
-                "fused_frac": work[fk][1] * f_f / (f_ms / 1e3) / 1e12 / X3_PEAK_TFLOPS, "fused_kernel": fk,
+                "fused_frac": per_frame * f_f / (f_ms / 1e3) / 1e12 / X3_PEAK_TFLOPS,
                 "basis": "one forward() over a group's frames, nothing else on the chip; the MLP on given indices "
-                         "is lidar_sa_group_mlp_x3 over the (B, M, 32) index tensor of the separate grid query"
-                         + ("; the fused kernel also computes SA2's per-point layer 1 (its epilogue), priced in "
-                            "fused_frac" if fk == "sa1_group_mlp_l1" else "")}
+                         "is lidar_sa_group_mlp_x3 over the (B, M, 32) index tensor of the separate grid query"}
 
     def roof(name, totals):
         """Roofline of one kernel over the launches `totals` recorded: achieved = the algorithmic
@@ -826,7 +815,7 @@ def main():
         else:
             a, p, u = w_total / s / 1e9, HBM_PEAK_GBS, "GB/s"
             basis = "HBM peak over compulsory bytes"
-        if name in ("sa1_group_mlp", "sa1_group_mlp_l1") and args.bq in ("bin", "main"):
+        if name == "sa1_group_mlp" and args.bq in ("bin", "main"):
             basis += "; the kernel also answers SA1's ball queries (lidar_sa_group_mlp_bq_f32), whose time is " \
                      "included and whose work is not priced"
         r = {"kernel": name, "bound": bound, "achieved": a, "peak": p, "unit": u, "frac": a / p,
@@ -850,7 +839,7 @@ def main():
     # main chain's device time; the chain lengths say which chain bounds a step.
     side = ("sa1_fps", "sa1_ball_query", "sa1_bq_bin") if args.bq == "side" else ("sa1_fps", "sa1_bq_bin")
     if args.l2_side:
-        side = side + ("sa2_fps", "sa2_ball_query", "sa2_centre_layer1")
+        side = side + ("sa2_fps", "sa2_ball_query")
     per_launch = {k: t / c for k, (c, f, t) in tot.items()}
     main_k = {k: v for k, v in per_launch.items() if k not in side}
     side_ms = sum(per_launch.get(k, 0) for k in side) / args.depth

@@ -233,24 +233,6 @@ int lidar_sa_group_mlp_bq_f32(lidar_handle *h, int32_t x1, const float *xyz, con
                               int32_t c2, int32_t c3, const void *packed, float *out, int64_t out_stride,
                               int64_t out_offset, int32_t *out_idx, void *stream);
 
-/* The SSG SA1 branch of lidar_sa_group_mlp_bq_f32 (x3; c1, c2, c3, nsample = 64, 64, 128, 32) with
- * the next level's per-point layer 1 fused as its epilogue (16 centres per workgroup = one MFMA
- * tile): pout (batch*m, p_stride >= 128) = f W1f + c W1x + b1 per centre c with f its 128 features —
- * the P operand of the next level's lidar_sa_group_mlp_x3_f32 (xyz_level 0, q = c2 W1x per SA2
- * centre), so SA1's features need not go through HBM into a separate GEMM.  out (the features,
- * bit-identical to lidar_sa_group_mlp_bq_f32's) may be NULL.  pimg: the device image
- * lidar_point_layer_pack_x3_f32 packs (host) from the next level's W1 (3 + 128, 128) in the canonical
- * row order [x, y, z, f...] and b1 (lidar_point_layer_packed_size_x3 bytes; -1 for other shapes).
- * P agrees with lidar_dense_x3f_f32 over [f, x, y, z] rows within h3's fp32-class error. */
-int64_t lidar_point_layer_packed_size_x3(int32_t cfeat, int32_t c1);
-int lidar_point_layer_pack_x3_f32(int32_t cfeat, int32_t c1, const float *w1_host, const float *b1_host,
-                                  void *packed_host);
-int lidar_sa_group_mlp_bq_l1_f32(lidar_handle *h, const float *xyz, const void *grid, const float *centres,
-                                 int64_t batch, int64_t n, int64_t m, float radius, int32_t nsample, int32_t c1,
-                                 int32_t c2, int32_t c3, const void *packed, float *out, int64_t out_stride,
-                                 int64_t out_offset, int32_t *out_idx, const void *pimg, float *pout,
-                                 int64_t p_stride, void *stream);
-
 /* y (batch*m, ldy) columns [col0, col0+3) = xyz rows; columns [col0+3, ldy) zeroed —
  * builds group_all's input [feats, xyz, 0-pad] next to features already in y. */
 int lidar_concat_xyz_pad_f32(lidar_handle *h, const float *xyz, int64_t rows, float *y,

@@ -66,10 +66,6 @@ SIGNATURES = {
     "lidar_fps_workspace_bytes": [I64, I64],
     "lidar_mlp_pack_x1_f32": [I32, I32, I32, P, P, P, P, P, P, P],
     "lidar_sa_group_mlp_bq_f32": [P, I32, P, P, P, I64, I64, I64, F32, I32, I32, I32, I32, P, P, I64, I64, P, P],
-    "lidar_point_layer_packed_size_x3": [I32, I32],
-    "lidar_point_layer_pack_x3_f32": [I32, I32, P, P, P],
-    "lidar_sa_group_mlp_bq_l1_f32": [P, P, P, P, I64, I64, I64, F32, I32, I32, I32, I32, P, P, I64, I64, P, P, P,
-                                     I64, P],
     "lidar_sa_group_mlp_x1_f32": [P, I32, P, I64, P, P, P, P, I64, I64, I64, I32, I32, I32, I32, P, P, I64, I64, P],
     "lidar_mlp_packed_size16": [I32, I32, I32, I32],
     "lidar_mlp_pack16_f32": [I32, I32, I32, I32, P, P, P, P, P, P, P],
@@ -102,7 +98,6 @@ _RESTYPES = {"lidar_last_error": ctypes.c_char_p,
              "lidar_mlp_packed_size16": I64, "lidar_mlp_packed_size_x3": I64,
              "lidar_ball_query_grid_bytes": ctypes.c_uint64,
              "lidar_dense_x3_packed_size": I64, "lidar_mlp_packed_size_x1": I64,
-             "lidar_point_layer_packed_size_x3": I64,
              "lidar_fps_workspace_bytes": ctypes.c_uint64, "lidar_voxel_batch_workspace_bytes": ctypes.c_uint64}
 
 

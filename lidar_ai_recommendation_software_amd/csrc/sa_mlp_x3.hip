@@ -132,37 +132,17 @@ __device__ __forceinline__ float max_row_groups(float v)
 #define LIDAR_BQ_CAP 512
 #endif
 constexpr int kBqCap = LIDAR_BQ_CAP;  // candidates per window a fused wave ranks in LDS (more: index-order scan)
-
-// The next level's per-point layer 1 as the epilogue of an xyz level (PE, SSG SA1 -> SA2): the
-// workgroup's 16 centres (CPW = 4 per wave) are the 16 rows of one MFMA tile, and
-//   P[c] = f[c] W1f + c W1x + b1       (f = the centre's C3 features, c its coordinates)
-// is the SA2 grouped layer 1's per-point term (relu(P[k] - Q[c2]) with Q = c2 W1x per SA2
-// centre), written straight to HBM: SA1's features need not round-trip through HBM into a
-// separate GEMM.  f W1f in h3 arithmetic (rows scaled by their own maximum: in the transposed form
-// D = W^T f^T a lane's row is its column, in and out), c W1x + b1 on the fp32 16x16x4 MFMA.
-// Image (lidar_point_layer_pack_x3_f32): [W1f: CP/32 chunks of PackX3's layer format (K = C3)]
-// [W1x fp32, CP/16 tiles x 64 lanes: lane (q, col) = W1x[q][16t + col], q < 3] [b1, CP fp32]
-// [tail: int32 exponent of W1f, 3 x int32 0].
-constexpr int kPeRows = 16;  // centres per workgroup of the PE kernel
-template <int C3, int CP>
-struct PointLayerImage {
-    static constexpr int KS = C3 / 32, CH = KS * 2 * 2 * 64;  // k-steps, chunk size (u4)
-    static constexpr int W1X = CP / 16 * 64;                  // fp32 of the W1x tiles
-    static constexpr int64_t bytes = (int64_t)CP / 32 * CH * 16 + (int64_t)(W1X + CP) * 4 + 16;
-};
-
-template <int C1, int C2, int C3, int NS, int L1, int R, bool X1, bool BQ, int CPW, bool PE>
-__device__ __forceinline__ void sa_x3_body(const float *__restrict__ P, int64_t stride, const float *__restrict__ Q,
-                                           const int32_t *__restrict__ idx, int n, int m, int64_t total,
-                                           const uint4 *__restrict__ packed, float *__restrict__ out,
-                                           int64_t out_stride, int64_t out_offset, const float *__restrict__ X,
-                                           const float *__restrict__ Cn, const char *__restrict__ grid_ws, float r,
-                                           float r2, int32_t *__restrict__ out_idx, const uint4 *__restrict__ pimg,
-                                           float *__restrict__ pout, int64_t pstride)
+template <int C1, int C2, int C3, int NS, int L1, int R, bool X1, bool BQ = false>
+__global__ __launch_bounds__(256, (BQ && !X1 && NS == 32) ? 5 : (R == 1 ? 3 : 2)) void sa_x3_kernel(const float *__restrict__ P, int64_t stride,
+                                                     const float *__restrict__ Q, const int32_t *__restrict__ idx,
+                                                     int n, int m, int64_t total, const uint4 *__restrict__ packed,
+                                                     float *__restrict__ out, int64_t out_stride, int64_t out_offset,
+                                                     const float *__restrict__ X, const float *__restrict__ Cn,
+                                                     const char *__restrict__ grid_ws, float r, float r2,
+                                                     int32_t *__restrict__ out_idx)
 {
     static_assert(!BQ || L1 == L1_XYZ, "fused ball query: xyz levels only");
     static_assert(NS % (16 * R) == 0 && C1 % 32 == 0 && C2 % 32 == 0 && C3 % 64 == 0, "tile shapes");
-    static_assert(!PE || (BQ && !X1 && CPW * 4 == kPeRows && C3 == 128), "point-layer epilogue: x3 SA1 form, 16 centres");
     constexpr bool XYZ = L1 == L1_XYZ, HASW1 = L1 != L1_PRE;
     using K = PackX3<C1, C2, C3, X1>;
     using PT = std::conditional_t<X1, bf16x8, f16x8>;  // MFMA operand pieces
@@ -192,10 +172,13 @@ __device__ __forceinline__ void sa_x3_body(const float *__restrict__ P, int64_t 
     // wave index in an SGPR: the LDS-DMA destinations (M0) and the unit below are wave-uniform
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int q = lane >> 4, col = lane & 15;
-    const int64_t blk = lidar::xcd_block();
+    const int64_t unit = lidar::xcd_block() * 4 + wave;
+    const bool live = unit < total;  // every wave takes part in the barriers
+    const int64_t cc = live ? unit : total - 1;
+    const int64_t b = cc / m;
 
     const uint4 *W2 = packed + (HASW1 ? K::W1U4 : 0);
-    const uint4 *W3 = W2 + (int64_t)(T2 / 2) * CH2;  // (not const: laundered per centre when CPW > 1)
+    const uint4 *W3 = W2 + (int64_t)(T2 / 2) * CH2;
     const float *Bias = reinterpret_cast<const float *>(W3 + (int64_t)(T3 / 2) * CH3);
     // h3: the layers' weight scaling exponents (X1: no scaling)
     int sw2 = 0, sw3 = 0;
@@ -223,34 +206,18 @@ __device__ __forceinline__ void sa_x3_body(const float *__restrict__ P, int64_t 
     for (int i = tid; i < C1 + C2 + C3; i += 256) bias_s[i] = Bias[i];
     if constexpr (HASW1)
         for (int i = tid; i < T1 * 64; i += 256) w1_s[i] = reinterpret_cast<const float *>(packed)[i];
-    // windows hold ~NS expected hits, so their candidates (27 cells of side >= r) scale with NS:
-    // about 220 at NS = 32 (SSG SA1), about 900 at NS = 128 (MSG's r = 0.4 branch), which past
-    // the cap would fall back to an index-order scan of the whole window
-    constexpr int QCAP = NS >= 128 ? 2 * kBqCap : kBqCap;
-    __shared__ int qidx[BQ ? 4 : 1][BQ ? NS : 1];           // this wave's ball-query result
-    __shared__ int qhits[BQ ? 4 : 1][BQ ? QCAP + 4 : 1];    // its per-window hit list
-    // PE: the wave's CPW feature rows stay in registers (relu'd, lane (q, col): channels 16 (4j + q) +
-    // col) until every chunk pass is done; then the workgroup's 16 rows (row 4 jc + wave) go to the
-    // free weight buffers: rows 0-7 in bufa, 8-15 in bufb, row stride C3 + 4 floats (a row's
-    // 16-byte reads spread over the banks)
-    constexpr int FST = C3 + 4;
-    static_assert(!PE || (SPLIT && 8 * FST * 4 <= CHMAX * 16), "PE: feature rows in the chunk buffers");
-    float resf[PE ? CPW : 1][T3 / 4];
-    int par0 = 0;
-    // one centre per call (jc: the wave's centre index); CPW == 1 runs it once, without a loop
-    auto centre = [&](const int jc) {
-    if constexpr (CPW > 1)  // recompute the addresses per centre rather than hold them across the loop
-        asm volatile("" : "+s"(W2), "+s"(W3), "+s"(P), "+s"(grid_ws), "+s"(Q), "+s"(out));
-    const int64_t unit = (blk * CPW + jc) * 4 + wave;
-    const bool live = unit < total;  // every wave takes part in the barriers
-    const int64_t cc = live ? unit : total - 1;
-    const int64_t b = cc / m;
     // layer 3's running max-pool of the raw accumulators in registers: mx[j] of row group q
     // holds channel 16 (4j + q) + col (register max, no LDS table: an LDS store here would make
     // the compiler wait for the weight prefetches in flight)
     float mx[T3 / 4];
 #pragma unroll
     for (int j = 0; j < T3 / 4; ++j) mx[j] = -INFINITY;
+    // windows hold ~NS expected hits, so their candidates (27 cells of side >= r) scale with NS:
+    // about 220 at NS = 32 (SSG SA1), about 900 at NS = 128 (MSG's r = 0.4 branch), which past
+    // the cap would fall back to an index-order scan of the whole window
+    constexpr int QCAP = NS >= 128 ? 2 * kBqCap : kBqCap;
+    __shared__ int qidx[BQ ? 4 : 1][BQ ? NS : 1];           // this wave's ball-query result
+    __shared__ int qhits[BQ ? 4 : 1][BQ ? QCAP + 4 : 1];    // its per-window hit list
     if constexpr (BQ) {
         const float *pf = P + (int64_t)b * n * 3;
         const char *fw = grid_ws + b * lidar_bq::grid_frame_bytes(n);
@@ -261,7 +228,7 @@ __device__ __forceinline__ void sa_x3_body(const float *__restrict__ P, int64_t 
     if constexpr (BQ)
         if (live && out_idx != nullptr)
             for (int i = lane; i < NS; i += 64) out_idx[unit * NS + i] = qidx[wave][i];
-    int &par = par0;  // the chunk buffer parity runs on across the wave's centres
+    int par = 0;
     // layer 3's max-pool runs on the raw accumulators: x -> relu(x + bias) is monotone in
     // fp32 (round-to-nearest addition never reverses an order), so max_i relu(a_i + b) ==
     // relu(max_i a_i + b) bit for bit — the bias and ReLU are applied once per output
@@ -335,7 +302,7 @@ __device__ __forceinline__ void sa_x3_body(const float *__restrict__ P, int64_t 
 #pragma unroll
         for (int c = 0; c < NCH; ++c) {
             const int cn = c + 1 < NCH ? c + 1 : 0;
-            const bool more = c + 1 < NCH || it + 1 < ITERS || jc + 1 < CPW;
+            const bool more = c + 1 < NCH || it + 1 < ITERS;
             if (more) fetch(cn, par ^ 1);  // lands during this chunk's MFMAs
             const uint4 *wb = bufp(par) + lane;
             f32x4 a0[R], a1[R];
@@ -459,16 +426,7 @@ __device__ __forceinline__ void sa_x3_body(const float *__restrict__ P, int64_t 
             par ^= 1;
         }
     }
-    if constexpr (PE) {
-#pragma unroll
-        for (int j = 0; j < T3 / 4; ++j) {
-            const int c3 = 16 * (4 * j + q) + col;
-            const float v = relu(mx[j] + bias_s[C1 + C2 + c3]);
-#pragma unroll
-            for (int k = 0; k < CPW; ++k) resf[k][j] = k == jc ? v : resf[k][j];  // no dynamic register index
-            if (live && out != nullptr) out[unit * out_stride + out_offset + c3] = v;
-        }
-    } else if (live) {
+    if (live) {
         float *o = out + unit * out_stride + out_offset;
 #pragma unroll
         for (int j = 0; j < T3 / 4; ++j) {
@@ -476,99 +434,6 @@ __device__ __forceinline__ void sa_x3_body(const float *__restrict__ P, int64_t 
             o[c3] = relu(mx[j] + bias_s[C1 + C2 + c3]);
         }
     }
-    };
-    if constexpr (CPW == 1) {
-        centre(0);
-    } else {
-#pragma unroll 1
-        for (int jc = 0; jc < CPW; ++jc) centre(jc);
-    }
-    if constexpr (PE) {
-        // ---- P = f W1f + c W1x + b1 for the workgroup's 16 centres; wave w: output tiles 2w, 2w + 1
-        using PI = PointLayerImage<C3, 128>;
-        constexpr int KSP = PI::KS;
-        const uint4 *wc = pimg + wave * PI::CH + lane;  // this wave's chunk (no reuse across waves: no LDS)
-        const float *pf32 = reinterpret_cast<const float *>(pimg + 128 / 32 * PI::CH);  // W1x tiles, b1, tail
-        const int sp = *reinterpret_cast<const int32_t *>(pf32 + PI::W1X + 128);
-        // the last chunk pass ended in a barrier and nothing was prefetched after it: both buffers are free
-        auto frow = [&](int rrow) -> float * {
-            return reinterpret_cast<float *>(rrow < 8 ? bufa[0] : bufb) + (rrow & 7) * FST;
-        };
-#pragma unroll
-        for (int k = 0; k < CPW; ++k)
-#pragma unroll
-            for (int j = 0; j < T3 / 4; ++j) frow(4 * k + wave)[16 * (4 * j + q) + col] = resf[k][j];
-        __syncthreads();  // the 16 rows complete
-        const float *fr = frow(col);
-        // the lane's row is col: element j of k-step s is channel in(s, q, j) = 32 s + 16 (j >> 2) +
-        // 4 q + (j & 3).  First the row's maximum (over its four lanes col, col + 16, col + 32, col + 48)
-        uint32_t mb = 0;
-#pragma unroll
-        for (int s = 0; s < KSP; ++s)
-#pragma unroll
-            for (int hh = 0; hh < 2; ++hh) {
-                const f32x4 v = *reinterpret_cast<const f32x4 *>(fr + 32 * s + 16 * hh + 4 * q);
-#pragma unroll
-                for (int t = 0; t < 4; ++t) mb = max(mb, __float_as_uint(v[t]));  // ReLU outputs: non-negative bits
-            }
-        const int e = lidar_h3::exp_of_bits(__float_as_uint(max_row_groups(__uint_as_float(mb))));
-        const float S = lidar_h3::scale_of(e);
-        f32x4 a[2] = {f32x4{}, f32x4{}};
-#pragma unroll
-        for (int s = 0; s < KSP; ++s) {
-            const f32x4 v0 = *reinterpret_cast<const f32x4 *>(fr + 32 * s + 4 * q);
-            const f32x4 v1 = *reinterpret_cast<const f32x4 *>(fr + 32 * s + 16 + 4 * q);
-            f16x8 xh, xl;
-            lidar_h3::split8(v0, v1, S, xh, xl);
-#pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                const f16x8 wh = __builtin_bit_cast(f16x8, wc[((s * 2 + t) * 2 + 0) * 64]);
-                const f16x8 wl = __builtin_bit_cast(f16x8, wc[((s * 2 + t) * 2 + 1) * 64]);
-                a[t] = mfma_bf(wh, xh, a[t]);
-                a[t] = mfma_bf(wh, xl, a[t]);
-                a[t] = mfma_bf(wl, xh, a[t]);
-            }
-        }
-        const int64_t grow = blk * kPeRows + col;  // the row's centre (a dead row repeats the last one)
-        const int64_t gcc = grow < total ? grow : total - 1;
-        const float xc = q < 3 ? Q[gcc * 3 + q] : 0.0f;  // B[k = q][row col] of the 16x16x4 MFMA
-        const float us = ldexpf(1.0f, e - 14 - sp);       // 2^-(s_row + s_w), per lane = per row
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-            const int tile = 2 * wave + t;
-            // c W1x + b1 (channel rows 16 tile + 4q + r; the bias is the accumulator's initial value)
-            f32x4 z = *reinterpret_cast<const f32x4 *>(pf32 + PI::W1X + 16 * tile + 4 * q);
-            z = mfma_f(pf32[tile * 64 + lane], xc, z);
-            f32x4 y;
-#pragma unroll
-            for (int rr = 0; rr < 4; ++rr) y[rr] = fmaf(a[t][rr], us, z[rr]);
-            if (grow < total) *reinterpret_cast<f32x4 *>(pout + grow * pstride + 16 * tile + 4 * q) = y;
-        }
-    }
-}
-
-template <int C1, int C2, int C3, int NS, int L1, int R, bool X1, bool BQ = false>
-__global__ __launch_bounds__(256, (BQ && !X1 && NS == 32) ? 5 : (R == 1 ? 3 : 2)) void sa_x3_kernel(
-    const float *__restrict__ P, int64_t stride, const float *__restrict__ Q, const int32_t *__restrict__ idx, int n,
-    int m, int64_t total, const uint4 *__restrict__ packed, float *__restrict__ out, int64_t out_stride,
-    int64_t out_offset, const float *__restrict__ X, const float *__restrict__ Cn, const char *__restrict__ grid_ws,
-    float r, float r2, int32_t *__restrict__ out_idx)
-{
-    sa_x3_body<C1, C2, C3, NS, L1, R, X1, BQ, 1, false>(P, stride, Q, idx, n, m, total, packed, out, out_stride,
-                                                         out_offset, X, Cn, grid_ws, r, r2, out_idx, nullptr, nullptr, 0);
-}
-// the SSG SA1 form with the next level's per-point layer 1 (PE): 16 centres per workgroup
-__global__ __launch_bounds__(256, 4) void sa_x3_pe_kernel(const float *__restrict__ xyz, const float *__restrict__ centres,
-                                                          int n, int m, int64_t total, const uint4 *__restrict__ packed,
-                                                          float *__restrict__ out, int64_t out_stride,
-                                                          int64_t out_offset, const char *__restrict__ grid_ws, float r,
-                                                          float r2, int32_t *__restrict__ out_idx,
-                                                          const uint4 *__restrict__ pimg, float *__restrict__ pout,
-                                                          int64_t pstride)
-{
-    sa_x3_body<64, 64, 128, 32, L1_XYZ, 2, false, true, kPeRows / 4, true>(
-        xyz, 3, centres, nullptr, n, m, total, packed, out, out_stride, out_offset, nullptr, nullptr, grid_ws, r, r2,
-        out_idx, pimg, pout, pstride);
 }
 
 // The wide feature levels (SA2): the arithmetic of sa_x3_kernel<.., L1_PRE, R = 2, false> in
@@ -832,21 +697,6 @@ int launch_x3_bq(const float *xyz, const char *grid, const float *centres, int64
     return LIDAR_OK;
 }
 
-// SSG SA1 with its ball queries inside and SA2's per-point layer 1 as the epilogue (PE)
-int launch_x3_bq_pe(const float *xyz, const char *grid, const float *centres, int64_t batch, int64_t n, int64_t m,
-                    float radius, const void *packed, float *out, int64_t os, int64_t oo, int32_t *out_idx,
-                    const void *pimg, float *pout, int64_t pstride, hipStream_t s)
-{
-    const int64_t total = batch * m;
-    const int64_t blocks = (total + kPeRows - 1) / kPeRows;
-    REQUIRE(blocks <= 0x7fffffff, "sa_group_mlp_bq_l1: too many centres");
-    hipLaunchKernelGGL(sa_x3_pe_kernel, dim3((unsigned)blocks), dim3(256), 0, s, xyz, centres, (int)n, (int)m, total,
-                       static_cast<const uint4 *>(packed), out, os, oo, grid, radius, radius * radius, out_idx,
-                       static_cast<const uint4 *>(pimg), pout, pstride);
-    LAUNCH_CHECK();
-    return LIDAR_OK;
-}
-
 __host__ uint16_t bf16_rne(float f)
 {
     uint32_t u;
@@ -887,23 +737,6 @@ __host__ int32_t layer_exp(const float *w, int64_t n)
     }
     return 14 - lidar_h3::exp_of_bits(m);
 }
-// one layer (cin, cout) of W 2^sexp in PackX3's chunk format (fp16 hi / lo fragments); returns the end
-__host__ uint16_t *pack_layer_x3(const float *w, int cin, int cout, int32_t sexp, uint16_t *u)
-{
-    const float sc = std::ldexp(1.0f, sexp);
-    for (int c = 0; c < cout / 32; ++c)
-        for (int s = 0; s < cin / 32; ++s)
-            for (int t = 0; t < 2; ++t)
-                for (int h = 0; h < 2; ++h)
-                    for (int l = 0; l < 64; ++l)
-                        for (int j = 0; j < 8; ++j) {
-                            const int in = 32 * s + 16 * (j >> 2) + 4 * (l >> 4) + (j & 3);
-                            const float v = w[(int64_t)in * cout + 16 * (2 * c + t) + (l & 15)] * sc;
-                            const uint16_t hi = f16_bits(v);
-                            *u++ = h == 0 ? hi : f16_bits(v - f16_to_f(hi));
-                        }
-    return u;
-}
 
 }  // namespace
 
@@ -939,7 +772,20 @@ LIDAR_EXPORT int lidar_mlp_pack_x3_f32(int32_t xyz_level, int32_t c1, int32_t c2
     tail.s2 = layer_exp(w2, (int64_t)c1 * c2);
     tail.s3 = layer_exp(w3, (int64_t)c2 * c3);
     auto layer = [&](const float *w, int cin, int cout, int32_t sexp) {
-        o = reinterpret_cast<char *>(pack_layer_x3(w, cin, cout, sexp, reinterpret_cast<uint16_t *>(o)));
+        const float sc = std::ldexp(1.0f, sexp);
+        uint16_t *u = reinterpret_cast<uint16_t *>(o);
+        for (int c = 0; c < cout / 32; ++c)
+            for (int s = 0; s < cin / 32; ++s)
+                for (int t = 0; t < 2; ++t)
+                    for (int h = 0; h < 2; ++h)
+                        for (int l = 0; l < 64; ++l)
+                            for (int j = 0; j < 8; ++j) {
+                                const int in = 32 * s + 16 * (j >> 2) + 4 * (l >> 4) + (j & 3);
+                                const float v = w[(int64_t)in * cout + 16 * (2 * c + t) + (l & 15)] * sc;
+                                const uint16_t hi = f16_bits(v);
+                                *u++ = h == 0 ? hi : f16_bits(v - f16_to_f(hi));
+                            }
+        o = reinterpret_cast<char *>(u);
     };
     layer(w2, c1, c2, tail.s2);
     layer(w3, c2, c3, tail.s3);
@@ -1113,67 +959,4 @@ LIDAR_EXPORT int lidar_sa_group_mlp_bq_f32(lidar_handle *h, int32_t x1, const fl
     LIDAR_SABQ(64, 96, 128, 128)
 #undef LIDAR_SABQ
     return lidar::fail(LIDAR_EINVAL, "lidar_sa_group_mlp_bq_f32: unsupported (widths, nsample) combination");
-}
-
-// ------------------------------------------------------------- SA1 + SA2's per-point layer 1
-// bytes of the point-layer image of a (3 + cfeat, c1) layer 1 (lidar_point_layer_pack_x3_f32)
-LIDAR_EXPORT int64_t lidar_point_layer_packed_size_x3(int32_t cfeat, int32_t c1)
-{
-    if (cfeat != 128 || c1 != 128) return -1;
-    return PointLayerImage<128, 128>::bytes;
-}
-
-// host packer: w1 (3 + cfeat, c1) in the canonical row order [x, y, z, f...] (the layer-1 weights of
-// the next level's branch, BN folded), b1 (c1) -> the image sa_x3_kernel's PE epilogue reads:
-// W1f (rows 3..) scaled by its power of two and split into fp16 hi / lo (PackX3 chunks), W1x (rows 0..2)
-// fp32 in the 16x16x4 MFMA's A order, b1, the exponent.  Shapes: cfeat = c1 = 128 (SSG SA2).
-LIDAR_EXPORT int lidar_point_layer_pack_x3_f32(int32_t cfeat, int32_t c1, const float *w1, const float *b1,
-                                               void *packed)
-{
-    REQUIRE(w1 && b1 && packed, "lidar_point_layer_pack_x3_f32: null pointer");
-    REQUIRE(cfeat == 128 && c1 == 128, "lidar_point_layer_pack_x3_f32: (cfeat, c1) must be (128, 128)");
-    using PI = PointLayerImage<128, 128>;
-    const float *wf = w1 + (int64_t)3 * c1;
-    const int32_t sexp = layer_exp(wf, (int64_t)cfeat * c1);
-    uint16_t *u = pack_layer_x3(wf, cfeat, c1, sexp, static_cast<uint16_t *>(packed));
-    float *f = reinterpret_cast<float *>(u);
-    for (int t = 0; t < c1 / 16; ++t)
-        for (int l = 0; l < 64; ++l) {
-            const int qq = l >> 4;
-            *f++ = qq < 3 ? w1[(int64_t)qq * c1 + 16 * t + (l & 15)] : 0.0f;
-        }
-    for (int i = 0; i < c1; ++i) *f++ = b1[i];
-    const int32_t tail[4] = {sexp, 0, 0, 0};
-    memcpy(f, tail, sizeof tail);
-    REQUIRE(reinterpret_cast<char *>(f) + sizeof tail - static_cast<char *>(packed) == PI::bytes,
-            "lidar_point_layer_pack_x3_f32: image size mismatch");
-    return LIDAR_OK;
-}
-
-// lidar_sa_group_mlp_bq_f32 (x3, SSG SA1: c1 = 64, c2 = 64, c3 = 128, nsample 32) with the next
-// level's per-point layer 1 fused as its epilogue: pout (batch*m, p_stride) = f W1f + c W1x + b1 per
-// centre c (f = its c3 features, pimg = lidar_point_layer_pack_x3_f32's image), the operand the next
-// level's grouped layer 1 reads as relu(P[k] - Q[c2]) (lidar_sa_group_mlp_x3_f32, xyz_level 0).  out
-// (the features themselves) may be NULL.  P matches lidar_dense_x3f_f32 of [f, x, y, z] rows within
-// h3's fp32-class error; the features equal lidar_sa_group_mlp_bq_f32's bit for bit.
-LIDAR_EXPORT int lidar_sa_group_mlp_bq_l1_f32(lidar_handle *h, const float *xyz, const void *grid,
-                                              const float *centres, int64_t batch, int64_t n, int64_t m,
-                                              float radius, int32_t nsample, int32_t c1, int32_t c2, int32_t c3,
-                                              const void *packed, float *out, int64_t out_stride,
-                                              int64_t out_offset, int32_t *out_idx, const void *pimg, float *pout,
-                                              int64_t p_stride, void *stream)
-{
-    REQUIRE(h && xyz && grid && centres && packed && pimg && pout, "lidar_sa_group_mlp_bq_l1_f32: null pointer");
-    REQUIRE(batch >= 0 && n >= 1 && n < 0x3fffffff && m >= 1 && m < 0x7fffffff,
-            "lidar_sa_group_mlp_bq_l1_f32: bad sizes");
-    REQUIRE(radius >= 0.0f, "lidar_sa_group_mlp_bq_l1_f32: negative radius");
-    REQUIRE(c1 == 64 && c2 == 64 && c3 == 128 && nsample == 32,
-            "lidar_sa_group_mlp_bq_l1_f32: (c1, c2, c3, nsample) must be (64, 64, 128, 32)");
-    REQUIRE(out == nullptr || (out_offset >= 0 && out_offset + c3 <= out_stride),
-            "lidar_sa_group_mlp_bq_l1_f32: output columns exceed out_stride");
-    REQUIRE(p_stride >= 128 && p_stride % 4 == 0, "lidar_sa_group_mlp_bq_l1_f32: p_stride >= 128, multiple of 4");
-    if (batch == 0) return LIDAR_OK;
-    ON_DEVICE(h->device);
-    return launch_x3_bq_pe(xyz, static_cast<const char *>(grid), centres, batch, n, m, radius, packed, out,
-                           out_stride, out_offset, out_idx, pimg, pout, p_stride, static_cast<hipStream_t>(stream));
 }

@@ -323,68 +323,6 @@ def layer1_weights(layer, cfeat, to_dev):
     return {"w1": to_dev(w1p), "b1": to_dev(bp), "wq": to_dev(wq), "zero": to_dev(np.zeros(cp, np.float32))}
 
 
-def has_point_layer_epilogue():
-    """Whether the loaded library has the SA1 kernel with SA2's per-point layer 1 as its epilogue
-    (lidar_sa_group_mlp_bq_l1_f32, ABI 4); A/B builds of earlier rounds, loaded through
-    LIDAR_AMD_LIB, run the separate per-point GEMM instead (the same arithmetic spec)."""
-    return getattr(nat.load_library(), "lidar_sa_group_mlp_bq_l1_f32", None) is not None
-
-
-def pack_point_layer_x3(layer, cfeat, device):
-    """(W1 (3 + cfeat, c1) canonical rows [x, y, z, f...], b1) -> the device image of
-    lidar_point_layer_pack_x3_f32 (W1f in h3 fp16 hi / lo fragments, W1x fp32, b1)."""
-    w1, b1 = layer
-    c1 = w1.shape[1]
-    lib = nat.load_library()
-    nbytes = lib.lidar_point_layer_packed_size_x3(int(cfeat), int(c1))
-    if nbytes < 0:
-        raise ValueError(f"no point-layer epilogue for (cfeat, c1) = ({cfeat}, {c1})")
-    out = np.zeros(nbytes, dtype=np.uint8)
-    arrs = [np.ascontiguousarray(a, dtype=np.float32) for a in (w1, b1)]
-    nat.check(lib.lidar_point_layer_pack_x3_f32(int(cfeat), int(c1), *[a.ctypes.data_as(ctypes.c_void_p) for a in arrs],
-                                                out.ctypes.data_as(ctypes.c_void_p)), "lidar_point_layer_pack_x3_f32")
-    return torch.from_numpy(out).to(device)
-
-
-def group_mlp_bq_l1(xyz, centres, grid, radius, nsample, packed, widths, pimg, pout, out=None, out_offset=0,
-                    out_idx=None):
-    """group_mlp_bq (x3, SSG SA1) with the next level's per-point layer 1 as the kernel's epilogue
-    (lidar_sa_group_mlp_bq_l1_f32): pout (B*M, stride >= 128) = f W1f + c W1x + b1 per centre, the
-    P operand of the next level's group_mlp_x3; out (the SA1 features) optional."""
-    B, n, _ = xyz.shape
-    M = centres.shape[1]
-    c1, c2, c3 = widths
-    if not (xyz.is_contiguous() and centres.is_contiguous()):
-        raise ValueError("group_mlp_bq_l1: xyz / centres must be contiguous")
-    if pout.shape[0] < B * M or pout.dim() != 2:
-        raise ValueError("group_mlp_bq_l1: pout must be (>= B*M, stride)")
-    _dev_check(xyz, centres, grid, packed, pimg, pout, out, out_idx)
-    nat.call("lidar_sa_group_mlp_bq_l1_f32", nat.handle(xyz.device.index), nat.ptr(xyz), nat.ptr(grid),
-             nat.ptr(centres), B, n, M, float(radius), int(nsample), c1, c2, c3, nat.ptr(packed), nat.ptr(out),
-             out.shape[-1] if out is not None else 0, out_offset, nat.ptr(out_idx), nat.ptr(pimg), nat.ptr(pout),
-             pout.shape[1], nat.stream_ptr())
-    return pout
-
-
-def centre_layer1(new_xyz, branches, out=None, slot=0):
-    """Q = [c, 0-pad] W1_xyz' per centre of a feature level for every branch (the per-centre half of
-    layer1_per_point; rows B*M rounded to 128): -> [Q per branch].  out: optional [(cpad (R, 16),
-    Q (R, cp)) per branch] preallocated buffers, cpad zero beyond row B*M."""
-    B, M, _ = new_xyz.shape
-    dev = new_xyz.device
-    h = nat.handle(dev.index, slot)
-    rq = (B * M + 127) // 128 * 128
-    res = []
-    for i, br in enumerate(branches):
-        pre = br["pre"]
-        cp = pre["w1"].shape[1]
-        cpad, q = out[i] if out is not None else (torch.zeros((rq, 16), dtype=torch.float32, device=dev), None)
-        cpad, q = cpad[:rq], (q[:rq] if q is not None else None)
-        nat.call("lidar_concat_xyz_pad_f32", h, nat.ptr(new_xyz), B * M, nat.ptr(cpad), 16, 0, nat.stream_ptr())
-        res.append(dense_x3s(cpad, pre["wq_x3"], pre["zero"], cp, relu=False, out=q, slot=slot))
-    return res
-
-
 def layer1_per_point(x_rows, xyz, cfeat, new_xyz, branches, x3=True):
     """Layer 1 of every branch of a level, per point instead of per grouped row.
 
@@ -445,7 +383,7 @@ def dense_relu(x, w, b, pool_rows=0, out=None):
     return dense(x, w, b, True, pool_rows, out)
 
 
-def dense_x3s(a, wpack, b, cout, relu=True, pool_rows=0, out=None, x1=False, slot=0):
+def dense_x3s(a, wpack, b, cout, relu=True, pool_rows=0, out=None, x1=False):
     """a (rows, k) fp32 @ W + b on the dense GEMM of csrc/dense_x3s.hip (lidar_dense_x3f_f32; wpack =
     pack_dense_x3(W), h3 arithmetic; x1: pack_dense_x3(W, x1=True), the bf16 spec).  Returns fp32
     rows (rows, cout) or, with pool_rows, the fp32 max over runs of pool_rows rows (ReLU)."""
@@ -460,7 +398,7 @@ def dense_x3s(a, wpack, b, cout, relu=True, pool_rows=0, out=None, x1=False, slo
         if out is None:
             out = torch.empty((rows, cout), dtype=torch.float32, device=dev)
     _dev_check(a, wpack, b, out)
-    nat.call("lidar_dense_x3f_f32", nat.handle(dev.index, slot), nat.ptr(a), lda, rows, lda, nat.ptr(wpack), nat.ptr(b),
+    nat.call("lidar_dense_x3f_f32", nat.handle(dev.index), nat.ptr(a), lda, rows, lda, nat.ptr(wpack), nat.ptr(b),
              cout, mode | (4 if x1 else 0), 1 if relu else 0, pool_rows, nat.ptr(out), 0, out.shape[1],
              nat.stream_ptr())
     return out
@@ -539,7 +477,7 @@ class PointNet2Backbone:
     (B, C_last) plus, with keep_levels, per level (new_xyz, features, fps_idx, [ball-query
     idx per branch])."""
 
-    def __init__(self, cfg=SSG, weights=None, device="cuda", seed=0, dtype="f32", x3=True, point_layer_epilogue=False):
+    def __init__(self, cfg=SSG, weights=None, device="cuda", seed=0, dtype="f32", x3=True):
         """dtype "f32" (the fp32 contract: features within 1e-4 of the fp32 oracle): x3=True (default)
         runs the MLPs on the fp16 matrix cores in h3 arithmetic (lidar_sa_group_mlp_x3_f32,
         lidar_dense_x3f_f32), x3=False on the native fp32 matrix cores (lidar_sa_group_mlp16_f32,
@@ -548,9 +486,7 @@ class PointNet2Backbone:
         (inputs, activations and weights rounded to bf16, fp32 accumulation); group_all stays in
         fp32 arithmetic on the x3 GEMM.
         Levels with point features run layer 1 per point (layer1_per_point / layer1_points_x1) and
-        the fused kernel from layer 2 on.  point_layer_epilogue (SSG, x3): SA1's kernel computes SA2's
-        per-point layer 1 as its epilogue (lidar_sa_group_mlp_bq_l1_f32) instead of the separate GEMM —
-        measured slower in the pipeline, so off by default."""
+        the fused kernel from layer 2 on."""
         if dtype not in ("f32", "bf16"):
             raise ValueError("dtype must be 'f32' or 'bf16'")
         self.bf16 = dtype == "bf16"
@@ -605,9 +541,6 @@ class PointNet2Backbone:
                         if x3:
                             br["pre"]["w1_x3"] = pack_dense_x3(br["pre"]["w1"])
                             br["pre"]["wq_x3"] = pack_dense_x3(br["pre"]["wq"])
-                            if point_layer_epilogue and cfeat == 128 and widths[0] == 128:
-                                # the previous (SSG SA1) level's kernel computes P itself (forward)
-                                br["pre"]["point_l1"] = pack_point_layer_x3(layers[0], cfeat, self.device)
                 branches.append(br)
             entry = {"div": lvl["npoint_div"], "branches": branches, "cfeat": cfeat}
             if not xyz_level:  # the previous level writes this level's padded rows [f, x, y, z, 0]
@@ -644,7 +577,6 @@ class PointNet2Backbone:
         rows = None  # flat padded (R, k) rows behind `feats` when the next level reads them
         out_levels = []
         fz = None  # previous level's FPS first_zero (nested-FPS shortcut)
-        pnext = None  # the next level's per-point layer-1 operand P, written by this level's kernel
         t = self.timers
         for li, lvl in enumerate(self.levels):
             if lvl.get("group_all"):
@@ -660,27 +592,6 @@ class PointNet2Backbone:
             fz = nfz
             ctot = sum(br["widths"][-1] for br in lvl["branches"])
             nxt = self.levels[li + 1] if li + 1 < len(self.levels) else None
-            br0 = lvl["branches"][0]
-            if (nxt is not None and nxt.get("pre") and len(lvl["branches"]) == 1 and len(nxt["branches"]) == 1
-                    and "point_l1" in nxt["branches"][0].get("pre", {}) and "packed_x3" in br0
-                    and tuple(br0["widths"]) == (64, 64, 128) and br0["ns"] == 32 and pl.get("bq") is None
-                    and (pl.get("grid") is not None or N >= BQ_GRID_MIN_N)):
-                # SSG SA1 -> SA2: the SA1 kernel (ball queries inside) writes SA2's per-point layer-1
-                # operand P itself; its features reach HBM only when the levels are kept
-                grid = (pl["grid"][0] if pl.get("grid") is not None else
-                        _call(t, f"sa{li + 1}_bq_bin", B, ball_query_bin, br0["r"], br0["ns"], xyz,
-                              self._grid_buffer(B, N, xyz.device)))
-                out = torch.empty((B, M, ctot), dtype=torch.float32, device=xyz.device) if keep_levels else None
-                gidx = torch.empty((B, M, br0["ns"]), dtype=torch.int32, device=xyz.device) if keep_levels else None
-                pnext = torch.empty((B * M, 128), dtype=torch.float32, device=xyz.device)
-                _call(t, f"sa{li + 1}_group_mlp_l1", B, group_mlp_bq_l1, xyz, new_xyz, grid, br0["r"], br0["ns"],
-                      br0["packed_x3"], br0["widths"], nxt["branches"][0]["pre"]["point_l1"], pnext, out=out,
-                      out_idx=gidx)
-                if keep_levels:
-                    out_levels.append((new_xyz, out, idx, [gidx]))
-                xyz, feats, rows = new_xyz, out, None
-                N = M
-                continue
             # a level feeding group_all or a per-point layer 1 writes straight into the
             # next level's padded input rows [f, x, y, z, 0-pad] (R = B*M rounded to 128)
             padded = nxt is not None and (nxt.get("group_all") or nxt.get("pre"))
@@ -689,10 +600,7 @@ class PointNet2Backbone:
             out_rows = torch.empty((R, stride), dtype=torch.float32, device=xyz.device)
             out = out_rows[:B * M].view(B, M, stride)
             pq = None
-            if lvl.get("pre") and pnext is not None:  # P from the previous level's kernel; Q per centre here
-                qs = pl.get("q") or _call(t, f"sa{li + 1}_centre_layer1", B, centre_layer1, new_xyz, lvl["branches"])
-                pq, pnext = [(pnext, qs[0])], None
-            elif lvl.get("pre") and self.bf16:
+            if lvl.get("pre") and self.bf16:
                 pq = _call(t, f"sa{li + 1}_layer1_points", B, layer1_points_x1, rows, xyz, lvl["cfeat"],
                            lvl["branches"])
             elif lvl.get("pre"):
@@ -768,6 +676,12 @@ class PointNet2Backbone:
             M, rows = mp, B * mp
         t = self.timers
         ws, bs = lvl["w"], lvl["b"]
+        if self.x3 and not hasattr(nat.load_library(), "lidar_dense_h3p_f32"):
+            # an earlier round's library (A/B through LIDAR_AMD_LIB): fp32 rows between the layers
+            wp = lvl["w_x3"]
+            h1 = _call(t, "sa3_dense1", B, dense_x3s, x2, wp[0], bs[0], ws[0].shape[1])
+            h2 = _call(t, "sa3_dense2", B, dense_x3s, h1, wp[1], bs[1], ws[1].shape[1])
+            return _call(t, "sa3_dense3_pool", B, dense_x3s, h2, wp[2], bs[2], ws[2].shape[1], pool_rows=M)
         if self.x3:  # h3 planes between the layers (split once, by the producer); dense3 fuses the max-pool
             wp, bd = lvl["w_x3"], lvl["h3_bounds"]
             h1, e1 = _call(t, "sa3_dense1", B, dense_h3p, x2, None, wp[0], bs[0], ws[0].shape[1], 1, bd[0])
@@ -853,13 +767,7 @@ class StreamingSSG:
             self.fz2 = [torch.empty(GB, dtype=torch.int32, device=dev) for _ in range(nslot)]
             self.gidx2 = [[torch.empty((GB, self.M2, br["ns"]), dtype=torch.int32, device=dev)
                            for br in lvl1["branches"]] for _ in range(nslot)]
-        # SA2's per-centre layer-1 term Q on the side stream too, when the SA1 kernel writes P itself
-        self.q2 = None
-        if self.l2 and all("point_l1" in br.get("pre", {}) for br in lvl1["branches"]):
-            rq = (GB * self.M2 + 127) // 128 * 128
-            self.q2 = [[(torch.zeros((rq, 16), dtype=torch.float32, device=dev),
-                         torch.empty((rq, br["pre"]["w1"].shape[1]), dtype=torch.float32, device=dev))
-                        for br in lvl1["branches"]] for _ in range(nslot)]
+
         # setup-time workspace sizing of the side handles (FPS + ball queries), so no stage's
         # first call grows a workspace (lidar_reserve; growth retires the old block, no device sync)
         if reserve:
@@ -912,9 +820,7 @@ class StreamingSSG:
                     tag = "sa2" + (f"_b{bi_}" if len(lvl1["branches"]) > 1 else "")
                     _call(t, f"{tag}_ball_query", g, ball_query, br["r"], br["ns"], c1, self.cxyz2[slot][:g],
                           out=self.gidx2[slot][bi_][:g], slot=hs)
-                if self.q2 is not None:
-                    _call(t, "sa2_centre_layer1", g, centre_layer1, self.cxyz2[slot][:g], lvl1["branches"],
-                          out=self.q2[slot], slot=hs)
+
             self.fps_done[slot].record(fs)
         return slot
 
@@ -930,13 +836,11 @@ class StreamingSSG:
         if self.l2:
             pre2 = {"fps": (self.idx2[slot][:g], self.cxyz2[slot][:g], self.fz2[slot][:g]),
                     "bq": [gi[:g] for gi in self.gidx2[slot]]}
-            if self.q2 is not None:
-                pre2["q"] = [q[:(g * self.M2 + 127) // 128 * 128] for _, q in self.q2[slot]]
+
         if self.keep:  # the slot's buffers are reused by a later group
             lvl0 = [a.clone() for a in lvl0[:3]] + [[gi.clone() for gi in lvl0[3]] if lvl0[3] is not None else None]
             if pre2 is not None:
-                pre2 = {k: (tuple(a.clone() for a in v) if k == "fps" else [a.clone() for a in v])
-                        for k, v in pre2.items()}
+                pre2 = {"fps": tuple(a.clone() for a in pre2["fps"]), "bq": [gi.clone() for gi in pre2["bq"]]}
         out, levels = self.bb.forward_from_sa1_fps(x, *lvl0, keep_levels=self.keep,
                                                    grids1=self.grid[slot] if self.grid is not None else None,
                                                    pre2=pre2)

@@ -330,62 +330,6 @@ def test_group_mlp_bq_matches_unfused(cuda, frame, widths, r, ns, x1):
     assert np.array_equal(got.cpu().numpy().view(np.uint32), want.cpu().numpy().view(np.uint32))
 
 
-@pytest.mark.parametrize("frame", ["uniform", "clump", "line", "all_equal", "lattice_ties"])
-@pytest.mark.parametrize("M", [301, 1024])
-def test_group_mlp_bq_l1_matches_unfused(cuda, frame, M):
-    """lidar_sa_group_mlp_bq_l1_f32 (SSG SA1 with SA2's per-point layer 1 as its epilogue, 16 centres
-    per workgroup): the features and ball-query indices equal lidar_sa_group_mlp_bq_f32's bit for bit,
-    and every element of P = f W1f + c W1x + b1 lies within its rigorous bound against the exact
-    (float64) product over the kernel's own features: h3's product terms on f W1f, the fp32 MFMA's
-    roundings on the xyz / bias term, one rounding of the sum.  M = 301: a partial last workgroup."""
-    if not pn.has_point_layer_epilogue():  # an earlier round's library loaded for an A/B (LIDAR_AMD_LIB)
-        pytest.skip("library without lidar_sa_group_mlp_bq_l1_f32")
-    B, N = 2, 6000
-    x = unit_frames(B, N, 43) if frame == "uniform" else np.stack([_bq_edge_frames()[frame]] * B)
-    x = np.ascontiguousarray(x)
-    N = x.shape[1]
-    c = np.ascontiguousarray(x[:, np.arange(M) * N // M])
-    rng = np.random.default_rng(5)
-    widths, r, ns = [64, 64, 128], 0.2, 32
-    layers, k = [], 3
-    for w in widths:
-        layers.append(((rng.standard_normal((k, w)) * (1.5 / np.sqrt(k))).astype(np.float32),
-                       (rng.standard_normal(w) * 0.1).astype(np.float32)))
-        k = w
-    w1 = (rng.standard_normal((131, 128)) / np.sqrt(131)).astype(np.float32)  # [x, y, z, f...] rows
-    b1 = (rng.standard_normal(128) * 0.1).astype(np.float32)
-    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(cuda)
-    xt, ct = T(x), T(c)
-    packed = T(pn.pack_branch_x3(layers, True))
-    pimg = pn.pack_point_layer_x3((w1, b1), 128, cuda)
-    grid = pn.ball_query_bin(r, ns, xt, pn.ball_query_grid_buffer(B, N, cuda))
-    want = torch.full((B, M, 132), -7.0, dtype=torch.float32, device=cuda)
-    wi = torch.full((B, M, ns), -5, dtype=torch.int32, device=cuda)
-    pn.group_mlp_bq(xt, ct, grid, r, ns, packed, widths, want, 2, out_idx=wi)
-    got = torch.full_like(want, -7.0)
-    gi = torch.full_like(wi, -5)
-    P = torch.full((B * M, 132), -9.0, dtype=torch.float32, device=cuda)
-    pn.group_mlp_bq_l1(xt, ct, grid, r, ns, packed, widths, pimg, P, out=got, out_offset=2, out_idx=gi)
-    assert torch.equal(gi, wi)
-    assert np.array_equal(got.cpu().numpy().view(np.uint32), want.cpu().numpy().view(np.uint32))
-    Pn = P.cpu().numpy()
-    assert np.all(Pn[:, 128:] == -9.0), "P columns past 128 must stay untouched"
-    f = got.cpu().numpy()[..., 2:130].reshape(B * M, 128)
-    exact_f, bnd = h3_gemm_bound(f, w1[3:])
-    xyz = c.reshape(B * M, 3).astype(np.float64)
-    w1x = w1[:3].astype(np.float64)
-    zx = xyz @ w1x + b1.astype(np.float64)
-    exact = exact_f + zx
-    bnd = bnd + 4 * U24 * (np.abs(xyz) @ np.abs(w1x) + np.abs(b1)) + U24 * np.abs(exact)
-    err = np.abs(Pn[:, :128].astype(np.float64) - exact)
-    worst = np.unravel_index(np.argmax(err / bnd), err.shape)
-    assert np.all(err <= bnd), f"P{worst}: |err| {err[worst]:.3e} > bound {bnd[worst]:.3e}"
-    # the pipeline's form without the features (out = NULL)
-    P2 = torch.full_like(P, -9.0)
-    pn.group_mlp_bq_l1(xt, ct, grid, r, ns, packed, widths, pimg, P2)
-    assert torch.equal(P2, P)
-
-
 def _h3_decode(planes, e):
     """h3 planes (2, rows, k) float16 + row exponents -> the values the next GEMM multiplies (float64)."""
     p = planes.cpu().numpy().astype(np.float64)

@@ -131,6 +131,12 @@ __device__ __forceinline__ float max_row_groups(float v)
 #ifndef LIDAR_BQ_CAP
 #define LIDAR_BQ_CAP 512
 #endif
+// LIDAR_SA_E3_BOUND: layer 3's input exponent in sa_x3_kernel from the bound colsum(W2) 2^e2 + max|b2|
+// (1, round 4: no pass over the tile, 95 VGPRs and no scratch; SA1 1.66 -> 1.62 ms alone per 128
+// frames) or a wave maximum over the tile (0)
+#ifndef LIDAR_SA_E3_BOUND
+#define LIDAR_SA_E3_BOUND 1
+#endif
 constexpr int kBqCap = LIDAR_BQ_CAP;  // candidates per window a fused wave ranks in LDS (more: index-order scan)
 template <int C1, int C2, int C3, int NS, int L1, int R, bool X1, bool BQ = false>
 __global__ __launch_bounds__(256, (BQ && !X1 && NS == 32) ? 5 : (R == 1 ? 3 : 2)) void sa_x3_kernel(const float *__restrict__ P, int64_t stride,
@@ -365,13 +371,19 @@ __global__ __launch_bounds__(256, (BQ && !X1 && NS == 32) ? 5 : (R == 1 ? 3 : 2)
 #pragma unroll
                     for (int rr = 0; rr < R; ++rr) {
                         float sc = 1.0f;
-                        if constexpr (!X1) {  // scaled by the tile's maximum
-                            uint32_t mb = 0;
+                        if constexpr (!X1) {
+#if LIDAR_SA_E3_BOUND
+                            // scaled by the bound colsum(W2) 2^e2 + max|b2| (the lean kernel's rule): no
+                            // pass over the tile
+                            e3[rr] = bound_exp3(*reinterpret_cast<const X3Tail *>(Bias + C1 + C2 + C3), e2[rr]);
+#else
+                            uint32_t mb = 0;  // scaled by the tile's maximum
 #pragma unroll
                             for (int t = 0; t < T2; ++t)
 #pragma unroll
                                 for (int r = 0; r < 4; ++r) mb = max(mb, __float_as_uint(y2[rr][t][r]));  // ReLU outputs: non-negative bits
                             e3[rr] = lidar_h3::wave_exp(mb);
+#endif
                             sc = lidar_h3::scale_of(e3[rr]);
                         }
 #pragma unroll

@@ -60,7 +60,12 @@ PREFIXES = (
     ("sa_x3_lean_kernel<128, 128, 256, 64,", "sa2_group_mlp"),
     ("sa16_kernel<64, 64, 128, 32, true", "sa1_group_mlp"),
     ("sa16_kernel<128, 128, 256, 64, false", "sa2_group_mlp"),
-    ("dense_x3_kernel<0, false>", "dense_rows"),  # SA2's layer 1 (points, centres), dense1, dense2: by grid
+    ("dense_x3_kernel<0, false, false>", "dense_rows"),  # round 4: SA2's layer 1 (points, centres), by grid
+    ("dense_x3_kernel<1, false, false>", "sa3_dense1"),  # fp32 rows in, h3 planes out
+    ("dense_x3_kernel<1, false, true>", "sa3_dense2"),  # h3 planes in and out
+    ("dense_x3_kernel<2, false, true>", "sa3_dense3_pool"),  # h3 planes in, max-pool out
+    ("dense_x3_kernel<0, true, false>", "dense_x1"),
+    ("dense_x3_kernel<0, false>", "dense_rows"),  # round 4 before the planes: layer 1, dense1, dense2 by grid
     ("dense_x3_kernel<2, false>", "sa3_dense3_pool"),
     ("dense_x3_kernel<0, true>", "dense_x1"),  # the bf16 spec's per-point layer 1 (MSG)
     ("dense_x3s_kernel<0, true, false>", "sa2_layer1"),  # round-3 names (split planes)

@@ -8,15 +8,22 @@
 // voxel.hip runs one frame in one workgroup; here every pass is spread over (tiles x frames)
 // workgroups:
 //
-//   bbox (min, max) -> keys (u32) + indices              grid (chunks, frames), atomics per frame
+//   bbox (min, max)                                       grid (chunks, frames), atomics per frame
+//   keys (u32) + indices per 4096-element tile, with the tile's histogram of radix digit 0 (LDS)
+//          -> hist[frame][digit][tile]; a point outside every bin takes the key nx ny nz (one past the
+//          last voxel), so every frame's key bits follow from its grid alone
 //   LSD radix sort, 8-bit digits, only the passes a frame's key range needs (per-frame parity):
-//     hist    per 4096-element tile, LDS histogram   -> hist[frame][digit][tile]
-//     scan    per frame, digit-major tile-minor        (exclusive: the tile's base per digit)
-//     scatter per tile, stable: 1024-element sub-tiles ranked by wave ballots (8 per digit) and
-//             per-wave prefix counts in LDS, running per-digit offsets
+//     hist    (passes after the first) per 4096-element tile, LDS histogram
+//     scatter per tile, stable: the tile's base per digit from the frame's tile histograms (its own
+//             scan of them, frames of <= 32 tiles; a separate scan launch above), then 1024-element
+//             sub-tiles ranked by wave ballots (8 per digit) and per-wave prefix counts in LDS, running
+//             per-digit offsets
 //   runs      per tile: run starts counted, then written from the frame's earlier tiles' counts
 //             -> voxel id per point, run offsets, voxel count
 //   centroid  one thread per voxel walks its run (index order: the sort is stable)
+// 6 + 2 passes launches (round 3: 6 + 3 passes: the first histogram and every scan were launches of their own).
+// (Counting the next pass's histogram with global atomics inside the scatter, and the centroids inside the
+// runs kernel, were measured slower: 499 vs 238 us per 32-frame call.)
 //
 // Memory-side bytes per point: xyz read 3x (36 B: bbox, keys, centroids) + keys/indices (8 B written) + per radix pass
 // 24 B (two reads, one write of 8 B) + runs 12 B + centroid gathers 12 B; the algorithmic floor is
@@ -34,9 +41,10 @@ constexpr int TILE = 4096;   // radix tile (elements per scatter workgroup)
 constexpr int ST = 1024;     // scatter / runs workgroup threads
 constexpr int SW = ST / 64;  // waves per scatter workgroup
 
-// per-frame meta words: [0..2] / [3..5] monotone bits of the min / max point, [6] key bits, [7] unusable
-// grid, [8] voxel count, [9] some point lies outside every bin (its key kOutside needs all 32 bits sorted)
+// per-frame meta words: [0..2] / [3..5] monotone bits of the min / max point, [6] key bits (of the
+// outside key), [7] unusable grid, [8] voxel count, [10] end of the last voxel's run, [11] the outside key
 constexpr int MW = 16;
+constexpr int kFuseScanTiles = 32;  // frames of at most this many tiles: the scatter scans the histograms itself
 
 __device__ __forceinline__ uint32_t ord(float f)  // monotone float -> u32
 {
@@ -91,31 +99,40 @@ __device__ __forceinline__ lidar_vox::Grid frame_grid(const uint32_t *m, double 
     return lidar_vox::make_grid(lo, hi, voxel);
 }
 
-__global__ __launch_bounds__(VT) void vb_keys_kernel(const float *__restrict__ xyz, int64_t n, double voxel,
+// grid (ntiles, frames): keys and indices of one 4096-element tile and the tile's histogram of digit 0
+__global__ __launch_bounds__(ST) void vb_keys_kernel(const float *__restrict__ xyz, int64_t n, double voxel,
                                                      uint32_t *meta, uint32_t *__restrict__ key,
-                                                     uint32_t *__restrict__ idx)
+                                                     uint32_t *__restrict__ idx, uint32_t *__restrict__ hist,
+                                                     int ntiles)
 {
-    const int f = blockIdx.y;
+    const int f = blockIdx.y, t = blockIdx.x;
     const float *p = xyz + (int64_t)f * n * 3;
     uint32_t *m = meta + (int64_t)f * MW;
     const lidar_vox::Grid g = frame_grid(m, voxel);
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        m[10] = (uint32_t)n;  // end of the last voxel's run, unless points lie outside every bin (runs kernel)
+    const uint32_t okey = g.ok ? (uint32_t)g.keys : 0u;
+    const int bits = g.ok ? 32 - __clz((int)okey) : 0;  // okey = nx ny nz >= 1
+    if (t == 0 && threadIdx.x == 0) {
         m[7] = g.ok ? 0u : 1u;
-        const uint64_t top = g.ok ? g.keys - 1 : 0;
-        m[6] = top == 0 ? 0u : (uint32_t)(64 - __clzll((long long)top));  // bits of the largest key
+        m[6] = (uint32_t)bits;
+        m[11] = okey;
+        m[10] = (uint32_t)n;  // end of the last voxel's run, unless points lie outside every bin (runs kernel)
     }
     if (!g.ok) return;
+    __shared__ uint32_t h[256];
+    if (threadIdx.x < 256) h[threadIdx.x] = 0;
+    __syncthreads();
     uint32_t *k = key + (int64_t)f * n;
     uint32_t *v = idx + (int64_t)f * n;
-    bool outside = false;
-    for (int64_t i = (int64_t)blockIdx.x * VT + threadIdx.x; i < n; i += (int64_t)gridDim.x * VT) {
-        const uint32_t kk = lidar_vox::key(g, p[3 * i], p[3 * i + 1], p[3 * i + 2]);
-        outside |= kk == lidar_vox::kOutside;
+    const int64_t i0 = (int64_t)t * TILE, i1 = min<int64_t>(n, i0 + TILE);
+    for (int64_t i = i0 + threadIdx.x; i < i1; i += ST) {
+        uint32_t kk = lidar_vox::key(g, p[3 * i], p[3 * i + 1], p[3 * i + 2]);
+        kk = kk == lidar_vox::kOutside ? okey : kk;  // sorts after every voxel's key
         k[i] = kk;
         v[i] = (uint32_t)i;
+        atomicAdd(&h[kk & 255u], 1u);
     }
-    if (__ballot(outside) && (threadIdx.x & 63) == 0) atomicOr(m + 9, 1u);
+    __syncthreads();
+    if (threadIdx.x < 256) hist[((int64_t)f * 256 + threadIdx.x) * ntiles + t] = h[threadIdx.x];
 }
 
 // key bits of frame f, read after vb_keys_kernel (0 when the grid overflowed: nothing is sorted,
@@ -123,7 +140,7 @@ __global__ __launch_bounds__(VT) void vb_keys_kernel(const float *__restrict__ x
 __device__ __forceinline__ int frame_bits(const uint32_t *meta, int f)
 {
     const uint32_t *m = meta + (int64_t)f * MW;
-    return m[7] ? 0 : (m[9] ? 32 : (int)m[6]);
+    return m[7] ? 0 : (int)m[6];
 }
 
 __global__ __launch_bounds__(VT) void vb_hist_kernel(const uint32_t *__restrict__ kin, int64_t n, int shift,
@@ -177,6 +194,10 @@ __global__ __launch_bounds__(ST) void vb_scan_kernel(uint32_t *__restrict__ hist
     }
 }
 
+// FUSED: the tile's base per digit from the frame's raw tile histograms (its own scan: the digit's
+// count in the frame's earlier tiles plus every smaller digit's total); else hist holds vb_scan_kernel's
+// exclusive offsets
+template <bool FUSED>
 __global__ __launch_bounds__(ST) void vb_scatter_kernel(const uint32_t *__restrict__ kin, const uint32_t *__restrict__ vin,
                                                         uint32_t *__restrict__ kout, uint32_t *__restrict__ vout,
                                                         int64_t n, int shift, int ntiles, const uint32_t *meta,
@@ -186,9 +207,32 @@ __global__ __launch_bounds__(ST) void vb_scatter_kernel(const uint32_t *__restri
     if (frame_bits(meta, f) <= shift) return;
     __shared__ uint32_t off[256];      // running global offset per digit
     __shared__ uint32_t wcnt[SW][256]; // per-wave digit counts of the current sub-tile
+    __shared__ uint32_t wtot[4];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t *hf = hist + (int64_t)f * 256 * ntiles;
-    for (int d = tid; d < 256; d += ST) off[d] = hf[(int64_t)d * ntiles + t];
+    if constexpr (FUSED) {
+        uint32_t tot = 0, pre = 0;  // thread d < 256: digit d's frame total and its count before tile t
+        if (tid < 256)
+            for (int u = 0; u < ntiles; ++u) {
+                const uint32_t c = hf[(int64_t)tid * ntiles + u];
+                tot += c;
+                pre += u < t ? c : 0u;
+            }
+        uint32_t inc = tot;  // exclusive scan of the totals over the 256 digits (waves 0-3)
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t u = (uint32_t)__shfl_up((int)inc, o, 64);
+            if (lane >= o) inc += u;
+        }
+        if (tid < 256 && lane == 63) wtot[wave] = inc;
+        __syncthreads();
+        if (tid < 256) {
+            uint32_t base = inc - tot;
+            for (int w = 0; w < wave; ++w) base += wtot[w];
+            off[tid] = base + pre;
+        }
+    } else {
+        for (int d = tid; d < 256; d += ST) off[d] = hf[(int64_t)d * ntiles + t];
+    }
     const uint32_t *k = kin + (int64_t)f * n;
     const uint32_t *v = vin + (int64_t)f * n;
     uint32_t *ko = kout + (int64_t)f * n;
@@ -232,7 +276,7 @@ __device__ __forceinline__ void sorted_bufs(const uint32_t *m, int f, int64_t n,
                                             const uint32_t *v0, const uint32_t *k1, const uint32_t *v1,
                                             const uint32_t *&sk, const uint32_t *&si)
 {
-    const int passes = ((m[9] ? 32 : (int)m[6]) + 7) / 8;  // the sorted data sits in buffer (passes run) % 2
+    const int passes = ((int)m[6] + 7) / 8;  // the sorted data sits in buffer (passes run) % 2
     sk = (passes & 1 ? k1 : k0) + (int64_t)f * n;
     si = (passes & 1 ? v1 : v0) + (int64_t)f * n;
 }
@@ -250,9 +294,10 @@ __global__ __launch_bounds__(ST) void vb_runs_count_kernel(const uint32_t *__res
     __shared__ uint32_t ws[SW];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int64_t i0 = (int64_t)t * TILE, i1 = min<int64_t>(n, i0 + TILE);
+    const uint32_t okey = m[11];
     uint32_t c = 0;
     for (int64_t i = i0 + tid; i < i1; i += ST)
-        c += (sk[i] != lidar_vox::kOutside && (i == 0 || sk[i] != sk[i - 1])) ? 1u : 0u;
+        c += (sk[i] != okey && (i == 0 || sk[i] != sk[i - 1])) ? 1u : 0u;
     for (int o = 32; o >= 1; o >>= 1) c += (uint32_t)__shfl_xor((int)c, o, 64);
     if (lane == 0) ws[wave] = c;
     __syncthreads();
@@ -282,12 +327,13 @@ __global__ __launch_bounds__(ST) void vb_runs_write_kernel(const uint32_t *__res
     uint32_t *vs = vstart + (int64_t)f * (n + 1);
     __shared__ uint32_t ws[SW];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t okey = m[11];
     uint32_t base = 0;
     for (int u = 0; u < t; ++u) base += tilecnt[(int64_t)f * ntiles + u];
     const int64_t i0 = (int64_t)t * TILE, i1 = min<int64_t>(n, i0 + TILE);
     for (int64_t b0 = i0; b0 < i1; b0 += ST) {
         const int64_t i = b0 + tid;
-        const bool in = i < i1 && sk[i] != lidar_vox::kOutside;
+        const bool in = i < i1 && sk[i] != okey;
         const bool st = in && (i == 0 || sk[i] != sk[i - 1]);
         const uint64_t mk = __ballot(st);
         const uint32_t inw = (uint32_t)__popcll(mk & ((1ull << lane) - 1));
@@ -304,7 +350,7 @@ __global__ __launch_bounds__(ST) void vb_runs_write_kernel(const uint32_t *__res
             if (st) vs[r] = (uint32_t)i;
         } else if (i < i1) {
             vf[si[i]] = -1;  // outside every bin (sorted after the last voxel)
-            if (i == 0 || sk[i - 1] != lidar_vox::kOutside) m[10] = (uint32_t)i;  // the last run's end
+            if (i == 0 || sk[i - 1] != okey) m[10] = (uint32_t)i;  // the last run's end
         }
         base += tot;
         __syncthreads();
@@ -323,7 +369,7 @@ __global__ __launch_bounds__(VT) void vb_centroid_kernel(const float *__restrict
     const int f = blockIdx.y;
     const uint32_t *m = meta + (int64_t)f * MW;
     if (m[7]) return;
-    const int passes = ((m[9] ? 32 : (int)m[6]) + 7) / 8;  // the sorted indices sit in buffer (passes run) % 2
+    const int passes = ((int)m[6] + 7) / 8;  // the sorted indices sit in buffer (passes run) % 2
     const uint32_t *si = (passes & 1 ? v1 : v0) + (int64_t)f * n;
     const uint32_t *vs = vstart + (int64_t)f * (n + 1);
     const float *p = xyz + (int64_t)f * n * 3;
@@ -383,13 +429,21 @@ LIDAR_EXPORT int lidar_voxel_downsample_batch_f32(lidar_handle *h, const float *
     const dim3 sg(chunks, (unsigned)batch);
     hipLaunchKernelGGL(vb_init_kernel, dim3((unsigned)((batch + 255) / 256)), dim3(256), 0, s, meta, (int)batch);
     hipLaunchKernelGGL(vb_bbox_kernel, sg, dim3(VT), 0, s, xyz, n, meta);
-    hipLaunchKernelGGL(vb_keys_kernel, sg, dim3(VT), 0, s, xyz, n, voxel, meta, U(ok0), U(ov0));
-    uint32_t *kin = U(ok0), *vin = U(ov0), *kout = U(ok1), *vout = U(ov1);
     const dim3 tg((unsigned)ntiles, (unsigned)batch);
+    // keys + the histogram of digit 0
+    hipLaunchKernelGGL(vb_keys_kernel, tg, dim3(ST), 0, s, xyz, n, voxel, meta, U(ok0), U(ov0), hist, ntiles);
+    uint32_t *kin = U(ok0), *vin = U(ov0), *kout = U(ok1), *vout = U(ov1);
+    const bool fused = ntiles <= kFuseScanTiles;
     for (int shift = 0; shift < 32; shift += 8) {  // frames past their key bits skip (per-frame parity)
-        hipLaunchKernelGGL(vb_hist_kernel, tg, dim3(VT), 0, s, kin, n, shift, ntiles, meta, hist);
-        hipLaunchKernelGGL(vb_scan_kernel, dim3((unsigned)batch), dim3(ST), 0, s, hist, ntiles, shift, meta);
-        hipLaunchKernelGGL(vb_scatter_kernel, tg, dim3(ST), 0, s, kin, vin, kout, vout, n, shift, ntiles, meta, hist);
+        if (shift > 0) hipLaunchKernelGGL(vb_hist_kernel, tg, dim3(VT), 0, s, kin, n, shift, ntiles, meta, hist);
+        if (fused) {
+            hipLaunchKernelGGL(vb_scatter_kernel<true>, tg, dim3(ST), 0, s, kin, vin, kout, vout, n, shift, ntiles, meta,
+                               hist);
+        } else {
+            hipLaunchKernelGGL(vb_scan_kernel, dim3((unsigned)batch), dim3(ST), 0, s, hist, ntiles, shift, meta);
+            hipLaunchKernelGGL(vb_scatter_kernel<false>, tg, dim3(ST), 0, s, kin, vin, kout, vout, n, shift, ntiles,
+                               meta, hist);
+        }
         std::swap(kin, kout);
         std::swap(vin, vout);
     }

@@ -137,12 +137,6 @@ __device__ __forceinline__ float max_row_groups(float v)
 #ifndef LIDAR_SA_E3_BOUND
 #define LIDAR_SA_E3_BOUND 1
 #endif
-// LIDAR_SA1_E2_BOUND (A/B builds): an xyz level with its ball queries inside (BQ) scales layer 2's input
-// by the bound max_c (sum_q |W1[q][c]| r + |b1[c]|) whenever every offset of the tile lies within r
-// (a ball-query hit always does), instead of a wave maximum over the tile
-#ifndef LIDAR_SA1_E2_BOUND
-#define LIDAR_SA1_E2_BOUND 0
-#endif
 constexpr int kBqCap = LIDAR_BQ_CAP;  // candidates per window a fused wave ranks in LDS (more: index-order scan)
 template <int C1, int C2, int C3, int NS, int L1, int R, bool X1, bool BQ = false>
 __global__ __launch_bounds__(256, (BQ && !X1 && NS == 32) ? 5 : (R == 1 ? 3 : 2)) void sa_x3_kernel(const float *__restrict__ P, int64_t stride,
@@ -237,17 +231,6 @@ __global__ __launch_bounds__(256, (BQ && !X1 && NS == 32) ? 5 : (R == 1 ? 3 : 2)
                                         qhits[wave], &qidx[wave][0]);
     }
     __syncthreads();
-    constexpr bool E2B = XYZ && BQ && !X1 && LIDAR_SA1_E2_BOUND;
-    int eb1 = 0;  // E2B: layer 2's input exponent for tiles of true neighbours (|offset| <= r)
-    if constexpr (E2B) {
-        float mb1 = 0.0f;
-        for (int c = lane; c < C1; c += 64) {
-            const float *w = &w1_s[(c >> 4) * 64 + (c & 15)];
-            mb1 = fmaxf(mb1, (fabsf(w[0]) + fabsf(w[16]) + fabsf(w[32])) * r + fabsf(bias_s[c]));
-        }
-        const float bnd = __int_as_float(lidar::wave_max_i32_dpp(__float_as_int(mb1))) * (1.0f + 0x1p-10f);
-        eb1 = __builtin_amdgcn_readfirstlane(lidar_h3::exp_of_bits(__float_as_uint(bnd)));
-    }
     if constexpr (BQ)
         if (live && out_idx != nullptr)
             for (int i = lane; i < NS; i += 64) out_idx[unit * NS + i] = qidx[wave][i];
@@ -266,12 +249,10 @@ __global__ __launch_bounds__(256, (BQ && !X1 && NS == 32) ? 5 : (R == 1 ? 3 : 2)
         for (int rr = 0; rr < R; ++rr) {
             const int64_t k = BQ ? qidx[wave][(it * R + rr) * 16 + col] : idx[cc * NS + (it * R + rr) * 16 + col];
             f32x4 y1[T1];
-            bool far = true;  // E2B: some offset of the tile is not within r (or is NaN)
             if constexpr (XYZ) {
                 const float *pr = P + ((int64_t)b * n + k) * 3;
                 const float *ce = Q + cc * 3;
                 float x = q < 3 ? pr[q] - ce[q] : 0.0f;  // lane group q: dx, dy, dz, 0
-                if constexpr (E2B) far = __ballot(!(fabsf(x) <= r)) != 0;
                 if constexpr (X1) x = bf16r(x);  // the bf16 spec rounds the offsets (W1 is pre-rounded)
 #pragma unroll
                 for (int t = 0; t < T1; ++t) {
@@ -310,16 +291,12 @@ __global__ __launch_bounds__(256, (BQ && !X1 && NS == 32) ? 5 : (R == 1 ? 3 : 2)
             }
             float sc = 1.0f;
             if constexpr (!X1) {
-                if (E2B && !far) {  // wave-uniform
-                    e2[rr] = eb1;
-                } else {
-                    uint32_t mb = 0;
+                uint32_t mb = 0;
 #pragma unroll
-                    for (int t = 0; t < T1; ++t)
+                for (int t = 0; t < T1; ++t)
 #pragma unroll
-                        for (int r = 0; r < 4; ++r) mb = max(mb, __float_as_uint(y1[t][r]));  // ReLU outputs: non-negative bits
-                    e2[rr] = lidar_h3::wave_exp(mb);
-                }
+                    for (int r = 0; r < 4; ++r) mb = max(mb, __float_as_uint(y1[t][r]));  // ReLU outputs: non-negative bits
+                e2[rr] = lidar_h3::wave_exp(mb);
                 sc = lidar_h3::scale_of(e2[rr]);
             }
 #pragma unroll

@@ -323,6 +323,25 @@ def layer1_weights(layer, cfeat, to_dev):
     return {"w1": to_dev(w1p), "b1": to_dev(bp), "wq": to_dev(wq), "zero": to_dev(np.zeros(cp, np.float32))}
 
 
+def centre_layer1(new_xyz, branches, out=None, slot=0):
+    """Q = [c, 0-pad] W1_xyz' per centre of a feature level, every branch (the per-centre half of
+    layer1_per_point, h3 GEMM; rows B*M rounded up to 128) -> [Q per branch].  out: [(cpad (R, 16) zeroed
+    past the centres' rows, Q (R, cp))] per branch, preallocated."""
+    B, M, _ = new_xyz.shape
+    dev = new_xyz.device
+    h = nat.handle(dev.index, slot)
+    rq = (B * M + 127) // 128 * 128
+    res = []
+    for i, br in enumerate(branches):
+        pre = br["pre"]
+        cp = pre["w1"].shape[1]
+        cpad, q = out[i] if out is not None else (torch.zeros((rq, 16), dtype=torch.float32, device=dev), None)
+        cpad, q = cpad[:rq], (q[:rq] if q is not None else None)
+        nat.call("lidar_concat_xyz_pad_f32", h, nat.ptr(new_xyz), B * M, nat.ptr(cpad), 16, 0, nat.stream_ptr())
+        res.append(dense_x3s(cpad, pre["wq_x3"], pre["zero"], cp, relu=False, out=q, slot=slot))
+    return res
+
+
 def layer1_per_point(x_rows, xyz, cfeat, new_xyz, branches, x3=True):
     """Layer 1 of every branch of a level, per point instead of per grouped row.
 
@@ -338,19 +357,15 @@ def layer1_per_point(x_rows, xyz, cfeat, new_xyz, branches, x3=True):
     dev = xyz.device
     h = nat.handle(dev.index)
     nat.call("lidar_concat_xyz_pad_f32", h, nat.ptr(xyz), B * N, nat.ptr(x_rows), kp, cfeat, nat.stream_ptr())
+    if x3:
+        qs = centre_layer1(new_xyz, branches)
+        return [(dense_x3s(x_rows, br["pre"]["w1_x3"], br["pre"]["b1"], br["pre"]["w1"].shape[1], relu=False), q)
+                for br, q in zip(branches, qs)]
     rq = (B * M + 127) // 128 * 128
     cpad = torch.zeros((rq, 16), dtype=torch.float32, device=dev)
     nat.call("lidar_concat_xyz_pad_f32", h, nat.ptr(new_xyz), B * M, nat.ptr(cpad), 16, 0, nat.stream_ptr())
-    out = []
-    for br in branches:
-        pre = br["pre"]
-        cp = pre["w1"].shape[1]
-        if x3:
-            out.append((dense_x3s(x_rows, pre["w1_x3"], pre["b1"], cp, relu=False),
-                        dense_x3s(cpad, pre["wq_x3"], pre["zero"], cp, relu=False)))
-        else:
-            out.append((dense(x_rows, pre["w1"], pre["b1"], relu=False), dense(cpad, pre["wq"], pre["zero"], relu=False)))
-    return out
+    return [(dense(x_rows, br["pre"]["w1"], br["pre"]["b1"], relu=False),
+             dense(cpad, br["pre"]["wq"], br["pre"]["zero"], relu=False)) for br in branches]
 
 
 def pack_dense_x3(w, x1=False):
@@ -383,7 +398,7 @@ def dense_relu(x, w, b, pool_rows=0, out=None):
     return dense(x, w, b, True, pool_rows, out)
 
 
-def dense_x3s(a, wpack, b, cout, relu=True, pool_rows=0, out=None, x1=False):
+def dense_x3s(a, wpack, b, cout, relu=True, pool_rows=0, out=None, x1=False, slot=0):
     """a (rows, k) fp32 @ W + b on the dense GEMM of csrc/dense_x3s.hip (lidar_dense_x3f_f32; wpack =
     pack_dense_x3(W), h3 arithmetic; x1: pack_dense_x3(W, x1=True), the bf16 spec).  Returns fp32
     rows (rows, cout) or, with pool_rows, the fp32 max over runs of pool_rows rows (ReLU)."""
@@ -398,7 +413,7 @@ def dense_x3s(a, wpack, b, cout, relu=True, pool_rows=0, out=None, x1=False):
         if out is None:
             out = torch.empty((rows, cout), dtype=torch.float32, device=dev)
     _dev_check(a, wpack, b, out)
-    nat.call("lidar_dense_x3f_f32", nat.handle(dev.index), nat.ptr(a), lda, rows, lda, nat.ptr(wpack), nat.ptr(b),
+    nat.call("lidar_dense_x3f_f32", nat.handle(dev.index, slot), nat.ptr(a), lda, rows, lda, nat.ptr(wpack), nat.ptr(b),
              cout, mode | (4 if x1 else 0), 1 if relu else 0, pool_rows, nat.ptr(out), 0, out.shape[1],
              nat.stream_ptr())
     return out
@@ -767,7 +782,6 @@ class StreamingSSG:
             self.fz2 = [torch.empty(GB, dtype=torch.int32, device=dev) for _ in range(nslot)]
             self.gidx2 = [[torch.empty((GB, self.M2, br["ns"]), dtype=torch.int32, device=dev)
                            for br in lvl1["branches"]] for _ in range(nslot)]
-
         # setup-time workspace sizing of the side handles (FPS + ball queries), so no stage's
         # first call grows a workspace (lidar_reserve; growth retires the old block, no device sync)
         if reserve:

@@ -11,6 +11,8 @@ import json
 import sys
 
 LABELS = [("sa_x3_lean", "sa2_group_mlp"), ("sa_x3_kernel", "sa1_group_mlp"), ("dense_x3s_kernel<2", "sa3_dense3_pool"),
+          ("dense_x3_kernel<2", "sa3_dense3_pool"), ("dense_x3_kernel<1", "sa3_dense1_dense2"),
+          ("dense_x3_kernel<0", "sa2_layer1_points_and_centres"),
           ("dense_x3s_kernel<1", "sa3_dense1_dense2"), ("dense_x3s_kernel<0", "sa2_layer1_points_and_centres"),
           ("fps_bucket", "fps"), ("bq_bin", "bq_bin"), ("bq_grid", "sa2_ball_query")]
 
@@ -33,7 +35,7 @@ def main(prefix, out):
         if lab:
             agg[lab][r["Counter_Name"]] += float(r["Counter_Value"])
             disp[lab].add(r["Dispatch_Id"])
-    res = {"source": "rocprofv3 --kernel-trace --pmc, three SQ/GRBM passes (tools/gpu_pmc_alone.sh): two SSG "
+    res = {"source": "rocprofv3 --kernel-trace --pmc, three SQ/GRBM passes (tools/pmc_kern.sh TAG tools/ssg_alone.py): two SSG "
                      "forward() calls over one 128-frame group, nothing else on the chip", "kernels": {}}
     for lab, a in agg.items():
         wc = a["SQ_WAVE_CYCLES"] or 1.0

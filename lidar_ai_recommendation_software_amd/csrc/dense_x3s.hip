@@ -108,8 +108,12 @@ __device__ __forceinline__ int out_bound_exp(float colsum, float bmax, int e_in)
 
 // MODE 0 / 1 / 2 as in the header; X1: the bf16 spec (one ah*bh product, no scaling); PL: A as h3
 // planes (hi at a, lo at a + a_plane halves, row exponents a_exp)
+// Launch bounds (256, 2): the 64 KiB LDS stage already limits this kernel to 2 workgroups per
+// CU. At (256, 4) the compiler capped VGPRs at 64+64 AGPRs and copied the 64 accumulators
+// AGPR<->VGPR around every K-stage pair (128 extra VALU per iteration); at (256, 2) they stay
+// in VGPRs (102-126 total, 0 AGPRs, no copies).
 template <int MODE, bool X1, bool PL = false>
-__global__ __launch_bounds__(256, 4) void dense_x3_kernel(const float *__restrict__ af, int lda,
+__global__ __launch_bounds__(256, 2) void dense_x3_kernel(const float *__restrict__ af, int lda,
                                                           const uint16_t *__restrict__ wp, int ks,
                                                           const int32_t *__restrict__ wexp,
                                                           const float *__restrict__ bias, int relu_on,

@@ -4,10 +4,12 @@ design, so run with --no-verify): the operator runs once per distinct shape and 
 is returned afterwards, so the pipeline keeps every other launch and the skipped one's upper-bound
 gain shows in the line.
 
-  python tools/skip_probe.py {none|l1|dense1|l1+dense1} [bench.py args ...]
+  python tools/skip_probe.py {none|l1|dense1|fps|l1+dense1|...} [bench.py args ...]
 
   l1      SA2's per-point layer 1 (layer1_per_point: 2 xyz-pad copies + the P and Q GEMMs)
   dense1  group_all's first dense layer
+  fps     SA1's FPS on the side streams (runs once per output buffer, which keeps its samples): prices
+          what the FPS's presence costs the main chain
 """
 import os
 import sys
@@ -49,6 +51,19 @@ def main():
                 return cache[key]
             return real(a, wpack, b, cout, *r, **k)
         pn.dense_x3s = dense_x3s
+    if "fps" in skip:
+        real_fps = pn.farthest_point_sample
+        done = {}
+
+        def fps(xyz, npoint, *a, **k):
+            oi = k.get("out_idx")
+            if oi is None or k.get("prefix_ok") is not None:  # only SA1's side-stream call is skipped
+                return real_fps(xyz, npoint, *a, **k)
+            key = (oi.data_ptr(), tuple(oi.shape))
+            if key not in done:
+                done[key] = real_fps(xyz, npoint, *a, **k)
+            return done[key]
+        pn.farthest_point_sample = fps
     sys.argv = [sys.argv[0]] + sys.argv[2:]
     bench.main()
 

@@ -83,6 +83,33 @@ def ssg_kernel_work(n):
     }
 
 
+def stack_mfma_work(cfg, n):
+    """Algorithmic MFMA work PER FRAME of every MLP kernel of a PointNet++ stack (`pointnet2` config,
+    n points), under the kernel names the backbone's timers use: level 1's grouped branches
+    (sa1[_b<i>]_group_mlp, xyz rows), level 2's per-point layer 1 (sa2_layer1_points: N/16 rows of [f, x]
+    and N/64 centre rows of c, every branch) and its grouped layers 2-3, group_all's three GEMMs."""
+    work = {}
+    m = [n // lv["npoint_div"] for lv in cfg["levels"] if not lv.get("group_all")]
+    cin = 0
+    for li, lv in enumerate(cfg["levels"]):
+        if lv.get("group_all"):
+            widths = [cin + 3] + lv["mlps"][0]
+            for j in range(3):
+                work[f"sa{li + 1}_dense{j + 1}" + ("_pool" if j == 2 else "")] = mlp_flops(m[-1], widths[j:j + 2])
+            break
+        many = len(lv["mlps"]) > 1
+        for b, (ns, mlp) in enumerate(zip(lv["nsamples"], lv["mlps"])):
+            tag = f"sa{li + 1}" + (f"_b{b}" if many else "")
+            if li == 0:
+                work[f"{tag}_group_mlp"] = mlp_flops(m[0] * ns, [3] + mlp)
+            else:
+                work[f"sa{li + 1}_layer1_points"] = (work.get(f"sa{li + 1}_layer1_points", 0)
+                                                     + 2 * m[li - 1] * (cin + 3) * mlp[0] + 2 * m[li] * 3 * mlp[0])
+                work[f"{tag}_group_mlp"] = mlp_flops(m[li] * ns, mlp)
+        cin = sum(mlp[-1] for mlp in lv["mlps"])
+    return work
+
+
 def pick_group(steps, want):
     """Batches per FPS launch: the steady-state window must hold whole groups (every launch
     inside it covers the same number of frames), so G divides K; `want` first, then 3, 4, 5, 2."""
@@ -160,6 +187,15 @@ def compact_line(rec, detail_path=None):
     line["cpu_baseline"] = None if cb is None else {
         "value": cb["value"], "unit": cb["unit"], "cores": cb["cores"], "kind": cb["kind"], "sample": cb["sample"][:200]}
     line["speedup_vs_cpu"] = rec.get("speedup_vs_cpu")
+    if rec.get("arithmetic_short"):
+        line["arithmetic"] = rec["arithmetic_short"]
+    bq = (rec.get("roofline_all") or {}).get("sa2_ball_query")
+    if bq:
+        # north_star asks >= 50 % of HBM on ball_query; the query is a chain of dependent loads
+        # (latency-bound), so the target is reported as unmet by design
+        line["ball_query_hbm"] = {"kernel": "sa2_ball_query", "frac_compulsory": bq["frac"],
+                                  "frac_measured": (bq.get("measured_gbs") or 0) / HBM_PEAK_GBS or None,
+                                  "target": 0.5, "met": False, "why": "latency-bound by design"}
     if rec.get("precision") is not None:
         line["precision"] = rec["precision"]
     d = rec.get("distributed") or {}
@@ -182,6 +218,10 @@ def compact_line(rec, detail_path=None):
         legs["ssg_native_fp32_mfma"] = rec["fp32_mfma_kernels"]["value"]
     for k, v in (rec.get("other_configs") or {}).items():
         legs[k] = v["M_points_per_s"]
+        if v.get("roofline"):
+            r = v["roofline"]
+            optional.insert(0, (f"roofline_{k.split('_')[0]}", {x: r[x] for x in (
+                "kernel", "bound", "achieved", "peak", "unit", "frac", "traffic", "stack_mfma_frac") if x in r}))
     dp_ = rec.get("density_path")
     if dp_:
         legs["density_path_32"] = dp_["value"]
@@ -613,6 +653,8 @@ def main():
                          "nearest of 3, 4, 5, 2 that does")
     ap.add_argument("--fps-threads", type=int, default=512, choices=[512, 1024],
                     help="SA1 FPS workgroup size in the pipeline (512: half the CU footprint beside the MLPs)")
+    ap.add_argument("--fps-lazy", type=int, default=0,
+                    help="1: SA1 FPS on the lazy-refresh kernel (LIDAR_FPS_LAZY; identical results)")
     ap.add_argument("--x3", type=int, default=1,
                     help="1: MLPs on the split-bf16 (x3) kernels, fp32 arithmetic within the 1e-4 contract; "
                          "0: the native fp32-MFMA kernels")
@@ -681,7 +723,8 @@ def main():
         refs = None if args.no_verify else [bb.forward(x)[0] for x in xs]
         ready = torch.cuda.Event()  # the inputs exist: the feed's FPS launches wait only for their slots
         ready.record()
-        pipe = pn.StreamingSSG(bb, B, N, depth=depth, fps_group=G, fps_threads=args.fps_threads, ramp=False,
+        pipe = pn.StreamingSSG(bb, B, N, depth=depth, fps_group=G, fps_threads=args.fps_threads,
+                               fps_lazy=bool(args.fps_lazy), ramp=False,
                                slots=args.slots or None, bq=args.bq,
                                l2_side=bool(args.l2_side))
         feed = pipe.feed()
@@ -773,6 +816,21 @@ def main():
                            "ms_per_step": el2 / st2 * 1e3, "frames_per_gpu": b2, "points_per_frame": n2,
                            "dtype": dtype, "batches_per_group": g2,
                            "kernel_ms_per_launch": {k: t / c for k, (c, f, t) in t2.items()}}
+            mw = stack_mfma_work(cfg, n2)
+            mk = {k: v for k, v in t2.items() if k in mw}
+            if mk:
+                # the leg's dominant MFMA kernel (most device time), priced on the dense peak of its
+                # arithmetic: bf16 (X1 kernels, one bf16 product per MFMA) or h3 (fp32 contract)
+                dk = max(mk, key=lambda k: mk[k][2])
+                c, f, ms = mk[dk]
+                peak = BF16_MFMA_PEAK_TFLOPS if dtype == "bf16" else X3_PEAK_TFLOPS
+                ach = mw[dk] * f / (ms / 1e3) / 1e12
+                extras[key]["roofline"] = {
+                    "kernel": dk, "bound": "mfma", "achieved": ach, "peak": peak, "unit": "TFLOP/s", "frac": ach / peak,
+                    "traffic": None, "work_per_launch": mw[dk] * f / c, "avg_launch_ms": ms / c, "launches": c,
+                    "frames": f, "peak_basis": "bf16 MFMA dense peak" if dtype == "bf16" else "bf16 dense peak / 3 (h3)",
+                    "stack_mfma_frac": sum(mw[k] * v[1] for k, v in mk.items()) / (sum(v[2] for v in mk.values()) / 1e3)
+                                       / 1e12 / peak}
 
     density = variant = voxel = host = None
     if not args.no_density:
@@ -871,6 +929,8 @@ def main():
                            "layer-1 xyz terms on fp32 MFMA; features within 1e-4 pure relative of the fp32 oracle on "
                            "every element >= 1e-2 RMS (tests/test_gpu_tier_n.py; `precision` below)")
                           if args.x3 else "fp32 MFMA (v_mfma_f32_*_f32)",
+            "arithmetic_short": ("h3: fp32 as fp16 hi+lo on fp16 MFMA (3 products), fp32 accumulate; "
+                                 "<=1e-4 rel on every element >=1e-2 RMS" if args.x3 else "fp32 MFMA"),
             "precision": None,
             "data": "synthetic: uniform [-1,1]^3 float32 frames (seeded per rank, %d distinct batches cycled), "
                     "random-init SSG weights" % max(1, args.rotate),
@@ -890,7 +950,8 @@ def main():
             "pipeline": {"executor": "pointnet2.StreamingSSG feed (steady state: the window pushes and completes "
                                      "exactly `steps` batches; pipeline fill and drain outside it)",
                          "side_streams": args.depth, "batches_per_group": G, "frames_per_launch": G * B,
-                         "fps_threads": args.fps_threads, "sa1_ball_queries": args.bq, **chains},
+                         "fps_threads": args.fps_threads, "fps_lazy": bool(args.fps_lazy),
+                         "sa1_ball_queries": args.bq, **chains},
             "fp32_mfma_kernels": fp32_mfma,
             "other_configs": extras,
             "density_path": density,

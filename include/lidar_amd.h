@@ -52,7 +52,7 @@ int lidar_reserve(lidar_handle *h, uint64_t bytes);
 int lidar_trim(lidar_handle *h, uint64_t *freed);
 
 const char *lidar_last_error(void);
-int lidar_version(void); /* 3 (what changed per version) */
+int lidar_version(void); /* 4 (what changed per version) */
 
 /* Per-phase timing of a handle's launches (bench.py's in-window kernel durations): with
  * lidar_profile(h, 1) every kernel phase issued on h is bracketed by two HIP events on its
@@ -84,7 +84,10 @@ int lidar_fps_f32(lidar_handle *h, const float *xyz, int64_t batch, int64_t n, i
                   void *stream);
 /* the same with an explicit workgroup size per frame: threads 0 (default, 1024), 1024 or 512.
  * 512 takes ~25 % longer per step and half the CU footprint (throughput pipelines that run
- * other kernels beside FPS).  Identical results. */
+ * other kernels beside FPS).  threads | LIDAR_FPS_LAZY (ABI v4): lazy bucket refresh — a bucket
+ * hit by a sample defers it in a pending list until its key could reach the frame maximum
+ * (DESIGN.md §4.3): ~2.3x less memory traffic, ~20 % longer steps.  Identical results. */
+#define LIDAR_FPS_LAZY 0x10000
 int lidar_fps_ex_f32(lidar_handle *h, const float *xyz, int64_t batch, int64_t n, int64_t npoint,
                      int32_t *idx, float *new_xyz, int32_t *first_zero, const int32_t *prefix_ok,
                      int32_t threads, void *stream);

@@ -275,6 +275,13 @@ __global__ __launch_bounds__(256, 2) void dense_x3_kernel(const float *__restric
             compute(1);
         }
     }
+    // an image of the other kind (h3 vs bf16) is never reinterpreted: NaN outputs instead
+    if (wexp[1] != (X1 ? lidar_h3::kTagX1 : lidar_h3::kTagH3)) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[j][r] = __builtin_nanf("");
+    }
     // unscaled by 2^-(s_a + s_w) per row: s_a = 14 - E, s_w from the packed image (X1: none); lane
     // (col, h) holds row row0 + 32 wave + col, channels tn 128 + 32 j + 8 g + 4 h + t (tile j,
     // register 4 g + t)

@@ -16,6 +16,11 @@
 // The scale keeps the group's maximum below 2^14 (fp16 holds up to 65504), so no value can
 // overflow; elements below 2^-14 of the maximum keep an absolute precision of 2^-38 of it.  A NaN
 // or inf sets its own group's scale (its fp32 products would be NaN / inf anyway).
+//
+// Non-finite operands: an inf splits into hi = inf, lo = inf - inf = NaN, and a 0 piece times an
+// inf one is NaN, so every output an inf or NaN operand reaches is NaN in h3 where fp32 would give
+// +-inf or NaN: non-finite outputs stay non-finite (tests/test_gpu_tier_n.py::test_dense_x3s_nonfinite),
+// only the class (inf vs NaN) may differ.  Finite rows are unaffected (scaling groups are per row / tile).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -28,6 +33,10 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// image-kind tags in the second int32 of a dense weight image's tail (x3_pack.hip): the GEMM
+// checks that the image matches its mode and writes NaN outputs otherwise (never a silent mix-up)
+constexpr int32_t kTagH3 = 0x33484d47;  // "GMH3": fp16 hi / lo of W 2^s, s in tail[0]
+constexpr int32_t kTagX1 = 0x31584d47;  // "GMX1": bf16(W) for the bf16 spec
 constexpr int kEmin = -100;  // exponent floor: groups whose maximum is 0 or below 2^-100
 constexpr int kEmax = 128;   // inf / NaN maxima (their products are inf / NaN anyway)
 

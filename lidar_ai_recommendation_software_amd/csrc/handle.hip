@@ -52,7 +52,7 @@ static void drop_records(Prof *p)
 
 }  // namespace lidar
 
-LIDAR_EXPORT int lidar_version(void) { return 3; }
+LIDAR_EXPORT int lidar_version(void) { return 4; }
 
 LIDAR_EXPORT const char *lidar_last_error(void) { return lidar::g_err.c_str(); }
 

@@ -4,7 +4,8 @@
 // two 2^s (max |W| 2^s < 2^14) and split ONCE (at backbone construction) into fp16 hi / lo MFMA B
 // fragments of v_mfma_f32_32x32x16_f16: per 32-column tile, 16-deep k-step and hi / lo half, 64
 // lanes x 8 fp16 — one contiguous KiB that a wave's LDS-DMA moves whole.  K is padded to whole
-// 32-deep stages with zero weights.  The image ends in a 256-byte tail whose first int32 is s.
+// 32-deep stages with zero weights.  The image ends in a 256-byte tail whose first int32 is s and
+// whose second is the image kind (h3.hpp kTagH3 / kTagX1, checked by the GEMM).
 // bf16 image (X1, the bf16 spec): the same fragment order, hi = bf16(w) (lo = bf16(w - hi), not
 // read by the X1 GEMM), no scaling.
 #include "h3.hpp"
@@ -37,10 +38,11 @@ __global__ __launch_bounds__(1024) void dense_absmax_kernel(const float *__restr
 // ((((t * KS + s) * 2 + half) * 64 + lane) * 8 + j), lane = 32 * ((kk % 16) / 8) + n % 32, j = kk % 8
 template <bool H3>
 __global__ void dense_pack_kernel(const float *__restrict__ w, int k, int cout, int ks, uint16_t *__restrict__ packed,
-                                  const int32_t *__restrict__ tail)
+                                  int32_t *__restrict__ tail)
 {
     const int64_t total = (int64_t)(cout / 32) * ks * 64;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) tail[1] = H3 ? lidar_h3::kTagH3 : lidar_h3::kTagX1;
     if (i >= total) return;
     const int lane = (int)(i % 64), s = (int)((i / 64) % ks), t = (int)(i / 64 / ks);
     const int n = 32 * t + (lane & 31);

@@ -89,9 +89,15 @@ def _dev_check(*ts):
             raise ValueError("liblidar_amd operators take contiguous CUDA tensors")
 
 
+FPS_LAZY = 0x10000  # include/lidar_amd.h LIDAR_FPS_LAZY
+
+
 def farthest_point_sample(xyz, npoint, return_xyz=False, first_zero=None, prefix_ok=None, slot=0,
-                          out_idx=None, out_xyz=None, threads=0):
+                          out_idx=None, out_xyz=None, threads=0, lazy=False):
     """xyz (B, N, 3) float32 CUDA -> idx (B, npoint) int32 [, new_xyz (B, npoint, 3)].
+
+    threads: workgroup size per frame (0 = 1024, 512); lazy: the lazy-refresh kernel (same results,
+    less memory traffic, longer steps).  n <= 262144 points per frame.
 
     first_zero: optional (B,) int32 output — first step whose winning distance was 0.
     prefix_ok: optional (B,) int32 — the parent run's first_zero when xyz is the parent's
@@ -106,8 +112,8 @@ def farthest_point_sample(xyz, npoint, return_xyz=False, first_zero=None, prefix
         new_xyz = out_xyz if out_xyz is not None else torch.empty((B, npoint, 3), dtype=torch.float32,
                                                                   device=xyz.device)
     nat.call("lidar_fps_ex_f32", nat.handle(xyz.device.index, slot), nat.ptr(xyz), B, N, npoint,
-             nat.ptr(idx), nat.ptr(new_xyz), nat.ptr(first_zero), nat.ptr(prefix_ok), int(threads),
-             nat.stream_ptr())
+             nat.ptr(idx), nat.ptr(new_xyz), nat.ptr(first_zero), nat.ptr(prefix_ok),
+             int(threads) | (FPS_LAZY if lazy else 0), nat.stream_ptr())
     return (idx, new_xyz) if return_xyz else idx
 
 
@@ -435,12 +441,25 @@ def dense_h3p(a, a_exp, wpack, b, cout, mode, bounds=(0.0, 0.0), relu=True, pool
     layer's A; 2 -> ReLU + max over runs of pool_rows rows (rows / pool_rows, cout) fp32.  bounds: the
     layer's h3_bounds(W, b) (mode 1)."""
     dev = a.device
+    # the two operand forms are told apart only by a_exp: check that the tensors match the form, so a
+    # mismatch raises instead of being reinterpreted by the kernel
     if a_exp is None:
+        if a.dtype != torch.float32 or a.dim() != 2:
+            raise ValueError(f"dense_h3p: fp32 rows (rows, k) expected without a_exp, got {a.dtype} {tuple(a.shape)}")
         rows, k = a.shape
-        lda = k
     else:
+        if a.dtype != torch.float16 or a.dim() != 3 or a.shape[0] != 2:
+            raise ValueError(f"dense_h3p: h3 planes (2, rows, k) float16 expected with a_exp, got {a.dtype} "
+                             f"{tuple(a.shape)}")
         _, rows, k = a.shape
-        lda = k
+        if a_exp.dtype != torch.int32 or tuple(a_exp.shape) != (rows,):
+            raise ValueError(f"dense_h3p: a_exp must be int32 of shape ({rows},), got {a_exp.dtype} "
+                             f"{tuple(a_exp.shape)}")
+    lda = k
+    if mode not in (0, 1, 2):
+        raise ValueError(f"dense_h3p: mode must be 0, 1 or 2, got {mode}")
+    if mode == 2 and (pool_rows <= 0 or rows % pool_rows):
+        raise ValueError(f"dense_h3p: pool_rows ({pool_rows}) must divide rows ({rows})")
     if mode == 2:
         out = torch.zeros((rows // pool_rows, cout), dtype=torch.float32, device=dev) if out is None else out
         oexp = None
@@ -732,7 +751,8 @@ class StreamingSSG:
     state of a LiDAR stream) and ``flush()`` drains it.
     """
 
-    def __init__(self, backbone, batch, n, depth=1, fps_group=1, fps_threads=0, side_priority=0, ramp=True,
+    def __init__(self, backbone, batch, n, depth=1, fps_group=1, fps_threads=0, fps_lazy=False, side_priority=0,
+                 ramp=True,
                  reserve=True, keep_levels=False, slots=None, bq="bin", l2_side=False):
         """fps_threads: SA1 FPS workgroup size (0 = 1024; 512: half the CU footprint beside the
         MLPs).  ramp: in run(), the first groups hold 1, 2, ... batches (a shorter pipeline fill).
@@ -749,6 +769,7 @@ class StreamingSSG:
         self.B, self.N, self.depth, self.G = batch, n, depth, max(1, int(fps_group))
         self.ramp = bool(ramp)
         self.fps_threads = int(fps_threads)
+        self.fps_lazy = bool(fps_lazy)  # SA1 FPS on the lazy-refresh kernel (same results)
         self.keep = bool(keep_levels)
         if bq not in ("side", "bin", "main"):
             raise ValueError("StreamingSSG: bq must be 'side', 'bin' or 'main'")
@@ -815,7 +836,8 @@ class StreamingSSG:
             for xj in xs:  # read on this stream: keep the caller's buffers alive until then
                 xj.record_stream(fs)
             _call(t, "sa1_fps", g, farthest_point_sample, x, self.M1, return_xyz=True, first_zero=self.fz[slot][:g],
-                  slot=hs, out_idx=self.idx[slot][:g], out_xyz=self.cxyz[slot][:g], threads=self.fps_threads)
+                  slot=hs, out_idx=self.idx[slot][:g], out_xyz=self.cxyz[slot][:g], threads=self.fps_threads,
+                  lazy=self.fps_lazy)
             lvl0 = self.bb.levels[0]
             for bi_, br in enumerate(lvl0["branches"]):
                 tag = "sa1" + (f"_b{bi_}" if len(lvl0["branches"]) > 1 else "")

@@ -30,6 +30,12 @@ def _with_ranks(rec, world):
                           "ranks": [{"rank": r, "device": r, "frames": 640, "ms": 32.948751933872 + r / 7}
                                     for r in range(world)]}
     stats = {"max_rel": 3.1415926e-05, "n_rel": 131000, "n": 131072, "max_tol_ratio": 0.123456789}
+    rec["arithmetic_short"] = ("h3: fp32 as fp16 hi+lo on fp16 MFMA (3 products), fp32 accumulate; "
+                               "<=1e-4 rel on every element >=1e-2 RMS")
+    msg = rec.setdefault("other_configs", {}).setdefault("configs[4]_msg_131k_bf16", {"M_points_per_s": 479.3})
+    msg["roofline"] = {"kernel": "sa1_b2_group_mlp", "bound": "mfma", "achieved": 543.0, "peak": 2500.0,
+                       "unit": "TFLOP/s", "frac": 0.2172, "traffic": None, "stack_mfma_frac": 0.19,
+                       "work_per_launch": 3.75e12, "avg_launch_ms": 6.9, "launches": 6, "frames": 576}
     rec["precision"] = {"contract": "max |got-want|/|want| over |want| >= 1e-2 RMS, and max err/(1e-4|want| + "
                                     "1e-4 RMS)", "frame": "batch 0 frame 0", "fps_exact": True,
                         "level1": stats, "level2": stats, "global": stats}
@@ -54,8 +60,15 @@ def test_compact_line_fits_and_keeps_the_contract(world):
     assert d["cpu_baseline"]["value"] > 0 and d["cpu_baseline"]["cores"] >= 1 and d["cpu_baseline"]["kind"] == "port"
     assert d["distributed"]["world_size"] == world == len(d["distributed"]["ranks"])
     assert d["precision"]["global"]["max_rel"] == pytest.approx(3.142e-05)
+    # the line says what "f32" means, where ball_query stands against north_star's HBM target, and
+    # prices the configs[4] MSG leg's dominant kernel on the bf16 peak
+    assert d["arithmetic"].startswith("h3: fp32 as fp16 hi+lo")
+    bq = d["ball_query_hbm"]
+    assert bq["target"] == 0.5 and bq["met"] is False and 0 < bq["frac_compulsory"] < 0.5
     if world <= 8:  # the optional parts survive at the driver's world sizes
         assert "legs_M_points_per_s" in d and "kernels" in d and d["detail"] == "gpurun_out/bench_detail.json"
+        r = d["roofline_configs[4]"]
+        assert r["kernel"] == "sa1_b2_group_mlp" and r["peak"] == 2500.0 and r["frac"] == pytest.approx(0.2172)
 
 
 def test_compact_line_drops_optional_parts_last_first():

@@ -121,15 +121,17 @@ def frames_for(kind, b, n, seed):
     ("grid", 1, 4096, 4096),
 ])
 @pytest.mark.parametrize("threads", [0, 512])
-def test_fps_bit_exact(cuda, kind, b, n, m, threads):
-    """threads 0 = the default 1 024-thread kernel, 512 = 8 waves per frame; bit-exact indices and
-    coordinates against the C oracle (incl. far-offset, zero-width, non-finite and lattice frames)."""
+@pytest.mark.parametrize("lazy", [False, True])
+def test_fps_bit_exact(cuda, kind, b, n, m, threads, lazy):
+    """threads 0 = the default 1 024-thread kernel, 512 = 8 waves per frame; lazy = the lazy-refresh
+    kernel; bit-exact indices and coordinates against the C oracle (incl. far-offset, zero-width,
+    non-finite and lattice frames; m up to n, so pending lists overflow and ring slots expire)."""
     x = frames_for(kind, b, n, 11)
     if threads and (n + 63) // 64 > 8 * threads:  # 8 buckets per lane at most
         with pytest.raises(LidarError, match="too many buckets"):
-            pn.farthest_point_sample(torch.from_numpy(x).to(cuda), m, threads=threads)
+            pn.farthest_point_sample(torch.from_numpy(x).to(cuda), m, threads=threads, lazy=lazy)
         return
-    idx, nx = pn.farthest_point_sample(torch.from_numpy(x).to(cuda), m, return_xyz=True, threads=threads)
+    idx, nx = pn.farthest_point_sample(torch.from_numpy(x).to(cuda), m, return_xyz=True, threads=threads, lazy=lazy)
     want = tier_n.fps(x, m)
     got = idx.cpu().numpy()
     assert np.array_equal(got, want), f"{(got != want).sum()} indices differ, first {np.argwhere(got != want)[:3]}"
@@ -417,6 +419,63 @@ def test_dense_x3s(cuda, rows, k, cout, pool):
         ex = np.maximum(exact, 0).reshape(rows // pool, pool, cout)
         bd = bound.reshape(rows // pool, pool, cout).max(axis=1)
         assert np.all(np.abs(got - ex.max(axis=1)) <= bd), "dense h3 pooled"
+
+
+def test_dense_x3s_nonfinite(cuda):
+    """csrc/h3.hpp's non-finite rule: a row holding inf / NaN gives non-finite outputs wherever the fp32
+    product is non-finite (NaN in h3 where fp32 may give +-inf), and the finite rows are untouched."""
+    rng = np.random.default_rng(9)
+    rows, k, cout = 256, 64, 128
+    x = rng.standard_normal((rows, k)).astype(np.float32)
+    w = (rng.standard_normal((k, cout)) / 8).astype(np.float32)
+    b = np.zeros(cout, np.float32)
+    x[3, 7] = np.inf
+    x[40, 0] = -np.inf
+    x[77, 63] = np.nan
+    T = lambda a: torch.from_numpy(a).to(cuda)
+    got = pn.dense_x3s(T(x), pn.pack_dense_x3(T(w)), T(b), cout, relu=False).cpu().numpy()
+    with np.errstate(invalid="ignore", over="ignore"):
+        want = x.astype(np.float64) @ w.astype(np.float64)
+    bad = np.zeros(rows, bool)
+    bad[[3, 40, 77]] = True
+    assert np.all(~np.isfinite(got[~np.isfinite(want)])), "a non-finite fp32 output came out finite"
+    assert np.all(~np.isfinite(got[bad])), "rows with a non-finite operand must be non-finite"
+    exact, bound = h3_gemm_bound(x[~bad], w, b)
+    assert np.all(np.abs(got[~bad] - exact) <= bound), "finite rows disturbed by a non-finite row"
+
+
+def test_dense_image_kind_checked(cuda):
+    """An image of the other kind (h3 vs bf16 spec) is refused by the GEMM: NaN outputs, never a
+    silent reinterpretation (the kind tag in the image tail, x3_pack.hip)."""
+    rng = np.random.default_rng(10)
+    x = rng.standard_normal((256, 32)).astype(np.float32)
+    w = (rng.standard_normal((32, 128)) / 6).astype(np.float32)
+    b = np.zeros(128, np.float32)
+    T = lambda a: torch.from_numpy(a).to(cuda)
+    h3img, x1img = pn.pack_dense_x3(T(w)), pn.pack_dense_x3(T(w), x1=True)
+    assert np.all(np.isfinite(pn.dense_x3s(T(x), h3img, T(b), 128, relu=False).cpu().numpy()))
+    assert np.all(np.isfinite(pn.dense_x3s(T(x), x1img, T(b), 128, relu=False, x1=True).cpu().numpy()))
+    assert np.all(np.isnan(pn.dense_x3s(T(x), x1img, T(b), 128, relu=False).cpu().numpy()))
+    assert np.all(np.isnan(pn.dense_x3s(T(x), h3img, T(b), 128, relu=False, x1=True).cpu().numpy()))
+    assert np.all(np.isnan(pn.dense_x3s(T(x), x1img, T(b), 128, pool_rows=128).cpu().numpy()))
+
+
+def test_dense_h3p_rejects_mismatched_operands(cuda):
+    """dense_h3p tells fp32 rows from h3 planes by a_exp only: a mismatch raises."""
+    w = torch.zeros((32, 128), device=cuda)
+    b = torch.zeros(128, device=cuda)
+    wp = pn.pack_dense_x3(w)
+    rows = torch.zeros((128, 32), device=cuda)
+    planes = torch.zeros((2, 128, 32), dtype=torch.float16, device=cuda)
+    e = torch.zeros(128, dtype=torch.int32, device=cuda)
+    with pytest.raises(ValueError):
+        pn.dense_h3p(rows, e, wp, b, 128, 0)
+    with pytest.raises(ValueError):
+        pn.dense_h3p(planes, None, wp, b, 128, 0)
+    with pytest.raises(ValueError):
+        pn.dense_h3p(planes, e[:64], wp, b, 128, 0)
+    with pytest.raises(ValueError):
+        pn.dense_h3p(rows, None, wp, b, 128, 2, pool_rows=48)
 
 
 def test_dense_x3_pack_image(cuda):

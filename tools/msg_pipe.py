@@ -1,6 +1,6 @@
 """configs[4] (MSG, bf16 spec, 131 072-point frames, 32 per step) through StreamingSSG at several
 (depth, group) settings: wall ms per 32-frame batch in the steady state, timed as bench.py does (the window
-starts and ends with `depth` groups in flight; its extras leg uses depth 3 and G = pick_group(steps, 3)).  usage: python tools/msg_pipe.py [steps]"""
+starts and ends with `depth` groups in flight; its extras leg uses depth 3 and G = pick_group(steps, 3)).  usage: python tools/msg_pipe.py [steps [lazy [depth,G ...]]]"""
 import os
 import sys
 import time
@@ -12,14 +12,16 @@ from lidar_ai_recommendation_software_amd import pointnet2 as pn  # noqa: E402
 from lidar_ai_recommendation_software_amd.synthetic import unit_frames  # noqa: E402
 
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 30
+lazy = len(sys.argv) > 2 and sys.argv[2] == '1'
+settings = [tuple(int(v) for v in a.split(',')) for a in sys.argv[3:]] or [(3, 3), (3, 2), (4, 2), (2, 3), (4, 3), (3, 5), (2, 5)]
 dev = torch.device("cuda:0")
 B, N = 32, 131072
 bb = pn.PointNet2Backbone(pn.MSG, device=dev, seed=0, dtype="bf16")
 xs = [torch.from_numpy(unit_frames(B, N, seed=s)).to(dev) for s in range(4)]
 ready = torch.cuda.Event()
 ready.record()
-for depth, G in [(3, 3), (3, 2), (4, 2), (2, 3), (4, 3), (3, 5), (2, 5)]:
-    pipe = pn.StreamingSSG(bb, B, N, depth=depth, fps_group=G, fps_threads=512, ramp=False, bq="bin", l2_side=True)
+for depth, G in settings:
+    pipe = pn.StreamingSSG(bb, B, N, depth=depth, fps_group=G, fps_threads=512, fps_lazy=lazy, ramp=False, bq="bin", l2_side=True)
     feed = pipe.feed()
     for i in range((depth + 1) * G):
         feed.push(xs[i % 4], ready)
@@ -30,7 +32,7 @@ for depth, G in [(3, 3), (3, 2), (4, 2), (2, 3), (4, 3), (3, 5), (2, 5)]:
         feed.push(xs[i % 4], ready)
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) / n * 1e3
-    print(f"depth {depth} G {G}: {ms:.3f} ms per batch, {B * N / ms / 1e3:.1f} M points/s", flush=True)
+    print(f"lazy {int(lazy)} depth {depth} G {G}: {ms:.3f} ms per batch, {B * N / ms / 1e3:.1f} M points/s", flush=True)
     feed.flush()
     del feed, pipe
     torch.cuda.synchronize()

@@ -20,10 +20,10 @@ int fail(int code, const std::string &msg)
 void *workspace(lidar_handle *h, uint64_t bytes)
 {
     if (bytes <= h->ws_bytes) return h->ws;
-    // 25 % headroom (a doubling policy held 2x the need live plus the retired blocks); the
-    // retired blocks are freed by lidar_trim where the caller knows the handle idle (the package
-    // trims after its synchronisations) or by lidar_destroy
-    const uint64_t want = align_up(bytes + bytes / 4, 1 << 20);
+    // 25 % headroom, and at least double the current block: the retired blocks (freed by lidar_trim
+    // where the caller knows the handle idle, or by lidar_destroy) then stay below the live block
+    // however demand grows
+    const uint64_t want = align_up(std::max(bytes + bytes / 4, 2 * h->ws_bytes), 1 << 20);
     void *fresh = nullptr;
     const hipError_t e = hipMalloc(&fresh, want);
     if (e != hipSuccess) {

@@ -5,30 +5,31 @@
 // margin, histogram2d's searchsorted-right binning with the last edge closed) per axis, key =
 // (bx*ny + by)*nz + bz; voxels in ascending key order, voxel id = rank of the key (-1 for a point
 // outside every bin), centroid = sequential fp32 sum of the voxel's points in point order / count.
-// voxel.hip runs one frame in one workgroup; here every pass is spread over (tiles x frames)
-// workgroups:
 //
-//   bbox (min, max)                                       grid (chunks, frames), atomics per frame
-//   keys (u32) + indices per 4096-element tile, with the tile's histogram of radix digit 0 (LDS)
-//          -> hist[frame][digit][tile]; a point outside every bin takes the key nx ny nz (one past the
-//          last voxel), so every frame's key bits follow from its grid alone
-//   LSD radix sort, 8-bit digits, only the passes a frame's key range needs (per-frame parity):
-//     hist    (passes after the first) per 4096-element tile, LDS histogram
-//     scatter per tile, stable: the tile's base per digit from the frame's tile histograms (its own
-//             scan of them, frames of <= 32 tiles; a separate scan launch above), then 1024-element
-//             sub-tiles ranked by wave ballots (8 per digit) and per-wave prefix counts in LDS, running
-//             per-digit offsets
-//   runs      per tile: run starts counted, then written from the frame's earlier tiles' counts
-//             -> voxel id per point, run offsets, voxel count
-//   centroid  one thread per voxel walks its run (index order: the sort is stable)
-// 6 + 2 passes launches (round 3: 6 + 3 passes: the first histogram and every scan were launches of their own).
-// (Counting the next pass's histogram with global atomics inside the scatter, and the centroids inside the
-// runs kernel, were measured slower: 499 vs 238 us per 32-frame call.)
+// Round 5: a two-level sort in four launches (round 4: an 8-bit LSD radix sort over global memory,
+// 13 launches and ~284 B of memory traffic per point):
 //
-// Memory-side bytes per point: xyz read 3x (36 B: bbox, keys, centroids) + keys/indices (8 B written) + per radix pass
-// 24 B (two reads, one write of 8 B) + runs 12 B + centroid gathers 12 B; the algorithmic floor is
-// 12 B in + 4 B voxel id out (+16 B per voxel).  No host synchronisation: nvox[f] lands on the
-// device (-1: the frame's extent is not finite, or its grid has 2^32 keys or more).
+//   bbox     grid (16 chunks, frames): per-chunk min / max (monotone bits) -> 16 partials per frame
+//   keys     grid (4096-point tiles, frames): the frame's grid from its partials (float64, every
+//            workgroup alike), the key of every point (a point outside every bin takes nx ny nz, one
+//            past the last voxel), and the tile's histogram over 1024 coarse bins (key >> hs, the
+//            top 10 bits of the frame's key range)
+//   scatter  grid (tiles, frames): each workgroup sums the frame's tile histograms itself (exclusive
+//            scan over the coarse bins, plus the counts of the tiles before it) and scatters its
+//            (key, index) pairs to their coarse bin (LDS atomics: order inside a bin is free, the
+//            buckets sort by (key, index) anyway)
+//   bucket   grid (buckets, frames): bucket b holds the coarse bins whose start falls in
+//            [b n / NB, (b + 1) n / NB) — ~1 536 points for a uniform frame.  It sorts its pairs by
+//            (key, index) in LDS (bitonic; a bucket above 4 096 pairs — clumped frames, huge voxels —
+//            sorts in global memory by a stable LSD radix over the bits that vary), counts its voxels,
+//            takes its voxel offset from the buckets before it by a decoupled look-back (each bucket
+//            publishes its count, then its inclusive prefix; every wait is on a lower workgroup
+//            index, i.e. one dispatched earlier), and writes every point's voxel id and, one thread
+//            per voxel walking its points in index order, the centroid and count.
+//
+// Memory-side bytes per point: xyz 12 (bbox) + 12 (keys) + key 4 + 4 + pair 8 + 8 + id 4 + the
+// centroid gathers 12 (+16 per voxel out); no host synchronisation: nvox[f] lands on the device
+// (-1: the frame's extent is not finite, or its grid has 2^32 - 1 keys or more).
 #include <algorithm>
 
 #include "common.hpp"
@@ -36,15 +37,21 @@
 
 namespace {
 
-constexpr int VT = 256;      // threads of the streaming kernels
-constexpr int TILE = 4096;   // radix tile (elements per scatter workgroup)
-constexpr int ST = 1024;     // scatter / runs workgroup threads
-constexpr int SW = ST / 64;  // waves per scatter workgroup
-
-// per-frame meta words: [0..2] / [3..5] monotone bits of the min / max point, [6] key bits (of the
-// outside key), [7] unusable grid, [8] voxel count, [10] end of the last voxel's run, [11] the outside key
-constexpr int MW = 16;
-constexpr int kFuseScanTiles = 32;  // frames of at most this many tiles: the scatter scans the histograms itself
+constexpr int BT = 256;            // bbox threads
+constexpr int NCH = 16;            // bbox chunks per frame
+constexpr int KT = 1024;           // keys / scatter threads
+constexpr int TILE = 4096;         // points per keys / scatter workgroup
+constexpr int HB = 12;             // coarse-bin bits of the key range
+constexpr int NBIN = 1 << HB;      // coarse bins per frame
+constexpr int BPT = NBIN / KT;     // coarse bins per scatter thread (its scan)
+constexpr int UT = 512;            // bucket threads
+constexpr int CAP = 2048;          // pairs a bucket sorts in LDS
+constexpr int KMAX = 4096;         // local key range of the LDS counting sort
+constexpr int SEGMAX = 32;         // longest equal-key run the counting sort orders by index itself
+constexpr int BUCKET = 1536;       // target points per bucket
+constexpr int MW = 8;              // meta words per frame: [0] grid ok, [1] outside key, [2] hs
+constexpr uint64_t kPad = ~0ull;   // bitonic padding: sorts last
+static_assert(NBIN % KT == 0 && NBIN % UT == 0, "bins per thread");
 
 __device__ __forceinline__ uint32_t ord(float f)  // monotone float -> u32
 {
@@ -56,336 +63,623 @@ __device__ __forceinline__ float unord(uint32_t u)
     return __uint_as_float(u ^ (((u >> 31) - 1u) | 0x80000000u));
 }
 
-__global__ void vb_init_kernel(uint32_t *meta, int batch)
+struct Ws {  // per-batch workspace, every array frame-major
+    uint32_t *part;    // [F][NCH][6] bbox partials (monotone bits)
+    uint32_t *meta;    // [F][MW]
+    uint32_t *key;     // [F][n]
+    uint16_t *thist;   // [F][T][NBIN] tile histograms of the coarse bins (a tile holds <= 4096 points)
+    uint32_t *base;    // [F][NBIN + 1] start of every coarse bin in bucket order
+    uint64_t *pairs;   // [F][n] (key << 32 | index), coarse-bin order
+    uint64_t *scratch; // [F][n] the global sort's other buffer
+    uint64_t *flags;   // [F][NB] look-back words: status << 32 | count
+};
+
+__device__ __forceinline__ int64_t n_buckets(int64_t n) { return (n + BUCKET - 1) / BUCKET; }
+
+// (frame, part) of a 1-D grid of `parts` workgroups per frame.  XCD-affine (batch >= 8): workgroup L
+// runs on XCD L % 8, which takes frames L % 8, L % 8 + 8, ... and their parts in order, so a frame's
+// scattered writes and gathers stay in one L2 and its part p - 1 is dispatched before part p (the
+// bucket look-back waits only on that); fewer frames: plain frame-major order.  false: padding.
+__device__ __forceinline__ bool frame_part(int64_t batch, int64_t parts, int64_t &f, int64_t &p)
 {
-    const int f = blockIdx.x * blockDim.x + threadIdx.x;
-    if (f >= batch) return;
-    uint32_t *m = meta + (int64_t)f * MW;
-    for (int a = 0; a < 3; ++a) {
-        m[a] = 0xffffffffu;  // >= ord(any float)
-        m[3 + a] = 0u;        // <= ord(any float)
+    const int64_t L = blockIdx.x;
+    if (batch >= 8) {
+        const int64_t x = L & 7, j = L >> 3;
+        f = x + 8 * (j / parts);
+        p = j % parts;
+    } else {
+        f = L / parts;
+        p = L % parts;
     }
-    m[6] = m[7] = m[8] = m[9] = 0u;
+    return f < batch;
+}
+__host__ __forceinline__ unsigned frame_grid(int64_t batch, int64_t parts)
+{
+    return (unsigned)(batch >= 8 ? 8 * ((batch + 7) / 8) * parts : batch * parts);
 }
 
-// per-frame bbox in one pass: min and max as monotone bit patterns (atomics per wave)
-__global__ __launch_bounds__(VT) void vb_bbox_kernel(const float *__restrict__ xyz, int64_t n, uint32_t *meta)
+// block-wide exclusive scan of one value per thread (T threads); returns the exclusive prefix and
+// the total through *tot.  Uses red[T / 64]; starts and ends with a barrier.
+template <int T>
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *red, uint32_t *tot)
 {
-    const int f = blockIdx.y;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t inc = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t u = (uint32_t)__shfl_up((int)inc, o, 64);
+        if (lane >= o) inc += u;
+    }
+    __syncthreads();  // red[] free (a previous scan's readers are done)
+    if (lane == 63) red[wave] = inc;
+    __syncthreads();
+    uint32_t pre = 0, all = 0;
+#pragma unroll
+    for (int w = 0; w < T / 64; ++w) {
+        pre += w < wave ? red[w] : 0u;
+        all += red[w];
+    }
+    *tot = all;
+    return pre + inc - v;
+}
+
+// ---------------------------------------------------------------------------------------- bbox
+__global__ __launch_bounds__(BT) void vx_bbox_kernel(const float *__restrict__ xyz, int64_t n, Ws w, int64_t nb)
+{
+    const int f = blockIdx.y, c = blockIdx.x;
     const float *p = xyz + (int64_t)f * n * 3;
+    const int64_t i0 = n * c / NCH, i1 = n * (c + 1) / NCH;
     uint32_t lo[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, hi[3] = {0u, 0u, 0u};
-    for (int64_t i = (int64_t)blockIdx.x * VT + threadIdx.x; i < n; i += (int64_t)gridDim.x * VT)
+    for (int64_t i = i0 + threadIdx.x; i < i1; i += BT)
+#pragma unroll
         for (int a = 0; a < 3; ++a) {
             const uint32_t o = ord(p[3 * i + a]);
             lo[a] = min(lo[a], o);
             hi[a] = max(hi[a], o);
         }
+    __shared__ uint32_t red[BT / 64][6];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
     for (int a = 0; a < 3; ++a) {
-        uint32_t v = lo[a], w = hi[a];
+        uint32_t v = lo[a], u = hi[a];
+#pragma unroll
         for (int m = 32; m >= 1; m >>= 1) {
             v = min(v, (uint32_t)__shfl_xor((int)v, m, 64));
-            w = max(w, (uint32_t)__shfl_xor((int)w, m, 64));
+            u = max(u, (uint32_t)__shfl_xor((int)u, m, 64));
         }
-        if ((threadIdx.x & 63) == 0) {
-            atomicMin(meta + (int64_t)f * MW + a, v);
-            atomicMax(meta + (int64_t)f * MW + 3 + a, w);
+        if (lane == 0) {
+            red[wave][a] = v;
+            red[wave][3 + a] = u;
         }
     }
-}
-
-__device__ __forceinline__ lidar_vox::Grid frame_grid(const uint32_t *m, double voxel)
-{
-    const double lo[3] = {unord(m[0]), unord(m[1]), unord(m[2])}, hi[3] = {unord(m[3]), unord(m[4]), unord(m[5])};
-    return lidar_vox::make_grid(lo, hi, voxel);
-}
-
-// grid (ntiles, frames): keys and indices of one 4096-element tile and the tile's histogram of digit 0
-__global__ __launch_bounds__(ST) void vb_keys_kernel(const float *__restrict__ xyz, int64_t n, double voxel,
-                                                     uint32_t *meta, uint32_t *__restrict__ key,
-                                                     uint32_t *__restrict__ idx, uint32_t *__restrict__ hist,
-                                                     int ntiles)
-{
-    const int f = blockIdx.y, t = blockIdx.x;
-    const float *p = xyz + (int64_t)f * n * 3;
-    uint32_t *m = meta + (int64_t)f * MW;
-    const lidar_vox::Grid g = frame_grid(m, voxel);
-    const uint32_t okey = g.ok ? (uint32_t)g.keys : 0u;
-    const int bits = g.ok ? 32 - __clz((int)okey) : 0;  // okey = nx ny nz >= 1
-    if (t == 0 && threadIdx.x == 0) {
-        m[7] = g.ok ? 0u : 1u;
-        m[6] = (uint32_t)bits;
-        m[11] = okey;
-        m[10] = (uint32_t)n;  // end of the last voxel's run, unless points lie outside every bin (runs kernel)
+    __syncthreads();
+    if (threadIdx.x < 6) {
+        const int a = threadIdx.x;
+        uint32_t v = red[0][a];
+        for (int q = 1; q < BT / 64; ++q) v = a < 3 ? min(v, red[q][a]) : max(v, red[q][a]);
+        w.part[((int64_t)f * NCH + c) * 6 + a] = v;
     }
-    if (!g.ok) return;
-    __shared__ uint32_t h[256];
-    if (threadIdx.x < 256) h[threadIdx.x] = 0;
-    __syncthreads();
-    uint32_t *k = key + (int64_t)f * n;
-    uint32_t *v = idx + (int64_t)f * n;
-    const int64_t i0 = (int64_t)t * TILE, i1 = min<int64_t>(n, i0 + TILE);
-    for (int64_t i = i0 + threadIdx.x; i < i1; i += ST) {
-        uint32_t kk = lidar_vox::key(g, p[3 * i], p[3 * i + 1], p[3 * i + 2]);
-        kk = kk == lidar_vox::kOutside ? okey : kk;  // sorts after every voxel's key
-        k[i] = kk;
-        v[i] = (uint32_t)i;
-        atomicAdd(&h[kk & 255u], 1u);
+    if (c == 0)  // the bucket launch's look-back words start at "nothing published"
+        for (int64_t b = threadIdx.x; b < nb; b += BT) w.flags[(int64_t)f * nb + b] = 0ull;
+}
+
+// ---------------------------------------------------------------------------------------- keys
+__global__ __launch_bounds__(KT) void vx_keys_kernel(const float *__restrict__ xyz, int64_t n, double voxel, Ws w,
+                                                     int ntiles, int64_t batch)
+{
+    int64_t f, t;
+    if (!frame_part(batch, ntiles, f, t)) return;
+    const int tid = threadIdx.x;
+    __shared__ uint32_t ext[6];
+    __shared__ uint32_t hist[NBIN];
+    if (tid < 6) {
+        const uint32_t *pp = w.part + (int64_t)f * NCH * 6 + tid;
+        uint32_t v = pp[0];
+        for (int c = 1; c < NCH; ++c) v = tid < 3 ? min(v, pp[6 * c]) : max(v, pp[6 * c]);
+        ext[tid] = v;
     }
-    __syncthreads();
-    if (threadIdx.x < 256) hist[((int64_t)f * 256 + threadIdx.x) * ntiles + t] = h[threadIdx.x];
-}
-
-// key bits of frame f, read after vb_keys_kernel (0 when the grid overflowed: nothing is sorted,
-// the runs kernel reports -1)
-__device__ __forceinline__ int frame_bits(const uint32_t *meta, int f)
-{
-    const uint32_t *m = meta + (int64_t)f * MW;
-    return m[7] ? 0 : (int)m[6];
-}
-
-__global__ __launch_bounds__(VT) void vb_hist_kernel(const uint32_t *__restrict__ kin, int64_t n, int shift,
-                                                     int ntiles, const uint32_t *meta, uint32_t *__restrict__ hist)
-{
-    const int f = blockIdx.y, t = blockIdx.x;
-    if (frame_bits(meta, f) <= shift) return;  // this frame needs no pass at this digit
-    __shared__ uint32_t h[256];
-    for (int d = threadIdx.x; d < 256; d += VT) h[d] = 0;
-    __syncthreads();
-    const uint32_t *k = kin + (int64_t)f * n;
-    const int64_t i0 = (int64_t)t * TILE, i1 = min<int64_t>(n, i0 + TILE);
-    for (int64_t i = i0 + threadIdx.x; i < i1; i += VT) atomicAdd(&h[(k[i] >> shift) & 255u], 1u);
-    __syncthreads();
-    uint32_t *hf = hist + (int64_t)f * 256 * ntiles;
-    for (int d = threadIdx.x; d < 256; d += VT) hf[(int64_t)d * ntiles + t] = h[d];
-}
-
-// per frame: exclusive scan of hist[f] in (digit, tile) order
-__global__ __launch_bounds__(ST) void vb_scan_kernel(uint32_t *__restrict__ hist, int ntiles, int shift,
-                                                     const uint32_t *meta)
-{
-    const int f = blockIdx.x;
-    if (frame_bits(meta, f) <= shift) return;
-    __shared__ uint32_t wsum[SW];
-    __shared__ uint32_t carry;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint32_t *hf = hist + (int64_t)f * 256 * ntiles;
-    const int64_t total = (int64_t)256 * ntiles;
-    if (threadIdx.x == 0) carry = 0;
-    __syncthreads();
-    for (int64_t b0 = 0; b0 < total; b0 += ST) {
-        const int64_t i = b0 + threadIdx.x;
-        const uint32_t v = i < total ? hf[i] : 0u;
-        uint32_t inc = v;
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t u = (uint32_t)__shfl_up((int)inc, o, 64);
-            if (lane >= o) inc += u;
-        }
-        if (lane == 63) wsum[wave] = inc;
-        __syncthreads();
-        uint32_t pre = carry, tot = 0;
-        for (int w = 0; w < SW; ++w) {
-            pre += w < wave ? wsum[w] : 0u;
-            tot += wsum[w];
-        }
-        if (i < total) hf[i] = pre + inc - v;
-        __syncthreads();
-        if (threadIdx.x == 0) carry += tot;
-        __syncthreads();
-    }
-}
-
-// FUSED: the tile's base per digit from the frame's raw tile histograms (its own scan: the digit's
-// count in the frame's earlier tiles plus every smaller digit's total); else hist holds vb_scan_kernel's
-// exclusive offsets
-template <bool FUSED>
-__global__ __launch_bounds__(ST) void vb_scatter_kernel(const uint32_t *__restrict__ kin, const uint32_t *__restrict__ vin,
-                                                        uint32_t *__restrict__ kout, uint32_t *__restrict__ vout,
-                                                        int64_t n, int shift, int ntiles, const uint32_t *meta,
-                                                        const uint32_t *__restrict__ hist)
-{
-    const int f = blockIdx.y, t = blockIdx.x;
-    if (frame_bits(meta, f) <= shift) return;
-    __shared__ uint32_t off[256];      // running global offset per digit
-    __shared__ uint32_t wcnt[SW][256]; // per-wave digit counts of the current sub-tile
-    __shared__ uint32_t wtot[4];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint32_t *hf = hist + (int64_t)f * 256 * ntiles;
-    if constexpr (FUSED) {
-        uint32_t tot = 0, pre = 0;  // thread d < 256: digit d's frame total and its count before tile t
-        if (tid < 256)
-            for (int u = 0; u < ntiles; ++u) {
-                const uint32_t c = hf[(int64_t)tid * ntiles + u];
-                tot += c;
-                pre += u < t ? c : 0u;
-            }
-        uint32_t inc = tot;  // exclusive scan of the totals over the 256 digits (waves 0-3)
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t u = (uint32_t)__shfl_up((int)inc, o, 64);
-            if (lane >= o) inc += u;
-        }
-        if (tid < 256 && lane == 63) wtot[wave] = inc;
-        __syncthreads();
-        if (tid < 256) {
-            uint32_t base = inc - tot;
-            for (int w = 0; w < wave; ++w) base += wtot[w];
-            off[tid] = base + pre;
-        }
-    } else {
-        for (int d = tid; d < 256; d += ST) off[d] = hf[(int64_t)d * ntiles + t];
-    }
-    const uint32_t *k = kin + (int64_t)f * n;
-    const uint32_t *v = vin + (int64_t)f * n;
-    uint32_t *ko = kout + (int64_t)f * n;
-    uint32_t *vo = vout + (int64_t)f * n;
-    const uint64_t below = (1ull << lane) - 1;
-    const int64_t i0 = (int64_t)t * TILE, i1 = min<int64_t>(n, i0 + TILE);
-    for (int64_t b0 = i0; b0 < i1; b0 += ST) {
-        const int64_t i = b0 + tid;
-        const bool valid = i < i1;
-        const uint32_t kk = valid ? k[i] : 0u, vv = valid ? v[i] : 0u;
-        const uint32_t dig = (kk >> shift) & 255u;
-        uint64_t same = __ballot(valid);
 #pragma unroll
-        for (int bit = 0; bit < 8; ++bit) {
-            const uint64_t bm = __ballot((dig >> bit) & 1u);
-            same &= ((dig >> bit) & 1u) ? bm : ~bm;
-        }
-        for (int d = lane; d < 256; d += 64) wcnt[wave][d] = 0;
-        __syncthreads();  // (also: off[] initialised / advanced)
-        if (valid && (same & below) == 0) wcnt[wave][dig] = (uint32_t)__popcll(same);
-        __syncthreads();
-        if (valid) {
-            uint32_t o = off[dig] + (uint32_t)__popcll(same & below);
-            for (int w = 0; w < wave; ++w) o += wcnt[w][dig];
-            ko[o] = kk;
-            vo[o] = vv;
-        }
-        __syncthreads();
-        for (int d = tid; d < 256; d += ST) {
-            uint32_t s = 0;
-            for (int w = 0; w < SW; ++w) s += wcnt[w][d];
-            off[d] += s;
-        }
-        __syncthreads();  // wcnt is reset by the next sub-tile
-    }
-}
-
-// run starts of the sorted keys, per 4096-element tile (chip-wide): count, then write with the
-// tile's base from the counts of the frame's earlier tiles (<= n / 4096 loads)
-__device__ __forceinline__ void sorted_bufs(const uint32_t *m, int f, int64_t n, const uint32_t *k0,
-                                            const uint32_t *v0, const uint32_t *k1, const uint32_t *v1,
-                                            const uint32_t *&sk, const uint32_t *&si)
-{
-    const int passes = ((int)m[6] + 7) / 8;  // the sorted data sits in buffer (passes run) % 2
-    sk = (passes & 1 ? k1 : k0) + (int64_t)f * n;
-    si = (passes & 1 ? v1 : v0) + (int64_t)f * n;
-}
-
-__global__ __launch_bounds__(ST) void vb_runs_count_kernel(const uint32_t *__restrict__ k0, const uint32_t *__restrict__ v0,
-                                                           const uint32_t *__restrict__ k1, const uint32_t *__restrict__ v1,
-                                                           int64_t n, int ntiles, const uint32_t *meta,
-                                                           uint32_t *__restrict__ tilecnt)
-{
-    const int f = blockIdx.y, t = blockIdx.x;
-    const uint32_t *m = meta + (int64_t)f * MW;
-    if (m[7]) return;
-    const uint32_t *sk, *si;
-    sorted_bufs(m, f, n, k0, v0, k1, v1, sk, si);
-    __shared__ uint32_t ws[SW];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int64_t i0 = (int64_t)t * TILE, i1 = min<int64_t>(n, i0 + TILE);
-    const uint32_t okey = m[11];
-    uint32_t c = 0;
-    for (int64_t i = i0 + tid; i < i1; i += ST)
-        c += (sk[i] != okey && (i == 0 || sk[i] != sk[i - 1])) ? 1u : 0u;
-    for (int o = 32; o >= 1; o >>= 1) c += (uint32_t)__shfl_xor((int)c, o, 64);
-    if (lane == 0) ws[wave] = c;
+    for (int j = 0; j < BPT; ++j) hist[tid + j * KT] = 0;
     __syncthreads();
-    if (tid == 0) {
-        uint32_t tot = 0;
-        for (int w = 0; w < SW; ++w) tot += ws[w];
-        tilecnt[(int64_t)f * ntiles + t] = tot;
+    const double lo[3] = {unord(ext[0]), unord(ext[1]), unord(ext[2])};
+    const double hi[3] = {unord(ext[3]), unord(ext[4]), unord(ext[5])};
+    const lidar_vox::Grid g = lidar_vox::make_grid(lo, hi, voxel);
+    uint32_t *m = w.meta + (int64_t)f * MW;
+    const uint32_t okey = g.ok ? (uint32_t)g.keys : 0u;  // nx ny nz >= 1: one past the last voxel
+    const int bits = g.ok ? 32 - __clz((int)okey) : 0;
+    const int hs = max(0, bits - HB);
+    if (t == 0 && tid == 0) {
+        m[0] = g.ok ? 1u : 0u;
+        m[1] = okey;
+        m[2] = (uint32_t)hs;
     }
-}
-
-__global__ __launch_bounds__(ST) void vb_runs_write_kernel(const uint32_t *__restrict__ k0, const uint32_t *__restrict__ v0,
-                                                           const uint32_t *__restrict__ k1, const uint32_t *__restrict__ v1,
-                                                           int64_t n, int ntiles, uint32_t *meta,
-                                                           const uint32_t *__restrict__ tilecnt,
-                                                           int32_t *__restrict__ vid, uint32_t *__restrict__ vstart,
-                                                           int32_t *__restrict__ nvox)
-{
-    const int f = blockIdx.y, t = blockIdx.x;
-    uint32_t *m = meta + (int64_t)f * MW;
-    if (m[7]) {
-        if (t == 0 && threadIdx.x == 0) nvox[f] = -1;
-        return;
-    }
-    const uint32_t *sk, *si;
-    sorted_bufs(m, f, n, k0, v0, k1, v1, sk, si);
-    int32_t *vf = vid + (int64_t)f * n;
-    uint32_t *vs = vstart + (int64_t)f * (n + 1);
-    __shared__ uint32_t ws[SW];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint32_t okey = m[11];
-    uint32_t base = 0;
-    for (int u = 0; u < t; ++u) base += tilecnt[(int64_t)f * ntiles + u];
-    const int64_t i0 = (int64_t)t * TILE, i1 = min<int64_t>(n, i0 + TILE);
-    for (int64_t b0 = i0; b0 < i1; b0 += ST) {
-        const int64_t i = b0 + tid;
-        const bool in = i < i1 && sk[i] != okey;
-        const bool st = in && (i == 0 || sk[i] != sk[i - 1]);
-        const uint64_t mk = __ballot(st);
-        const uint32_t inw = (uint32_t)__popcll(mk & ((1ull << lane) - 1));
-        if (lane == 0) ws[wave] = (uint32_t)__popcll(mk);
-        __syncthreads();
-        uint32_t pre = 0, tot = 0;
-        for (int w = 0; w < SW; ++w) {
-            pre += w < wave ? ws[w] : 0u;
-            tot += ws[w];
-        }
-        if (in) {
-            const uint32_t r = base + pre + inw + (st ? 1u : 0u) - 1u;  // my voxel's rank
-            vf[si[i]] = (int32_t)r;
-            if (st) vs[r] = (uint32_t)i;
-        } else if (i < i1) {
-            vf[si[i]] = -1;  // outside every bin (sorted after the last voxel)
-            if (i == 0 || sk[i - 1] != okey) m[10] = (uint32_t)i;  // the last run's end
-        }
-        base += tot;
-        __syncthreads();
-    }
-    if (t == ntiles - 1 && tid == 0) {
-        m[8] = base;
-        nvox[f] = (int32_t)base;
-    }
-}
-
-__global__ __launch_bounds__(VT) void vb_centroid_kernel(const float *__restrict__ xyz, int64_t n,
-                                                         const uint32_t *__restrict__ v0, const uint32_t *__restrict__ v1,
-                                                         const uint32_t *meta, const uint32_t *__restrict__ vstart,
-                                                         float *__restrict__ cent, int32_t *__restrict__ counts)
-{
-    const int f = blockIdx.y;
-    const uint32_t *m = meta + (int64_t)f * MW;
-    if (m[7]) return;
-    const int passes = ((int)m[6] + 7) / 8;  // the sorted indices sit in buffer (passes run) % 2
-    const uint32_t *si = (passes & 1 ? v1 : v0) + (int64_t)f * n;
-    const uint32_t *vs = vstart + (int64_t)f * (n + 1);
+    if (!g.ok) return;  // whole workgroup (uniform)
     const float *p = xyz + (int64_t)f * n * 3;
-    const uint32_t V = m[8];
-    for (uint32_t v = blockIdx.x * VT + threadIdx.x; v < V; v += gridDim.x * VT) {
-        const uint32_t a = vs[v], b = v + 1 < V ? vs[v + 1] : m[10];
-        float s[3] = {0.f, 0.f, 0.f};
-        for (uint32_t t = a; t < b; ++t) {
-            const uint32_t i = si[t];
-            for (int c = 0; c < 3; ++c) s[c] = __fadd_rn(s[c], p[3 * i + c]);
+    uint32_t *k = w.key + (int64_t)f * n;
+#pragma unroll
+    for (int j = 0; j < TILE / KT; ++j) {
+        const int64_t i = (int64_t)t * TILE + j * KT + tid;
+        if (i < n) {
+            uint32_t kk = lidar_vox::key(g, p[3 * i], p[3 * i + 1], p[3 * i + 2]);
+            kk = kk == lidar_vox::kOutside ? okey : kk;  // sorts after every voxel's key
+            k[i] = kk;
+            atomicAdd(&hist[kk >> hs], 1u);
         }
-        const float cnt = (float)(b - a);
-        float *o = cent + ((int64_t)f * n + v) * 3;
-        for (int c = 0; c < 3; ++c) o[c] = __fdiv_rn(s[c], cnt);
-        counts[(int64_t)f * n + v] = (int32_t)(b - a);
     }
+    __syncthreads();
+    uint16_t *th = w.thist + ((int64_t)f * ntiles + t) * NBIN;
+#pragma unroll
+    for (int j = 0; j < BPT; ++j) th[tid + j * KT] = (uint16_t)hist[tid + j * KT];
+}
+
+// ------------------------------------------------------------------------------------- scatter
+__global__ __launch_bounds__(KT) void vx_scatter_kernel(int64_t n, Ws w, int ntiles, int64_t batch)
+{
+    int64_t f, t;
+    if (!frame_part(batch, ntiles, f, t)) return;
+    const int tid = threadIdx.x;
+    const uint32_t *m = w.meta + (int64_t)f * MW;
+    if (!m[0]) return;
+    const int hs = (int)m[2];
+    __shared__ uint32_t off[NBIN];
+    __shared__ uint32_t red[KT / 64];
+    // coarse bins BPT tid .. BPT tid + BPT - 1: frame totals and the counts of the tiles before this one
+    uint32_t tot[BPT], pre[BPT], sum = 0;
+#pragma unroll
+    for (int j = 0; j < BPT; ++j) tot[j] = pre[j] = 0;
+    const uint16_t *th = w.thist + (int64_t)f * ntiles * NBIN + BPT * tid;
+    for (int u = 0; u < ntiles; ++u) {
+        const uint2 c4 = *reinterpret_cast<const uint2 *>(th + (int64_t)u * NBIN);  // 4 u16
+        const uint32_t c[4] = {c4.x & 0xffffu, c4.x >> 16, c4.y & 0xffffu, c4.y >> 16};
+#pragma unroll
+        for (int j = 0; j < BPT; ++j) {
+            tot[j] += c[j];
+            pre[j] += u < t ? c[j] : 0u;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < BPT; ++j) sum += tot[j];
+    uint32_t all;
+    uint32_t ex = block_excl_scan<KT>(sum, red, &all);
+    uint32_t *bs = w.base + (int64_t)f * (NBIN + 1);
+#pragma unroll
+    for (int j = 0; j < BPT; ++j) {
+        if (t == 0) bs[BPT * tid + j] = ex;
+        off[BPT * tid + j] = ex + pre[j];
+        ex += tot[j];
+    }
+    if (t == 0 && tid == 0) bs[NBIN] = all;
+    __syncthreads();
+    const uint32_t *k = w.key + (int64_t)f * n;
+    uint64_t *pr = w.pairs + (int64_t)f * n;
+#pragma unroll
+    for (int j = 0; j < TILE / KT; ++j) {
+        const int64_t i = (int64_t)t * TILE + j * KT + tid;
+        if (i < n) {
+            const uint32_t kk = k[i];
+            const uint32_t pos = atomicAdd(&off[kk >> hs], 1u);
+            pr[pos] = ((uint64_t)kk << 32) | (uint32_t)i;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------- buckets
+// stable LSD radix sort of m pairs in global memory by one workgroup (a bucket above CAP), over the
+// 8-bit digits whose bits vary across the bucket; returns the buffer holding the result
+__device__ uint64_t *bucket_radix(uint64_t *a, uint64_t *b, int64_t m, uint32_t *cnt, uint32_t (*wc)[256],
+                                  uint32_t *red, unsigned long long *vary)
+{
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid == 0) *vary = 0ull;
+    __syncthreads();
+    const uint64_t v0 = a[0];
+    uint64_t x = 0;
+    for (int64_t i = tid; i < m; i += UT) x |= a[i] ^ v0;
+    for (int o = 32; o >= 1; o >>= 1) x |= (uint64_t)__shfl_xor((long long)x, o, 64);
+    if (lane == 0) atomicOr(vary, (unsigned long long)x);
+    __syncthreads();
+    const uint64_t vb = *vary;
+    for (int shift = 0; shift < 64; shift += 8) {
+        if (((vb >> shift) & 0xffull) == 0) continue;  // uniform: this digit is constant
+        if (tid < 256) cnt[tid] = 0;
+        __syncthreads();
+        for (int64_t i = tid; i < m; i += UT) atomicAdd(&cnt[(a[i] >> shift) & 255u], 1u);
+        __syncthreads();
+        uint32_t all;
+        const uint32_t ex = block_excl_scan<UT>(tid < 256 ? cnt[tid] : 0u, red, &all);
+        __syncthreads();
+        if (tid < 256) cnt[tid] = ex;  // running offset per digit
+        const uint64_t below = (1ull << lane) - 1;
+        for (int64_t c0 = 0; c0 < m; c0 += UT) {
+            const int64_t i = c0 + tid;
+            const bool valid = i < m;
+            const uint64_t v = valid ? a[i] : 0ull;
+            const uint32_t dig = (uint32_t)(v >> shift) & 255u;
+            uint64_t same = __ballot(valid);
+#pragma unroll
+            for (int bit = 0; bit < 8; ++bit) {
+                const uint64_t bm = __ballot((dig >> bit) & 1u);
+                same &= ((dig >> bit) & 1u) ? bm : ~bm;
+            }
+            for (int d = lane; d < 256; d += 64) wc[wave][d] = 0;
+            __syncthreads();  // (also: cnt advanced by the previous chunk)
+            if (valid && (same & below) == 0) wc[wave][dig] = (uint32_t)__popcll(same);
+            __syncthreads();
+            if (valid) {
+                uint32_t o = cnt[dig] + (uint32_t)__popcll(same & below);
+                for (int q = 0; q < wave; ++q) o += wc[q][dig];
+                b[o] = v;
+            }
+            __syncthreads();
+            if (tid < 256) {
+                uint32_t s = 0;
+                for (int q = 0; q < UT / 64; ++q) s += wc[q][tid];
+                cnt[tid] += s;
+            }
+        }
+        __syncthreads();
+        uint64_t *tmp = a;
+        a = b;
+        b = tmp;
+    }
+    return a;
+}
+
+// the bucket's voxel offset: the sum of the earlier buckets' voxel counts, by a decoupled look-back
+// over 64 predecessors at a time (one wave; each lane one look-back word).  Publishes the bucket's
+// own count first, its inclusive prefix last.  Waits only on lower part indices of the same frame,
+// i.e. on workgroups dispatched before this one; every spin is bounded (*hung: a bug, not a hang).
+// A look-back word is its own payload (status << 32 | count, one 8-byte sc1 store, read by sc1 loads
+// that bypass the L1): relaxed agent-scope atomics, no fences (an acquire would invalidate the CU's
+// L1 per poll and a release write back the XCD's L2 per store: MI355X_MICROARCH.md, ~1.7 us each).
+__device__ uint64_t look_back(unsigned long long *fl, int64_t b, uint32_t nv, bool *hung, uint32_t *nspins = nullptr)
+{
+    const int lane = threadIdx.x & 63;
+    if (lane == 0)
+        __hip_atomic_store(&fl[b], ((b == 0 ? 2ull : 1ull) << 32) | nv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint64_t pre = 0;
+    *hung = false;
+    int64_t top = b - 1;
+    uint32_t spins = 0;
+    while (top >= 0) {
+        const int64_t q = top - lane;
+        const unsigned long long v =
+            q >= 0 ? __hip_atomic_load(&fl[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : (2ull << 32);
+        const uint32_t st = (uint32_t)(v >> 32);
+        const uint64_t incl = __ballot(st == 2);
+        const int k = incl ? __ffsll((unsigned long long)incl) - 1 : 63;
+        const uint64_t upto = k == 63 ? ~0ull : ((2ull << k) - 1);
+        if (__ballot(st == 0) & upto) {  // a predecessor before the first inclusive one has not published
+            __builtin_amdgcn_s_sleep(2);
+            if (++spins == (1u << 24)) {
+                *hung = true;
+                break;
+            }
+            continue;
+        }
+        uint64_t s = lane <= k ? (v & 0xffffffffull) : 0ull;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) s += (uint64_t)__shfl_xor((long long)s, o, 64);
+        pre += s;
+        if (incl) break;
+        top -= 64;
+    }
+    if (nspins) *nspins = spins;
+    if (lane == 0 && b > 0)
+        __hip_atomic_store(&fl[b], (2ull << 32) | (pre + nv), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return pre;
+}
+
+struct BucketLds {
+    uint64_t a[CAP];         // pairs as loaded, then the bitonic array
+    uint64_t s[CAP];         // counting-sort output
+    uint32_t cnt[KMAX];      // counting-sort counters / starts (the radix path's digit tables)
+    float xyz[CAP * 3];      // the bucket's points, for the centroid walks
+};
+
+__global__ __launch_bounds__(UT) void vx_bucket_kernel(const float *__restrict__ xyz, int64_t n, Ws w,
+                                                       int32_t *__restrict__ vid, float *__restrict__ cent,
+                                                       int32_t *__restrict__ counts, int32_t *__restrict__ nvox,
+                                                       int64_t batch)
+{
+    const int64_t nb = n_buckets(n);
+    int64_t f, b;
+    if (!frame_part(batch, nb, f, b)) return;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#ifdef VX_DIAG_PHASES
+    uint64_t ts[7];
+    auto stamp = [&](int k) {
+        uint64_t t;
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+        ts[k] = t;
+    };
+#define VX_STAMP(k) stamp(k)
+#else
+#define VX_STAMP(k)
+#endif
+    VX_STAMP(0);
+    const uint32_t *m = w.meta + (int64_t)f * MW;
+    if (!m[0]) {
+        if (b == 0 && tid == 0) nvox[f] = -1;
+        return;  // every bucket of the frame returns: nothing waits on this frame's look-back words
+    }
+    const uint32_t okey = m[1];
+    const int hs = (int)m[2];
+    __shared__ __attribute__((aligned(16))) BucketLds L;
+    __shared__ uint32_t rng[4];
+    __shared__ uint32_t red[UT / 64];
+    __shared__ uint32_t flag;
+    __shared__ unsigned long long prefix, vary;
+#ifdef VX_DIAG_PHASES
+    __shared__ uint32_t spins_dbg;
+#endif
+    // the bucket: coarse bins whose start s lies in [b S, (b + 1) S), S = n / nb (every workgroup of
+    // the frame evaluates the same monotone float expression, so the buckets tile the bins exactly)
+    if (tid < 4) rng[tid] = tid < 2 ? (uint32_t)n : (uint32_t)NBIN;
+    if (tid == 0) flag = 0;
+    __syncthreads();
+    {
+        const float inv = (float)nb / (float)n;
+        const uint32_t *bs = w.base + (int64_t)f * (NBIN + 1);
+        uint32_t m0 = (uint32_t)n, m1 = (uint32_t)n, c0 = NBIN, c1 = NBIN;
+        uint32_t sv[NBIN / UT];
+#pragma unroll
+        for (int j = 0; j < NBIN / UT; ++j) sv[j] = bs[NBIN - 1 - tid - j * UT];  // all loads in flight
+#pragma unroll
+        for (int j = 0; j < NBIN / UT; ++j) {  // descending bins: the min is the last hit
+            const int c = NBIN - 1 - tid - j * UT;
+            const int64_t bk = min<int64_t>((int64_t)((float)sv[j] * inv), nb - 1);
+            if (bk >= b) {
+                m0 = sv[j];
+                c0 = (uint32_t)c;
+            }
+            if (bk >= b + 1) {
+                m1 = sv[j];
+                c1 = (uint32_t)c;
+            }
+        }
+        // wave minima first: 512 threads on 4 LDS words would serialise ~2 000 atomics
+        m0 = (uint32_t)lidar::wave_min_u32_dpp(m0);
+        m1 = (uint32_t)lidar::wave_min_u32_dpp(m1);
+        c0 = (uint32_t)lidar::wave_min_u32_dpp(c0);
+        c1 = (uint32_t)lidar::wave_min_u32_dpp(c1);
+        if (lane == 0) {
+            atomicMin(&rng[0], m0);
+            atomicMin(&rng[1], m1);
+            atomicMin(&rng[2], c0);
+            atomicMin(&rng[3], c1);
+        }
+    }
+    __syncthreads();
+    VX_STAMP(1);
+    const int64_t p0 = rng[0], size = (int64_t)rng[1] - rng[0];
+    const uint64_t k0 = (uint64_t)rng[2] << hs, krange = (uint64_t)(rng[3] - rng[2]) << hs;
+    const uint64_t *gp = w.pairs + (int64_t)f * n + p0;
+    const float *p = xyz + (int64_t)f * n * 3;
+    const uint64_t *seq;   // the bucket sorted by (key, index): LDS or global
+    bool staged = false;   // xyz of the sorted pairs in L.xyz
+    if (size <= CAP) {
+        {
+            uint64_t v[CAP / UT];
+#pragma unroll
+            for (int j = 0; j < CAP / UT; ++j) v[j] = tid + j * UT < size ? gp[tid + j * UT] : 0ull;
+#pragma unroll
+            for (int j = 0; j < CAP / UT; ++j)
+                if (tid + j * UT < size) L.a[tid + j * UT] = v[j];
+        }
+        const bool counting = krange <= KMAX;
+        if (counting)
+            for (int64_t c = tid; c < (int64_t)krange; c += UT) L.cnt[c] = 0;
+        __syncthreads();
+        uint32_t rk[CAP / UT], lk[CAP / UT];
+        if (counting) {
+            // counting sort by local key: a rank inside the key from an LDS atomic, starts by a scan
+#pragma unroll
+            for (int j = 0; j < CAP / UT; ++j) {
+                const int64_t i = tid + j * UT;
+                if (i < size) {
+                    lk[j] = (uint32_t)((L.a[i] >> 32) - k0);
+                    rk[j] = atomicAdd(&L.cnt[lk[j]], 1u);
+                    if (rk[j] == SEGMAX) flag = 1;  // a long equal-key run: the bitonic path instead
+                }
+            }
+            __syncthreads();
+            if (!flag) {
+                // exclusive scan of the counters, KMAX / UT consecutive per thread
+                constexpr int PT = KMAX / UT;
+                uint32_t v[PT], sum = 0;
+#pragma unroll
+                for (int j = 0; j < PT; ++j) {
+                    const int64_t c = PT * tid + j;
+                    v[j] = c < (int64_t)krange ? L.cnt[c] : 0u;
+                    sum += v[j];
+                }
+                uint32_t all;
+                uint32_t ex = block_excl_scan<UT>(sum, red, &all);
+#pragma unroll
+                for (int j = 0; j < PT; ++j) {
+                    const int64_t c = PT * tid + j;
+                    if (c < (int64_t)krange) L.cnt[c] = ex;
+                    ex += v[j];
+                }
+                __syncthreads();
+#pragma unroll
+                for (int j = 0; j < CAP / UT; ++j) {
+                    const int64_t i = tid + j * UT;
+                    if (i < size) L.s[L.cnt[lk[j]] + rk[j]] = L.a[i];
+                }
+                __syncthreads();
+                // equal-key runs (< SEGMAX long) in index order: the thread of a run's first slot sorts it
+#pragma unroll
+                for (int j = 0; j < CAP / UT; ++j) {
+                    const int64_t i = tid + j * UT;
+                    if (i < size && rk[j] == 0) {
+                        const int64_t st = L.cnt[lk[j]];
+                        const uint64_t kk = L.a[i] >> 32;
+                        int64_t e = st + 1;
+                        while (e < size && (L.s[e] >> 32) == kk) ++e;
+                        for (int64_t x = st + 1; x < e; ++x) {  // insertion sort (full 64-bit order)
+                            const uint64_t v2 = L.s[x];
+                            int64_t y = x - 1;
+                            while (y >= st && L.s[y] > v2) {
+                                L.s[y + 1] = L.s[y];
+                                --y;
+                            }
+                            L.s[y + 1] = v2;
+                        }
+                    }
+                }
+                __syncthreads();
+                seq = L.s;
+            }
+        }
+        if (!counting || flag) {  // bitonic sort of the loaded pairs
+            int64_t P = 1;
+            while (P < size) P <<= 1;
+            for (int64_t i = size + tid; i < P; i += UT) L.a[i] = kPad;
+            __syncthreads();
+            for (int64_t k2 = 2; k2 <= P; k2 <<= 1)
+                for (int64_t j = k2 >> 1; j > 0; j >>= 1) {
+                    for (int64_t i = tid; i < P; i += UT) {
+                        const int64_t l = i ^ j;
+                        if (l > i) {
+                            const uint64_t x = L.a[i], y = L.a[l];
+                            if ((x > y) == ((i & k2) == 0)) {
+                                L.a[i] = y;
+                                L.a[l] = x;
+                            }
+                        }
+                    }
+                    __syncthreads();
+                }
+            seq = L.a;
+        }
+        __syncthreads();
+        VX_STAMP(2);
+        // the bucket's points, gathered in parallel (one memory round trip) for the centroid walks
+        {
+            float g[CAP / UT][3];
+#pragma unroll
+            for (int j = 0; j < CAP / UT; ++j) {
+                const int64_t i = tid + j * UT;
+                const int64_t idx = i < size ? (int64_t)(uint32_t)seq[i] : 0;
+#pragma unroll
+                for (int a = 0; a < 3; ++a) g[j][a] = p[3 * idx + a];
+            }
+#pragma unroll
+            for (int j = 0; j < CAP / UT; ++j) {
+                const int64_t i = tid + j * UT;
+                if (i < size)
+#pragma unroll
+                    for (int a = 0; a < 3; ++a) L.xyz[3 * i + a] = g[j][a];
+            }
+        }
+        staged = true;
+    } else {
+        seq = bucket_radix(const_cast<uint64_t *>(gp), w.scratch + (int64_t)f * n + p0, size, L.cnt,
+                           reinterpret_cast<uint32_t(*)[256]>(L.cnt + 256), red, &vary);
+    }
+    __syncthreads();
+    VX_STAMP(3);
+    // voxel starts: this thread's elements are CH consecutive ones per chunk of CH UT
+    constexpr int CH = 4;
+    auto key_at = [&](int64_t i) { return (uint32_t)(seq[i] >> 32); };
+    auto start_at = [&](int64_t i) {
+        const uint32_t kk = key_at(i);
+        return kk != okey && (i == 0 || kk != key_at(i - 1));
+    };
+    uint32_t nvl = 0;
+    for (int64_t c0 = 0; c0 < size; c0 += CH * UT) {
+        uint32_t s = 0;
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+            const int64_t i = c0 + CH * tid + j;
+            if (i < size) s += start_at(i) ? 1u : 0u;
+        }
+        uint32_t all;
+        block_excl_scan<UT>(s, red, &all);
+        nvl += all;
+    }
+    VX_STAMP(4);
+    if (wave == 0) {
+        bool hung;
+        uint32_t nsp = 0;
+        const uint64_t pre = look_back(reinterpret_cast<unsigned long long *>(w.flags + (int64_t)f * nb), b, nvl,
+                                       &hung, &nsp);
+#ifdef VX_DIAG_PHASES
+        if (lane == 0) spins_dbg = nsp;
+#endif
+        if (lane == 0) {
+            prefix = pre;
+            if (hung) nvox[f] = -2;
+            else if (b == nb - 1) nvox[f] = (int32_t)(pre + nvl);
+        }
+    }
+    __syncthreads();
+    VX_STAMP(5);
+    const uint32_t O = (uint32_t)prefix;
+    int32_t *vf = vid + (int64_t)f * n;
+    float *cf = cent + (int64_t)f * n * 3;
+    int32_t *nf = counts + (int64_t)f * n;
+    uint32_t carry = 0;
+    for (int64_t c0 = 0; c0 < size; c0 += CH * UT) {
+        bool st[CH];
+        uint32_t s = 0;
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+            const int64_t i = c0 + CH * tid + j;
+            st[j] = i < size && start_at(i);
+            s += st[j] ? 1u : 0u;
+        }
+        uint32_t all;
+        uint32_t r = O + carry + block_excl_scan<UT>(s, red, &all);  // voxels before this thread's elements
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+            const int64_t i = c0 + CH * tid + j;
+            if (i >= size) break;
+            const uint64_t v = seq[i];
+            const uint32_t kk = (uint32_t)(v >> 32);
+            r += st[j] ? 1u : 0u;
+            vf[(uint32_t)v] = kk == okey ? -1 : (int32_t)(r - 1);
+            if (st[j]) {  // this voxel's points in index order: the sequential fp32 sums
+                float sx = 0.f, sy = 0.f, sz = 0.f;
+                int64_t e = i;
+                for (; e < size && key_at(e) == kk; ++e) {
+                    float px, py, pz;
+                    if (staged) {
+                        px = L.xyz[3 * e];
+                        py = L.xyz[3 * e + 1];
+                        pz = L.xyz[3 * e + 2];
+                    } else {
+                        const int64_t idx = (uint32_t)seq[e];
+                        px = p[3 * idx];
+                        py = p[3 * idx + 1];
+                        pz = p[3 * idx + 2];
+                    }
+                    sx = __fadd_rn(sx, px);
+                    sy = __fadd_rn(sy, py);
+                    sz = __fadd_rn(sz, pz);
+                }
+                const int64_t o = r - 1;
+                const float c = (float)(e - i);
+                cf[3 * o] = __fdiv_rn(sx, c);
+                cf[3 * o + 1] = __fdiv_rn(sy, c);
+                cf[3 * o + 2] = __fdiv_rn(sz, c);
+                nf[o] = (int32_t)(e - i);
+            }
+        }
+        carry += all;
+    }
+#ifdef VX_DIAG_PHASES
+    VX_STAMP(6);
+    if (tid == 0)  // diagnostic build only: phase cycles into the scratch tail of the counts output
+    {
+        for (int k = 0; k < 6; ++k) nf[n - 1 - (8 * b + k)] = (int32_t)(ts[k + 1] - ts[k]);
+        nf[n - 1 - (8 * b + 6)] = (int32_t)spins_dbg;
+        nf[n - 1 - (8 * b + 7)] = (int32_t)(ts[4] & 0x7fffffff);  // look-back start (absolute, low bits)
+    }
+#endif
+#undef VX_STAMP
 }
 
 }  // namespace
@@ -393,15 +687,23 @@ __global__ __launch_bounds__(VT) void vb_centroid_kernel(const float *__restrict
 // workspace bytes of lidar_voxel_downsample_batch_f32 for (batch, n)
 LIDAR_EXPORT uint64_t lidar_voxel_batch_workspace_bytes(int64_t batch, int64_t n)
 {
-    const int64_t ntiles = (n + TILE - 1) / TILE;
-    return (uint64_t)batch * ((uint64_t)n * 16 + (uint64_t)(n + 1) * 4 + (uint64_t)257 * ntiles * 4 + MW * 4) + 2048;
+    const int64_t ntiles = (n + TILE - 1) / TILE, nb = (n + BUCKET - 1) / BUCKET;
+    lidar::Carver cv;
+    cv.take<uint32_t>(batch * NCH * 6);
+    cv.take<uint32_t>(batch * MW);
+    cv.take<uint32_t>(batch * n);
+    cv.take<uint16_t>(batch * ntiles * NBIN);
+    cv.take<uint32_t>(batch * (NBIN + 1));
+    cv.take<uint64_t>(batch * n);
+    cv.take<uint64_t>(batch * n);
+    cv.take<uint64_t>(batch * nb);
+    return cv.off;
 }
 
 // Voxel downsampling of `batch` frames of n points (xyz (batch, n, 3) fp32), all on the device:
 // voxel_id (batch, n) int32, centroids (batch, n, 3) and counts (batch, n) with the first nvox[f]
 // rows of frame f valid, nvox (batch,) int32 (-1: the frame's extent is not finite or its voxel grid
-// has 2^32 keys or more; voxel_id -1: a point outside every bin).
-// Same results as lidar_voxel_downsample_f32 per frame.
+// has 2^32 - 1 keys or more; voxel_id -1: a point outside every bin).
 LIDAR_EXPORT int lidar_voxel_downsample_batch_f32(lidar_handle *h, const float *xyz, int64_t batch, int64_t n,
                                                   double voxel, int32_t *voxel_id, float *centroids, int32_t *counts,
                                                   int32_t *nvox, void *stream)
@@ -414,47 +716,32 @@ LIDAR_EXPORT int lidar_voxel_downsample_batch_f32(lidar_handle *h, const float *
     ON_DEVICE(h->device);
     hipStream_t s = static_cast<hipStream_t>(stream);
     const int ntiles = (int)((n + TILE - 1) / TILE);
+    const int64_t nb = (n + BUCKET - 1) / BUCKET;
+    REQUIRE((int64_t)frame_grid(batch, std::max<int64_t>(ntiles, nb)) < 0x7fffffff,
+            "lidar_voxel_downsample_batch_f32: batch * n too large");
     lidar::Carver cv;
-    const uint64_t ok0 = cv.take<uint32_t>(batch * n), ov0 = cv.take<uint32_t>(batch * n);
-    const uint64_t ok1 = cv.take<uint32_t>(batch * n), ov1 = cv.take<uint32_t>(batch * n);
-    const uint64_t ost = cv.take<uint32_t>(batch * (n + 1));
-    const uint64_t oh = cv.take<uint32_t>(batch * 256 * (int64_t)ntiles);
-    const uint64_t om = cv.take<uint32_t>(batch * MW);
-    const uint64_t otc = cv.take<uint32_t>(batch * (int64_t)ntiles);
+    const uint64_t opart = cv.take<uint32_t>(batch * NCH * 6), ometa = cv.take<uint32_t>(batch * MW);
+    const uint64_t okey = cv.take<uint32_t>(batch * n), oth = cv.take<uint16_t>(batch * ntiles * NBIN);
+    const uint64_t obase = cv.take<uint32_t>(batch * (NBIN + 1));
+    const uint64_t opairs = cv.take<uint64_t>(batch * n), oscr = cv.take<uint64_t>(batch * n);
+    const uint64_t oflags = cv.take<uint64_t>(batch * nb);
     char *base = static_cast<char *>(lidar::workspace(h, cv.off));
     if (!base) return LIDAR_ENOMEM;
-    auto U = [&](uint64_t o) { return reinterpret_cast<uint32_t *>(base + o); };
-    uint32_t *meta = U(om), *hist = U(oh);
-    const unsigned chunks = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + VT * 8 - 1) / (VT * 8), 256));
-    const dim3 sg(chunks, (unsigned)batch);
-    hipLaunchKernelGGL(vb_init_kernel, dim3((unsigned)((batch + 255) / 256)), dim3(256), 0, s, meta, (int)batch);
-    hipLaunchKernelGGL(vb_bbox_kernel, sg, dim3(VT), 0, s, xyz, n, meta);
-    const dim3 tg((unsigned)ntiles, (unsigned)batch);
-    // keys + the histogram of digit 0
-    hipLaunchKernelGGL(vb_keys_kernel, tg, dim3(ST), 0, s, xyz, n, voxel, meta, U(ok0), U(ov0), hist, ntiles);
-    uint32_t *kin = U(ok0), *vin = U(ov0), *kout = U(ok1), *vout = U(ov1);
-    const bool fused = ntiles <= kFuseScanTiles;
-    for (int shift = 0; shift < 32; shift += 8) {  // frames past their key bits skip (per-frame parity)
-        if (shift > 0) hipLaunchKernelGGL(vb_hist_kernel, tg, dim3(VT), 0, s, kin, n, shift, ntiles, meta, hist);
-        if (fused) {
-            hipLaunchKernelGGL(vb_scatter_kernel<true>, tg, dim3(ST), 0, s, kin, vin, kout, vout, n, shift, ntiles, meta,
-                               hist);
-        } else {
-            hipLaunchKernelGGL(vb_scan_kernel, dim3((unsigned)batch), dim3(ST), 0, s, hist, ntiles, shift, meta);
-            hipLaunchKernelGGL(vb_scatter_kernel<false>, tg, dim3(ST), 0, s, kin, vin, kout, vout, n, shift, ntiles,
-                               meta, hist);
-        }
-        std::swap(kin, kout);
-        std::swap(vin, vout);
-    }
-    hipLaunchKernelGGL(vb_runs_count_kernel, tg, dim3(ST), 0, s, U(ok0), U(ov0), U(ok1), U(ov1), n, ntiles, meta,
-                       U(otc));
-    hipLaunchKernelGGL(vb_runs_write_kernel, tg, dim3(ST), 0, s, U(ok0), U(ov0), U(ok1), U(ov1), n, ntiles, meta,
-                       U(otc), voxel_id, U(ost), nvox);
-    // one thread per (possible) voxel: the gathers of a voxel's points are a dependent chain
-    const dim3 cg((unsigned)((n + VT - 1) / VT), (unsigned)batch);
-    hipLaunchKernelGGL(vb_centroid_kernel, cg, dim3(VT), 0, s, xyz, n, U(ov0), U(ov1), meta, U(ost), centroids,
-                       counts);
+    Ws w;
+    w.part = reinterpret_cast<uint32_t *>(base + opart);
+    w.meta = reinterpret_cast<uint32_t *>(base + ometa);
+    w.key = reinterpret_cast<uint32_t *>(base + okey);
+    w.thist = reinterpret_cast<uint16_t *>(base + oth);
+    w.base = reinterpret_cast<uint32_t *>(base + obase);
+    w.pairs = reinterpret_cast<uint64_t *>(base + opairs);
+    w.scratch = reinterpret_cast<uint64_t *>(base + oscr);
+    w.flags = reinterpret_cast<uint64_t *>(base + oflags);
+    hipLaunchKernelGGL(vx_bbox_kernel, dim3(NCH, (unsigned)batch), dim3(BT), 0, s, xyz, n, w, nb);
+    hipLaunchKernelGGL(vx_keys_kernel, dim3(frame_grid(batch, ntiles)), dim3(KT), 0, s, xyz, n, voxel, w, ntiles,
+                       batch);
+    hipLaunchKernelGGL(vx_scatter_kernel, dim3(frame_grid(batch, ntiles)), dim3(KT), 0, s, n, w, ntiles, batch);
+    hipLaunchKernelGGL(vx_bucket_kernel, dim3(frame_grid(batch, nb)), dim3(UT), 0, s, xyz, n, w, voxel_id, centroids,
+                       counts, nvox, batch);
     LAUNCH_CHECK();
     return LIDAR_OK;
 }

@@ -377,6 +377,40 @@ def test_voxel_downsample_batch_vs_oracle(cuda):
     assert nv.cpu().numpy().tolist() == [-1, -1]
 
 
+@pytest.mark.parametrize("n", [150001, 300000])
+def test_voxel_downsample_large_frames_vs_oracle(cuda, n):
+    """Real LiDAR frame sizes (100k-300k points): many tiles and buckets per frame, through
+    the batched path (a uniform frame, a clumped frame whose dense core overflows a bucket's LDS sort,
+    and a frame with points outside every bin) and the drop-in dp.voxel_downsample."""
+    import torch
+    from lidar_ai_recommendation_software_amd import pointnet2 as pn
+    rng = np.random.default_rng(n)
+    x = rng.uniform(-20, 20, (2, n, 3)).astype(np.float32)
+    x[1, : n // 2] *= np.float32(0.002)  # half the frame inside ~0.1 m: a few coarse bins hold it
+    xo, vo = _outside_frame(n)
+    for xb, voxel in ((x, 0.25), (x, 0.07), (xo[None], vo)):
+        c, vid, cnt, nv = (t.cpu().numpy() for t in pn.voxel_downsample_batch(torch.from_numpy(xb).to(cuda), voxel))
+        for f in range(len(xb)):
+            wc, wvid, wcnt = tier_n.voxel_downsample(xb[f], voxel)
+            assert nv[f] == len(wcnt), (voxel, f)
+            assert np.array_equal(vid[f], wvid) and np.array_equal(cnt[f, :nv[f]], wcnt), (voxel, f)
+            assert np.array_equal(c[f, :nv[f]].view(np.uint32), wc.view(np.uint32)), (voxel, f)
+    c, vid, cnt = dp.voxel_downsample(x[0], 0.25)
+    wc, wvid, wcnt = tier_n.voxel_downsample(x[0], 0.25)
+    assert np.array_equal(vid, wvid) and np.array_equal(cnt, wcnt) and np.array_equal(c, wc)
+
+
+def test_voxel_downsample_one_huge_voxel(cuda):
+    """Every point in one voxel (a voxel larger than the frame): one bucket holds the whole frame and
+    sorts it in global memory; the centroid is the index-order fp32 sum."""
+    x = uniform_frame(70000, 2, -1, 1).astype(np.float32)
+    for v in (100.0, 0.9):
+        c, vid, cnt = dp.voxel_downsample(x, v)
+        wc, wvid, wcnt = tier_n.voxel_downsample(x, v)
+        assert np.array_equal(vid, wvid) and np.array_equal(cnt, wcnt)
+        assert np.array_equal(c.view(np.uint32), wc.view(np.uint32))
+
+
 @pytest.mark.parametrize("name", list(VOXEL_CASES))
 def test_voxel_downsample_pinned_to_reference(cuda, name):
     """SURVEY §8a N1's voxel key is calculate_grid_density's grid hash extended to z: the GPU's voxel

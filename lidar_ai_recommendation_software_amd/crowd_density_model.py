@@ -60,9 +60,10 @@ class CrowdDensityModel:
         return ((p - (lo + hi) / 2) / max(float((hi - lo).max()) / 2, 1e-9)).astype(np.float32)
 
     def encode(self, points):
-        """PointNet++ (SSG/MSG) global feature of one frame over ALL its points (any N >= 1;
-        SA levels take max(1, N/16) and max(1, N/64) centres).  Not part of the reference
-        (SURVEY §8a N6)."""
+        """PointNet++ (SSG/MSG) global feature of one frame over ALL its points (1 <= N <= 4 194 304:
+        the FPS kernel's limit, lidar_fps_ex_f32; frames above 262 144 points run it on buckets of
+        64 x PPL points; a larger frame raises LidarError naming the limit).  SA levels take
+        max(1, N/16) and max(1, N/64) centres.  Not part of the reference."""
         import torch
         from . import pointnet2 as pn
         if self._net is None:

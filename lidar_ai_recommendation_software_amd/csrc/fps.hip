@@ -37,6 +37,10 @@ namespace {
 // across waves; the merge is an LDS atomic max).  lidar_fps_ex_f32 also offers 512 (8 waves,
 // 2 buckets per lane: ~25 % longer steps, half the CU footprint beside other kernels)
 constexpr int kThreads = FPS_THREADS;
+// one point per lane: 8 bucket slots per lane of a 512-thread workgroup (the register budget) hold
+// 262 144 points; larger frames take buckets of 64 x PPL points (PPL 2 .. 16: up to 4 Mi points)
+constexpr int64_t kMaxBucketPoints = 8 * 512 * 64;
+constexpr int64_t kMaxFpsPoints = 16 * kMaxBucketPoints;
 constexpr int kGrid = 16;  // Morton cells per axis for the bucket ordering
 constexpr int kCells = kGrid * kGrid * kGrid;
 
@@ -63,8 +67,9 @@ __device__ __forceinline__ float gap(float q, float lo, float hi)
 
 // Update K active buckets of one owner slot (their loads issued together, their DPP
 // reductions interleaved): new distances against q, bucket max + its lowest-index argmax
-// point into the owner lane's registers.
-template <int K, int NW>
+// point into the owner lane's registers.  A bucket is 64 lanes x PPL points (lane l holds the
+// bucket's points j * 64 + l: coalesced per j); bp encodes the argmax member as j * 64 + lane.
+template <int K, int NW, int PPL = 1>
 __device__ __forceinline__ void update_batch(uint64_t &mask, const FrameWs &W, int wave, int q, int lane,
                                              float qx, float qy, float qz, float &bd, uint32_t &bi, float *bx,
                                              int &bp, int target, bool &hit)
@@ -73,39 +78,54 @@ __device__ __forceinline__ void update_batch(uint64_t &mask, const FrameWs &W, i
     // (dist -1: never the max, never updated since every real d >= 0)
     int bbs[K];
     uint32_t pos[K];  // unsigned: the loads take the SGPR base + 32-bit offset form
-    float4 P[K];
-    float D[K];
-    uint32_t I[K];
+    float4 P[K][PPL];
+    float D[K][PPL];
 #pragma unroll
     for (int u = 0; u < K; ++u) {
         bbs[u] = __ffsll((unsigned long long)mask) - 1;
         mask &= mask - 1;
-        pos[u] = (uint32_t)((wave + NW * (q * 64 + bbs[u])) * 64 + lane);
+        pos[u] = (uint32_t)((wave + NW * (q * 64 + bbs[u])) * 64 * PPL + lane);
     }
 #pragma unroll
-    for (int u = 0; u < K; ++u) {
-        P[u] = W.p[pos[u]];
-        D[u] = W.d[pos[u]];
-    }
+    for (int u = 0; u < K; ++u)
 #pragma unroll
-    for (int u = 0; u < K; ++u) I[u] = __float_as_uint(P[u].w);
-    // distances in bit space (>= +0 or the -1 sentinel: signed int order = float order)
-    int od[K], dm[K];
+        for (int j = 0; j < PPL; ++j) {
+            P[u][j] = W.p[pos[u] + 64 * j];
+            D[u][j] = W.d[pos[u] + 64 * j];
+        }
+    // distances in bit space (>= +0 or the -1 sentinel: signed int order = float order); per lane
+    // the best of its PPL points (max dist, lowest index)
+    int od[K], dm[K], lj[K];
+    uint32_t I[K];
     // a bucket's key (max dist, lowest index) can only change if its argmax member got
     // closer: distances only decrease, so with that member untouched the max and its
-    // lowest-index holder stand — the reduction is skipped (bp = the member's lane, -1 unknown)
+    // lowest-index holder stand — the reduction is skipped (bp = the member, -1 unknown)
     bool redo[K];
 #pragma unroll
     for (int u = 0; u < K; ++u) {
-        // d >= +0 or NaN; the sign bit cleared, a NaN d (inf - inf) orders above every dist and never
-        // replaces one, as in the oracle (a bare bit compare let a negative NaN in)
-        const int db = __float_as_int(lidar::dist2f(P[u].x, P[u].y, P[u].z, qx, qy, qz)) & 0x7fffffff;
-        od[u] = min(db, __float_as_int(D[u]));
-        const bool lower = od[u] != __float_as_int(D[u]);
-        if (lower) W.d[pos[u]] = __int_as_float(od[u]);  // only changed members dirty a line
-        const uint64_t ch = __ballot(lower);
+        od[u] = -1;
+        I[u] = 0xffffffffu;
+        lj[u] = 0;
+        uint64_t chm = 0;
         const int bpu = __builtin_amdgcn_readlane(bp, bbs[u]);
-        redo[u] = bpu < 0 || ((ch >> bpu) & 1ull);
+#pragma unroll
+        for (int j = 0; j < PPL; ++j) {
+            // d >= +0 or NaN; the sign bit cleared, a NaN d (inf - inf) orders above every dist and never
+            // replaces one, as in the oracle (a bare bit compare let a negative NaN in)
+            const int db = __float_as_int(lidar::dist2f(P[u][j].x, P[u][j].y, P[u][j].z, qx, qy, qz)) & 0x7fffffff;
+            const int o = min(db, __float_as_int(D[u][j]));
+            const bool lower = o != __float_as_int(D[u][j]);
+            if (lower) W.d[pos[u] + 64 * j] = __int_as_float(o);  // only changed members dirty a line
+            const uint64_t ch = __ballot(lower);
+            if (PPL == 1 || (bpu >> 6) == j) chm = ch;
+            const uint32_t ij = __float_as_uint(P[u][j].w);
+            if (PPL == 1 || o > od[u] || (o == od[u] && ij < I[u])) {
+                od[u] = o;
+                I[u] = ij;
+                lj[u] = j;
+            }
+        }
+        redo[u] = bpu < 0 || ((chm >> (bpu & 63)) & 1ull);
     }
 #pragma unroll
     for (int u = 0; u < K; ++u) {
@@ -124,12 +144,17 @@ __device__ __forceinline__ void update_batch(uint64_t &mask, const FrameWs &W, i
             const uint32_t mi = lidar::wave_min_u32_dpp(od[u] == dm[u] ? I[u] : 0xffffffffu);
             wl = __ffsll((unsigned long long)__ballot(od[u] == dm[u] && I[u] == mi)) - 1;
         }
+        float4 pb = P[u][0];
+#pragma unroll
+        for (int j = 1; j < PPL; ++j)
+            if (lj[u] == j) pb = P[u][j];
         const uint32_t wi = (uint32_t)__builtin_amdgcn_readlane((int)I[u], wl);
-        const float wx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(P[u].x), wl));
-        const float wy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(P[u].y), wl));
-        const float wz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(P[u].z), wl));
+        const float wx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pb.x), wl));
+        const float wy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pb.y), wl));
+        const float wz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pb.z), wl));
+        const int wj = PPL == 1 ? 0 : __builtin_amdgcn_readlane(lj[u], wl);
         const bool me = lane == bbs[u];
-        bp = me ? wl : bp;
+        bp = me ? wj * 64 + wl : bp;
         bd = me ? __int_as_float(dm[u]) : bd;
         bi = me ? wi : bi;
         bx[0] = me ? wx : bx[0];
@@ -149,11 +174,10 @@ __device__ __forceinline__ uint64_t stamp()
 // by 16^3 Morton cell into W (padded to whole buckets with dist -1 sentinels).  Ends with a
 // barrier (hist is free afterwards).
 template <int T>
-__device__ __forceinline__ void fps_prologue(const float *__restrict__ p, int n, const FrameWs &W,
+__device__ __forceinline__ void fps_prologue(const float *__restrict__ p, int n, int npad, const FrameWs &W,
                                              uint32_t *hist, float (*red)[T / 64], uint32_t *wsum)
 {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int npad = (n + 63) / 64 * 64;
     // ---- frame bounding box
     float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
     for (int i = tid; i < n; i += T) {
@@ -244,7 +268,7 @@ __device__ __forceinline__ void fps_prologue(const float *__restrict__ p, int n,
 // DIAG builds (lidar_diag_fps_phases only) accumulate per-phase shader cycles per wave:
 // [0] bucket tests + active-bucket updates, [1] wave argmax + LDS publish, [2] barrier
 // wait, [3] 16-way merge, [4] active-bucket batches processed, [5] steps
-template <int T, int BPL, bool DIAG = false>
+template <int T, int BPL, bool DIAG = false, int PPL = 1>
 __global__ __launch_bounds__(T) void fps_bucket_kernel(const float *__restrict__ xyz,
                                                               int n, int npoint,
                                                               int32_t *__restrict__ out_idx,
@@ -279,7 +303,7 @@ __global__ __launch_bounds__(T) void fps_bucket_kernel(const float *__restrict__
     }
 
     float *wsb = ws + (int64_t)b * ws_stride;
-    const int npad = (n + 63) / 64 * 64;  // whole buckets; the tail holds sentinel points
+    const int npad = (n + 64 * PPL - 1) / (64 * PPL) * (64 * PPL);  // whole buckets; the tail holds sentinels
     FrameWs W{reinterpret_cast<float4 *>(wsb), wsb + 4 * (int64_t)npad};
 
     __shared__ uint32_t hist[kCells];
@@ -291,8 +315,8 @@ __global__ __launch_bounds__(T) void fps_bucket_kernel(const float *__restrict__
     __shared__ unsigned long long mkey[3];
     __shared__ __attribute__((aligned(16))) float mcrd[2][(T / 64)][4];
 
-    fps_prologue<T>(p, n, W, hist, red, wsum);
-    const int nb = (n + 63) / 64;
+    fps_prologue<T>(p, n, npad, W, hist, red, wsum);
+    const int nb = npad / (64 * PPL);
         // ---- per-bucket state in the owner lane: bucket = wave + 4 * (q * 64 + lane)
     float bmin[BPL][3], bmax[BPL][3], bx[BPL][3], bd[BPL];
     uint32_t bi[BPL];
@@ -311,13 +335,19 @@ __global__ __launch_bounds__(T) void fps_bucket_kernel(const float *__restrict__
     static_assert(kCells >= 512 * 6, "bbox pass table");
     for (int p0 = 0; p0 < nb; p0 += 512) {
         for (int bucket = p0 + wave; bucket < nb && bucket < p0 + 512; bucket += (T / 64)) {
-            const int pos = bucket * 64 + lane;
             float v[3] = {INFINITY, INFINITY, INFINITY}, u[3] = {-INFINITY, -INFINITY, -INFINITY};
-            if (pos < n) {
-                const float4 P = W.p[pos];
-                v[0] = u[0] = P.x;
-                v[1] = u[1] = P.y;
-                v[2] = u[2] = P.z;
+#pragma unroll
+            for (int j = 0; j < PPL; ++j) {
+                const int pos = (bucket * PPL + j) * 64 + lane;
+                if (pos < n) {
+                    const float4 P = W.p[pos];
+                    v[0] = fminf(v[0], P.x);
+                    v[1] = fminf(v[1], P.y);
+                    v[2] = fminf(v[2], P.z);
+                    u[0] = fmaxf(u[0], P.x);
+                    u[1] = fmaxf(u[1], P.y);
+                    u[2] = fmaxf(u[2], P.z);
+                }
             }
 #pragma unroll
             for (int a = 0; a < 3; ++a) {
@@ -396,18 +426,19 @@ __global__ __launch_bounds__(T) void fps_bucket_kernel(const float *__restrict__
             while (mask) {  // wave-uniform
                 if constexpr (DIAG) dacc[4]++;
                 const int cnt = __popcll(mask);
-                if (cnt >= 4)
-                    update_batch<4, T / 64>(mask, W, wave, q, lane, qx, qy, qz, bd[q], bi[q], bx[q], bp[q], target,
-                                             wave_dirty);
-                else if (cnt == 3)  // one round trip instead of 2 + 1
-                    update_batch<3, T / 64>(mask, W, wave, q, lane, qx, qy, qz, bd[q], bi[q], bx[q], bp[q], target,
-                                             wave_dirty);
-                else if (cnt >= 2)
-                    update_batch<2, T / 64>(mask, W, wave, q, lane, qx, qy, qz, bd[q], bi[q], bx[q], bp[q], target,
-                                             wave_dirty);
+                // up to 4 loads per lane in flight: K buckets of PPL points
+                if (PPL == 1 && cnt >= 4)
+                    update_batch<4, T / 64, PPL>(mask, W, wave, q, lane, qx, qy, qz, bd[q], bi[q], bx[q], bp[q],
+                                                 target, wave_dirty);
+                else if (PPL == 1 && cnt == 3)  // one round trip instead of 2 + 1
+                    update_batch<3, T / 64, PPL>(mask, W, wave, q, lane, qx, qy, qz, bd[q], bi[q], bx[q], bp[q],
+                                                 target, wave_dirty);
+                else if (PPL <= 2 && cnt >= 2)
+                    update_batch<2, T / 64, PPL>(mask, W, wave, q, lane, qx, qy, qz, bd[q], bi[q], bx[q], bp[q],
+                                                 target, wave_dirty);
                 else
-                    update_batch<1, T / 64>(mask, W, wave, q, lane, qx, qy, qz, bd[q], bi[q], bx[q], bp[q], target,
-                                             wave_dirty);
+                    update_batch<1, T / 64, PPL>(mask, W, wave, q, lane, qx, qy, qz, bd[q], bi[q], bx[q], bp[q],
+                                                 target, wave_dirty);
             }
         }
         if constexpr (DIAG) {
@@ -452,11 +483,11 @@ __global__ __launch_bounds__(T) void fps_bucket_kernel(const float *__restrict__
             t0 = t1;
             __builtin_amdgcn_sched_barrier(0);
         }
-        // key: dist bits (d >= 0 orders as unsigned) | (2^18 - idx) << 4 | wave; a larger key
-        // is a larger distance, then a smaller index (n <= 2^18); empty slots carry field 0
+        // key: dist bits (d >= 0 orders as unsigned) | (2^27 - idx) << 4 | wave; a larger key
+        // is a larger distance, then a smaller index (n <= 2^27); empty slots carry field 0
         const int slot = cur3, cslot = it & 1;
         if (lane == 0) {
-            const uint32_t fld = w_i < (1u << 18) ? (1u << 18) - w_i : 0u;
+            const uint32_t fld = w_i < (1u << 27) ? (1u << 27) - w_i : 0u;
             const unsigned long long key =
                 ((unsigned long long)__float_as_uint(w_d) << 32) | (fld << 4) | (uint32_t)wave;
             mcrd[cslot][wave][0] = w_x;
@@ -483,7 +514,7 @@ __global__ __launch_bounds__(T) void fps_bucket_kernel(const float *__restrict__
                 cand = *reinterpret_cast<const float4 *>(mcrd[cslot][lane]);
             const int ww = __builtin_amdgcn_readfirstlane((int)(key & 15u));
             const float gdist = __uint_as_float((uint32_t)(key >> 32));
-            const uint32_t gidx = (1u << 18) - (((uint32_t)key) >> 4);
+            const uint32_t gidx = (1u << 27) - (((uint32_t)key) >> 4);
             qx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cand.x), ww));
             qy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cand.y), ww));
             qz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cand.z), ww));
@@ -726,7 +757,7 @@ __global__ __launch_bounds__(T) void fps_lazy_kernel(const float *__restrict__ x
     uint32_t *hist = reinterpret_cast<uint32_t *>(smem);
     LazyLds<T, BPL> &L = *reinterpret_cast<LazyLds<T, BPL> *>(smem);
 
-    fps_prologue<T>(p, n, W, hist, red, wsum);
+    fps_prologue<T>(p, n, npad, W, hist, red, wsum);
     const int nb = (n + 63) / 64;
     float bmin[BPL][3], bmax[BPL][3], bd[BPL];
     uint32_t bk[BPL];  // argmax lane (low byte, 0xff unknown) | pending count << 8 | oldest pending id << 16
@@ -886,7 +917,7 @@ __global__ __launch_bounds__(T) void fps_lazy_kernel(const float *__restrict__ x
         }
         const int slot = cur3, cslot = it & 1;
         if (lane == 0) {
-            const uint32_t fld = w_i < (1u << 18) ? (1u << 18) - w_i : 0u;
+            const uint32_t fld = w_i < (1u << 27) ? (1u << 27) - w_i : 0u;
             const unsigned long long key =
                 ((unsigned long long)__float_as_uint(w_d) << 32) | (fld << 4) | (uint32_t)wave;
             mcrd[cslot][wave][0] = w_x;
@@ -905,7 +936,7 @@ __global__ __launch_bounds__(T) void fps_lazy_kernel(const float *__restrict__ x
             if (lane < NW) cand = *reinterpret_cast<const float4 *>(mcrd[cslot][lane]);
             const int ww = __builtin_amdgcn_readfirstlane((int)(key & 15u));
             const float gdist = __uint_as_float((uint32_t)(key >> 32));
-            const uint32_t gidx = (1u << 18) - (((uint32_t)key) >> 4);
+            const uint32_t gidx = (1u << 27) - (((uint32_t)key) >> 4);
             qx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cand.x), ww));
             qy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cand.y), ww));
             qz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cand.z), ww));
@@ -958,7 +989,17 @@ static int launch_fps(const float *xyz, int64_t batch, int64_t n, int64_t npoint
         hipLaunchKernelGGL(kern, grid, block, 0, s, xyz, (int)n, (int)npoint, idx, new_xyz, first_zero, prefix_ok, ws,
                            stride, nullptr);
     };
-    if (lazy) {
+    if (n > kMaxBucketPoints) {
+        // large frames: 8 bucket slots per lane at 512 threads, each bucket 64 x PPL points
+        // (lidar_fps_ex_f32 sends every n > kMaxBucketPoints here with T = 512, lazy off)
+        if constexpr (T == 512) {
+            const int64_t ppl = (n + kMaxBucketPoints - 1) / kMaxBucketPoints;
+            if (ppl <= 2) go(fps_bucket_kernel<T, 8, false, 2>);
+            else if (ppl <= 4) go(fps_bucket_kernel<T, 8, false, 4>);
+            else if (ppl <= 8) go(fps_bucket_kernel<T, 8, false, 8>);
+            else go(fps_bucket_kernel<T, 8, false, 16>);
+        }
+    } else if (lazy) {
         if (nb <= lanes) go(fps_lazy_kernel<T, 1>);
         else if (nb <= 2 * lanes) go(fps_lazy_kernel<T, 2>);
         else if (nb <= 4 * lanes) go(fps_lazy_kernel<T, 4>);
@@ -974,9 +1015,15 @@ static int launch_fps(const float *xyz, int64_t batch, int64_t n, int64_t npoint
 }
 
 // workspace bytes lidar_fps_f32 / lidar_fps_ex_f32 take from the handle for (batch, n)
+static int64_t fps_stride(int64_t n)  // floats per frame: (x, y, z, index) + dist over whole buckets
+{
+    const int64_t unit = n > kMaxBucketPoints ? 64 * 16 : 64;
+    return lidar::align_up(5 * lidar::align_up(n, unit), 64);
+}
+
 LIDAR_EXPORT uint64_t lidar_fps_workspace_bytes(int64_t batch, int64_t n)
 {
-    return (uint64_t)(batch * lidar::align_up(5 * lidar::align_up(n, 64), 64)) * 4;
+    return (uint64_t)(batch * fps_stride(n)) * 4;
 }
 
 // threads: workgroup size per frame, 0 (the build default, 1024), 1024 or 512 — same results
@@ -986,17 +1033,22 @@ LIDAR_EXPORT int lidar_fps_ex_f32(lidar_handle *h, const float *xyz, int64_t bat
 {
     REQUIRE(h && xyz && idx, "lidar_fps_f32: null pointer");
     REQUIRE(batch >= 0 && n >= 1 && npoint >= 1, "lidar_fps_f32: need n >= 1 and npoint >= 1");
-    REQUIRE(n <= 4 * 65536, "lidar_fps_f32: n > 262144 points per frame");
-    const bool lazy = (threads & LIDAR_FPS_LAZY) != 0;
+    REQUIRE(n <= kMaxFpsPoints, "lidar_fps_f32: n > 4194304 points per frame");
+    bool lazy = (threads & LIDAR_FPS_LAZY) != 0;
     threads &= ~LIDAR_FPS_LAZY;
     if (threads == 0) threads = kThreads;
     REQUIRE(threads == 1024 || threads == 512, "lidar_fps_ex_f32: threads must be 0, 512 or 1024 (| LIDAR_FPS_LAZY)");
-    REQUIRE((n + 63) / 64 <= 8 * (int64_t)threads, "lidar_fps_f32: too many buckets for this workgroup size");
+    if (n > kMaxBucketPoints) {  // the large-frame kernel: 512 threads, eager
+        threads = 512;
+        lazy = false;
+    }
+    REQUIRE(n > kMaxBucketPoints || (n + 63) / 64 <= 8 * (int64_t)threads,
+            "lidar_fps_f32: too many buckets for this workgroup size");
     REQUIRE(batch <= 0x7fffffff, "lidar_fps_f32: batch too large");
     if (batch == 0) return LIDAR_OK;
     ON_DEVICE(h->device);
     REQUIRE(prefix_ok == nullptr || npoint <= n, "lidar_fps_f32: prefix_ok needs npoint <= n");
-    int64_t stride = lidar::align_up(5 * lidar::align_up(n, 64), 64);
+    const int64_t stride = fps_stride(n);
     float *ws = static_cast<float *>(lidar::workspace(h, (uint64_t)(batch * stride) * 4));
     if (!ws) return LIDAR_ENOMEM;
     hipStream_t s = static_cast<hipStream_t>(stream);

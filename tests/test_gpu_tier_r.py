@@ -528,6 +528,22 @@ def test_density_model_backbone_option(cuda, name):
     assert got.shape == (1024,) and np.all(np.abs(got - want) <= 1e-4 * np.abs(want) + 1e-4 * scale)
 
 
+def test_density_model_backbone_large_frame(cuda):
+    """The backbone over a frame of more than 262 144 inlier points: the SSG
+    stack runs over all of them (FPS on 64 x PPL-point buckets) and matches the oracle at 1e-4."""
+    from lidar_ai_recommendation_software_amd import pointnet2 as pn
+    pts = uniform_frame(300000, 5, -15, 15)
+    pd = dp.preprocess_lidar_data(pts)
+    assert len(pd["points"]) > 262144
+    m = CrowdDensityModel(backbone="ssg")
+    res = m.analyze(pd)
+    unit = CrowdDensityModel.normalise(pd["points"])
+    want, _ = tier_n.sa_stack(unit, {"levels": pn.resolve(pn.SSG, len(unit))}, m._net.weights)
+    got = res["backbone_feature"]
+    scale = np.sqrt(np.mean(want.astype(np.float64) ** 2)) + 1e-30
+    assert got.shape == (1024,) and np.all(np.abs(got - want) <= 1e-4 * np.abs(want) + 1e-4 * scale)
+
+
 def test_downsample_point_cloud_device_gather(cuda):
     """A13: the draw is the global legacy RNG's (same indices and RNG state as the reference),
     the gather runs on the GPU — numpy in / numpy out of any dtype, CUDA tensor in / out."""

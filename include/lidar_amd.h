@@ -236,6 +236,22 @@ int lidar_sa_group_mlp_bq_f32(lidar_handle *h, int32_t x1, const float *xyz, con
                               int32_t c2, int32_t c3, const void *packed, float *out, int64_t out_stride,
                               int64_t out_offset, int32_t *out_idx, void *stream);
 
+/* A set-abstraction branch of any shape (csrc/sa_generic.hip; the fused kernels above cover six):
+ * grouped rows -> the dense GEMMs (lidar_dense_x3f_f32 / lidar_dense_f32, one per layer, ReLU)
+ * -> the max over each group's nsample rows.  Replaces, for every other (c1, c2, c3, nsample),
+ * pointnet2's QueryAndGroup(use_xyz) + shared MLP + max_pool2d of PointnetSAModuleMSG.forward.
+ *
+ * lidar_sa_group_rows_f32: rows_out[(b*m + j)*nsample + s] = [feat[b*n + idx] (cfeat columns,
+ * row stride ldf; feat may be NULL when cfeat = 0), xyz[b*n + idx] - centres[b*m + j] (fp32),
+ * zeros to ldr]; rows_out rows [batch*m*nsample, rows) are zeroed.  ldr % 4 == 0, ldr >= cfeat + 3.
+ * lidar_group_max_f32: out[g*ldo + out_offset + c] = max_s in[(g*nsample + s)*ldi + c], c < C,
+ * g < groups (a NaN propagates). */
+int lidar_sa_group_rows_f32(lidar_handle *h, const float *feat, int64_t ldf, int32_t cfeat, const float *xyz,
+                            const float *centres, const int32_t *idx, int64_t batch, int64_t n, int64_t m,
+                            int32_t nsample, float *rows_out, int64_t rows, int64_t ldr, void *stream);
+int lidar_group_max_f32(lidar_handle *h, const float *in, int64_t ldi, int64_t groups, int32_t nsample, int32_t c,
+                        float *out, int64_t ldo, int64_t out_offset, void *stream);
+
 /* y (batch*m, ldy) columns [col0, col0+3) = xyz rows; columns [col0+3, ldy) zeroed —
  * builds group_all's input [feats, xyz, 0-pad] next to features already in y. */
 int lidar_concat_xyz_pad_f32(lidar_handle *h, const float *xyz, int64_t rows, float *y,

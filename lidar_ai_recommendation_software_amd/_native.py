@@ -74,6 +74,8 @@ SIGNATURES = {
     "lidar_mlp_pack_x3_f32": [I32, I32, I32, I32, P, P, P, P, P, P, P],
     "lidar_sa_group_mlp_x3_f32": [P, I32, P, I64, P, P, I64, I64, I64, I32, I32, I32, I32, P, P, I64, I64, P],
     "lidar_concat_xyz_pad_f32": [P, P, I64, P, I64, I64, P],
+    "lidar_sa_group_rows_f32": [P, P, I64, I32, P, P, P, I64, I64, I64, I32, P, I64, I64, P],
+    "lidar_group_max_f32": [P, P, I64, I64, I32, I32, P, I64, I64, P],
     "lidar_voxel_downsample_f32": [P, P, I64, F64, P, P, P, P, P],
     "lidar_voxel_batch_workspace_bytes": [I64, I64],
     "lidar_voxel_downsample_batch_f32": [P, P, I64, I64, F64, P, P, P, P, P],

@@ -40,7 +40,8 @@ namespace {
 constexpr int BT = 256;            // bbox threads
 constexpr int NCH = 16;            // bbox chunks per frame
 constexpr int KT = 1024;           // keys / scatter threads
-constexpr int TILE = 4096;         // points per keys / scatter workgroup
+constexpr int TILE = 8192;         // points per keys / scatter workgroup (one round of the chip at B = 32)
+constexpr int PPT = TILE / KT;     // points per keys / scatter thread
 constexpr int HB = 12;             // coarse-bin bits of the key range
 constexpr int NBIN = 1 << HB;      // coarse bins per frame
 constexpr int BPT = NBIN / KT;     // coarse bins per scatter thread (its scan)
@@ -67,7 +68,7 @@ struct Ws {  // per-batch workspace, every array frame-major
     uint32_t *part;    // [F][NCH][6] bbox partials (monotone bits)
     uint32_t *meta;    // [F][MW]
     uint32_t *key;     // [F][n]
-    uint16_t *thist;   // [F][T][NBIN] tile histograms of the coarse bins (a tile holds <= 4096 points)
+    uint16_t *thist;   // [F][T][NBIN] tile histograms of the coarse bins (a tile holds <= 8192 points)
     uint32_t *base;    // [F][NBIN + 1] start of every coarse bin in bucket order
     uint64_t *pairs;   // [F][n] (key << 32 | index), coarse-bin order
     uint64_t *scratch; // [F][n] the global sort's other buffer
@@ -196,11 +197,18 @@ __global__ __launch_bounds__(KT) void vx_keys_kernel(const float *__restrict__ x
     if (!g.ok) return;  // whole workgroup (uniform)
     const float *p = xyz + (int64_t)f * n * 3;
     uint32_t *k = w.key + (int64_t)f * n;
+    float q[PPT][3];  // every load in flight before the first key
 #pragma unroll
-    for (int j = 0; j < TILE / KT; ++j) {
+    for (int j = 0; j < PPT; ++j) {
+        const int64_t i = (int64_t)t * TILE + j * KT + tid;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) q[j][a] = i < n ? p[3 * i + a] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < PPT; ++j) {
         const int64_t i = (int64_t)t * TILE + j * KT + tid;
         if (i < n) {
-            uint32_t kk = lidar_vox::key(g, p[3 * i], p[3 * i + 1], p[3 * i + 2]);
+            uint32_t kk = lidar_vox::key(g, q[j][0], q[j][1], q[j][2]);
             kk = kk == lidar_vox::kOutside ? okey : kk;  // sorts after every voxel's key
             k[i] = kk;
             atomicAdd(&hist[kk >> hs], 1u);
@@ -252,13 +260,18 @@ __global__ __launch_bounds__(KT) void vx_scatter_kernel(int64_t n, Ws w, int nti
     __syncthreads();
     const uint32_t *k = w.key + (int64_t)f * n;
     uint64_t *pr = w.pairs + (int64_t)f * n;
+    uint32_t kv[PPT];
 #pragma unroll
-    for (int j = 0; j < TILE / KT; ++j) {
+    for (int j = 0; j < PPT; ++j) {
+        const int64_t i = (int64_t)t * TILE + j * KT + tid;
+        kv[j] = i < n ? k[i] : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < PPT; ++j) {
         const int64_t i = (int64_t)t * TILE + j * KT + tid;
         if (i < n) {
-            const uint32_t kk = k[i];
-            const uint32_t pos = atomicAdd(&off[kk >> hs], 1u);
-            pr[pos] = ((uint64_t)kk << 32) | (uint32_t)i;
+            const uint32_t pos = atomicAdd(&off[kv[j] >> hs], 1u);
+            pr[pos] = ((uint64_t)kv[j] << 32) | (uint32_t)i;
         }
     }
 }
@@ -375,6 +388,7 @@ struct BucketLds {
     uint64_t s[CAP];         // counting-sort output
     uint32_t cnt[KMAX];      // counting-sort counters / starts (the radix path's digit tables)
     float xyz[CAP * 3];      // the bucket's points, for the centroid walks
+    uint16_t vstart[CAP + 1];  // the staged emit: voxel v's first sorted position, then the voxels' end
 };
 
 __global__ __launch_bounds__(UT) void vx_bucket_kernel(const float *__restrict__ xyz, int64_t n, Ws w,
@@ -387,11 +401,13 @@ __global__ __launch_bounds__(UT) void vx_bucket_kernel(const float *__restrict__
     if (!frame_part(batch, nb, f, b)) return;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 #ifdef VX_DIAG_PHASES
-    uint64_t ts[7];
+    uint64_t ts[8], rt[8];
     auto stamp = [&](int k) {
-        uint64_t t;
+        uint64_t t, r;
         asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r)::"memory");
         ts[k] = t;
+        rt[k] = r;
     };
 #define VX_STAMP(k) stamp(k)
 #else
@@ -404,7 +420,6 @@ __global__ __launch_bounds__(UT) void vx_bucket_kernel(const float *__restrict__
         return;  // every bucket of the frame returns: nothing waits on this frame's look-back words
     }
     const uint32_t okey = m[1];
-    const int hs = (int)m[2];
     __shared__ __attribute__((aligned(16))) BucketLds L;
     __shared__ uint32_t rng[4];
     __shared__ uint32_t red[UT / 64];
@@ -415,58 +430,69 @@ __global__ __launch_bounds__(UT) void vx_bucket_kernel(const float *__restrict__
 #endif
     // the bucket: coarse bins whose start s lies in [b S, (b + 1) S), S = n / nb (every workgroup of
     // the frame evaluates the same monotone float expression, so the buckets tile the bins exactly)
-    if (tid < 4) rng[tid] = tid < 2 ? (uint32_t)n : (uint32_t)NBIN;
+    if (tid < 4) rng[tid] = tid < 3 ? (tid < 2 ? (uint32_t)n : 0xffffffffu) : 0u;  // [2], [3]: key min / max
     if (tid == 0) flag = 0;
     __syncthreads();
     {
         const float inv = (float)nb / (float)n;
         const uint32_t *bs = w.base + (int64_t)f * (NBIN + 1);
-        uint32_t m0 = (uint32_t)n, m1 = (uint32_t)n, c0 = NBIN, c1 = NBIN;
+        uint32_t m0 = (uint32_t)n, m1 = (uint32_t)n;
         uint32_t sv[NBIN / UT];
 #pragma unroll
         for (int j = 0; j < NBIN / UT; ++j) sv[j] = bs[NBIN - 1 - tid - j * UT];  // all loads in flight
 #pragma unroll
         for (int j = 0; j < NBIN / UT; ++j) {  // descending bins: the min is the last hit
-            const int c = NBIN - 1 - tid - j * UT;
             const int64_t bk = min<int64_t>((int64_t)((float)sv[j] * inv), nb - 1);
-            if (bk >= b) {
-                m0 = sv[j];
-                c0 = (uint32_t)c;
-            }
-            if (bk >= b + 1) {
-                m1 = sv[j];
-                c1 = (uint32_t)c;
-            }
+            if (bk >= b) m0 = sv[j];
+            if (bk >= b + 1) m1 = sv[j];
         }
-        // wave minima first: 512 threads on 4 LDS words would serialise ~2 000 atomics
+        // wave minima first: 512 threads on 2 LDS words would serialise ~1 000 atomics
         m0 = (uint32_t)lidar::wave_min_u32_dpp(m0);
         m1 = (uint32_t)lidar::wave_min_u32_dpp(m1);
-        c0 = (uint32_t)lidar::wave_min_u32_dpp(c0);
-        c1 = (uint32_t)lidar::wave_min_u32_dpp(c1);
         if (lane == 0) {
             atomicMin(&rng[0], m0);
             atomicMin(&rng[1], m1);
-            atomicMin(&rng[2], c0);
-            atomicMin(&rng[3], c1);
         }
     }
     __syncthreads();
     VX_STAMP(1);
     const int64_t p0 = rng[0], size = (int64_t)rng[1] - rng[0];
-    const uint64_t k0 = (uint64_t)rng[2] << hs, krange = (uint64_t)(rng[3] - rng[2]) << hs;
     const uint64_t *gp = w.pairs + (int64_t)f * n + p0;
     const float *p = xyz + (int64_t)f * n * 3;
     const uint64_t *seq;   // the bucket sorted by (key, index): LDS or global
     bool staged = false;   // xyz of the sorted pairs in L.xyz
     if (size <= CAP) {
+        // the pairs and their points' xyz (the gathers fly while the keys sort), and the range of the
+        // keys they hold (not of their coarse bins: the first and last buckets' bins reach over the
+        // grid's empty margins, past the counting sort's range)
+        uint64_t v[CAP / UT];
+        float g[CAP / UT][3];
         {
-            uint64_t v[CAP / UT];
+            uint32_t kmin = 0xffffffffu, kmax = 0u;
 #pragma unroll
             for (int j = 0; j < CAP / UT; ++j) v[j] = tid + j * UT < size ? gp[tid + j * UT] : 0ull;
 #pragma unroll
+            for (int j = 0; j < CAP / UT; ++j) {
+                const int64_t idx = (uint32_t)v[j];  // 0 past the end
+#pragma unroll
+                for (int c = 0; c < 3; ++c) g[j][c] = p[3 * idx + c];
+            }
+#pragma unroll
             for (int j = 0; j < CAP / UT; ++j)
-                if (tid + j * UT < size) L.a[tid + j * UT] = v[j];
+                if (tid + j * UT < size) {
+                    const uint32_t kk = (uint32_t)(v[j] >> 32);
+                    kmin = min(kmin, kk);
+                    kmax = max(kmax, kk);
+                }
+            kmin = lidar::wave_min_u32_dpp(kmin);
+            kmax = ~lidar::wave_min_u32_dpp(~kmax);
+            if (lane == 0) {
+                atomicMin(&rng[2], kmin);
+                atomicMax(&rng[3], kmax);
+            }
         }
+        __syncthreads();
+        const uint64_t k0 = rng[2], krange = size ? (uint64_t)rng[3] - rng[2] + 1 : 0;
         const bool counting = krange <= KMAX;
         if (counting)
             for (int64_t c = tid; c < (int64_t)krange; c += UT) L.cnt[c] = 0;
@@ -478,7 +504,7 @@ __global__ __launch_bounds__(UT) void vx_bucket_kernel(const float *__restrict__
             for (int j = 0; j < CAP / UT; ++j) {
                 const int64_t i = tid + j * UT;
                 if (i < size) {
-                    lk[j] = (uint32_t)((L.a[i] >> 32) - k0);
+                    lk[j] = (uint32_t)((v[j] >> 32) - k0);
                     rk[j] = atomicAdd(&L.cnt[lk[j]], 1u);
                     if (rk[j] == SEGMAX) flag = 1;  // a long equal-key run: the bitonic path instead
                 }
@@ -487,12 +513,12 @@ __global__ __launch_bounds__(UT) void vx_bucket_kernel(const float *__restrict__
             if (!flag) {
                 // exclusive scan of the counters, KMAX / UT consecutive per thread
                 constexpr int PT = KMAX / UT;
-                uint32_t v[PT], sum = 0;
+                uint32_t cv[PT], sum = 0;
 #pragma unroll
                 for (int j = 0; j < PT; ++j) {
                     const int64_t c = PT * tid + j;
-                    v[j] = c < (int64_t)krange ? L.cnt[c] : 0u;
-                    sum += v[j];
+                    cv[j] = c < (int64_t)krange ? L.cnt[c] : 0u;
+                    sum += cv[j];
                 }
                 uint32_t all;
                 uint32_t ex = block_excl_scan<UT>(sum, red, &all);
@@ -500,42 +526,45 @@ __global__ __launch_bounds__(UT) void vx_bucket_kernel(const float *__restrict__
                 for (int j = 0; j < PT; ++j) {
                     const int64_t c = PT * tid + j;
                     if (c < (int64_t)krange) L.cnt[c] = ex;
-                    ex += v[j];
+                    ex += cv[j];
                 }
                 __syncthreads();
+                // each key's run, unordered
+                uint32_t st[CAP / UT], en[CAP / UT];
 #pragma unroll
                 for (int j = 0; j < CAP / UT; ++j) {
                     const int64_t i = tid + j * UT;
-                    if (i < size) L.s[L.cnt[lk[j]] + rk[j]] = L.a[i];
-                }
-                __syncthreads();
-                // equal-key runs (< SEGMAX long) in index order: the thread of a run's first slot sorts it
-#pragma unroll
-                for (int j = 0; j < CAP / UT; ++j) {
-                    const int64_t i = tid + j * UT;
-                    if (i < size && rk[j] == 0) {
-                        const int64_t st = L.cnt[lk[j]];
-                        const uint64_t kk = L.a[i] >> 32;
-                        int64_t e = st + 1;
-                        while (e < size && (L.s[e] >> 32) == kk) ++e;
-                        for (int64_t x = st + 1; x < e; ++x) {  // insertion sort (full 64-bit order)
-                            const uint64_t v2 = L.s[x];
-                            int64_t y = x - 1;
-                            while (y >= st && L.s[y] > v2) {
-                                L.s[y + 1] = L.s[y];
-                                --y;
-                            }
-                            L.s[y + 1] = v2;
-                        }
+                    if (i < size) {
+                        st[j] = L.cnt[lk[j]];
+                        en[j] = lk[j] + 1 < krange ? L.cnt[lk[j] + 1] : (uint32_t)size;
+                        L.s[st[j] + rk[j]] = v[j];
                     }
                 }
                 __syncthreads();
-                seq = L.s;
+                // index order inside a run (< SEGMAX long): every element counts the smaller pairs of
+                // its run, in parallel; the sorted pair and its xyz land in L.a / L.xyz
+#pragma unroll
+                for (int j = 0; j < CAP / UT; ++j) {
+                    const int64_t i = tid + j * UT;
+                    if (i < size) {
+                        uint32_t r = 0;
+                        for (uint32_t x = st[j]; x < en[j]; ++x) r += L.s[x] < v[j] ? 1u : 0u;
+                        const uint32_t o = st[j] + r;
+                        L.a[o] = v[j];
+#pragma unroll
+                        for (int c = 0; c < 3; ++c) L.xyz[3 * o + c] = g[j][c];
+                    }
+                }
+                __syncthreads();
+                seq = L.a;
             }
         }
-        if (!counting || flag) {  // bitonic sort of the loaded pairs
+        if (!counting || flag) {  // bitonic sort of the loaded pairs, then their xyz in sorted order
             int64_t P = 1;
             while (P < size) P <<= 1;
+#pragma unroll
+            for (int j = 0; j < CAP / UT; ++j)
+                if (tid + j * UT < size) L.a[tid + j * UT] = v[j];
             for (int64_t i = size + tid; i < P; i += UT) L.a[i] = kPad;
             __syncthreads();
             for (int64_t k2 = 2; k2 <= P; k2 <<= 1)
@@ -553,27 +582,24 @@ __global__ __launch_bounds__(UT) void vx_bucket_kernel(const float *__restrict__
                     __syncthreads();
                 }
             seq = L.a;
-        }
-        __syncthreads();
-        VX_STAMP(2);
-        // the bucket's points, gathered in parallel (one memory round trip) for the centroid walks
-        {
-            float g[CAP / UT][3];
+            float h[CAP / UT][3];
 #pragma unroll
             for (int j = 0; j < CAP / UT; ++j) {
                 const int64_t i = tid + j * UT;
                 const int64_t idx = i < size ? (int64_t)(uint32_t)seq[i] : 0;
 #pragma unroll
-                for (int a = 0; a < 3; ++a) g[j][a] = p[3 * idx + a];
+                for (int c = 0; c < 3; ++c) h[j][c] = p[3 * idx + c];
             }
 #pragma unroll
             for (int j = 0; j < CAP / UT; ++j) {
                 const int64_t i = tid + j * UT;
                 if (i < size)
 #pragma unroll
-                    for (int a = 0; a < 3; ++a) L.xyz[3 * i + a] = g[j][a];
+                    for (int c = 0; c < 3; ++c) L.xyz[3 * i + c] = h[j][c];
             }
         }
+        __syncthreads();
+        VX_STAMP(2);
         staged = true;
     } else {
         seq = bucket_radix(const_cast<uint64_t *>(gp), w.scratch + (int64_t)f * n + p0, size, L.cnt,
@@ -622,7 +648,65 @@ __global__ __launch_bounds__(UT) void vx_bucket_kernel(const float *__restrict__
     float *cf = cent + (int64_t)f * n * 3;
     int32_t *nf = counts + (int64_t)f * n;
     uint32_t carry = 0;
-    for (int64_t c0 = 0; c0 < size; c0 += CH * UT) {
+    if (staged) {
+        // one chunk (size <= CAP = CH UT): ids per element, the voxels' first positions into LDS, then
+        // one thread per voxel (known run length: the sequential sums' loads pipeline; consecutive
+        // threads write consecutive centroids)
+        static_assert(CAP <= CH * UT, "the staged emit is one chunk");
+        bool st[CH];
+        uint32_t s = 0;
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+            const int64_t i = CH * tid + j;
+            st[j] = i < size && start_at(i);
+            s += st[j] ? 1u : 0u;
+        }
+        uint32_t all;
+        uint32_t r = block_excl_scan<UT>(s, red, &all);  // the bucket's voxels before this thread's elements
+        VX_STAMP(6);
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+            const int64_t i = CH * tid + j;
+            if (i < size) {
+                const uint64_t v = seq[i];
+                const uint32_t kk = (uint32_t)(v >> 32);
+                if (st[j]) L.vstart[r] = (uint16_t)i;
+                r += st[j] ? 1u : 0u;
+                vf[(uint32_t)v] = kk == okey ? -1 : (int32_t)(O + r - 1);
+                // the end of the last voxel: the first outside point, or the bucket's end
+                if (kk != okey && (i + 1 == size || key_at(i + 1) == okey)) L.vstart[all] = (uint16_t)(i + 1);
+            }
+        }
+        __syncthreads();
+        for (uint32_t v = tid; v < all; v += UT) {
+            const int i0 = L.vstart[v], i1 = L.vstart[v + 1];
+            float sx = 0.f, sy = 0.f, sz = 0.f;
+            int e = i0;
+            for (; e + 4 <= i1; e += 4) {
+                float q[12];
+#pragma unroll
+                for (int k = 0; k < 12; ++k) q[k] = L.xyz[3 * e + k];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    sx = __fadd_rn(sx, q[3 * k]);
+                    sy = __fadd_rn(sy, q[3 * k + 1]);
+                    sz = __fadd_rn(sz, q[3 * k + 2]);
+                }
+            }
+            for (; e < i1; ++e) {
+                sx = __fadd_rn(sx, L.xyz[3 * e]);
+                sy = __fadd_rn(sy, L.xyz[3 * e + 1]);
+                sz = __fadd_rn(sz, L.xyz[3 * e + 2]);
+            }
+            const int64_t o = (int64_t)O + v;
+            const float c = (float)(i1 - i0);
+            cf[3 * o] = __fdiv_rn(sx, c);
+            cf[3 * o + 1] = __fdiv_rn(sy, c);
+            cf[3 * o + 2] = __fdiv_rn(sz, c);
+            nf[o] = i1 - i0;
+        }
+    }
+    for (int64_t c0 = 0; !staged && c0 < size; c0 += CH * UT) {
         bool st[CH];
         uint32_t s = 0;
 #pragma unroll
@@ -645,20 +729,10 @@ __global__ __launch_bounds__(UT) void vx_bucket_kernel(const float *__restrict__
                 float sx = 0.f, sy = 0.f, sz = 0.f;
                 int64_t e = i;
                 for (; e < size && key_at(e) == kk; ++e) {
-                    float px, py, pz;
-                    if (staged) {
-                        px = L.xyz[3 * e];
-                        py = L.xyz[3 * e + 1];
-                        pz = L.xyz[3 * e + 2];
-                    } else {
-                        const int64_t idx = (uint32_t)seq[e];
-                        px = p[3 * idx];
-                        py = p[3 * idx + 1];
-                        pz = p[3 * idx + 2];
-                    }
-                    sx = __fadd_rn(sx, px);
-                    sy = __fadd_rn(sy, py);
-                    sz = __fadd_rn(sz, pz);
+                    const int64_t idx = (uint32_t)seq[e];
+                    sx = __fadd_rn(sx, p[3 * idx]);
+                    sy = __fadd_rn(sy, p[3 * idx + 1]);
+                    sz = __fadd_rn(sz, p[3 * idx + 2]);
                 }
                 const int64_t o = r - 1;
                 const float c = (float)(e - i);
@@ -671,12 +745,13 @@ __global__ __launch_bounds__(UT) void vx_bucket_kernel(const float *__restrict__
         carry += all;
     }
 #ifdef VX_DIAG_PHASES
-    VX_STAMP(6);
+    VX_STAMP(7);
     if (tid == 0)  // diagnostic build only: phase cycles into the scratch tail of the counts output
     {
-        for (int k = 0; k < 6; ++k) nf[n - 1 - (8 * b + k)] = (int32_t)(ts[k + 1] - ts[k]);
-        nf[n - 1 - (8 * b + 6)] = (int32_t)spins_dbg;
-        nf[n - 1 - (8 * b + 7)] = (int32_t)(ts[4] & 0x7fffffff);  // look-back start (absolute, low bits)
+        int32_t *d = nf + n - 16 * (b + 1);
+        for (int k = 0; k < 7; ++k) d[k] = (int32_t)(ts[k + 1] - ts[k]);
+        d[7] = (int32_t)spins_dbg;
+        for (int k = 0; k < 8; ++k) d[8 + k] = (int32_t)(rt[k] & 0x7fffffff);  // 100 MHz, chip-wide
     }
 #endif
 #undef VX_STAMP

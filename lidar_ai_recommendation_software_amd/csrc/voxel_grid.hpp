@@ -23,6 +23,7 @@ constexpr uint32_t kOutside = 0xffffffffu;  // key of a point outside every bin 
 struct Axis {
     double start, e1, delta;  // e[0], e[1], e[1] - e[0]
     double inv;               // 1 / delta (rounded: only the guess of `bin` uses it)
+    double last;              // e[L - 1], the closed edge
     int64_t nb;               // bins (edges - 1)
 };
 
@@ -39,6 +40,7 @@ __host__ __device__ inline bool make_axis(double lo, double hi, double v, Axis &
     ax.delta = ax.e1 - start;
     ax.inv = ax.delta > 0.0 ? 1.0 / ax.delta : 0.0;
     ax.nb = (int64_t)len - 1;
+    ax.last = ax.nb == 0 ? start : (ax.nb == 1 ? ax.e1 : start + (double)ax.nb * ax.delta);
     return true;
 }
 
@@ -47,22 +49,30 @@ __host__ __device__ inline double edge(const Axis &ax, int64_t i)
     return i == 0 ? ax.start : (i == 1 ? ax.e1 : ax.start + (double)i * ax.delta);
 }
 
+// e[i] for i in [0, L), -inf below, +inf above: branch-free (selects), the fast path of `bin`
+__host__ __device__ inline double edge_or_inf(const Axis &ax, int64_t i, int64_t L)
+{
+    const uint32_t u = (uint32_t)(i < 0 ? 0 : (i >= L ? 0 : i));  // L - 1 <= 2^32 - 1 (make_axis)
+    const double e = ax.start + (double)u * ax.delta;
+    const double r = u == 0 ? ax.start : (u == 1 ? ax.e1 : e);
+    return i < 0 ? -INFINITY : (i >= L ? INFINITY : r);
+}
+
 // histogram2d's bin of p on this axis, -1 outside
 __host__ __device__ inline int64_t bin(const Axis &ax, double p)
 {
     const int64_t L = ax.nb + 1;
     // c = number of edges <= p (the edges are non-decreasing): guess from the spacing (a multiply
     // by the rounded reciprocal; the guess only has to be within one edge), verify, step one edge
-    // down or up when the verification fails, else binary search
+    // down or up when the verification fails (every candidate edge evaluated up front, branch-free:
+    // the key launch runs this three times per point), else binary search
     int64_t c = -1;
     if (ax.delta > 0.0) {
-        const double g = floor((p - ax.start) * ax.inv) + 1.0;
-        if (g >= 0.0 && g <= (double)L) {
-            int64_t t = (int64_t)g;
-            if (t > 0 && edge(ax, t - 1) > p) --t;
-            else if (t < L && edge(ax, t) <= p) ++t;
-            if ((t == 0 || edge(ax, t - 1) <= p) && (t == L || edge(ax, t) > p)) c = t;
-        }
+        const double g = fmin(fmax(floor((p - ax.start) * ax.inv) + 1.0, 0.0), (double)L);  // NaN -> 0
+        const int64_t t = (int64_t)g;
+        const double em = edge_or_inf(ax, t - 2, L), ea = edge_or_inf(ax, t - 1, L);
+        const double eb = edge_or_inf(ax, t, L), ep = edge_or_inf(ax, t + 1, L);
+        c = (ea <= p && p < eb) ? t : ((ea > p && em <= p) ? t - 1 : ((eb <= p && p < ep) ? t + 1 : -1));
     }
     if (c < 0) {
         int64_t lo = 0, hi = L;
@@ -73,7 +83,7 @@ __host__ __device__ inline int64_t bin(const Axis &ax, double p)
         }
         c = lo;
     }
-    if (p == edge(ax, L - 1)) --c;  // the last edge is closed
+    if (p == ax.last) --c;  // the last edge is closed
     return (c >= 1 && c <= ax.nb) ? c - 1 : -1;
 }
 

@@ -311,6 +311,82 @@ def group_mlp_bq(xyz, centres, grid, radius, nsample, packed, widths, out, out_o
     return out
 
 
+def generic_branch_weights(layers, cfeat, to_dev, arith):
+    """Dense-GEMM operands of an SA branch of any shape (sa_branch_generic): layer 1's rows reordered
+    from the canonical [x, y, z, f...] to the grouped rows' [f..., x, y, z, 0-pad] (k padded to 16),
+    every layer's columns (and the next layer's rows) zero-padded to a multiple of 128.  arith: "x3"
+    (h3 images), "x1" (bf16-spec images) or "f32" (the native fp32 GEMM's plain weights)."""
+    kp = (cfeat + 3 + 15) // 16 * 16
+    out = {"k": kp, "layers": [], "c3": layers[-1][0].shape[1], "arith": arith}
+    kin = kp
+    for li, (w, b) in enumerate(layers):
+        w = np.asarray(w, np.float32)
+        cin, c = w.shape
+        cp = (c + 127) // 128 * 128
+        wp = np.zeros((kin, cp), np.float32)
+        if li == 0:
+            wp[:cfeat, :c] = w[3:]
+            wp[cfeat:cfeat + 3, :c] = w[:3]
+        else:
+            wp[:cin, :c] = w
+        bp = np.zeros(cp, np.float32)
+        bp[:c] = b
+        wd = to_dev(wp)
+        lay = {"w": wd, "b": to_dev(bp), "cout": cp}
+        if arith != "f32":
+            lay["packed"] = pack_dense_x3(wd, x1=arith == "x1")
+        out["layers"].append(lay)
+        kin = cp
+    return out
+
+
+def sa_branch_generic(feat, cfeat, xyz, centres, idx, gw, out, out_offset=0, max_bytes=1 << 30, slot=0):
+    """One SA branch of any (widths, nsample) on the byte-moving kernels of csrc/sa_generic.hip and the
+    dense GEMMs: grouped rows [f[idx], xyz[idx] - centre, 0-pad] -> per layer x W + b, ReLU (h3 / bf16
+    spec / fp32 as gw["arith"]) -> max over each centre's nsample rows -> out[..., off:off + c3].
+    feat: (B, n, >= cfeat) fp32 with unit column stride (None when cfeat = 0); idx (B, M, ns) int32
+    (ball_query); gw = generic_branch_weights(...).  Frames run in chunks whose activations stay
+    under max_bytes."""
+    B, M, ns = idx.shape
+    n = xyz.shape[1]
+    if out.dim() != 3 or out.shape[0] != B or out.shape[1] != M or out.stride(2) != 1 or out.stride(1) != out.shape[2]:
+        raise ValueError("sa_branch_generic: out must be a contiguous (B, M, stride) tensor")
+    if out_offset < 0 or out_offset + gw["c3"] > out.shape[2]:
+        raise ValueError("sa_branch_generic: out columns out of range")
+    if cfeat and (feat is None or feat.shape[0] != B or feat.shape[1] != n or feat.shape[2] < cfeat
+                  or feat.stride(2) != 1 or feat.stride(0) != n * feat.stride(1)):
+        raise ValueError("sa_branch_generic: feat must be (B, n, >= cfeat) with rows of one stride")
+    if not (xyz.is_contiguous() and centres.is_contiguous() and idx.is_contiguous()):
+        raise ValueError("sa_branch_generic: xyz / centres / idx must be contiguous")
+    _dev_check(xyz, centres, idx, out)
+    if cfeat and not feat.is_cuda:  # strided rows (checked above), not necessarily contiguous
+        raise ValueError("sa_branch_generic: feat must be a CUDA tensor")
+    dev = xyz.device
+    h = nat.handle(dev.index, slot)
+    kp = gw["k"]
+    cmax = max([kp] + [lay["cout"] for lay in gw["layers"]])
+    fc = max(1, min(B, max_bytes // max(1, 2 * M * ns * cmax * 4)))
+    ldf = feat.stride(1) if cfeat else 0
+    for b0 in range(0, B, fc):
+        nb = min(B, b0 + fc) - b0
+        grouped = nb * M * ns
+        R = (grouped + 127) // 128 * 128
+        rows = torch.empty((R, kp), dtype=torch.float32, device=dev)
+        nat.call("lidar_sa_group_rows_f32", h, nat.ptr(feat[b0:b0 + nb]) if cfeat else None, ldf, cfeat,
+                 nat.ptr(xyz[b0:b0 + nb]), nat.ptr(centres[b0:b0 + nb]), nat.ptr(idx[b0:b0 + nb]), nb, n, M, ns,
+                 nat.ptr(rows), R, kp, nat.stream_ptr())
+        a = rows
+        for lay in gw["layers"]:
+            if gw["arith"] == "f32":
+                a = dense(a, lay["w"], lay["b"], relu=True)
+            else:
+                a = dense_x3s(a, lay["packed"], lay["b"], lay["cout"], relu=True, x1=gw["arith"] == "x1", slot=slot)
+        dst = out[b0:b0 + nb]
+        nat.call("lidar_group_max_f32", h, nat.ptr(a), a.shape[1], nb * M, ns, gw["c3"], nat.ptr(dst),
+                 out.shape[2], out_offset, nat.stream_ptr())
+    return out
+
+
 def layer1_weights(layer, cfeat, to_dev):
     """(W1 (3 + cfeat, c1), b1) -> the per-point GEMM operands of layer1_per_point:
     w1 rows [f..., x, y, z, 0-pad] (k padded to 16), wq rows [x, y, z, 0-pad] (16), columns
@@ -520,7 +596,14 @@ class PointNet2Backbone:
         (inputs, activations and weights rounded to bf16, fp32 accumulation); group_all stays in
         fp32 arithmetic on the x3 GEMM.
         Levels with point features run layer 1 per point (layer1_per_point / layer1_points_x1) and
-        the fused kernel from layer 2 on."""
+        the fused kernel from layer 2 on.
+
+        cfg: any SSG / MSG configuration (levels of radii / nsamples / mlps with three layers per
+        branch, then optionally group_all).  The fused branch kernels are instantiated for the six
+        (xyz level, c1, c2, c3, nsample) shapes of MLP16_SHAPES (the SSG / MSG configurations of
+        SURVEY §8a); a branch of any other shape runs sa_branch_generic — its grouped rows
+        materialised in HBM, the same dense GEMMs (same arithmetic: h3, bf16 spec or fp32), then the
+        max over nsample — with the same results contract and HBM-bound speed."""
         if dtype not in ("f32", "bf16"):
             raise ValueError("dtype must be 'f32' or 'bf16'")
         self.bf16 = dtype == "bf16"
@@ -535,26 +618,34 @@ class PointNet2Backbone:
             kp = (cfeat + 3 + 15) // 16 * 16
             if lvl.get("group_all"):
                 (w1, b1), (w2, b2), (w3, b3) = wl[0]
-                # canonical rows [x, y, z, f...] -> physical input [f..., x, y, z, 0-pad]
-                w1p = np.zeros((kp, w1.shape[1]), np.float32)
-                w1p[:cfeat] = w1[3:]
-                w1p[cfeat:cfeat + 3] = w1[:3]
-                entry = {"group_all": True, "k": kp, "cfeat": cfeat, "w": [t(w1p), t(w2), t(w3)],
-                         "b": [t(b1), t(b2), t(b3)]}
+                # canonical rows [x, y, z, f...] -> physical input [f..., x, y, z, 0-pad]; every
+                # width zero-padded to the GEMM's 128 columns (and the next layer's rows)
+                cp = [(w.shape[1] + 127) // 128 * 128 for w in (w1, w2, w3)]
+                w1p = np.zeros((kp, cp[0]), np.float32)
+                w1p[:cfeat, :w1.shape[1]] = w1[3:]
+                w1p[cfeat:cfeat + 3, :w1.shape[1]] = w1[:3]
+                w2p = np.zeros((cp[0], cp[1]), np.float32)
+                w2p[:w2.shape[0], :w2.shape[1]] = w2
+                w3p = np.zeros((cp[1], cp[2]), np.float32)
+                w3p[:w3.shape[0], :w3.shape[1]] = w3
+                bp = [np.pad(np.asarray(bb_, np.float32), (0, c - len(bb_))) for bb_, c in zip((b1, b2, b3), cp)]
+                entry = {"group_all": True, "k": kp, "cfeat": cfeat, "cout": w3.shape[1],
+                         "w": [t(w1p), t(w2p), t(w3p)], "b": [t(v) for v in bp]}
                 if self.x3:  # packed once into x3 B fragments
                     entry["w_x3"] = [pack_dense_x3(w) for w in entry["w"]]
-                    entry["h3_bounds"] = [h3_bounds(w1p, b1), h3_bounds(w2, b2), h3_bounds(w3, b3)]
+                    entry["h3_bounds"] = [h3_bounds(w1p, bp[0]), h3_bounds(w2p, bp[1]), h3_bounds(w3p, bp[2])]
                 self.levels.append(entry)
                 cfeat = w3.shape[1]
                 continue
             xyz_level = cfeat == 0
             branches = []
             for (r, ns, widths, layers) in zip(lvl["radii"], lvl["nsamples"], lvl["mlps"], wl):
-                if (xyz_level, *widths, ns) not in MLP16_SHAPES:
-                    raise ValueError(f"SA branch (widths {widths}, nsample {ns}, xyz level {xyz_level}) has no "
-                                     f"instantiated kernel; instantiated: {sorted(MLP16_SHAPES)}")
                 br = {"r": r, "ns": ns, "widths": widths}
-                if self.bf16:
+                if (xyz_level, *widths, ns) not in MLP16_SHAPES:
+                    # no fused kernel for this shape: grouped rows in HBM + the dense GEMMs (sa_branch_generic)
+                    arith = "x1" if self.bf16 else ("x3" if x3 else "f32")
+                    br["generic"] = generic_branch_weights(layers, cfeat, t, arith)
+                elif self.bf16:
                     br["packed_x1"] = torch.from_numpy(pack_branch_x1(layers)).to(self.device)
                     if not xyz_level:  # W1_f: rows [f..., (x, y, z) = 0, 0-pad], columns to 128
                         w1, b1 = layers[0]
@@ -614,7 +705,8 @@ class PointNet2Backbone:
         t = self.timers
         for li, lvl in enumerate(self.levels):
             if lvl.get("group_all"):
-                return self._group_all(xyz, feats, lvl, rows), out_levels
+                g = self._group_all(xyz, feats, lvl, rows)
+                return (g if g.shape[1] == lvl["cout"] else g[:, :lvl["cout"]].contiguous()), out_levels
             M = max(1, N0 // lvl["div"])
             pl = pre.get(li, {})
             if pl.get("fps") is not None:
@@ -633,17 +725,32 @@ class PointNet2Backbone:
             R = (B * M + 127) // 128 * 128 if padded else B * M
             out_rows = torch.empty((R, stride), dtype=torch.float32, device=xyz.device)
             out = out_rows[:B * M].view(B, M, stride)
-            pq = None
-            if lvl.get("pre") and self.bf16:
-                pq = _call(t, f"sa{li + 1}_layer1_points", B, layer1_points_x1, rows, xyz, lvl["cfeat"],
-                           lvl["branches"])
-            elif lvl.get("pre"):
-                pq = _call(t, f"sa{li + 1}_layer1_points", B, layer1_per_point, rows, xyz, lvl["cfeat"], new_xyz,
-                           lvl["branches"], x3=self.x3)
+            pq = None  # per-point layer 1 of the fused branches: {branch index: rows}
+            fb = [i for i, br in enumerate(lvl["branches"]) if "generic" not in br]
+            if lvl.get("pre") and fb:
+                fbr = [lvl["branches"][i] for i in fb]
+                if self.bf16:
+                    res = _call(t, f"sa{li + 1}_layer1_points", B, layer1_points_x1, rows, xyz, lvl["cfeat"], fbr)
+                else:
+                    res = _call(t, f"sa{li + 1}_layer1_points", B, layer1_per_point, rows, xyz, lvl["cfeat"],
+                                new_xyz, fbr, x3=self.x3)
+                pq = dict(zip(fb, res))
             off = 0
             gidxs = []
             for bi_, br in enumerate(lvl["branches"]):
                 tag = f"sa{li + 1}" + (f"_b{bi_}" if len(lvl["branches"]) > 1 else "")
+                if "generic" in br:
+                    if pl.get("bq") is not None:
+                        gidx = pl["bq"][bi_]
+                    else:
+                        grid = pl["grid"][bi_] if pl.get("grid") is not None else None
+                        gidx = _call(t, f"{tag}_ball_query", B, ball_query, br["r"], br["ns"], xyz, new_xyz,
+                                     grid=grid)
+                    gidxs.append(gidx)
+                    _call(t, f"{tag}_group_mlp", B, sa_branch_generic, feats, lvl["cfeat"], xyz, new_xyz, gidx,
+                          br["generic"], out, off)
+                    off += br["widths"][-1]
+                    continue
                 fused = pq is None and pl.get("bq") is None and (self.bf16 or "packed_x3" in br) and (
                     pl.get("grid") is not None or N >= BQ_GRID_MIN_N)
                 if fused:

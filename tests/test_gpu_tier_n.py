@@ -850,3 +850,109 @@ def test_backbone_bf16_vs_oracle(cuda, cfg_name, n):
     ga = tier_n.group_all(pts, feats, bb.weights[len(levels)][0], False)  # re-anchored group_all, fp32 contract
     feat_close(g.cpu().numpy()[0], ga, f"{cfg_name} group_all on the GPU's last level", strict=True)
     bf16_close(g.cpu().numpy()[0], want, "bf16 global feature (whole-stack oracle)")
+
+
+# branch shapes with no fused kernel (sa_branch_generic) beside fused ones at both an xyz and a feature
+# level, and group_all widths off the GEMM's 128-column grid
+ODD = {"name": "odd", "levels": [
+    {"npoint_div": 16, "radii": [0.15, 0.2], "nsamples": [24, 32], "mlps": [[40, 48, 96], [64, 64, 128]]},
+    {"npoint_div": 64, "radii": [0.3, 0.4], "nsamples": [20, 64], "mlps": [[96, 100, 160], [128, 128, 256]]},
+    {"group_all": True, "mlps": [[200, 300, 400]]}]}
+
+
+def test_sa_group_rows_and_max(cuda):
+    """The generic branch's byte-moving kernels: grouped rows bit-exact against the oracle's grouping
+    (the fp32 offsets, then the features; a feature operand with a row stride wider than its columns),
+    the zero tail rows, and the group max (NaN propagates, as max_pool2d)."""
+    rng = np.random.default_rng(5)
+    B, N, M, ns, C = 2, 500, 40, 12, 13
+    x = unit_frames(B, N, 4)
+    fwide = rng.standard_normal((B, N, 16)).astype(np.float32)
+    c = x[:, :M].copy()
+    gi = tier_n.ball_query(x, c, 0.3, ns)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(cuda)
+    kp = 32
+    R = (B * M * ns + 127) // 128 * 128
+    rows = torch.full((R, kp), 7.0, dtype=torch.float32, device=cuda)
+    h = pn.nat.handle(0)
+    ft, xt, ct, it = T(fwide), T(x), T(c), T(gi.astype(np.int32))  # held: the calls take raw pointers
+    pn.nat.call("lidar_sa_group_rows_f32", h, pn.nat.ptr(ft), 16, C, pn.nat.ptr(xt), pn.nat.ptr(ct),
+                pn.nat.ptr(it), B, N, M, ns, pn.nat.ptr(rows), R, kp, pn.nat.stream_ptr())
+    got = rows.cpu().numpy()
+    for b in range(B):
+        want = tier_n.group(x[b], fwide[b, :, :C], c[b], gi[b])  # [xyz - centre, f]
+        blk = got[b * M * ns:(b + 1) * M * ns]
+        assert np.array_equal(blk[:, :C], want[:, 3:]), "features"
+        assert np.array_equal(blk[:, C:C + 3], want[:, :3]), "offsets"
+        assert not blk[:, C + 3:].any(), "padding columns"
+    assert not got[B * M * ns:].any(), "tail rows"
+    G, ldi = 37, 24
+    a = rng.standard_normal((G * ns, ldi)).astype(np.float32)
+    a[5 * ns + 3, 2] = np.nan
+    out = torch.zeros((G, 20), dtype=torch.float32, device=cuda)
+    at = T(a)
+    pn.nat.call("lidar_group_max_f32", h, pn.nat.ptr(at), ldi, G, ns, C, pn.nat.ptr(out), 20, 4,
+                pn.nat.stream_ptr())
+    want = a[:, :C].reshape(G, ns, C).max(axis=1)
+    got = out.cpu().numpy()
+    assert np.array_equal(got[:, 4:4 + C], want, equal_nan=True)
+    assert np.isnan(got[5, 4 + 2]) and not got[:, :4].any() and not got[:, 4 + C:].any()
+    with pytest.raises(LidarError):
+        pn.nat.call("lidar_sa_group_rows_f32", h, None, 0, 0, pn.nat.ptr(xt), pn.nat.ptr(ct), pn.nat.ptr(it),
+                    B, N, M, ns, pn.nat.ptr(rows), R, 2, pn.nat.stream_ptr())  # ldr < cfeat + 3
+
+
+@pytest.mark.parametrize("x3", [True, False])
+def test_backbone_generic_shapes_vs_oracle(cuda, x3):
+    """PointNet2Backbone on a configuration outside MLP16_SHAPES: the generic branches (grouped rows in
+    HBM + the dense GEMMs, h3 or native fp32) beside fused ones, group_all padded to the 128 grid.
+    FPS / ball-query indices bit-exact, every level and the global feature within the 1e-4 contract."""
+    bb = pn.PointNet2Backbone(ODD, device=cuda, seed=4, x3=x3)
+    assert ["generic" in br for br in bb.levels[0]["branches"]] == [True, False]
+    assert ["generic" in br for br in bb.levels[1]["branches"]] == [True, False]
+    n, B = 8192, 2
+    x = unit_frames(B, n, 31)
+    g, levels = bb.forward(torch.from_numpy(x).to(cuda), keep_levels=True)
+    torch.cuda.synchronize()
+    assert tuple(g.shape) == (B, 400)
+    lv_cfg = pn.resolve(ODD, n)
+    for f in range(B):
+        want, wl = tier_n.sa_stack(x[f], {"levels": lv_cfg}, bb.weights)
+        pts = x[f]
+        for li, ((nx, nf, ni, ngi), (ox, of, oi)) in enumerate(zip(levels, wl)):
+            assert np.array_equal(ni.cpu().numpy()[f], oi), f"frame {f} level {li} FPS indices differ"
+            assert np.array_equal(nx.cpu().numpy()[f], ox)
+            for bi, (r, ns) in enumerate(zip(lv_cfg[li]["radii"], lv_cfg[li]["nsamples"])):
+                assert np.array_equal(ngi[bi].cpu().numpy()[f], tier_n.ball_query(pts, ox, r, ns)), f"L{li} br {bi}"
+            feat_close(nf.cpu().numpy()[f], of, f"x3={x3} frame {f} level {li} features")
+            pts = ox
+        feat_close(g.cpu().numpy()[f], want, f"x3={x3} frame {f} global feature")
+
+
+def test_backbone_generic_shapes_bf16(cuda):
+    """The bf16 spec on the generic branches (the X1 dense GEMM over whole grouped rows): every element of
+    every level and branch within x1_forward_bound re-anchored per level, group_all (fp32 contract) strict."""
+    bb = pn.PointNet2Backbone(ODD, device=cuda, seed=4, dtype="bf16")
+    n = 8192
+    x = unit_frames(1, n, 32)
+    g, levels = bb.forward(torch.from_numpy(x).to(cuda), keep_levels=True)
+    torch.cuda.synchronize()
+    lv_cfg = pn.resolve(ODD, n)
+    _, wl = tier_n.sa_stack(x[0], {"levels": lv_cfg}, bb.weights, bf16=True)
+    pts, feats = x[0], None
+    for li, ((nx, nf, ni, ngi), (ox, of, oi)) in enumerate(zip(levels, wl)):
+        assert np.array_equal(ni.cpu().numpy()[0], oi)
+        cx = nx.cpu().numpy()[0]
+        gf = nf.cpu().numpy()[0]
+        off = 0
+        for bi, (r, ns) in enumerate(zip(lv_cfg[li]["radii"], lv_cfg[li]["nsamples"])):
+            gi = ngi[bi].cpu().numpy()[0]
+            assert np.array_equal(gi, tier_n.ball_query(pts, ox, r, ns))
+            layers = bb.weights[li][bi]
+            cout = layers[-1][0].shape[1]
+            fin = None if feats is None else tier_n.bf16_round(feats)
+            _x1_level_check(pts, fin, cx, gi, layers, ns, gf[:, off:off + cout], f"odd bf16 level {li} br {bi}")
+            off += cout
+        pts, feats = cx, gf
+    ga = tier_n.group_all(pts, feats, bb.weights[len(levels)][0], False)
+    feat_close(g.cpu().numpy()[0], ga, "odd bf16 group_all on the GPU's last level", strict=True)

@@ -1,5 +1,6 @@
-"""Phase cycles of the voxel bucket kernel (diagnostic build -DVX_DIAG_PHASES: s_memtime stamps of
-workgroup thread 0, written into the scratch tail of the counts output).  usage:
+"""Phase cycles of the voxel bucket kernel (diagnostic build -DVX_DIAG_PHASES: s_memtime and
+s_memrealtime stamps of workgroup thread 0, written into the scratch tail of the counts output,
+16 words per bucket).  usage:
 LIDAR_AMD_LIB=tools/ablib/liblidar_vx_PHASES.so python tools/micro/voxel_phases.py [B] [voxel]"""
 import os
 import sys
@@ -19,13 +20,20 @@ for _ in range(3):
     c, vid, cnt, nv = pn.voxel_downsample_batch(x, voxel)
 torch.cuda.synchronize()
 nb = (N + 1535) // 1536
-cnt = cnt.cpu().numpy()
-ph = np.stack([cnt[:, N - 1 - (8 * b + np.arange(8))] for b in range(nb)], 1).astype(np.float64)  # (B, nb, 8)
-names = ["range", "load+sort", "xyz gather", "count", "look-back", "emit"]
+cnt = cnt.cpu().numpy().astype(np.int64)
+d = np.stack([cnt[:, N - 16 * (b + 1):N - 16 * b] for b in range(nb)], 1)  # (B, nb, 16)
+ph = d[:, :, :7].astype(np.float64)
+names = ["range", "load+sort", "xyz gather", "count", "look-back", "emit scan", "emit walk"]
 print(f"B={B} voxel={voxel} buckets/frame={nb}: mean cycles per phase " +
       ", ".join(f"{k} {v:.0f}" for k, v in zip(names, ph.mean(axis=(0, 1)))))
-print("look-back cycles by bucket index (mean over frames):", np.round(ph[:, :, 4].mean(0)).astype(int).tolist())
-print("spins by bucket index (mean):", np.round(ph[:, :, 6].mean(0), 1).tolist())
-t = ph[:, :, 7]
-print("frame 0: look-back start relative to bucket 0's (cycles):", (t[0] - t[0, 0]).astype(int).tolist())
-print("frame 8: look-back start relative to bucket 0's (cycles):", (t[8] - t[8, 0]).astype(int).tolist())
+for k, nm in enumerate(names):
+    print(f"{nm:10s} by bucket:", np.round(ph[:, :, k].mean(0)).astype(int).tolist())
+print("spins by bucket:", np.round(d[:, :, 7].mean(0), 1).tolist())
+rt = d[:, :, 8:16].astype(np.float64)  # realtime (100 MHz = 10 ns) stamps 0..7
+t0 = rt[:, :, 0].min()
+us = (rt - t0) * 0.01
+for f in (0, 8, 1, 31 if B > 31 else B - 1):
+    print(f"frame {f}: start us", np.round(us[f, :, 0], 1).tolist())
+    print(f"frame {f}: look-back start us", np.round(us[f, :, 4], 1).tolist())
+    print(f"frame {f}: look-back end us", np.round(us[f, :, 5], 1).tolist())
+print("kernel span us", round(us[:, :, 7].max(), 1))

@@ -165,6 +165,41 @@ __global__ __launch_bounds__(BT) void vx_bbox_kernel(const float *__restrict__ x
 }
 
 // ---------------------------------------------------------------------------------------- keys
+constexpr int ETAB = 4096;  // edges per axis of the keys launch's LDS tables
+
+// float threshold of a float64 edge: the least float >= e, so that for every float p, p >= e (in
+// float64) <=> p >= ru_float(e) (no float lies between e and it)
+__device__ __forceinline__ float ru_float(double e)
+{
+    const float f = (float)e;
+    if (!((double)f < e)) return f;
+    // the next float up from a finite f (e is finite: |e| < 1e38 on this path)
+    const uint32_t u = __float_as_uint(f);
+    return f == 0.f ? __uint_as_float(1u) : __uint_as_float(f > 0.f ? u + 1u : u - 1u);
+}
+
+// lidar_vox::bin of float p from the axis' threshold table E[0, L) (E[i] = ru_float(e[i])): the same
+// count of edges <= p, found with float compares; lastf = e[L - 1] when it is a float, else NaN
+__device__ __forceinline__ uint32_t bin_tab(const float *E, int L, float p, float s0, float inv, float lastf)
+{
+    const float gf = floorf((p - s0) * inv);                           // the bin's guess (any error: fixed below)
+    const int b = (int)fminf(fmaxf(gf, 0.f), (float)(L - 1));          // NaN -> 0
+    const float e0 = E[b > 0 ? b - 1 : 0], e1 = E[b], e2 = E[b + 1 < L ? b + 1 : b];
+    // c = #{i : E[i] <= p}: b + 1 when E[b] <= p < E[b + 1], b when E[b - 1] <= p < E[b]
+    int c = e1 <= p ? (b + 1 == L ? L : (p < e2 ? b + 1 : -1)) : (b == 0 ? 0 : (e0 <= p ? b : -1));
+    if (c < 0) {  // the guess was off by more than one bin: binary search
+        int lo = 0, hi = L;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (E[mid] <= p) lo = mid + 1;
+            else hi = mid;
+        }
+        c = lo;
+    }
+    if (p == lastf) --c;  // the last edge is closed
+    return (c >= 1 && c <= L - 1) ? (uint32_t)(c - 1) : lidar_vox::kOutside;
+}
+
 __global__ __launch_bounds__(KT) void vx_keys_kernel(const float *__restrict__ xyz, int64_t n, double voxel, Ws w,
                                                      int ntiles, int64_t batch)
 {
@@ -173,6 +208,15 @@ __global__ __launch_bounds__(KT) void vx_keys_kernel(const float *__restrict__ x
     const int tid = threadIdx.x;
     __shared__ uint32_t ext[6];
     __shared__ uint32_t hist[NBIN];
+    __shared__ float etab[3][ETAB];
+    const float *p = xyz + (int64_t)f * n * 3;
+    float q[PPT][3];  // every load in flight before the grid is known
+#pragma unroll
+    for (int j = 0; j < PPT; ++j) {
+        const int64_t i = (int64_t)t * TILE + j * KT + tid;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) q[j][a] = i < n ? p[3 * i + a] : 0.f;
+    }
     if (tid < 6) {
         const uint32_t *pp = w.part + (int64_t)f * NCH * 6 + tid;
         uint32_t v = pp[0];
@@ -195,21 +239,44 @@ __global__ __launch_bounds__(KT) void vx_keys_kernel(const float *__restrict__ x
         m[2] = (uint32_t)hs;
     }
     if (!g.ok) return;  // whole workgroup (uniform)
-    const float *p = xyz + (int64_t)f * n * 3;
-    uint32_t *k = w.key + (int64_t)f * n;
-    float q[PPT][3];  // every load in flight before the first key
+    // the float thresholds of every axis' edges in LDS when each axis has <= ETAB edges and the grid's
+    // span is a float range (uniform); else every point runs lidar_vox::key in float64
+    bool tab = true;
+    int L[3];
+    float s0[3], inv[3], lastf[3];
 #pragma unroll
-    for (int j = 0; j < PPT; ++j) {
-        const int64_t i = (int64_t)t * TILE + j * KT + tid;
-#pragma unroll
-        for (int a = 0; a < 3; ++a) q[j][a] = i < n ? p[3 * i + a] : 0.f;
+    for (int a = 0; a < 3; ++a) {
+        const lidar_vox::Axis &ax = g.ax[a];
+        L[a] = (int)min<int64_t>(ax.nb + 1, (int64_t)ETAB + 1);
+        tab = tab && ax.nb + 1 <= ETAB && ax.delta > 0.0 && fabs(ax.start) < 1e38 && fabs(ax.last) < 1e38;
+        s0[a] = (float)ax.start;
+        inv[a] = (float)ax.inv;
+        lastf[a] = (double)(float)ax.last == ax.last ? (float)ax.last : __builtin_nanf("");
     }
+    if (tab) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a)
+            for (int i = tid; i < L[a]; i += KT) etab[a][i] = ru_float(lidar_vox::edge(g.ax[a], i));
+        __syncthreads();
+    }
+    const uint32_t ny = (uint32_t)g.ax[1].nb, nz = (uint32_t)g.ax[2].nb;
+    uint32_t *k = w.key + (int64_t)f * n;
 #pragma unroll
     for (int j = 0; j < PPT; ++j) {
         const int64_t i = (int64_t)t * TILE + j * KT + tid;
         if (i < n) {
-            uint32_t kk = lidar_vox::key(g, q[j][0], q[j][1], q[j][2]);
-            kk = kk == lidar_vox::kOutside ? okey : kk;  // sorts after every voxel's key
+            uint32_t kk;
+            if (tab) {
+                const uint32_t bx = bin_tab(etab[0], L[0], q[j][0], s0[0], inv[0], lastf[0]);
+                const uint32_t by = bin_tab(etab[1], L[1], q[j][1], s0[1], inv[1], lastf[1]);
+                const uint32_t bz = bin_tab(etab[2], L[2], q[j][2], s0[2], inv[2], lastf[2]);
+                // (bx ny + by) nz + bz < nx ny nz < 2^32: exact in 32 bits
+                const bool out = bx == lidar_vox::kOutside || by == lidar_vox::kOutside || bz == lidar_vox::kOutside;
+                kk = out ? okey : (bx * ny + by) * nz + bz;
+            } else {
+                kk = lidar_vox::key(g, q[j][0], q[j][1], q[j][2]);
+                kk = kk == lidar_vox::kOutside ? okey : kk;  // sorts after every voxel's key
+            }
             k[i] = kk;
             atomicAdd(&hist[kk >> hs], 1u);
         }

@@ -102,6 +102,53 @@ def test_voxel_downsample_vs_oracle(cuda, n, v):
     assert np.array_equal(c, wc)
 
 
+def _edge_frame(n, v, seed):
+    """A [-1, 1] frame plus points on (and one float either side of) every grid edge inside the extent,
+    on every axis: the keys launch's float threshold tables must bin them as the float64 edges do."""
+    x = uniform_frame(n, seed, -1, 1).astype(np.float32)
+    lo, hi = x.min(axis=0).astype(np.float64), x.max(axis=0).astype(np.float64)
+    extra = []
+    for a in range(3):
+        e = np.arange(lo[a] - 2 * v, (hi[a] + 2 * v) + v, v)
+        e = e[(e >= lo[a]) & (e <= hi[a])]
+        for c in (np.float32(e), np.nextafter(np.float32(e), np.float32(np.inf)),
+                  np.nextafter(np.float32(e), np.float32(-np.inf))):
+            c = c[(c >= lo[a]) & (c <= hi[a])]
+            pts = x[: len(c)].copy()
+            pts[:, a] = c
+            extra.append(pts)
+    return np.concatenate([x] + extra).astype(np.float32)
+
+
+@pytest.mark.parametrize("case", ["edges", "edges_coarse", "long_axis", "near_table_limit", "far_offset"])
+def test_voxel_keys_table_and_float64_paths(cuda, case):
+    """The keys launch bins in float against per-axis tables of the float64 edges' float thresholds
+    (<= 4 096 edges per axis) and in float64 otherwise: both bit-exact against the oracle, points on
+    the edges included, guesses off by more than a bin (large offsets) included."""
+    rng = np.random.default_rng(11)
+    if case == "edges":
+        x, v = _edge_frame(20000, 0.05, 5), 0.05
+    elif case == "edges_coarse":
+        x, v = _edge_frame(5000, 0.3, 6), 0.3
+    else:
+        n = 50000
+        x = rng.random((n, 3)).astype(np.float32)
+        x[:, 1:] *= np.float32(0.002)
+        if case == "long_axis":  # x: ~10 000 edges, past the table
+            v = 1e-4
+        elif case == "near_table_limit":  # x: ~4 005 edges, in the table
+            x[:, 0] *= np.float32(0.4)
+            v = 1e-4
+        else:  # coordinates near 1 000: float spacing 6e-5 against a 1e-3 voxel
+            x[:, 0] = x[:, 0] + np.float32(1000.0)
+            v = 1e-3
+    c, vid, cnt = dp.voxel_downsample(x, v)
+    wc, wvid, wcnt = tier_n.voxel_downsample(x, v)
+    assert np.array_equal(vid, wvid), case
+    assert np.array_equal(cnt, wcnt), case
+    assert np.array_equal(c, wc), case
+
+
 def test_fps_extension(cuda):
     x = uniform_frame(5000, 1, -1, 1).astype(np.float32)
     assert np.array_equal(dp.farthest_point_sample(x, 256), tier_n.fps(x, 256))

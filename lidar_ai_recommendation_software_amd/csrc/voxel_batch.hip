@@ -69,7 +69,7 @@ struct Ws {  // per-batch workspace, every array frame-major
     uint32_t *meta;    // [F][MW]
     uint32_t *key;     // [F][n]
     uint16_t *thist;   // [F][T][NBIN] tile histograms of the coarse bins (a tile holds <= 8192 points)
-    uint32_t *base;    // [F][NBIN + 1] start of every coarse bin in bucket order
+    uint32_t *bstart;  // [F][NB + 1] the buckets' first pairs (bstart[NB] = n)
     uint64_t *pairs;   // [F][n] (key << 32 | index), coarse-bin order
     uint64_t *scratch; // [F][n] the global sort's other buffer
     uint64_t *flags;   // [F][NB] look-back words: status << 32 | count
@@ -298,6 +298,13 @@ __global__ __launch_bounds__(KT) void vx_scatter_kernel(int64_t n, Ws w, int nti
     const int hs = (int)m[2];
     __shared__ uint32_t off[NBIN];
     __shared__ uint32_t red[KT / 64];
+    const uint32_t *k = w.key + (int64_t)f * n;
+    uint32_t kv[PPT];  // the tile's keys in flight while the histograms sum
+#pragma unroll
+    for (int j = 0; j < PPT; ++j) {
+        const int64_t i = (int64_t)t * TILE + j * KT + tid;
+        kv[j] = i < n ? k[i] : 0u;
+    }
     // coarse bins BPT tid .. BPT tid + BPT - 1: frame totals and the counts of the tiles before this one
     uint32_t tot[BPT], pre[BPT], sum = 0;
 #pragma unroll
@@ -316,23 +323,36 @@ __global__ __launch_bounds__(KT) void vx_scatter_kernel(int64_t n, Ws w, int nti
     for (int j = 0; j < BPT; ++j) sum += tot[j];
     uint32_t all;
     uint32_t ex = block_excl_scan<KT>(sum, red, &all);
-    uint32_t *bs = w.base + (int64_t)f * (NBIN + 1);
+    uint32_t bsv[BPT];  // the frame-level start of each of this thread's bins
 #pragma unroll
     for (int j = 0; j < BPT; ++j) {
-        if (t == 0) bs[BPT * tid + j] = ex;
+        bsv[j] = ex;
         off[BPT * tid + j] = ex + pre[j];
         ex += tot[j];
     }
-    if (t == 0 && tid == 0) bs[NBIN] = all;
     __syncthreads();
-    const uint32_t *k = w.key + (int64_t)f * n;
-    uint64_t *pr = w.pairs + (int64_t)f * n;
-    uint32_t kv[PPT];
+    if (t == 0) {
+        // the bucket table: bucket b = the bins whose start s has bk(s) = min(s nb / n, nb - 1) = b, so
+        // its first pair is the start of the first bin with bk >= b; buckets past the last bin's bk start
+        // at n (empty), and bstart[nb] = n.  The previous bin's start: off[] still holds the frame-level
+        // starts in this workgroup (t = 0: no earlier tiles), read before the barrier below lets the
+        // scatter's atomics move them.
+        const int64_t nb = n_buckets(n);
+        const float inv = (float)nb / (float)n;
+        auto bk = [&](uint32_t st) { return min<int64_t>((int64_t)((float)st * inv), nb - 1); };
+        uint32_t *bst = w.bstart + (int64_t)f * (nb + 1);
+        int64_t prev = tid == 0 ? -1 : bk(off[BPT * tid - 1]);
 #pragma unroll
-    for (int j = 0; j < PPT; ++j) {
-        const int64_t i = (int64_t)t * TILE + j * KT + tid;
-        kv[j] = i < n ? k[i] : 0u;
+        for (int j = 0; j < BPT; ++j) {
+            const int64_t cur = bk(bsv[j]);
+            for (int64_t q = prev + 1; q <= cur; ++q) bst[q] = bsv[j];
+            prev = cur;
+        }
+        if (tid == KT - 1)
+            for (int64_t q = prev + 1; q <= nb; ++q) bst[q] = (uint32_t)n;
+        __syncthreads();  // (uniform: t is the workgroup's)
     }
+    uint64_t *pr = w.pairs + (int64_t)f * n;
 #pragma unroll
     for (int j = 0; j < PPT; ++j) {
         const int64_t i = (int64_t)t * TILE + j * KT + tid;
@@ -450,15 +470,18 @@ __device__ uint64_t look_back(unsigned long long *fl, int64_t b, uint32_t nv, bo
     return pre;
 }
 
+// 52 KiB: three 512-thread workgroups per CU
 struct BucketLds {
-    uint64_t a[CAP];         // pairs as loaded, then the bitonic array
-    uint64_t s[CAP];         // counting-sort output
-    uint32_t cnt[KMAX];      // counting-sort counters / starts (the radix path's digit tables)
-    float xyz[CAP * 3];      // the bucket's points, for the centroid walks
+    uint64_t a[CAP];           // the sorted pairs (the bitonic path: its array)
+    uint32_t s[CAP];           // the counting sort's unordered runs: point indices (a run is one key)
+    union {
+        uint32_t cnt[KMAX];    // counting-sort counters / starts (the radix path's digit tables)
+        float xyz[CAP * 3];    // the sorted points' xyz, for the centroid sums (written once cnt is dead)
+    };
     uint16_t vstart[CAP + 1];  // the staged emit: voxel v's first sorted position, then the voxels' end
 };
 
-__global__ __launch_bounds__(UT) void vx_bucket_kernel(const float *__restrict__ xyz, int64_t n, Ws w,
+__global__ __launch_bounds__(UT, 6) void vx_bucket_kernel(const float *__restrict__ xyz, int64_t n, Ws w,
                                                        int32_t *__restrict__ vid, float *__restrict__ cent,
                                                        int32_t *__restrict__ counts, int32_t *__restrict__ nvox,
                                                        int64_t batch)
@@ -495,32 +518,11 @@ __global__ __launch_bounds__(UT) void vx_bucket_kernel(const float *__restrict__
 #ifdef VX_DIAG_PHASES
     __shared__ uint32_t spins_dbg;
 #endif
-    // the bucket: coarse bins whose start s lies in [b S, (b + 1) S), S = n / nb (every workgroup of
-    // the frame evaluates the same monotone float expression, so the buckets tile the bins exactly)
-    if (tid < 4) rng[tid] = tid < 3 ? (tid < 2 ? (uint32_t)n : 0xffffffffu) : 0u;  // [2], [3]: key min / max
+    // the bucket's pairs [bstart[b], bstart[b + 1]) (the scatter launch's bucket table)
+    if (tid < 2) rng[tid] = w.bstart[(int64_t)f * (nb + 1) + b + tid];
+    if (tid == 2) rng[2] = 0xffffffffu;  // [2], [3]: key min / max
+    if (tid == 3) rng[3] = 0u;
     if (tid == 0) flag = 0;
-    __syncthreads();
-    {
-        const float inv = (float)nb / (float)n;
-        const uint32_t *bs = w.base + (int64_t)f * (NBIN + 1);
-        uint32_t m0 = (uint32_t)n, m1 = (uint32_t)n;
-        uint32_t sv[NBIN / UT];
-#pragma unroll
-        for (int j = 0; j < NBIN / UT; ++j) sv[j] = bs[NBIN - 1 - tid - j * UT];  // all loads in flight
-#pragma unroll
-        for (int j = 0; j < NBIN / UT; ++j) {  // descending bins: the min is the last hit
-            const int64_t bk = min<int64_t>((int64_t)((float)sv[j] * inv), nb - 1);
-            if (bk >= b) m0 = sv[j];
-            if (bk >= b + 1) m1 = sv[j];
-        }
-        // wave minima first: 512 threads on 2 LDS words would serialise ~1 000 atomics
-        m0 = (uint32_t)lidar::wave_min_u32_dpp(m0);
-        m1 = (uint32_t)lidar::wave_min_u32_dpp(m1);
-        if (lane == 0) {
-            atomicMin(&rng[0], m0);
-            atomicMin(&rng[1], m1);
-        }
-    }
     __syncthreads();
     VX_STAMP(1);
     const int64_t p0 = rng[0], size = (int64_t)rng[1] - rng[0];
@@ -604,18 +606,18 @@ __global__ __launch_bounds__(UT) void vx_bucket_kernel(const float *__restrict__
                     if (i < size) {
                         st[j] = L.cnt[lk[j]];
                         en[j] = lk[j] + 1 < krange ? L.cnt[lk[j] + 1] : (uint32_t)size;
-                        L.s[st[j] + rk[j]] = v[j];
+                        L.s[st[j] + rk[j]] = (uint32_t)v[j];
                     }
                 }
                 __syncthreads();
-                // index order inside a run (< SEGMAX long): every element counts the smaller pairs of
+                // index order inside a run (< SEGMAX long): every element counts the smaller indices of
                 // its run, in parallel; the sorted pair and its xyz land in L.a / L.xyz
 #pragma unroll
                 for (int j = 0; j < CAP / UT; ++j) {
                     const int64_t i = tid + j * UT;
                     if (i < size) {
                         uint32_t r = 0;
-                        for (uint32_t x = st[j]; x < en[j]; ++x) r += L.s[x] < v[j] ? 1u : 0u;
+                        for (uint32_t x = st[j]; x < en[j]; ++x) r += L.s[x] < (uint32_t)v[j] ? 1u : 0u;
                         const uint32_t o = st[j] + r;
                         L.a[o] = v[j];
 #pragma unroll
@@ -730,7 +732,6 @@ __global__ __launch_bounds__(UT) void vx_bucket_kernel(const float *__restrict__
         }
         uint32_t all;
         uint32_t r = block_excl_scan<UT>(s, red, &all);  // the bucket's voxels before this thread's elements
-        VX_STAMP(6);
 #pragma unroll
         for (int j = 0; j < CH; ++j) {
             const int64_t i = CH * tid + j;
@@ -745,6 +746,7 @@ __global__ __launch_bounds__(UT) void vx_bucket_kernel(const float *__restrict__
             }
         }
         __syncthreads();
+        VX_STAMP(6);
         for (uint32_t v = tid; v < all; v += UT) {
             const int i0 = L.vstart[v], i1 = L.vstart[v + 1];
             float sx = 0.f, sy = 0.f, sz = 0.f;
@@ -835,7 +837,7 @@ LIDAR_EXPORT uint64_t lidar_voxel_batch_workspace_bytes(int64_t batch, int64_t n
     cv.take<uint32_t>(batch * MW);
     cv.take<uint32_t>(batch * n);
     cv.take<uint16_t>(batch * ntiles * NBIN);
-    cv.take<uint32_t>(batch * (NBIN + 1));
+    cv.take<uint32_t>(batch * (nb + 1));
     cv.take<uint64_t>(batch * n);
     cv.take<uint64_t>(batch * n);
     cv.take<uint64_t>(batch * nb);
@@ -864,7 +866,7 @@ LIDAR_EXPORT int lidar_voxel_downsample_batch_f32(lidar_handle *h, const float *
     lidar::Carver cv;
     const uint64_t opart = cv.take<uint32_t>(batch * NCH * 6), ometa = cv.take<uint32_t>(batch * MW);
     const uint64_t okey = cv.take<uint32_t>(batch * n), oth = cv.take<uint16_t>(batch * ntiles * NBIN);
-    const uint64_t obase = cv.take<uint32_t>(batch * (NBIN + 1));
+    const uint64_t obst = cv.take<uint32_t>(batch * (nb + 1));
     const uint64_t opairs = cv.take<uint64_t>(batch * n), oscr = cv.take<uint64_t>(batch * n);
     const uint64_t oflags = cv.take<uint64_t>(batch * nb);
     char *base = static_cast<char *>(lidar::workspace(h, cv.off));
@@ -874,7 +876,7 @@ LIDAR_EXPORT int lidar_voxel_downsample_batch_f32(lidar_handle *h, const float *
     w.meta = reinterpret_cast<uint32_t *>(base + ometa);
     w.key = reinterpret_cast<uint32_t *>(base + okey);
     w.thist = reinterpret_cast<uint16_t *>(base + oth);
-    w.base = reinterpret_cast<uint32_t *>(base + obase);
+    w.bstart = reinterpret_cast<uint32_t *>(base + obst);
     w.pairs = reinterpret_cast<uint64_t *>(base + opairs);
     w.scratch = reinterpret_cast<uint64_t *>(base + oscr);
     w.flags = reinterpret_cast<uint64_t *>(base + oflags);

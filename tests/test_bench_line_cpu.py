@@ -37,7 +37,9 @@ def _with_ranks(rec, world):
                        "unit": "TFLOP/s", "frac": 0.2172, "traffic": None, "stack_mfma_frac": 0.19,
                        "work_per_launch": 3.75e12, "avg_launch_ms": 6.9, "launches": 6, "frames": 576}
     rec["precision"] = {"contract": "max |got-want|/|want| over |want| >= 1e-2 RMS, and max err/(1e-4|want| + "
-                                    "1e-4 RMS)", "frame": "batch 0 frame 0", "fps_exact": True,
+                                    "1e-4 RMS)", "frames": [0, 31, 64, 127], "fps_exact": True,
+                        "per_frame": {str(f): {"level1": 3.1e-05, "level2": 2.9e-05, "global": 3.1e-05}
+                                      for f in (0, 31, 64, 127)},
                         "level1": stats, "level2": stats, "global": stats}
     return rec
 
@@ -60,6 +62,7 @@ def test_compact_line_fits_and_keeps_the_contract(world):
     assert d["cpu_baseline"]["value"] > 0 and d["cpu_baseline"]["cores"] >= 1 and d["cpu_baseline"]["kind"] == "port"
     assert d["distributed"]["world_size"] == world == len(d["distributed"]["ranks"])
     assert d["precision"]["global"]["max_rel"] == pytest.approx(3.142e-05)
+    assert d["precision"]["frames"] == [0, 31, 64, 127] and "per_frame" not in d["precision"]
     # the line says what "f32" means, where ball_query stands against north_star's HBM target, and
     # prices the configs[4] MSG leg's dominant kernel on the bf16 peak
     assert d["arithmetic"].startswith("h3: fp32 as fp16 hi+lo")

@@ -33,6 +33,7 @@ struct lidar_handle {
     uint64_t retired_bytes = 0;
     void *host_pinned = nullptr;  // small pinned host buffer for scalar read-backs
     lidar::Prof *prof = nullptr;  // non-null while lidar_profile(h, 1) is on
+    uint32_t epoch = 0;           // per-call tag of in-launch hand-offs (voxel_batch.hip's extent granules)
 };
 
 namespace lidar {

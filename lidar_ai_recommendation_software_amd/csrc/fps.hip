@@ -19,7 +19,7 @@
 // padded to whole buckets with dist -1 sentinels so the batch is branch-free), updated,
 // and re-reduced with DPP argmax reductions (max dist, lowest index on ties).  A wave
 // whose buckets changed recomputes its DPP argmax; every wave then submits
-// (dist bits << 32 | (2^18 - index) << 4 | wave) to ONE LDS 64-bit atomic max and its
+// (dist bits << 32 | (2^27 - index) << 4 | wave) to ONE LDS 64-bit atomic max and its
 // coordinates to a per-wave slot, so the frame argmax costs a single barrier per step.
 //
 // Nested FPS (SA2 samples SA1's centroids): FPS over the first m points of an FPS ordering

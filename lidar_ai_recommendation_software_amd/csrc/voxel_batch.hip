@@ -6,30 +6,34 @@
 // (bx*ny + by)*nz + bz; voxels in ascending key order, voxel id = rank of the key (-1 for a point
 // outside every bin), centroid = sequential fp32 sum of the voxel's points in point order / count.
 //
-// Round 5: a two-level sort in four launches (round 4: an 8-bit LSD radix sort over global memory,
+// Round 5: a two-level sort in three launches (round 4: an 8-bit LSD radix sort over global memory,
 // 13 launches and ~284 B of memory traffic per point):
 //
-//   bbox     grid (16 chunks, frames): per-chunk min / max (monotone bits) -> 16 partials per frame
-//   keys     grid (4096-point tiles, frames): the frame's grid from its partials (float64, every
-//            workgroup alike), the key of every point (a point outside every bin takes nx ny nz, one
-//            past the last voxel), and the tile's histogram over 1024 coarse bins (key >> hs, the
-//            top 10 bits of the frame's key range)
+//   keys     grid (8192-point tiles, frames; a frame's tiles on one XCD, dispatched together): each
+//            tile loads its points once, publishes its extent as self-tagged 8-byte granules and
+//            polls its frame's other tiles' (an in-launch hand-off instead of a bbox launch), builds
+//            the frame's grid (float64, every workgroup alike), bins every point in float against
+//            per-axis LDS tables of the float64 edges' float thresholds (float64 beyond 4096 edges per
+//            axis; a point outside every bin takes nx ny nz, one past the last voxel), and writes its
+//            keys and its histogram over 4096 coarse bins (key >> hs, the top 12 bits of the range)
 //   scatter  grid (tiles, frames): each workgroup sums the frame's tile histograms itself (exclusive
 //            scan over the coarse bins, plus the counts of the tiles before it) and scatters its
 //            (key, index) pairs to their coarse bin (LDS atomics: order inside a bin is free, the
-//            buckets sort by (key, index) anyway)
-//   bucket   grid (buckets, frames): bucket b holds the coarse bins whose start falls in
-//            [b n / NB, (b + 1) n / NB) — ~1 536 points for a uniform frame.  It sorts its pairs by
-//            (key, index) in LDS (bitonic; a bucket above 4 096 pairs — clumped frames, huge voxels —
-//            sorts in global memory by a stable LSD radix over the bits that vary), counts its voxels,
-//            takes its voxel offset from the buckets before it by a decoupled look-back (each bucket
-//            publishes its count, then its inclusive prefix; every wait is on a lower workgroup
-//            index, i.e. one dispatched earlier), and writes every point's voxel id and, one thread
-//            per voxel walking its points in index order, the centroid and count.
+//            buckets sort by (key, index) anyway); tile 0 also writes the bucket table (bucket b =
+//            the coarse bins whose start s has min(s NB / n, NB - 1) = b, ~1 536 points uniform)
+//   bucket   grid (buckets, frames; 3 workgroups per CU): each bucket loads its pairs and gathers
+//            their xyz, sorts by (key, index) in LDS (a counting sort over the bucket's own key range
+//            with equal-key runs ranked by index in parallel; bitonic when the range or a run is too
+//            long; a bucket above 2048 pairs — clumped frames, huge voxels — sorts in global memory by
+//            a stable LSD radix over the bits that vary), counts its voxels, takes its voxel offset
+//            from the buckets before it by a decoupled look-back (each bucket publishes its count,
+//            then its inclusive prefix; every wait is on a lower workgroup index, i.e. one dispatched
+//            earlier), writes every point's voxel id and, one thread per voxel summing its points in
+//            index order, the centroids and counts.
 //
-// Memory-side bytes per point: xyz 12 (bbox) + 12 (keys) + key 4 + 4 + pair 8 + 8 + id 4 + the
-// centroid gathers 12 (+16 per voxel out); no host synchronisation: nvox[f] lands on the device
-// (-1: the frame's extent is not finite, or its grid has 2^32 - 1 keys or more).
+// Memory-side bytes per point: xyz 12 (keys) + key 4 + 4 + pair 8 + 8 + id 4 + the xyz gather 12
+// (+16 per voxel out); no host synchronisation: nvox[f] lands on the device (-1: the frame's extent is
+// not finite, or its grid has 2^32 - 1 keys or more).
 #include <algorithm>
 
 #include "common.hpp"
@@ -37,11 +41,10 @@
 
 namespace {
 
-constexpr int BT = 256;            // bbox threads
-constexpr int NCH = 16;            // bbox chunks per frame
 constexpr int KT = 1024;           // keys / scatter threads
 constexpr int TILE = 8192;         // points per keys / scatter workgroup (one round of the chip at B = 32)
 constexpr int PPT = TILE / KT;     // points per keys / scatter thread
+constexpr int kFuseTiles = 16;     // frames of up to this many tiles take their extent inside the keys launch
 constexpr int HB = 12;             // coarse-bin bits of the key range
 constexpr int NBIN = 1 << HB;      // coarse bins per frame
 constexpr int BPT = NBIN / KT;     // coarse bins per scatter thread (its scan)
@@ -65,7 +68,7 @@ __device__ __forceinline__ float unord(uint32_t u)
 }
 
 struct Ws {  // per-batch workspace, every array frame-major
-    uint32_t *part;    // [F][NCH][6] bbox partials (monotone bits)
+    unsigned long long *gran;  // [F][T][6] the tiles' extents: epoch << 32 | monotone bits (self-tagged granules)
     uint32_t *meta;    // [F][MW]
     uint32_t *key;     // [F][n]
     uint16_t *thist;   // [F][T][NBIN] tile histograms of the coarse bins (a tile holds <= 8192 points)
@@ -124,46 +127,6 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *red, u
     return pre + inc - v;
 }
 
-// ---------------------------------------------------------------------------------------- bbox
-__global__ __launch_bounds__(BT) void vx_bbox_kernel(const float *__restrict__ xyz, int64_t n, Ws w, int64_t nb)
-{
-    const int f = blockIdx.y, c = blockIdx.x;
-    const float *p = xyz + (int64_t)f * n * 3;
-    const int64_t i0 = n * c / NCH, i1 = n * (c + 1) / NCH;
-    uint32_t lo[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, hi[3] = {0u, 0u, 0u};
-    for (int64_t i = i0 + threadIdx.x; i < i1; i += BT)
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            const uint32_t o = ord(p[3 * i + a]);
-            lo[a] = min(lo[a], o);
-            hi[a] = max(hi[a], o);
-        }
-    __shared__ uint32_t red[BT / 64][6];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        uint32_t v = lo[a], u = hi[a];
-#pragma unroll
-        for (int m = 32; m >= 1; m >>= 1) {
-            v = min(v, (uint32_t)__shfl_xor((int)v, m, 64));
-            u = max(u, (uint32_t)__shfl_xor((int)u, m, 64));
-        }
-        if (lane == 0) {
-            red[wave][a] = v;
-            red[wave][3 + a] = u;
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x < 6) {
-        const int a = threadIdx.x;
-        uint32_t v = red[0][a];
-        for (int q = 1; q < BT / 64; ++q) v = a < 3 ? min(v, red[q][a]) : max(v, red[q][a]);
-        w.part[((int64_t)f * NCH + c) * 6 + a] = v;
-    }
-    if (c == 0)  // the bucket launch's look-back words start at "nothing published"
-        for (int64_t b = threadIdx.x; b < nb; b += BT) w.flags[(int64_t)f * nb + b] = 0ull;
-}
-
 // ---------------------------------------------------------------------------------------- keys
 constexpr int ETAB = 4096;  // edges per axis of the keys launch's LDS tables
 
@@ -200,31 +163,123 @@ __device__ __forceinline__ uint32_t bin_tab(const float *E, int L, float p, floa
     return (c >= 1 && c <= L - 1) ? (uint32_t)(c - 1) : lidar_vox::kOutside;
 }
 
-__global__ __launch_bounds__(KT) void vx_keys_kernel(const float *__restrict__ xyz, int64_t n, double voxel, Ws w,
-                                                     int ntiles, int64_t batch)
+// the tile's extent (min / max of ord() over its points in q) as six {epoch, value} granules gr[t * 6 ..]
+template <typename Q>
+__device__ __forceinline__ void publish_extent(const Q &q, int64_t n, int64_t t, unsigned long long *gr,
+                                               uint32_t epoch, uint32_t (*red6)[6])
+{
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    uint32_t lo3[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, hi3[3] = {0u, 0u, 0u};
+#pragma unroll
+    for (int j = 0; j < PPT; ++j)
+        if ((int64_t)t * TILE + j * KT + tid < n)
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                lo3[a] = min(lo3[a], ord(q[j][a]));
+                hi3[a] = max(hi3[a], ord(q[j][a]));
+            }
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        lo3[a] = lidar::wave_min_u32_dpp(lo3[a]);
+        hi3[a] = ~lidar::wave_min_u32_dpp(~hi3[a]);
+    }
+    if (lane == 0)
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            red6[wave][a] = lo3[a];
+            red6[wave][3 + a] = hi3[a];
+        }
+    __syncthreads();
+    if (tid < 6) {
+        uint32_t v = red6[0][tid];
+        for (int q2 = 1; q2 < KT / 64; ++q2) v = tid < 3 ? min(v, red6[q2][tid]) : max(v, red6[q2][tid]);
+        __hip_atomic_store(&gr[t * 6 + tid], ((unsigned long long)epoch << 32) | v, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// the extents of frames with more tiles than an XCD holds workgroups (the keys launch's poll then finds
+// every granule already written): one launch more and the points read twice
+__global__ __launch_bounds__(KT) void vx_extent_kernel(const float *__restrict__ xyz, int64_t n, Ws w, int ntiles,
+                                                       int64_t batch, uint32_t epoch)
 {
     int64_t f, t;
     if (!frame_part(batch, ntiles, f, t)) return;
-    const int tid = threadIdx.x;
+    __shared__ uint32_t red6[KT / 64][6];
+    const float *p = xyz + (int64_t)f * n * 3;
+    float q[PPT][3];
+#pragma unroll
+    for (int j = 0; j < PPT; ++j) {
+        const int64_t i = (int64_t)t * TILE + j * KT + threadIdx.x;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) q[j][a] = i < n ? p[3 * i + a] : 0.f;
+    }
+    publish_extent(q, n, t, w.gran + (int64_t)f * ntiles * 6, epoch, red6);
+}
+
+__global__ __launch_bounds__(KT) void vx_keys_kernel(const float *__restrict__ xyz, int64_t n, double voxel, Ws w,
+                                                     int ntiles, int64_t batch, uint32_t epoch, int64_t nb)
+{
+    int64_t f, t;
+    if (!frame_part(batch, ntiles, f, t)) return;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     __shared__ uint32_t ext[6];
+    __shared__ uint32_t red6[KT / 64][6];
     __shared__ uint32_t hist[NBIN];
     __shared__ float etab[3][ETAB];
     const float *p = xyz + (int64_t)f * n * 3;
-    float q[PPT][3];  // every load in flight before the grid is known
+    float q[PPT][3];  // the tile's points, loaded once: its extent, then its keys
 #pragma unroll
     for (int j = 0; j < PPT; ++j) {
         const int64_t i = (int64_t)t * TILE + j * KT + tid;
 #pragma unroll
         for (int a = 0; a < 3; ++a) q[j][a] = i < n ? p[3 * i + a] : 0.f;
     }
-    if (tid < 6) {
-        const uint32_t *pp = w.part + (int64_t)f * NCH * 6 + tid;
-        uint32_t v = pp[0];
-        for (int c = 1; c < NCH; ++c) v = tid < 3 ? min(v, pp[6 * c]) : max(v, pp[6 * c]);
-        ext[tid] = v;
-    }
 #pragma unroll
     for (int j = 0; j < BPT; ++j) hist[tid + j * KT] = 0;
+    if (t == 0)  // the bucket launch's look-back words start at "nothing published"
+        for (int64_t b = tid; b < nb; b += KT) w.flags[(int64_t)f * nb + b] = 0ull;
+    {
+        // the tile's extent (monotone bits: min / max of ord()), then the frame's from every tile's
+        // granules: {epoch, value} in one 8-byte agent-scope store each, polled until every tag is this
+        // call's (self-contained: no fence; MI355X_MICROARCH.md R2).  A tile waits only on tiles of its
+        // frame, which frame_part dispatches together, at most kFuseTiles of them (an XCD holds 32
+        // workgroups of this launch; larger frames run vx_extent_kernel first); the spin is bounded (a
+        // frame whose tiles never all arrive reports a non-finite extent: nvox -1).
+        unsigned long long *gr = w.gran + (int64_t)f * ntiles * 6;
+        publish_extent(q, n, t, gr, epoch, red6);
+        if (wave == 0) {
+            uint32_t m[6] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0u, 0u, 0u};
+            bool ok = true;
+            for (int64_t c0 = 0; c0 < (int64_t)ntiles * 6; c0 += 60) {  // 10 tiles per pass, lane l: word l % 6
+                const int64_t c = c0 + lane;
+                const bool mine = lane < 60 && c < (int64_t)ntiles * 6;
+                unsigned long long v = 0;
+                uint32_t spins = 0;
+                while (true) {
+                    v = mine ? __hip_atomic_load(&gr[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+                    const bool ready = !mine || (uint32_t)(v >> 32) == epoch;
+                    if (__ballot(!ready) == 0) break;
+                    if (++spins == (1u << 22)) {
+                        ok = false;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(2);
+                }
+                const int k = lane % 6;
+                const uint32_t x = (uint32_t)v;
+#pragma unroll
+                for (int kk = 0; kk < 6; ++kk) {  // fold word kk over the lanes that hold it
+                    uint32_t y = mine && k == kk ? x : (kk < 3 ? 0xffffffffu : 0u);
+                    y = kk < 3 ? lidar::wave_min_u32_dpp(y) : ~lidar::wave_min_u32_dpp(~y);
+                    m[kk] = kk < 3 ? min(m[kk], y) : max(m[kk], y);
+                }
+            }
+#pragma unroll
+            for (int kk = 0; kk < 6; ++kk)  // hung: NaN extent, the grid fails
+                if (lane == kk) ext[kk] = ok ? m[kk] : ord(__builtin_nanf(""));
+        }
+    }
     __syncthreads();
     const double lo[3] = {unord(ext[0]), unord(ext[1]), unord(ext[2])};
     const double hi[3] = {unord(ext[3]), unord(ext[4]), unord(ext[5])};
@@ -833,7 +888,7 @@ LIDAR_EXPORT uint64_t lidar_voxel_batch_workspace_bytes(int64_t batch, int64_t n
 {
     const int64_t ntiles = (n + TILE - 1) / TILE, nb = (n + BUCKET - 1) / BUCKET;
     lidar::Carver cv;
-    cv.take<uint32_t>(batch * NCH * 6);
+    cv.take<unsigned long long>(batch * ntiles * 6);
     cv.take<uint32_t>(batch * MW);
     cv.take<uint32_t>(batch * n);
     cv.take<uint16_t>(batch * ntiles * NBIN);
@@ -864,7 +919,7 @@ LIDAR_EXPORT int lidar_voxel_downsample_batch_f32(lidar_handle *h, const float *
     REQUIRE((int64_t)frame_grid(batch, std::max<int64_t>(ntiles, nb)) < 0x7fffffff,
             "lidar_voxel_downsample_batch_f32: batch * n too large");
     lidar::Carver cv;
-    const uint64_t opart = cv.take<uint32_t>(batch * NCH * 6), ometa = cv.take<uint32_t>(batch * MW);
+    const uint64_t ogran = cv.take<unsigned long long>(batch * ntiles * 6), ometa = cv.take<uint32_t>(batch * MW);
     const uint64_t okey = cv.take<uint32_t>(batch * n), oth = cv.take<uint16_t>(batch * ntiles * NBIN);
     const uint64_t obst = cv.take<uint32_t>(batch * (nb + 1));
     const uint64_t opairs = cv.take<uint64_t>(batch * n), oscr = cv.take<uint64_t>(batch * n);
@@ -872,7 +927,7 @@ LIDAR_EXPORT int lidar_voxel_downsample_batch_f32(lidar_handle *h, const float *
     char *base = static_cast<char *>(lidar::workspace(h, cv.off));
     if (!base) return LIDAR_ENOMEM;
     Ws w;
-    w.part = reinterpret_cast<uint32_t *>(base + opart);
+    w.gran = reinterpret_cast<unsigned long long *>(base + ogran);
     w.meta = reinterpret_cast<uint32_t *>(base + ometa);
     w.key = reinterpret_cast<uint32_t *>(base + okey);
     w.thist = reinterpret_cast<uint16_t *>(base + oth);
@@ -880,9 +935,12 @@ LIDAR_EXPORT int lidar_voxel_downsample_batch_f32(lidar_handle *h, const float *
     w.pairs = reinterpret_cast<uint64_t *>(base + opairs);
     w.scratch = reinterpret_cast<uint64_t *>(base + oscr);
     w.flags = reinterpret_cast<uint64_t *>(base + oflags);
-    hipLaunchKernelGGL(vx_bbox_kernel, dim3(NCH, (unsigned)batch), dim3(BT), 0, s, xyz, n, w, nb);
+    const uint32_t epoch = ++h->epoch == 0 ? ++h->epoch : h->epoch;  // never 0 (fresh memory)
+    if (ntiles > kFuseTiles)
+        hipLaunchKernelGGL(vx_extent_kernel, dim3(frame_grid(batch, ntiles)), dim3(KT), 0, s, xyz, n, w, ntiles, batch,
+                           epoch);
     hipLaunchKernelGGL(vx_keys_kernel, dim3(frame_grid(batch, ntiles)), dim3(KT), 0, s, xyz, n, voxel, w, ntiles,
-                       batch);
+                       batch, epoch, nb);
     hipLaunchKernelGGL(vx_scatter_kernel, dim3(frame_grid(batch, ntiles)), dim3(KT), 0, s, n, w, ntiles, batch);
     hipLaunchKernelGGL(vx_bucket_kernel, dim3(frame_grid(batch, nb)), dim3(UT), 0, s, xyz, n, w, voxel_id, centroids,
                        counts, nvox, batch);

@@ -3,7 +3,7 @@ separate passes, over tools/voxel_micro.py = one warm-up-free run of 20 lidar_vo
 calls on 32 x 65 536-point unit frames at voxel 0.05, the bench's voxel leg shape) to memory-side bytes per
 call and per kernel.  Units and the gfx950 correction as tools/pmc_traffic.py (FETCH_SIZE in KiB, doubled;
 WRITE_SIZE in KiB); the calibration passes of the same profile_round.sh call check both factors.  A call is
-the dispatches from one vb_bbox_kernel to the next.
+the dispatches from one vx_bbox_kernel to the next.
 
 usage: python tools/pmc_voxel.py gpurun_out/<tag> profiles/<round>/pmc_voxel.json
 """
@@ -21,9 +21,9 @@ FRAMES, N = 32, 65536
 def per_call(rs, counter):
     calls, cur = [], None
     for r in sorted(rs, key=lambda r: int(r["Dispatch_Id"])):
-        if r["Counter_Name"] != counter or "vb_" not in r["Kernel_Name"]:
+        if r["Counter_Name"] != counter or "vx_" not in r["Kernel_Name"]:
             continue
-        name = r["Kernel_Name"].split("vb_", 1)[1].split("(", 1)[0].split("<", 1)[0]
+        name = r["Kernel_Name"].split("vx_", 1)[1].split("(", 1)[0].split("<", 1)[0]
         if name == "bbox_kernel":
             cur = defaultdict(float)
             calls.append(cur)

@@ -52,6 +52,10 @@ PREFIXES = (
     ("fps_bucket_kernel<512,", "sa1_fps"),  # the pipeline's SA1 FPS (--fps-threads 512)
     ("fps_bucket_kernel<1024, 1, false>", "fps_1024"),  # SA2's nested FPS (and SA1 at --fps-threads 1024)
     ("fps_bucket_kernel<1024, 1, true>", "fps_1024"),
+    ("fps_bucket_kernel<1024, 1, false, 1>", "fps_1024"),  # round 5: + points per lane
+    ("fps_bucket_kernel<1024, 1, true, 1>", "fps_1024"),
+    ("fps_lazy_kernel<512,", "sa1_fps"),  # --fps-lazy
+    ("fps_lazy_kernel<1024,", "fps_1024"),
     ("bq_bin_kernel", "bq_bin"),
     ("bq_grid_kernel", "sa2_ball_query"),  # SA1's queries run inside its MLP kernel (bq="bin")
     ("ball_query_kernel", "ball_query_scan"),
@@ -76,6 +80,9 @@ PREFIXES = (
     ("dense_pack_kernel", "weight_pack"),
     ("dense_absmax_kernel", "weight_pack"),
     ("vb_", "voxel_batch"),
+    ("vx_", "voxel_batch"),
+    ("group_rows_kernel", "sa_generic"),
+    ("group_max_kernel", "sa_generic"),
     ("concat_xyz_pad_kernel", "concat"),
     ("dense_relu_kernel", "dense_relu_fp32"),
     ("__amd_rocclr_", "runtime_copy"),

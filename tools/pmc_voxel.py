@@ -3,7 +3,7 @@ separate passes, over tools/voxel_micro.py = one warm-up-free run of 20 lidar_vo
 calls on 32 x 65 536-point unit frames at voxel 0.05, the bench's voxel leg shape) to memory-side bytes per
 call and per kernel.  Units and the gfx950 correction as tools/pmc_traffic.py (FETCH_SIZE in KiB, doubled;
 WRITE_SIZE in KiB); the calibration passes of the same profile_round.sh call check both factors.  A call is
-the dispatches from one vx_bbox_kernel to the next.
+the dispatches from one call's first launch to the next's.
 
 usage: python tools/pmc_voxel.py gpurun_out/<tag> profiles/<round>/pmc_voxel.json
 """
@@ -24,9 +24,11 @@ def per_call(rs, counter):
         if r["Counter_Name"] != counter or "vx_" not in r["Kernel_Name"]:
             continue
         name = r["Kernel_Name"].split("vx_", 1)[1].split("(", 1)[0].split("<", 1)[0]
-        if name == "bbox_kernel":
-            cur = defaultdict(float)
-            calls.append(cur)
+        # a call starts at its first launch: bbox (round 4), extent (frames above 16 tiles) or keys
+        if name in ("bbox_kernel", "extent_kernel") or (name == "keys_kernel" and (cur is None or "keys_kernel" in cur)):
+            if not (name == "keys_kernel" and cur is not None and "extent_kernel" in cur and "keys_kernel" not in cur):
+                cur = defaultdict(float)
+                calls.append(cur)
         if cur is not None:
             cur[name] += float(r["Counter_Value"]) * 1024.0
     return calls[1:] if len(calls) > 1 else calls  # the first call also pays first-touch effects

@@ -956,3 +956,17 @@ def test_backbone_generic_shapes_bf16(cuda):
         pts, feats = cx, gf
     ga = tier_n.group_all(pts, feats, bb.weights[len(levels)][0], False)
     feat_close(g.cpu().numpy()[0], ga, "odd bf16 group_all on the GPU's last level", strict=True)
+
+
+@pytest.mark.parametrize("bq,l2", [("bin", True), ("side", False)])
+def test_streaming_generic_shapes_matches_forward(cuda, bq, l2):
+    """StreamingSSG over a configuration with generic branches at both level kinds (their ball queries
+    precomputed or binned on the side streams): bit-identical to forward()."""
+    bb = pn.PointNet2Backbone(ODD, device=cuda, seed=5)
+    xs = [torch.from_numpy(unit_frames(2, 4096, 40 + s)).to(cuda) for s in range(5)]
+    want = [bb.forward(x)[0] for x in xs]
+    got = pn.StreamingSSG(bb, 2, 4096, depth=2, fps_group=2, bq=bq, l2_side=l2).run(xs)
+    torch.cuda.synchronize()
+    assert len(got) == len(xs)
+    for a, b in zip(got, want):
+        assert torch.equal(a, b)

@@ -271,7 +271,7 @@ int lidar_voxel_downsample_f32(lidar_handle *h, const float *xyz, int64_t n, dou
 /* Voxel downsampling of `batch` frames of n points over the whole chip (csrc/voxel_batch.hip):
  * xyz (batch, n, 3) fp32; voxel_id (batch, n) int32; centroids (batch, n, 3) and counts (batch, n),
  * the first nvox[f] rows of frame f valid; nvox (batch,) int32 on the device (-1: the frame's extent
- * is not finite or its grid has 2^32 keys or more).  No host synchronisation; per frame equal to
+ * is not finite or its grid has 2^32 keys or more; -2: a bounded in-launch wait timed out, a bug).  No host synchronisation; per frame equal to
  * lidar_voxel_downsample_f32.  Workspace: lidar_voxel_batch_workspace_bytes(batch, n). */
 uint64_t lidar_voxel_batch_workspace_bytes(int64_t batch, int64_t n);
 int lidar_voxel_downsample_batch_f32(lidar_handle *h, const float *xyz, int64_t batch, int64_t n, double voxel,

@@ -467,15 +467,22 @@ __global__ __launch_bounds__(256, (BQ && !X1 && NS == 32) ? 5 : (R == 1 ? 3 : 2)
 #ifndef LIDAR_SA_ABL
 #define LIDAR_SA_ABL 0
 #endif
+// LIDAR_LEAN_R / LIDAR_LEAN_W: A/B builds only (tiles per layer-3 weight fragment; launch-bound waves)
+#ifndef LIDAR_LEAN_R
+#define LIDAR_LEAN_R 2
+#endif
+#ifndef LIDAR_LEAN_W
+#define LIDAR_LEAN_W 4
+#endif
 template <int C1, int C2, int C3, int NS, bool PFX>
-__global__ __launch_bounds__(256, 4) void sa_x3_lean_kernel(const float *__restrict__ P, int64_t stride,
+__global__ __launch_bounds__(256, LIDAR_LEAN_W) void sa_x3_lean_kernel(const float *__restrict__ P, int64_t stride,
                                                             const float *__restrict__ Q,
                                                             const int32_t *__restrict__ idx, int n, int m,
                                                             int64_t total, const uint4 *__restrict__ packed,
                                                             float *__restrict__ out, int64_t out_stride,
                                                             int64_t out_offset)
 {
-    constexpr int R = 2;
+    constexpr int R = LIDAR_LEAN_R;
     static_assert(NS % (16 * R) == 0 && C1 % 32 == 0 && C2 % 32 == 0 && C3 % 64 == 0, "tile shapes");
     using K = PackX3<C1, C2, C3, false>;
     constexpr int T2 = K::T2, T3 = K::T3, KS2 = K::KS2, KS3 = K::KS3;

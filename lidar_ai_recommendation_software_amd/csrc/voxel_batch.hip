@@ -6,7 +6,7 @@
 // (bx*ny + by)*nz + bz; voxels in ascending key order, voxel id = rank of the key (-1 for a point
 // outside every bin), centroid = sequential fp32 sum of the voxel's points in point order / count.
 //
-// Round 5: a two-level sort in three launches (round 4: an 8-bit LSD radix sort over global memory,
+// Round 5: a two-level sort in two launches (round 4: an 8-bit LSD radix sort over global memory,
 // 13 launches and ~284 B of memory traffic per point):
 //
 //   keys     grid (8192-point tiles, frames; a frame's tiles on one XCD, dispatched together): each
@@ -14,13 +14,15 @@
 //            polls its frame's other tiles' (an in-launch hand-off instead of a bbox launch), builds
 //            the frame's grid (float64, every workgroup alike), bins every point in float against
 //            per-axis LDS tables of the float64 edges' float thresholds (float64 beyond 4096 edges per
-//            axis; a point outside every bin takes nx ny nz, one past the last voxel), and writes its
-//            keys and its histogram over 4096 coarse bins (key >> hs, the top 12 bits of the range)
-//   scatter  grid (tiles, frames): each workgroup sums the frame's tile histograms itself (exclusive
-//            scan over the coarse bins, plus the counts of the tiles before it) and scatters its
-//            (key, index) pairs to their coarse bin (LDS atomics: order inside a bin is free, the
-//            buckets sort by (key, index) anyway); tile 0 also writes the bucket table (bucket b =
-//            the coarse bins whose start s has min(s NB / n, NB - 1) = b, ~1 536 points uniform)
+//            axis; a point outside every bin takes nx ny nz, one past the last voxel), and publishes
+//            its histogram over 4096 coarse bins (key >> hs, the top 12 bits of the range) as tagged
+//            granules too; then, from the frame's histograms (polled), the exclusive scan over the
+//            coarse bins plus the counts of the tiles before it, and it scatters its (key, index)
+//            pairs from registers to their coarse bins (LDS atomics: order inside a bin is free, the
+//            buckets sort by (key, index) anyway); tile 0 also writes the bucket table (bucket b = the
+//            coarse bins whose start s has min(s NB / n, NB - 1) = b, ~1 536 points uniform).
+//            Frames of more than 16 tiles (more than an XCD co-schedules) split this into an extent
+//            launch, a keys launch that writes the keys, and a scatter launch.
 //   bucket   grid (buckets, frames; 3 workgroups per CU): each bucket loads its pairs and gathers
 //            their xyz, sorts by (key, index) in LDS (a counting sort over the bucket's own key range
 //            with equal-key runs ranked by index in parallel; bitonic when the range or a run is too
@@ -31,7 +33,7 @@
 //            earlier), writes every point's voxel id and, one thread per voxel summing its points in
 //            index order, the centroids and counts.
 //
-// Memory-side bytes per point: xyz 12 (keys) + key 4 + 4 + pair 8 + 8 + id 4 + the xyz gather 12
+// Memory-side bytes per point: xyz 12 (keys) + pair 8 + 8 + id 4 + the xyz gather 12
 // (+16 per voxel out); no host synchronisation: nvox[f] lands on the device (-1: the frame's extent is
 // not finite, or its grid has 2^32 - 1 keys or more).
 #include <algorithm>
@@ -53,7 +55,7 @@ constexpr int CAP = 2048;          // pairs a bucket sorts in LDS
 constexpr int KMAX = 4096;         // local key range of the LDS counting sort
 constexpr int SEGMAX = 32;         // longest equal-key run the counting sort orders by index itself
 constexpr int BUCKET = 1536;       // target points per bucket
-constexpr int MW = 8;              // meta words per frame: [0] grid ok, [1] outside key, [2] hs
+constexpr int MW = 8;              // meta words per frame: [0] grid ok, [1] outside key, [2] hs, [3] hung
 constexpr uint64_t kPad = ~0ull;   // bitonic padding: sorts last
 static_assert(NBIN % KT == 0 && NBIN % UT == 0, "bins per thread");
 
@@ -71,7 +73,7 @@ struct Ws {  // per-batch workspace, every array frame-major
     unsigned long long *gran;  // [F][T][6] the tiles' extents: epoch << 32 | monotone bits (self-tagged granules)
     uint32_t *meta;    // [F][MW]
     uint32_t *key;     // [F][n]
-    uint16_t *thist;   // [F][T][NBIN] tile histograms of the coarse bins (a tile holds <= 8192 points)
+    unsigned long long *hgran;  // [F][T][NBIN / 2] tile histograms: epoch << 32 | count(2g + 1) << 16 | count(2g)
     uint32_t *bstart;  // [F][NB + 1] the buckets' first pairs (bstart[NB] = n)
     uint64_t *pairs;   // [F][n] (key << 32 | index), coarse-bin order
     uint64_t *scratch; // [F][n] the global sort's other buffer
@@ -125,6 +127,91 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *red, u
     }
     *tot = all;
     return pre + inc - v;
+}
+
+// ------------------------------------------------------------------------------------- scatter
+// tile t of frame f: sums the frame's tile histograms (polling their granules until every tag is this
+// call's), the exclusive scan over the coarse bins plus the counts of the tiles before it, the bucket
+// table (tile 0), then its (key, index) pairs to their coarse bins.  kv: the tile's keys (thread tid:
+// points t TILE + j KT + tid); off: NBIN words of LDS; red: KT / 64 words.
+__device__ __forceinline__ void scatter_tile(const uint32_t (&kv)[PPT], int64_t f, int64_t t, int64_t n, int ntiles,
+                                             int hs, uint32_t epoch, const Ws &w, uint32_t *off, uint32_t *red,
+                                             int64_t batch)
+{
+    const int tid = threadIdx.x;
+    // coarse bins BPT tid .. BPT tid + BPT - 1: frame totals and the counts of the tiles before this one
+    uint32_t tot[BPT], pre[BPT], sum = 0;
+#pragma unroll
+    for (int j = 0; j < BPT; ++j) tot[j] = pre[j] = 0;
+    const unsigned long long *hg = w.hgran + (int64_t)f * ntiles * (NBIN / 2) + (BPT / 2) * tid;
+    bool hung = false;
+    for (int u = 0; u < ntiles; ++u) {
+        unsigned long long g2[BPT / 2];
+        uint32_t spins = 0;
+        while (true) {  // bounded: a tile that never publishes is a bug, reported as nvox -2
+            bool ready = true;
+#pragma unroll
+            for (int e = 0; e < BPT / 2; ++e) {
+                g2[e] = __hip_atomic_load(&hg[(int64_t)u * (NBIN / 2) + e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ready = ready && (uint32_t)(g2[e] >> 32) == epoch;
+            }
+            if (ready) break;
+            if (++spins == (1u << 22)) {
+                hung = true;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+#pragma unroll
+        for (int j = 0; j < BPT; ++j) {
+            const uint32_t c = (uint32_t)(g2[j >> 1] >> (16 * (j & 1))) & 0xffffu;
+            tot[j] += c;
+            pre[j] += u < t ? c : 0u;
+        }
+    }
+    if (hung) w.meta[f * MW + 3] = 1u;
+#pragma unroll
+    for (int j = 0; j < BPT; ++j) sum += tot[j];
+    uint32_t all;
+    uint32_t ex = block_excl_scan<KT>(sum, red, &all);
+    uint32_t bsv[BPT];  // the frame-level start of each of this thread's bins
+#pragma unroll
+    for (int j = 0; j < BPT; ++j) {
+        bsv[j] = ex;
+        off[BPT * tid + j] = ex + pre[j];
+        ex += tot[j];
+    }
+    __syncthreads();
+    if (t == 0) {
+        // the bucket table: bucket b = the bins whose start s has bk(s) = min(s nb / n, nb - 1) = b, so
+        // its first pair is the start of the first bin with bk >= b; buckets past the last bin's bk start
+        // at n (empty), and bstart[nb] = n.  The previous bin's start: off[] still holds the frame-level
+        // starts in this workgroup (t = 0: no earlier tiles), read before the barrier below lets the
+        // scatter's atomics move them.
+        const int64_t nb = n_buckets(n);
+        const float inv = (float)nb / (float)n;
+        auto bk = [&](uint32_t st) { return min<int64_t>((int64_t)((float)st * inv), nb - 1); };
+        uint32_t *bst = w.bstart + (int64_t)f * (nb + 1);
+        int64_t prev = tid == 0 ? -1 : bk(off[BPT * tid - 1]);
+#pragma unroll
+        for (int j = 0; j < BPT; ++j) {
+            const int64_t cur = bk(bsv[j]);
+            for (int64_t q = prev + 1; q <= cur; ++q) bst[q] = bsv[j];
+            prev = cur;
+        }
+        if (tid == KT - 1)
+            for (int64_t q = prev + 1; q <= nb; ++q) bst[q] = (uint32_t)n;
+        __syncthreads();  // (uniform: t is the workgroup's)
+    }
+    uint64_t *pr = w.pairs + (int64_t)f * n;
+#pragma unroll
+    for (int j = 0; j < PPT; ++j) {
+        const int64_t i = (int64_t)t * TILE + j * KT + tid;
+        if (i < n) {
+            const uint32_t pos = atomicAdd(&off[kv[j] >> hs], 1u);
+            if (pos < (uint64_t)n) pr[pos] = ((uint64_t)kv[j] << 32) | (uint32_t)i;  // (hung: counts unknown)
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------------------- keys
@@ -217,6 +304,7 @@ __global__ __launch_bounds__(KT) void vx_extent_kernel(const float *__restrict__
     publish_extent(q, n, t, w.gran + (int64_t)f * ntiles * 6, epoch, red6);
 }
 
+template <bool FUSED>
 __global__ __launch_bounds__(KT) void vx_keys_kernel(const float *__restrict__ xyz, int64_t n, double voxel, Ws w,
                                                      int ntiles, int64_t batch, uint32_t epoch, int64_t nb)
 {
@@ -292,6 +380,7 @@ __global__ __launch_bounds__(KT) void vx_keys_kernel(const float *__restrict__ x
         m[0] = g.ok ? 1u : 0u;
         m[1] = okey;
         m[2] = (uint32_t)hs;
+        m[3] = 0u;  // set by a scatter whose histogram poll timed out (a bug): the frame reports nvox -2
     }
     if (!g.ok) return;  // whole workgroup (uniform)
     // the float thresholds of every axis' edges in LDS when each axis has <= ETAB edges and the grid's
@@ -315,10 +404,11 @@ __global__ __launch_bounds__(KT) void vx_keys_kernel(const float *__restrict__ x
         __syncthreads();
     }
     const uint32_t ny = (uint32_t)g.ax[1].nb, nz = (uint32_t)g.ax[2].nb;
-    uint32_t *k = w.key + (int64_t)f * n;
+    uint32_t kv[PPT];
 #pragma unroll
     for (int j = 0; j < PPT; ++j) {
         const int64_t i = (int64_t)t * TILE + j * KT + tid;
+        kv[j] = 0u;
         if (i < n) {
             uint32_t kk;
             if (tab) {
@@ -332,18 +422,37 @@ __global__ __launch_bounds__(KT) void vx_keys_kernel(const float *__restrict__ x
                 kk = lidar_vox::key(g, q[j][0], q[j][1], q[j][2]);
                 kk = kk == lidar_vox::kOutside ? okey : kk;  // sorts after every voxel's key
             }
-            k[i] = kk;
+            kv[j] = kk;
             atomicAdd(&hist[kk >> hs], 1u);
         }
     }
     __syncthreads();
-    uint16_t *th = w.thist + ((int64_t)f * ntiles + t) * NBIN;
+    // the tile's histogram as self-tagged granules (bins 2g, 2g + 1 in granule g; thread tid publishes
+    // the granules of its own scatter bins BPT tid .. BPT tid + 3)
+    unsigned long long *hg = w.hgran + ((int64_t)f * ntiles + t) * (NBIN / 2);
 #pragma unroll
-    for (int j = 0; j < BPT; ++j) th[tid + j * KT] = (uint16_t)hist[tid + j * KT];
+    for (int e = 0; e < BPT / 2; ++e) {
+        const int gi = (BPT / 2) * tid + e;
+        const unsigned long long v = ((unsigned long long)epoch << 32) | (hist[2 * gi + 1] << 16) | hist[2 * gi];
+        __hip_atomic_store(&hg[gi], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if constexpr (!FUSED) {  // the scatter launch follows
+        uint32_t *k = w.key + (int64_t)f * n;
+#pragma unroll
+        for (int j = 0; j < PPT; ++j) {
+            const int64_t i = (int64_t)t * TILE + j * KT + tid;
+            if (i < n) k[i] = kv[j];
+        }
+    } else {
+        // every tile of the frame is resident (<= kFuseTiles, one XCD): scatter straight from registers
+        __syncthreads();  // hist[] becomes the scatter's offsets
+        scatter_tile(kv, f, t, n, ntiles, hs, epoch, w, hist, &red6[0][0], batch);
+    }
 }
 
 // ------------------------------------------------------------------------------------- scatter
-__global__ __launch_bounds__(KT) void vx_scatter_kernel(int64_t n, Ws w, int ntiles, int64_t batch)
+// the scatter of frames above kFuseTiles tiles (the keys launch wrote the keys)
+__global__ __launch_bounds__(KT) void vx_scatter_kernel(int64_t n, Ws w, int ntiles, int64_t batch, uint32_t epoch)
 {
     int64_t f, t;
     if (!frame_part(batch, ntiles, f, t)) return;
@@ -354,68 +463,13 @@ __global__ __launch_bounds__(KT) void vx_scatter_kernel(int64_t n, Ws w, int nti
     __shared__ uint32_t off[NBIN];
     __shared__ uint32_t red[KT / 64];
     const uint32_t *k = w.key + (int64_t)f * n;
-    uint32_t kv[PPT];  // the tile's keys in flight while the histograms sum
+    uint32_t kv[PPT];
 #pragma unroll
     for (int j = 0; j < PPT; ++j) {
         const int64_t i = (int64_t)t * TILE + j * KT + tid;
         kv[j] = i < n ? k[i] : 0u;
     }
-    // coarse bins BPT tid .. BPT tid + BPT - 1: frame totals and the counts of the tiles before this one
-    uint32_t tot[BPT], pre[BPT], sum = 0;
-#pragma unroll
-    for (int j = 0; j < BPT; ++j) tot[j] = pre[j] = 0;
-    const uint16_t *th = w.thist + (int64_t)f * ntiles * NBIN + BPT * tid;
-    for (int u = 0; u < ntiles; ++u) {
-        const uint2 c4 = *reinterpret_cast<const uint2 *>(th + (int64_t)u * NBIN);  // 4 u16
-        const uint32_t c[4] = {c4.x & 0xffffu, c4.x >> 16, c4.y & 0xffffu, c4.y >> 16};
-#pragma unroll
-        for (int j = 0; j < BPT; ++j) {
-            tot[j] += c[j];
-            pre[j] += u < t ? c[j] : 0u;
-        }
-    }
-#pragma unroll
-    for (int j = 0; j < BPT; ++j) sum += tot[j];
-    uint32_t all;
-    uint32_t ex = block_excl_scan<KT>(sum, red, &all);
-    uint32_t bsv[BPT];  // the frame-level start of each of this thread's bins
-#pragma unroll
-    for (int j = 0; j < BPT; ++j) {
-        bsv[j] = ex;
-        off[BPT * tid + j] = ex + pre[j];
-        ex += tot[j];
-    }
-    __syncthreads();
-    if (t == 0) {
-        // the bucket table: bucket b = the bins whose start s has bk(s) = min(s nb / n, nb - 1) = b, so
-        // its first pair is the start of the first bin with bk >= b; buckets past the last bin's bk start
-        // at n (empty), and bstart[nb] = n.  The previous bin's start: off[] still holds the frame-level
-        // starts in this workgroup (t = 0: no earlier tiles), read before the barrier below lets the
-        // scatter's atomics move them.
-        const int64_t nb = n_buckets(n);
-        const float inv = (float)nb / (float)n;
-        auto bk = [&](uint32_t st) { return min<int64_t>((int64_t)((float)st * inv), nb - 1); };
-        uint32_t *bst = w.bstart + (int64_t)f * (nb + 1);
-        int64_t prev = tid == 0 ? -1 : bk(off[BPT * tid - 1]);
-#pragma unroll
-        for (int j = 0; j < BPT; ++j) {
-            const int64_t cur = bk(bsv[j]);
-            for (int64_t q = prev + 1; q <= cur; ++q) bst[q] = bsv[j];
-            prev = cur;
-        }
-        if (tid == KT - 1)
-            for (int64_t q = prev + 1; q <= nb; ++q) bst[q] = (uint32_t)n;
-        __syncthreads();  // (uniform: t is the workgroup's)
-    }
-    uint64_t *pr = w.pairs + (int64_t)f * n;
-#pragma unroll
-    for (int j = 0; j < PPT; ++j) {
-        const int64_t i = (int64_t)t * TILE + j * KT + tid;
-        if (i < n) {
-            const uint32_t pos = atomicAdd(&off[kv[j] >> hs], 1u);
-            pr[pos] = ((uint64_t)kv[j] << 32) | (uint32_t)i;
-        }
-    }
+    scatter_tile(kv, f, t, n, ntiles, hs, epoch, w, off, red, batch);
 }
 
 // ------------------------------------------------------------------------------------- buckets
@@ -560,8 +614,8 @@ __global__ __launch_bounds__(UT, 6) void vx_bucket_kernel(const float *__restric
 #endif
     VX_STAMP(0);
     const uint32_t *m = w.meta + (int64_t)f * MW;
-    if (!m[0]) {
-        if (b == 0 && tid == 0) nvox[f] = -1;
+    if (!m[0] || m[3]) {
+        if (b == 0 && tid == 0) nvox[f] = m[0] ? -2 : -1;
         return;  // every bucket of the frame returns: nothing waits on this frame's look-back words
     }
     const uint32_t okey = m[1];
@@ -891,7 +945,7 @@ LIDAR_EXPORT uint64_t lidar_voxel_batch_workspace_bytes(int64_t batch, int64_t n
     cv.take<unsigned long long>(batch * ntiles * 6);
     cv.take<uint32_t>(batch * MW);
     cv.take<uint32_t>(batch * n);
-    cv.take<uint16_t>(batch * ntiles * NBIN);
+    cv.take<unsigned long long>(batch * ntiles * (NBIN / 2));
     cv.take<uint32_t>(batch * (nb + 1));
     cv.take<uint64_t>(batch * n);
     cv.take<uint64_t>(batch * n);
@@ -920,7 +974,7 @@ LIDAR_EXPORT int lidar_voxel_downsample_batch_f32(lidar_handle *h, const float *
             "lidar_voxel_downsample_batch_f32: batch * n too large");
     lidar::Carver cv;
     const uint64_t ogran = cv.take<unsigned long long>(batch * ntiles * 6), ometa = cv.take<uint32_t>(batch * MW);
-    const uint64_t okey = cv.take<uint32_t>(batch * n), oth = cv.take<uint16_t>(batch * ntiles * NBIN);
+    const uint64_t okey = cv.take<uint32_t>(batch * n), oth = cv.take<unsigned long long>(batch * ntiles * (NBIN / 2));
     const uint64_t obst = cv.take<uint32_t>(batch * (nb + 1));
     const uint64_t opairs = cv.take<uint64_t>(batch * n), oscr = cv.take<uint64_t>(batch * n);
     const uint64_t oflags = cv.take<uint64_t>(batch * nb);
@@ -930,7 +984,7 @@ LIDAR_EXPORT int lidar_voxel_downsample_batch_f32(lidar_handle *h, const float *
     w.gran = reinterpret_cast<unsigned long long *>(base + ogran);
     w.meta = reinterpret_cast<uint32_t *>(base + ometa);
     w.key = reinterpret_cast<uint32_t *>(base + okey);
-    w.thist = reinterpret_cast<uint16_t *>(base + oth);
+    w.hgran = reinterpret_cast<unsigned long long *>(base + oth);
     w.bstart = reinterpret_cast<uint32_t *>(base + obst);
     w.pairs = reinterpret_cast<uint64_t *>(base + opairs);
     w.scratch = reinterpret_cast<uint64_t *>(base + oscr);
@@ -939,9 +993,15 @@ LIDAR_EXPORT int lidar_voxel_downsample_batch_f32(lidar_handle *h, const float *
     if (ntiles > kFuseTiles)
         hipLaunchKernelGGL(vx_extent_kernel, dim3(frame_grid(batch, ntiles)), dim3(KT), 0, s, xyz, n, w, ntiles, batch,
                            epoch);
-    hipLaunchKernelGGL(vx_keys_kernel, dim3(frame_grid(batch, ntiles)), dim3(KT), 0, s, xyz, n, voxel, w, ntiles,
-                       batch, epoch, nb);
-    hipLaunchKernelGGL(vx_scatter_kernel, dim3(frame_grid(batch, ntiles)), dim3(KT), 0, s, n, w, ntiles, batch);
+    if (ntiles <= kFuseTiles) {  // keys + scatter in one launch (a frame's tiles all resident)
+        hipLaunchKernelGGL(vx_keys_kernel<true>, dim3(frame_grid(batch, ntiles)), dim3(KT), 0, s, xyz, n, voxel, w,
+                           ntiles, batch, epoch, nb);
+    } else {
+        hipLaunchKernelGGL(vx_keys_kernel<false>, dim3(frame_grid(batch, ntiles)), dim3(KT), 0, s, xyz, n, voxel, w,
+                           ntiles, batch, epoch, nb);
+        hipLaunchKernelGGL(vx_scatter_kernel, dim3(frame_grid(batch, ntiles)), dim3(KT), 0, s, n, w, ntiles, batch,
+                           epoch);
+    }
     hipLaunchKernelGGL(vx_bucket_kernel, dim3(frame_grid(batch, nb)), dim3(UT), 0, s, xyz, n, w, voxel_id, centroids,
                        counts, nvox, batch);
     LAUNCH_CHECK();

@@ -122,7 +122,8 @@ def voxel_downsample_batch(xyz, voxel, slot=0):
     (lidar_voxel_downsample_batch_f32; per frame equal to data_processing.voxel_downsample).
     Returns device tensors (centroids (B, N, 3), voxel_id (B, N) int32, counts (B, N) int32,
     nvox (B,) int32): the first nvox[f] centroid / count rows of frame f are valid; nvox -1 marks
-    a frame whose extent is not finite or whose voxel grid has 2^32 keys or more.  Voxels are
+    a frame whose extent is not finite or whose voxel grid has 2^32 keys or more (-2: one of the
+    launch's bounded in-launch waits timed out — a bug, never expected).  Voxels are
     calculate_grid_density's grid extended to z (data_processing.voxel_downsample)."""
     _dev_check(xyz)
     if xyz.dtype != torch.float32 or xyz.dim() != 3 or xyz.shape[2] != 3:

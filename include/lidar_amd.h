@@ -50,6 +50,9 @@ int lidar_reserve(lidar_handle *h, uint64_t bytes);
 /* free the workspaces retired by growth (*freed = their bytes, may be NULL); the caller guarantees
  * that the work it queued with this handle before the growth has completed */
 int lidar_trim(lidar_handle *h, uint64_t *freed);
+/* testing aid: grow the workspace to `bytes` and fill it with tag-like garbage (high halves 1..64) on
+ * `stream` — the library never trusts what an earlier call left in the workspace */
+int lidar_debug_fill_workspace(lidar_handle *h, uint64_t bytes, uint64_t seed, void *stream);
 
 const char *lidar_last_error(void);
 int lidar_version(void); /* 4 (what changed per version) */

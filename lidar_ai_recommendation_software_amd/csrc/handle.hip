@@ -110,6 +110,31 @@ LIDAR_EXPORT int lidar_reserve(lidar_handle *h, uint64_t bytes)
     return LIDAR_OK;
 }
 
+namespace {
+__global__ void fill_workspace_kernel(unsigned long long *w, uint64_t words, unsigned long long seed)
+{
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += (uint64_t)gridDim.x * blockDim.x)
+        w[i] = ((unsigned long long)(i % 64 + 1) << 32) | (unsigned long long)(uint32_t)(seed * (i + 1));
+}
+}  // namespace
+
+// Testing aid: grows the workspace to `bytes` and fills it with words whose high halves cycle through
+// 1..64 (the tags the next in-launch hand-offs of a fresh handle use), on `stream`: no operation may
+// trust what an earlier one left there (tests/test_gpu_tier_r.py::test_voxel_ignores_workspace_leftovers).
+LIDAR_EXPORT int lidar_debug_fill_workspace(lidar_handle *h, uint64_t bytes, uint64_t seed, void *stream)
+{
+    REQUIRE(h != nullptr, "lidar_debug_fill_workspace: null handle");
+    ON_DEVICE(h->device);
+    void *w = lidar::workspace(h, bytes);
+    if (!w) return LIDAR_ENOMEM;
+    const uint64_t words = h->ws_bytes / 8;
+    if (words == 0) return LIDAR_OK;
+    hipLaunchKernelGGL(fill_workspace_kernel, dim3(1024), dim3(256), 0, static_cast<hipStream_t>(stream),
+                       static_cast<unsigned long long *>(h->ws), words, (unsigned long long)seed);
+    LAUNCH_CHECK();
+    return LIDAR_OK;
+}
+
 // Frees the workspaces retired by growth.  The caller guarantees that no work it queued with this
 // handle before the growth is still pending (e.g. after synchronising the streams it used).
 LIDAR_EXPORT int lidar_trim(lidar_handle *h, uint64_t *freed)

@@ -628,13 +628,13 @@ __global__ __launch_bounds__(UT, 6) void vx_bucket_kernel(const float *__restric
     __shared__ uint32_t spins_dbg;
 #endif
     // the bucket's pairs [bstart[b], bstart[b + 1]) (the scatter launch's bucket table)
-    if (tid < 2) rng[tid] = w.bstart[(int64_t)f * (nb + 1) + b + tid];
+    if (tid < 2) rng[tid] = min(w.bstart[(int64_t)f * (nb + 1) + b + tid], (uint32_t)n);  // (defensive: <= n)
     if (tid == 2) rng[2] = 0xffffffffu;  // [2], [3]: key min / max
     if (tid == 3) rng[3] = 0u;
     if (tid == 0) flag = 0;
     __syncthreads();
     VX_STAMP(1);
-    const int64_t p0 = rng[0], size = (int64_t)rng[1] - rng[0];
+    const int64_t p0 = rng[0], size = max<int64_t>(0, (int64_t)rng[1] - rng[0]);
     const uint64_t *gp = w.pairs + (int64_t)f * n + p0;
     const float *p = xyz + (int64_t)f * n * 3;
     const uint64_t *seq;   // the bucket sorted by (key, index): LDS or global
@@ -942,10 +942,9 @@ LIDAR_EXPORT uint64_t lidar_voxel_batch_workspace_bytes(int64_t batch, int64_t n
 {
     const int64_t ntiles = (n + TILE - 1) / TILE, nb = (n + BUCKET - 1) / BUCKET;
     lidar::Carver cv;
-    cv.take<unsigned long long>(batch * ntiles * 6);
+    cv.take<unsigned long long>(batch * ntiles * (6 + NBIN / 2));
     cv.take<uint32_t>(batch * MW);
     cv.take<uint32_t>(batch * n);
-    cv.take<unsigned long long>(batch * ntiles * (NBIN / 2));
     cv.take<uint32_t>(batch * (nb + 1));
     cv.take<uint64_t>(batch * n);
     cv.take<uint64_t>(batch * n);
@@ -973,8 +972,11 @@ LIDAR_EXPORT int lidar_voxel_downsample_batch_f32(lidar_handle *h, const float *
     REQUIRE((int64_t)frame_grid(batch, std::max<int64_t>(ntiles, nb)) < 0x7fffffff,
             "lidar_voxel_downsample_batch_f32: batch * n too large");
     lidar::Carver cv;
-    const uint64_t ogran = cv.take<unsigned long long>(batch * ntiles * 6), ometa = cv.take<uint32_t>(batch * MW);
-    const uint64_t okey = cv.take<uint32_t>(batch * n), oth = cv.take<unsigned long long>(batch * ntiles * (NBIN / 2));
+    // the granules of the in-launch hand-offs (extents, then histograms), zeroed below: a tag is only
+    // ever read from words this call zeroed or published, never from another operation's leftovers
+    const int64_t ngran = batch * ntiles * (6 + NBIN / 2);
+    const uint64_t ogran = cv.take<unsigned long long>(ngran), ometa = cv.take<uint32_t>(batch * MW);
+    const uint64_t okey = cv.take<uint32_t>(batch * n);
     const uint64_t obst = cv.take<uint32_t>(batch * (nb + 1));
     const uint64_t opairs = cv.take<uint64_t>(batch * n), oscr = cv.take<uint64_t>(batch * n);
     const uint64_t oflags = cv.take<uint64_t>(batch * nb);
@@ -984,12 +986,13 @@ LIDAR_EXPORT int lidar_voxel_downsample_batch_f32(lidar_handle *h, const float *
     w.gran = reinterpret_cast<unsigned long long *>(base + ogran);
     w.meta = reinterpret_cast<uint32_t *>(base + ometa);
     w.key = reinterpret_cast<uint32_t *>(base + okey);
-    w.hgran = reinterpret_cast<unsigned long long *>(base + oth);
+    w.hgran = w.gran + batch * ntiles * 6;
     w.bstart = reinterpret_cast<uint32_t *>(base + obst);
     w.pairs = reinterpret_cast<uint64_t *>(base + opairs);
     w.scratch = reinterpret_cast<uint64_t *>(base + oscr);
     w.flags = reinterpret_cast<uint64_t *>(base + oflags);
-    const uint32_t epoch = ++h->epoch == 0 ? ++h->epoch : h->epoch;  // never 0 (fresh memory)
+    const uint32_t epoch = ++h->epoch == 0 ? ++h->epoch : h->epoch;  // never 0 (the zeroed granules)
+    HIP_TRY(hipMemsetAsync(w.gran, 0, (size_t)ngran * sizeof(unsigned long long), s));
     if (ntiles > kFuseTiles)
         hipLaunchKernelGGL(vx_extent_kernel, dim3(frame_grid(batch, ntiles)), dim3(KT), 0, s, xyz, n, w, ntiles, batch,
                            epoch);

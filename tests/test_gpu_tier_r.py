@@ -149,6 +149,31 @@ def test_voxel_keys_table_and_float64_paths(cuda, case):
     assert np.array_equal(c, wc), case
 
 
+@pytest.mark.parametrize("B,n", [(32, 65536), (3, 20000), (1, 150001)])
+def test_voxel_ignores_workspace_leftovers(cuda, B, n):
+    """The batched voxel path's in-launch hand-offs read only granules the same call zeroed or published:
+    a workspace full of tag-like garbage (high halves 1..64, the next calls' tags) changes nothing."""
+    import torch
+    from lidar_ai_recommendation_software_amd import _native as nat
+    from lidar_ai_recommendation_software_amd import pointnet2 as pn
+    from lidar_ai_recommendation_software_amd.synthetic import unit_frames
+    x = unit_frames(B, n, 8)
+    xt = torch.from_numpy(x).to(cuda)
+    h = nat.handle(0)
+    need = nat.load_library().lidar_voxel_batch_workspace_bytes(B, n) + (1 << 20)
+    for seed in (1, 2, 3):
+        nat.call("lidar_debug_fill_workspace", h, need, seed, nat.stream_ptr())
+        c, vid, cnt, nv = pn.voxel_downsample_batch(xt, 0.05)
+        torch.cuda.synchronize()
+        nv = nv.cpu().numpy()
+        for f in (0, B - 1):
+            wc, wvid, wcnt = tier_n.voxel_downsample(x[f], 0.05)
+            assert nv[f] == len(wc), (seed, f)
+            assert np.array_equal(vid[f].cpu().numpy(), wvid)
+            assert np.array_equal(cnt[f, :nv[f]].cpu().numpy(), wcnt)
+            assert np.array_equal(c[f, :nv[f]].cpu().numpy(), wc)
+
+
 def test_fps_extension(cuda):
     x = uniform_frame(5000, 1, -1, 1).astype(np.float32)
     assert np.array_equal(dp.farthest_point_sample(x, 256), tier_n.fps(x, 256))

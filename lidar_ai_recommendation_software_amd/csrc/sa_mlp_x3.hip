@@ -665,10 +665,19 @@ __global__ __launch_bounds__(256, LIDAR_LEAN_W) void sa_x3_lean_kernel(const flo
     }
 }
 
-// LIDAR_X3_ROWS: 16-row tiles per wavefront (A/B builds; 2 unless NS = 16)
+// LIDAR_X3_ROWS: 16-row tiles per wavefront (A/B builds; 2 unless NS = 16); LIDAR_X1_ROWS the same for
+// the bf16 spec's kernels (X1: half the registers per tile)
 #ifndef LIDAR_X3_ROWS
 #define LIDAR_X3_ROWS 2
 #endif
+#ifndef LIDAR_X1_ROWS
+#define LIDAR_X1_ROWS 2
+#endif
+template <int NS, bool X1>
+constexpr int rows_for()
+{
+    return X1 && NS >= 16 * LIDAR_X1_ROWS ? LIDAR_X1_ROWS : (NS >= 16 * LIDAR_X3_ROWS ? LIDAR_X3_ROWS : 1);
+}
 
 template <int C1, int C2, int C3, int NS>
 int launch_x3_lean(const float *p, int64_t stride, const float *q, const int32_t *idx, int64_t batch, int64_t n,
@@ -689,7 +698,7 @@ int launch_x3(const float *p, int64_t stride, const float *q, const int32_t *idx
               int64_t m, const void *packed, float *out, int64_t os, int64_t oo, hipStream_t s,
               const float *xyz = nullptr, const float *centres = nullptr)
 {
-    constexpr int R = NS >= 16 * LIDAR_X3_ROWS ? LIDAR_X3_ROWS : 1;
+    constexpr int R = rows_for<NS, X1>();
     const int64_t total = batch * m;
     const int64_t blocks = (total + 3) / 4;
     REQUIRE(blocks <= 0x7fffffff, "sa_group_mlp_x3: too many centres");
@@ -705,7 +714,7 @@ int launch_x3_bq(const float *xyz, const char *grid, const float *centres, int64
                  float radius, const void *packed, float *out, int64_t os, int64_t oo, int32_t *out_idx,
                  hipStream_t s)
 {
-    constexpr int R = NS >= 16 * LIDAR_X3_ROWS ? LIDAR_X3_ROWS : 1;
+    constexpr int R = rows_for<NS, X1>();
     const int64_t total = batch * m;
     const int64_t blocks = (total + 3) / 4;
     REQUIRE(blocks <= 0x7fffffff, "sa_group_mlp_bq: too many centres");

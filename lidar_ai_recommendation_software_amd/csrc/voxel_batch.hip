@@ -366,6 +366,7 @@ __global__ __launch_bounds__(KT) void vx_keys_kernel(const float *__restrict__ x
 #pragma unroll
             for (int kk = 0; kk < 6; ++kk)  // hung: NaN extent, the grid fails
                 if (lane == kk) ext[kk] = ok ? m[kk] : ord(__builtin_nanf(""));
+            if (!ok && lane == 0) w.meta[f * MW + 3] = 1u;  // reported as nvox -2
         }
     }
     __syncthreads();
@@ -379,8 +380,7 @@ __global__ __launch_bounds__(KT) void vx_keys_kernel(const float *__restrict__ x
     if (t == 0 && tid == 0) {
         m[0] = g.ok ? 1u : 0u;
         m[1] = okey;
-        m[2] = (uint32_t)hs;
-        m[3] = 0u;  // set by a scatter whose histogram poll timed out (a bug): the frame reports nvox -2
+        m[2] = (uint32_t)hs;  // (m[3], the hung flag, starts at 0: the host's memset)
     }
     if (!g.ok) return;  // whole workgroup (uniform)
     // the float thresholds of every axis' edges in LDS when each axis has <= ETAB edges and the grid's
@@ -615,7 +615,7 @@ __global__ __launch_bounds__(UT, 6) void vx_bucket_kernel(const float *__restric
     VX_STAMP(0);
     const uint32_t *m = w.meta + (int64_t)f * MW;
     if (!m[0] || m[3]) {
-        if (b == 0 && tid == 0) nvox[f] = m[0] ? -2 : -1;
+        if (b == 0 && tid == 0) nvox[f] = m[3] ? -2 : -1;
         return;  // every bucket of the frame returns: nothing waits on this frame's look-back words
     }
     const uint32_t okey = m[1];
@@ -992,7 +992,8 @@ LIDAR_EXPORT int lidar_voxel_downsample_batch_f32(lidar_handle *h, const float *
     w.scratch = reinterpret_cast<uint64_t *>(base + oscr);
     w.flags = reinterpret_cast<uint64_t *>(base + oflags);
     const uint32_t epoch = ++h->epoch == 0 ? ++h->epoch : h->epoch;  // never 0 (the zeroed granules)
-    HIP_TRY(hipMemsetAsync(w.gran, 0, (size_t)ngran * sizeof(unsigned long long), s));
+    // granules and the meta words (adjacent in the carve): tags and the hung flag start at 0
+    HIP_TRY(hipMemsetAsync(base + ogran, 0, (size_t)(ometa + batch * MW * sizeof(uint32_t) - ogran), s));
     if (ntiles > kFuseTiles)
         hipLaunchKernelGGL(vx_extent_kernel, dim3(frame_grid(batch, ntiles)), dim3(KT), 0, s, xyz, n, w, ntiles, batch,
                            epoch);

@@ -78,6 +78,7 @@ struct Ws {  // per-batch workspace, every array frame-major
     uint64_t *pairs;   // [F][n] (key << 32 | index), coarse-bin order
     uint64_t *scratch; // [F][n] the global sort's other buffer
     uint64_t *flags;   // [F][NB] look-back words: status << 32 | count
+    float *cent_diag;  // VX_DIAG_KEYS builds only: the centroids output, whose tail rows take the stamps
 };
 
 __device__ __forceinline__ int64_t n_buckets(int64_t n) { return (n + BUCKET - 1) / BUCKET; }
@@ -134,9 +135,19 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *red, u
 // call's), the exclusive scan over the coarse bins plus the counts of the tiles before it, the bucket
 // table (tile 0), then its (key, index) pairs to their coarse bins.  kv: the tile's keys (thread tid:
 // points t TILE + j KT + tid); off: NBIN words of LDS; red: KT / 64 words.
+#ifdef VX_DIAG_KEYS
+#define VX_KSTAMP(k)                                                                  \
+    do {                                                                              \
+        uint64_t t_;                                                                  \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");  \
+        kts[k] = t_;                                                                  \
+    } while (0)
+#else
+#define VX_KSTAMP(k)
+#endif
 __device__ __forceinline__ void scatter_tile(const uint32_t (&kv)[PPT], int64_t f, int64_t t, int64_t n, int ntiles,
                                              int hs, uint32_t epoch, const Ws &w, uint32_t *off, uint32_t *red,
-                                             int64_t batch)
+                                             int64_t batch, uint64_t *kts = nullptr)
 {
     const int tid = threadIdx.x;
     // coarse bins BPT tid .. BPT tid + BPT - 1: frame totals and the counts of the tiles before this one
@@ -145,16 +156,25 @@ __device__ __forceinline__ void scatter_tile(const uint32_t (&kv)[PPT], int64_t 
     for (int j = 0; j < BPT; ++j) tot[j] = pre[j] = 0;
     const unsigned long long *hg = w.hgran + (int64_t)f * ntiles * (NBIN / 2) + (BPT / 2) * tid;
     bool hung = false;
-    for (int u = 0; u < ntiles; ++u) {
-        unsigned long long g2[BPT / 2];
+    // four tiles' granules per pass, every load in flight together (one round trip per pass, not per tile)
+    constexpr int UCH = 4;
+    for (int u0 = 0; u0 < ntiles; u0 += UCH) {
+        unsigned long long g2[UCH][BPT / 2];
         uint32_t spins = 0;
         while (true) {  // bounded: a tile that never publishes is a bug, reported as nvox -2
             bool ready = true;
 #pragma unroll
-            for (int e = 0; e < BPT / 2; ++e) {
-                g2[e] = __hip_atomic_load(&hg[(int64_t)u * (NBIN / 2) + e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                ready = ready && (uint32_t)(g2[e] >> 32) == epoch;
-            }
+            for (int uu = 0; uu < UCH; ++uu)
+#pragma unroll
+                for (int e = 0; e < BPT / 2; ++e) {
+                    g2[uu][e] = u0 + uu < ntiles ? __hip_atomic_load(&hg[(int64_t)(u0 + uu) * (NBIN / 2) + e],
+                                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                                 : ((unsigned long long)epoch << 32);
+                }
+#pragma unroll
+            for (int uu = 0; uu < UCH; ++uu)
+#pragma unroll
+                for (int e = 0; e < BPT / 2; ++e) ready = ready && (uint32_t)(g2[uu][e] >> 32) == epoch;
             if (ready) break;
             if (++spins == (1u << 22)) {
                 hung = true;
@@ -163,13 +183,16 @@ __device__ __forceinline__ void scatter_tile(const uint32_t (&kv)[PPT], int64_t 
             __builtin_amdgcn_s_sleep(2);
         }
 #pragma unroll
-        for (int j = 0; j < BPT; ++j) {
-            const uint32_t c = (uint32_t)(g2[j >> 1] >> (16 * (j & 1))) & 0xffffu;
-            tot[j] += c;
-            pre[j] += u < t ? c : 0u;
-        }
+        for (int uu = 0; uu < UCH; ++uu)
+#pragma unroll
+            for (int j = 0; j < BPT; ++j) {
+                const uint32_t c = (uint32_t)(g2[uu][j >> 1] >> (16 * (j & 1))) & 0xffffu;  // 0 past ntiles
+                tot[j] += c;
+                pre[j] += u0 + uu < t ? c : 0u;
+            }
     }
     if (hung) w.meta[f * MW + 3] = 1u;
+    VX_KSTAMP(6);
 #pragma unroll
     for (int j = 0; j < BPT; ++j) sum += tot[j];
     uint32_t all;
@@ -203,7 +226,10 @@ __device__ __forceinline__ void scatter_tile(const uint32_t (&kv)[PPT], int64_t 
             for (int64_t q = prev + 1; q <= nb; ++q) bst[q] = (uint32_t)n;
         __syncthreads();  // (uniform: t is the workgroup's)
     }
+    VX_KSTAMP(8);
+    VX_KSTAMP(7);
     uint64_t *pr = w.pairs + (int64_t)f * n;
+    (void)kts;
 #pragma unroll
     for (int j = 0; j < PPT; ++j) {
         const int64_t i = (int64_t)t * TILE + j * KT + tid;
@@ -230,22 +256,26 @@ __device__ __forceinline__ float ru_float(double e)
 
 // lidar_vox::bin of float p from the axis' threshold table E[0, L) (E[i] = ru_float(e[i])): the same
 // count of edges <= p, found with float compares; lastf = e[L - 1] when it is a float, else NaN
-__device__ __forceinline__ uint32_t bin_tab(const float *E, int L, float p, float s0, float inv, float lastf)
+__device__ __forceinline__ int bin_tab_c(const float *E, int L, float p, float s0, float inv)
 {
     const float gf = floorf((p - s0) * inv);                           // the bin's guess (any error: fixed below)
     const int b = (int)fminf(fmaxf(gf, 0.f), (float)(L - 1));          // NaN -> 0
     const float e0 = E[b > 0 ? b - 1 : 0], e1 = E[b], e2 = E[b + 1 < L ? b + 1 : b];
-    // c = #{i : E[i] <= p}: b + 1 when E[b] <= p < E[b + 1], b when E[b - 1] <= p < E[b]
-    int c = e1 <= p ? (b + 1 == L ? L : (p < e2 ? b + 1 : -1)) : (b == 0 ? 0 : (e0 <= p ? b : -1));
-    if (c < 0) {  // the guess was off by more than one bin: binary search
-        int lo = 0, hi = L;
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (E[mid] <= p) lo = mid + 1;
-            else hi = mid;
-        }
-        c = lo;
+    // c = #{i : E[i] <= p}: b + 1 when E[b] <= p < E[b + 1], b when E[b - 1] <= p < E[b]; -1: search
+    return e1 <= p ? (b + 1 == L ? L : (p < e2 ? b + 1 : -1)) : (b == 0 ? 0 : (e0 <= p ? b : -1));
+}
+__device__ __forceinline__ int bin_tab_search(const float *E, int L, float p)  // the guess was off by > 1 bin
+{
+    int lo = 0, hi = L;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (E[mid] <= p) lo = mid + 1;
+        else hi = mid;
     }
+    return lo;
+}
+__device__ __forceinline__ uint32_t bin_of_c(int c, float p, float lastf, int L)
+{
     if (p == lastf) --c;  // the last edge is closed
     return (c >= 1 && c <= L - 1) ? (uint32_t)(c - 1) : lidar_vox::kOutside;
 }
@@ -311,6 +341,12 @@ __global__ __launch_bounds__(KT) void vx_keys_kernel(const float *__restrict__ x
     int64_t f, t;
     if (!frame_part(batch, ntiles, f, t)) return;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#ifdef VX_DIAG_KEYS
+    uint64_t kts[10] = {};
+#else
+    uint64_t *kts = nullptr;
+#endif
+    VX_KSTAMP(0);
     __shared__ uint32_t ext[6];
     __shared__ uint32_t red6[KT / 64][6];
     __shared__ uint32_t hist[NBIN];
@@ -336,6 +372,7 @@ __global__ __launch_bounds__(KT) void vx_keys_kernel(const float *__restrict__ x
         // frame whose tiles never all arrive reports a non-finite extent: nvox -1).
         unsigned long long *gr = w.gran + (int64_t)f * ntiles * 6;
         publish_extent(q, n, t, gr, epoch, red6);
+        VX_KSTAMP(1);
         if (wave == 0) {
             uint32_t m[6] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0u, 0u, 0u};
             bool ok = true;
@@ -397,36 +434,62 @@ __global__ __launch_bounds__(KT) void vx_keys_kernel(const float *__restrict__ x
         inv[a] = (float)ax.inv;
         lastf[a] = (double)(float)ax.last == ax.last ? (float)ax.last : __builtin_nanf("");
     }
+    VX_KSTAMP(2);
     if (tab) {
 #pragma unroll
         for (int a = 0; a < 3; ++a)
             for (int i = tid; i < L[a]; i += KT) etab[a][i] = ru_float(lidar_vox::edge(g.ax[a], i));
         __syncthreads();
     }
+    VX_KSTAMP(3);
     const uint32_t ny = (uint32_t)g.ax[1].nb, nz = (uint32_t)g.ax[2].nb;
     uint32_t kv[PPT];
+    if (tab) {
+        // the table lookups of half the tile's points in flight together (branch-free), the rare guess
+        // off by more than a bin fixed afterwards
+        constexpr int H = PPT / 2;
+#pragma unroll
+        for (int h0 = 0; h0 < PPT; h0 += H) {
+            int c[H][3];
+            bool miss = false;
+#pragma unroll
+            for (int j = 0; j < H; ++j)
+#pragma unroll
+                for (int a = 0; a < 3; ++a) {
+                    c[j][a] = bin_tab_c(etab[a], L[a], q[h0 + j][a], s0[a], inv[a]);
+                    miss = miss || c[j][a] < 0;
+                }
+            if (miss)
+#pragma unroll
+                for (int j = 0; j < H; ++j)
+#pragma unroll
+                    for (int a = 0; a < 3; ++a)
+                        if (c[j][a] < 0) c[j][a] = bin_tab_search(etab[a], L[a], q[h0 + j][a]);
+#pragma unroll
+            for (int j = 0; j < H; ++j) {
+                const uint32_t bx = bin_of_c(c[j][0], q[h0 + j][0], lastf[0], L[0]);
+                const uint32_t by = bin_of_c(c[j][1], q[h0 + j][1], lastf[1], L[1]);
+                const uint32_t bz = bin_of_c(c[j][2], q[h0 + j][2], lastf[2], L[2]);
+                // (bx ny + by) nz + bz < nx ny nz < 2^32: exact in 32 bits
+                const bool out = bx == lidar_vox::kOutside || by == lidar_vox::kOutside || bz == lidar_vox::kOutside;
+                kv[h0 + j] = out ? okey : (bx * ny + by) * nz + bz;
+            }
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < PPT; ++j) {
+            const uint32_t kk = lidar_vox::key(g, q[j][0], q[j][1], q[j][2]);
+            kv[j] = kk == lidar_vox::kOutside ? okey : kk;  // sorts after every voxel's key
+        }
+    }
 #pragma unroll
     for (int j = 0; j < PPT; ++j) {
         const int64_t i = (int64_t)t * TILE + j * KT + tid;
-        kv[j] = 0u;
-        if (i < n) {
-            uint32_t kk;
-            if (tab) {
-                const uint32_t bx = bin_tab(etab[0], L[0], q[j][0], s0[0], inv[0], lastf[0]);
-                const uint32_t by = bin_tab(etab[1], L[1], q[j][1], s0[1], inv[1], lastf[1]);
-                const uint32_t bz = bin_tab(etab[2], L[2], q[j][2], s0[2], inv[2], lastf[2]);
-                // (bx ny + by) nz + bz < nx ny nz < 2^32: exact in 32 bits
-                const bool out = bx == lidar_vox::kOutside || by == lidar_vox::kOutside || bz == lidar_vox::kOutside;
-                kk = out ? okey : (bx * ny + by) * nz + bz;
-            } else {
-                kk = lidar_vox::key(g, q[j][0], q[j][1], q[j][2]);
-                kk = kk == lidar_vox::kOutside ? okey : kk;  // sorts after every voxel's key
-            }
-            kv[j] = kk;
-            atomicAdd(&hist[kk >> hs], 1u);
-        }
+        if (i < n) atomicAdd(&hist[kv[j] >> hs], 1u);
+        else kv[j] = 0u;
     }
     __syncthreads();
+    VX_KSTAMP(4);
     // the tile's histogram as self-tagged granules (bins 2g, 2g + 1 in granule g; thread tid publishes
     // the granules of its own scatter bins BPT tid .. BPT tid + 3)
     unsigned long long *hg = w.hgran + ((int64_t)f * ntiles + t) * (NBIN / 2);
@@ -446,8 +509,16 @@ __global__ __launch_bounds__(KT) void vx_keys_kernel(const float *__restrict__ x
     } else {
         // every tile of the frame is resident (<= kFuseTiles, one XCD): scatter straight from registers
         __syncthreads();  // hist[] becomes the scatter's offsets
-        scatter_tile(kv, f, t, n, ntiles, hs, epoch, w, hist, &red6[0][0], batch);
+        VX_KSTAMP(5);
+        scatter_tile(kv, f, t, n, ntiles, hs, epoch, w, hist, &red6[0][0], batch, kts);
     }
+#ifdef VX_DIAG_KEYS
+    VX_KSTAMP(9);
+    if (tid == 0) {  // diagnostic build only: stamps into the tail rows of the frame's centroids
+        uint64_t *d = reinterpret_cast<uint64_t *>(w.cent_diag + (f + 1) * n * 3) - 10 * (t + 1);
+        for (int k = 0; k < 10; ++k) d[k] = kts[k];
+    }
+#endif
 }
 
 // ------------------------------------------------------------------------------------- scatter
@@ -991,6 +1062,7 @@ LIDAR_EXPORT int lidar_voxel_downsample_batch_f32(lidar_handle *h, const float *
     w.pairs = reinterpret_cast<uint64_t *>(base + opairs);
     w.scratch = reinterpret_cast<uint64_t *>(base + oscr);
     w.flags = reinterpret_cast<uint64_t *>(base + oflags);
+    w.cent_diag = centroids;
     const uint32_t epoch = ++h->epoch == 0 ? ++h->epoch : h->epoch;  // never 0 (the zeroed granules)
     // granules and the meta words (adjacent in the carve): tags and the hung flag start at 0
     HIP_TRY(hipMemsetAsync(base + ogran, 0, (size_t)(ometa + batch * MW * sizeof(uint32_t) - ogran), s));

@@ -37,6 +37,11 @@ namespace {
 // across waves; the merge is an LDS atomic max).  lidar_fps_ex_f32 also offers 512 (8 waves,
 // 2 buckets per lane: ~25 % longer steps, half the CU footprint beside other kernels)
 constexpr int kThreads = FPS_THREADS;
+// FPS_MAXK: the most active buckets of one owner slot updated per memory round trip (A/B builds: fewer
+// means fewer registers)
+#ifndef FPS_MAXK
+#define FPS_MAXK 4
+#endif
 // one point per lane: 8 bucket slots per lane of a 512-thread workgroup (the register budget) hold
 // 262 144 points; larger frames take buckets of 64 x PPL points (PPL 2 .. 16: up to 4 Mi points)
 constexpr int64_t kMaxBucketPoints = 8 * 512 * 64;
@@ -427,10 +432,10 @@ __global__ __launch_bounds__(T) void fps_bucket_kernel(const float *__restrict__
                 if constexpr (DIAG) dacc[4]++;
                 const int cnt = __popcll(mask);
                 // up to 4 loads per lane in flight: K buckets of PPL points
-                if (PPL == 1 && cnt >= 4)
+                if (PPL == 1 && FPS_MAXK >= 4 && cnt >= 4)
                     update_batch<4, T / 64, PPL>(mask, W, wave, q, lane, qx, qy, qz, bd[q], bi[q], bx[q], bp[q],
                                                  target, wave_dirty);
-                else if (PPL == 1 && cnt == 3)  // one round trip instead of 2 + 1
+                else if (PPL == 1 && FPS_MAXK >= 3 && cnt == 3)  // one round trip instead of 2 + 1
                     update_batch<3, T / 64, PPL>(mask, W, wave, q, lane, qx, qy, qz, bd[q], bi[q], bx[q], bp[q],
                                                  target, wave_dirty);
                 else if (PPL <= 2 && cnt >= 2)

@@ -241,44 +241,12 @@ __device__ __forceinline__ void scatter_tile(const uint32_t (&kv)[PPT], int64_t 
 }
 
 // ---------------------------------------------------------------------------------------- keys
-constexpr int ETAB = 4096;  // edges per axis of the keys launch's LDS tables
+constexpr int ETAB = lidar_vox::kTabEdges;  // edges per axis of the keys launch's LDS tables
 
-// float threshold of a float64 edge: the least float >= e, so that for every float p, p >= e (in
-// float64) <=> p >= ru_float(e) (no float lies between e and it)
-__device__ __forceinline__ float ru_float(double e)
-{
-    const float f = (float)e;
-    if (!((double)f < e)) return f;
-    // the next float up from a finite f (e is finite: |e| < 1e38 on this path)
-    const uint32_t u = __float_as_uint(f);
-    return f == 0.f ? __uint_as_float(1u) : __uint_as_float(f > 0.f ? u + 1u : u - 1u);
-}
-
-// lidar_vox::bin of float p from the axis' threshold table E[0, L) (E[i] = ru_float(e[i])): the same
-// count of edges <= p, found with float compares; lastf = e[L - 1] when it is a float, else NaN
-__device__ __forceinline__ int bin_tab_c(const float *E, int L, float p, float s0, float inv)
-{
-    const float gf = floorf((p - s0) * inv);                           // the bin's guess (any error: fixed below)
-    const int b = (int)fminf(fmaxf(gf, 0.f), (float)(L - 1));          // NaN -> 0
-    const float e0 = E[b > 0 ? b - 1 : 0], e1 = E[b], e2 = E[b + 1 < L ? b + 1 : b];
-    // c = #{i : E[i] <= p}: b + 1 when E[b] <= p < E[b + 1], b when E[b - 1] <= p < E[b]; -1: search
-    return e1 <= p ? (b + 1 == L ? L : (p < e2 ? b + 1 : -1)) : (b == 0 ? 0 : (e0 <= p ? b : -1));
-}
-__device__ __forceinline__ int bin_tab_search(const float *E, int L, float p)  // the guess was off by > 1 bin
-{
-    int lo = 0, hi = L;
-    while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (E[mid] <= p) lo = mid + 1;
-        else hi = mid;
-    }
-    return lo;
-}
-__device__ __forceinline__ uint32_t bin_of_c(int c, float p, float lastf, int L)
-{
-    if (p == lastf) --c;  // the last edge is closed
-    return (c >= 1 && c <= L - 1) ? (uint32_t)(c - 1) : lidar_vox::kOutside;
-}
+using lidar_vox::bin_of_c;
+using lidar_vox::bin_tab_c;
+using lidar_vox::bin_tab_search;
+using lidar_vox::ru_float;
 
 // the tile's extent (min / max of ord() over its points in q) as six {epoch, value} granules gr[t * 6 ..]
 template <typename Q>
@@ -333,6 +301,7 @@ __global__ __launch_bounds__(KT) void vx_extent_kernel(const float *__restrict__
     }
     publish_extent(q, n, t, w.gran + (int64_t)f * ntiles * 6, epoch, red6);
 }
+
 
 template <bool FUSED>
 __global__ __launch_bounds__(KT) void vx_keys_kernel(const float *__restrict__ xyz, int64_t n, double voxel, Ws w,
@@ -427,12 +396,12 @@ __global__ __launch_bounds__(KT) void vx_keys_kernel(const float *__restrict__ x
     float s0[3], inv[3], lastf[3];
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
-        const lidar_vox::Axis &ax = g.ax[a];
-        L[a] = (int)min<int64_t>(ax.nb + 1, (int64_t)ETAB + 1);
-        tab = tab && ax.nb + 1 <= ETAB && ax.delta > 0.0 && fabs(ax.start) < 1e38 && fabs(ax.last) < 1e38;
-        s0[a] = (float)ax.start;
-        inv[a] = (float)ax.inv;
-        lastf[a] = (double)(float)ax.last == ax.last ? (float)ax.last : __builtin_nanf("");
+        const lidar_vox::FAxis fa = lidar_vox::faxis(g.ax[a], ETAB);
+        tab = tab && fa.ok;
+        L[a] = fa.L;
+        s0[a] = fa.s0;
+        inv[a] = fa.inv;
+        lastf[a] = fa.lastf;
     }
     VX_KSTAMP(2);
     if (tab) {

@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
+#include <string.h>
 
 namespace lidar_vox {
 
@@ -112,6 +113,66 @@ __host__ __device__ inline uint32_t key(const Grid &g, float x, float y, float z
     const int64_t bx = bin(g.ax[0], (double)x), by = bin(g.ax[1], (double)y), bz = bin(g.ax[2], (double)z);
     if (bx < 0 || by < 0 || bz < 0) return kOutside;
     return (uint32_t)(((uint64_t)bx * (uint64_t)g.ax[1].nb + (uint64_t)by) * (uint64_t)g.ax[2].nb + (uint64_t)bz);
+}
+
+// ---- the keys launch's float binning (voxel_batch.hip; tests/test_voxel_grid_host.py runs it on the host)
+constexpr int kTabEdges = 4096;  // edges per axis of its LDS threshold tables
+
+// The least float >= e: for every float p, p >= e (in float64) <=> p >= ru_float(e), as no float lies
+// between e and it — so counting the float thresholds <= p counts the float64 edges <= p.
+__host__ __device__ inline float ru_float(double e)
+{
+    const float f = (float)e;
+    if (!((double)f < e)) return f;
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    u = f == 0.0f ? 1u : (f > 0.0f ? u + 1u : u - 1u);  // the next float up (e finite)
+    float r;
+    memcpy(&r, &u, 4);
+    return r;
+}
+
+struct FAxis {     // one axis of the float binning
+    bool ok;       // <= max_edges edges, a span within the float range: the table applies
+    int L;         // edges (the table's length)
+    float s0, inv; // the spacing guess: floor((p - s0) inv) ~ the bin
+    float lastf;   // e[L - 1] when it is a float (the closed edge), else NaN
+};
+__host__ __device__ inline FAxis faxis(const Axis &ax, int max_edges)
+{
+    FAxis f;
+    f.ok = ax.nb + 1 <= max_edges && ax.delta > 0.0 && fabs(ax.start) < 1e38 && fabs(ax.last) < 1e38;
+    f.L = (int)(ax.nb + 1 < max_edges + 1 ? ax.nb + 1 : max_edges + 1);
+    f.s0 = (float)ax.start;
+    f.inv = (float)ax.inv;
+    f.lastf = (double)(float)ax.last == ax.last ? (float)ax.last : NAN;
+    return f;
+}
+
+// c = #{i : E[i] <= p} from the spacing guess and its neighbouring thresholds, branch-free; -1 when the
+// guess is off by more than one bin (bin_tab_search then)
+__host__ __device__ inline int bin_tab_c(const float *E, int L, float p, float s0, float inv)
+{
+    const float gf = floorf((p - s0) * inv);
+    const int b = (int)fminf(fmaxf(gf, 0.f), (float)(L - 1));  // NaN -> 0
+    const float e0 = E[b > 0 ? b - 1 : 0], e1 = E[b], e2 = E[b + 1 < L ? b + 1 : b];
+    return e1 <= p ? (b + 1 == L ? L : (p < e2 ? b + 1 : -1)) : (b == 0 ? 0 : (e0 <= p ? b : -1));
+}
+__host__ __device__ inline int bin_tab_search(const float *E, int L, float p)
+{
+    int lo = 0, hi = L;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (E[mid] <= p) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+// the bin (kOutside outside every bin) from the count c, the last edge closed
+__host__ __device__ inline uint32_t bin_of_c(int c, float p, float lastf, int L)
+{
+    if (p == lastf) --c;
+    return (c >= 1 && c <= L - 1) ? (uint32_t)(c - 1) : kOutside;
 }
 
 }  // namespace lidar_vox

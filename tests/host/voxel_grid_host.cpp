@@ -1,6 +1,9 @@
 // Host harness for csrc/voxel_grid.hpp (tests/test_voxel_grid_host.py): the device kernels' binning,
 // compiled for the host.  stdin: int64 n, double voxel, float32 xyz[n][3]; stdout: int64 ok, nx, ny,
-// nz, then int64 bins[n][3] (-1 outside) and uint32 keys[n].
+// nz, then int64 bins[n][3] (-1 outside) and uint32 keys[n], then the keys launch's float binning
+// (voxel_batch.hip: thresholds ru_float(edge) per axis, the spacing guess, the search on a miss): int64
+// tab (1 when every axis' table applies, else the launch runs key() and so does this) and int64
+// fbins[n][3], computed the same way as the launch.
 #include <stdio.h>
 #include <vector>
 
@@ -33,5 +36,30 @@ int main()
     }
     fwrite(b.data(), 8, b.size(), stdout);
     fwrite(k.data(), 4, k.size(), stdout);
+
+    lidar_vox::FAxis fa[3];
+    std::vector<float> E[3];
+    int64_t tab = 1;
+    for (int a = 0; a < 3; ++a) {
+        fa[a] = lidar_vox::faxis(g.ax[a], lidar_vox::kTabEdges);
+        tab = tab && fa[a].ok;
+    }
+    if (tab)
+        for (int a = 0; a < 3; ++a)
+            for (int i = 0; i < fa[a].L; ++i) E[a].push_back(lidar_vox::ru_float(lidar_vox::edge(g.ax[a], i)));
+    for (int64_t i = 0; i < n; ++i)
+        for (int a = 0; a < 3; ++a) {
+            const float q = p[3 * i + a];
+            if (!tab) {
+                b[3 * i + a] = lidar_vox::bin(g.ax[a], (double)q);
+                continue;
+            }
+            int c = lidar_vox::bin_tab_c(E[a].data(), fa[a].L, q, fa[a].s0, fa[a].inv);
+            if (c < 0) c = lidar_vox::bin_tab_search(E[a].data(), fa[a].L, q);
+            const uint32_t bb = lidar_vox::bin_of_c(c, q, fa[a].lastf, fa[a].L);
+            b[3 * i + a] = bb == lidar_vox::kOutside ? -1 : (int64_t)bb;
+        }
+    fwrite(&tab, 8, 1, stdout);
+    fwrite(b.data(), 8, b.size(), stdout);
     return 0;
 }

@@ -1,4 +1,5 @@
-"""The voxel binning the kernels run (csrc/voxel_grid.hpp: make_grid, bin, key), compiled for the host
+"""The voxel binning the kernels run (csrc/voxel_grid.hpp: make_grid, bin, key, and the keys launch's
+float-threshold tables: ru_float, faxis, bin_tab_c / bin_tab_search / bin_of_c), compiled for the host
 (tests/host/voxel_grid_host.cpp, hipcc, -ffp-contract=off as the library) and compared with
 oracle/tier_n.voxel_bins — numpy's searchsorted on np.arange edges, itself pinned to the reference's
 calculate_grid_density (test_oracle.py::test_voxel_bins_pinned_to_reference) — on the golden frames and
@@ -38,14 +39,18 @@ def run(exe, x, v):
         return None, None, None
     n = len(x)
     bins = np.frombuffer(out[32:32 + 24 * n], np.int64).reshape(n, 3)
-    keys = np.frombuffer(out[32 + 24 * n:], np.uint32)
+    o = 32 + 24 * n
+    keys = np.frombuffer(out[o:o + 4 * n], np.uint32)
+    run.tab = int(np.frombuffer(out[o + 4 * n:o + 4 * n + 8], np.int64)[0])
+    run.fbins = np.frombuffer(out[o + 4 * n + 8:], np.int64).reshape(n, 3)
     return bins, tuple(int(d) for d in head[1:]), keys
 
 
-def near_edges(seed, v, lo, n=3000):
+def near_edges(seed, v, lo, n=3000, bins=40, yz_bins=None):
     """Points at, one ulp below and one ulp above the float32 values nearest to interior edges."""
     rng = np.random.default_rng(seed)
-    x = (rng.random((n, 3)) * 40 * v + lo).astype(np.float32)
+    span = np.array([bins, yz_bins or bins, yz_bins or bins]) * v
+    x = (rng.random((n, 3)) * span + lo).astype(np.float32)
     e = tier_n.voxel_edges(float(x[:, 0].min()), float(x[:, 0].max()), v)
     pick = e[rng.integers(2, len(e) - 2, n // 3)].astype(np.float32)
     x[: n // 3, 0] = pick
@@ -61,6 +66,9 @@ ADVERSARIAL = {
     "v_0.3_near_edges": (lambda: near_edges(3, 0.3, -5.0), 0.3),
     "v_0.07_near_edges": (lambda: near_edges(4, 0.07, 123.0), 0.07),
     "v_1e-3_near_edges": (lambda: near_edges(5, 1e-3, 0.5), 1e-3),
+    # about 4000 bins on x: the widest tables; 5000: past them (float64 key())
+    "tab_4000_bins": (lambda: near_edges(7, 0.05, -77.7, n=6000, bins=4000, yz_bins=30), 0.05),
+    "tab_5000_bins": (lambda: near_edges(8, 0.05, 31.3, n=6000, bins=5000, yz_bins=30), 0.05),
     "negative_far": (lambda: (np.random.default_rng(6).random((3000, 3)) * -50 - 2.5e4).astype(np.float32), 0.37),
 }
 
@@ -79,6 +87,9 @@ def outside_frame(n=999):
 ADVERSARIAL["outside_2p30"] = (outside_frame, 3.3 * 2.0 ** -22)
 
 
+K_TAB_EDGES = 4096  # csrc/voxel_grid.hpp kTabEdges: a finer axis runs lidar_vox::key in float64
+
+
 @pytest.mark.parametrize("name", sorted(VOXEL_CASES) + sorted(ADVERSARIAL))
 def test_kernel_binning_equals_oracle(harness, name):
     make, v = (VOXEL_CASES.get(name) or ADVERSARIAL[name])
@@ -92,10 +103,17 @@ def test_kernel_binning_equals_oracle(harness, name):
     assert dims == wdims
     bad = np.flatnonzero((bins != want).any(axis=1))
     assert bad.size == 0, f"{bad.size} points binned differently, first {x[bad[:3]]}: {bins[bad[:3]]} vs {want[bad[:3]]}"
+    # the keys launch's float tables (csrc/voxel_grid.hpp kTabEdges edges per axis at most): the same bins
+    assert run.tab == int(all(d + 1 <= K_TAB_EDGES for d in dims))
+    bad = np.flatnonzero((run.fbins != want).any(axis=1))
+    assert bad.size == 0, (f"float tables: {bad.size} points binned differently, first {x[bad[:3]]}: "
+                           f"{run.fbins[bad[:3]]} vs {want[bad[:3]]}")
     inside = (want >= 0).all(axis=1)
     wkey = (want[:, 0] * wdims[1] + want[:, 1]) * wdims[2] + want[:, 2]
     assert np.array_equal(keys[inside], wkey[inside].astype(np.uint32))
     assert (keys[~inside] == 0xffffffff).all()
+    if name.startswith("tab_"):
+        assert run.tab == int(name == "tab_4000_bins")
     if name == "outside_2p30":
         assert 0 < (~inside).sum() < len(x)
 

@@ -274,8 +274,11 @@ int lidar_voxel_downsample_f32(lidar_handle *h, const float *xyz, int64_t n, dou
 /* Voxel downsampling of `batch` frames of n points over the whole chip (csrc/voxel_batch.hip):
  * xyz (batch, n, 3) fp32; voxel_id (batch, n) int32; centroids (batch, n, 3) and counts (batch, n),
  * the first nvox[f] rows of frame f valid; nvox (batch,) int32 on the device (-1: the frame's extent
- * is not finite or its grid has 2^32 keys or more; -2: a bounded in-launch wait timed out, a bug).  No host synchronisation; per frame equal to
- * lidar_voxel_downsample_f32.  Workspace: lidar_voxel_batch_workspace_bytes(batch, n). */
+ * is not finite or its grid has 2^32 keys or more; -2: a bounded in-launch wait timed out, a bug).  No host
+ * synchronisation; per frame equal to lidar_voxel_downsample_f32.  Workspace:
+ * lidar_voxel_batch_workspace_bytes(batch, n), plus the handle's own voxel tag block (the in-launch
+ * hand-offs' epoch-tagged granules, 8 KiB per 8 192-point tile; grown and zeroed on demand, written by
+ * voxel calls only).  Calls on one handle must not run concurrently (as for the workspace). */
 uint64_t lidar_voxel_batch_workspace_bytes(int64_t batch, int64_t n);
 int lidar_voxel_downsample_batch_f32(lidar_handle *h, const float *xyz, int64_t batch, int64_t n, double voxel,
                                      int32_t *voxel_id, float *centroids, int32_t *counts, int32_t *nvox,

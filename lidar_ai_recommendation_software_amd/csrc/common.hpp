@@ -33,7 +33,11 @@ struct lidar_handle {
     uint64_t retired_bytes = 0;
     void *host_pinned = nullptr;  // small pinned host buffer for scalar read-backs
     lidar::Prof *prof = nullptr;  // non-null while lidar_profile(h, 1) is on
-    uint32_t epoch = 0;           // per-call tag of in-launch hand-offs (voxel_batch.hip's extent granules)
+    uint32_t epoch = 0;           // per-call tag of in-launch hand-offs (voxel_batch.hip's granules)
+    // voxel_batch.hip's granules and meta words: their own block, written only by voxel calls (tags of
+    // earlier calls, never the current one; zeroed when allocated and when the epoch wraps)
+    void *vx_tags = nullptr;
+    uint64_t vx_tags_bytes = 0;
 };
 
 namespace lidar {

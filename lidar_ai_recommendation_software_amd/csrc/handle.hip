@@ -95,6 +95,7 @@ LIDAR_EXPORT int lidar_destroy(lidar_handle *h)
             delete h->prof;
         }
         if (h->ws) note(hipFree(h->ws), "lidar_destroy: hipFree");
+        if (h->vx_tags) note(hipFree(h->vx_tags), "lidar_destroy: hipFree (voxel tags)");
         for (void *r : h->retired) note(hipFree(r), "lidar_destroy: hipFree (retired workspace)");
         if (h->host_pinned) note(hipHostFree(h->host_pinned), "lidar_destroy: hipHostFree");
     }

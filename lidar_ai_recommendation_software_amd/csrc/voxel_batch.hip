@@ -55,7 +55,7 @@ constexpr int CAP = 2048;          // pairs a bucket sorts in LDS
 constexpr int KMAX = 4096;         // local key range of the LDS counting sort
 constexpr int SEGMAX = 32;         // longest equal-key run the counting sort orders by index itself
 constexpr int BUCKET = 1536;       // target points per bucket
-constexpr int MW = 8;              // meta words per frame: [0] grid ok, [1] outside key, [2] hs, [3] hung
+constexpr int MW = 8;              // meta words per frame: [0] grid ok, [1] outside key, [2] hs, [3] hung tag
 constexpr uint64_t kPad = ~0ull;   // bitonic padding: sorts last
 static_assert(NBIN % KT == 0 && NBIN % UT == 0, "bins per thread");
 
@@ -71,7 +71,7 @@ __device__ __forceinline__ float unord(uint32_t u)
 
 struct Ws {  // per-batch workspace, every array frame-major
     unsigned long long *gran;  // [F][T][6] the tiles' extents: epoch << 32 | monotone bits (self-tagged granules)
-    uint32_t *meta;    // [F][MW]
+    uint32_t *meta;    // [F][MW] ([3]: the call's epoch when a hand-off timed out)
     uint32_t *key;     // [F][n]
     unsigned long long *hgran;  // [F][T][NBIN / 2] tile histograms: epoch << 32 | count(2g + 1) << 16 | count(2g)
     uint32_t *bstart;  // [F][NB + 1] the buckets' first pairs (bstart[NB] = n)
@@ -191,7 +191,7 @@ __device__ __forceinline__ void scatter_tile(const uint32_t (&kv)[PPT], int64_t 
                 pre[j] += u0 + uu < t ? c : 0u;
             }
     }
-    if (hung) w.meta[f * MW + 3] = 1u;
+    if (hung) w.meta[f * MW + 3] = epoch;
     VX_KSTAMP(6);
 #pragma unroll
     for (int j = 0; j < BPT; ++j) sum += tot[j];
@@ -372,7 +372,7 @@ __global__ __launch_bounds__(KT) void vx_keys_kernel(const float *__restrict__ x
 #pragma unroll
             for (int kk = 0; kk < 6; ++kk)  // hung: NaN extent, the grid fails
                 if (lane == kk) ext[kk] = ok ? m[kk] : ord(__builtin_nanf(""));
-            if (!ok && lane == 0) w.meta[f * MW + 3] = 1u;  // reported as nvox -2
+            if (!ok && lane == 0) w.meta[f * MW + 3] = epoch;  // reported as nvox -2
         }
     }
     __syncthreads();
@@ -386,7 +386,7 @@ __global__ __launch_bounds__(KT) void vx_keys_kernel(const float *__restrict__ x
     if (t == 0 && tid == 0) {
         m[0] = g.ok ? 1u : 0u;
         m[1] = okey;
-        m[2] = (uint32_t)hs;  // (m[3], the hung flag, starts at 0: the host's memset)
+        m[2] = (uint32_t)hs;  // (m[3]: the hung tag, this call's epoch only when set by this call)
     }
     if (!g.ok) return;  // whole workgroup (uniform)
     // the float thresholds of every axis' edges in LDS when each axis has <= ETAB edges and the grid's
@@ -581,19 +581,31 @@ __device__ uint64_t *bucket_radix(uint64_t *a, uint64_t *b, int64_t m, uint32_t 
 // A look-back word is its own payload (status << 32 | count, one 8-byte sc1 store, read by sc1 loads
 // that bypass the L1): relaxed agent-scope atomics, no fences (an acquire would invalidate the CU's
 // L1 per poll and a release write back the XCD's L2 per store: MI355X_MICROARCH.md, ~1.7 us each).
-__device__ uint64_t look_back(unsigned long long *fl, int64_t b, uint32_t nv, bool *hung, uint32_t *nspins = nullptr)
+// (published: the count went out earlier, by look_back_publish.)
+__device__ __forceinline__ void look_back_publish(unsigned long long *fl, int64_t b, uint32_t nv)
+{
+    __hip_atomic_store(&fl[b], ((b == 0 ? 2ull : 1ull) << 32) | nv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// (first: the words of the first window, loaded earlier by look_back_first, or null.)
+__device__ __forceinline__ unsigned long long look_back_first(const unsigned long long *fl, int64_t b)
+{
+    const int64_t q = b - 1 - (threadIdx.x & 63);
+    return q >= 0 ? __hip_atomic_load(&fl[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : (2ull << 32);
+}
+__device__ uint64_t look_back(unsigned long long *fl, int64_t b, uint32_t nv, bool *hung, uint32_t *nspins = nullptr,
+                              bool published = false, const unsigned long long *first = nullptr)
 {
     const int lane = threadIdx.x & 63;
-    if (lane == 0)
-        __hip_atomic_store(&fl[b], ((b == 0 ? 2ull : 1ull) << 32) | nv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0 && !published) look_back_publish(fl, b, nv);
     uint64_t pre = 0;
     *hung = false;
     int64_t top = b - 1;
     uint32_t spins = 0;
     while (top >= 0) {
         const int64_t q = top - lane;
-        const unsigned long long v =
-            q >= 0 ? __hip_atomic_load(&fl[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : (2ull << 32);
+        const unsigned long long v = first && top == b - 1 && spins == 0 ? *first
+                                     : q >= 0 ? __hip_atomic_load(&fl[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                              : (2ull << 32);
         const uint32_t st = (uint32_t)(v >> 32);
         const uint64_t incl = __ballot(st == 2);
         const int k = incl ? __ffsll((unsigned long long)incl) - 1 : 63;
@@ -619,28 +631,30 @@ __device__ uint64_t look_back(unsigned long long *fl, int64_t b, uint32_t nv, bo
     return pre;
 }
 
-// 52 KiB: three 512-thread workgroups per CU
+// 36 KiB (three 512-thread workgroups per CU at <= 84 VGPRs)
 struct BucketLds {
-    uint64_t a[CAP];           // the sorted pairs (the bitonic path: its array)
     uint32_t s[CAP];           // the counting sort's unordered runs: point indices (a run is one key)
     union {
-        uint32_t cnt[KMAX];    // counting-sort counters / starts (the radix path's digit tables)
+        uint32_t cnt[KMAX];    // counting-sort counters, then per key its first sorted position | its voxel's
+                               // rank in the bucket << 16 (the radix path: its digit tables)
         float xyz[CAP * 3];    // the sorted points' xyz, for the centroid sums (written once cnt is dead)
+        uint64_t a[CAP];       // the bitonic path's pairs
     };
-    uint16_t vstart[CAP + 1];  // the staged emit: voxel v's first sorted position, then the voxels' end
+    uint16_t vstart[CAP + 1];  // voxel v's first sorted position, then the voxels' end
 };
+static_assert(CAP < 65536, "packed first position | voxel rank");
 
 __global__ __launch_bounds__(UT, 6) void vx_bucket_kernel(const float *__restrict__ xyz, int64_t n, Ws w,
                                                        int32_t *__restrict__ vid, float *__restrict__ cent,
                                                        int32_t *__restrict__ counts, int32_t *__restrict__ nvox,
-                                                       int64_t batch)
+                                                       int64_t batch, uint32_t epoch)
 {
     const int64_t nb = n_buckets(n);
     int64_t f, b;
     if (!frame_part(batch, nb, f, b)) return;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 #ifdef VX_DIAG_PHASES
-    uint64_t ts[8], rt[8];
+    uint64_t ts[8] = {}, rt[8] = {};
     auto stamp = [&](int k) {
         uint64_t t, r;
         asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
@@ -653,9 +667,12 @@ __global__ __launch_bounds__(UT, 6) void vx_bucket_kernel(const float *__restric
 #define VX_STAMP(k)
 #endif
     VX_STAMP(0);
+    // the bucket's pairs [bstart[b], bstart[b + 1]) (the scatter launch's bucket table), loaded beside the
+    // frame's meta words
+    const uint32_t bs = tid < 2 ? w.bstart[(int64_t)f * (nb + 1) + b + tid] : 0u;
     const uint32_t *m = w.meta + (int64_t)f * MW;
-    if (!m[0] || m[3]) {
-        if (b == 0 && tid == 0) nvox[f] = m[3] ? -2 : -1;
+    if (!m[0] || m[3] == epoch) {
+        if (b == 0 && tid == 0) nvox[f] = m[3] == epoch ? -2 : -1;
         return;  // every bucket of the frame returns: nothing waits on this frame's look-back words
     }
     const uint32_t okey = m[1];
@@ -666,9 +683,9 @@ __global__ __launch_bounds__(UT, 6) void vx_bucket_kernel(const float *__restric
     __shared__ unsigned long long prefix, vary;
 #ifdef VX_DIAG_PHASES
     __shared__ uint32_t spins_dbg;
+    if (tid == 0) spins_dbg = 0;
 #endif
-    // the bucket's pairs [bstart[b], bstart[b + 1]) (the scatter launch's bucket table)
-    if (tid < 2) rng[tid] = min(w.bstart[(int64_t)f * (nb + 1) + b + tid], (uint32_t)n);  // (defensive: <= n)
+    if (tid < 2) rng[tid] = min(bs, (uint32_t)n);  // (defensive: <= n)
     if (tid == 2) rng[2] = 0xffffffffu;  // [2], [3]: key min / max
     if (tid == 3) rng[3] = 0u;
     if (tid == 0) flag = 0;
@@ -677,8 +694,11 @@ __global__ __launch_bounds__(UT, 6) void vx_bucket_kernel(const float *__restric
     const int64_t p0 = rng[0], size = max<int64_t>(0, (int64_t)rng[1] - rng[0]);
     const uint64_t *gp = w.pairs + (int64_t)f * n + p0;
     const float *p = xyz + (int64_t)f * n * 3;
-    const uint64_t *seq;   // the bucket sorted by (key, index): LDS or global
-    bool staged = false;   // xyz of the sorted pairs in L.xyz
+    unsigned long long *fl = reinterpret_cast<unsigned long long *>(w.flags + (int64_t)f * nb);
+    int32_t *vf = vid + (int64_t)f * n;
+    float *cf = cent + (int64_t)f * n * 3;
+    int32_t *nf = counts + (int64_t)f * n;
+    const uint64_t *seq = nullptr;  // the slow paths: the bucket sorted by (key, index), LDS or global
     if (size <= CAP) {
         // the pairs and their points' xyz (the gathers fly while the keys sort), and the range of the
         // keys they hold (not of their coarse bins: the first and last buckets' bins reach over the
@@ -715,75 +735,141 @@ __global__ __launch_bounds__(UT, 6) void vx_bucket_kernel(const float *__restric
         if (counting)
             for (int64_t c = tid; c < (int64_t)krange; c += UT) L.cnt[c] = 0;
         __syncthreads();
-        uint32_t rk[CAP / UT], lk[CAP / UT];
+        uint32_t lr[CAP / UT];  // local key | rank inside the key << 16
         if (counting) {
-            // counting sort by local key: a rank inside the key from an LDS atomic, starts by a scan
+            // counting sort by local key: a rank inside the key from an LDS atomic
 #pragma unroll
             for (int j = 0; j < CAP / UT; ++j) {
                 const int64_t i = tid + j * UT;
                 if (i < size) {
-                    lk[j] = (uint32_t)((v[j] >> 32) - k0);
-                    rk[j] = atomicAdd(&L.cnt[lk[j]], 1u);
-                    if (rk[j] == SEGMAX) flag = 1;  // a long equal-key run: the bitonic path instead
+                    const uint32_t lk = (uint32_t)((v[j] >> 32) - k0), rk = atomicAdd(&L.cnt[lk], 1u);
+                    lr[j] = lk | rk << 16;
+                    if (rk == SEGMAX) flag = 1;  // a long equal-key run: the bitonic path instead
                 }
             }
             __syncthreads();
-            if (!flag) {
-                // exclusive scan of the counters, KMAX / UT consecutive per thread
-                constexpr int PT = KMAX / UT;
-                uint32_t cv[PT], sum = 0;
-#pragma unroll
-                for (int j = 0; j < PT; ++j) {
-                    const int64_t c = PT * tid + j;
-                    cv[j] = c < (int64_t)krange ? L.cnt[c] : 0u;
-                    sum += cv[j];
-                }
-                uint32_t all;
-                uint32_t ex = block_excl_scan<UT>(sum, red, &all);
-#pragma unroll
-                for (int j = 0; j < PT; ++j) {
-                    const int64_t c = PT * tid + j;
-                    if (c < (int64_t)krange) L.cnt[c] = ex;
-                    ex += cv[j];
-                }
-                __syncthreads();
-                // each key's run, unordered
-                uint32_t st[CAP / UT], en[CAP / UT];
-#pragma unroll
-                for (int j = 0; j < CAP / UT; ++j) {
-                    const int64_t i = tid + j * UT;
-                    if (i < size) {
-                        st[j] = L.cnt[lk[j]];
-                        en[j] = lk[j] + 1 < krange ? L.cnt[lk[j] + 1] : (uint32_t)size;
-                        L.s[st[j] + rk[j]] = (uint32_t)v[j];
-                    }
-                }
-                __syncthreads();
-                // index order inside a run (< SEGMAX long): every element counts the smaller indices of
-                // its run, in parallel; the sorted pair and its xyz land in L.a / L.xyz
-#pragma unroll
-                for (int j = 0; j < CAP / UT; ++j) {
-                    const int64_t i = tid + j * UT;
-                    if (i < size) {
-                        uint32_t r = 0;
-                        for (uint32_t x = st[j]; x < en[j]; ++x) r += L.s[x] < (uint32_t)v[j] ? 1u : 0u;
-                        const uint32_t o = st[j] + r;
-                        L.a[o] = v[j];
-#pragma unroll
-                        for (int c = 0; c < 3; ++c) L.xyz[3 * o + c] = g[j][c];
-                    }
-                }
-                __syncthreads();
-                seq = L.a;
-            }
         }
-        if (!counting || flag) {  // bitonic sort of the loaded pairs, then their xyz in sorted order
-            int64_t P = 1;
-            while (P < size) P <<= 1;
+        VX_STAMP(2);
+        if (counting && !flag) {
+            // one exclusive scan of (count | occupied << 16) over the local keys gives every key its first
+            // sorted position and its voxel's rank in the bucket (the outside key occupies no voxel), and
+            // the bucket's voxel count, published at once for the later buckets' look-back
+            constexpr int PT = KMAX / UT;
+            uint32_t cv[PT], sum = 0;
+#pragma unroll
+            for (int j = 0; j < PT; ++j) {
+                const int64_t c = PT * tid + j;
+                const uint32_t x = c < (int64_t)krange ? L.cnt[c] : 0u;
+                cv[j] = x + (x != 0u && (uint32_t)(k0 + c) != okey ? 0x10000u : 0u);
+                sum += cv[j];
+            }
+            uint32_t all;
+            uint32_t ex = block_excl_scan<UT>(sum, red, &all);
+#pragma unroll
+            for (int j = 0; j < PT; ++j) {
+                const int64_t c = PT * tid + j;
+                if (c < (int64_t)krange) L.cnt[c] = ex;
+                ex += cv[j];
+            }
+            const uint32_t nvl = all >> 16;
+            if (tid == 0) look_back_publish(fl, b, nvl);
+            __syncthreads();
+            VX_STAMP(3);
+            // each key's run, unordered; the voxels' first positions (the run's rank-0 element writes it;
+            // the outside key's run, when present, is the last and ends the last voxel)
+            // (sv: the run's first position | its length << 11 | the voxel's rank << 17 — every field
+            // below 2^11 with CAP = 2048, lengths <= SEGMAX)
+            static_assert(CAP <= 2048 && SEGMAX < 64, "packed run fields");
+            uint32_t sv[CAP / UT];
+#pragma unroll
+            for (int j = 0; j < CAP / UT; ++j) {
+                const int64_t i = tid + j * UT;
+                if (i < size) {
+                    const uint32_t lk = lr[j] & 0xffffu, rk = lr[j] >> 16, e = L.cnt[lk];
+                    const uint32_t st = e & 0xffffu, vp = e >> 16;
+                    const uint32_t en = lk + 1 < krange ? L.cnt[lk + 1] & 0xffffu : (uint32_t)size;
+                    sv[j] = st | (en - st) << 11 | vp << 17;
+                    L.s[st + rk] = (uint32_t)v[j];
+                    if (rk == 0) L.vstart[vp] = (uint16_t)st;  // the outside key's run: vp = nvl
+                }
+            }
+            if (tid == 0 && rng[3] != okey) L.vstart[nvl] = (uint16_t)size;
+            __syncthreads();
+            // wave 0: the look-back's first window in flight during the placement below (the earlier
+            // buckets publish their counts at the same point of their lives)
+            unsigned long long lb0 = 0;
+            if (wave == 0) lb0 = look_back_first(fl, b);
+            // index order inside a run (< SEGMAX long): every element counts the smaller indices of its
+            // run; its xyz lands at its sorted position
+#pragma unroll
+            for (int j = 0; j < CAP / UT; ++j) {
+                const int64_t i = tid + j * UT;
+                if (i < size) {
+                    const uint32_t st = sv[j] & 0x7ffu, en = st + ((sv[j] >> 11) & 0x3fu);
+                    uint32_t r = 0;
+                    for (uint32_t x = st; x < en; ++x) r += L.s[x] < (uint32_t)v[j] ? 1u : 0u;
+                    const uint32_t o = st + r;
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) L.xyz[3 * o + c] = g[j][c];
+                }
+            }
+            VX_STAMP(4);
+            if (wave == 0) {  // the earlier buckets have published their counts by now (one pass, no wait)
+                bool hung;
+                uint32_t nsp = 0;
+                const uint64_t pre = look_back(fl, b, nvl, &hung, &nsp, true, &lb0);
+#ifdef VX_DIAG_PHASES
+                if (lane == 0) spins_dbg = nsp;
+#endif
+                if (lane == 0) {
+                    prefix = pre;
+                    if (hung) nvox[f] = -2;
+                    else if (b == nb - 1) nvox[f] = (int32_t)(pre + nvl);
+                }
+            }
+            __syncthreads();
+            VX_STAMP(5);
+            const uint32_t O = (uint32_t)prefix;
+            // the points' voxel ids (from registers), then one thread per voxel: its sequential fp32 sums
+            // over its points in index order (known run length: the LDS loads pipeline; consecutive
+            // threads write consecutive centroids)
 #pragma unroll
             for (int j = 0; j < CAP / UT; ++j)
-                if (tid + j * UT < size) L.a[tid + j * UT] = v[j];
-            for (int64_t i = size + tid; i < P; i += UT) L.a[i] = kPad;
+                if (tid + j * UT < size)
+                    vf[(uint32_t)v[j]] = (sv[j] >> 17) == nvl ? -1 : (int32_t)(O + (sv[j] >> 17));  // nvl: outside
+            VX_STAMP(6);
+            for (uint32_t vv = tid; vv < nvl; vv += UT) {
+                const int i0 = L.vstart[vv], i1 = L.vstart[vv + 1];
+                float sx = 0.f, sy = 0.f, sz = 0.f;
+                int e = i0;
+                for (; e + 4 <= i1; e += 4) {
+                    float q[12];
+#pragma unroll
+                    for (int k = 0; k < 12; ++k) q[k] = L.xyz[3 * e + k];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        sx = __fadd_rn(sx, q[3 * k]);
+                        sy = __fadd_rn(sy, q[3 * k + 1]);
+                        sz = __fadd_rn(sz, q[3 * k + 2]);
+                    }
+                }
+                for (; e < i1; ++e) {
+                    sx = __fadd_rn(sx, L.xyz[3 * e]);
+                    sy = __fadd_rn(sy, L.xyz[3 * e + 1]);
+                    sz = __fadd_rn(sz, L.xyz[3 * e + 2]);
+                }
+                const int64_t o = (int64_t)O + vv;
+                const float c = (float)(i1 - i0);
+                cf[3 * o] = __fdiv_rn(sx, c);
+                cf[3 * o + 1] = __fdiv_rn(sy, c);
+                cf[3 * o + 2] = __fdiv_rn(sz, c);
+                nf[o] = i1 - i0;
+            }
+        } else {
+            // bitonic sort of the loaded pairs in LDS (a key range past the counting sort, or a long run)
+            int64_t P = 1;
+            while (P < size) P <<= 1;
+            for (int64_t i = tid; i < P; i += UT) L.a[i] = i < size ? gp[i] : kPad;  // (rare: reloaded)
             __syncthreads();
             for (int64_t k2 = 2; k2 <= P; k2 <<= 1)
                 for (int64_t j = k2 >> 1; j > 0; j >>= 1) {
@@ -800,167 +886,82 @@ __global__ __launch_bounds__(UT, 6) void vx_bucket_kernel(const float *__restric
                     __syncthreads();
                 }
             seq = L.a;
-            float h[CAP / UT][3];
-#pragma unroll
-            for (int j = 0; j < CAP / UT; ++j) {
-                const int64_t i = tid + j * UT;
-                const int64_t idx = i < size ? (int64_t)(uint32_t)seq[i] : 0;
-#pragma unroll
-                for (int c = 0; c < 3; ++c) h[j][c] = p[3 * idx + c];
-            }
-#pragma unroll
-            for (int j = 0; j < CAP / UT; ++j) {
-                const int64_t i = tid + j * UT;
-                if (i < size)
-#pragma unroll
-                    for (int c = 0; c < 3; ++c) L.xyz[3 * i + c] = h[j][c];
-            }
         }
-        __syncthreads();
-        VX_STAMP(2);
-        staged = true;
     } else {
         seq = bucket_radix(const_cast<uint64_t *>(gp), w.scratch + (int64_t)f * n + p0, size, L.cnt,
                            reinterpret_cast<uint32_t(*)[256]>(L.cnt + 256), red, &vary);
     }
-    __syncthreads();
-    VX_STAMP(3);
-    // voxel starts: this thread's elements are CH consecutive ones per chunk of CH UT
-    constexpr int CH = 4;
-    auto key_at = [&](int64_t i) { return (uint32_t)(seq[i] >> 32); };
-    auto start_at = [&](int64_t i) {
-        const uint32_t kk = key_at(i);
-        return kk != okey && (i == 0 || kk != key_at(i - 1));
-    };
-    uint32_t nvl = 0;
-    for (int64_t c0 = 0; c0 < size; c0 += CH * UT) {
-        uint32_t s = 0;
+    if (seq) {
+        // the slow paths: voxel starts over the sorted sequence, the look-back, then ids and sums
+        __syncthreads();
+        constexpr int CH = 4;  // this thread's elements are CH consecutive ones per chunk of CH UT
+        auto key_at = [&](int64_t i) { return (uint32_t)(seq[i] >> 32); };
+        auto start_at = [&](int64_t i) {
+            const uint32_t kk = key_at(i);
+            return kk != okey && (i == 0 || kk != key_at(i - 1));
+        };
+        uint32_t nvl = 0;
+        for (int64_t c0 = 0; c0 < size; c0 += CH * UT) {
+            uint32_t s = 0;
 #pragma unroll
-        for (int j = 0; j < CH; ++j) {
-            const int64_t i = c0 + CH * tid + j;
-            if (i < size) s += start_at(i) ? 1u : 0u;
+            for (int j = 0; j < CH; ++j) {
+                const int64_t i = c0 + CH * tid + j;
+                if (i < size) s += start_at(i) ? 1u : 0u;
+            }
+            uint32_t all;
+            block_excl_scan<UT>(s, red, &all);
+            nvl += all;
         }
-        uint32_t all;
-        block_excl_scan<UT>(s, red, &all);
-        nvl += all;
-    }
-    VX_STAMP(4);
-    if (wave == 0) {
-        bool hung;
-        uint32_t nsp = 0;
-        const uint64_t pre = look_back(reinterpret_cast<unsigned long long *>(w.flags + (int64_t)f * nb), b, nvl,
-                                       &hung, &nsp);
-#ifdef VX_DIAG_PHASES
-        if (lane == 0) spins_dbg = nsp;
-#endif
-        if (lane == 0) {
-            prefix = pre;
-            if (hung) nvox[f] = -2;
-            else if (b == nb - 1) nvox[f] = (int32_t)(pre + nvl);
-        }
-    }
-    __syncthreads();
-    VX_STAMP(5);
-    const uint32_t O = (uint32_t)prefix;
-    int32_t *vf = vid + (int64_t)f * n;
-    float *cf = cent + (int64_t)f * n * 3;
-    int32_t *nf = counts + (int64_t)f * n;
-    uint32_t carry = 0;
-    if (staged) {
-        // one chunk (size <= CAP = CH UT): ids per element, the voxels' first positions into LDS, then
-        // one thread per voxel (known run length: the sequential sums' loads pipeline; consecutive
-        // threads write consecutive centroids)
-        static_assert(CAP <= CH * UT, "the staged emit is one chunk");
-        bool st[CH];
-        uint32_t s = 0;
-#pragma unroll
-        for (int j = 0; j < CH; ++j) {
-            const int64_t i = CH * tid + j;
-            st[j] = i < size && start_at(i);
-            s += st[j] ? 1u : 0u;
-        }
-        uint32_t all;
-        uint32_t r = block_excl_scan<UT>(s, red, &all);  // the bucket's voxels before this thread's elements
-#pragma unroll
-        for (int j = 0; j < CH; ++j) {
-            const int64_t i = CH * tid + j;
-            if (i < size) {
-                const uint64_t v = seq[i];
-                const uint32_t kk = (uint32_t)(v >> 32);
-                if (st[j]) L.vstart[r] = (uint16_t)i;
-                r += st[j] ? 1u : 0u;
-                vf[(uint32_t)v] = kk == okey ? -1 : (int32_t)(O + r - 1);
-                // the end of the last voxel: the first outside point, or the bucket's end
-                if (kk != okey && (i + 1 == size || key_at(i + 1) == okey)) L.vstart[all] = (uint16_t)(i + 1);
+        if (wave == 0) {
+            bool hung;
+            const uint64_t pre = look_back(fl, b, nvl, &hung);
+            if (lane == 0) {
+                prefix = pre;
+                if (hung) nvox[f] = -2;
+                else if (b == nb - 1) nvox[f] = (int32_t)(pre + nvl);
             }
         }
         __syncthreads();
-        VX_STAMP(6);
-        for (uint32_t v = tid; v < all; v += UT) {
-            const int i0 = L.vstart[v], i1 = L.vstart[v + 1];
-            float sx = 0.f, sy = 0.f, sz = 0.f;
-            int e = i0;
-            for (; e + 4 <= i1; e += 4) {
-                float q[12];
+        const uint32_t O = (uint32_t)prefix;
+        uint32_t carry = 0;
+        for (int64_t c0 = 0; c0 < size; c0 += CH * UT) {
+            bool st[CH];
+            uint32_t s = 0;
 #pragma unroll
-                for (int k = 0; k < 12; ++k) q[k] = L.xyz[3 * e + k];
+            for (int j = 0; j < CH; ++j) {
+                const int64_t i = c0 + CH * tid + j;
+                st[j] = i < size && start_at(i);
+                s += st[j] ? 1u : 0u;
+            }
+            uint32_t all;
+            uint32_t r = O + carry + block_excl_scan<UT>(s, red, &all);  // voxels before this thread's elements
 #pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    sx = __fadd_rn(sx, q[3 * k]);
-                    sy = __fadd_rn(sy, q[3 * k + 1]);
-                    sz = __fadd_rn(sz, q[3 * k + 2]);
+            for (int j = 0; j < CH; ++j) {
+                const int64_t i = c0 + CH * tid + j;
+                if (i >= size) break;
+                const uint64_t v = seq[i];
+                const uint32_t kk = (uint32_t)(v >> 32);
+                r += st[j] ? 1u : 0u;
+                vf[(uint32_t)v] = kk == okey ? -1 : (int32_t)(r - 1);
+                if (st[j]) {  // this voxel's points in index order: the sequential fp32 sums
+                    float sx = 0.f, sy = 0.f, sz = 0.f;
+                    int64_t e = i;
+                    for (; e < size && key_at(e) == kk; ++e) {
+                        const int64_t idx = (uint32_t)seq[e];
+                        sx = __fadd_rn(sx, p[3 * idx]);
+                        sy = __fadd_rn(sy, p[3 * idx + 1]);
+                        sz = __fadd_rn(sz, p[3 * idx + 2]);
+                    }
+                    const int64_t o = r - 1;
+                    const float c = (float)(e - i);
+                    cf[3 * o] = __fdiv_rn(sx, c);
+                    cf[3 * o + 1] = __fdiv_rn(sy, c);
+                    cf[3 * o + 2] = __fdiv_rn(sz, c);
+                    nf[o] = (int32_t)(e - i);
                 }
             }
-            for (; e < i1; ++e) {
-                sx = __fadd_rn(sx, L.xyz[3 * e]);
-                sy = __fadd_rn(sy, L.xyz[3 * e + 1]);
-                sz = __fadd_rn(sz, L.xyz[3 * e + 2]);
-            }
-            const int64_t o = (int64_t)O + v;
-            const float c = (float)(i1 - i0);
-            cf[3 * o] = __fdiv_rn(sx, c);
-            cf[3 * o + 1] = __fdiv_rn(sy, c);
-            cf[3 * o + 2] = __fdiv_rn(sz, c);
-            nf[o] = i1 - i0;
+            carry += all;
         }
-    }
-    for (int64_t c0 = 0; !staged && c0 < size; c0 += CH * UT) {
-        bool st[CH];
-        uint32_t s = 0;
-#pragma unroll
-        for (int j = 0; j < CH; ++j) {
-            const int64_t i = c0 + CH * tid + j;
-            st[j] = i < size && start_at(i);
-            s += st[j] ? 1u : 0u;
-        }
-        uint32_t all;
-        uint32_t r = O + carry + block_excl_scan<UT>(s, red, &all);  // voxels before this thread's elements
-#pragma unroll
-        for (int j = 0; j < CH; ++j) {
-            const int64_t i = c0 + CH * tid + j;
-            if (i >= size) break;
-            const uint64_t v = seq[i];
-            const uint32_t kk = (uint32_t)(v >> 32);
-            r += st[j] ? 1u : 0u;
-            vf[(uint32_t)v] = kk == okey ? -1 : (int32_t)(r - 1);
-            if (st[j]) {  // this voxel's points in index order: the sequential fp32 sums
-                float sx = 0.f, sy = 0.f, sz = 0.f;
-                int64_t e = i;
-                for (; e < size && key_at(e) == kk; ++e) {
-                    const int64_t idx = (uint32_t)seq[e];
-                    sx = __fadd_rn(sx, p[3 * idx]);
-                    sy = __fadd_rn(sy, p[3 * idx + 1]);
-                    sz = __fadd_rn(sz, p[3 * idx + 2]);
-                }
-                const int64_t o = r - 1;
-                const float c = (float)(e - i);
-                cf[3 * o] = __fdiv_rn(sx, c);
-                cf[3 * o + 1] = __fdiv_rn(sy, c);
-                cf[3 * o + 2] = __fdiv_rn(sz, c);
-                nf[o] = (int32_t)(e - i);
-            }
-        }
-        carry += all;
     }
 #ifdef VX_DIAG_PHASES
     VX_STAMP(7);
@@ -977,13 +978,12 @@ __global__ __launch_bounds__(UT, 6) void vx_bucket_kernel(const float *__restric
 
 }  // namespace
 
-// workspace bytes of lidar_voxel_downsample_batch_f32 for (batch, n)
+// workspace bytes of lidar_voxel_downsample_batch_f32 for (batch, n) (the granules and meta words live in
+// the handle's own tag block, beside it)
 LIDAR_EXPORT uint64_t lidar_voxel_batch_workspace_bytes(int64_t batch, int64_t n)
 {
-    const int64_t ntiles = (n + TILE - 1) / TILE, nb = (n + BUCKET - 1) / BUCKET;
+    const int64_t nb = (n + BUCKET - 1) / BUCKET;
     lidar::Carver cv;
-    cv.take<unsigned long long>(batch * ntiles * (6 + NBIN / 2));
-    cv.take<uint32_t>(batch * MW);
     cv.take<uint32_t>(batch * n);
     cv.take<uint32_t>(batch * (nb + 1));
     cv.take<uint64_t>(batch * n);
@@ -991,6 +991,46 @@ LIDAR_EXPORT uint64_t lidar_voxel_batch_workspace_bytes(int64_t batch, int64_t n
     cv.take<uint64_t>(batch * nb);
     return cv.off;
 }
+
+namespace {
+// the handle's tag block of at least `bytes` (granules + meta words), and this call's epoch.  The block
+// is written by voxel calls only, so every tag in it is an earlier call's epoch or 0: no per-call reset.
+// A larger block replaces a smaller one (the old one retired like a workspace: queued calls may still
+// use it) and starts zeroed; so does the block when the epoch wraps.
+void *vx_tags(lidar_handle *h, uint64_t bytes, hipStream_t s, uint32_t *epoch)
+{
+    if (bytes > h->vx_tags_bytes) {
+        const uint64_t want = lidar::align_up(std::max(bytes + bytes / 4, 2 * h->vx_tags_bytes), 1 << 16);
+        void *fresh = nullptr;
+        const hipError_t e = hipMalloc(&fresh, want);
+        if (e != hipSuccess) {
+            lidar::set_error(std::string("voxel tag block hipMalloc(") + std::to_string(want) + "): " +
+                             hipGetErrorString(e));
+            return nullptr;
+        }
+        if (hipMemsetAsync(fresh, 0, want, s) != hipSuccess) {
+            (void)hipFree(fresh);
+            lidar::set_error("voxel tag block: hipMemsetAsync failed");
+            return nullptr;
+        }
+        if (h->vx_tags) {
+            h->retired.push_back(h->vx_tags);
+            h->retired_bytes += h->vx_tags_bytes;
+        }
+        h->vx_tags = fresh;
+        h->vx_tags_bytes = want;
+    }
+    if (++h->epoch == 0) {  // wrapped: no tag may equal a new epoch
+        if (hipMemsetAsync(h->vx_tags, 0, h->vx_tags_bytes, s) != hipSuccess) {
+            lidar::set_error("voxel tag block: hipMemsetAsync failed");
+            return nullptr;
+        }
+        h->epoch = 1;
+    }
+    *epoch = h->epoch;
+    return h->vx_tags;
+}
+}  // namespace
 
 // Voxel downsampling of `batch` frames of n points (xyz (batch, n, 3) fp32), all on the device:
 // voxel_id (batch, n) int32, centroids (batch, n, 3) and counts (batch, n) with the first nvox[f]
@@ -1011,11 +1051,14 @@ LIDAR_EXPORT int lidar_voxel_downsample_batch_f32(lidar_handle *h, const float *
     const int64_t nb = (n + BUCKET - 1) / BUCKET;
     REQUIRE((int64_t)frame_grid(batch, std::max<int64_t>(ntiles, nb)) < 0x7fffffff,
             "lidar_voxel_downsample_batch_f32: batch * n too large");
+    // the in-launch hand-offs' granules (extents, then histograms) and the meta words: the tag block
+    lidar::Carver ct;
+    const uint64_t ogran = ct.take<unsigned long long>(batch * ntiles * (6 + NBIN / 2));
+    const uint64_t ometa = ct.take<uint32_t>(batch * MW);
+    uint32_t epoch = 0;
+    char *tags = static_cast<char *>(vx_tags(h, ct.off, s, &epoch));
+    if (!tags) return LIDAR_ENOMEM;
     lidar::Carver cv;
-    // the granules of the in-launch hand-offs (extents, then histograms), zeroed below: a tag is only
-    // ever read from words this call zeroed or published, never from another operation's leftovers
-    const int64_t ngran = batch * ntiles * (6 + NBIN / 2);
-    const uint64_t ogran = cv.take<unsigned long long>(ngran), ometa = cv.take<uint32_t>(batch * MW);
     const uint64_t okey = cv.take<uint32_t>(batch * n);
     const uint64_t obst = cv.take<uint32_t>(batch * (nb + 1));
     const uint64_t opairs = cv.take<uint64_t>(batch * n), oscr = cv.take<uint64_t>(batch * n);
@@ -1023,8 +1066,8 @@ LIDAR_EXPORT int lidar_voxel_downsample_batch_f32(lidar_handle *h, const float *
     char *base = static_cast<char *>(lidar::workspace(h, cv.off));
     if (!base) return LIDAR_ENOMEM;
     Ws w;
-    w.gran = reinterpret_cast<unsigned long long *>(base + ogran);
-    w.meta = reinterpret_cast<uint32_t *>(base + ometa);
+    w.gran = reinterpret_cast<unsigned long long *>(tags + ogran);
+    w.meta = reinterpret_cast<uint32_t *>(tags + ometa);
     w.key = reinterpret_cast<uint32_t *>(base + okey);
     w.hgran = w.gran + batch * ntiles * 6;
     w.bstart = reinterpret_cast<uint32_t *>(base + obst);
@@ -1032,9 +1075,6 @@ LIDAR_EXPORT int lidar_voxel_downsample_batch_f32(lidar_handle *h, const float *
     w.scratch = reinterpret_cast<uint64_t *>(base + oscr);
     w.flags = reinterpret_cast<uint64_t *>(base + oflags);
     w.cent_diag = centroids;
-    const uint32_t epoch = ++h->epoch == 0 ? ++h->epoch : h->epoch;  // never 0 (the zeroed granules)
-    // granules and the meta words (adjacent in the carve): tags and the hung flag start at 0
-    HIP_TRY(hipMemsetAsync(base + ogran, 0, (size_t)(ometa + batch * MW * sizeof(uint32_t) - ogran), s));
     if (ntiles > kFuseTiles)
         hipLaunchKernelGGL(vx_extent_kernel, dim3(frame_grid(batch, ntiles)), dim3(KT), 0, s, xyz, n, w, ntiles, batch,
                            epoch);
@@ -1048,7 +1088,7 @@ LIDAR_EXPORT int lidar_voxel_downsample_batch_f32(lidar_handle *h, const float *
                            epoch);
     }
     hipLaunchKernelGGL(vx_bucket_kernel, dim3(frame_grid(batch, nb)), dim3(UT), 0, s, xyz, n, w, voxel_id, centroids,
-                       counts, nvox, batch);
+                       counts, nvox, batch, epoch);
     LAUNCH_CHECK();
     return LIDAR_OK;
 }

@@ -151,8 +151,9 @@ def test_voxel_keys_table_and_float64_paths(cuda, case):
 
 @pytest.mark.parametrize("B,n", [(32, 65536), (3, 20000), (1, 150001)])
 def test_voxel_ignores_workspace_leftovers(cuda, B, n):
-    """The batched voxel path's in-launch hand-offs read only granules the same call zeroed or published:
-    a workspace full of tag-like garbage (high halves 1..64, the next calls' tags) changes nothing."""
+    """The batched voxel path's in-launch hand-offs read only granules of the handle's tag block, which
+    holds earlier calls' tags at other layouts: a workspace full of tag-like garbage (high halves 1..64,
+    the next calls' tags) and the other layout's leftovers change nothing."""
     import torch
     from lidar_ai_recommendation_software_amd import _native as nat
     from lidar_ai_recommendation_software_amd import pointnet2 as pn
@@ -161,7 +162,10 @@ def test_voxel_ignores_workspace_leftovers(cuda, B, n):
     xt = torch.from_numpy(x).to(cuda)
     h = nat.handle(0)
     need = nat.load_library().lidar_voxel_batch_workspace_bytes(B, n) + (1 << 20)
+    other = torch.from_numpy(unit_frames(5, 7001, 9)).to(cuda)
     for seed in (1, 2, 3):
+        # the tag block: tags of earlier calls at another layout (never this call's epoch)
+        pn.voxel_downsample_batch(other, 0.02 * seed)
         nat.call("lidar_debug_fill_workspace", h, need, seed, nat.stream_ptr())
         c, vid, cnt, nv = pn.voxel_downsample_batch(xt, 0.05)
         torch.cuda.synchronize()

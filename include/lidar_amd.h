@@ -53,6 +53,9 @@ int lidar_trim(lidar_handle *h, uint64_t *freed);
 /* testing aid: grow the workspace to `bytes` and fill it with tag-like garbage (high halves 1..64) on
  * `stream` — the library never trusts what an earlier call left in the workspace */
 int lidar_debug_fill_workspace(lidar_handle *h, uint64_t bytes, uint64_t seed, void *stream);
+/* testing aid: set the handle's call epoch (the tag of the voxel calls' in-launch hand-offs; the next
+ * call takes epoch + 1, and at the wrap the tag block is zeroed again) */
+int lidar_debug_set_epoch(lidar_handle *h, uint32_t epoch);
 
 const char *lidar_last_error(void);
 int lidar_version(void); /* 4 (what changed per version) */

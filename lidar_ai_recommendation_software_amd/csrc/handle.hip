@@ -136,6 +136,14 @@ LIDAR_EXPORT int lidar_debug_fill_workspace(lidar_handle *h, uint64_t bytes, uin
     return LIDAR_OK;
 }
 
+// Testing aid: sets the handle's call epoch (the next voxel call takes epoch + 1; 0xffffffff: it wraps).
+LIDAR_EXPORT int lidar_debug_set_epoch(lidar_handle *h, uint32_t epoch)
+{
+    REQUIRE(h != nullptr, "lidar_debug_set_epoch: null handle");
+    h->epoch = epoch;
+    return LIDAR_OK;
+}
+
 // Frees the workspaces retired by growth.  The caller guarantees that no work it queued with this
 // handle before the growth is still pending (e.g. after synchronising the streams it used).
 LIDAR_EXPORT int lidar_trim(lidar_handle *h, uint64_t *freed)

@@ -178,6 +178,30 @@ def test_voxel_ignores_workspace_leftovers(cuda, B, n):
             assert np.array_equal(c[f, :nv[f]].cpu().numpy(), wc)
 
 
+def test_voxel_epoch_wrap(cuda):
+    """The voxel calls' tags across the 32-bit epoch wrap (the tag block zeroed again there): the calls
+    before, at and after the wrap all equal the oracle."""
+    import torch
+    from lidar_ai_recommendation_software_amd import _native as nat
+    from lidar_ai_recommendation_software_amd import pointnet2 as pn
+    from lidar_ai_recommendation_software_amd.synthetic import unit_frames
+    x = unit_frames(3, 20000, 12)
+    xt = torch.from_numpy(x).to(cuda)
+    want = [tier_n.voxel_downsample(x[f], 0.05) for f in range(3)]
+    h = nat.handle(0)
+    nat.call("lidar_debug_set_epoch", h, 0xfffffffd)
+    for _ in range(4):  # epochs 0xfffffffe, 0xffffffff, then 1 (wrapped), 2
+        c, vid, cnt, nv = pn.voxel_downsample_batch(xt, 0.05)
+        torch.cuda.synchronize()
+        nv = nv.cpu().numpy()
+        for f in range(3):
+            wc, wvid, wcnt = want[f]
+            assert nv[f] == len(wc)
+            assert np.array_equal(vid[f].cpu().numpy(), wvid)
+            assert np.array_equal(cnt[f, :nv[f]].cpu().numpy(), wcnt)
+            assert np.array_equal(c[f, :nv[f]].cpu().numpy(), wc)
+
+
 def test_fps_extension(cuda):
     x = uniform_frame(5000, 1, -1, 1).astype(np.float32)
     assert np.array_equal(dp.farthest_point_sample(x, 256), tier_n.fps(x, 256))

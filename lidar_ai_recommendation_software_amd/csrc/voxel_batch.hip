@@ -813,31 +813,11 @@ __global__ __launch_bounds__(UT, 6) void vx_bucket_kernel(const float *__restric
                     for (int c = 0; c < 3; ++c) L.xyz[3 * o + c] = g[j][c];
                 }
             }
-            VX_STAMP(4);
-            if (wave == 0) {  // the earlier buckets have published their counts by now (one pass, no wait)
-                bool hung;
-                uint32_t nsp = 0;
-                const uint64_t pre = look_back(fl, b, nvl, &hung, &nsp, true, &lb0);
-#ifdef VX_DIAG_PHASES
-                if (lane == 0) spins_dbg = nsp;
-#endif
-                if (lane == 0) {
-                    prefix = pre;
-                    if (hung) nvox[f] = -2;
-                    else if (b == nb - 1) nvox[f] = (int32_t)(pre + nvl);
-                }
-            }
             __syncthreads();
-            VX_STAMP(5);
-            const uint32_t O = (uint32_t)prefix;
-            // the points' voxel ids (from registers), then one thread per voxel: its sequential fp32 sums
-            // over its points in index order (known run length: the LDS loads pipeline; consecutive
-            // threads write consecutive centroids)
-#pragma unroll
-            for (int j = 0; j < CAP / UT; ++j)
-                if (tid + j * UT < size)
-                    vf[(uint32_t)v[j]] = (sv[j] >> 17) == nvl ? -1 : (int32_t)(O + (sv[j] >> 17));  // nvl: outside
-            VX_STAMP(6);
+            VX_STAMP(4);
+            // one thread per voxel: its sequential fp32 sums over its points in index order (known run
+            // length: the LDS loads pipeline), the centroid written over the voxel's first point — while
+            // wave 0's look-back words arrive; no other voxel reads that range
             for (uint32_t vv = tid; vv < nvl; vv += UT) {
                 const int i0 = L.vstart[vv], i1 = L.vstart[vv + 1];
                 float sx = 0.f, sy = 0.f, sz = 0.f;
@@ -858,11 +838,40 @@ __global__ __launch_bounds__(UT, 6) void vx_bucket_kernel(const float *__restric
                     sy = __fadd_rn(sy, L.xyz[3 * e + 1]);
                     sz = __fadd_rn(sz, L.xyz[3 * e + 2]);
                 }
-                const int64_t o = (int64_t)O + vv;
                 const float c = (float)(i1 - i0);
-                cf[3 * o] = __fdiv_rn(sx, c);
-                cf[3 * o + 1] = __fdiv_rn(sy, c);
-                cf[3 * o + 2] = __fdiv_rn(sz, c);
+                L.xyz[3 * i0] = __fdiv_rn(sx, c);
+                L.xyz[3 * i0 + 1] = __fdiv_rn(sy, c);
+                L.xyz[3 * i0 + 2] = __fdiv_rn(sz, c);
+            }
+            VX_STAMP(5);
+            if (wave == 0) {  // the earlier buckets have published their counts by now (one pass, no wait)
+                bool hung;
+                uint32_t nsp = 0;
+                const uint64_t pre = look_back(fl, b, nvl, &hung, &nsp, true, &lb0);
+#ifdef VX_DIAG_PHASES
+                if (lane == 0) spins_dbg = nsp;
+#endif
+                if (lane == 0) {
+                    prefix = pre;
+                    if (hung) nvox[f] = -2;
+                    else if (b == nb - 1) nvox[f] = (int32_t)(pre + nvl);
+                }
+            }
+            __syncthreads();
+            VX_STAMP(6);
+            const uint32_t O = (uint32_t)prefix;
+            // the points' voxel ids (from registers), then the centroids and counts (consecutive threads:
+            // consecutive voxels)
+#pragma unroll
+            for (int j = 0; j < CAP / UT; ++j)
+                if (tid + j * UT < size)
+                    vf[(uint32_t)v[j]] = (sv[j] >> 17) == nvl ? -1 : (int32_t)(O + (sv[j] >> 17));  // nvl: outside
+            for (uint32_t vv = tid; vv < nvl; vv += UT) {
+                const int i0 = L.vstart[vv], i1 = L.vstart[vv + 1];
+                const int64_t o = (int64_t)O + vv;
+                cf[3 * o] = L.xyz[3 * i0];
+                cf[3 * o + 1] = L.xyz[3 * i0 + 1];
+                cf[3 * o + 2] = L.xyz[3 * i0 + 2];
                 nf[o] = i1 - i0;
             }
         } else {

@@ -23,7 +23,7 @@ nb = (N + 1535) // 1536
 cnt = cnt.cpu().numpy().astype(np.int64)
 d = np.stack([cnt[:, N - 16 * (b + 1):N - 16 * b] for b in range(nb)], 1)  # (B, nb, 16)
 ph = d[:, :, :7].astype(np.float64)
-names = ["range", "load+rank", "scan", "runs+place", "look-back", "ids", "sums"]
+names = ["range", "load+rank", "scan", "runs+place", "sums", "look-back", "stores"]
 print(f"B={B} voxel={voxel} buckets/frame={nb}: mean cycles per phase " +
       ", ".join(f"{k} {v:.0f}" for k, v in zip(names, ph.mean(axis=(0, 1)))))
 for k, nm in enumerate(names):

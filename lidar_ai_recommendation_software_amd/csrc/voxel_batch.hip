@@ -311,7 +311,8 @@ __global__ __launch_bounds__(KT) void vx_keys_kernel(const float *__restrict__ x
     if (!frame_part(batch, ntiles, f, t)) return;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 #ifdef VX_DIAG_KEYS
-    uint64_t kts[10] = {};
+    uint64_t kts[12] = {};
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(kts[10])::"memory");
 #else
     uint64_t *kts = nullptr;
 #endif
@@ -319,7 +320,7 @@ __global__ __launch_bounds__(KT) void vx_keys_kernel(const float *__restrict__ x
     __shared__ uint32_t ext[6];
     __shared__ uint32_t red6[KT / 64][6];
     __shared__ uint32_t hist[NBIN];
-    __shared__ float etab[3][ETAB];
+    __shared__ float etab[3][ETAB + 2];  // -inf, the thresholds, +inf
     const float *p = xyz + (int64_t)f * n * 3;
     float q[PPT][3];  // the tile's points, loaded once: its extent, then its keys
 #pragma unroll
@@ -407,7 +408,8 @@ __global__ __launch_bounds__(KT) void vx_keys_kernel(const float *__restrict__ x
     if (tab) {
 #pragma unroll
         for (int a = 0; a < 3; ++a)
-            for (int i = tid; i < L[a]; i += KT) etab[a][i] = ru_float(lidar_vox::edge(g.ax[a], i));
+            for (int i = tid; i < L[a] + 2; i += KT)
+                etab[a][i] = i == 0 ? -INFINITY : i > L[a] ? INFINITY : ru_float(lidar_vox::edge(g.ax[a], i - 1));
         __syncthreads();
     }
     VX_KSTAMP(3);
@@ -425,7 +427,7 @@ __global__ __launch_bounds__(KT) void vx_keys_kernel(const float *__restrict__ x
             for (int j = 0; j < H; ++j)
 #pragma unroll
                 for (int a = 0; a < 3; ++a) {
-                    c[j][a] = bin_tab_c(etab[a], L[a], q[h0 + j][a], s0[a], inv[a]);
+                    c[j][a] = bin_tab_c(etab[a] + 1, L[a], q[h0 + j][a], s0[a], inv[a]);
                     miss = miss || c[j][a] < 0;
                 }
             if (miss)
@@ -433,7 +435,7 @@ __global__ __launch_bounds__(KT) void vx_keys_kernel(const float *__restrict__ x
                 for (int j = 0; j < H; ++j)
 #pragma unroll
                     for (int a = 0; a < 3; ++a)
-                        if (c[j][a] < 0) c[j][a] = bin_tab_search(etab[a], L[a], q[h0 + j][a]);
+                        if (c[j][a] < 0) c[j][a] = bin_tab_search(etab[a] + 1, L[a], q[h0 + j][a]);
 #pragma unroll
             for (int j = 0; j < H; ++j) {
                 const uint32_t bx = bin_of_c(c[j][0], q[h0 + j][0], lastf[0], L[0]);
@@ -483,9 +485,10 @@ __global__ __launch_bounds__(KT) void vx_keys_kernel(const float *__restrict__ x
     }
 #ifdef VX_DIAG_KEYS
     VX_KSTAMP(9);
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(kts[11])::"memory");
     if (tid == 0) {  // diagnostic build only: stamps into the tail rows of the frame's centroids
-        uint64_t *d = reinterpret_cast<uint64_t *>(w.cent_diag + (f + 1) * n * 3) - 10 * (t + 1);
-        for (int k = 0; k < 10; ++k) d[k] = kts[k];
+        uint64_t *d = reinterpret_cast<uint64_t *>(w.cent_diag + (f + 1) * n * 3) - 12 * (t + 1);
+        for (int k = 0; k < 12; ++k) d[k] = kts[k];
     }
 #endif
 }

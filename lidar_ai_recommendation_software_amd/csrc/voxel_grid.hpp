@@ -149,14 +149,15 @@ __host__ __device__ inline FAxis faxis(const Axis &ax, int max_edges)
     return f;
 }
 
-// c = #{i : E[i] <= p} from the spacing guess and its neighbouring thresholds, branch-free; -1 when the
-// guess is off by more than one bin (bin_tab_search then)
+// c = #{i : E[i] <= p} for a finite p from the spacing guess and its neighbouring thresholds, branch-free;
+// -1 when the guess is off by more than one bin (bin_tab_search then).  E[-1] = -inf and E[L] = +inf
+// (sentinels: the three thresholds are consecutive words, whatever the guess)
 __host__ __device__ inline int bin_tab_c(const float *E, int L, float p, float s0, float inv)
 {
     const float gf = floorf((p - s0) * inv);
     const int b = (int)fminf(fmaxf(gf, 0.f), (float)(L - 1));  // NaN -> 0
-    const float e0 = E[b > 0 ? b - 1 : 0], e1 = E[b], e2 = E[b + 1 < L ? b + 1 : b];
-    return e1 <= p ? (b + 1 == L ? L : (p < e2 ? b + 1 : -1)) : (b == 0 ? 0 : (e0 <= p ? b : -1));
+    const float e0 = E[b - 1], e1 = E[b], e2 = E[b + 1];
+    return e1 <= p ? (p < e2 ? b + 1 : -1) : (e0 <= p ? b : -1);
 }
 __host__ __device__ inline int bin_tab_search(const float *E, int L, float p)
 {

@@ -45,8 +45,11 @@ int main()
         tab = tab && fa[a].ok;
     }
     if (tab)
-        for (int a = 0; a < 3; ++a)
+        for (int a = 0; a < 3; ++a) {  // -inf, the thresholds, +inf (as the launch's LDS tables)
+            E[a].push_back(-INFINITY);
             for (int i = 0; i < fa[a].L; ++i) E[a].push_back(lidar_vox::ru_float(lidar_vox::edge(g.ax[a], i)));
+            E[a].push_back(INFINITY);
+        }
     for (int64_t i = 0; i < n; ++i)
         for (int a = 0; a < 3; ++a) {
             const float q = p[3 * i + a];
@@ -54,8 +57,8 @@ int main()
                 b[3 * i + a] = lidar_vox::bin(g.ax[a], (double)q);
                 continue;
             }
-            int c = lidar_vox::bin_tab_c(E[a].data(), fa[a].L, q, fa[a].s0, fa[a].inv);
-            if (c < 0) c = lidar_vox::bin_tab_search(E[a].data(), fa[a].L, q);
+            int c = lidar_vox::bin_tab_c(E[a].data() + 1, fa[a].L, q, fa[a].s0, fa[a].inv);
+            if (c < 0) c = lidar_vox::bin_tab_search(E[a].data() + 1, fa[a].L, q);
             const uint32_t bb = lidar_vox::bin_of_c(c, q, fa[a].lastf, fa[a].L);
             b[3 * i + a] = bb == lidar_vox::kOutside ? -1 : (int64_t)bb;
         }

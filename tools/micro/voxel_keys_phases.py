@@ -20,7 +20,9 @@ for _ in range(3):
     c, vid, cnt, nv = pn.voxel_downsample_batch(x, voxel)
 torch.cuda.synchronize()
 raw = c.cpu().numpy().reshape(B, -1).view(np.uint64)  # (B, 1.5 N) words
-st = np.stack([raw[:, raw.shape[1] - 10 * (t + 1): raw.shape[1] - 10 * t] for t in range(T)], 1).astype(np.int64)
+st = np.stack([raw[:, raw.shape[1] - 12 * (t + 1): raw.shape[1] - 12 * t] for t in range(T)], 1).astype(np.int64)
+rt = st[:, :, 10:12].astype(np.float64) * 0.01  # s_memrealtime (100 MHz): start, end in us
+st = st[:, :, :10]
 d = np.diff(st, axis=2).astype(np.float64)  # (B, T, 9)
 names = ["extent publish", "extent poll", "grid+tables", "keys+hist", "hist publish", "hist poll", "scan+offsets",
          "bucket table", "scatter"]
@@ -28,3 +30,7 @@ print(f"B={B}: mean cycles per phase " + ", ".join(f"{k} {v:.0f}" for k, v in zi
 print("total per tile (mean, max):", round(float(d.sum(2).mean())), round(float(d.sum(2).max())))
 for k, nm in enumerate(names):
     print(f"{nm:14s} by tile:", np.round(d[:, :, k].mean(0)).astype(int).tolist())
+t0 = rt[:, :, 0].min()
+print("realtime: span us %.1f, start spread us %.1f, tile life us mean %.1f max %.1f, clock GHz %.2f" % (
+    rt[:, :, 1].max() - t0, rt[:, :, 0].max() - t0, (rt[:, :, 1] - rt[:, :, 0]).mean(), (rt[:, :, 1] - rt[:, :, 0]).max(),
+    d.sum(2).mean() / (rt[:, :, 1] - rt[:, :, 0]).mean() / 1e3))

@@ -51,10 +51,12 @@ constexpr int HB = 12;             // coarse-bin bits of the key range
 constexpr int NBIN = 1 << HB;      // coarse bins per frame
 constexpr int BPT = NBIN / KT;     // coarse bins per scatter thread (its scan)
 constexpr int UT = 512;            // bucket threads
-constexpr int CAP = 2048;          // pairs a bucket sorts in LDS
+constexpr int CAP = 2560;          // pairs a bucket sorts in LDS
+constexpr int BITONIC_MAX = 2048;  // pairs the LDS bitonic fallback sorts (a power of two)
 constexpr int KMAX = 4096;         // local key range of the LDS counting sort
 constexpr int SEGMAX = 32;         // longest equal-key run the counting sort orders by index itself
-constexpr int BUCKET = 1536;       // target points per bucket
+constexpr int BUCKET = 2048;       // target points per bucket (32 x 65 536 points: 1 024 buckets, one round of
+                                   // four workgroups per CU)
 constexpr int MW = 8;              // meta words per frame: [0] grid ok, [1] outside key, [2] hs, [3] hung tag
 constexpr uint64_t kPad = ~0ull;   // bitonic padding: sorts last
 static_assert(NBIN % KT == 0 && NBIN % UT == 0, "bins per thread");
@@ -634,20 +636,20 @@ __device__ uint64_t look_back(unsigned long long *fl, int64_t b, uint32_t nv, bo
     return pre;
 }
 
-// 36 KiB (three 512-thread workgroups per CU at <= 84 VGPRs)
+// 35 KiB: four 512-thread workgroups per CU (at <= 64 VGPRs)
 struct BucketLds {
     uint32_t s[CAP];           // the counting sort's unordered runs: point indices (a run is one key)
     union {
         uint32_t cnt[KMAX];    // counting-sort counters, then per key its first sorted position | its voxel's
                                // rank in the bucket << 16 (the radix path: its digit tables)
-        float xyz[CAP * 3];    // the sorted points' xyz, for the centroid sums (written once cnt is dead)
-        uint64_t a[CAP];       // the bitonic path's pairs
+        uint32_t idx[CAP];     // the point indices in sorted order (written once cnt is dead)
+        uint64_t a[BITONIC_MAX];  // the bitonic path's pairs
     };
     uint16_t vstart[CAP + 1];  // voxel v's first sorted position, then the voxels' end
 };
 static_assert(CAP < 65536, "packed first position | voxel rank");
 
-__global__ __launch_bounds__(UT, 6) void vx_bucket_kernel(const float *__restrict__ xyz, int64_t n, Ws w,
+__global__ __launch_bounds__(UT, 8) void vx_bucket_kernel(const float *__restrict__ xyz, int64_t n, Ws w,
                                                        int32_t *__restrict__ vid, float *__restrict__ cent,
                                                        int32_t *__restrict__ counts, int32_t *__restrict__ nvox,
                                                        int64_t batch, uint32_t epoch)
@@ -702,22 +704,16 @@ __global__ __launch_bounds__(UT, 6) void vx_bucket_kernel(const float *__restric
     float *cf = cent + (int64_t)f * n * 3;
     int32_t *nf = counts + (int64_t)f * n;
     const uint64_t *seq = nullptr;  // the slow paths: the bucket sorted by (key, index), LDS or global
+    bool radix = false;
     if (size <= CAP) {
-        // the pairs and their points' xyz (the gathers fly while the keys sort), and the range of the
-        // keys they hold (not of their coarse bins: the first and last buckets' bins reach over the
-        // grid's empty margins, past the counting sort's range)
+        // the pairs, and the range of the keys they hold (not of their coarse bins: the first and last
+        // buckets' bins reach over the grid's empty margins, past the counting sort's range)
+        static_assert(CAP % UT == 0, "pairs per thread");
         uint64_t v[CAP / UT];
-        float g[CAP / UT][3];
         {
             uint32_t kmin = 0xffffffffu, kmax = 0u;
 #pragma unroll
             for (int j = 0; j < CAP / UT; ++j) v[j] = tid + j * UT < size ? gp[tid + j * UT] : 0ull;
-#pragma unroll
-            for (int j = 0; j < CAP / UT; ++j) {
-                const int64_t idx = (uint32_t)v[j];  // 0 past the end
-#pragma unroll
-                for (int c = 0; c < 3; ++c) g[j][c] = p[3 * idx + c];
-            }
 #pragma unroll
             for (int j = 0; j < CAP / UT; ++j)
                 if (tid + j * UT < size) {
@@ -753,7 +749,7 @@ __global__ __launch_bounds__(UT, 6) void vx_bucket_kernel(const float *__restric
             __syncthreads();
         }
         VX_STAMP(2);
-        if (counting && !flag) {
+        if (counting && !flag) {  // (uniform)
             // one exclusive scan of (count | occupied << 16) over the local keys gives every key its first
             // sorted position and its voxel's rank in the bucket (the outside key occupies no voxel), and
             // the bucket's voxel count, published at once for the later buckets' look-back
@@ -780,9 +776,9 @@ __global__ __launch_bounds__(UT, 6) void vx_bucket_kernel(const float *__restric
             VX_STAMP(3);
             // each key's run, unordered; the voxels' first positions (the run's rank-0 element writes it;
             // the outside key's run, when present, is the last and ends the last voxel)
-            // (sv: the run's first position | its length << 11 | the voxel's rank << 17 — every field
-            // below 2^11 with CAP = 2048, lengths <= SEGMAX)
-            static_assert(CAP <= 2048 && SEGMAX < 64, "packed run fields");
+            // (sv: the run's first position | its length << 12 | the voxel's rank << 18 — positions and
+            // ranks below 2^12 with CAP <= 4096, lengths <= SEGMAX)
+            static_assert(CAP <= 4096 && SEGMAX < 64, "packed run fields");
             uint32_t sv[CAP / UT];
 #pragma unroll
             for (int j = 0; j < CAP / UT; ++j) {
@@ -791,7 +787,7 @@ __global__ __launch_bounds__(UT, 6) void vx_bucket_kernel(const float *__restric
                     const uint32_t lk = lr[j] & 0xffffu, rk = lr[j] >> 16, e = L.cnt[lk];
                     const uint32_t st = e & 0xffffu, vp = e >> 16;
                     const uint32_t en = lk + 1 < krange ? L.cnt[lk + 1] & 0xffffu : (uint32_t)size;
-                    sv[j] = st | (en - st) << 11 | vp << 17;
+                    sv[j] = st | (en - st) << 12 | vp << 18;
                     L.s[st + rk] = (uint32_t)v[j];
                     if (rk == 0) L.vstart[vp] = (uint16_t)st;  // the outside key's run: vp = nvl
                 }
@@ -803,50 +799,18 @@ __global__ __launch_bounds__(UT, 6) void vx_bucket_kernel(const float *__restric
             unsigned long long lb0 = 0;
             if (wave == 0) lb0 = look_back_first(fl, b);
             // index order inside a run (< SEGMAX long): every element counts the smaller indices of its
-            // run; its xyz lands at its sorted position
+            // run; its index lands at its sorted position
 #pragma unroll
             for (int j = 0; j < CAP / UT; ++j) {
                 const int64_t i = tid + j * UT;
                 if (i < size) {
-                    const uint32_t st = sv[j] & 0x7ffu, en = st + ((sv[j] >> 11) & 0x3fu);
+                    const uint32_t st = sv[j] & 0xfffu, en = st + ((sv[j] >> 12) & 0x3fu);
                     uint32_t r = 0;
                     for (uint32_t x = st; x < en; ++x) r += L.s[x] < (uint32_t)v[j] ? 1u : 0u;
-                    const uint32_t o = st + r;
-#pragma unroll
-                    for (int c = 0; c < 3; ++c) L.xyz[3 * o + c] = g[j][c];
+                    L.idx[st + r] = (uint32_t)v[j];
                 }
             }
-            __syncthreads();
             VX_STAMP(4);
-            // one thread per voxel: its sequential fp32 sums over its points in index order (known run
-            // length: the LDS loads pipeline), the centroid written over the voxel's first point — while
-            // wave 0's look-back words arrive; no other voxel reads that range
-            for (uint32_t vv = tid; vv < nvl; vv += UT) {
-                const int i0 = L.vstart[vv], i1 = L.vstart[vv + 1];
-                float sx = 0.f, sy = 0.f, sz = 0.f;
-                int e = i0;
-                for (; e + 4 <= i1; e += 4) {
-                    float q[12];
-#pragma unroll
-                    for (int k = 0; k < 12; ++k) q[k] = L.xyz[3 * e + k];
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        sx = __fadd_rn(sx, q[3 * k]);
-                        sy = __fadd_rn(sy, q[3 * k + 1]);
-                        sz = __fadd_rn(sz, q[3 * k + 2]);
-                    }
-                }
-                for (; e < i1; ++e) {
-                    sx = __fadd_rn(sx, L.xyz[3 * e]);
-                    sy = __fadd_rn(sy, L.xyz[3 * e + 1]);
-                    sz = __fadd_rn(sz, L.xyz[3 * e + 2]);
-                }
-                const float c = (float)(i1 - i0);
-                L.xyz[3 * i0] = __fdiv_rn(sx, c);
-                L.xyz[3 * i0 + 1] = __fdiv_rn(sy, c);
-                L.xyz[3 * i0 + 2] = __fdiv_rn(sz, c);
-            }
-            VX_STAMP(5);
             if (wave == 0) {  // the earlier buckets have published their counts by now (one pass, no wait)
                 bool hung;
                 uint32_t nsp = 0;
@@ -861,23 +825,45 @@ __global__ __launch_bounds__(UT, 6) void vx_bucket_kernel(const float *__restric
                 }
             }
             __syncthreads();
-            VX_STAMP(6);
+            VX_STAMP(5);
             const uint32_t O = (uint32_t)prefix;
-            // the points' voxel ids (from registers), then the centroids and counts (consecutive threads:
-            // consecutive voxels)
+            // the points' voxel ids (from registers)
 #pragma unroll
             for (int j = 0; j < CAP / UT; ++j)
                 if (tid + j * UT < size)
-                    vf[(uint32_t)v[j]] = (sv[j] >> 17) == nvl ? -1 : (int32_t)(O + (sv[j] >> 17));  // nvl: outside
+                    vf[(uint32_t)v[j]] = (sv[j] >> 18) == nvl ? -1 : (int32_t)(O + (sv[j] >> 18));  // nvl: outside
+            VX_STAMP(6);
+            // one thread per voxel: the sequential fp32 sums over its points in index order, their xyz
+            // gathered GB at a time (the frame's points are L2-resident since the keys launch), the
+            // centroid and count (consecutive threads: consecutive voxels)
             for (uint32_t vv = tid; vv < nvl; vv += UT) {
                 const int i0 = L.vstart[vv], i1 = L.vstart[vv + 1];
+                float sx = 0.f, sy = 0.f, sz = 0.f;
+                constexpr int GB = 8;  // one round trip for most voxels
+                for (int e0 = i0; e0 < i1; e0 += GB) {
+                    float q[GB][3];
+#pragma unroll
+                    for (int k = 0; k < GB; ++k) {
+                        const int64_t id = e0 + k < i1 ? (int64_t)L.idx[e0 + k] : (int64_t)L.idx[i0];
+#pragma unroll
+                        for (int c = 0; c < 3; ++c) q[k][c] = p[3 * id + c];
+                    }
+#pragma unroll
+                    for (int k = 0; k < GB; ++k)
+                        if (e0 + k < i1) {
+                            sx = __fadd_rn(sx, q[k][0]);
+                            sy = __fadd_rn(sy, q[k][1]);
+                            sz = __fadd_rn(sz, q[k][2]);
+                        }
+                }
                 const int64_t o = (int64_t)O + vv;
-                cf[3 * o] = L.xyz[3 * i0];
-                cf[3 * o + 1] = L.xyz[3 * i0 + 1];
-                cf[3 * o + 2] = L.xyz[3 * i0 + 2];
+                const float c = (float)(i1 - i0);
+                cf[3 * o] = __fdiv_rn(sx, c);
+                cf[3 * o + 1] = __fdiv_rn(sy, c);
+                cf[3 * o + 2] = __fdiv_rn(sz, c);
                 nf[o] = i1 - i0;
             }
-        } else {
+        } else if (size <= BITONIC_MAX) {
             // bitonic sort of the loaded pairs in LDS (a key range past the counting sort, or a long run)
             int64_t P = 1;
             while (P < size) P <<= 1;
@@ -898,8 +884,14 @@ __global__ __launch_bounds__(UT, 6) void vx_bucket_kernel(const float *__restric
                     __syncthreads();
                 }
             seq = L.a;
+        } else {
+            radix = true;
         }
     } else {
+        radix = true;
+    }
+    if (radix) {  // (uniform) a bucket past the LDS sorts: LSD radix sort in global memory
+        __syncthreads();
         seq = bucket_radix(const_cast<uint64_t *>(gp), w.scratch + (int64_t)f * n + p0, size, L.cnt,
                            reinterpret_cast<uint32_t(*)[256]>(L.cnt + 256), red, &vary);
     }

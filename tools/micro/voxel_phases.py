@@ -19,11 +19,11 @@ x = torch.from_numpy(unit_frames(B, N, 0)).to("cuda:0")
 for _ in range(3):
     c, vid, cnt, nv = pn.voxel_downsample_batch(x, voxel)
 torch.cuda.synchronize()
-nb = (N + 1535) // 1536
+nb = (N + 2047) // 2048
 cnt = cnt.cpu().numpy().astype(np.int64)
 d = np.stack([cnt[:, N - 16 * (b + 1):N - 16 * b] for b in range(nb)], 1)  # (B, nb, 16)
 ph = d[:, :, :7].astype(np.float64)
-names = ["range", "load+rank", "scan", "runs+place", "sums", "look-back", "stores"]
+names = ["range", "load+rank", "scan", "runs+place", "look-back", "ids", "sums"]
 print(f"B={B} voxel={voxel} buckets/frame={nb}: mean cycles per phase " +
       ", ".join(f"{k} {v:.0f}" for k, v in zip(names, ph.mean(axis=(0, 1)))))
 for k, nm in enumerate(names):
@@ -37,3 +37,6 @@ for f in (0, 8, 1, 31 if B > 31 else B - 1):
     print(f"frame {f}: look-back start us", np.round(us[f, :, 4], 1).tolist())
     print(f"frame {f}: look-back end us", np.round(us[f, :, 5], 1).tolist())
 print("kernel span us", round(us[:, :, 7].max(), 1))
+rd = np.mod(np.diff(rt, axis=2), 2.0 ** 31) * 0.01  # (B, nb, 7) realtime per phase, us (stamps kept mod 2^31)
+print("realtime us per phase: " + ", ".join(f"{k} {v:.2f}" for k, v in zip(names, rd.mean(axis=(0, 1)))) +
+      f"; workgroup life {rd.sum(2).mean():.1f} us")

@@ -52,13 +52,13 @@ constexpr int NBIN = 1 << HB;      // coarse bins per frame
 constexpr int BPT = NBIN / KT;     // coarse bins per scatter thread (its scan)
 constexpr int UT = 512;            // bucket threads
 constexpr int CAP = 2560;          // pairs a bucket sorts in LDS
-constexpr int BITONIC_MAX = 2048;  // pairs the LDS bitonic fallback sorts (a power of two)
+constexpr int BITONIC_P = 2048;    // the LDS bitonic fallback's array (a power of two; larger buckets
+                                   // sort in global memory: at P = 4 096 the LDS network is the slower)
 constexpr int KMAX = 4096;         // local key range of the LDS counting sort
-constexpr int SEGMAX = 32;         // longest equal-key run the counting sort orders by index itself
+constexpr int SEGMAX = 128;        // longest equal-key run the counting sort orders by index itself
 constexpr int BUCKET = 2048;       // target points per bucket (32 x 65 536 points: 1 024 buckets, one round of
                                    // four workgroups per CU)
 constexpr int MW = 8;              // meta words per frame: [0] grid ok, [1] outside key, [2] hs, [3] hung tag
-constexpr uint64_t kPad = ~0ull;   // bitonic padding: sorts last
 static_assert(NBIN % KT == 0 && NBIN % UT == 0, "bins per thread");
 
 __device__ __forceinline__ uint32_t ord(float f)  // monotone float -> u32
@@ -636,14 +636,18 @@ __device__ uint64_t look_back(unsigned long long *fl, int64_t b, uint32_t nv, bo
     return pre;
 }
 
-// 35 KiB: four 512-thread workgroups per CU (at <= 64 VGPRs)
+// 31 KiB: four 512-thread workgroups per CU (at <= 64 VGPRs)
 struct BucketLds {
-    uint32_t s[CAP];           // the counting sort's unordered runs: point indices (a run is one key)
     union {
-        uint32_t cnt[KMAX];    // counting-sort counters, then per key its first sorted position | its voxel's
-                               // rank in the bucket << 16 (the radix path: its digit tables)
-        uint32_t idx[CAP];     // the point indices in sorted order (written once cnt is dead)
-        uint64_t a[BITONIC_MAX];  // the bitonic path's pairs
+        struct {
+            uint32_t s[CAP];   // the counting sort's unordered runs: point indices (a run is one key)
+            union {
+                uint32_t cnt[KMAX];  // counting-sort counters, then per key its first sorted position | its
+                                     // voxel's rank in the bucket << 16 (the radix path: its digit tables)
+                uint32_t idx[CAP];   // the point indices in sorted order (written once cnt is dead)
+            };
+        };
+        uint64_t a[BITONIC_P];  // the bitonic path's pairs (over the above)
     };
     uint16_t vstart[CAP + 1];  // voxel v's first sorted position, then the voxels' end
 };
@@ -776,9 +780,9 @@ __global__ __launch_bounds__(UT, 8) void vx_bucket_kernel(const float *__restric
             VX_STAMP(3);
             // each key's run, unordered; the voxels' first positions (the run's rank-0 element writes it;
             // the outside key's run, when present, is the last and ends the last voxel)
-            // (sv: the run's first position | its length << 12 | the voxel's rank << 18 — positions and
-            // ranks below 2^12 with CAP <= 4096, lengths <= SEGMAX)
-            static_assert(CAP <= 4096 && SEGMAX < 64, "packed run fields");
+            // (sv: the run's first position | the voxel's rank << 16; the run's end: the next voxel's
+            // first position, or the bucket's end for the outside key's run, the last)
+            static_assert(CAP < 65536, "packed run fields");
             uint32_t sv[CAP / UT];
 #pragma unroll
             for (int j = 0; j < CAP / UT; ++j) {
@@ -786,8 +790,7 @@ __global__ __launch_bounds__(UT, 8) void vx_bucket_kernel(const float *__restric
                 if (i < size) {
                     const uint32_t lk = lr[j] & 0xffffu, rk = lr[j] >> 16, e = L.cnt[lk];
                     const uint32_t st = e & 0xffffu, vp = e >> 16;
-                    const uint32_t en = lk + 1 < krange ? L.cnt[lk + 1] & 0xffffu : (uint32_t)size;
-                    sv[j] = st | (en - st) << 12 | vp << 18;
+                    sv[j] = st | vp << 16;
                     L.s[st + rk] = (uint32_t)v[j];
                     if (rk == 0) L.vstart[vp] = (uint16_t)st;  // the outside key's run: vp = nvl
                 }
@@ -804,7 +807,8 @@ __global__ __launch_bounds__(UT, 8) void vx_bucket_kernel(const float *__restric
             for (int j = 0; j < CAP / UT; ++j) {
                 const int64_t i = tid + j * UT;
                 if (i < size) {
-                    const uint32_t st = sv[j] & 0xfffu, en = st + ((sv[j] >> 12) & 0x3fu);
+                    const uint32_t st = sv[j] & 0xffffu, vp = sv[j] >> 16;
+                    const uint32_t en = vp == nvl ? (uint32_t)size : L.vstart[vp + 1];
                     uint32_t r = 0;
                     for (uint32_t x = st; x < en; ++x) r += L.s[x] < (uint32_t)v[j] ? 1u : 0u;
                     L.idx[st + r] = (uint32_t)v[j];
@@ -831,7 +835,7 @@ __global__ __launch_bounds__(UT, 8) void vx_bucket_kernel(const float *__restric
 #pragma unroll
             for (int j = 0; j < CAP / UT; ++j)
                 if (tid + j * UT < size)
-                    vf[(uint32_t)v[j]] = (sv[j] >> 18) == nvl ? -1 : (int32_t)(O + (sv[j] >> 18));  // nvl: outside
+                    vf[(uint32_t)v[j]] = (sv[j] >> 16) == nvl ? -1 : (int32_t)(O + (sv[j] >> 16));  // nvl: outside
             VX_STAMP(6);
             // one thread per voxel: the sequential fp32 sums over its points in index order, their xyz
             // gathered GB at a time (the frame's points are L2-resident since the keys launch), the
@@ -863,14 +867,16 @@ __global__ __launch_bounds__(UT, 8) void vx_bucket_kernel(const float *__restric
                 cf[3 * o + 2] = __fdiv_rn(sz, c);
                 nf[o] = i1 - i0;
             }
-        } else if (size <= BITONIC_MAX) {
-            // bitonic sort of the loaded pairs in LDS (a key range past the counting sort, or a long run)
+        } else if (size <= BITONIC_P) {
+            // bitonic sort of the pairs in LDS (a key range past the counting sort, or a long run)
+            __syncthreads();  // (the counting attempt's cnt reads are done: a overlays it)
             int64_t P = 1;
             while (P < size) P <<= 1;
-            for (int64_t i = tid; i < P; i += UT) L.a[i] = i < size ? gp[i] : kPad;  // (rare: reloaded)
+            for (int64_t i = tid; i < P; i += UT) L.a[i] = i < size ? gp[i] : ~0ull;  // (reloaded; pads last)
             __syncthreads();
             for (int64_t k2 = 2; k2 <= P; k2 <<= 1)
                 for (int64_t j = k2 >> 1; j > 0; j >>= 1) {
+#pragma unroll 1
                     for (int64_t i = tid; i < P; i += UT) {
                         const int64_t l = i ^ j;
                         if (l > i) {

@@ -178,6 +178,35 @@ def test_voxel_ignores_workspace_leftovers(cuda, B, n):
             assert np.array_equal(c[f, :nv[f]].cpu().numpy(), wc)
 
 
+@pytest.mark.parametrize("case", ["wide_keys", "runs_128", "runs_129", "runs_600"])
+def test_voxel_bucket_sort_paths(cuda, case):
+    """The bucket launch's sorts: the LDS counting sort (runs of up to SEGMAX = 128 equal keys ordered by
+    index in place), the LDS bitonic sort (a key range past 4 096, or a longer run, in buckets of up to
+    2 048 pairs) and the global radix sort (the same in larger buckets) — each bit-exact against the oracle,
+    through the batched path (two frames) and the drop-in."""
+    import torch
+    from lidar_ai_recommendation_software_amd import pointnet2 as pn
+    rng = np.random.default_rng(21)
+    if case == "wide_keys":  # ~100^3 keys over 65 536 points: every bucket past the counting range
+        x, v = rng.random((65536, 3)).astype(np.float32), 0.01
+    else:  # clusters of exactly r points inside one voxel each, plus uniform points
+        r = int(case.split("_")[1])
+        k = 40000 // r
+        c = (rng.integers(0, 20, (k, 3)) * 0.05 + 0.025).astype(np.float32)
+        pts = np.repeat(c, r, axis=0) + rng.uniform(-0.01, 0.01, (k * r, 3)).astype(np.float32)
+        x = np.concatenate([pts, rng.random((8000, 3)).astype(np.float32)])[rng.permutation(k * r + 8000)]
+        v = 0.05
+    xb = np.stack([x, x[::-1].copy()])
+    c, vid, cnt, nv = (t.cpu().numpy() for t in pn.voxel_downsample_batch(torch.from_numpy(xb).to(cuda), v))
+    for f in range(2):
+        wc, wvid, wcnt = tier_n.voxel_downsample(xb[f], v)
+        assert nv[f] == len(wcnt), (case, f)
+        assert np.array_equal(vid[f], wvid) and np.array_equal(cnt[f, :nv[f]], wcnt), (case, f)
+        assert np.array_equal(c[f, :nv[f]].view(np.uint32), wc.view(np.uint32)), (case, f)
+    c1, vid1, cnt1 = dp.voxel_downsample(x, v)
+    assert np.array_equal(vid1, vid[0]) and np.array_equal(c1.view(np.uint32), c[0, :nv[0]].view(np.uint32))
+
+
 def test_voxel_epoch_wrap(cuda):
     """The voxel calls' tags across the 32-bit epoch wrap (the tag block zeroed again there): the calls
     before, at and after the wrap all equal the oracle."""

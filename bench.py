@@ -590,7 +590,8 @@ def voxel_leg(dev, rank, world, B=32, n=65536, voxel=0.05, steps=20, cpu=True):
            "voxels_per_frame": nv / B, "parity": "bit-exact vs oracle/tier_n.voxel_downsample "
            "(tests/test_gpu_tier_r.py::test_voxel_downsample_batch_vs_oracle)",
            "roofline": {"kernel": "voxel_downsample_batch (2 launches: extents + keys + coarse-bin scatter with "
-                                  "in-launch hand-offs, per-bucket LDS sort + look-back + ids / centroids)", "bound": "hbm",
+                                  "in-launch hand-offs; one round of 2048-point buckets: LDS counting sort + "
+                                  "look-back + ids / centroids; no memset)", "bound": "hbm",
                         "achieved": algo / per_launch / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": algo / per_launch / 1e9 / HBM_PEAK_GBS, "traffic": None,
                         "work_per_launch": algo, "avg_launch_ms": per_launch * 1e3,

@@ -644,12 +644,17 @@ struct BucketLds {
             union {
                 uint32_t cnt[KMAX];  // counting-sort counters, then per key its first sorted position | its
                                      // voxel's rank in the bucket << 16 (the radix path: its digit tables)
-                uint32_t idx[CAP];   // the point indices in sorted order (written once cnt is dead)
+                struct {
+                    uint32_t idx[CAP];     // the point indices in sorted order (written once cnt is dead;
+                                           // the shifted sort: bit 31 marks a voxel's first point)
+                    uint16_t vpos[CAP];    // the shifted sort: voxels up to each sorted position
+                };
             };
         };
         uint64_t a[BITONIC_P];  // the bitonic path's pairs (over the above)
     };
     uint16_t vstart[CAP + 1];  // voxel v's first sorted position, then the voxels' end
+    uint8_t rank[CAP];         // the dense sort: each pair's rank inside its key (load order)
 };
 static_assert(CAP < 65536, "packed first position | voxel rank");
 
@@ -713,17 +718,20 @@ __global__ __launch_bounds__(UT, 8) void vx_bucket_kernel(const float *__restric
         // the pairs, and the range of the keys they hold (not of their coarse bins: the first and last
         // buckets' bins reach over the grid's empty margins, past the counting sort's range)
         static_assert(CAP % UT == 0, "pairs per thread");
-        uint64_t v[CAP / UT];
+        uint32_t kk[CAP / UT], id[CAP / UT];  // the pairs' keys and point indices
         {
             uint32_t kmin = 0xffffffffu, kmax = 0u;
 #pragma unroll
-            for (int j = 0; j < CAP / UT; ++j) v[j] = tid + j * UT < size ? gp[tid + j * UT] : 0ull;
+            for (int j = 0; j < CAP / UT; ++j) {
+                const uint64_t x = tid + j * UT < size ? gp[tid + j * UT] : 0ull;
+                kk[j] = (uint32_t)(x >> 32);
+                id[j] = (uint32_t)x;
+            }
 #pragma unroll
             for (int j = 0; j < CAP / UT; ++j)
                 if (tid + j * UT < size) {
-                    const uint32_t kk = (uint32_t)(v[j] >> 32);
-                    kmin = min(kmin, kk);
-                    kmax = max(kmax, kk);
+                    kmin = min(kmin, kk[j]);
+                    kmax = max(kmax, kk[j]);
                 }
             kmin = lidar::wave_min_u32_dpp(kmin);
             kmax = ~lidar::wave_min_u32_dpp(~kmax);
@@ -734,85 +742,186 @@ __global__ __launch_bounds__(UT, 8) void vx_bucket_kernel(const float *__restric
         }
         __syncthreads();
         const uint64_t k0 = rng[2], krange = size ? (uint64_t)rng[3] - rng[2] + 1 : 0;
-        const bool counting = krange <= KMAX;
-        if (counting)
-            for (int64_t c = tid; c < (int64_t)krange; c += UT) L.cnt[c] = 0;
+        // local keys: (key - k0) >> sh, below KMAX.  sh = 0: one counter per key; sh > 0 (a sparse grid):
+        // runs of a counter hold several keys, ordered by (key, index) as one 32-bit word (key's low sh
+        // bits << ib | index) when that fits
+        static_assert(KMAX == 4096, "12-bit local keys");
+        const int kb = krange > 1 ? 64 - __clzll((unsigned long long)(krange - 1)) : 0;
+        const int sh = max(0, kb - 12);
+        const int ib = 32 - __clz((uint32_t)max<int64_t>(n - 1, 1));
+        const bool counting = sh == 0 || sh + ib <= 32;
+        const uint32_t nbin = counting && krange ? (uint32_t)((krange - 1) >> sh) + 1u : 0u;
+        for (int64_t c = tid; c < (int64_t)nbin; c += UT) L.cnt[c] = 0;
         __syncthreads();
-        uint32_t lr[CAP / UT];  // local key | rank inside the key << 16
+        auto lkey = [&](uint32_t key) { return (key - (uint32_t)k0) >> sh; };
         if (counting) {
-            // counting sort by local key: a rank inside the key from an LDS atomic
+            // counting sort by local key: a rank inside the local key from an LDS atomic (a run past
+            // SEGMAX: the bitonic path instead)
+            static_assert(SEGMAX < 256, "8-bit ranks");
 #pragma unroll
-            for (int j = 0; j < CAP / UT; ++j) {
-                const int64_t i = tid + j * UT;
-                if (i < size) {
-                    const uint32_t lk = (uint32_t)((v[j] >> 32) - k0), rk = atomicAdd(&L.cnt[lk], 1u);
-                    lr[j] = lk | rk << 16;
-                    if (rk == SEGMAX) flag = 1;  // a long equal-key run: the bitonic path instead
+            for (int j = 0; j < CAP / UT; ++j)
+                if (tid + j * UT < size) {
+                    const uint32_t r = atomicAdd(&L.cnt[lkey(kk[j])], 1u);
+                    L.rank[tid + j * UT] = (uint8_t)r;
+                    if (r == SEGMAX) flag = 1;
                 }
-            }
             __syncthreads();
         }
         VX_STAMP(2);
         if (counting && !flag) {  // (uniform)
-            // one exclusive scan of (count | occupied << 16) over the local keys gives every key its first
-            // sorted position and its voxel's rank in the bucket (the outside key occupies no voxel), and
-            // the bucket's voxel count, published at once for the later buckets' look-back
-            constexpr int PT = KMAX / UT;
-            uint32_t cv[PT], sum = 0;
-#pragma unroll
-            for (int j = 0; j < PT; ++j) {
-                const int64_t c = PT * tid + j;
-                const uint32_t x = c < (int64_t)krange ? L.cnt[c] : 0u;
-                cv[j] = x + (x != 0u && (uint32_t)(k0 + c) != okey ? 0x10000u : 0u);
-                sum += cv[j];
-            }
-            uint32_t all;
-            uint32_t ex = block_excl_scan<UT>(sum, red, &all);
-#pragma unroll
-            for (int j = 0; j < PT; ++j) {
-                const int64_t c = PT * tid + j;
-                if (c < (int64_t)krange) L.cnt[c] = ex;
-                ex += cv[j];
-            }
-            const uint32_t nvl = all >> 16;
-            if (tid == 0) look_back_publish(fl, b, nvl);
-            __syncthreads();
-            VX_STAMP(3);
-            // each key's run, unordered; the voxels' first positions (the run's rank-0 element writes it;
-            // the outside key's run, when present, is the last and ends the last voxel)
-            // (sv: the run's first position | the voxel's rank << 16; the run's end: the next voxel's
-            // first position, or the bucket's end for the outside key's run, the last)
-            static_assert(CAP < 65536, "packed run fields");
-            uint32_t sv[CAP / UT];
-#pragma unroll
-            for (int j = 0; j < CAP / UT; ++j) {
-                const int64_t i = tid + j * UT;
-                if (i < size) {
-                    const uint32_t lk = lr[j] & 0xffffu, rk = lr[j] >> 16, e = L.cnt[lk];
-                    const uint32_t st = e & 0xffffu, vp = e >> 16;
-                    sv[j] = st | vp << 16;
-                    L.s[st + rk] = (uint32_t)v[j];
-                    if (rk == 0) L.vstart[vp] = (uint16_t)st;  // the outside key's run: vp = nvl
-                }
-            }
-            if (tid == 0 && rng[3] != okey) L.vstart[nvl] = (uint16_t)size;
-            __syncthreads();
-            // wave 0: the look-back's first window in flight during the placement below (the earlier
-            // buckets publish their counts at the same point of their lives)
+            uint32_t nvl;
+            uint32_t sv[CAP / UT];  // finally: the point's voxel rank in the bucket (nvl: outside every bin)
             unsigned long long lb0 = 0;
-            if (wave == 0) lb0 = look_back_first(fl, b);
-            // index order inside a run (< SEGMAX long): every element counts the smaller indices of its
-            // run; its index lands at its sorted position
+            constexpr int PT = KMAX / UT;
+            static_assert(CAP < 4096 && SEGMAX < 256, "packed run fields");
+            if (sh == 0) {
+                // one exclusive scan of (count | occupied << 16) over the keys gives every key its first
+                // sorted position and its voxel's rank in the bucket (the outside key occupies no voxel),
+                // and the bucket's voxel count, published at once for the later buckets' look-back
+                uint32_t cv[PT], sum = 0;
 #pragma unroll
-            for (int j = 0; j < CAP / UT; ++j) {
-                const int64_t i = tid + j * UT;
-                if (i < size) {
-                    const uint32_t st = sv[j] & 0xffffu, vp = sv[j] >> 16;
-                    const uint32_t en = vp == nvl ? (uint32_t)size : L.vstart[vp + 1];
-                    uint32_t r = 0;
-                    for (uint32_t x = st; x < en; ++x) r += L.s[x] < (uint32_t)v[j] ? 1u : 0u;
-                    L.idx[st + r] = (uint32_t)v[j];
+                for (int j = 0; j < PT; ++j) {
+                    const int64_t c = PT * tid + j;
+                    const uint32_t x = c < (int64_t)nbin ? L.cnt[c] : 0u;
+                    cv[j] = x + (x != 0u && (uint32_t)(k0 + c) != okey ? 0x10000u : 0u);
+                    sum += cv[j];
                 }
+                uint32_t all;
+                uint32_t ex = block_excl_scan<UT>(sum, red, &all);
+#pragma unroll
+                for (int j = 0; j < PT; ++j) {
+                    const int64_t c = PT * tid + j;
+                    if (c < (int64_t)nbin) L.cnt[c] = ex;
+                    if (cv[j]) L.vstart[ex >> 16] = (uint16_t)ex;  // a voxel's first position (the outside
+                    ex += cv[j];                                    // key's run, the last: vstart[nvl])
+                }
+                nvl = all >> 16;
+                if (tid == 0) look_back_publish(fl, b, nvl);
+                if (tid == 0 && rng[3] != okey) L.vstart[nvl] = (uint16_t)size;
+                __syncthreads();
+                VX_STAMP(3);
+                // each key's run, unordered (sv: the point's voxel rank; the run: vstart[vp] ..
+                // vstart[vp + 1], or the bucket's end for the outside key's run)
+#pragma unroll
+                for (int j = 0; j < CAP / UT; ++j)
+                    if (tid + j * UT < size) {
+                        const uint32_t e = L.cnt[lkey(kk[j])];
+                        L.s[(e & 0xffffu) + L.rank[tid + j * UT]] = id[j];
+                        sv[j] = e >> 16;
+                    }
+                __syncthreads();
+                // wave 0: the look-back's first window in flight during the placement below (the
+                // earlier buckets publish their counts at the same point of their lives)
+                if (wave == 0) lb0 = look_back_first(fl, b);
+                // index order inside a run (< SEGMAX long): every element counts the smaller indices of
+                // its run; its index lands at its sorted position
+#pragma unroll
+                for (int j = 0; j < CAP / UT; ++j) {
+                    const int64_t i = tid + j * UT;
+                    if (i < size) {
+                        const uint32_t vp = sv[j], st = L.vstart[vp];
+                        const uint32_t en = vp == nvl ? (uint32_t)size : L.vstart[vp + 1];
+                        uint32_t r = 0;
+                        for (uint32_t x = st; x < en; ++x) r += L.s[x] < id[j] ? 1u : 0u;
+                        L.idx[st + r] = id[j];
+                    }
+                }
+            } else {
+                // the shifted sort: starts of the local keys' runs by an exclusive scan of the counts
+                uint32_t cv[PT], sum = 0;
+#pragma unroll
+                for (int j = 0; j < PT; ++j) {
+                    const int64_t c = PT * tid + j;
+                    cv[j] = c < (int64_t)nbin ? L.cnt[c] : 0u;
+                    sum += cv[j];
+                }
+                uint32_t all;
+                uint32_t ex = block_excl_scan<UT>(sum, red, &all);
+#pragma unroll
+                for (int j = 0; j < PT; ++j) {
+                    const int64_t c = PT * tid + j;
+                    if (c < (int64_t)nbin) L.cnt[c] = ex;
+                    ex += cv[j];
+                }
+                __syncthreads();
+                VX_STAMP(3);
+                const uint32_t kmask = (1u << sh) - 1u;
+                // each run, unordered (sv: its first position | its length << 12 | outside << 20; then a
+                // slot from the local key's cursor for the point's word — (key's low sh bits, index) in
+                // order — which replaces its key in kk)
+#pragma unroll
+                for (int j = 0; j < CAP / UT; ++j)
+                    if (tid + j * UT < size) {
+                        const uint32_t lk = lkey(kk[j]), st = L.cnt[lk];
+                        const uint32_t en = lk + 1 < nbin ? L.cnt[lk + 1] : (uint32_t)size;
+                        sv[j] = st | (en - st) << 12 | (kk[j] == okey ? 1u << 20 : 0u);
+                    }
+                __syncthreads();
+#pragma unroll
+                for (int j = 0; j < CAP / UT; ++j)
+                    if (tid + j * UT < size) {
+                        const uint32_t lk = lkey(kk[j]);
+                        kk[j] = ((kk[j] - (uint32_t)k0) & kmask) << ib | id[j];
+                        L.s[atomicAdd(&L.cnt[lk], 1u)] = kk[j];
+                    }
+                __syncthreads();
+                // (key, index) order inside a run: every element counts the smaller words of its run, and
+                // whether one of them holds its key (else it is its voxel's first point; the outside key
+                // is no voxel)
+#pragma unroll
+                for (int j = 0; j < CAP / UT; ++j) {
+                    const int64_t i = tid + j * UT;
+                    if (i < size) {
+                        const uint32_t st = sv[j] & 0xfffu, en = st + ((sv[j] >> 12) & 0xffu), wd = kk[j];
+                        const uint32_t hi = ib == 32 ? 0u : wd >> ib;
+                        uint32_t r = 0;
+                        bool dup = false;
+                        for (uint32_t x = st; x < en; ++x) {
+                            const uint32_t w2 = L.s[x];
+                            r += w2 < wd ? 1u : 0u;
+                            dup = dup || (w2 < wd && (ib == 32 ? 0u : w2 >> ib) == hi);
+                        }
+                        const bool out = (sv[j] >> 20) & 1u;
+                        L.idx[st + r] = id[j] | (!dup && !out ? 0x80000000u : 0u);
+                        sv[j] = (st + r) | (!dup ? 1u << 16 : 0u) | (out ? 1u << 17 : 0u);
+                    }
+                }
+                __syncthreads();
+                // voxel ranks: the voxels' first points up to each sorted position (CAP / UT consecutive
+                // positions per thread), the bucket's count published at once
+                constexpr int CH = CAP / UT;
+                uint32_t bits = 0, fc = 0;
+#pragma unroll
+                for (int k = 0; k < CH; ++k) {
+                    const int64_t o = CH * tid + k;
+                    const uint32_t fb = o < size ? L.idx[o] >> 31 : 0u;
+                    bits |= fb << k;
+                    fc += fb;
+                }
+                uint32_t allv;
+                uint32_t inc = block_excl_scan<UT>(fc, red, &allv);
+#pragma unroll
+                for (int k = 0; k < CH; ++k) {
+                    const int64_t o = CH * tid + k;
+                    inc += (bits >> k) & 1u;
+                    if (o < size) L.vpos[o] = (uint16_t)inc;
+                }
+                nvl = allv;
+                if (tid == 0) look_back_publish(fl, b, nvl);
+                __syncthreads();
+                if (wave == 0) lb0 = look_back_first(fl, b);
+#pragma unroll
+                for (int j = 0; j < CAP / UT; ++j) {
+                    const int64_t i = tid + j * UT;
+                    if (i < size) {
+                        const uint32_t o = sv[j] & 0xffffu;
+                        const bool first = (sv[j] >> 16) & 1u, out = (sv[j] >> 17) & 1u;
+                        const uint32_t vp = out ? nvl : (uint32_t)L.vpos[o] - 1u;
+                        if (first) L.vstart[vp] = (uint16_t)o;  // the outside key's first point ends the last voxel
+                        sv[j] = vp;
+                    }
+                }
+                if (tid == 0 && rng[3] != okey) L.vstart[nvl] = (uint16_t)size;
             }
             VX_STAMP(4);
             if (wave == 0) {  // the earlier buckets have published their counts by now (one pass, no wait)
@@ -835,7 +944,7 @@ __global__ __launch_bounds__(UT, 8) void vx_bucket_kernel(const float *__restric
 #pragma unroll
             for (int j = 0; j < CAP / UT; ++j)
                 if (tid + j * UT < size)
-                    vf[(uint32_t)v[j]] = (sv[j] >> 16) == nvl ? -1 : (int32_t)(O + (sv[j] >> 16));  // nvl: outside
+                    vf[id[j]] = sv[j] == nvl ? -1 : (int32_t)(O + sv[j]);  // nvl: outside
             VX_STAMP(6);
             // one thread per voxel: the sequential fp32 sums over its points in index order, their xyz
             // gathered GB at a time (the frame's points are L2-resident since the keys launch), the
@@ -848,7 +957,7 @@ __global__ __launch_bounds__(UT, 8) void vx_bucket_kernel(const float *__restric
                     float q[GB][3];
 #pragma unroll
                     for (int k = 0; k < GB; ++k) {
-                        const int64_t id = e0 + k < i1 ? (int64_t)L.idx[e0 + k] : (int64_t)L.idx[i0];
+                        const int64_t id = (e0 + k < i1 ? L.idx[e0 + k] : L.idx[i0]) & 0x7fffffffu;
 #pragma unroll
                         for (int c = 0; c < 3; ++c) q[k][c] = p[3 * id + c];
                     }

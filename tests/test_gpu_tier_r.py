@@ -178,17 +178,20 @@ def test_voxel_ignores_workspace_leftovers(cuda, B, n):
             assert np.array_equal(c[f, :nv[f]].cpu().numpy(), wc)
 
 
-@pytest.mark.parametrize("case", ["wide_keys", "runs_128", "runs_129", "runs_600"])
+@pytest.mark.parametrize("case", ["wide_keys", "lidar_sparse", "runs_128", "runs_129", "runs_600"])
 def test_voxel_bucket_sort_paths(cuda, case):
     """The bucket launch's sorts: the LDS counting sort (runs of up to SEGMAX = 128 equal keys ordered by
-    index in place), the LDS bitonic sort (a key range past 4 096, or a longer run, in buckets of up to
-    2 048 pairs) and the global radix sort (the same in larger buckets) — each bit-exact against the oracle,
+    index in place), its shifted form for sparse grids (a key range past 4 096: counters over the keys'
+    high bits, each run ordered by (key, index) words), the LDS bitonic sort (a longer run, in buckets of
+    up to 2 048 pairs) and the global radix sort (the same in larger buckets) — each bit-exact against the oracle,
     through the batched path (two frames) and the drop-in."""
     import torch
     from lidar_ai_recommendation_software_amd import pointnet2 as pn
     rng = np.random.default_rng(21)
     if case == "wide_keys":  # ~100^3 keys over 65 536 points: every bucket past the counting range
         x, v = rng.random((65536, 3)).astype(np.float32), 0.01
+    elif case == "lidar_sparse":  # 200 x 200 x 10 m at 5 cm: ~3.3e9 keys, a bucket's keys far apart
+        x, v = (rng.uniform(-1, 1, (65536, 3)) * [100, 100, 5]).astype(np.float32), 0.05
     else:  # clusters of exactly r points inside one voxel each, plus uniform points
         r = int(case.split("_")[1])
         k = 40000 // r

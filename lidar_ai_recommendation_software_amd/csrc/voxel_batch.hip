@@ -636,7 +636,7 @@ __device__ uint64_t look_back(unsigned long long *fl, int64_t b, uint32_t nv, bo
     return pre;
 }
 
-// 31 KiB: four 512-thread workgroups per CU (at <= 64 VGPRs)
+// 34 KiB: four 512-thread workgroups per CU (at <= 64 VGPRs)
 struct BucketLds {
     union {
         struct {

@@ -210,6 +210,42 @@ def test_voxel_bucket_sort_paths(cuda, case):
     assert np.array_equal(vid1, vid[0]) and np.array_equal(c1.view(np.uint32), c[0, :nv[0]].view(np.uint32))
 
 
+@pytest.mark.parametrize("seed", range(12))
+def test_voxel_random_frames_vs_oracle(cuda, seed):
+    """Randomised frames through the batched path (three frames per call): sizes from 1 to 40 000 points,
+    extents from centimetres to hundreds of metres, voxel sizes over four decades, duplicated points and
+    tight clusters — every sort path (dense / shifted counting, bitonic, radix) in some bucket; ids, counts
+    and centroids bit-exact against the oracle, nvox -1 exactly where the oracle refuses the grid."""
+    import torch
+    from lidar_ai_recommendation_software_amd import pointnet2 as pn
+    rng = np.random.default_rng(1000 + seed)
+    n = int(rng.choice([1, 7, 300, 5000, 20000, 40000]))
+    frames = []
+    for _ in range(3):
+        ext = 10.0 ** rng.uniform(-2, 2.5, 3)
+        x = (rng.uniform(-1, 1, (n, 3)) * ext + rng.uniform(-50, 50, 3)).astype(np.float32)
+        if n > 10 and rng.random() < 0.5:  # duplicates
+            k = int(n * rng.uniform(0.1, 0.5))
+            x[rng.integers(0, n, k)] = x[rng.integers(0, n, k)]
+        if n > 100 and rng.random() < 0.5:  # a tight cluster
+            k = int(n * rng.uniform(0.05, 0.3))
+            x[:k] = x[0] + rng.normal(0, 1e-3, (k, 3)).astype(np.float32)
+        frames.append(x)
+    xb = np.stack(frames)
+    span = float(np.median((xb.max(axis=1) - xb.min(axis=1)).max(axis=1)))
+    v = float(span / 10.0 ** rng.uniform(0.5, 3.3)) or 1.0
+    c, vid, cnt, nv = (t.cpu().numpy() for t in pn.voxel_downsample_batch(torch.from_numpy(xb).to(cuda), v))
+    for f in range(3):
+        try:
+            wc, wvid, wcnt = tier_n.voxel_downsample(xb[f], v)
+        except ValueError:
+            assert nv[f] == -1, (seed, f)
+            continue
+        assert nv[f] == len(wcnt), (seed, f, n, v)
+        assert np.array_equal(vid[f], wvid) and np.array_equal(cnt[f, :nv[f]], wcnt), (seed, f, n, v)
+        assert np.array_equal(c[f, :nv[f]].view(np.uint32), wc.view(np.uint32)), (seed, f, n, v)
+
+
 def test_voxel_epoch_wrap(cuda):
     """The voxel calls' tags across the 32-bit epoch wrap (the tag block zeroed again there): the calls
     before, at and after the wrap all equal the oracle."""

@@ -116,7 +116,7 @@ __host__ __device__ inline uint32_t key(const Grid &g, float x, float y, float z
 }
 
 // ---- the keys launch's float binning (voxel_batch.hip; tests/test_voxel_grid_host.py runs it on the host)
-constexpr int kTabEdges = 4096;  // edges per axis of its LDS threshold tables
+constexpr int kTabEdges = 8192;  // edges per axis of its LDS threshold tables (±200 m at 5 cm)
 
 // The least float >= e: for every float p, p >= e (in float64) <=> p >= ru_float(e), as no float lies
 // between e and it — so counting the float thresholds <= p counts the float64 edges <= p.

@@ -120,10 +120,10 @@ def _edge_frame(n, v, seed):
     return np.concatenate([x] + extra).astype(np.float32)
 
 
-@pytest.mark.parametrize("case", ["edges", "edges_coarse", "long_axis", "near_table_limit", "far_offset"])
+@pytest.mark.parametrize("case", ["edges", "edges_coarse", "long_axis", "near_table_limit", "far_offset", "lidar_400m"])
 def test_voxel_keys_table_and_float64_paths(cuda, case):
     """The keys launch bins in float against per-axis tables of the float64 edges' float thresholds
-    (<= 4 096 edges per axis) and in float64 otherwise: both bit-exact against the oracle, points on
+    (<= 8 192 edges per axis) and in float64 otherwise: both bit-exact against the oracle, points on
     the edges included, guesses off by more than a bin (large offsets) included."""
     rng = np.random.default_rng(11)
     if case == "edges":
@@ -136,9 +136,12 @@ def test_voxel_keys_table_and_float64_paths(cuda, case):
         x[:, 1:] *= np.float32(0.002)
         if case == "long_axis":  # x: ~10 000 edges, past the table
             v = 1e-4
-        elif case == "near_table_limit":  # x: ~4 005 edges, in the table
-            x[:, 0] *= np.float32(0.4)
+        elif case == "near_table_limit":  # x: ~8 005 edges, in the table
+            x[:, 0] *= np.float32(0.8)
             v = 1e-4
+        elif case == "lidar_400m":  # ±200 m (±1 m in z) at 5 cm: ~8 000 edges on x and y, in the tables
+            x = (rng.uniform(-1, 1, (n, 3)) * [200, 200, 1]).astype(np.float32)
+            v = 0.05
         else:  # coordinates near 1 000: float spacing 6e-5 against a 1e-3 voxel
             x[:, 0] = x[:, 0] + np.float32(1000.0)
             v = 1e-3

@@ -66,9 +66,9 @@ ADVERSARIAL = {
     "v_0.3_near_edges": (lambda: near_edges(3, 0.3, -5.0), 0.3),
     "v_0.07_near_edges": (lambda: near_edges(4, 0.07, 123.0), 0.07),
     "v_1e-3_near_edges": (lambda: near_edges(5, 1e-3, 0.5), 1e-3),
-    # about 4000 bins on x: the widest tables; 5000: past them (float64 key())
-    "tab_4000_bins": (lambda: near_edges(7, 0.05, -77.7, n=6000, bins=4000, yz_bins=30), 0.05),
-    "tab_5000_bins": (lambda: near_edges(8, 0.05, 31.3, n=6000, bins=5000, yz_bins=30), 0.05),
+    # about 8000 bins on x: the widest tables; 9000: past them (float64 key())
+    "tab_8000_bins": (lambda: near_edges(7, 0.05, -77.7, n=6000, bins=8000, yz_bins=30), 0.05),
+    "tab_9000_bins": (lambda: near_edges(8, 0.05, 31.3, n=6000, bins=9000, yz_bins=30), 0.05),
     "negative_far": (lambda: (np.random.default_rng(6).random((3000, 3)) * -50 - 2.5e4).astype(np.float32), 0.37),
 }
 
@@ -87,7 +87,7 @@ def outside_frame(n=999):
 ADVERSARIAL["outside_2p30"] = (outside_frame, 3.3 * 2.0 ** -22)
 
 
-K_TAB_EDGES = 4096  # csrc/voxel_grid.hpp kTabEdges: a finer axis runs lidar_vox::key in float64
+K_TAB_EDGES = 8192  # csrc/voxel_grid.hpp kTabEdges: a finer axis runs lidar_vox::key in float64
 
 
 @pytest.mark.parametrize("name", sorted(VOXEL_CASES) + sorted(ADVERSARIAL))
@@ -113,7 +113,7 @@ def test_kernel_binning_equals_oracle(harness, name):
     assert np.array_equal(keys[inside], wkey[inside].astype(np.uint32))
     assert (keys[~inside] == 0xffffffff).all()
     if name.startswith("tab_"):
-        assert run.tab == int(name == "tab_4000_bins")
+        assert run.tab == int(name == "tab_8000_bins")
     if name == "outside_2p30":
         assert 0 < (~inside).sum() < len(x)
 

@@ -1,5 +1,5 @@
 """Voxel batch micro (python tools/voxel_micro.py [B] [voxel] [scale]): 20 launches on 32 x 65536 frames
-(scale: the unit frames stretched by (scale, scale, scale / 20) — a LiDAR-like sparse grid at scale 100)."""
+(scale: the unit frames stretched by (scale, scale, scale / 200) — a LiDAR-like sparse grid at scale 100-200)."""
 import os
 import sys
 
@@ -14,7 +14,7 @@ voxel = float(sys.argv[2]) if len(sys.argv) > 2 else 0.05
 scale = float(sys.argv[3]) if len(sys.argv) > 3 else 1.0
 f = unit_frames(B, 65536, 0)
 if scale != 1.0:
-    f = (f * [scale, scale, scale / 20]).astype("float32")
+    f = (f * [scale, scale, scale / 200]).astype("float32")
 x = torch.from_numpy(f).to("cuda:0")
 for _ in range(20):
     pn.voxel_downsample_batch(x, voxel)

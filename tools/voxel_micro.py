@@ -1,4 +1,4 @@
-"""Voxel batch micro (python tools/voxel_micro.py [B] [voxel] [scale]): 20 launches on 32 x 65536 frames
+"""Voxel batch micro (python tools/voxel_micro.py [B] [voxel] [scale] [N]): 20 launches on 32 x 65536 frames
 (scale: the unit frames stretched by (scale, scale, scale / 200) — a LiDAR-like sparse grid at scale 100-200)."""
 import os
 import sys
@@ -12,7 +12,8 @@ from lidar_ai_recommendation_software_amd.synthetic import unit_frames  # noqa: 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 32
 voxel = float(sys.argv[2]) if len(sys.argv) > 2 else 0.05
 scale = float(sys.argv[3]) if len(sys.argv) > 3 else 1.0
-f = unit_frames(B, 65536, 0)
+N = int(sys.argv[4]) if len(sys.argv) > 4 else 65536
+f = unit_frames(B, N, 0)
 if scale != 1.0:
     f = (f * [scale, scale, scale / 200]).astype("float32")
 x = torch.from_numpy(f).to("cuda:0")

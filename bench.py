@@ -183,6 +183,11 @@ def compact_line(rec, detail_path=None):
     line["roofline"] = {k: roof[k] for k in keep_roof if k in roof}
     if roof.get("traffic") is not None:
         line["roofline"]["traffic_basis"] = "HBM-side bytes per launch, rocprofv3 PMC (FETCH_SIZE x2 + WRITE_SIZE)"
+    if roof.get("kernel") == "sa1_group_mlp":
+        line["roofline"]["note"] = "time includes SA1's ball queries, whose work is not priced"
+    gm = rec.get("roofline_grouped_mlp")
+    if gm:  # north_star's MFMA figure (SA2 layers 2-3), whichever kernel dominates the window
+        line["roofline_grouped_mlp"] = {k: gm[k] for k in ("kernel", "frac", "achieved", "avg_launch_ms") if k in gm}
     cb = rec.get("cpu_baseline")
     line["cpu_baseline"] = None if cb is None else {
         "value": cb["value"], "unit": cb["unit"], "cores": cb["cores"], "kind": cb["kind"], "sample": cb["sample"][:200]}

@@ -68,6 +68,14 @@ def test_compact_line_fits_and_keeps_the_contract(world):
     assert d["arithmetic"].startswith("h3: fp32 as fp16 hi+lo")
     bq = d["ball_query_hbm"]
     assert bq["target"] == 0.5 and bq["met"] is False and 0 < bq["frac_compulsory"] < 0.5
+    # north_star's MFMA figure is on the line whichever kernel dominates the window (the fused SA1 kernel and
+    # the SA2 grouped MLP tie within box noise; SA1's time includes its ball queries, said in a note)
+    if rec.get("roofline_grouped_mlp"):
+        g = d["roofline_grouped_mlp"]
+        assert g["kernel"] == "sa2_group_mlp" and 0 < g["frac"] < 1
+    rec2 = json.loads(json.dumps(rec))
+    rec2["roofline"]["kernel"] = "sa1_group_mlp"
+    assert "ball queries" in bench.compact_line(rec2)["roofline"]["note"]
     if world <= 8:  # the optional parts survive at the driver's world sizes
         assert "legs_M_points_per_s" in d and "kernels" in d and d["detail"] == "gpurun_out/bench_detail.json"
         r = d["roofline_configs[4]"]

@@ -13,28 +13,30 @@
 //            tile loads its points once, publishes its extent as self-tagged 8-byte granules and
 //            polls its frame's other tiles' (an in-launch hand-off instead of a bbox launch), builds
 //            the frame's grid (float64, every workgroup alike), bins every point in float against
-//            per-axis LDS tables of the float64 edges' float thresholds (float64 beyond 4096 edges per
+//            per-axis LDS tables of the float64 edges' float thresholds (float64 beyond 8192 edges per
 //            axis; a point outside every bin takes nx ny nz, one past the last voxel), and publishes
 //            its histogram over 4096 coarse bins (key >> hs, the top 12 bits of the range) as tagged
 //            granules too; then, from the frame's histograms (polled), the exclusive scan over the
 //            coarse bins plus the counts of the tiles before it, and it scatters its (key, index)
 //            pairs from registers to their coarse bins (LDS atomics: order inside a bin is free, the
 //            buckets sort by (key, index) anyway); tile 0 also writes the bucket table (bucket b = the
-//            coarse bins whose start s has min(s NB / n, NB - 1) = b, ~1 536 points uniform).
-//            Frames of more than 16 tiles (more than an XCD co-schedules) split this into an extent
-//            launch, a keys launch that writes the keys, and a scatter launch.
-//   bucket   grid (buckets, frames; 3 workgroups per CU): each bucket loads its pairs and gathers
-//            their xyz, sorts by (key, index) in LDS (a counting sort over the bucket's own key range
-//            with equal-key runs ranked by index in parallel; bitonic when the range or a run is too
-//            long; a bucket above 2048 pairs — clumped frames, huge voxels — sorts in global memory by
-//            a stable LSD radix over the bits that vary), counts its voxels, takes its voxel offset
-//            from the buckets before it by a decoupled look-back (each bucket publishes its count,
-//            then its inclusive prefix; every wait is on a lower workgroup index, i.e. one dispatched
-//            earlier), writes every point's voxel id and, one thread per voxel summing its points in
-//            index order, the centroids and counts.
+//            coarse bins whose start s has min(s NB / n, NB - 1) = b, ~2 048 points uniform).
+//            Frames of more than 16 tiles (more than an XCD co-schedules with margin) split this into
+//            an extent launch, a keys launch that writes the keys, and a scatter launch.  The granules
+//            live in the handle's tag block: every tag there is an earlier call's epoch (no memset).
+//   bucket   grid (buckets, frames; 4 workgroups per CU, the bench shape's 1 024 buckets in one round):
+//            each bucket loads its pairs and counting-sorts them in LDS over its own key range — one
+//            counter per key, whose exclusive scan of (count | occupied << 16) also gives every key its
+//            voxel rank; or, for a sparse grid (a range past 4096 keys), counters over the keys' high
+//            bits with each run ordered by (key low bits, index) words and the voxel ranks from a scan
+//            of first-point flags — equal-key runs ranked by index in parallel; runs past 128: bitonic
+//            in LDS, or a stable LSD radix in global memory above 2048 pairs.  Its voxel count goes out
+//            at once for the decoupled look-back (every wait is on a lower workgroup index, i.e. one
+//            dispatched earlier), then every point's voxel id from registers and, one thread per voxel
+//            summing its points' xyz (gathered) in index order, the centroids and counts.
 //
 // Memory-side bytes per point: xyz 12 (keys) + pair 8 + 8 + id 4 + the xyz gather 12
-// (+16 per voxel out); no host synchronisation: nvox[f] lands on the device (-1: the frame's extent is
+// (+16 per voxel out; 62.9 measured by PMC at the bench shape); no host synchronisation: nvox[f] lands on the device (-1: the frame's extent is
 // not finite, or its grid has 2^32 - 1 keys or more).
 #include <algorithm>
 

@@ -111,16 +111,24 @@ __host__ __forceinline__ unsigned frame_grid(int64_t batch, int64_t parts)
 
 // block-wide exclusive scan of one value per thread (T threads); returns the exclusive prefix and
 // the total through *tot.  Uses red[T / 64]; starts and ends with a barrier.
+// wave64 inclusive prefix sum by DPP: row_shr 1, 2, 4, 8 inside each 16-lane row (lanes without a
+// source add 0), then row_bcast 15 / 31 carry the rows' totals (no LDS traffic, unlike __shfl_up)
+__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v)
+{
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);
+    return v;
+}
+
 template <int T>
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *red, uint32_t *tot)
 {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint32_t inc = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t u = (uint32_t)__shfl_up((int)inc, o, 64);
-        if (lane >= o) inc += u;
-    }
+    const uint32_t inc = wave_incl_scan_u32(v);
     __syncthreads();  // red[] free (a previous scan's readers are done)
     if (lane == 63) red[wave] = inc;
     __syncthreads();

@@ -122,12 +122,7 @@ __device__ __forceinline__ void grid_query_wave(const float *__restrict__ p, con
             st = tab[s1];
             len = tab[s1 + (hiz - loz) + 1] - st;
         }
-        int incl = clen;
-#pragma unroll
-        for (int d = 1; d < 16; d <<= 1) {
-            const int v = __shfl_up(incl, d, 64);
-            if (lane >= d) incl += v;
-        }
+        const int incl = lidar::row_incl_scan_i32(clen);  // lanes 0..8 (row 0): the columns' prefix
         const int tot = full ? CAP + 1 : __builtin_amdgcn_readlane(incl, 8);
         if (tot == 0) continue;
         if (tot > CAP) {

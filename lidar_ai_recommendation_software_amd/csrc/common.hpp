@@ -213,6 +213,15 @@ __device__ __forceinline__ int dpp_i(int v)
 {
     return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, true);
 }
+// inclusive prefix sum inside each 16-lane row (row_shr 1, 2, 4, 8; lanes without a source add 0)
+__device__ __forceinline__ int row_incl_scan_i32(int v)
+{
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);
+    return v;
+}
 __device__ __forceinline__ float wave_max_dpp(float v)
 {
     v = fmaxf(v, __int_as_float(dpp_i<0xB1>(__float_as_int(v))));

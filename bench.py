@@ -223,6 +223,8 @@ def compact_line(rec, detail_path=None):
         legs["ssg_native_fp32_mfma"] = rec["fp32_mfma_kernels"]["value"]
     for k, v in (rec.get("other_configs") or {}).items():
         legs[k] = v["M_points_per_s"]
+        if v.get("chains_ms_per_group"):
+            optional.append((f"chains_{k.split('_')[0]}", v["chains_ms_per_group"]))
         if v.get("roofline"):
             r = v["roofline"]
             optional.insert(0, (f"roofline_{k.split('_')[0]}", {x: r[x] for x in (
@@ -585,7 +587,17 @@ def voxel_leg(dev, rank, world, B=32, n=65536, voxel=0.05, steps=20, cpu=True):
     x = torch.from_numpy(unit_frames(B, n, seed=sharding.frame_seed(rank, base=77))).to(dev)
     out = pn.voxel_downsample_batch(x, voxel)
     torch.cuda.synchronize(dev)
-    el = sharding.timed(lambda: [pn.voxel_downsample_batch(x, voxel) for _ in range(steps)], dev, world)
+    # the timed loop leaves nvox on the device (no host read-back per call); checked afterwards
+    last = [None]
+
+    def loop():
+        for _ in range(steps):
+            last[0] = pn.voxel_downsample_batch(x, voxel, check=False)
+
+    el = sharding.timed(loop, dev, world)
+    pn.check_voxel_counts(last[0][3])
+    assert torch.equal(last[0][3], out[3]) and torch.equal(last[0][1], out[1]), "voxel path not deterministic"
+    del last
     nv = int(out[3].sum().item())
     per_launch = el / steps
     algo = B * n * 16 + nv * 16
@@ -674,8 +686,6 @@ def main():
                          "nearest of 3, 4, 5, 2 that does")
     ap.add_argument("--fps-threads", type=int, default=512, choices=[512, 1024],
                     help="SA1 FPS workgroup size in the pipeline (512: half the CU footprint beside the MLPs)")
-    ap.add_argument("--fps-lazy", type=int, default=0,
-                    help="1: SA1 FPS on the lazy-refresh kernel (LIDAR_FPS_LAZY; identical results)")
     ap.add_argument("--x3", type=int, default=1,
                     help="1: MLPs on the split-bf16 (x3) kernels, fp32 arithmetic within the 1e-4 contract; "
                          "0: the native fp32-MFMA kernels")
@@ -696,6 +706,9 @@ def main():
     ap.add_argument("--msg-batch", type=int, default=32,
                     help="frames per GPU per step of the configs[4] MSG leg (32: the per-GPU share of 256 frames)")
     ap.add_argument("--msg-steps", type=int, default=30)
+    ap.add_argument("--msg-side-ns", type=int, default=128,
+                    help="configs[4] leg: level-0 branches of >= this many samples answer their ball queries on "
+                         "the side streams (StreamingSSG side_query_ns; 0: every branch fused on the main stream)")
     ap.add_argument("--no-extras", action="store_true", help="skip the configs[1]/[4] side measurements")
     ap.add_argument("--no-density", action="store_true", help="skip the Tier R / variant / voxel / host-frame legs")
     ap.add_argument("--seed-rank", type=int, default=None,
@@ -730,7 +743,7 @@ def main():
     digests = {}
     local_ms = {}  # this rank's own window time per leg (the line reports the max over ranks)
 
-    def measure(key, cfg, dtype, B, N, steps, warmup, depth, G, x3=True, events=True):
+    def measure(key, cfg, dtype, B, N, steps, warmup, depth, G, x3=True, events=True, side_query_ns=128):
         """Steady-state window of `steps` batches through StreamingSSG's feed.  events: HIP
         events around every launch inside the timed window (the headline: the roofline durations
         come from the same window); False: the window runs clean and the per-kernel durations come
@@ -745,9 +758,9 @@ def main():
         ready = torch.cuda.Event()  # the inputs exist: the feed's FPS launches wait only for their slots
         ready.record()
         pipe = pn.StreamingSSG(bb, B, N, depth=depth, fps_group=G, fps_threads=args.fps_threads,
-                               fps_lazy=bool(args.fps_lazy), ramp=False,
+                               ramp=False,
                                slots=args.slots or None, bq=args.bq,
-                               l2_side=bool(args.l2_side))
+                               l2_side=bool(args.l2_side), side_query_ns=side_query_ns)
         feed = pipe.feed()
         nwarm = (depth + max(1, warmup)) * G  # whole groups; `depth` groups in flight when the window opens
         outs = []
@@ -832,11 +845,19 @@ def main():
                 ("configs[4]_msg_131k_bf16", pn.MSG, "bf16", args.msg_batch, 131072, args.msg_steps)]
         for key, cfg, dtype, b2, n2, st2 in legs:
             g2 = pick_group(st2, 3)
-            el2, t2, _, _ = measure(key, cfg, dtype, b2, n2, st2, 1, 3, g2, events=False)
+            sq = (args.msg_side_ns or None) if cfg is pn.MSG else 128
+            el2, t2, _, _ = measure(key, cfg, dtype, b2, n2, st2, 1, 3, g2, events=False, side_query_ns=sq)
+            pl2 = {k: t / c for k, (c, f, t) in t2.items()}
+            # the two chains per group: the side streams' FPS / binning / queries (3 streams) and the
+            # main stream's MLP kernels, from the per-launch HIP-event durations of the second window
+            side_k = [k for k in pl2 if k.endswith("_fps") or "_bq_bin" in k or "_ball_query" in k]
             extras[key] = {"M_points_per_s": sharding.aggregate_rate(b2 * n2 * st2, world, el2) / 1e6,
                            "ms_per_step": el2 / st2 * 1e3, "frames_per_gpu": b2, "points_per_frame": n2,
-                           "dtype": dtype, "batches_per_group": g2,
-                           "kernel_ms_per_launch": {k: t / c for k, (c, f, t) in t2.items()}}
+                           "dtype": dtype, "batches_per_group": g2, "side_query_ns": sq,
+                           "chains_ms_per_group": {"main": sum(v for k, v in pl2.items() if k not in side_k),
+                                                   "side": sum(pl2[k] for k in side_k) / 3,
+                                                   "step_ms_per_group": el2 / st2 * 1e3 * g2},
+                           "kernel_ms_per_launch": pl2}
             mw = stack_mfma_work(cfg, n2)
             mk = {k: v for k, v in t2.items() if k in mw}
             if mk:
@@ -971,7 +992,7 @@ def main():
             "pipeline": {"executor": "pointnet2.StreamingSSG feed (steady state: the window pushes and completes "
                                      "exactly `steps` batches; pipeline fill and drain outside it)",
                          "side_streams": args.depth, "batches_per_group": G, "frames_per_launch": G * B,
-                         "fps_threads": args.fps_threads, "fps_lazy": bool(args.fps_lazy),
+                         "fps_threads": args.fps_threads,
                          "sa1_ball_queries": args.bq, **chains},
             "fp32_mfma_kernels": fp32_mfma,
             "other_configs": extras,

@@ -50,15 +50,8 @@ int lidar_reserve(lidar_handle *h, uint64_t bytes);
 /* free the workspaces retired by growth (*freed = their bytes, may be NULL); the caller guarantees
  * that the work it queued with this handle before the growth has completed */
 int lidar_trim(lidar_handle *h, uint64_t *freed);
-/* testing aid: grow the workspace to `bytes` and fill it with tag-like garbage (high halves 1..64) on
- * `stream` — the library never trusts what an earlier call left in the workspace */
-int lidar_debug_fill_workspace(lidar_handle *h, uint64_t bytes, uint64_t seed, void *stream);
-/* testing aid: set the handle's call epoch (the tag of the voxel calls' in-launch hand-offs; the next
- * call takes epoch + 1, and at the wrap the tag block is zeroed again) */
-int lidar_debug_set_epoch(lidar_handle *h, uint32_t epoch);
-
 const char *lidar_last_error(void);
-int lidar_version(void); /* 4 (what changed per version) */
+int lidar_version(void); /* 5 (what changed per version) */
 
 /* Per-phase timing of a handle's launches (bench.py's in-window kernel durations): with
  * lidar_profile(h, 1) every kernel phase issued on h is bracketed by two HIP events on its
@@ -90,10 +83,7 @@ int lidar_fps_f32(lidar_handle *h, const float *xyz, int64_t batch, int64_t n, i
                   void *stream);
 /* the same with an explicit workgroup size per frame: threads 0 (default, 1024), 1024 or 512.
  * 512 takes ~25 % longer per step and half the CU footprint (throughput pipelines that run
- * other kernels beside FPS).  threads | LIDAR_FPS_LAZY (ABI v4): lazy bucket refresh — a bucket
- * hit by a sample defers it in a pending list until its key could reach the frame maximum
- * (DESIGN.md §4.3): ~2.3x less memory traffic, ~20 % longer steps.  Identical results. */
-#define LIDAR_FPS_LAZY 0x10000
+ * other kernels beside FPS).  Identical results. */
 int lidar_fps_ex_f32(lidar_handle *h, const float *xyz, int64_t batch, int64_t n, int64_t npoint,
                      int32_t *idx, float *new_xyz, int32_t *first_zero, const int32_t *prefix_ok,
                      int32_t threads, void *stream);
@@ -277,7 +267,8 @@ int lidar_voxel_downsample_f32(lidar_handle *h, const float *xyz, int64_t n, dou
 /* Voxel downsampling of `batch` frames of n points over the whole chip (csrc/voxel_batch.hip):
  * xyz (batch, n, 3) fp32; voxel_id (batch, n) int32; centroids (batch, n, 3) and counts (batch, n),
  * the first nvox[f] rows of frame f valid; nvox (batch,) int32 on the device (-1: the frame's extent
- * is not finite or its grid has 2^32 keys or more; -2: a bounded in-launch wait timed out, a bug).  No host
+ * is not finite or its grid has 2^32 keys or more; library bugs, never expected, and sticky — they win over
+ * the count: -2 a bounded in-launch wait timed out, -3 an inconsistent bucket table).  No host
  * synchronisation; per frame equal to lidar_voxel_downsample_f32.  Workspace:
  * lidar_voxel_batch_workspace_bytes(batch, n), plus the handle's own voxel tag block (the in-launch
  * hand-offs' epoch-tagged granules, 8 KiB per 8 192-point tile; grown and zeroed on demand, written by

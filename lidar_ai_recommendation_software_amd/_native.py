@@ -42,8 +42,6 @@ SIGNATURES = {
     "lidar_destroy": [P],
     "lidar_reserve": [P, ctypes.c_uint64],
     "lidar_trim": [P, P],
-    "lidar_debug_fill_workspace": [P, ctypes.c_uint64, ctypes.c_uint64, P],
-    "lidar_debug_set_epoch": [P, ctypes.c_uint32],
     "lidar_last_error": [],
     "lidar_version": [],
     "lidar_profile": [P, I32],

@@ -551,441 +551,12 @@ __global__ __launch_bounds__(T) void fps_bucket_kernel(const float *__restrict__
     }
 }
 
-// ------------------------------------------------------------------------------------------------
-// Lazy bucket refresh (round 5).  The eager kernel above streams every bucket whose box lower bound
-// lb(q) is below its max at every step (~21 of 1 024 buckets of a 65 536-point frame).  Here a
-// bucket hit by q (lb < its key) only records q in a short pending list (kCap sample ids: u16
-// slots of an LDS ring of the recent samples); its key becomes an UPPER bound of its max.  A stale
-// bucket is refreshed — one load of its 64 points, every pending sample and q applied, exact max
-// and argmax recomputed — only when its upper bound reaches L_w, the largest exact key among the
-// wave's buckets q did not hit (a lower bound of the new frame maximum: a bucket left stale has
-// key < L_w <= the frame max, so it can neither hold nor tie the argmax), when its list is full,
-// or when its oldest pending sample is about to leave the ring.  dist(p) = min over samples of
-// d(p, s) is order-free, so every dist, every key and every argmax equals the eager kernel's:
-// bit-exact by construction.  tools/fps_lazy_sim.py: ~7 bucket loads per step instead of ~21.
-//
-// Registers per bucket slot: the box (6), the key (1) and bk = argmax lane | pending count << 8 (1).
-// LDS: the argmax point of every bucket (x, y, z, original index), its pending ids, the ring.
-constexpr int kRing = 512;  // samples kept in LDS for pending lists (16 B each: 8 KiB)
-constexpr int kCap = 4;     // pending samples per bucket (u16 ids)
-#ifndef FPS_LAZY_K
-#define FPS_LAZY_K 2
-#endif
-#ifndef FPS_LAZY_WAVEL
-#define FPS_LAZY_WAVEL 0
-#endif
-
-template <int T, int BPL>
-struct LazyLds {
-    float4 arg[BPL][T];          // argmax point of the bucket owned by (slot, thread): x, y, z, index bits
-    uint16_t pend[kCap][BPL][T]; // pending sample ids (ring slots mod 2^16), oldest first
-    float4 ring[kRing];          // the last kRing samples
-};
-
-// Refresh up to K buckets of the wave taken from the per-slot masks m[] (slot 0 first): their loads
-// issued together (one memory round trip), then q and every pending sample applied, the changed
-// dists stored, the key and argmax point recomputed (skipped when the argmax member did not get
-// closer).  Clears the buckets' pending lists.
-template <int K, int T, int BPL>
-__device__ __forceinline__ void refresh_batch(uint64_t *m, const FrameWs &W, LazyLds<T, BPL> &L, int wave, int lane,
-                                              float qx, float qy, float qz, float *bd, uint32_t *bk, int w_q,
-                                              int w_lane, int w_db, bool &hit)
-{
-    constexpr int NW = T / 64;
-    int bq[K], bl[K];  // slot and owner lane of entry u (wave-uniform; bl = -1: no entry)
-    uint32_t pos[K];
-#pragma unroll
-    for (int u = 0; u < K; ++u) {
-        bq[u] = 0;
-        bl[u] = -1;
-#pragma unroll
-        for (int q = BPL - 1; q >= 0; --q)
-            if (m[q]) bq[u] = q;
-#pragma unroll
-        for (int q = 0; q < BPL; ++q)
-            if (q == bq[u] && m[q]) {
-                bl[u] = __ffsll((unsigned long long)m[q]) - 1;
-                m[q] &= m[q] - 1;
-            }
-        // an empty entry re-reads entry 0's bucket (harmless, never applied)
-        const int qq = bl[u] < 0 ? bq[0] : bq[u], ll = bl[u] < 0 ? bl[0] : bl[u];
-        pos[u] = (uint32_t)((wave + NW * (qq * 64 + ll)) * 64 + lane);
-    }
-    float4 P[K];
-    float D[K];
-#pragma unroll
-    for (int u = 0; u < K; ++u) {
-        P[u] = W.p[pos[u]];
-        D[u] = W.d[pos[u]];
-    }
-    // pending samples of all K buckets in one pair of LDS round trips (overlapping the loads above):
-    // lane 4u + j reads bucket u's j-th pending id, then that sample's coordinates
-    uint32_t bkv[K];  // the owner lane's bk of entry u (argmax lane | pending count << 8)
-#pragma unroll
-    for (int u = 0; u < K; ++u) {
-        uint32_t bkq = bk[0];
-#pragma unroll
-        for (int q = 1; q < BPL; ++q) bkq = bq[u] == q ? bk[q] : bkq;
-        bkv[u] = bl[u] < 0 ? 0u : (uint32_t)__builtin_amdgcn_readlane((int)bkq, max(bl[u], 0));
-    }
-    float4 smp = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    {
-        const int u = lane >> 2, j = lane & 3;
-        int qq = bq[0], ll = bl[0];
-        uint32_t cu = bkv[0];
-#pragma unroll
-        for (int v = 1; v < K; ++v)
-            if (u == v) {
-                qq = bq[v];
-                ll = bl[v];
-                cu = bkv[v];
-            }
-        if (u < K && (uint32_t)j < ((cu >> 8) & 0xffu)) smp = L.ring[L.pend[j][qq][wave * 64 + ll] % kRing];
-    }
-    int od[K];
-    bool redo[K];
-#pragma unroll
-    for (int u = 0; u < K; ++u) {
-        redo[u] = false;
-        if (bl[u] < 0) continue;  // wave-uniform
-        const uint32_t bku = bkv[u];
-        int mm = __float_as_int(lidar::dist2f(P[u].x, P[u].y, P[u].z, qx, qy, qz)) & 0x7fffffff;
-        const uint32_t npend = (bku >> 8) & 0xffu;
-#pragma unroll
-        for (int j = 0; j < kCap; ++j) {
-            if ((uint32_t)j >= npend) break;  // wave-uniform
-            const float sx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(smp.x), 4 * u + j));
-            const float sy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(smp.y), 4 * u + j));
-            const float sz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(smp.z), 4 * u + j));
-            mm = min(mm, __float_as_int(lidar::dist2f(P[u].x, P[u].y, P[u].z, sx, sy, sz)) & 0x7fffffff);
-        }
-        od[u] = min(mm, __float_as_int(D[u]));
-        const bool lower = od[u] != __float_as_int(D[u]);
-        if (lower) W.d[pos[u]] = __int_as_float(od[u]);
-        const uint64_t ch = __ballot(lower);
-        const uint32_t bpu = bku & 0xffu;  // 0xff: argmax member unknown
-        redo[u] = bpu == 0xffu || ((ch >> bpu) & 1ull);
-        if (npend > 0 && !redo[u]) {
-            // a stale bucket whose argmax member stands: its key is exact again and joins the wave's
-            // exact set — the candidate (max over that set) is recounted if it may be overtaken
-            float bdq = bd[0];
-#pragma unroll
-            for (int q = 1; q < BPL; ++q) bdq = bq[u] == q ? bd[q] : bdq;
-            hit = hit || __builtin_amdgcn_readlane(__float_as_int(bdq), bl[u]) >= w_db;
-        }
-        if (lane == bl[u]) {  // pending list applied
-#pragma unroll
-            for (int q = 0; q < BPL; ++q)
-                if (q == bq[u]) bk[q] = bpu;
-        }
-    }
-#pragma unroll
-    for (int u = 0; u < K; ++u) {
-        if (!redo[u]) continue;  // wave-uniform: the exact key stands
-        const int dm = lidar::wave_max_i32_dpp(od[u]);
-        // the candidate is recounted when its bucket changed or when this key may overtake it (a
-        // bucket that was stale is not part of the candidate's exact set)
-        hit = hit || (bq[u] == w_q && bl[u] == w_lane) || dm >= w_db;
-        const uint64_t c = __ballot(od[u] == dm);
-        int wl;
-        const uint32_t I = __float_as_uint(P[u].w);
-        if (__popcll(c) == 1) {
-            wl = __ffsll((unsigned long long)c) - 1;
-        } else {
-            const uint32_t mi = lidar::wave_min_u32_dpp(od[u] == dm ? I : 0xffffffffu);
-            wl = __ffsll((unsigned long long)__ballot(od[u] == dm && I == mi)) - 1;
-        }
-        if (lane == bl[u]) {  // the owner lane takes the key, the argmax member's lane its point
-#pragma unroll
-            for (int q = 0; q < BPL; ++q)
-                if (q == bq[u]) {
-                    bd[q] = __int_as_float(dm);
-                    bk[q] = (uint32_t)wl;
-                }
-        }
-        if (lane == wl) L.arg[bq[u]][wave * 64 + bl[u]] = make_float4(P[u].x, P[u].y, P[u].z, P[u].w);
-    }
-}
-
-// DIAG builds (lidar_diag_fps_lazy_phases only) accumulate per-wave shader cycles per phase: [0] tests, L
-// and deferrals, [1] refresh batches, [2] candidate recount + publish, [3] barrier wait, [4] merge;
-// counts: [5] refresh batches, [6] recounts, [7] steps
-template <int T, int BPL, bool DIAG = false>
-__global__ __launch_bounds__(T) void fps_lazy_kernel(const float *__restrict__ xyz, int n, int npoint,
-                                                     int32_t *__restrict__ out_idx, float *__restrict__ out_xyz,
-                                                     int32_t *__restrict__ first_zero,
-                                                     const int32_t *__restrict__ prefix_ok, float *__restrict__ ws,
-                                                     int64_t ws_stride, uint64_t *__restrict__ diag = nullptr)
-{
-    uint64_t dacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    uint64_t t0 = 0, t1 = 0;
-#define LZ_STAMP(k)                                  \
-    if constexpr (DIAG) {                            \
-        __builtin_amdgcn_sched_barrier(0);           \
-        t1 = stamp();                                \
-        dacc[k] += t1 - t0;                          \
-        t0 = t1;                                     \
-        __builtin_amdgcn_sched_barrier(0);           \
-    }
-    constexpr int NW = T / 64;
-    const int b = blockIdx.x;
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = tid >> 6;
-    const float *p = xyz + (int64_t)b * n * 3;
-
-    if (prefix_ok != nullptr && prefix_ok[b] >= npoint) {  // nested FPS shortcut
-        for (int i = tid; i < npoint; i += T) {
-            out_idx[(int64_t)b * npoint + i] = i;
-            if (out_xyz) {
-                float *o = out_xyz + ((int64_t)b * npoint + i) * 3;
-                o[0] = p[3 * i];
-                o[1] = p[3 * i + 1];
-                o[2] = p[3 * i + 2];
-            }
-        }
-        if (first_zero && tid == 0) first_zero[b] = prefix_ok[b];
-        return;
-    }
-
-    float *wsb = ws + (int64_t)b * ws_stride;
-    const int npad = (n + 63) / 64 * 64;
-    FrameWs W{reinterpret_cast<float4 *>(wsb), wsb + 4 * (int64_t)npad};
-
-    // the prologue's histogram and the step loop's state share one LDS block
-    constexpr size_t kPro = kCells * 4, kState = sizeof(LazyLds<T, BPL>);
-    __shared__ __attribute__((aligned(16))) unsigned char smem[kPro > kState ? kPro : kState];
-    __shared__ float red[6][NW];
-    __shared__ uint32_t wsum[NW];
-    __shared__ unsigned long long mkey[3];
-    __shared__ __attribute__((aligned(16))) float mcrd[2][NW][4];
-    uint32_t *hist = reinterpret_cast<uint32_t *>(smem);
-    LazyLds<T, BPL> &L = *reinterpret_cast<LazyLds<T, BPL> *>(smem);
-
-    fps_prologue<T>(p, n, npad, W, hist, red, wsum);
-    const int nb = (n + 63) / 64;
-    float bmin[BPL][3], bmax[BPL][3], bd[BPL];
-    uint32_t bk[BPL];  // argmax lane (low byte, 0xff unknown) | pending count << 8 | oldest pending id << 16
-#pragma unroll
-    for (int q = 0; q < BPL; ++q)
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            bmin[q][a] = INFINITY;
-            bmax[q][a] = -INFINITY;
-        }
-    float *tab = reinterpret_cast<float *>(hist);
-    for (int p0 = 0; p0 < nb; p0 += 512) {
-        for (int bucket = p0 + wave; bucket < nb && bucket < p0 + 512; bucket += NW) {
-            const int pos = bucket * 64 + lane;
-            float v[3] = {INFINITY, INFINITY, INFINITY}, u[3] = {-INFINITY, -INFINITY, -INFINITY};
-            if (pos < n) {
-                const float4 P = W.p[pos];
-                v[0] = u[0] = P.x;
-                v[1] = u[1] = P.y;
-                v[2] = u[2] = P.z;
-            }
-#pragma unroll
-            for (int a = 0; a < 3; ++a) {
-                v[a] = lidar::wave_min_f(v[a]);
-                u[a] = lidar::wave_max_f(u[a]);
-            }
-            if (lane == 0) {
-#pragma unroll
-                for (int a = 0; a < 3; ++a) {
-                    tab[(bucket - p0) * 6 + a] = v[a];
-                    tab[(bucket - p0) * 6 + 3 + a] = u[a];
-                }
-            }
-        }
-        __syncthreads();
-#pragma unroll
-        for (int q = 0; q < BPL; ++q) {
-            const int bucket = wave + NW * (q * 64 + lane);
-            if (bucket >= p0 && bucket < p0 + 512 && bucket < nb)
-#pragma unroll
-                for (int a = 0; a < 3; ++a) {
-                    bmin[q][a] = tab[(bucket - p0) * 6 + a];
-                    bmax[q][a] = tab[(bucket - p0) * 6 + 3 + a];
-                }
-        }
-        __syncthreads();
-    }
-    // (the last barrier above: the table is dead, L may overwrite it)
-#pragma unroll
-    for (int q = 0; q < BPL; ++q) {
-        const int bucket = wave + NW * (q * 64 + lane);
-        const bool have = bucket < nb;
-        bk[q] = 0xffu;
-        bd[q] = have ? INFINITY : 0.0f;  // empty slot: never hit, never the argmax
-        L.arg[q][tid] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(have ? 0u : 0xffffffffu));
-    }
-
-    float qx = p[0], qy = p[1], qz = p[2];
-    if (tid == 0) {
-        out_idx[(int64_t)b * npoint] = 0;
-        if (out_xyz) {
-            float *o = out_xyz + (int64_t)b * npoint * 3;
-            o[0] = qx;
-            o[1] = qy;
-            o[2] = qz;
-        }
-        L.ring[0] = make_float4(qx, qy, qz, 0.0f);
-    }
-    int zero_at = npoint;
-    float w_d = 0.0f, w_x = 0.0f, w_y = 0.0f, w_z = 0.0f;
-    uint32_t w_i = 0xffffffffu;
-    if (tid < 3) mkey[tid] = 0ull;
-    __syncthreads();
-    int cur3 = 1, nxt3 = 2;
-    int w_q = 0, w_lane = 0;
-    int lg = -1;  // this lane's L_g term: no candidates before the first merge
-    if constexpr (DIAG) t0 = stamp();
-    for (int it = 1; it < npoint; ++it) {
-        bool wave_dirty = it == 1;
-        const uint32_t qid = (uint32_t)(it - 1) & 0xffffu;  // q = sample it-1, in ring slot qid % kRing
-        // hits, and L_w = the largest exact key among the wave's buckets q does not hit; with L_g (the
-        // previous step's wave candidates brought up to date against q, computed after the merge) a
-        // lower bound of the new frame maximum
-        bool hitq[BPL];
-        int lw = -1;
-#pragma unroll
-        for (int q = 0; q < BPL; ++q) {
-            const float gx = gap(qx, bmin[q][0], bmax[q][0]);
-            const float gy = gap(qy, bmin[q][1], bmax[q][1]);
-            const float gz = gap(qz, bmin[q][2], bmax[q][2]);
-            const float lb = __fadd_rn(__fadd_rn(__fmul_rn(gx, gx), __fmul_rn(gy, gy)), __fmul_rn(gz, gz));
-            hitq[q] = lb < bd[q];
-            if (!hitq[q] && bk[q] < 0x100u) lw = max(lw, __float_as_int(bd[q]));
-        }
-#if FPS_LAZY_WAVEL
-        lw = max(lidar::wave_max_i32_dpp(lw), lg);  // lg: the candidates' bound (uniform)
-#else
-        lw = max(lw, lg);  // this lane's own exact keys and the candidates' bound: no cross-lane step
-#endif
-        uint64_t need_m[BPL];
-#pragma unroll
-        for (int q = 0; q < BPL; ++q) {
-            const uint32_t pc = (bk[q] >> 8) & 0xffu;
-            const uint32_t npend = pc + (hitq[q] ? 1u : 0u);
-            // the oldest pending sample must be applied before its ring slot is reused
-            const uint32_t age = pc > 0 ? (qid - (bk[q] >> 16)) & 0xffffu : 0u;
-            const bool need = npend > 0 && (__float_as_int(bd[q]) >= lw || npend > (uint32_t)kCap ||
-                                            age >= (uint32_t)(kRing - 2));
-            need_m[q] = __ballot(need);
-            const bool defer = hitq[q] && !need;
-            if (defer) {  // q joins the pending list
-                L.pend[pc][q][tid] = (uint16_t)qid;
-                bk[q] = pc == 0 ? ((bk[q] & 0xffu) | 0x100u | (qid << 16)) : bk[q] + 0x100u;
-            }
-            // the wave's candidate must stay exact (L_g reads it): a deferred argmax bucket is recounted
-            if (q == w_q && ((__ballot(defer) >> w_lane) & 1ull)) wave_dirty = true;
-        }
-        LZ_STAMP(0)
-        for (;;) {  // wave-uniform
-            bool any = false;
-#pragma unroll
-            for (int q = 0; q < BPL; ++q) any = any || need_m[q] != 0;
-            if (!any) break;
-            if constexpr (DIAG) dacc[5]++;
-            refresh_batch<FPS_LAZY_K, T, BPL>(need_m, W, L, wave, lane, qx, qy, qz, bd, bk, w_q, w_lane,
-                                              __float_as_int(w_d), wave_dirty);
-        }
-        LZ_STAMP(1)
-        if (wave_dirty) {  // the wave argmax over its EXACT buckets (stale keys are < L <= the frame max)
-            if constexpr (DIAG) dacc[6]++;
-            float4 a = L.arg[0][tid];
-            int best = bk[0] < 0x100u ? __float_as_int(bd[0]) : -1;
-            uint32_t besti = bk[0] < 0x100u ? __float_as_uint(a.w) : 0xffffffffu;
-            int bq = 0;
-#pragma unroll
-            for (int q = 1; q < BPL; ++q) {
-                const float4 aq = L.arg[q][tid];
-                const int dq = bk[q] < 0x100u ? __float_as_int(bd[q]) : -1;
-                const uint32_t iq = bk[q] < 0x100u ? __float_as_uint(aq.w) : 0xffffffffu;
-                if (dq > best || (dq == best && iq < besti)) {
-                    best = dq;
-                    besti = iq;
-                    a = aq;
-                    bq = q;
-                }
-            }
-            int wdb;
-            const int wl = lidar::wave_argmax_lane_i32(best, besti, &wdb);
-            // a wave whose buckets are all stale (their keys below L) offers (0, no index): never the winner
-            w_d = wdb < 0 ? 0.0f : __int_as_float(wdb);
-            w_i = wdb < 0 ? 0xffffffffu : (uint32_t)__builtin_amdgcn_readlane((int)besti, wl);
-            w_x = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(a.x), wl));
-            w_y = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(a.y), wl));
-            w_z = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(a.z), wl));
-            w_lane = wl;
-            w_q = BPL > 1 ? __builtin_amdgcn_readlane(bq, wl) : 0;
-        }
-        const int slot = cur3, cslot = it & 1;
-        if (lane == 0) {
-            const uint32_t fld = w_i < (1u << 27) ? (1u << 27) - w_i : 0u;
-            const unsigned long long key =
-                ((unsigned long long)__float_as_uint(w_d) << 32) | (fld << 4) | (uint32_t)wave;
-            mcrd[cslot][wave][0] = w_x;
-            mcrd[cslot][wave][1] = w_y;
-            mcrd[cslot][wave][2] = w_z;
-            mcrd[cslot][wave][3] = w_d;
-            atomicMax(&mkey[slot], key);
-        }
-        if (tid == 0) mkey[nxt3] = 0ull;
-        LZ_STAMP(2)
-        __syncthreads();
-        LZ_STAMP(3)
-        {
-            const unsigned long long key = mkey[slot];
-            float4 cand = make_float4(0.0f, 0.0f, 0.0f, -1.0f);
-            if (lane < NW) cand = *reinterpret_cast<const float4 *>(mcrd[cslot][lane]);
-            const int ww = __builtin_amdgcn_readfirstlane((int)(key & 15u));
-            const float gdist = __uint_as_float((uint32_t)(key >> 32));
-            const uint32_t gidx = (1u << 27) - (((uint32_t)key) >> 4);
-            qx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cand.x), ww));
-            qy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cand.y), ww));
-            qz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cand.z), ww));
-            // L_g for the next step: every wave's candidate is a point whose dist was exactly cand.w;
-            // after q it is min(cand.w, d(cand, q)) — a point's exact dist, so their max is a lower
-            // bound of the next frame maximum (the winner's own candidate gives 0)
-            const int cd = __float_as_int(lidar::dist2f(cand.x, cand.y, cand.z, qx, qy, qz)) & 0x7fffffff;
-            const int lgl = lane < NW ? min(__float_as_int(cand.w), cd) : -1;
-            lg = __builtin_amdgcn_readfirstlane(lgl);
-#pragma unroll
-            for (int w = 1; w < NW; ++w) lg = max(lg, __builtin_amdgcn_readlane(lgl, w));
-            if (tid == 0) {
-                out_idx[(int64_t)b * npoint + it] = (int32_t)gidx;
-                if (out_xyz) {
-                    float *o = out_xyz + ((int64_t)b * npoint + it) * 3;
-                    o[0] = qx;
-                    o[1] = qy;
-                    o[2] = qz;
-                }
-                // sample `it` into its ring slot: read from the next step on (after a barrier),
-                // never while a pending id still names the sample it replaces (the age rule)
-                L.ring[it % kRing] = make_float4(qx, qy, qz, 0.0f);
-            }
-            if (zero_at == npoint && gdist == 0.0f) zero_at = it;
-        }
-        cur3 = nxt3;
-        nxt3 = nxt3 == 2 ? 0 : nxt3 + 1;
-        LZ_STAMP(4)
-        if constexpr (DIAG) dacc[7]++;
-    }
-    if (first_zero && tid == 0) first_zero[b] = zero_at;
-    if constexpr (DIAG) {
-        if (lane == 0)
-            for (int k = 0; k < 8; ++k) diag[((int64_t)b * NW + wave) * 8 + k] = dacc[k];
-    }
-#undef LZ_STAMP
-}
 
 }  // namespace
 
 template <int T>
 static int launch_fps(const float *xyz, int64_t batch, int64_t n, int64_t npoint, int32_t *idx, float *new_xyz,
-                      int32_t *first_zero, const int32_t *prefix_ok, float *ws, int64_t stride, bool lazy,
-                      hipStream_t s)
+                      int32_t *first_zero, const int32_t *prefix_ok, float *ws, int64_t stride, hipStream_t s)
 {
     dim3 grid((unsigned)batch), block(T);
     const int nb = (int)((n + 63) / 64);
@@ -996,7 +567,7 @@ static int launch_fps(const float *xyz, int64_t batch, int64_t n, int64_t npoint
     };
     if (n > kMaxBucketPoints) {
         // large frames: 8 bucket slots per lane at 512 threads, each bucket 64 x PPL points
-        // (lidar_fps_ex_f32 sends every n > kMaxBucketPoints here with T = 512, lazy off)
+        // (lidar_fps_ex_f32 sends every n > kMaxBucketPoints here with T = 512)
         if constexpr (T == 512) {
             const int64_t ppl = (n + kMaxBucketPoints - 1) / kMaxBucketPoints;
             if (ppl <= 2) go(fps_bucket_kernel<T, 8, false, 2>);
@@ -1004,11 +575,6 @@ static int launch_fps(const float *xyz, int64_t batch, int64_t n, int64_t npoint
             else if (ppl <= 8) go(fps_bucket_kernel<T, 8, false, 8>);
             else go(fps_bucket_kernel<T, 8, false, 16>);
         }
-    } else if (lazy) {
-        if (nb <= lanes) go(fps_lazy_kernel<T, 1>);
-        else if (nb <= 2 * lanes) go(fps_lazy_kernel<T, 2>);
-        else if (nb <= 4 * lanes) go(fps_lazy_kernel<T, 4>);
-        else go(fps_lazy_kernel<T, (T >= 1024 ? 4 : 8)>);  // unreachable for T = 1024 (n <= 4 * 65536)
     } else {
         if (nb <= lanes) go(fps_bucket_kernel<T, 1>);
         else if (nb <= 2 * lanes) go(fps_bucket_kernel<T, 2>);
@@ -1039,14 +605,9 @@ LIDAR_EXPORT int lidar_fps_ex_f32(lidar_handle *h, const float *xyz, int64_t bat
     REQUIRE(h && xyz && idx, "lidar_fps_f32: null pointer");
     REQUIRE(batch >= 0 && n >= 1 && npoint >= 1, "lidar_fps_f32: need n >= 1 and npoint >= 1");
     REQUIRE(n <= kMaxFpsPoints, "lidar_fps_f32: n > 4194304 points per frame");
-    bool lazy = (threads & LIDAR_FPS_LAZY) != 0;
-    threads &= ~LIDAR_FPS_LAZY;
     if (threads == 0) threads = kThreads;
-    REQUIRE(threads == 1024 || threads == 512, "lidar_fps_ex_f32: threads must be 0, 512 or 1024 (| LIDAR_FPS_LAZY)");
-    if (n > kMaxBucketPoints) {  // the large-frame kernel: 512 threads, eager
-        threads = 512;
-        lazy = false;
-    }
+    REQUIRE(threads == 1024 || threads == 512, "lidar_fps_ex_f32: threads must be 0, 512 or 1024");
+    if (n > kMaxBucketPoints) threads = 512;  // the large-frame kernel: 512 threads
     REQUIRE(n > kMaxBucketPoints || (n + 63) / 64 <= 8 * (int64_t)threads,
             "lidar_fps_f32: too many buckets for this workgroup size");
     REQUIRE(batch <= 0x7fffffff, "lidar_fps_f32: batch too large");
@@ -1058,8 +619,8 @@ LIDAR_EXPORT int lidar_fps_ex_f32(lidar_handle *h, const float *xyz, int64_t bat
     if (!ws) return LIDAR_ENOMEM;
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (threads == 512)
-        return launch_fps<512>(xyz, batch, n, npoint, idx, new_xyz, first_zero, prefix_ok, ws, stride, lazy, s);
-    return launch_fps<1024>(xyz, batch, n, npoint, idx, new_xyz, first_zero, prefix_ok, ws, stride, lazy, s);
+        return launch_fps<512>(xyz, batch, n, npoint, idx, new_xyz, first_zero, prefix_ok, ws, stride, s);
+    return launch_fps<1024>(xyz, batch, n, npoint, idx, new_xyz, first_zero, prefix_ok, ws, stride, s);
 }
 
 LIDAR_EXPORT int lidar_fps_f32(lidar_handle *h, const float *xyz, int64_t batch, int64_t n, int64_t npoint,
@@ -1072,26 +633,6 @@ LIDAR_EXPORT int lidar_fps_f32(lidar_handle *h, const float *xyz, int64_t batch,
 #ifdef LIDAR_DIAG
 // diagnostic build only (`make diag`, not part of the product library or ABI): per-wave phase cycle
 // totals of one FPS run
-// per-wave phase cycles of the lazy kernel at 512 threads (BPL from n), diag[(frame * 8 + wave) * 8 + k]
-LIDAR_EXPORT int lidar_diag_fps_lazy_phases(lidar_handle *h, const float *xyz, int64_t batch, int64_t n,
-                                            int64_t npoint, int32_t *idx, uint64_t *diag, void *stream)
-{
-    REQUIRE(h && xyz && idx && diag && n <= 65536 && n >= 1 && npoint >= 1, "lidar_diag_fps_lazy_phases: bad args");
-    ON_DEVICE(h->device);
-    int64_t stride = lidar::align_up(5 * lidar::align_up(n, 64), 64);
-    float *ws = static_cast<float *>(lidar::workspace(h, (uint64_t)(batch * stride) * 4));
-    if (!ws) return LIDAR_ENOMEM;
-    const int nb = (int)((n + 63) / 64);
-    auto go = [&](auto kern) {
-        hipLaunchKernelGGL(kern, dim3((unsigned)batch), dim3(512), 0, static_cast<hipStream_t>(stream), xyz, (int)n,
-                           (int)npoint, idx, nullptr, nullptr, nullptr, ws, stride, diag);
-    };
-    if (nb <= 512) go(fps_lazy_kernel<512, 1, true>);
-    else go(fps_lazy_kernel<512, 2, true>);
-    LAUNCH_CHECK();
-    return LIDAR_OK;
-}
-
 // the eager kernel's phases at 512 threads (BPL from n), diag[(frame * 8 + wave) * 6 + k]
 LIDAR_EXPORT int lidar_diag_fps_eager512_phases(lidar_handle *h, const float *xyz, int64_t batch, int64_t n,
                                                 int64_t npoint, int32_t *idx, uint64_t *diag, void *stream)

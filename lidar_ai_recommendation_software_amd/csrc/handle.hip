@@ -52,7 +52,7 @@ static void drop_records(Prof *p)
 
 }  // namespace lidar
 
-LIDAR_EXPORT int lidar_version(void) { return 4; }
+LIDAR_EXPORT int lidar_version(void) { return 5; }
 
 LIDAR_EXPORT const char *lidar_last_error(void) { return lidar::g_err.c_str(); }
 
@@ -111,6 +111,8 @@ LIDAR_EXPORT int lidar_reserve(lidar_handle *h, uint64_t bytes)
     return LIDAR_OK;
 }
 
+#ifdef LIDAR_DIAG
+// testing aids: the diagnostic library only (`make diag`, liblidar_amd_diag.so), not the product ABI
 namespace {
 __global__ void fill_workspace_kernel(unsigned long long *w, uint64_t words, unsigned long long seed)
 {
@@ -143,6 +145,7 @@ LIDAR_EXPORT int lidar_debug_set_epoch(lidar_handle *h, uint32_t epoch)
     h->epoch = epoch;
     return LIDAR_OK;
 }
+#endif  // LIDAR_DIAG
 
 // Frees the workspaces retired by growth.  The caller guarantees that no work it queued with this
 // handle before the growth is still pending (e.g. after synchronising the streams it used).

@@ -33,6 +33,7 @@ LIDAR_EXPORT int lidar_voxel_downsample_f32(lidar_handle *h, const float *xyz, i
     if (rc != LIDAR_OK) return rc;
     HIP_TRY(hipStreamSynchronize(s));
     REQUIRE(hm[0] != -2, "lidar_voxel_downsample_f32: an in-launch hand-off timed out (a bug; please report)");
+    REQUIRE(hm[0] != -3, "lidar_voxel_downsample_f32: an inconsistent voxel bucket table (a bug; please report)");
     REQUIRE(hm[0] >= 0, "lidar_voxel_downsample_f32: the extent is not finite or the voxel grid has 2^32 keys or more");
     *nvox_host = hm[0];
     return LIDAR_OK;

@@ -61,6 +61,7 @@ constexpr int SEGMAX = 128;        // longest equal-key run the counting sort or
 constexpr int BUCKET = 2048;       // target points per bucket (32 x 65 536 points: 1 024 buckets, one round of
                                    // four workgroups per CU)
 constexpr int MW = 8;              // meta words per frame: [0] grid ok, [1] outside key, [2] hs, [3] hung tag
+                                   // (keys / scatter), [4] the bucket launch's failure tag, [5] its nvox code
 static_assert(NBIN % KT == 0 && NBIN % UT == 0, "bins per thread");
 
 __device__ __forceinline__ uint32_t ord(float f)  // monotone float -> u32
@@ -351,7 +352,7 @@ __global__ __launch_bounds__(KT) void vx_keys_kernel(const float *__restrict__ x
         // call's (self-contained: no fence; MI355X_MICROARCH.md R2).  A tile waits only on tiles of its
         // frame, which frame_part dispatches together, at most kFuseTiles of them (an XCD holds 32
         // workgroups of this launch; larger frames run vx_extent_kernel first); the spin is bounded (a
-        // frame whose tiles never all arrive reports a non-finite extent: nvox -1).
+        // frame whose tiles never all arrive sets the hung tag meta[3]: nvox -2).
         unsigned long long *gr = w.gran + (int64_t)f * ntiles * 6;
         publish_extent(q, n, t, gr, epoch, red6);
         VX_KSTAMP(1);
@@ -646,6 +647,32 @@ __device__ uint64_t look_back(unsigned long long *fl, int64_t b, uint32_t nv, bo
     return pre;
 }
 
+#ifdef LIDAR_DIAG
+__device__ int64_t g_vx_inject_bad = -1;  // the diagnostic library's failure injection (a bucket index)
+#endif
+
+// A bucket's outcome for nvox[f] (lane 0 of wave 0).  A failure — a look-back wait that timed out (hung:
+// nvox -2) or a bucket table that is not a partition of [0, n) (bad: nvox -3), both bugs upstream, never
+// expected — tags the frame's meta[4] with this call's epoch before it stores its code, and the frame's
+// last bucket reads that tag after its own look-back has completed.  A failed bucket ends its wait before
+// the predecessor it waited for publishes, and the last bucket's look-back needs that publication, so the
+// tag is set before the last bucket reads it: a failure always wins over the frame's voxel count (the
+// count alone, written by the last bucket, would look valid with ids and centroids at wrong offsets).
+__device__ __forceinline__ void bucket_report(int32_t *nvox, uint32_t *m, int64_t f, int64_t b, int64_t nb,
+                                              uint64_t total, bool hung, bool bad, uint32_t epoch)
+{
+    if (hung || bad) {
+        const uint32_t code = bad ? 3u : 2u;
+        __hip_atomic_store(&m[5], code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&m[4], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        nvox[f] = -(int32_t)code;
+    } else if (b == nb - 1) {
+        nvox[f] = __hip_atomic_load(&m[4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch
+                      ? -(int32_t)__hip_atomic_load(&m[5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                      : (int32_t)total;
+    }
+}
+
 // 34 KiB: four 512-thread workgroups per CU (at <= 64 VGPRs)
 struct BucketLds {
     union {
@@ -694,7 +721,7 @@ __global__ __launch_bounds__(UT, 8) void vx_bucket_kernel(const float *__restric
     // the bucket's pairs [bstart[b], bstart[b + 1]) (the scatter launch's bucket table), loaded beside the
     // frame's meta words
     const uint32_t bs = tid < 2 ? w.bstart[(int64_t)f * (nb + 1) + b + tid] : 0u;
-    const uint32_t *m = w.meta + (int64_t)f * MW;
+    uint32_t *m = w.meta + (int64_t)f * MW;
     if (!m[0] || m[3] == epoch) {
         if (b == 0 && tid == 0) nvox[f] = m[3] == epoch ? -2 : -1;
         return;  // every bucket of the frame returns: nothing waits on this frame's look-back words
@@ -709,13 +736,19 @@ __global__ __launch_bounds__(UT, 8) void vx_bucket_kernel(const float *__restric
     __shared__ uint32_t spins_dbg;
     if (tid == 0) spins_dbg = 0;
 #endif
-    if (tid < 2) rng[tid] = min(bs, (uint32_t)n);  // (defensive: <= n)
+    if (tid < 2) rng[tid] = bs;
     if (tid == 2) rng[2] = 0xffffffffu;  // [2], [3]: key min / max
     if (tid == 3) rng[3] = 0u;
     if (tid == 0) flag = 0;
     __syncthreads();
     VX_STAMP(1);
-    const int64_t p0 = rng[0], size = max<int64_t>(0, (int64_t)rng[1] - rng[0]);
+    // a bucket table that is not a partition of [0, n) is a bug upstream: the bucket sorts nothing (its
+    // count 0 still goes out, so the frame's later buckets do not wait on it) and reports nvox -3
+    bool bad = rng[0] > rng[1] || (int64_t)rng[1] > n;  // (uniform)
+#ifdef LIDAR_DIAG
+    bad = bad || b == g_vx_inject_bad;  // testing aid (lidar_debug_voxel_inject): this bucket's table is "bad"
+#endif
+    const int64_t p0 = bad ? 0 : rng[0], size = bad ? 0 : (int64_t)rng[1] - rng[0];
     const uint64_t *gp = w.pairs + (int64_t)f * n + p0;
     const float *p = xyz + (int64_t)f * n * 3;
     unsigned long long *fl = reinterpret_cast<unsigned long long *>(w.flags + (int64_t)f * nb);
@@ -943,8 +976,7 @@ __global__ __launch_bounds__(UT, 8) void vx_bucket_kernel(const float *__restric
 #endif
                 if (lane == 0) {
                     prefix = pre;
-                    if (hung) nvox[f] = -2;
-                    else if (b == nb - 1) nvox[f] = (int32_t)(pre + nvl);
+                    bucket_report(nvox, m, f, b, nb, pre + nvl, hung, bad, epoch);
                 }
             }
             __syncthreads();
@@ -1046,8 +1078,7 @@ __global__ __launch_bounds__(UT, 8) void vx_bucket_kernel(const float *__restric
             const uint64_t pre = look_back(fl, b, nvl, &hung);
             if (lane == 0) {
                 prefix = pre;
-                if (hung) nvox[f] = -2;
-                else if (b == nb - 1) nvox[f] = (int32_t)(pre + nvl);
+                bucket_report(nvox, m, f, b, nb, pre + nvl, hung, bad, epoch);
             }
         }
         __syncthreads();
@@ -1106,6 +1137,16 @@ __global__ __launch_bounds__(UT, 8) void vx_bucket_kernel(const float *__restric
 }
 
 }  // namespace
+
+#ifdef LIDAR_DIAG
+// testing aid (the diagnostic library only): the bucket launches that follow treat bucket `bucket` of every
+// frame as having an inconsistent bucket table (-1: none), so the sticky failure report can be tested
+LIDAR_EXPORT int lidar_debug_voxel_inject(int64_t bucket)
+{
+    const hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_vx_inject_bad), &bucket, sizeof(bucket));
+    return e == hipSuccess ? LIDAR_OK : lidar::fail(LIDAR_EHIP, "lidar_debug_voxel_inject: hipMemcpyToSymbol");
+}
+#endif
 
 // workspace bytes of lidar_voxel_downsample_batch_f32 for (batch, n) (the granules and meta words live in
 // the handle's own tag block, beside it)

@@ -378,7 +378,8 @@ def voxel_downsample(points, voxel_size):
     histogram2d's binning (searchsorted right, the last edge closed).  Summed over z, the
     counts are the reference's 2-D histogram of the points' (x, y) on its own edges.  Raises
     ValueError (as ``np.arange`` does) for a non-finite extent, or when the grid has 2^32 keys
-    or more."""
+    or more; a library failure (nvox <= -2: an in-launch wait timed out, or an inconsistent bucket
+    table) raises LidarError instead, naming it."""
     import torch
     from .pointnet2 import voxel_downsample_batch
     if not 0 < voxel_size < np.inf:
@@ -390,8 +391,8 @@ def voxel_downsample(points, voxel_size):
     # the chip-wide batched path with one frame (csrc/voxel_batch.hip; same results as the
     # single-workgroup lidar_voxel_downsample_f32)
     cent, vid, cnt, nv = voxel_downsample_batch(x[None].contiguous(), float(voxel_size))
-    v = int(nv[0].item())
-    if v < 0:
+    v = int(nv[0].item())  # (<= -2 raised LidarError inside voxel_downsample_batch)
+    if v == -1:
         raise ValueError("voxel_downsample: the extent is not finite or the voxel grid has 2^32 keys or more")
     return cent[0, :v].cpu().numpy(), vid[0].cpu().numpy(), cnt[0, :v].cpu().numpy()
 

@@ -21,6 +21,7 @@ import numpy as np
 import torch
 
 from . import _native as nat
+from .streams import side_streams
 
 
 class DensityStream:
@@ -30,7 +31,7 @@ class DensityStream:
             self.device = torch.device("cuda", torch.cuda.current_device())
         self.workers = workers
         self.grid_size = float(grid_size)
-        self._streams = [torch.cuda.Stream(device=self.device) for _ in range(workers)]
+        self._streams = side_streams(self.device, workers)
         self._bufs = [{} for _ in range(workers)]
         # one persistent host thread per lane: the library's handles (workspaces) are per thread,
         # so a lane keeps its handles from call to call instead of creating them per call
@@ -163,7 +164,7 @@ class DensityStream:
         out = [None] * len(batches)
         lanes = max(1, min(int(lanes), len(batches)))
         caller = torch.cuda.current_stream(self.device)
-        streams = [torch.cuda.Stream(device=self.device) for _ in range(lanes)]
+        streams = side_streams(self.device, lanes)
         for st in streams:
             st.wait_stream(caller)  # the frames exist on the caller's stream
 

@@ -17,6 +17,7 @@ import torch
 
 from .data_processing import _reference_shape_errors, load_lidar_data
 from .density_stream import DensityStream
+from .streams import side_streams
 
 
 class HostFrameFeed:
@@ -24,7 +25,7 @@ class HostFrameFeed:
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.batch = max(1, int(batch))
         self.ds = DensityStream(self.device, workers=1, grid_size=grid_size)
-        self.copy_stream = torch.cuda.Stream(device=self.device)
+        self.copy_stream = side_streams(self.device, 1)[0]
         self._pinned = [None, None]  # host staging, double-buffered
         self._dev = [None, None]
         self._pool = concurrent.futures.ThreadPoolExecutor(max_workers=1)

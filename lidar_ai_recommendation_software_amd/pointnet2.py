@@ -21,6 +21,7 @@ import numpy as np
 import torch
 
 from . import _native as nat
+from .streams import side_streams
 
 # ------------------------------------------------------------------ configs
 # BASELINE.json configs: C2 = one SA1 layer, C3 = 3-level SSG, C5 = 3-level MSG.
@@ -89,15 +90,12 @@ def _dev_check(*ts):
             raise ValueError("liblidar_amd operators take contiguous CUDA tensors")
 
 
-FPS_LAZY = 0x10000  # include/lidar_amd.h LIDAR_FPS_LAZY
-
-
 def farthest_point_sample(xyz, npoint, return_xyz=False, first_zero=None, prefix_ok=None, slot=0,
-                          out_idx=None, out_xyz=None, threads=0, lazy=False):
+                          out_idx=None, out_xyz=None, threads=0):
     """xyz (B, N, 3) float32 CUDA -> idx (B, npoint) int32 [, new_xyz (B, npoint, 3)].
 
-    threads: workgroup size per frame (0 = 1024, 512); lazy: the lazy-refresh kernel (same results,
-    less memory traffic, longer steps).  n <= 262144 points per frame.
+    threads: workgroup size per frame (0 = 1024, 512; frames above 262 144 points always take 512).
+    n <= 4 194 304 points per frame.
 
     first_zero: optional (B,) int32 output — first step whose winning distance was 0.
     prefix_ok: optional (B,) int32 — the parent run's first_zero when xyz is the parent's
@@ -113,18 +111,22 @@ def farthest_point_sample(xyz, npoint, return_xyz=False, first_zero=None, prefix
                                                                   device=xyz.device)
     nat.call("lidar_fps_ex_f32", nat.handle(xyz.device.index, slot), nat.ptr(xyz), B, N, npoint,
              nat.ptr(idx), nat.ptr(new_xyz), nat.ptr(first_zero), nat.ptr(prefix_ok),
-             int(threads) | (FPS_LAZY if lazy else 0), nat.stream_ptr())
+             int(threads), nat.stream_ptr())
     return (idx, new_xyz) if return_xyz else idx
 
 
-def voxel_downsample_batch(xyz, voxel, slot=0):
+def voxel_downsample_batch(xyz, voxel, slot=0, check=True):
     """Voxel downsampling of (B, N, 3) float32 CUDA frames on the whole chip
     (lidar_voxel_downsample_batch_f32; per frame equal to data_processing.voxel_downsample).
     Returns device tensors (centroids (B, N, 3), voxel_id (B, N) int32, counts (B, N) int32,
     nvox (B,) int32): the first nvox[f] centroid / count rows of frame f are valid; nvox -1 marks
-    a frame whose extent is not finite or whose voxel grid has 2^32 keys or more (-2: one of the
-    launch's bounded in-launch waits timed out — a bug, never expected).  Voxels are
-    calculate_grid_density's grid extended to z (data_processing.voxel_downsample)."""
+    a frame whose extent is not finite or whose voxel grid has 2^32 keys or more.  Voxels are
+    calculate_grid_density's grid extended to z (data_processing.voxel_downsample).
+
+    nvox <= -2 is a library failure, never expected: -2 one of the launch's bounded in-launch waits
+    timed out, -3 a bucket table that is not a partition of the frame.  check=True (default) reads
+    nvox back (a host synchronisation on the stream) and raises LidarError on either; check=False
+    leaves nvox on the device (throughput loops: check_voxel_counts(nvox) later)."""
     _dev_check(xyz)
     if xyz.dtype != torch.float32 or xyz.dim() != 3 or xyz.shape[2] != 3:
         raise ValueError("xyz must be (B, N, 3) float32")
@@ -137,7 +139,22 @@ def voxel_downsample_batch(xyz, voxel, slot=0):
     if B and N:
         nat.call("lidar_voxel_downsample_batch_f32", nat.handle(dev.index, slot), nat.ptr(xyz), B, N,
                  float(voxel), nat.ptr(vid), nat.ptr(cent), nat.ptr(cnt), nat.ptr(nvox), nat.stream_ptr())
+        if check:
+            check_voxel_counts(nvox)
     return cent, vid, cnt, nvox
+
+
+VOXEL_FAILURES = {-2: "an in-launch hand-off of the voxel launches timed out",
+                  -3: "a voxel bucket table is not a partition of its frame"}
+
+
+def check_voxel_counts(nvox):
+    """Raise LidarError if any frame's nvox reports a library failure (<= -2; reads nvox back)."""
+    bad = nvox[nvox <= -2]
+    if bad.numel():
+        code = int(bad.min().item())
+        raise nat.LidarError(f"voxel_downsample_batch: {VOXEL_FAILURES.get(code, 'unknown failure')} "
+                             f"(nvox {code} in {bad.numel()} frame(s); a library bug, please report)")
 
 
 BQ_MODES = {"auto": 0, "scan": 1, "grid": 2}
@@ -740,24 +757,27 @@ class PointNet2Backbone:
             gidxs = []
             for bi_, br in enumerate(lvl["branches"]):
                 tag = f"sa{li + 1}" + (f"_b{bi_}" if len(lvl["branches"]) > 1 else "")
+                # work done elsewhere for this branch (StreamingSSG's side streams): its ball-query
+                # indices, or the binning of its frames (None per branch: not done)
+                pb = pl["bq"][bi_] if pl.get("bq") is not None else None
+                pg = pl["grid"][bi_] if pl.get("grid") is not None else None
                 if "generic" in br:
-                    if pl.get("bq") is not None:
-                        gidx = pl["bq"][bi_]
+                    if pb is not None:
+                        gidx = pb
                     else:
-                        grid = pl["grid"][bi_] if pl.get("grid") is not None else None
                         gidx = _call(t, f"{tag}_ball_query", B, ball_query, br["r"], br["ns"], xyz, new_xyz,
-                                     grid=grid)
+                                     grid=pg)
                     gidxs.append(gidx)
                     _call(t, f"{tag}_group_mlp", B, sa_branch_generic, feats, lvl["cfeat"], xyz, new_xyz, gidx,
                           br["generic"], out, off)
                     off += br["widths"][-1]
                     continue
-                fused = pq is None and pl.get("bq") is None and (self.bf16 or "packed_x3" in br) and (
-                    pl.get("grid") is not None or N >= BQ_GRID_MIN_N)
+                fused = pq is None and pb is None and (self.bf16 or "packed_x3" in br) and (
+                    pg is not None or N >= BQ_GRID_MIN_N)
                 if fused:
                     # xyz level: the MLP kernel answers the ball queries from the frame's grid
-                    if pl.get("grid") is not None:
-                        grid = pl["grid"][bi_]
+                    if pg is not None:
+                        grid = pg
                     else:
                         grid = _call(t, f"{tag}_bq_bin", B, ball_query_bin, br["r"], br["ns"], xyz,
                                      self._grid_buffer(B, N, xyz.device))
@@ -769,11 +789,10 @@ class PointNet2Backbone:
                     gidxs.append(gidx)
                     off += br["widths"][-1]
                     continue
-                if pl.get("bq") is not None:
-                    gidx = pl["bq"][bi_]
+                if pb is not None:
+                    gidx = pb
                 else:
-                    grid = pl["grid"][bi_] if pl.get("grid") is not None else None
-                    gidx = _call(t, f"{tag}_ball_query", B, ball_query, br["r"], br["ns"], xyz, new_xyz, grid=grid)
+                    gidx = _call(t, f"{tag}_ball_query", B, ball_query, br["r"], br["ns"], xyz, new_xyz, grid=pg)
                 gidxs.append(gidx)
                 if self.bf16:
                     if pq is not None:
@@ -859,9 +878,9 @@ class StreamingSSG:
     state of a LiDAR stream) and ``flush()`` drains it.
     """
 
-    def __init__(self, backbone, batch, n, depth=1, fps_group=1, fps_threads=0, fps_lazy=False, side_priority=0,
+    def __init__(self, backbone, batch, n, depth=1, fps_group=1, fps_threads=0, side_priority=0,
                  ramp=True,
-                 reserve=True, keep_levels=False, slots=None, bq="bin", l2_side=False):
+                 reserve=True, keep_levels=False, slots=None, bq="bin", l2_side=False, side_query_ns=128):
         """fps_threads: SA1 FPS workgroup size (0 = 1024; 512: half the CU footprint beside the
         MLPs).  ramp: in run(), the first groups hold 1, 2, ... batches (a shorter pipeline fill).
         slots: staging slots (>= depth + 1; default depth + 3).  Group k's FPS reuses the slot of
@@ -872,12 +891,15 @@ class StreamingSSG:
         [ball-query idx per branch])) instead of the global feature alone.  l2_side: level 1's FPS
         (nested: the prefix shortcut over SA1's centroids) and ball queries depend only on SA1's
         FPS output, so they run on the side stream too (the main stream then runs only MLP work
-        and level 1's per-point layer 1)."""
+        and level 1's per-point layer 1).  side_query_ns: with bq="bin", a level-0 branch of at
+        least this many samples also answers its ball queries on the side stream (from the same
+        grid), and the main stream runs its MLP on the given indices (bit-identical): configs[4]'s
+        ns = 128 branch spent ~40 % of its fused kernel on the queries, in the main chain that bounds
+        the MSG pipeline, while its side streams had slack."""
         self.bb = backbone
         self.B, self.N, self.depth, self.G = batch, n, depth, max(1, int(fps_group))
         self.ramp = bool(ramp)
         self.fps_threads = int(fps_threads)
-        self.fps_lazy = bool(fps_lazy)  # SA1 FPS on the lazy-refresh kernel (same results)
         self.keep = bool(keep_levels)
         if bq not in ("side", "bin", "main"):
             raise ValueError("StreamingSSG: bq must be 'side', 'bin' or 'main'")
@@ -887,7 +909,9 @@ class StreamingSSG:
         self.M1 = max(1, n // lvl0["div"])
         # side_priority < 0 puts the latency-bound FPS chains ahead of the MLP waves in the
         # dispatcher (HIP stream priority); results do not depend on it
-        self.fps_streams = [torch.cuda.Stream(device=dev, priority=side_priority) for _ in range(depth)]
+        # the process's shared side streams: a pipeline created after another keeps its queues
+        # (streams.py: fresh streams can land on the main stream's hardware queue)
+        self.fps_streams = side_streams(dev, depth, priority=side_priority)
         nslot = depth + 3 if slots is None else int(slots)
         if nslot < depth + 1:
             raise ValueError("StreamingSSG: slots must be >= depth + 1")
@@ -898,8 +922,13 @@ class StreamingSSG:
         self.idx = [torch.empty((GB, self.M1), dtype=torch.int32, device=dev) for _ in range(nslot)]
         self.cxyz = [torch.empty((GB, self.M1, 3), dtype=torch.float32, device=dev) for _ in range(nslot)]
         self.fz = [torch.empty(GB, dtype=torch.int32, device=dev) for _ in range(nslot)]
-        self.gidx = [[torch.empty((GB, self.M1, br["ns"]), dtype=torch.int32, device=dev)
-                      for br in lvl0["branches"]] for _ in range(nslot)] if bq == "side" else None
+        # level-0 ball-query indices computed on the side streams: every branch with bq="side",
+        # the branches of >= side_query_ns samples with bq="bin" (None: the MLP kernel answers them)
+        self.side_q = [bq == "side" or (bq == "bin" and side_query_ns is not None and br["ns"] >= side_query_ns)
+                       for br in lvl0["branches"]]
+        self.gidx = [[torch.empty((GB, self.M1, br["ns"]), dtype=torch.int32, device=dev) if sq else None
+                      for br, sq in zip(lvl0["branches"], self.side_q)]
+                     for _ in range(nslot)] if any(self.side_q) else None
         self.grid = [[ball_query_grid_buffer(GB, n, dev) for br in lvl0["branches"]]
                      for _ in range(nslot)] if bq == "bin" else None
         lvl1 = backbone.levels[1] if len(backbone.levels) > 1 else None
@@ -944,8 +973,7 @@ class StreamingSSG:
             for xj in xs:  # read on this stream: keep the caller's buffers alive until then
                 xj.record_stream(fs)
             _call(t, "sa1_fps", g, farthest_point_sample, x, self.M1, return_xyz=True, first_zero=self.fz[slot][:g],
-                  slot=hs, out_idx=self.idx[slot][:g], out_xyz=self.cxyz[slot][:g], threads=self.fps_threads,
-                  lazy=self.fps_lazy)
+                  slot=hs, out_idx=self.idx[slot][:g], out_xyz=self.cxyz[slot][:g], threads=self.fps_threads)
             lvl0 = self.bb.levels[0]
             for bi_, br in enumerate(lvl0["branches"]):
                 tag = "sa1" + (f"_b{bi_}" if len(lvl0["branches"]) > 1 else "")
@@ -954,6 +982,9 @@ class StreamingSSG:
                           out=self.gidx[slot][bi_][:g], slot=hs)
                 elif self.bq == "bin":  # depends only on the points: the queries run on the main stream
                     _call(t, f"{tag}_bq_bin", g, ball_query_bin, br["r"], br["ns"], x, self.grid[slot][bi_], slot=hs)
+                    if self.side_q[bi_]:  # ... or here, from the same grid
+                        _call(t, f"{tag}_ball_query", g, ball_query, br["r"], br["ns"], x, self.cxyz[slot][:g],
+                              out=self.gidx[slot][bi_][:g], slot=hs, grid=self.grid[slot][bi_])
             if self.l2:
                 c1 = self.cxyz[slot][:g]
                 _call(t, "sa2_fps", g, farthest_point_sample, c1, self.M2, return_xyz=True,
@@ -975,14 +1006,15 @@ class StreamingSSG:
         B, g = self.B, len(xs) * self.B
         x = self.stage[slot][:g] if self.G > 1 else xs[0]
         lvl0 = [self.idx[slot][:g], self.cxyz[slot][:g], self.fz[slot][:g],
-                [gi[:g] for gi in self.gidx[slot]] if self.gidx is not None else None]
+                [gi[:g] if gi is not None else None for gi in self.gidx[slot]] if self.gidx is not None else None]
         pre2 = None
         if self.l2:
             pre2 = {"fps": (self.idx2[slot][:g], self.cxyz2[slot][:g], self.fz2[slot][:g]),
                     "bq": [gi[:g] for gi in self.gidx2[slot]]}
 
         if self.keep:  # the slot's buffers are reused by a later group
-            lvl0 = [a.clone() for a in lvl0[:3]] + [[gi.clone() for gi in lvl0[3]] if lvl0[3] is not None else None]
+            lvl0 = [a.clone() for a in lvl0[:3]] + [[gi.clone() if gi is not None else None for gi in lvl0[3]]
+                                                    if lvl0[3] is not None else None]
             if pre2 is not None:
                 pre2 = {"fps": tuple(a.clone() for a in pre2["fps"]), "bq": [gi.clone() for gi in pre2["bq"]]}
         out, levels = self.bb.forward_from_sa1_fps(x, *lvl0, keep_levels=self.keep,

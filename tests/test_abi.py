@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
 def test_abi_version_matches_integration_doc():
     # a host call (no GPU needed); INTEGRATION.md lists what changed in this version
     v = nat.load_library().lidar_version()
-    assert v == 4
+    assert v == 5
     assert f"### ABI version {v} (`lidar_version() == {v}`" in open(os.path.join(REPO, "INTEGRATION.md")).read()
 
 

@@ -121,17 +121,16 @@ def frames_for(kind, b, n, seed):
     ("grid", 1, 4096, 4096),
 ])
 @pytest.mark.parametrize("threads", [0, 512])
-@pytest.mark.parametrize("lazy", [False, True])
-def test_fps_bit_exact(cuda, kind, b, n, m, threads, lazy):
-    """threads 0 = the default 1 024-thread kernel, 512 = 8 waves per frame; lazy = the lazy-refresh
-    kernel; bit-exact indices and coordinates against the C oracle (incl. far-offset, zero-width,
-    non-finite and lattice frames; m up to n, so pending lists overflow and ring slots expire)."""
+def test_fps_bit_exact(cuda, kind, b, n, m, threads):
+    """threads 0 = the default 1 024-thread kernel, 512 = 8 waves per frame; bit-exact indices and
+    coordinates against the C oracle (incl. far-offset, zero-width, non-finite and lattice frames, m up to
+    n)."""
     x = frames_for(kind, b, n, 11)
     if threads and (n + 63) // 64 > 8 * threads:  # 8 buckets per lane at most
         with pytest.raises(LidarError, match="too many buckets"):
-            pn.farthest_point_sample(torch.from_numpy(x).to(cuda), m, threads=threads, lazy=lazy)
+            pn.farthest_point_sample(torch.from_numpy(x).to(cuda), m, threads=threads)
         return
-    idx, nx = pn.farthest_point_sample(torch.from_numpy(x).to(cuda), m, return_xyz=True, threads=threads, lazy=lazy)
+    idx, nx = pn.farthest_point_sample(torch.from_numpy(x).to(cuda), m, return_xyz=True, threads=threads)
     want = tier_n.fps(x, m)
     got = idx.cpu().numpy()
     assert np.array_equal(got, want), f"{(got != want).sum()} indices differ, first {np.argwhere(got != want)[:3]}"
@@ -621,6 +620,27 @@ def test_streaming_bench_policy_matches_forward(cuda, group, depth, threads, nb,
     assert len(got) == nb
     for a, b in zip(got, want):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("side_ns,dtype", [(None, "bf16"), (16, "bf16"), (32, "bf16"), (128, "bf16"), (16, "f32")])
+def test_streaming_side_queries_match_forward(cuda, side_ns, dtype):
+    """MSG (configs[4]'s branches ns 16 / 32 / 128): the level-0 branches of >= side_query_ns samples
+    answer their ball queries on the side streams from the binned grid, the main stream runs their
+    MLPs on the given indices, the others stay fused; bit-identical to forward() (fused everywhere),
+    indices included."""
+    bb = pn.PointNet2Backbone(pn.MSG, device=cuda, seed=6, dtype=dtype)
+    xs = [torch.from_numpy(unit_frames(2, 8192, 80 + s)).to(cuda) for s in range(5)]
+    want = [bb.forward(x, keep_levels=True) for x in xs]
+    got = pn.StreamingSSG(bb, 2, 8192, depth=2, fps_group=2, fps_threads=512, bq="bin", l2_side=True,
+                          keep_levels=True, side_query_ns=side_ns).run(xs)
+    torch.cuda.synchronize()
+    assert len(got) == len(xs)
+    for (g, lv), (wg, wlv) in zip(got, want):
+        assert torch.equal(g, wg)
+        for (nx, nf, ni, ngi), (wx, wf, wi, wgi) in zip(lv, wlv):
+            assert torch.equal(nf, wf) and torch.equal(ni, wi)
+            for a, b in zip(ngi, wgi):
+                assert a is not None and torch.equal(a, b)
 
 
 def test_streaming_feed_steady_state(cuda):

@@ -152,25 +152,77 @@ def test_voxel_keys_table_and_float64_paths(cuda, case):
     assert np.array_equal(c, wc), case
 
 
+class DiagVoxel:
+    """The diagnostic build (liblidar_amd_diag.so, `make diag`): the product library plus its testing aids
+    (lidar_debug_fill_workspace / _set_epoch / _voxel_inject), which the product ABI does not export.  It is
+    loaded beside the product library and keeps handles of its own, so the voxel calls below run the diag
+    build's copy of csrc/voxel_batch.hip (the same source)."""
+
+    _lib = None
+
+    def __init__(self, device=0):
+        import ctypes
+        from lidar_ai_recommendation_software_amd import _native as nat
+        if DiagVoxel._lib is None:
+            path = os.path.join(os.path.dirname(nat.__file__), "liblidar_amd_diag.so")
+            assert os.path.exists(path), "liblidar_amd_diag.so not built (__graft_entry__.build(): make diag)"
+            lib = ctypes.CDLL(path)
+            for name, at in nat.SIGNATURES.items():
+                fn = getattr(lib, name)
+                fn.argtypes = at
+                fn.restype = nat._RESTYPES.get(name, ctypes.c_int)
+            lib.lidar_debug_fill_workspace.argtypes = [nat.P, ctypes.c_uint64, ctypes.c_uint64, nat.P]
+            lib.lidar_debug_set_epoch.argtypes = [nat.P, ctypes.c_uint32]
+            lib.lidar_debug_voxel_inject.argtypes = [ctypes.c_int64]
+            lib.lidar_last_error.restype = ctypes.c_char_p
+            DiagVoxel._lib = lib
+        self.lib, self.nat = DiagVoxel._lib, nat
+        hp = nat.P()
+        self.call("lidar_create", int(device), ctypes.byref(hp))
+        self.h = hp
+
+    def call(self, name, *args):
+        rc = getattr(self.lib, name)(*args)
+        assert rc == 0, (name, rc, self.lib.lidar_last_error())
+
+    def voxel(self, xt, voxel):
+        import torch
+        B, N, _ = xt.shape
+        cent = torch.empty((B, N, 3), dtype=torch.float32, device=xt.device)
+        vid = torch.empty((B, N), dtype=torch.int32, device=xt.device)
+        cnt = torch.empty((B, N), dtype=torch.int32, device=xt.device)
+        nvox = torch.empty(B, dtype=torch.int32, device=xt.device)
+        p = self.nat.ptr
+        self.call("lidar_voxel_downsample_batch_f32", self.h, p(xt), B, N, float(voxel), p(vid), p(cent), p(cnt),
+                  p(nvox), self.nat.stream_ptr())
+        return cent, vid, cnt, nvox
+
+
+def test_product_abi_has_no_testing_aids(cuda):
+    from lidar_ai_recommendation_software_amd import _native as nat
+    lib = nat.load_library()
+    for name in ("lidar_debug_fill_workspace", "lidar_debug_set_epoch", "lidar_debug_voxel_inject"):
+        assert getattr(DiagVoxel().lib, name, None) is not None
+        assert not hasattr(lib, name), name
+
+
 @pytest.mark.parametrize("B,n", [(32, 65536), (3, 20000), (1, 150001)])
 def test_voxel_ignores_workspace_leftovers(cuda, B, n):
     """The batched voxel path's in-launch hand-offs read only granules of the handle's tag block, which
     holds earlier calls' tags at other layouts: a workspace full of tag-like garbage (high halves 1..64,
-    the next calls' tags) and the other layout's leftovers change nothing."""
+    the next calls' tags) and the other layout's leftovers change nothing (the diagnostic build)."""
     import torch
-    from lidar_ai_recommendation_software_amd import _native as nat
-    from lidar_ai_recommendation_software_amd import pointnet2 as pn
     from lidar_ai_recommendation_software_amd.synthetic import unit_frames
+    dv = DiagVoxel()
     x = unit_frames(B, n, 8)
     xt = torch.from_numpy(x).to(cuda)
-    h = nat.handle(0)
-    need = nat.load_library().lidar_voxel_batch_workspace_bytes(B, n) + (1 << 20)
+    need = dv.lib.lidar_voxel_batch_workspace_bytes(B, n) + (1 << 20)
     other = torch.from_numpy(unit_frames(5, 7001, 9)).to(cuda)
     for seed in (1, 2, 3):
         # the tag block: tags of earlier calls at another layout (never this call's epoch)
-        pn.voxel_downsample_batch(other, 0.02 * seed)
-        nat.call("lidar_debug_fill_workspace", h, need, seed, nat.stream_ptr())
-        c, vid, cnt, nv = pn.voxel_downsample_batch(xt, 0.05)
+        dv.voxel(other, 0.02 * seed)
+        dv.call("lidar_debug_fill_workspace", dv.h, need, seed, dv.nat.stream_ptr())
+        c, vid, cnt, nv = dv.voxel(xt, 0.05)
         torch.cuda.synchronize()
         nv = nv.cpu().numpy()
         for f in (0, B - 1):
@@ -179,6 +231,72 @@ def test_voxel_ignores_workspace_leftovers(cuda, B, n):
             assert np.array_equal(vid[f].cpu().numpy(), wvid)
             assert np.array_equal(cnt[f, :nv[f]].cpu().numpy(), wcnt)
             assert np.array_equal(c[f, :nv[f]].cpu().numpy(), wc)
+
+
+@pytest.mark.parametrize("B,n,bucket", [(32, 65536, 3), (2, 65536, 31), (3, 300000, 0), (4, 20000, 9)])
+def test_voxel_failure_is_sticky(cuda, B, n, bucket):
+    """A bucket that fails (here: the diagnostic build's injected inconsistent bucket table at `bucket` of
+    every frame, nvox -3) wins over the voxel count the frame's last bucket writes — in the middle, at the
+    last bucket, at the first one (the look-back's start), on a frame of the three-launch keys path; the
+    Python layer raises LidarError on it, and the next call is clean again."""
+    import torch
+    from lidar_ai_recommendation_software_amd import _native as nat
+    from lidar_ai_recommendation_software_amd import pointnet2 as pn
+    from lidar_ai_recommendation_software_amd.synthetic import unit_frames
+    dv = DiagVoxel()
+    x = torch.from_numpy(unit_frames(B, n, 31)).to(cuda)
+    nb = (n + 2047) // 2048
+    assert bucket < nb
+    dv.call("lidar_debug_voxel_inject", bucket)
+    try:
+        _, _, _, nv = dv.voxel(x, 0.05)
+        torch.cuda.synchronize()
+    finally:
+        dv.call("lidar_debug_voxel_inject", -1)
+    assert (nv.cpu().numpy() == -3).all(), nv
+    with pytest.raises(nat.LidarError, match="bucket table"):
+        pn.check_voxel_counts(nv)
+    c, vid, cnt, nv = dv.voxel(x, 0.05)
+    torch.cuda.synchronize()
+    wc, wvid, wcnt = tier_n.voxel_downsample(x[B - 1].cpu().numpy(), 0.05)
+    assert nv[B - 1].item() == len(wc) and np.array_equal(vid[B - 1].cpu().numpy(), wvid)
+
+
+def test_voxel_beside_ssg_feed(cuda):
+    """The fused keys launch's in-launch hand-offs assume a frame's <= 16 tiles become co-resident (one
+    XCD, dispatched together).  Here 32 x 65 536-point batched voxel calls run on their own stream and
+    handle slot while the SSG feed (512-thread SA1 FPS on three side streams, the MFMA levels on the main
+    stream) occupies the chip: every call bit-exact against the oracle (frames 0 and 31), no nvox < 0."""
+    import torch
+    from lidar_ai_recommendation_software_amd import pointnet2 as pn
+    from lidar_ai_recommendation_software_amd.synthetic import unit_frames
+    from lidar_ai_recommendation_software_amd.streams import side_streams
+    B, N = 32, 65536
+    xv = torch.from_numpy(unit_frames(B, N, 41)).to(cuda)
+    want = {f: tier_n.voxel_downsample(xv[f].cpu().numpy(), 0.05) for f in (0, B - 1)}
+    bb = pn.PointNet2Backbone(pn.SSG, device=cuda, seed=0)
+    xs = [torch.from_numpy(unit_frames(B, N, 60 + i)).to(cuda) for i in range(2)]
+    feed = pn.StreamingSSG(bb, B, N, depth=3, fps_group=2, fps_threads=512, ramp=False, bq="bin",
+                           l2_side=True).feed()
+    vs = side_streams(cuda, 1, start=3)[0]  # beyond the feed's three side streams
+    outs = []
+    for i in range(16):
+        outs += feed.push(xs[i % 2])
+        if i >= 6:  # the pipeline is full: FPS workgroups resident, MFMA levels queued
+            with torch.cuda.stream(vs):
+                c, vid, cnt, nv = pn.voxel_downsample_batch(xv, 0.05, slot=12, check=False)
+                outs_v = (c, vid, cnt, nv)
+            vs.synchronize()
+            nvh = nv.cpu().numpy()
+            assert (nvh >= 0).all(), (i, nvh)
+            for f, (wc, wvid, wcnt) in want.items():
+                assert nvh[f] == len(wc), (i, f)
+                assert np.array_equal(vid[f].cpu().numpy(), wvid), (i, f)
+                assert np.array_equal(c[f, :nvh[f]].cpu().numpy(), wc), (i, f)
+    outs += feed.flush()
+    torch.cuda.synchronize()
+    assert len(outs) == 16
+    del outs_v
 
 
 @pytest.mark.parametrize("case", ["wide_keys", "lidar_sparse", "runs_128", "runs_129", "runs_600"])
@@ -276,18 +394,16 @@ def test_voxel_random_large_sparse_frames_vs_oracle(cuda, seed):
 
 def test_voxel_epoch_wrap(cuda):
     """The voxel calls' tags across the 32-bit epoch wrap (the tag block zeroed again there): the calls
-    before, at and after the wrap all equal the oracle."""
+    before, at and after the wrap all equal the oracle (the diagnostic build's epoch setter)."""
     import torch
-    from lidar_ai_recommendation_software_amd import _native as nat
-    from lidar_ai_recommendation_software_amd import pointnet2 as pn
     from lidar_ai_recommendation_software_amd.synthetic import unit_frames
     x = unit_frames(3, 20000, 12)
     xt = torch.from_numpy(x).to(cuda)
     want = [tier_n.voxel_downsample(x[f], 0.05) for f in range(3)]
-    h = nat.handle(0)
-    nat.call("lidar_debug_set_epoch", h, 0xfffffffd)
+    dv = DiagVoxel()
+    dv.call("lidar_debug_set_epoch", dv.h, 0xfffffffd)
     for _ in range(4):  # epochs 0xfffffffe, 0xffffffff, then 1 (wrapped), 2
-        c, vid, cnt, nv = pn.voxel_downsample_batch(xt, 0.05)
+        c, vid, cnt, nv = dv.voxel(xt, 0.05)
         torch.cuda.synchronize()
         nv = nv.cpu().numpy()
         for f in range(3):

@@ -1,6 +1,6 @@
 """configs[4] (MSG, bf16 spec, 131 072-point frames, 32 per step) through StreamingSSG at several
 (depth, group) settings: wall ms per 32-frame batch in the steady state, timed as bench.py does (the window
-starts and ends with `depth` groups in flight; its extras leg uses depth 3 and G = pick_group(steps, 3)).  usage: python tools/msg_pipe.py [steps [lazy [depth,G ...]]]"""
+starts and ends with `depth` groups in flight; its extras leg uses depth 3 and G = pick_group(steps, 3)).  usage: python tools/msg_pipe.py [steps [unused [depth,G[,side_query_ns] ...]]]"""
 import os
 import sys
 import time
@@ -12,16 +12,19 @@ from lidar_ai_recommendation_software_amd import pointnet2 as pn  # noqa: E402
 from lidar_ai_recommendation_software_amd.synthetic import unit_frames  # noqa: E402
 
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 30
-lazy = len(sys.argv) > 2 and sys.argv[2] == '1'
-settings = [tuple(int(v) for v in a.split(',')) for a in sys.argv[3:]] or [(3, 3), (3, 2), (4, 2), (2, 3), (4, 3), (3, 5), (2, 5)]
+settings = [tuple(int(v) for v in a.split(',')) + ((128,) if a.count(',') == 1 else ()) for a in sys.argv[3:]] or [(3, 3, 128), (3, 2, 128), (4, 2, 128), (2, 3, 128)]
 dev = torch.device("cuda:0")
 B, N = 32, 131072
 bb = pn.PointNet2Backbone(pn.MSG, device=dev, seed=0, dtype="bf16")
 xs = [torch.from_numpy(unit_frames(B, N, seed=s)).to(dev) for s in range(4)]
 ready = torch.cuda.Event()
 ready.record()
-for depth, G in settings:
-    pipe = pn.StreamingSSG(bb, B, N, depth=depth, fps_group=G, fps_threads=512, fps_lazy=lazy, ramp=False, bq="bin", l2_side=True)
+# MSG_SKIP_STREAMS=k: take k pool streams first (the bench's MSG leg runs after three other
+# StreamingSSG legs took 9); MSG_PRIO=-1: side streams from the high-priority pool
+_skip = [torch.cuda.Stream(device=dev) for _ in range(int(os.environ.get("MSG_SKIP_STREAMS", "0")))]
+prio = int(os.environ.get("MSG_PRIO", "0"))
+for depth, G, sq in settings:
+    pipe = pn.StreamingSSG(bb, B, N, depth=depth, fps_group=G, fps_threads=512, side_priority=prio, ramp=False, bq="bin", l2_side=True, side_query_ns=sq or None)
     feed = pipe.feed()
     for i in range((depth + 1) * G):
         feed.push(xs[i % 4], ready)
@@ -32,7 +35,7 @@ for depth, G in settings:
         feed.push(xs[i % 4], ready)
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) / n * 1e3
-    print(f"lazy {int(lazy)} depth {depth} G {G}: {ms:.3f} ms per batch, {B * N / ms / 1e3:.1f} M points/s", flush=True)
+    print(f"side_ns {sq} prio {prio} skip {len(_skip)} depth {depth} G {G}: {ms:.3f} ms per batch, {B * N / ms / 1e3:.1f} M points/s", flush=True)
     feed.flush()
     del feed, pipe
     torch.cuda.synchronize()

@@ -54,8 +54,6 @@ PREFIXES = (
     ("fps_bucket_kernel<1024, 1, true>", "fps_1024"),
     ("fps_bucket_kernel<1024, 1, false, 1>", "fps_1024"),  # round 5: + points per lane
     ("fps_bucket_kernel<1024, 1, true, 1>", "fps_1024"),
-    ("fps_lazy_kernel<512,", "sa1_fps"),  # --fps-lazy
-    ("fps_lazy_kernel<1024,", "fps_1024"),
     ("bq_bin_kernel", "bq_bin"),
     ("bq_grid_kernel", "sa2_ball_query"),  # SA1's queries run inside its MLP kernel (bq="bin")
     ("ball_query_kernel", "ball_query_scan"),

@@ -6,7 +6,11 @@ density grid, statistics and hotspots come from the gfx950 kernels behind
 ``data_processing.extract_people_positions`` / ``lidar_density_grid_f64`` (the numpy
 pairwise mean of the occupied cells and the stable top-5 ordering are restated on the
 device).  The optional ``backbone`` ("ssg" / "msg") adds a PointNet++ global feature of
-the frame; the default ``None`` keeps the reference behaviour exactly.
+the frame, computed with ``backbone_weights`` when given (trained weights: the
+nested [level][branch][layer] = (W, b) lists of ``pointnet2.init_weights``'s layout, or an ``.npz``
+written by ``pointnet2.save_weights``) and with the deterministic random init otherwise; the result
+says which (``backbone_weights``: "supplied" / "random-init").  The default ``None`` keeps the
+reference behaviour exactly.
 """
 import numpy as np
 
@@ -16,10 +20,23 @@ from . import data_processing as dp
 class CrowdDensityModel:
     """Model for analyzing crowd density from LiDAR point cloud data."""
 
-    def __init__(self, grid_size=1.0, backbone=None):
+    def __init__(self, grid_size=1.0, backbone=None, backbone_weights=None):
+        """grid_size as the reference (models/crowd_density_model.py:14-22); backbone None / "ssg" / "msg";
+        backbone_weights: the backbone's weights (validated against its configuration here, so a
+        mismatched set fails at construction), or None for the seed-0 random init."""
         self.grid_size = grid_size
         self.backbone = backbone
         self._net = None
+        self._weights = None
+        if backbone_weights is not None:
+            from . import pointnet2 as pn
+            if backbone is None:
+                raise ValueError("backbone_weights given without a backbone")
+            cfg = pn.CONFIGS[backbone]
+            if isinstance(backbone_weights, (str, bytes)) or hasattr(backbone_weights, "__fspath__"):
+                self._weights = pn.load_weights(backbone_weights, cfg)
+            else:
+                self._weights = pn.check_weights(cfg, backbone_weights)
 
     def analyze(self, processed_data):
         people = dp.extract_people_positions(processed_data)
@@ -49,6 +66,7 @@ class CrowdDensityModel:
         }
         if self.backbone is not None:
             res["backbone_feature"] = self.encode(processed_data["points"])
+            res["backbone_weights"] = "supplied" if self._weights is not None else "random-init"
         return res
 
     @staticmethod
@@ -67,7 +85,7 @@ class CrowdDensityModel:
         import torch
         from . import pointnet2 as pn
         if self._net is None:
-            self._net = pn.PointNet2Backbone(pn.CONFIGS[self.backbone], device="cuda")
+            self._net = pn.PointNet2Backbone(pn.CONFIGS[self.backbone], weights=self._weights, device="cuda")
         unit = self.normalise(points)
         g, _ = self._net.forward(torch.from_numpy(np.ascontiguousarray(unit))[None].cuda())
         return g[0].cpu().numpy()

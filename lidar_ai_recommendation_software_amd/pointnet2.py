@@ -83,6 +83,50 @@ def init_weights(cfg, seed=0):
     return weights
 
 
+def check_weights(cfg, weights):
+    """Validate [level][branch][layer] = (W (cin, cout), b (cout,)) against cfg's widths (cin = 3 + the
+    previous level's channels); returns them as contiguous float32 arrays.  Raises ValueError naming the
+    first mismatch."""
+    out, cin_feat = [], 0
+    if len(weights) != len(cfg["levels"]):
+        raise ValueError(f"weights: {len(weights)} levels, the configuration has {len(cfg['levels'])}")
+    for li, (lvl, wl) in enumerate(zip(cfg["levels"], weights)):
+        if len(wl) != len(lvl["mlps"]):
+            raise ValueError(f"weights level {li}: {len(wl)} branches, the configuration has {len(lvl['mlps'])}")
+        branches = []
+        for bi, (widths, layers) in enumerate(zip(lvl["mlps"], wl)):
+            if len(layers) != len(widths):
+                raise ValueError(f"weights level {li} branch {bi}: {len(layers)} layers, expected {len(widths)}")
+            cin, conv = 3 + cin_feat, []
+            for j, (cout, (W, b)) in enumerate(zip(widths, layers)):
+                W = np.ascontiguousarray(W, dtype=np.float32)
+                b = np.ascontiguousarray(b, dtype=np.float32).reshape(-1)
+                if W.shape != (cin, cout) or b.shape != (cout,):
+                    raise ValueError(f"weights level {li} branch {bi} layer {j}: W {W.shape}, b {b.shape}; "
+                                     f"expected ({cin}, {cout}) and ({cout},)")
+                conv.append((W, b))
+                cin = cout
+            branches.append(conv)
+        out.append(branches)
+        cin_feat = sum(w[-1] for w in lvl["mlps"])
+    return out
+
+
+def save_weights(path, weights):
+    """Weights to an .npz of plain arrays (keys l<level>_b<branch>_<layer>_{W,b}; no pickled objects)."""
+    arrs = {f"l{li}_b{bi}_{j}_{k}": a for li, wl in enumerate(weights) for bi, layers in enumerate(wl)
+            for j, wb in enumerate(layers) for k, a in zip("Wb", wb)}
+    np.savez(path, **arrs)
+
+
+def load_weights(path, cfg):
+    """The .npz save_weights wrote, in cfg's layout (loaded with allow_pickle=False), validated."""
+    with np.load(path, allow_pickle=False) as z:
+        w = [[[(z[f"l{li}_b{bi}_{j}_W"], z[f"l{li}_b{bi}_{j}_b"]) for j in range(len(widths))]
+              for bi, widths in enumerate(lvl["mlps"])] for li, lvl in enumerate(cfg["levels"])]
+    return check_weights(cfg, w)
+
+
 # --------------------------------------------------------------- functional ops
 def _dev_check(*ts):
     for t in ts:

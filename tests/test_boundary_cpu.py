@@ -98,3 +98,29 @@ def test_grid_dims_errors_match_numpy(x_max, err):
     with pytest.raises(err):
         nat.grid_dims(0.0, x_max, 0.0, 1.0, 1.0)
     assert nat.grid_dims(0.0, 30.0, -15.0, 15.0, 1.0) == (34, 34)
+
+
+def test_backbone_weights_roundtrip_and_validation(tmp_path):
+    """pointnet2.save_weights / load_weights (plain .npz, no pickles) round-trip bit for bit; check_weights
+    names the first mismatch; CrowdDensityModel refuses weights without a backbone (no GPU needed)."""
+    import numpy as np
+    import pytest
+    from lidar_ai_recommendation_software_amd import pointnet2 as pn
+    from lidar_ai_recommendation_software_amd.crowd_density_model import CrowdDensityModel
+    for cfg in (pn.SSG, pn.MSG):
+        w = pn.init_weights(cfg, 5)
+        p = tmp_path / f"{cfg['name']}.npz"
+        pn.save_weights(str(p), w)
+        got = pn.load_weights(str(p), cfg)
+        for la, lb in zip(w, got):
+            for ba, bb in zip(la, lb):
+                for (wa, ca), (wb, cb) in zip(ba, bb):
+                    assert np.array_equal(wa, wb) and np.array_equal(ca, cb)
+    w = pn.init_weights(pn.SSG, 0)
+    w[1][0][2] = (w[1][0][2][0][:, :100], w[1][0][2][1][:100])
+    with pytest.raises(ValueError, match="level 1 branch 0 layer 2"):
+        pn.check_weights(pn.SSG, w)
+    with pytest.raises(ValueError, match="without a backbone"):
+        CrowdDensityModel(backbone_weights=pn.init_weights(pn.SSG, 0))
+    m = CrowdDensityModel(backbone="ssg", backbone_weights=str(tmp_path / "ssg.npz"))
+    assert m._weights is not None

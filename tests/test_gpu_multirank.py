@@ -56,3 +56,45 @@ def test_bench_two_ranks_on_one_gpu(cuda, tmp_path):
         assert w1["world"] == 1 and w1["seed_rank"] == rank
         assert w2["digests"] == w1["digests"], f"rank {rank}: outputs differ from its 1-rank run"
     assert json.load(open(tmp_path / "w2.rank0.json"))["digests"] != json.load(open(tmp_path / "w2.rank1.json"))["digests"]
+
+
+ARGS_C3 = ["--batch", "32", "--points", "65536", "--steps", "4", "--warmup", "1", "--rotate", "4", "--no-extras",
+           "--no-density", "--no-cpu-baseline", "--no-fp32-mfma-leg", "--no-standalone"]
+
+
+@pytest.mark.timeout(900)
+def test_bench_configs3_eight_ranks_on_one_gpu(cuda, tmp_path):
+    """BASELINE configs[3] (256 x 65 536-point frames sharded per frame over 8 GPUs, no collectives) at
+    its real shape through plain `bench.py --gpus 8`: eight ranks of 32 frames each share the one GPU
+    (gloo for the timing collectives).  The line reports world 8 and 256 frames per step over the ranks,
+    its value is the whole job's points over the max-over-ranks window, and ranks 0 and 7 compute exactly
+    what their own frames give in a 1-rank run (`--seed-rank`).  A rehearsal of the 8-GPU code path, not
+    a scaling measurement (the ranks share one GPU)."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="2")
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, "-u", "bench.py", "--gpus", "8", *ARGS_C3, "--dump", str(tmp_path / "w8"),
+           "--detail", str(tmp_path / "detail.json")]
+    r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    line = _last_json(r.stdout)
+    steps = 4
+    assert line["n_gpus"] == 8 and line["steps"] == steps
+    assert line["config"]["global_batch_frames"] == 256 and line["config"]["frames_per_gpu"] == 32
+    d = line["distributed"]
+    assert d["world_size"] == 8 and sorted(row[0] for row in d["ranks"]) == list(range(8))
+    assert sum(row[2] for row in d["ranks"]) == 256 * steps  # every rank's 32 frames per step
+    assert abs(line["value"] - 8 * 32 * 65536 * steps / (line["ms_per_step"] * steps / 1e3) / 1e6) \
+        <= 1e-6 * line["value"]
+    # the window is the max over ranks: no rank's own window is longer
+    assert max(row[3] for row in d["ranks"]) <= line["ms_per_step"] * steps * (1 + 1e-6)
+    for rank in (0, 7):
+        w8 = json.load(open(tmp_path / f"w8.rank{rank}.json"))
+        assert w8["world"] == 8 and w8["seed_rank"] == rank
+        r1 = subprocess.run([sys.executable, "bench.py", *ARGS_C3, "--seed-rank", str(rank), "--dump",
+                             str(tmp_path / f"w1_{rank}")], cwd=REPO, env=env, capture_output=True, text=True,
+                            timeout=300)
+        assert r1.returncode == 0, r1.stderr[-4000:]
+        w1 = json.load(open(tmp_path / f"w1_{rank}.rank0.json"))
+        assert w1["world"] == 1 and w1["seed_rank"] == rank
+        assert w8["digests"] == w1["digests"], f"rank {rank}: outputs differ from its 1-rank run"
+    assert json.load(open(tmp_path / "w8.rank0.json"))["digests"] != json.load(open(tmp_path / "w8.rank7.json"))["digests"]

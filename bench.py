@@ -192,6 +192,9 @@ def compact_line(rec, detail_path=None):
     line["cpu_baseline"] = None if cb is None else {
         "value": cb["value"], "unit": cb["unit"], "cores": cb["cores"], "kind": cb["kind"], "sample": cb["sample"][:200]}
     line["speedup_vs_cpu"] = rec.get("speedup_vs_cpu")
+    if rec.get("ssg_host_feed"):  # the H2D-inclusive rate, reported beside the device-resident value
+        line["ssg_host_feed"] = {"value": rec["ssg_host_feed"]["value"], "unit": "M points/s",
+                                 "input": "host NumPy frames, PCIe included"}
     if rec.get("arithmetic_short"):
         line["arithmetic"] = rec["arithmetic_short"]
     bq = (rec.get("roofline_all") or {}).get("sa2_ball_query")
@@ -706,7 +709,10 @@ def main():
     ap.add_argument("--msg-batch", type=int, default=32,
                     help="frames per GPU per step of the configs[4] MSG leg (32: the per-GPU share of 256 frames)")
     ap.add_argument("--msg-steps", type=int, default=30)
-    ap.add_argument("--msg-side-ns", type=int, default=128,
+    ap.add_argument("--msg-group", type=int, default=3, help="configs[4] leg: batches per SA1-FPS launch")
+    ap.add_argument("--msg-depth", type=int, default=3, help="configs[4] leg: side streams")
+    ap.add_argument("--no-host-feed", action="store_true", help="skip the host-frame (PCIe-inclusive) SSG leg")
+    ap.add_argument("--msg-side-ns", type=int, default=0,
                     help="configs[4] leg: level-0 branches of >= this many samples answer their ball queries on "
                          "the side streams (StreamingSSG side_query_ns; 0: every branch fused on the main stream)")
     ap.add_argument("--no-extras", action="store_true", help="skip the configs[1]/[4] side measurements")
@@ -743,18 +749,25 @@ def main():
     digests = {}
     local_ms = {}  # this rank's own window time per leg (the line reports the max over ranks)
 
-    def measure(key, cfg, dtype, B, N, steps, warmup, depth, G, x3=True, events=True, side_query_ns=128):
+    def measure(key, cfg, dtype, B, N, steps, warmup, depth, G, x3=True, events=True, side_query_ns=None,
+                host=False, bb=None, xs=None, refs=None):
         """Steady-state window of `steps` batches through StreamingSSG's feed.  events: HIP
         events around every launch inside the timed window (the headline: the roofline durations
         come from the same window); False: the window runs clean and the per-kernel durations come
         from a second window of the same length (with ~25 launches per step, as MSG has, the
-        events cost ~1/3)."""
-        bb = pn.PointNet2Backbone(cfg, device=dev, seed=0, dtype=dtype, x3=x3)
+        events cost ~1/3).  host: the batches enter as host NumPy frames through feed().push_host
+        (pinned staging, the device copy on the side streams: PCIe-inclusive), reusing the device
+        leg's backbone, batches and references."""
+        bb = bb or pn.PointNet2Backbone(cfg, device=dev, seed=0, dtype=dtype, x3=x3)
         nb = max(1, args.rotate)
-        xs = [torch.from_numpy(unit_frames(B, N, seed=sharding.frame_seed(seed_rank, step=i))).to(dev) for i in range(nb)]
+        if xs is None:
+            xs = [torch.from_numpy(unit_frames(B, N, seed=sharding.frame_seed(seed_rank, step=i))).to(dev)
+                  for i in range(nb)]
         # one-batch forward(): what every pipeline output must equal (--no-verify: not issued, so a
         # counter pass sees only the pipeline's launches)
-        refs = None if args.no_verify else [bb.forward(x)[0] for x in xs]
+        if refs is None and not args.no_verify:
+            refs = [bb.forward(x)[0] for x in xs]
+        hxs = [x.cpu().numpy() for x in xs] if host else None
         ready = torch.cuda.Event()  # the inputs exist: the feed's FPS launches wait only for their slots
         ready.record()
         pipe = pn.StreamingSSG(bb, B, N, depth=depth, fps_group=G, fps_threads=args.fps_threads,
@@ -762,16 +775,17 @@ def main():
                                slots=args.slots or None, bq=args.bq,
                                l2_side=bool(args.l2_side), side_query_ns=side_query_ns)
         feed = pipe.feed()
+        push = (lambda i: feed.push_host(hxs[i % nb])) if host else (lambda i: feed.push(xs[i % nb], ready))
         nwarm = (depth + max(1, warmup)) * G  # whole groups; `depth` groups in flight when the window opens
         outs = []
         for i in range(nwarm):
-            outs += feed.push(xs[i % nb], ready)
+            outs += push(i)
         timers = pn._Timers()
         win = []
 
         def window(i0, sink):
             for i in range(i0, i0 + steps):
-                sink.extend(feed.push(xs[i % nb], ready))
+                sink.extend(push(i))
 
         if events:
             bb.timers = timers
@@ -797,14 +811,26 @@ def main():
             assert not bad, f"{key}: streaming outputs differ from forward() for batches {bad[:5]}"
             digests[key] = [hashlib.sha256(r.cpu().numpy().tobytes()).hexdigest() for r in refs]
         local_ms[key] = local * 1e3
-        return elapsed, timers.totals(), bb, xs
+        return elapsed, timers.totals(), bb, xs, refs
 
     tot_x3 = None
-    elapsed, tot, bb, xs = measure("ssg", pn.SSG, "f32", B, N, args.steps, args.warmup, args.depth, G, x3=bool(args.x3))
+    elapsed, tot, bb, xs, refs = measure("ssg", pn.SSG, "f32", B, N, args.steps, args.warmup, args.depth, G,
+                                         x3=bool(args.x3))
+    host_feed = None
+    if not args.no_host_feed:
+        # the same workload entering as host NumPy frames (PCIe-inclusive: pinned staging by host threads,
+        # the device copy on the side streams); outputs checked against the same forward() references
+        el_h, _, _, _, _ = measure("ssg_host", pn.SSG, "f32", B, N, args.steps, args.warmup, args.depth, G,
+                                   x3=bool(args.x3), events=False, host=True, bb=bb, xs=xs, refs=refs)
+        host_feed = {"value": sharding.aggregate_rate(B * N * args.steps, world, el_h) / 1e6, "unit": "M points/s",
+                     "ms_per_step": el_h / args.steps * 1e3,
+                     "input": "host NumPy (B, N, 3) float32 batches -> feed().push_host (8 host threads into a "
+                              "pinned ring, H2D on the side streams ahead of each group's FPS)",
+                     "parity": "every output bit-equal to forward() of the same batch"}
     fp32_mfma = None
     if args.x3 and not args.no_fp32_mfma_leg:
         # the same workload on the native fp32-MFMA kernels (clean window), for comparison
-        el_f, t_f, _, _ = measure("ssg_fp32_mfma", pn.SSG, "f32", B, N, args.steps, args.warmup, args.depth, G,
+        el_f, t_f, _, _, _ = measure("ssg_fp32_mfma", pn.SSG, "f32", B, N, args.steps, args.warmup, args.depth, G,
                                   x3=False, events=False)
         fp32_mfma = {"value": sharding.aggregate_rate(B * N * args.steps, world, el_f) / 1e6, "unit": "M points/s",
                      "ms_per_step": el_f / args.steps * 1e3,
@@ -844,18 +870,20 @@ def main():
         legs = [("configs[1]_sa1_16k_f32", pn.SA1_ONLY, "f32", 32, 16384, 40),
                 ("configs[4]_msg_131k_bf16", pn.MSG, "bf16", args.msg_batch, 131072, args.msg_steps)]
         for key, cfg, dtype, b2, n2, st2 in legs:
-            g2 = pick_group(st2, 3)
-            sq = (args.msg_side_ns or None) if cfg is pn.MSG else 128
-            el2, t2, _, _ = measure(key, cfg, dtype, b2, n2, st2, 1, 3, g2, events=False, side_query_ns=sq)
+            msg = cfg is pn.MSG
+            g2 = pick_group(st2, args.msg_group if msg else 3)
+            d2 = args.msg_depth if msg else 3
+            sq = (args.msg_side_ns or None) if cfg is pn.MSG else None
+            el2, t2, _, _, _ = measure(key, cfg, dtype, b2, n2, st2, 1, d2, g2, events=False, side_query_ns=sq)
             pl2 = {k: t / c for k, (c, f, t) in t2.items()}
             # the two chains per group: the side streams' FPS / binning / queries (3 streams) and the
             # main stream's MLP kernels, from the per-launch HIP-event durations of the second window
             side_k = [k for k in pl2 if k.endswith("_fps") or "_bq_bin" in k or "_ball_query" in k]
             extras[key] = {"M_points_per_s": sharding.aggregate_rate(b2 * n2 * st2, world, el2) / 1e6,
                            "ms_per_step": el2 / st2 * 1e3, "frames_per_gpu": b2, "points_per_frame": n2,
-                           "dtype": dtype, "batches_per_group": g2, "side_query_ns": sq,
+                           "dtype": dtype, "batches_per_group": g2, "side_streams": d2, "side_query_ns": sq,
                            "chains_ms_per_group": {"main": sum(v for k, v in pl2.items() if k not in side_k),
-                                                   "side": sum(pl2[k] for k in side_k) / 3,
+                                                   "side": sum(pl2[k] for k in side_k) / d2,
                                                    "step_ms_per_group": el2 / st2 * 1e3 * g2},
                            "kernel_ms_per_launch": pl2}
             mw = stack_mfma_work(cfg, n2)
@@ -995,6 +1023,7 @@ def main():
                          "fps_threads": args.fps_threads,
                          "sa1_ball_queries": args.bq, **chains},
             "fp32_mfma_kernels": fp32_mfma,
+            "ssg_host_feed": host_feed,
             "other_configs": extras,
             "density_path": density,
             "host_frames": host,

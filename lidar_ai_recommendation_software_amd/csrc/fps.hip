@@ -26,6 +26,9 @@
 // is the identity 0..m-1 while the parent's winning distance stayed > 0 — the parent
 // run records the first step whose winning distance was 0 (`first_zero`), the child run
 // takes it as `prefix_ok` and copies the prefix when m <= prefix_ok.
+#include <algorithm>
+#include <atomic>
+
 #include "common.hpp"
 
 namespace {
@@ -554,6 +557,16 @@ __global__ __launch_bounds__(T) void fps_bucket_kernel(const float *__restrict__
 
 }  // namespace
 
+#ifdef LIDAR_DIAG
+// diagnostic build only: phase stamps of the SA1 FPS launches a pipeline issues (lidar_diag_fps_record).
+// Every 512-thread, one-point-per-lane launch without prefix_ok (SA1, not SA2's nested FPS) of n <= 65 536
+// points takes the DIAG instantiation and appends its per-(frame, wave) phase totals (6 words, as
+// lidar_diag_fps_eager512_phases) to the registered buffer while it has room.
+static uint64_t *g_fps_rec = nullptr;
+static int64_t g_fps_rec_cap = 0;
+static std::atomic<int64_t> g_fps_rec_used{0};
+#endif
+
 template <int T>
 static int launch_fps(const float *xyz, int64_t batch, int64_t n, int64_t npoint, int32_t *idx, float *new_xyz,
                       int32_t *first_zero, const int32_t *prefix_ok, float *ws, int64_t stride, hipStream_t s)
@@ -576,6 +589,24 @@ static int launch_fps(const float *xyz, int64_t batch, int64_t n, int64_t npoint
             else go(fps_bucket_kernel<T, 8, false, 16>);
         }
     } else {
+#ifdef LIDAR_DIAG
+        if constexpr (T == 512) {
+            if (g_fps_rec && prefix_ok == nullptr && nb <= 2 * lanes) {
+                const int64_t need = batch * (T / 64) * 6;
+                const int64_t off = g_fps_rec_used.fetch_add(need);
+                if (off + need <= g_fps_rec_cap) {
+                    auto god = [&](auto kern) {
+                        hipLaunchKernelGGL(kern, grid, block, 0, s, xyz, (int)n, (int)npoint, idx, new_xyz, first_zero,
+                                           prefix_ok, ws, stride, g_fps_rec + off);
+                    };
+                    if (nb <= lanes) god(fps_bucket_kernel<T, 1, true>);
+                    else god(fps_bucket_kernel<T, 2, true>);
+                    LAUNCH_CHECK();
+                    return LIDAR_OK;
+                }
+            }
+        }
+#endif
         if (nb <= lanes) go(fps_bucket_kernel<T, 1>);
         else if (nb <= 2 * lanes) go(fps_bucket_kernel<T, 2>);
         else if (nb <= 4 * lanes) go(fps_bucket_kernel<T, 4>);
@@ -633,6 +664,17 @@ LIDAR_EXPORT int lidar_fps_f32(lidar_handle *h, const float *xyz, int64_t batch,
 #ifdef LIDAR_DIAG
 // diagnostic build only (`make diag`, not part of the product library or ABI): per-wave phase cycle
 // totals of one FPS run
+// register (buf, cap_words) for the SA1 FPS launches' phase records (buf NULL: stop); returns 0
+LIDAR_EXPORT int lidar_diag_fps_record(uint64_t *buf, int64_t cap_words)
+{
+    g_fps_rec = buf;
+    g_fps_rec_cap = buf ? cap_words : 0;
+    g_fps_rec_used = 0;
+    return LIDAR_OK;
+}
+// words the registered buffer has received so far (launches past its capacity ran unstamped)
+LIDAR_EXPORT int64_t lidar_diag_fps_recorded(void) { return std::min<int64_t>(g_fps_rec_used, g_fps_rec_cap); }
+
 // the eager kernel's phases at 512 threads (BPL from n), diag[(frame * 8 + wave) * 6 + k]
 LIDAR_EXPORT int lidar_diag_fps_eager512_phases(lidar_handle *h, const float *xyz, int64_t batch, int64_t n,
                                                 int64_t npoint, int32_t *idx, uint64_t *diag, void *stream)

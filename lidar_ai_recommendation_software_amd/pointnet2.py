@@ -924,7 +924,7 @@ class StreamingSSG:
 
     def __init__(self, backbone, batch, n, depth=1, fps_group=1, fps_threads=0, side_priority=0,
                  ramp=True,
-                 reserve=True, keep_levels=False, slots=None, bq="bin", l2_side=False, side_query_ns=128):
+                 reserve=True, keep_levels=False, slots=None, bq="bin", l2_side=False, side_query_ns=None):
         """fps_threads: SA1 FPS workgroup size (0 = 1024; 512: half the CU footprint beside the
         MLPs).  ramp: in run(), the first groups hold 1, 2, ... batches (a shorter pipeline fill).
         slots: staging slots (>= depth + 1; default depth + 3).  Group k's FPS reuses the slot of
@@ -937,9 +937,13 @@ class StreamingSSG:
         FPS output, so they run on the side stream too (the main stream then runs only MLP work
         and level 1's per-point layer 1).  side_query_ns: with bq="bin", a level-0 branch of at
         least this many samples also answers its ball queries on the side stream (from the same
-        grid), and the main stream runs its MLP on the given indices (bit-identical): configs[4]'s
-        ns = 128 branch spent ~40 % of its fused kernel on the queries, in the main chain that bounds
-        the MSG pipeline, while its side streams had slack."""
+        grid), and the main stream runs its MLP on the given indices (bit-identical).  Off by
+        default: for configs[4]'s MSG pipeline (ns = 128 / 32 / 16) it measured 462-475 against
+        502-535 M points/s fused.
+
+        Host frames: feed().push_host(frames) takes a batch of host NumPy frames, stages it in
+        pinned memory (parallel host threads) and copies it to the device on the group's side
+        stream ahead of its FPS (the PCIe-inclusive feed; results equal push() of the same data)."""
         self.bb = backbone
         self.B, self.N, self.depth, self.G = batch, n, depth, max(1, int(fps_group))
         self.ramp = bool(ramp)
@@ -963,6 +967,7 @@ class StreamingSSG:
         GB = self.G * batch
         self.stage = [torch.empty((GB, n, 3), dtype=torch.float32, device=dev) if self.G > 1 else None
                       for _ in range(nslot)]
+        self.staged = [self.G > 1] * nslot  # the slot's group lives in stage[slot] (else in the caller's batch)
         self.idx = [torch.empty((GB, self.M1), dtype=torch.int32, device=dev) for _ in range(nslot)]
         self.cxyz = [torch.empty((GB, self.M1, 3), dtype=torch.float32, device=dev) for _ in range(nslot)]
         self.fz = [torch.empty(GB, dtype=torch.int32, device=dev) for _ in range(nslot)]
@@ -1007,15 +1012,24 @@ class StreamingSSG:
             fs.wait_event(ev)
         g = len(xs) * self.B
         t = self.bb.timers
+        host = any(isinstance(xj, _HostBatch) for xj in xs)
+        self.staged[slot] = self.G > 1 or host
+        if self.staged[slot] and self.stage[slot] is None:  # (G = 1 fed from the host)
+            self.stage[slot] = torch.empty((self.G * self.B, self.N, 3), dtype=torch.float32, device=self.bb.device)
         with torch.cuda.stream(fs):
-            if self.G > 1:
+            if self.staged[slot]:
                 x = self.stage[slot][:g]
                 for j, xj in enumerate(xs):
-                    x[j * self.B:(j + 1) * self.B].copy_(xj, non_blocking=True)
+                    if isinstance(xj, _HostBatch):  # pinned host -> device, then the buffer may be refilled
+                        x[j * self.B:(j + 1) * self.B].copy_(xj.pinned, non_blocking=True)
+                        xj.copied.record(fs)
+                    else:
+                        x[j * self.B:(j + 1) * self.B].copy_(xj, non_blocking=True)
             else:
                 x = xs[0]
             for xj in xs:  # read on this stream: keep the caller's buffers alive until then
-                xj.record_stream(fs)
+                if not isinstance(xj, _HostBatch):
+                    xj.record_stream(fs)
             _call(t, "sa1_fps", g, farthest_point_sample, x, self.M1, return_xyz=True, first_zero=self.fz[slot][:g],
                   slot=hs, out_idx=self.idx[slot][:g], out_xyz=self.cxyz[slot][:g], threads=self.fps_threads)
             lvl0 = self.bb.levels[0]
@@ -1048,7 +1062,7 @@ class StreamingSSG:
         frame, so the per-batch outputs are views of the group's), split back per batch."""
         main.wait_event(self.fps_done[slot])
         B, g = self.B, len(xs) * self.B
-        x = self.stage[slot][:g] if self.G > 1 else xs[0]
+        x = self.stage[slot][:g] if self.staged[slot] else xs[0]
         lvl0 = [self.idx[slot][:g], self.cxyz[slot][:g], self.fz[slot][:g],
                 [gi[:g] if gi is not None else None for gi in self.gidx[slot]] if self.gidx is not None else None]
         pre2 = None
@@ -1090,22 +1104,81 @@ class StreamingSSG:
         return outs + f.flush()
 
 
+_HOST_READY = object()  # push_host's "ready" marker: the batch sits in pinned host memory already
+
+
+class _HostBatch:
+    """One batch of host frames in a pinned buffer; `copied` is recorded on the side stream after its
+    host-to-device copy (the buffer may be refilled once it has completed)."""
+
+    def __init__(self, pinned):
+        self.pinned = pinned
+        self.copied = torch.cuda.Event()
+        self.copied.record()  # (a fresh buffer is free)
+
+
 class _Feed:
     """StreamingSSG's persistent feed: push(batch) stages batches; every full group of G issues
     its SA1 FPS on a side stream and, once `depth` groups are in flight, the oldest group's
     remaining levels on the main stream (the caller's current stream).  push returns the
     outputs of the batches that call completed (in input order); flush() issues a partial last
-    group and drains the pipeline."""
+    group and drains the pipeline.  push_host(frames) is push() for host NumPy frames."""
 
     def __init__(self, pipe):
         self.p = pipe
         self.main = torch.cuda.current_stream(pipe.bb.device)
         self.buf, self.pending, self.k = [], [], 0
         self.readies = []  # push()'s ready event per buffered batch
+        self._ring, self._ri, self._pool = [], 0, None  # push_host's pinned buffers and copy threads
+
+    def push_host(self, frames, threads=8):
+        """frames: one batch of host frames, a (B, N, 3) array or B arrays of shape (N, 3), of any real
+        dtype (converted to float32 as numpy's astype does).  They are copied into a pinned buffer by
+        `threads` host threads (frames split between them; numpy releases the GIL in the copy), and the
+        group's side stream copies the buffer to the device ahead of its FPS.  The pinned ring holds
+        (depth + 2) G batches; a buffer is refilled only after its device copy has completed (a host wait
+        on that event, the feed's back-pressure).  Returns push()'s outputs; every output equals
+        forward() of the same frames on the device."""
+        import numpy as _np
+        p = self.p
+        B, N = p.B, p.N
+        if isinstance(frames, _np.ndarray):
+            if frames.shape != (B, N, 3):
+                raise ValueError(f"push_host: frames must be ({B}, {N}, 3), got {frames.shape}")
+            parts = list(frames)
+        else:
+            parts = [_np.asarray(f) for f in frames]
+            if len(parts) != B or any(f.shape != (N, 3) for f in parts):
+                raise ValueError(f"push_host: {B} frames of shape ({N}, 3) expected")
+        if not self._ring:
+            import concurrent.futures
+            self._ring = [_HostBatch(torch.empty((B, N, 3), dtype=torch.float32, pin_memory=True))
+                          for _ in range((p.depth + 2) * p.G)]
+            self._nthreads = max(1, int(threads))
+            self._pool = concurrent.futures.ThreadPoolExecutor(max_workers=self._nthreads)
+        hb = self._ring[self._ri]
+        self._ri = (self._ri + 1) % len(self._ring)
+        hb.copied.synchronize()  # its previous batch has reached the device
+        dst = hb.pinned.numpy()
+        step = -(-B // self._nthreads)
+
+        def fill(lo):
+            for j in range(lo, min(B, lo + step)):
+                _np.copyto(dst[j], parts[j], casting="unsafe")
+
+        for f in [self._pool.submit(fill, lo) for lo in range(0, B, step)]:
+            f.result()
+        self.buf.append(hb)
+        self.readies.append(_HOST_READY)  # filled by the host: no device event to wait for
+        if len(self.buf) < p.G:
+            return []
+        xs, evs = self.buf, self.readies
+        self.buf, self.readies = [], []
+        return self._issue(xs, evs)
 
     def _issue(self, xs, readies=None):
-        evs = [e for e in (readies or [None]) if e is not None]
-        if readies is None or len(evs) < len(readies):
+        evs = [e for e in (readies or [None]) if e is not None and e is not _HOST_READY]
+        if readies is None or any(e is None for e in readies):
             ev = torch.cuda.Event()
             ev.record(self.main)  # the inputs exist on the caller's stream
             evs.append(ev)

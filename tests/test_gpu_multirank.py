@@ -86,7 +86,7 @@ def test_bench_configs3_eight_ranks_on_one_gpu(cuda, tmp_path):
     assert abs(line["value"] - 8 * 32 * 65536 * steps / (line["ms_per_step"] * steps / 1e3) / 1e6) \
         <= 1e-6 * line["value"]
     # the window is the max over ranks: no rank's own window is longer
-    assert max(row[3] for row in d["ranks"]) <= line["ms_per_step"] * steps * (1 + 1e-6)
+    assert max(row[3] for row in d["ranks"]) <= line["ms_per_step"] * steps * (1 + 1e-3)  # (4 digits in the line)
     for rank in (0, 7):
         w8 = json.load(open(tmp_path / f"w8.rank{rank}.json"))
         assert w8["world"] == 8 and w8["seed_rank"] == rank

@@ -137,10 +137,11 @@ def test_fps_bit_exact(cuda, kind, b, n, m, threads):
     assert np.array_equal(nx.cpu().numpy(), np.take_along_axis(x, want[..., None].astype(np.int64), 1))
 
 
-@pytest.mark.parametrize("n,m", [(300000, 2048), (600000, 700), (1100000, 300)])
+@pytest.mark.parametrize("n,m", [(300000, 2048), (600000, 700), (1100000, 300), (2200000, 96), (4194304, 40)])
 def test_fps_large_frames_bit_exact(cuda, n, m):
     """Frames above 262 144 points (8 bucket slots per lane at 512 threads) take buckets of 64 x PPL
-    points (PPL 2 / 4 / 8 here): bit-exact against the C oracle (no cliff)."""
+    points (PPL 2 / 4 / 8 / 16 here; 16 — the most registers, P[K][16] — from 2 097 153 points up to the
+    4 194 304-point limit): bit-exact against the C oracle (no cliff)."""
     x = frames_for("uniform", 1, n, 13)
     x[0, n // 3: n // 3 + 1000] = x[0, :1000]  # duplicates: exact ties at distance 0
     idx, nx = pn.farthest_point_sample(torch.from_numpy(x).to(cuda), m, return_xyz=True)
@@ -641,6 +642,33 @@ def test_streaming_side_queries_match_forward(cuda, side_ns, dtype):
             assert torch.equal(nf, wf) and torch.equal(ni, wi)
             for a, b in zip(ngi, wgi):
                 assert a is not None and torch.equal(a, b)
+
+
+@pytest.mark.parametrize("G,depth,dtype,mixed", [(1, 2, np.float32, False), (3, 2, np.float64, False),
+                                                 (2, 3, np.float32, True), (4, 3, np.float32, False)])
+def test_streaming_host_feed_matches_forward(cuda, G, depth, dtype, mixed):
+    """feed().push_host(host frames): pinned staging by host threads, the device copy on the group's side
+    stream ahead of its FPS; (B, N, 3) arrays and lists of (N, 3) frames, float64 frames converted as
+    astype(float32) does, device batches mixed into the same groups (mixed), more batches than the pinned
+    ring holds (its back-pressure); every output equal to forward() of the same frames."""
+    bb = pn.PointNet2Backbone(pn.SSG, device=cuda, seed=7)
+    hx = [unit_frames(2, 8192, 90 + s).astype(dtype) for s in range(4 * (depth + 2) * G + 1)]
+    want = [bb.forward(torch.from_numpy(h.astype(np.float32)).to(cuda))[0] for h in hx]
+    feed = pn.StreamingSSG(bb, 2, 8192, depth=depth, fps_group=G, fps_threads=512, ramp=False, bq="bin",
+                           l2_side=True).feed()
+    outs = []
+    for i, h in enumerate(hx):
+        if mixed and i % 3 == 2:
+            outs += feed.push(torch.from_numpy(h.astype(np.float32)).to(cuda))
+        else:
+            outs += feed.push_host(h if i % 2 else list(h))
+    outs += feed.flush()
+    torch.cuda.synchronize()
+    assert len(outs) == len(hx)
+    for i, (a, b) in enumerate(zip(outs, want)):
+        assert torch.equal(a, b), i
+    with pytest.raises(ValueError, match="push_host"):
+        feed.push_host(hx[0][:1])
 
 
 def test_streaming_feed_steady_state(cuda):

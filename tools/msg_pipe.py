@@ -39,3 +39,4 @@ for depth, G, sq in settings:
     feed.flush()
     del feed, pipe
     torch.cuda.synchronize()
+    time.sleep(float(os.environ.get("MSG_SLEEP", "0")))  # idle between settings (clock / power recovery probe)

@@ -9,6 +9,8 @@
 #     the SSG bench at the driver's shape (FETCH_SIZE; WRITE_SIZE; the SQ / GRBM VALU group)
 #   5 the voxel leg's kernels (tools/voxel_micro.py: 20 batched launches at the bench's shape): kernel
 #     trace, FETCH_SIZE and WRITE_SIZE passes (tools/pmc_voxel.py reduces them)
+#   6 (round 6) configs[4]'s MSG pipeline: kernel trace + FETCH_SIZE / WRITE_SIZE passes (tools/pmc_msg.py), and
+#     the SA1 FPS step phases inside the SSG pipeline (tools/micro/fps_pipe_phases.py, diagnostic library)
 # reduce afterwards (CPU): tools/pmc_traffic.py and tools/pmc_valu.py with the passes' bench lines
 # usage (on the box): bash tools/profile_round.sh TAG [tests|notests]
 set -o pipefail
@@ -47,4 +49,16 @@ timeout -s KILL 120 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format cs
     python3 $R/tools/voxel_micro.py > $O/vpmc_fetch.log 2>&1 || exit 21
 timeout -s KILL 120 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $O/vpmc_write -o v -- \
     python3 $R/tools/voxel_micro.py > $O/vpmc_write.log 2>&1 || exit 22
+# configs[4] (round 6): kernel trace of the MSG pipeline alone (tools/msg_pipe.py, the bench's MSG settings), then
+# FETCH_SIZE / WRITE_SIZE passes over the same run (tools/pmc_msg.py reduces them)
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/mprof -o m -- \
+    python3 $R/tools/msg_pipe.py 30 0 3,3,0 > $O/mprof.log 2>&1 || exit 23
+timeout -s KILL 200 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $O/mpmc_fetch -o m -- \
+    python3 $R/tools/msg_pipe.py 30 0 3,3,0 > $O/mpmc_fetch.log 2>&1 || exit 24
+timeout -s KILL 200 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $O/mpmc_write -o m -- \
+    python3 $R/tools/msg_pipe.py 30 0 3,3,0 > $O/mpmc_write.log 2>&1 || exit 25
+# the SA1 FPS step phases in the pipeline and alone (the diagnostic library)
+cd $R
+LIDAR_AMD_LIB=$R/lidar_ai_recommendation_software_amd/liblidar_amd_diag.so timeout -k 10 300 \
+    python3 tools/micro/fps_pipe_phases.py 20 4 $O/fps_pipe_phases.json > $O/fps_pipe_phases.log 2>&1 || exit 26
 exit 0

@@ -32,6 +32,10 @@
 #ifndef LIDAR_BQ_WIN
 #define LIDAR_BQ_WIN 1.0
 #endif
+// the same for queries of ns >= 64, whose windows are ranked by the bitmap (bq_grid.hpp)
+#ifndef LIDAR_BQ_WIN_BIG
+#define LIDAR_BQ_WIN_BIG 1.0
+#endif
 
 namespace {
 
@@ -139,7 +143,8 @@ __device__ BqGrid bin_params(const float mn[3], const float mx[3], int n, float 
     double vol = 1.0;
     for (int a = 0; a < 3; ++a) vol *= fmax((double)ext[a], 2.0 * rr);
     const double hits = vol > 0.0 ? n * (4.18879020478639 * rr * rr * rr) / vol : (double)n;
-    const double want = fmin(64.0, fmax(1.0, LIDAR_BQ_WIN * hits / (double)max(ns, 1)));
+    const double wf = ns >= 64 ? LIDAR_BQ_WIN_BIG : LIDAR_BQ_WIN;
+    const double want = fmin(64.0, fmax(1.0, wf * hits / (double)max(ns, 1)));
     int shift = 6;
     while (shift < 30 && ((int64_t)n >> shift) > 64) ++shift;                      // <= 64 windows
     while (shift < 30 && (double)(1ll << shift) * want < (double)n) ++shift;       // ~want windows
@@ -272,7 +277,7 @@ __global__ __launch_bounds__(256) void bq_grid_kernel(const float *__restrict__ 
                                                       int64_t total, int64_t per_xcd, float r, float r2, int ns,
                                                       int32_t *__restrict__ out)
 {
-    __shared__ int hits[4][kCap + 4];
+    __shared__ __attribute__((aligned(8))) int hits[4][kCap + 4];  // per wave: a window's hits / bitmap
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int64_t L = blockIdx.x;
     const int64_t w = ((L & 7) * per_xcd + (L >> 3)) * 4 + wid;

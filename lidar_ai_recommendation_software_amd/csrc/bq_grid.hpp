@@ -72,8 +72,19 @@ __device__ __forceinline__ void lds_wave_sync()
 // One wavefront answers the ball query of centre (cx, cy, cz) of the frame whose points are p
 // (n of them) and whose grid (bq_bin_kernel) is fw: the first ns indices with d < r2 in index
 // order into o[0, ns), unused slots repeating the first hit (0 with no hit).  hw: this wave's
-// LDS scratch of CAP + 4 ints (windows with more than CAP candidates are scanned in index order).
-template <int CAP, class Out>
+// LDS scratch of CAP + 4 ints (8-byte aligned).
+//
+// A window's hits are put in index order by one of two rankings.  Bitmap (round 6; queries of ns >= 64,
+// whose windows hold ~ns hits, and windows of up to 32 CAP indices, i.e. 16 384 at CAP = 512; BM = 0
+// compiles it out, for the fused kernels of fewer samples): every hit sets its bit (index - window start) in an LDS
+// bitmap (ds_or_b64), then lane l takes 64-bit word c 64 + l, and a popcount, a wave prefix sum and the
+// word's own bit order give every hit its rank — O(window / 64) per lane, with no bound on the window's
+// candidates.  List (fewer samples, larger windows): the hits go to an LDS list and each is ranked by counting
+// the smaller ones, O(hits^2 / 64) per lane, cheaper up to ~64 hits (MSG: the bitmap took its ns = 128 branch's
+// fused kernel from 7.95 to 6.96 ms per 96 frames but its ns = 32 one from 1.92 to 2.17); a window with more
+// than CAP candidates is then scanned in index order.
+// Both give the same indices in the same order (tests/test_gpu_tier_n.py::test_ball_query_*).
+template <int CAP, class Out, bool BM = true>
 __device__ __forceinline__ void grid_query_wave(const float *__restrict__ p, const char *__restrict__ fw, int n,
                                                 float cx, float cy, float cz, float r, float r2, int ns,
                                                 int lane, int *hw, Out *o)
@@ -114,6 +125,9 @@ __device__ __forceinline__ void grid_query_wave(const float *__restrict__ p, con
         st = tab[colbase];
         len = tab[colbase + (hiz - loz) + 1] - st;
     }
+    // the bitmap ranking: 64-bit words of the window's index span in hw
+    const bool bitmap = BM && ns >= 64 && !full && ((int64_t)1 << g.win_shift) <= 32 * (int64_t)CAP;
+    unsigned long long *bm = reinterpret_cast<unsigned long long *>(hw);
     for (int win = 0; win < g.nwin && cnt < ns; ++win) {
         const int wlo = win << g.win_shift, whi = min(n, (win + 1) << g.win_shift);
         const int cst = st, clen = len;
@@ -125,9 +139,14 @@ __device__ __forceinline__ void grid_query_wave(const float *__restrict__ p, con
         const int incl = lidar::row_incl_scan_i32(clen);  // lanes 0..8 (row 0): the columns' prefix
         const int tot = full ? CAP + 1 : __builtin_amdgcn_readlane(incl, 8);
         if (tot == 0) continue;
-        if (tot > CAP) {
+        if (!bitmap && tot > CAP) {
             scan_range(p, wlo, whi, cx, cy, cz, r2, ns, lane, below, cnt, first, o);
             continue;
+        }
+        const int nwords = (whi - wlo + 63) >> 6;
+        if (bitmap) {
+            for (int i = lane; i < nwords; i += 64) bm[i] = 0ull;
+            lds_wave_sync();
         }
         const int excl = incl - clen;
         int e[9], s[9];
@@ -153,11 +172,41 @@ __device__ __forceinline__ void grid_query_wave(const float *__restrict__ p, con
                 const int t = t0 + 64 * u + lane;
                 const bool hit = t < tot && lidar::dist2f(qv[u].x, qv[u].y, qv[u].z, cx, cy, cz) < r2;
                 const uint64_t mk = __ballot(hit);
-                if (hit) hw[hc + __popcll(mk & below)] = __float_as_int(qv[u].w);
+                if (hit) {
+                    if (bitmap) {
+                        const int o1 = __float_as_int(qv[u].w) - wlo;
+                        atomicOr(&bm[o1 >> 6], 1ull << (o1 & 63));
+                    } else {
+                        hw[hc + __popcll(mk & below)] = __float_as_int(qv[u].w);
+                    }
+                }
                 hc += __popcll(mk);
             }
         }
         if (hc == 0) continue;
+        if (bitmap) {
+            lds_wave_sync();
+            // the window's hits in index order: word c 64 + lane, ranked by the set bits before it
+            int base = 0, mnv = 0x7fffffff;
+            for (int c0 = 0; c0 < nwords && cnt + base < ns; c0 += 64) {
+                const int wi = c0 + lane;
+                unsigned long long wd = wi < nwords ? bm[wi] : 0ull;
+                const int pc = __popcll(wd);
+                const int ex = lidar::wave_incl_scan_i32(pc) - pc;  // hits of the lower words of the chunk
+                if (wd) mnv = min(mnv, wlo + 64 * wi + (int)__ffsll(wd) - 1);
+                int rk = cnt + base + ex;
+                while (wd && rk < ns) {
+                    const int j = __ffsll(wd) - 1;
+                    o[rk++] = wlo + 64 * wi + j;
+                    wd &= wd - 1;
+                }
+                base += __builtin_amdgcn_readlane(ex + pc, 63);
+            }
+            if (first < 0) first = (int)lidar::wave_min_u32_dpp((uint32_t)mnv);
+            cnt += hc;
+            lds_wave_sync();
+            continue;
+        }
         if (lane < 4) hw[hc + lane] = 0x7fffffff;
         lds_wave_sync();
         // rank every hit by index among the window's hits (indices are distinct)

@@ -222,6 +222,14 @@ __device__ __forceinline__ int row_incl_scan_i32(int v)
     v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);
     return v;
 }
+// inclusive prefix sum over the wave: the row scans above, then row_bcast 15 / 31 carry the rows' totals
+__device__ __forceinline__ int wave_incl_scan_i32(int v)
+{
+    v = row_incl_scan_i32(v);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);
+    return v;
+}
 __device__ __forceinline__ float wave_max_dpp(float v)
 {
     v = fmaxf(v, __int_as_float(dpp_i<0xB1>(__float_as_int(v))));

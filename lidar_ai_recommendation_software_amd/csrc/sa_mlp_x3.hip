@@ -223,11 +223,11 @@ __global__ __launch_bounds__(256, (BQ && !X1 && NS == 32) ? 5 : (R == 1 ? 3 : 2)
     // the cap would fall back to an index-order scan of the whole window
     constexpr int QCAP = NS >= 128 ? 2 * kBqCap : kBqCap;
     __shared__ int qidx[BQ ? 4 : 1][BQ ? NS : 1];           // this wave's ball-query result
-    __shared__ int qhits[BQ ? 4 : 1][BQ ? QCAP + 4 : 1];    // its per-window hit list
+    __shared__ __attribute__((aligned(8))) int qhits[BQ ? 4 : 1][BQ ? QCAP + 4 : 1];  // its per-window hits / bitmap
     if constexpr (BQ) {
         const float *pf = P + (int64_t)b * n * 3;
         const char *fw = grid_ws + b * lidar_bq::grid_frame_bytes(n);
-        lidar_bq::grid_query_wave<QCAP>(pf, fw, n, Q[cc * 3], Q[cc * 3 + 1], Q[cc * 3 + 2], r, r2, NS, lane,
+        lidar_bq::grid_query_wave<QCAP, int, (NS >= 64)>(pf, fw, n, Q[cc * 3], Q[cc * 3 + 1], Q[cc * 3 + 2], r, r2, NS, lane,
                                         qhits[wave], &qidx[wave][0]);
     }
     __syncthreads();

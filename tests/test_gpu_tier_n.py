@@ -215,6 +215,23 @@ def test_ball_query_grid_edge_frames(cuda, name, r, ns):
         assert np.array_equal(got, want), f"{mode}: {(got != want).sum()} differ"
 
 
+@pytest.mark.parametrize("n,m,r,ns", [(200000, 600, 0.01, 32), (131072, 700, 0.4, 128), (40000, 500, 0.25, 300),
+                                      (65536, 800, 0.2, 32)])
+def test_ball_query_window_rankings(cuda, n, m, r, ns):
+    """The grid query ranks a window's hits by an LDS bitmap over the window's index span (windows of up
+    to 32 CAP indices, round 6) or by the hit list (larger windows: here the r = 0.01 frame, whose
+    ~4 expected hits per ball make one window of 2^18 indices); MSG's r = 0.4 / ns = 128 shape (~900
+    candidates, ~137 hits per 4 096-index window), a 300-sample query over several windows, SSG's SA1
+    shape — bit-exact against the oracle (the fused SA1 kernel runs the same grid_query_wave:
+    test_group_mlp_bq_matches_unfused and the bench-shape tests check its indices)."""
+    x = unit_frames(2, n, 17)
+    c = np.ascontiguousarray(x[:, ::n // m][:, :m])
+    xt, ct = torch.from_numpy(x).to(cuda), torch.from_numpy(c).to(cuda)
+    want = tier_n.ball_query(x, c, r, ns)
+    got = pn.ball_query(r, ns, xt, ct, mode="grid").cpu().numpy()
+    assert np.array_equal(got, want), f"{(got != want).sum()} differ"
+
+
 def test_ball_query_binned_reuse(cuda):
     """one binning (lidar_ball_query_bin_f32) serves queries at smaller, equal and larger
     radii and other nsample values, exactly."""

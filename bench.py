@@ -591,16 +591,18 @@ def voxel_leg(dev, rank, world, B=32, n=65536, voxel=0.05, steps=20, cpu=True):
     out = pn.voxel_downsample_batch(x, voxel)
     torch.cuda.synchronize(dev)
     # the timed loop leaves nvox on the device (no host read-back per call); checked afterwards
-    last = [None]
+    # a stream of batches: the outputs allocated once and written by every call, nvox left on the device
+    # (no host read-back per call) and checked afterwards
+    res = tuple(torch.empty_like(t) for t in out)
 
     def loop():
         for _ in range(steps):
-            last[0] = pn.voxel_downsample_batch(x, voxel, check=False)
+            pn.voxel_downsample_batch(x, voxel, check=False, out=res)
 
     el = sharding.timed(loop, dev, world)
-    pn.check_voxel_counts(last[0][3])
-    assert torch.equal(last[0][3], out[3]) and torch.equal(last[0][1], out[1]), "voxel path not deterministic"
-    del last
+    pn.check_voxel_counts(res[3])
+    assert torch.equal(res[3], out[3]) and torch.equal(res[1], out[1]), "voxel path not deterministic"
+    del res
     nv = int(out[3].sum().item())
     per_launch = el / steps
     algo = B * n * 16 + nv * 16
@@ -702,6 +704,9 @@ def main():
                     help="1: SA2's nested FPS and ball queries on the side streams as well (StreamingSSG l2_side; "
                          "1 213-1 227 vs 1 195-1 207 M pts/s in one A/B); 0: on the main stream")
     ap.add_argument("--rotate", type=int, default=8, help="distinct device-resident input batches the feed cycles over")
+    ap.add_argument("--hw-queues", type=int, default=0,
+                    help="GPU_MAX_HW_QUEUES for this process (HIP's hardware queues per priority level; 0: leave "
+                         "the environment's, HIP's default 4); set before HIP initialises")
     ap.add_argument("--no-fp32-mfma-leg", action="store_true",
                     help="skip the extra measurement of the native fp32-MFMA kernels (when --x3 is on)")
     ap.add_argument("--no-standalone", action="store_true",
@@ -727,6 +732,8 @@ def main():
                     help="file for the full record (rank 0); the last stdout line is the compact one")
     args = ap.parse_args()
 
+    if args.hw_queues:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, max(1, args.hw_queues)))
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         # N ranks, one per GPU: a child torch.distributed.run, started before any GPU call
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))

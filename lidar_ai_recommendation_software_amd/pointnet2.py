@@ -159,7 +159,7 @@ def farthest_point_sample(xyz, npoint, return_xyz=False, first_zero=None, prefix
     return (idx, new_xyz) if return_xyz else idx
 
 
-def voxel_downsample_batch(xyz, voxel, slot=0, check=True):
+def voxel_downsample_batch(xyz, voxel, slot=0, check=True, out=None):
     """Voxel downsampling of (B, N, 3) float32 CUDA frames on the whole chip
     (lidar_voxel_downsample_batch_f32; per frame equal to data_processing.voxel_downsample).
     Returns device tensors (centroids (B, N, 3), voxel_id (B, N) int32, counts (B, N) int32,
@@ -170,16 +170,25 @@ def voxel_downsample_batch(xyz, voxel, slot=0, check=True):
     nvox <= -2 is a library failure, never expected: -2 one of the launch's bounded in-launch waits
     timed out, -3 a bucket table that is not a partition of the frame.  check=True (default) reads
     nvox back (a host synchronisation on the stream) and raises LidarError on either; check=False
-    leaves nvox on the device (throughput loops: check_voxel_counts(nvox) later)."""
+    leaves nvox on the device (throughput loops: check_voxel_counts(nvox) later).  out: the four output
+    tensors of an earlier call of the same shape, written again (a stream of batches allocates once)."""
     _dev_check(xyz)
     if xyz.dtype != torch.float32 or xyz.dim() != 3 or xyz.shape[2] != 3:
         raise ValueError("xyz must be (B, N, 3) float32")
     B, N, _ = xyz.shape
     dev = xyz.device
-    cent = torch.empty((B, N, 3), dtype=torch.float32, device=dev)
-    vid = torch.empty((B, N), dtype=torch.int32, device=dev)
-    cnt = torch.empty((B, N), dtype=torch.int32, device=dev)
-    nvox = torch.empty(B, dtype=torch.int32, device=dev)
+    if out is not None:
+        cent, vid, cnt, nvox = out
+        if (tuple(cent.shape) != (B, N, 3) or tuple(vid.shape) != (B, N) or tuple(cnt.shape) != (B, N)
+                or tuple(nvox.shape) != (B,) or cent.dtype != torch.float32
+                or any(t.dtype != torch.int32 for t in (vid, cnt, nvox))):
+            raise ValueError("voxel_downsample_batch: out must be (B, N, 3) float32, (B, N) int32 x 2, (B,) int32")
+        _dev_check(cent, vid, cnt, nvox)
+    else:
+        cent = torch.empty((B, N, 3), dtype=torch.float32, device=dev)
+        vid = torch.empty((B, N), dtype=torch.int32, device=dev)
+        cnt = torch.empty((B, N), dtype=torch.int32, device=dev)
+        nvox = torch.empty(B, dtype=torch.int32, device=dev)
     if B and N:
         nat.call("lidar_voxel_downsample_batch_f32", nat.handle(dev.index, slot), nat.ptr(xyz), B, N,
                  float(voxel), nat.ptr(vid), nat.ptr(cent), nat.ptr(cnt), nat.ptr(nvox), nat.stream_ptr())

@@ -299,6 +299,26 @@ def test_voxel_beside_ssg_feed(cuda):
     del outs_v
 
 
+def test_voxel_batch_output_reuse(cuda):
+    """out=: a stream of batches writes the same four output tensors call after call (check=False leaves
+    nvox on the device); every call equals a fresh call, and a mismatched out is refused."""
+    import torch
+    from lidar_ai_recommendation_software_amd import pointnet2 as pn
+    from lidar_ai_recommendation_software_amd.synthetic import unit_frames
+    xs = [torch.from_numpy(unit_frames(4, 30000, 50 + i)).to(cuda) for i in range(3)]
+    res = pn.voxel_downsample_batch(xs[0], 0.05)
+    for x in xs[1:] + xs[:1]:
+        pn.voxel_downsample_batch(x, 0.05, check=False, out=res)
+        want = pn.voxel_downsample_batch(x, 0.05)
+        pn.check_voxel_counts(res[3])
+        assert torch.equal(res[3], want[3]) and torch.equal(res[1], want[1])
+        for f in range(4):
+            v = int(want[3][f])
+            assert torch.equal(res[0][f, :v], want[0][f, :v]) and torch.equal(res[2][f, :v], want[2][f, :v])
+    with pytest.raises(ValueError, match="out must be"):
+        pn.voxel_downsample_batch(xs[0][:2].contiguous(), 0.05, out=res)
+
+
 @pytest.mark.parametrize("case", ["wide_keys", "lidar_sparse", "runs_128", "runs_129", "runs_600"])
 def test_voxel_bucket_sort_paths(cuda, case):
     """The bucket launch's sorts: the LDS counting sort (runs of up to SEGMAX = 128 equal keys ordered by

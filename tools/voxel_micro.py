@@ -17,7 +17,9 @@ f = unit_frames(B, N, 0)
 if scale != 1.0:
     f = (f * [scale, scale, scale / 200]).astype("float32")
 x = torch.from_numpy(f).to("cuda:0")
-for _ in range(20):
-    pn.voxel_downsample_batch(x, voxel)
+res = pn.voxel_downsample_batch(x, voxel)
+for _ in range(19):
+    pn.voxel_downsample_batch(x, voxel, check=False, out=res)
 torch.cuda.synchronize()
+pn.check_voxel_counts(res[3])
 print("ok")

@@ -716,6 +716,8 @@ def main():
     ap.add_argument("--msg-steps", type=int, default=30)
     ap.add_argument("--msg-group", type=int, default=3, help="configs[4] leg: batches per SA1-FPS launch")
     ap.add_argument("--msg-depth", type=int, default=3, help="configs[4] leg: side streams")
+    ap.add_argument("--msg-fps-threads", type=int, default=0, choices=[0, 512, 1024],
+                    help="configs[4] leg: SA1 FPS workgroup size (0: --fps-threads)")
     ap.add_argument("--no-host-feed", action="store_true", help="skip the host-frame (PCIe-inclusive) SSG leg")
     ap.add_argument("--msg-side-ns", type=int, default=0,
                     help="configs[4] leg: level-0 branches of >= this many samples answer their ball queries on "
@@ -757,7 +759,7 @@ def main():
     local_ms = {}  # this rank's own window time per leg (the line reports the max over ranks)
 
     def measure(key, cfg, dtype, B, N, steps, warmup, depth, G, x3=True, events=True, side_query_ns=None,
-                host=False, bb=None, xs=None, refs=None):
+                host=False, bb=None, xs=None, refs=None, fps_threads=None):
         """Steady-state window of `steps` batches through StreamingSSG's feed.  events: HIP
         events around every launch inside the timed window (the headline: the roofline durations
         come from the same window); False: the window runs clean and the per-kernel durations come
@@ -777,7 +779,7 @@ def main():
         hxs = [x.cpu().numpy() for x in xs] if host else None
         ready = torch.cuda.Event()  # the inputs exist: the feed's FPS launches wait only for their slots
         ready.record()
-        pipe = pn.StreamingSSG(bb, B, N, depth=depth, fps_group=G, fps_threads=args.fps_threads,
+        pipe = pn.StreamingSSG(bb, B, N, depth=depth, fps_group=G, fps_threads=fps_threads or args.fps_threads,
                                ramp=False,
                                slots=args.slots or None, bq=args.bq,
                                l2_side=bool(args.l2_side), side_query_ns=side_query_ns)
@@ -881,7 +883,8 @@ def main():
             g2 = pick_group(st2, args.msg_group if msg else 3)
             d2 = args.msg_depth if msg else 3
             sq = (args.msg_side_ns or None) if cfg is pn.MSG else None
-            el2, t2, _, _, _ = measure(key, cfg, dtype, b2, n2, st2, 1, d2, g2, events=False, side_query_ns=sq)
+            el2, t2, _, _, _ = measure(key, cfg, dtype, b2, n2, st2, 1, d2, g2, events=False, side_query_ns=sq,
+                                       fps_threads=(args.msg_fps_threads or None) if msg else None)
             pl2 = {k: t / c for k, (c, f, t) in t2.items()}
             # the two chains per group: the side streams' FPS / binning / queries (3 streams) and the
             # main stream's MLP kernels, from the per-launch HIP-event durations of the second window

@@ -1,0 +1,13 @@
+set -o pipefail
+R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/r06/msgfps; mkdir -p $O; cd $R
+LIDAR_AMD_LIB=$R/tools/ablib/ppl2.so timeout -k 10 600 python -u -m pytest tests/test_gpu_tier_n.py -q --timeout 300 --timeout-method thread -k "fps or msg" > $O/tests_ppl2.log 2>&1 || exit 11
+for rep in 1 2; do
+for arm in prod t1024 ppl2; do
+L=$R/lidar_ai_recommendation_software_amd/liblidar_amd.so; X=""
+case $arm in t1024) X="--msg-fps-threads 1024";; ppl2) L=$R/tools/ablib/ppl2.so;; esac
+LIDAR_AMD_LIB=$L timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 --no-density --no-fp32-mfma-leg --no-standalone --no-cpu-baseline --no-host-feed $X --detail $O/d_${arm}_$rep.json > $O/b_${arm}_$rep.json 2> $O/b_${arm}_$rep.err || exit 12
+python3 -c "
+import json;d=json.load(open('$O/d_${arm}_$rep.json'));m=d['other_configs']['configs[4]_msg_131k_bf16'];k=m['kernel_ms_per_launch']
+print('$arm rep $rep ssg', round(d['value'],1), '| msg', round(m['M_points_per_s'],1), {kk:round(v,2) for kk,v in m['chains_ms_per_group'].items()}, 'fps', round(k['sa1_fps'],2), 'b2', round(k['sa1_b2_group_mlp'],2), 'l1', round(k['sa2_layer1_points'],2), 'sa2b2', round(k['sa2_b2_group_mlp'],2))"
+done
+done

@@ -719,6 +719,7 @@ def main():
     ap.add_argument("--msg-fps-threads", type=int, default=0, choices=[0, 512, 1024],
                     help="configs[4] leg: SA1 FPS workgroup size (0: --fps-threads)")
     ap.add_argument("--no-host-feed", action="store_true", help="skip the host-frame (PCIe-inclusive) SSG leg")
+    ap.add_argument("--host-threads", type=int, default=4, help="host-frame leg: threads filling the pinned ring (4: 1 062-1 083, 8: 1 011-1 053, 16: 998-1 057 M points/s in one A/B)")
     ap.add_argument("--msg-side-ns", type=int, default=0,
                     help="configs[4] leg: level-0 branches of >= this many samples answer their ball queries on "
                          "the side streams (StreamingSSG side_query_ns; 0: every branch fused on the main stream)")
@@ -784,7 +785,8 @@ def main():
                                slots=args.slots or None, bq=args.bq,
                                l2_side=bool(args.l2_side), side_query_ns=side_query_ns)
         feed = pipe.feed()
-        push = (lambda i: feed.push_host(hxs[i % nb])) if host else (lambda i: feed.push(xs[i % nb], ready))
+        push = ((lambda i: feed.push_host(hxs[i % nb], threads=args.host_threads)) if host
+                else (lambda i: feed.push(xs[i % nb], ready)))
         nwarm = (depth + max(1, warmup)) * G  # whole groups; `depth` groups in flight when the window opens
         outs = []
         for i in range(nwarm):
@@ -833,8 +835,8 @@ def main():
                                    x3=bool(args.x3), events=False, host=True, bb=bb, xs=xs, refs=refs)
         host_feed = {"value": sharding.aggregate_rate(B * N * args.steps, world, el_h) / 1e6, "unit": "M points/s",
                      "ms_per_step": el_h / args.steps * 1e3,
-                     "input": "host NumPy (B, N, 3) float32 batches -> feed().push_host (8 host threads into a "
-                              "pinned ring, H2D on the side streams ahead of each group's FPS)",
+                     "input": f"host NumPy (B, N, 3) float32 batches -> feed().push_host ({args.host_threads} host threads "
+                              "into a pinned ring, H2D on the side streams ahead of each group's FPS)",
                      "parity": "every output bit-equal to forward() of the same batch"}
     fp32_mfma = None
     if args.x3 and not args.no_fp32_mfma_leg:

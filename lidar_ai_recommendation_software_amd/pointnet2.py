@@ -1140,7 +1140,7 @@ class _Feed:
         self.readies = []  # push()'s ready event per buffered batch
         self._ring, self._ri, self._pool = [], 0, None  # push_host's pinned buffers and copy threads
 
-    def push_host(self, frames, threads=8):
+    def push_host(self, frames, threads=4):
         """frames: one batch of host frames, a (B, N, 3) array or B arrays of shape (N, 3), of any real
         dtype (converted to float32 as numpy's astype does).  They are copied into a pinned buffer by
         `threads` host threads (frames split between them; numpy releases the GIL in the copy), and the

@@ -302,11 +302,15 @@ def rel_stats(got, want, rtol=1e-4):
             "max_tol_ratio": float((err / (rtol * np.abs(want) + rtol * rms)).max())}
 
 
-def precision_check(bb, xs, cfg, n, picks=((0, 0), (0, 31), (2, 0), (3, 31))):
-    """Frames of the bench's first group (picks: (batch, frame) — frames 0, 31, 64 and 127 of a
-    4 x 32-frame group) through forward(keep_levels) against the fp32 oracle (the checker, in the
-    CPU-baseline leg): per level and for the global feature the worst rel_stats over the frames,
-    each frame's own numbers beside; FPS indices compared bit for bit."""
+PRECISION_PICKS = tuple((b, 0) for b in range(8)) + ((0, 31), (7, 31))
+
+
+def precision_check(bb, xs, cfg, n, picks=PRECISION_PICKS):
+    """Frames of the bench's input batches (picks: (batch, frame) — the first frame of each of the 8
+    rotating 32-frame batches, both groups of the driver's window, and the last frame of the first and
+    last batch) through forward(keep_levels) against the fp32 oracle (the checker, in the CPU-baseline
+    leg): per level and for the global feature the worst rel_stats over the frames, each frame's own
+    numbers beside; FPS indices compared bit for bit."""
     import torch
     from oracle import tier_n
     from lidar_ai_recommendation_software_amd import pointnet2 as pn
@@ -716,6 +720,8 @@ def main():
     ap.add_argument("--msg-steps", type=int, default=30)
     ap.add_argument("--msg-group", type=int, default=3, help="configs[4] leg: batches per SA1-FPS launch")
     ap.add_argument("--msg-depth", type=int, default=3, help="configs[4] leg: side streams")
+    ap.add_argument("--no-layer1-fuse", action="store_true",
+                    help="configs[4] leg: one per-point layer-1 GEMM per branch (pointnet2.FUSE_LAYER1 off)")
     ap.add_argument("--msg-fps-threads", type=int, default=0, choices=[0, 512, 1024],
                     help="configs[4] leg: SA1 FPS workgroup size (0: --fps-threads)")
     ap.add_argument("--no-host-feed", action="store_true", help="skip the host-frame (PCIe-inclusive) SSG leg")
@@ -825,6 +831,7 @@ def main():
         return elapsed, timers.totals(), bb, xs, refs
 
     tot_x3 = None
+    pn.FUSE_LAYER1 = not args.no_layer1_fuse
     elapsed, tot, bb, xs, refs = measure("ssg", pn.SSG, "f32", B, N, args.steps, args.warmup, args.depth, G,
                                          x3=bool(args.x3))
     host_feed = None
@@ -1052,7 +1059,7 @@ def main():
         }
         if not args.no_cpu_baseline:
             # rank 0 at every world size, after the timed windows (the other ranks wait at the
-            # final barrier); the oracle also checks frames 0, 31, 64 and 127 of the bench's first group
+            # final barrier); the oracle also checks ten frames spread over the 8 input batches
             rec["cpu_baseline"] = cpu_baseline(N, args.cpu_budget)
             rec["speedup_vs_cpu"] = value / rec["cpu_baseline"]["value"]
             rec["precision"] = precision_check(bb, xs, pn.SSG, N)

@@ -315,8 +315,9 @@ def pack_branch_x1(layers):
 
 def group_mlp_x1(p, idx, n, packed, widths, out, out_offset=0, xyz=None, centres=None):
     """One SA branch in the bf16 spec (lidar_sa_group_mlp_x1_f32).  xyz level: p = the level's
-    points (B, n, 3), centres (B, M, 3).  Feature level: p (B*n, stride) = bf16(f) bf16(W1_f) + b1
-    per point (layer1_points_x1), xyz = the level's points, centres."""
+    points (B, n, 3), centres (B, M, 3).  Feature level: p (B*n, >= c1) = bf16(f) bf16(W1_f) + b1
+    per point (layer1_points_x1): rows of one stride, possibly a column slice of the level's fused
+    layer-1 output; xyz = the level's points, centres."""
     B, M, ns = idx.shape
     c1, c2, c3 = widths
     mode = 2 if xyz is not None else 0
@@ -324,9 +325,11 @@ def group_mlp_x1(p, idx, n, packed, widths, out, out_offset=0, xyz=None, centres
         _dev_check(p, centres, idx, packed, out)
         stride = 3
     else:
-        _dev_check(p, xyz, centres, idx, packed, out)
-        stride = p.shape[-1]
-        if p.shape[0] < B * n or stride < c1:
+        _dev_check(xyz, centres, idx, packed, out)
+        if not p.is_cuda or p.dim() != 2 or p.stride(1) != 1:
+            raise ValueError("group_mlp_x1: per-point rows must be a CUDA (rows, cols) tensor with unit column stride")
+        stride = p.stride(0)
+        if p.shape[0] < B * n or p.shape[1] < c1:
             raise ValueError("group_mlp_x1: per-point rows do not match the batch")
     nat.call("lidar_sa_group_mlp_x1_f32", nat.handle(p.device.index), mode, nat.ptr(p), stride,
              nat.ptr(centres) if mode == 0 else None, nat.ptr(xyz), nat.ptr(centres), nat.ptr(idx), B, n, M, ns,
@@ -334,15 +337,39 @@ def group_mlp_x1(p, idx, n, packed, widths, out, out_offset=0, xyz=None, centres
     return out
 
 
-def layer1_points_x1(x_rows, xyz, cfeat, branches):
+def layer1_points_x1(x_rows, xyz, cfeat, branches, cat=None):
     """Per-point layer-1 feature part of a bf16-spec level: P = bf16(f) bf16(W1_f) + b1 for every
     branch (x_rows: the level's padded rows [f, x, y, z, 0-pad]; the xyz rows of W1_f are zero,
-    the offsets' part runs per grouped row in lidar_sa_group_mlp_x1_f32)."""
+    the offsets' part runs per grouped row in lidar_sa_group_mlp_x1_f32).  cat: the branches' W1_f
+    side by side (fused_layer1_x1): one GEMM reads the rows once for every branch, and each branch's
+    P is its column slice — the same products in the same order per column (the bf16 spec's image has
+    no per-matrix scale), so bit-identical to one GEMM per branch."""
     B, N, _ = xyz.shape
     nat.call("lidar_concat_xyz_pad_f32", nat.handle(xyz.device.index), nat.ptr(xyz), B * N, nat.ptr(x_rows),
              x_rows.shape[1], cfeat, nat.stream_ptr())
+    if cat is not None:
+        full = dense_x3s(x_rows, cat["w1f_x1"], cat["b1"], cat["w1f"].shape[1], relu=False, x1=True)
+        return [full[:, o:o + w] for o, w in cat["cols"]]
     return [dense_x3s(x_rows, br["pre_x1"]["w1f_x1"], br["pre_x1"]["b1"], br["pre_x1"]["w1f"].shape[1],
                       relu=False, x1=True) for br in branches]
+
+
+FUSE_LAYER1 = True  # backbones built while True fuse a bf16 level's per-point layer-1 GEMMs (A/B switch)
+
+
+def fused_layer1_x1(branches):
+    """The bf16-spec branches' per-point layer-1 weights side by side: {"w1f" (k, sum cp), "b1", "w1f_x1"
+    (the packed image), "cols": [(column offset, cp) per branch]} — None for fewer than two branches."""
+    if len(branches) < 2 or any("pre_x1" not in br for br in branches):
+        return None
+    ws = [br["pre_x1"]["w1f"] for br in branches]
+    cols, o = [], 0
+    for w in ws:
+        cols.append((o, w.shape[1]))
+        o += w.shape[1]
+    w1f = torch.cat(ws, dim=1).contiguous()
+    b1 = torch.cat([br["pre_x1"]["b1"] for br in branches]).contiguous()
+    return {"w1f": w1f, "b1": b1, "w1f_x1": pack_dense_x3(w1f, x1=True), "cols": cols}
 
 
 def group_mlp_x3(p, q, idx, n, packed, widths, out, out_offset=0, xyz_level=False):
@@ -741,6 +768,8 @@ class PointNet2Backbone:
             entry = {"div": lvl["npoint_div"], "branches": branches, "cfeat": cfeat}
             if not xyz_level:  # the previous level writes this level's padded rows [f, x, y, z, 0]
                 entry.update(pre=True, k=kp)
+                if self.bf16 and FUSE_LAYER1 and all("pre_x1" in br for br in branches):
+                    entry["pre_x1_cat"] = fused_layer1_x1(branches)  # one layer-1 GEMM for every branch
             self.levels.append(entry)
             cfeat = sum(w[-1] for w in lvl["mlps"])
         self.out_channels = cfeat
@@ -801,7 +830,9 @@ class PointNet2Backbone:
             if lvl.get("pre") and fb:
                 fbr = [lvl["branches"][i] for i in fb]
                 if self.bf16:
-                    res = _call(t, f"sa{li + 1}_layer1_points", B, layer1_points_x1, rows, xyz, lvl["cfeat"], fbr)
+                    cat = lvl.get("pre_x1_cat") if len(fbr) == len(lvl["branches"]) else None
+                    res = _call(t, f"sa{li + 1}_layer1_points", B, layer1_points_x1, rows, xyz, lvl["cfeat"], fbr,
+                                cat=cat)
                 else:
                     res = _call(t, f"sa{li + 1}_layer1_points", B, layer1_per_point, rows, xyz, lvl["cfeat"],
                                 new_xyz, fbr, x3=self.x3)

@@ -688,6 +688,34 @@ def test_streaming_host_feed_matches_forward(cuda, G, depth, dtype, mixed):
         feed.push_host(hx[0][:1])
 
 
+def test_fused_layer1_x1_matches_per_branch(cuda):
+    """MSG's level-2 per-point layer 1 in the bf16 spec: one GEMM over the three branches' W1_f side by side
+    (fused_layer1_x1) gives every branch's P bit for bit as its own GEMM does, and forward() over the fused
+    level equals forward() with the fused weights removed."""
+    bb = pn.PointNet2Backbone(pn.MSG, device=cuda, seed=8, dtype="bf16")
+    lvl = bb.levels[1]
+    assert lvl.get("pre_x1_cat") is not None
+    x = torch.from_numpy(unit_frames(2, 8192, 91)).to(cuda)
+    _, levels = bb.forward(x, keep_levels=True)
+    feats = levels[0][1]  # level 1's features (B, M1, 320)
+    M1 = feats.shape[1]
+    R = (2 * M1 + 127) // 128 * 128
+    rows = torch.zeros((R, lvl["k"]), dtype=torch.float32, device=cuda)
+    rows[:2 * M1, :feats.shape[2]] = feats.reshape(2 * M1, -1)
+    cen = levels[0][0].contiguous()
+    got = pn.layer1_points_x1(rows.clone(), cen, lvl["cfeat"], lvl["branches"], cat=lvl["pre_x1_cat"])
+    want = pn.layer1_points_x1(rows.clone(), cen, lvl["cfeat"], lvl["branches"])
+    for g, w in zip(got, want):
+        assert g.shape == w.shape and torch.equal(g, w)
+    g1, _ = bb.forward(x)
+    cat = lvl.pop("pre_x1_cat")
+    try:
+        g2, _ = bb.forward(x)
+    finally:
+        lvl["pre_x1_cat"] = cat
+    assert torch.equal(g1, g2)
+
+
 def test_streaming_feed_steady_state(cuda):
     """the persistent feed bench.py times: push() keeps `depth` groups in flight; after the fill
     every group of G pushes completes exactly G batches, in order; flush() drains the rest."""

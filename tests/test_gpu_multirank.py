@@ -98,3 +98,38 @@ def test_bench_configs3_eight_ranks_on_one_gpu(cuda, tmp_path):
         assert w1["world"] == 1 and w1["seed_rank"] == rank
         assert w8["digests"] == w1["digests"], f"rank {rank}: outputs differ from its 1-rank run"
     assert json.load(open(tmp_path / "w8.rank0.json"))["digests"] != json.load(open(tmp_path / "w8.rank7.json"))["digests"]
+
+
+ARGS_C4 = ["--batch", "4", "--points", "8192", "--steps", "3", "--warmup", "1", "--rotate", "2", "--msg-batch", "32",
+           "--msg-steps", "3", "--no-density", "--no-cpu-baseline", "--no-fp32-mfma-leg", "--no-standalone",
+           "--no-host-feed"]
+
+
+@pytest.mark.timeout(900)
+def test_bench_configs4_eight_ranks_on_one_gpu(cuda, tmp_path):
+    """BASELINE configs[4] (the MSG bf16 stack on 131 072-point frames over 8 GPUs) through bench.py's
+    8-rank path on the one GPU: its MSG leg runs 32 frames of that shape per rank (the per-GPU share of
+    256); ranks 0 and 7 compute exactly what their own frames give in a 1-rank run.  A rehearsal of the
+    8-GPU code path (the ranks share one GPU), not a scaling measurement."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="2")
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, "-u", "bench.py", "--gpus", "8", *ARGS_C4, "--dump", str(tmp_path / "w8"),
+           "--detail", str(tmp_path / "detail.json")]
+    r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=800)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    line = _last_json(r.stdout)
+    assert line["n_gpus"] == 8 and line["distributed"]["world_size"] == 8
+    msg = json.load(open(tmp_path / "detail.json"))["other_configs"]["configs[4]_msg_131k_bf16"]
+    assert msg["frames_per_gpu"] == 32 and msg["points_per_frame"] == 131072
+    key = "configs[4]_msg_131k_bf16"
+    for rank in (0, 7):
+        w8 = json.load(open(tmp_path / f"w8.rank{rank}.json"))
+        assert w8["world"] == 8 and key in w8["digests"]
+        r1 = subprocess.run([sys.executable, "bench.py", *ARGS_C4, "--seed-rank", str(rank), "--dump",
+                             str(tmp_path / f"w1_{rank}")], cwd=REPO, env=env, capture_output=True, text=True,
+                            timeout=400)
+        assert r1.returncode == 0, r1.stderr[-4000:]
+        w1 = json.load(open(tmp_path / f"w1_{rank}.rank0.json"))
+        assert w8["digests"][key] == w1["digests"][key], f"rank {rank}: MSG outputs differ from its 1-rank run"
+    assert json.load(open(tmp_path / "w8.rank0.json"))["digests"][key] != \
+        json.load(open(tmp_path / "w8.rank7.json"))["digests"][key]

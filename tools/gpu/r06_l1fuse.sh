@@ -1,6 +1,6 @@
 set -o pipefail
 R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/r06/l1fuse; mkdir -p $O; cd $R
-timeout -k 10 600 python -u -m pytest tests/test_gpu_tier_n.py -q --timeout 300 --timeout-method thread -k "fused_layer1 or msg or bf16" > $O/tests.log 2>&1 || exit 11
+timeout -k 10 600 python -u -m pytest tests/test_gpu_tier_n.py -q --timeout 300 --timeout-method thread -k "fused_layer1 or msg or bf16" > $O/tests.log 2>&1 && timeout -k 10 900 python -u -m pytest tests/test_gpu_multirank.py -q --timeout 900 --timeout-method thread -k configs4 >> $O/tests.log 2>&1 || exit 11
 for rep in 1 2; do
 for arm in fuse nofuse; do
 X=""; [ $arm = nofuse ] && X="--no-layer1-fuse"

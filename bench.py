@@ -726,9 +726,6 @@ def main():
                     help="configs[4] leg: SA1 FPS workgroup size (0: --fps-threads)")
     ap.add_argument("--no-host-feed", action="store_true", help="skip the host-frame (PCIe-inclusive) SSG leg")
     ap.add_argument("--host-threads", type=int, default=4, help="host-frame leg: threads filling the pinned ring (4: 1 062-1 083, 8: 1 011-1 053, 16: 998-1 057 M points/s in one A/B)")
-    ap.add_argument("--msg-side-ns", type=int, default=0,
-                    help="configs[4] leg: level-0 branches of >= this many samples answer their ball queries on "
-                         "the side streams (StreamingSSG side_query_ns; 0: every branch fused on the main stream)")
     ap.add_argument("--no-extras", action="store_true", help="skip the configs[1]/[4] side measurements")
     ap.add_argument("--no-density", action="store_true", help="skip the Tier R / variant / voxel / host-frame legs")
     ap.add_argument("--seed-rank", type=int, default=None,
@@ -765,7 +762,7 @@ def main():
     digests = {}
     local_ms = {}  # this rank's own window time per leg (the line reports the max over ranks)
 
-    def measure(key, cfg, dtype, B, N, steps, warmup, depth, G, x3=True, events=True, side_query_ns=None,
+    def measure(key, cfg, dtype, B, N, steps, warmup, depth, G, x3=True, events=True,
                 host=False, bb=None, xs=None, refs=None, fps_threads=None):
         """Steady-state window of `steps` batches through StreamingSSG's feed.  events: HIP
         events around every launch inside the timed window (the headline: the roofline durations
@@ -789,7 +786,7 @@ def main():
         pipe = pn.StreamingSSG(bb, B, N, depth=depth, fps_group=G, fps_threads=fps_threads or args.fps_threads,
                                ramp=False,
                                slots=args.slots or None, bq=args.bq,
-                               l2_side=bool(args.l2_side), side_query_ns=side_query_ns)
+                               l2_side=bool(args.l2_side))
         feed = pipe.feed()
         push = ((lambda i: feed.push_host(hxs[i % nb], threads=args.host_threads)) if host
                 else (lambda i: feed.push(xs[i % nb], ready)))
@@ -891,8 +888,7 @@ def main():
             msg = cfg is pn.MSG
             g2 = pick_group(st2, args.msg_group if msg else 3)
             d2 = args.msg_depth if msg else 3
-            sq = (args.msg_side_ns or None) if cfg is pn.MSG else None
-            el2, t2, _, _, _ = measure(key, cfg, dtype, b2, n2, st2, 1, d2, g2, events=False, side_query_ns=sq,
+            el2, t2, _, _, _ = measure(key, cfg, dtype, b2, n2, st2, 1, d2, g2, events=False,
                                        fps_threads=(args.msg_fps_threads or None) if msg else None)
             pl2 = {k: t / c for k, (c, f, t) in t2.items()}
             # the two chains per group: the side streams' FPS / binning / queries (3 streams) and the
@@ -900,7 +896,7 @@ def main():
             side_k = [k for k in pl2 if k.endswith("_fps") or "_bq_bin" in k or "_ball_query" in k]
             extras[key] = {"M_points_per_s": sharding.aggregate_rate(b2 * n2 * st2, world, el2) / 1e6,
                            "ms_per_step": el2 / st2 * 1e3, "frames_per_gpu": b2, "points_per_frame": n2,
-                           "dtype": dtype, "batches_per_group": g2, "side_streams": d2, "side_query_ns": sq,
+                           "dtype": dtype, "batches_per_group": g2, "side_streams": d2,
                            "chains_ms_per_group": {"main": sum(v for k, v in pl2.items() if k not in side_k),
                                                    "side": sum(pl2[k] for k in side_k) / d2,
                                                    "step_ms_per_group": el2 / st2 * 1e3 * g2},

@@ -964,7 +964,7 @@ class StreamingSSG:
 
     def __init__(self, backbone, batch, n, depth=1, fps_group=1, fps_threads=0, side_priority=0,
                  ramp=True,
-                 reserve=True, keep_levels=False, slots=None, bq="bin", l2_side=False, side_query_ns=None):
+                 reserve=True, keep_levels=False, slots=None, bq="bin", l2_side=False):
         """fps_threads: SA1 FPS workgroup size (0 = 1024; 512: half the CU footprint beside the
         MLPs).  ramp: in run(), the first groups hold 1, 2, ... batches (a shorter pipeline fill).
         slots: staging slots (>= depth + 1; default depth + 3).  Group k's FPS reuses the slot of
@@ -975,11 +975,7 @@ class StreamingSSG:
         [ball-query idx per branch])) instead of the global feature alone.  l2_side: level 1's FPS
         (nested: the prefix shortcut over SA1's centroids) and ball queries depend only on SA1's
         FPS output, so they run on the side stream too (the main stream then runs only MLP work
-        and level 1's per-point layer 1).  side_query_ns: with bq="bin", a level-0 branch of at
-        least this many samples also answers its ball queries on the side stream (from the same
-        grid), and the main stream runs its MLP on the given indices (bit-identical).  Off by
-        default: for configs[4]'s MSG pipeline (ns = 128 / 32 / 16) it measured 462-475 against
-        502-535 M points/s fused.
+        and level 1's per-point layer 1).
 
         Host frames: feed().push_host(frames) takes a batch of host NumPy frames, stages it in
         pinned memory (parallel host threads) and copies it to the device on the group's side
@@ -1011,10 +1007,9 @@ class StreamingSSG:
         self.idx = [torch.empty((GB, self.M1), dtype=torch.int32, device=dev) for _ in range(nslot)]
         self.cxyz = [torch.empty((GB, self.M1, 3), dtype=torch.float32, device=dev) for _ in range(nslot)]
         self.fz = [torch.empty(GB, dtype=torch.int32, device=dev) for _ in range(nslot)]
-        # level-0 ball-query indices computed on the side streams: every branch with bq="side",
-        # the branches of >= side_query_ns samples with bq="bin" (None: the MLP kernel answers them)
-        self.side_q = [bq == "side" or (bq == "bin" and side_query_ns is not None and br["ns"] >= side_query_ns)
-                       for br in lvl0["branches"]]
+        # level-0 ball-query indices computed on the side streams (bq="side"; with "bin" the MLP kernel
+        # answers them from the side streams' grids)
+        self.side_q = [bq == "side" for br in lvl0["branches"]]
         self.gidx = [[torch.empty((GB, self.M1, br["ns"]), dtype=torch.int32, device=dev) if sq else None
                       for br, sq in zip(lvl0["branches"], self.side_q)]
                      for _ in range(nslot)] if any(self.side_q) else None
@@ -1080,9 +1075,6 @@ class StreamingSSG:
                           out=self.gidx[slot][bi_][:g], slot=hs)
                 elif self.bq == "bin":  # depends only on the points: the queries run on the main stream
                     _call(t, f"{tag}_bq_bin", g, ball_query_bin, br["r"], br["ns"], x, self.grid[slot][bi_], slot=hs)
-                    if self.side_q[bi_]:  # ... or here, from the same grid
-                        _call(t, f"{tag}_ball_query", g, ball_query, br["r"], br["ns"], x, self.cxyz[slot][:g],
-                              out=self.gidx[slot][bi_][:g], slot=hs, grid=self.grid[slot][bi_])
             if self.l2:
                 c1 = self.cxyz[slot][:g]
                 _call(t, "sa2_fps", g, farthest_point_sample, c1, self.M2, return_xyz=True,

@@ -640,27 +640,6 @@ def test_streaming_bench_policy_matches_forward(cuda, group, depth, threads, nb,
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("side_ns,dtype", [(None, "bf16"), (16, "bf16"), (32, "bf16"), (128, "bf16"), (16, "f32")])
-def test_streaming_side_queries_match_forward(cuda, side_ns, dtype):
-    """MSG (configs[4]'s branches ns 16 / 32 / 128): the level-0 branches of >= side_query_ns samples
-    answer their ball queries on the side streams from the binned grid, the main stream runs their
-    MLPs on the given indices, the others stay fused; bit-identical to forward() (fused everywhere),
-    indices included."""
-    bb = pn.PointNet2Backbone(pn.MSG, device=cuda, seed=6, dtype=dtype)
-    xs = [torch.from_numpy(unit_frames(2, 8192, 80 + s)).to(cuda) for s in range(5)]
-    want = [bb.forward(x, keep_levels=True) for x in xs]
-    got = pn.StreamingSSG(bb, 2, 8192, depth=2, fps_group=2, fps_threads=512, bq="bin", l2_side=True,
-                          keep_levels=True, side_query_ns=side_ns).run(xs)
-    torch.cuda.synchronize()
-    assert len(got) == len(xs)
-    for (g, lv), (wg, wlv) in zip(got, want):
-        assert torch.equal(g, wg)
-        for (nx, nf, ni, ngi), (wx, wf, wi, wgi) in zip(lv, wlv):
-            assert torch.equal(nf, wf) and torch.equal(ni, wi)
-            for a, b in zip(ngi, wgi):
-                assert a is not None and torch.equal(a, b)
-
-
 @pytest.mark.parametrize("G,depth,dtype,mixed", [(1, 2, np.float32, False), (3, 2, np.float64, False),
                                                  (2, 3, np.float32, True), (4, 3, np.float32, False)])
 def test_streaming_host_feed_matches_forward(cuda, G, depth, dtype, mixed):

@@ -1,6 +1,6 @@
 """configs[4] (MSG, bf16 spec, 131 072-point frames, 32 per step) through StreamingSSG at several
 (depth, group) settings: wall ms per 32-frame batch in the steady state, timed as bench.py does (the window
-starts and ends with `depth` groups in flight; its extras leg uses depth 3 and G = pick_group(steps, 3)).  usage: python tools/msg_pipe.py [steps [unused [depth,G[,side_query_ns] ...]]]"""
+starts and ends with `depth` groups in flight; its extras leg uses depth 3 and G = pick_group(steps, 3)).  usage: python tools/msg_pipe.py [steps [unused [depth,G[,unused] ...]]]"""
 import os
 import sys
 import time
@@ -24,7 +24,7 @@ ready.record()
 _skip = [torch.cuda.Stream(device=dev) for _ in range(int(os.environ.get("MSG_SKIP_STREAMS", "0")))]
 prio = int(os.environ.get("MSG_PRIO", "0"))
 for depth, G, sq in settings:
-    pipe = pn.StreamingSSG(bb, B, N, depth=depth, fps_group=G, fps_threads=512, side_priority=prio, ramp=False, bq="bin", l2_side=True, side_query_ns=sq or None)
+    pipe = pn.StreamingSSG(bb, B, N, depth=depth, fps_group=G, fps_threads=512, side_priority=prio, ramp=False, bq="bin", l2_side=True)
     feed = pipe.feed()
     for i in range((depth + 1) * G):
         feed.push(xs[i % 4], ready)

@@ -1233,6 +1233,19 @@ class _Feed:
         self.buf, self.readies = [], []
         return self._issue(xs, evs)
 
+    def close(self):
+        """Stop push_host's copy threads (the pinned ring is freed with the feed)."""
+        if self._pool is not None:
+            self._pool.shutdown(wait=False)
+            self._pool = None
+            self._ring = []
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
     def flush(self, trim=True):
         """Issue a partial last group and drain the pipeline.  trim: then wait for the side streams
         and free the workspaces the library's handles retired while growing (lidar_trim)."""

@@ -1036,6 +1036,18 @@ class StreamingSSG:
         for e in self.slot_free:
             e.record(torch.cuda.current_stream(dev))
 
+    def _stage(self, slot, fs):
+        """The slot's staging buffer (allocated on first use when G = 1) — from the pool of the side stream
+        that writes it: a block the caching allocator took from the main stream's pool could be one a
+        main-stream pass still queued on the device has just freed, and the side stream does not wait
+        for the main stream.  Main-stream passes read it too (record_stream: its block outlives them)."""
+        if self.stage[slot] is None:
+            with torch.cuda.stream(fs):
+                st = torch.empty((self.G * self.B, self.N, 3), dtype=torch.float32, device=self.bb.device)
+            st.record_stream(torch.cuda.current_stream(self.bb.device))
+            self.stage[slot] = st
+        return self.stage[slot]
+
     def _fps(self, k, xs, ready):
         """SA1 FPS + level-0 ball queries of group k (the batches in xs, readable after the
         events in `ready`) on a side stream."""
@@ -1049,17 +1061,27 @@ class StreamingSSG:
         t = self.bb.timers
         host = any(isinstance(xj, _HostBatch) for xj in xs)
         self.staged[slot] = self.G > 1 or host
-        if self.staged[slot] and self.stage[slot] is None:  # (G = 1 fed from the host)
-            self.stage[slot] = torch.empty((self.G * self.B, self.N, 3), dtype=torch.float32, device=self.bb.device)
+        if self.staged[slot]:
+            self._stage(slot, fs)
         with torch.cuda.stream(fs):
             if self.staged[slot]:
                 x = self.stage[slot][:g]
-                for j, xj in enumerate(xs):
-                    if isinstance(xj, _HostBatch):  # pinned host -> device, then the buffer may be refilled
-                        x[j * self.B:(j + 1) * self.B].copy_(xj.pinned, non_blocking=True)
-                        xj.copied.record(fs)
+                B, j = self.B, 0
+                grp = None
+                while j < len(xs):
+                    if isinstance(xs[j], _HostBatch):
+                        # a run of host batches (consecutive rows of one pinned group buffer): one DMA copy
+                        e = j
+                        while e + 1 < len(xs) and isinstance(xs[e + 1], _HostBatch):
+                            e += 1
+                        grp = xs[j].grp
+                        x[j * B:(e + 1) * B].copy_(grp.pinned[j * B:(e + 1) * B], non_blocking=True)
+                        j = e + 1
                     else:
-                        x[j * self.B:(j + 1) * self.B].copy_(xj, non_blocking=True)
+                        x[j * B:(j + 1) * B].copy_(xs[j], non_blocking=True)
+                        j += 1
+                if grp is not None:  # the group buffer may be refilled once its copies have completed
+                    grp.copied.record(fs)
             else:
                 x = xs[0]
             for xj in xs:  # read on this stream: keep the caller's buffers alive until then
@@ -1139,14 +1161,21 @@ class StreamingSSG:
 _HOST_READY = object()  # push_host's "ready" marker: the batch sits in pinned host memory already
 
 
-class _HostBatch:
-    """One batch of host frames in a pinned buffer; `copied` is recorded on the side stream after its
+class _HostGroup:
+    """A group's pinned host buffer (G batches of rows); `copied` is recorded on the side stream after its
     host-to-device copy (the buffer may be refilled once it has completed)."""
 
     def __init__(self, pinned):
         self.pinned = pinned
         self.copied = torch.cuda.Event()
         self.copied.record()  # (a fresh buffer is free)
+
+
+class _HostBatch:
+    """One batch of host frames: rows j*B .. (j+1)*B of a pinned group buffer."""
+
+    def __init__(self, grp, j):
+        self.grp, self.j = grp, j
 
 
 class _Feed:
@@ -1161,16 +1190,21 @@ class _Feed:
         self.main = torch.cuda.current_stream(pipe.bb.device)
         self.buf, self.pending, self.k = [], [], 0
         self.readies = []  # push()'s ready event per buffered batch
-        self._ring, self._ri, self._pool = [], 0, None  # push_host's pinned buffers and copy threads
+        # push_host's ring of pinned group buffers, the current group's, and the fill threads
+        self._ring, self._ri, self._grp, self._pool = [], 0, None, None
 
     def push_host(self, frames, threads=4):
         """frames: one batch of host frames, a (B, N, 3) array or B arrays of shape (N, 3), of any real
-        dtype (converted to float32 as numpy's astype does).  They are copied into a pinned buffer by
-        `threads` host threads (frames split between them; numpy releases the GIL in the copy), and the
-        group's side stream copies the buffer to the device ahead of its FPS.  The pinned ring holds
-        (depth + 2) G batches; a buffer is refilled only after its device copy has completed (a host wait
-        on that event, the feed's back-pressure).  Returns push()'s outputs; every output equals
-        forward() of the same frames on the device."""
+        dtype (converted to float32 as numpy's astype does).  They are copied into the group's pinned
+        buffer (G batches of rows) by `threads` host threads (frames split between them; numpy releases
+        the GIL in the copy), and the group's side stream copies the buffer to the device ahead of its FPS
+        in one DMA copy (a copy per batch, queued behind the side stream's kernels, held the calling
+        thread for milliseconds now and then).  The pinned ring holds depth + 2 groups; a buffer is
+        refilled only after its device copy has completed (a host wait on that event, the feed's
+        back-pressure).  The batch that opens a group issues the oldest
+        in-flight group's main-stream pass (push() issues it when the new group completes), so the main
+        stream works while the host fills.  Returns the outputs of the batches that call completed, in
+        input order; every output equals forward() of the same frames on the device."""
         import numpy as _np
         p = self.p
         B, N = p.B, p.N
@@ -1182,16 +1216,24 @@ class _Feed:
             parts = [_np.asarray(f) for f in frames]
             if len(parts) != B or any(f.shape != (N, 3) for f in parts):
                 raise ValueError(f"push_host: {B} frames of shape ({N}, 3) expected")
+        out = []
+        if not self.buf and len(self.pending) >= p.depth:
+            # the batch opens a group whose completion would issue the oldest group's main-stream pass:
+            # issue it now, so the main stream runs it while the host fills this group's batches
+            slot, pxs = self.pending.pop(0)
+            out = p._rest(slot, pxs, self.main)
         if not self._ring:
             import concurrent.futures
-            self._ring = [_HostBatch(torch.empty((B, N, 3), dtype=torch.float32, pin_memory=True))
-                          for _ in range((p.depth + 2) * p.G)]
+            self._ring = [_HostGroup(torch.empty((p.G * B, N, 3), dtype=torch.float32, pin_memory=True))
+                          for _ in range(p.depth + 2)]
             self._nthreads = max(1, int(threads))
             self._pool = concurrent.futures.ThreadPoolExecutor(max_workers=self._nthreads)
-        hb = self._ring[self._ri]
-        self._ri = (self._ri + 1) % len(self._ring)
-        hb.copied.synchronize()  # its previous batch has reached the device
-        dst = hb.pinned.numpy()
+        if self._grp is None:  # the group's first host batch takes the next pinned group buffer
+            self._grp = self._ring[self._ri]
+            self._ri = (self._ri + 1) % len(self._ring)
+            self._grp.copied.synchronize()  # its previous group has reached the device
+        hb = _HostBatch(self._grp, len(self.buf))
+        dst = self._grp.pinned[hb.j * B:(hb.j + 1) * B].numpy()
         step = -(-B // self._nthreads)
 
         def fill(lo):
@@ -1203,12 +1245,13 @@ class _Feed:
         self.buf.append(hb)
         self.readies.append(_HOST_READY)  # filled by the host: no device event to wait for
         if len(self.buf) < p.G:
-            return []
+            return out
         xs, evs = self.buf, self.readies
         self.buf, self.readies = [], []
-        return self._issue(xs, evs)
+        return out + self._issue(xs, evs)
 
     def _issue(self, xs, readies=None):
+        self._grp = None  # the next group's host batches take a fresh pinned group buffer
         evs = [e for e in (readies or [None]) if e is not None and e is not _HOST_READY]
         if readies is None or any(e is None for e in readies):
             ev = torch.cuda.Event()
@@ -1234,11 +1277,13 @@ class _Feed:
         return self._issue(xs, evs)
 
     def close(self):
-        """Stop push_host's copy threads (the pinned ring is freed with the feed)."""
+        """Stop push_host's copy threads and free the pinned ring (once its copies have completed)."""
         if self._pool is not None:
             self._pool.shutdown(wait=False)
             self._pool = None
-            self._ring = []
+            for grp in self._ring:
+                grp.copied.synchronize()
+            self._ring, self._grp = [], None
 
     def __del__(self):
         try:

@@ -46,7 +46,7 @@ def run(host):
 
 for host in (False, True, False, True):
     w, ins = run(host)
-    print(f"{'host  ' if host else 'device'}: {w:.3f} ms per batch wall, {ins:.3f} ms inside push per call "
+    print(f"{'host' if host else 'device':6s}: {w:.3f} ms per batch wall, {ins:.3f} ms inside push per call "
           f"({B * N / w / 1e3:.0f} M points/s)", flush=True)
 pin = torch.empty((B, N, 3), dtype=torch.float32, pin_memory=True).numpy()
 pool = concurrent.futures.ThreadPoolExecutor(max_workers=threads)

@@ -1036,7 +1036,7 @@ class StreamingSSG:
         for e in self.slot_free:
             e.record(torch.cuda.current_stream(dev))
 
-    def _stage(self, slot, fs):
+    def _stage(self, slot, fs, main):
         """The slot's staging buffer (allocated on first use when G = 1) — from the pool of the side stream
         that writes it: a block the caching allocator took from the main stream's pool could be one a
         main-stream pass still queued on the device has just freed, and the side stream does not wait
@@ -1044,13 +1044,13 @@ class StreamingSSG:
         if self.stage[slot] is None:
             with torch.cuda.stream(fs):
                 st = torch.empty((self.G * self.B, self.N, 3), dtype=torch.float32, device=self.bb.device)
-            st.record_stream(torch.cuda.current_stream(self.bb.device))
+            st.record_stream(main)
             self.stage[slot] = st
         return self.stage[slot]
 
-    def _fps(self, k, xs, ready):
+    def _fps(self, k, xs, ready, main=None):
         """SA1 FPS + level-0 ball queries of group k (the batches in xs, readable after the
-        events in `ready`) on a side stream."""
+        events in `ready`) on a side stream; `main` the stream the group's MFMA levels will run on."""
         slot = k % self.nslot
         fs = self.fps_streams[k % self.depth]
         hs = 1 + k % self.depth  # the side stream's own library handle
@@ -1062,7 +1062,7 @@ class StreamingSSG:
         host = any(isinstance(xj, _HostBatch) for xj in xs)
         self.staged[slot] = self.G > 1 or host
         if self.staged[slot]:
-            self._stage(slot, fs)
+            self._stage(slot, fs, main if main is not None else torch.cuda.current_stream(self.bb.device))
         with torch.cuda.stream(fs):
             if self.staged[slot]:
                 x = self.stage[slot][:g]
@@ -1257,7 +1257,7 @@ class _Feed:
             ev = torch.cuda.Event()
             ev.record(self.main)  # the inputs exist on the caller's stream
             evs.append(ev)
-        self.pending.append((self.p._fps(self.k, xs, evs), xs))
+        self.pending.append((self.p._fps(self.k, xs, evs, self.main), xs))
         self.k += 1
         if len(self.pending) > self.p.depth:
             slot, pxs = self.pending.pop(0)

@@ -96,37 +96,6 @@ for rep in range(3):
     torch.cuda.synchronize()
     print("after a wait on another busy stream's event, host ms per copy_ call:", calls,
           f"(drain {(time.perf_counter() - t) * 1e3:.1f} ms)", flush=True)
-# lidar_copy_from_host (the pull kernel): bit-equality, device time, and the host time of the call on a busy stream
-import os, sys  # noqa: E401,E402
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
-from lidar_ai_recommendation_software_amd import _native as nat  # noqa: E402
-h = nat.handle(0)
-pin.copy_(torch.randn(nbytes // 4))
-for blocks in (64, 128, 256, 512):
-    for rep in range(2):
-        dst.zero_()
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        nat.call("lidar_copy_from_host", h, pin.data_ptr(), nbytes, dst.data_ptr(), blocks, nat.stream_ptr())
-        e1.record()
-        torch.cuda.synchronize()
-        ok = torch.equal(dst.cpu(), pin)
-        print(f"pull kernel, {blocks} workgroups: {e0.elapsed_time(e1):.3f} ms ({nbytes / e0.elapsed_time(e1) / 1e6:.1f} GB/s), "
-              f"equal {ok}", flush=True)
-with torch.cuda.stream(s):
-    busy(10)
-    t = time.perf_counter()
-    nat.call("lidar_copy_from_host", h, pin.data_ptr(), nbytes, dst.data_ptr(), 0, nat.stream_ptr(s))
-    print(f"pull kernel call on a busy stream: {(time.perf_counter() - t) * 1e3:.3f} ms on the host", flush=True)
-torch.cuda.synchronize()
-try:
-    import numpy as np  # noqa: E402
-    pageable = np.zeros(1024, dtype=np.float32)
-    nat.call("lidar_copy_from_host", h, pageable.ctypes.data, 4096, dst.data_ptr(), 0, nat.stream_ptr())
-    print("pageable source: accepted (unexpected)")
-except nat.LidarError as e:
-    print("pageable source: refused:", e)
 # many kernels and events queued on the stream (and on others) ahead of the copy: does the call then block?
 small = torch.empty(1024, device=dev)
 for nk, nev in ((50, 0), (200, 0), (20, 20), (50, 50), (200, 200)):

@@ -665,6 +665,16 @@ def test_streaming_host_feed_matches_forward(cuda, G, depth, dtype, mixed):
         assert torch.equal(a, b), i
     with pytest.raises(ValueError, match="push_host"):
         feed.push_host(hx[0][:1])
+    # the feed goes on after a flush (a partial group, then whole ones), and close() releases the ring
+    again = []
+    for h in hx[:2 * G + 1]:
+        again += feed.push_host(h)
+    again += feed.flush()
+    assert len(again) == 2 * G + 1
+    for i, (a, b) in enumerate(zip(again, want)):
+        assert torch.equal(a, b), i
+    feed.close()
+    assert feed._ring == [] and feed._pool is None
 
 
 def test_fused_layer1_x1_matches_per_branch(cuda):

@@ -195,6 +195,9 @@ def compact_line(rec, detail_path=None):
     if rec.get("ssg_host_feed"):  # the H2D-inclusive rate, reported beside the device-resident value
         line["ssg_host_feed"] = {"value": rec["ssg_host_feed"]["value"], "unit": "M points/s",
                                  "input": "host NumPy frames, PCIe included"}
+        lw = rec["ssg_host_feed"].get("long_window")
+        if lw:
+            line["ssg_host_feed"][f"value_{lw['batches']}_batches"] = round(lw["value"], 1)
     if rec.get("arithmetic_short"):
         line["arithmetic"] = rec["arithmetic_short"]
     bq = (rec.get("roofline_all") or {}).get("sa2_ball_query")
@@ -842,6 +845,14 @@ def main():
                      "input": f"host NumPy (B, N, 3) float32 batches -> feed().push_host ({args.host_threads} host threads "
                               "into a pinned ring, H2D on the side streams ahead of each group's FPS)",
                      "parity": "every output bit-equal to forward() of the same batch"}
+        if args.steps < 80:
+            # the same feed over a longer window as well: the host feed pays more of its start than the device
+            # one does within a short window
+            n_long = G * -(-80 // G)
+            el_l, _, _, _, _ = measure("ssg_host_long", pn.SSG, "f32", B, N, n_long, args.warmup, args.depth, G,
+                                       x3=bool(args.x3), events=False, host=True, bb=bb, xs=xs, refs=refs)
+            host_feed["long_window"] = {"batches": n_long, "value": sharding.aggregate_rate(B * N * n_long, world,
+                                                                                            el_l) / 1e6}
     fp32_mfma = None
     if args.x3 and not args.no_fp32_mfma_leg:
         # the same workload on the native fp32-MFMA kernels (clean window), for comparison

@@ -37,7 +37,8 @@ def _with_ranks(rec, world):
                        "unit": "TFLOP/s", "frac": 0.2172, "traffic": None, "stack_mfma_frac": 0.19,
                        "work_per_launch": 3.75e12, "avg_launch_ms": 6.9, "launches": 6, "frames": 576}
     msg["chains_ms_per_group"] = {"main": 19.87654, "side": 10.34567, "step_ms_per_group": 22.123456}
-    rec["ssg_host_feed"] = {"value": 1049.123456, "unit": "M points/s", "ms_per_step": 2.0012345}
+    rec["ssg_host_feed"] = {"value": 1049.123456, "unit": "M points/s", "ms_per_step": 2.0012345,
+                            "long_window": {"batches": 80, "value": 1172.3456}}
     rec["precision"] = {"contract": "max |got-want|/|want| over |want| >= 1e-2 RMS, and max err/(1e-4|want| + "
                                     "1e-4 RMS)", "frames": [0, 31, 64, 127], "fps_exact": True,
                         "per_frame": {str(f): {"level1": 3.1e-05, "level2": 2.9e-05, "global": 3.1e-05}
@@ -61,6 +62,7 @@ def test_compact_line_fits_and_keeps_the_contract(world):
         assert k in r
     assert r["frac"] == pytest.approx(r["achieved"] / r["peak"], rel=2e-3)
     assert d["ssg_host_feed"]["value"] == pytest.approx(1049.123456, rel=1e-3)  # SURVEY §8(d), always kept
+    assert d["ssg_host_feed"]["value_80_batches"] == pytest.approx(1172.3, rel=1e-3)
     assert r["achieved"] == pytest.approx(r["work_per_launch"] / (r["avg_launch_ms"] * 1e-3) / 1e12, rel=2e-3)
     assert d["cpu_baseline"]["value"] > 0 and d["cpu_baseline"]["cores"] >= 1 and d["cpu_baseline"]["kind"] == "port"
     assert d["distributed"]["world_size"] == world == len(d["distributed"]["ranks"])

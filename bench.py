@@ -722,6 +722,9 @@ def main():
                     help="frames per GPU per step of the configs[4] MSG leg (32: the per-GPU share of 256 frames)")
     ap.add_argument("--msg-steps", type=int, default=30)
     ap.add_argument("--msg-group", type=int, default=3, help="configs[4] leg: batches per SA1-FPS launch")
+    ap.add_argument("--cfg1-group", type=int, default=8,
+                    help="configs[1] leg: batches per SA1-FPS launch (16 384-point frames: 8 measured 2 678-2 751 "
+                         "vs 2 262-2 297 M points/s at 4, tools/micro/cfg1_ab.py)")
     ap.add_argument("--msg-depth", type=int, default=3, help="configs[4] leg: side streams")
     ap.add_argument("--no-layer1-fuse", action="store_true",
                     help="configs[4] leg: one per-point layer-1 GEMM per branch (pointnet2.FUSE_LAYER1 off)")
@@ -897,7 +900,7 @@ def main():
                 ("configs[4]_msg_131k_bf16", pn.MSG, "bf16", args.msg_batch, 131072, args.msg_steps)]
         for key, cfg, dtype, b2, n2, st2 in legs:
             msg = cfg is pn.MSG
-            g2 = pick_group(st2, args.msg_group if msg else 3)
+            g2 = pick_group(st2, args.msg_group if msg else args.cfg1_group)
             d2 = args.msg_depth if msg else 3
             el2, t2, _, _, _ = measure(key, cfg, dtype, b2, n2, st2, 1, d2, g2, events=False,
                                        fps_threads=(args.msg_fps_threads or None) if msg else None)

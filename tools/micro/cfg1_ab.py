@@ -1,0 +1,48 @@
+"""configs[1] (SA1 only, 32 x 16 384-point frames) through StreamingSSG's feed: M points/s per pipeline setting
+(FPS workgroup size, side streams, batches per group), each over a steady-state window of `steps` batches.
+usage: python tools/micro/cfg1_ab.py [steps]"""
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+from lidar_ai_recommendation_software_amd import pointnet2 as pn  # noqa: E402
+from lidar_ai_recommendation_software_amd.synthetic import unit_frames  # noqa: E402
+
+steps = int(sys.argv[1]) if len(sys.argv) > 1 else 80
+B, N = 32, 16384
+dev = torch.device("cuda:0")
+bb = pn.PointNet2Backbone(pn.SA1_ONLY, device=dev, seed=0)
+xs = [torch.from_numpy(unit_frames(B, N, seed=500 + i)).to(dev) for i in range(8)]
+refs = [bb.forward(x)[0] for x in xs]
+ready = torch.cuda.Event()
+ready.record()
+
+
+def run(threads, depth, G):
+    pipe = pn.StreamingSSG(bb, B, N, depth=depth, fps_group=G, fps_threads=threads, ramp=False, bq="bin",
+                           l2_side=True)
+    feed = pipe.feed()
+    outs = []
+    w = (depth + 3) * G
+    for i in range(w):
+        outs += feed.push(xs[i % 8], ready)
+    torch.cuda.synchronize()
+    n = G * (steps // G)
+    t0 = time.perf_counter()
+    for i in range(w, w + n):
+        outs += feed.push(xs[i % 8], ready)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    outs += feed.flush()
+    bad = [i for i, o in enumerate(outs) if not torch.equal(o, refs[i % 8])]
+    assert not bad, bad[:4]
+    return B * N * n / el / 1e6
+
+
+for rep in range(2):
+    for threads, depth, G in ((512, 3, 4), (512, 3, 8), (512, 3, 10), (512, 3, 16), (512, 3, 20), (512, 2, 8),
+                              (512, 2, 16), (512, 4, 8), (1024, 3, 8), (1024, 3, 16)):
+        print(f"threads {threads:4d} depth {depth} G {G}: {run(threads, depth, G):7.1f} M points/s", flush=True)

@@ -1,6 +1,7 @@
 """configs[1] (SA1 only, 32 x 16 384-point frames) through StreamingSSG's feed: M points/s per pipeline setting
-(FPS workgroup size, side streams, batches per group), each over a steady-state window of `steps` batches.
-usage: python tools/micro/cfg1_ab.py [steps]"""
+(FPS workgroup size, side streams, batches per group), each over a steady-state window of `steps` batches;
+with `ssg`, the headline's SSG stack on 32 x 65 536-point frames instead.
+usage: python tools/micro/cfg1_ab.py [steps] [ssg]"""
 import os
 import sys
 import time
@@ -12,9 +13,10 @@ from lidar_ai_recommendation_software_amd import pointnet2 as pn  # noqa: E402
 from lidar_ai_recommendation_software_amd.synthetic import unit_frames  # noqa: E402
 
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 80
-B, N = 32, 16384
+ssg = len(sys.argv) > 2 and sys.argv[2] == "ssg"
+B, N = (32, 65536) if ssg else (32, 16384)
 dev = torch.device("cuda:0")
-bb = pn.PointNet2Backbone(pn.SA1_ONLY, device=dev, seed=0)
+bb = pn.PointNet2Backbone(pn.SSG if ssg else pn.SA1_ONLY, device=dev, seed=0)
 xs = [torch.from_numpy(unit_frames(B, N, seed=500 + i)).to(dev) for i in range(8)]
 refs = [bb.forward(x)[0] for x in xs]
 ready = torch.cuda.Event()
@@ -42,7 +44,9 @@ def run(threads, depth, G):
     return B * N * n / el / 1e6
 
 
+SETS = (((512, 3, 4), (512, 3, 5), (512, 3, 10), (512, 2, 5), (512, 2, 10), (1024, 3, 5)) if ssg else
+        ((512, 3, 4), (512, 3, 8), (512, 3, 10), (512, 3, 16), (512, 3, 20), (512, 2, 8), (512, 2, 16), (512, 4, 8),
+         (1024, 3, 8), (1024, 3, 16)))
 for rep in range(2):
-    for threads, depth, G in ((512, 3, 4), (512, 3, 8), (512, 3, 10), (512, 3, 16), (512, 3, 20), (512, 2, 8),
-                              (512, 2, 16), (512, 4, 8), (1024, 3, 8), (1024, 3, 16)):
+    for threads, depth, G in SETS:
         print(f"threads {threads:4d} depth {depth} G {G}: {run(threads, depth, G):7.1f} M points/s", flush=True)

@@ -423,7 +423,7 @@ def eps_pairs(x):
 
 
 def tier_r_leg(dev, rank, world, frames=32, n=65536, steps=3, cpu=True, cpu_budget=12.0, wide=256,
-               lanes=int(os.environ.get("LIDAR_DENSITY_LANES", "4"))):
+               lanes=int(os.environ.get("LIDAR_DENSITY_LANES", "3"))):
     """The reference's own path (Tier R: preprocess -> DBSCAN -> people -> density grid) on
     device-resident uniform +-15 m frames: batches of `frames` frames through
     density_stream.DensityStream.run_batch (one launch per phase over the CSR batch), with
@@ -514,8 +514,9 @@ def tier_r_leg(dev, rank, world, frames=32, n=65536, steps=3, cpu=True, cpu_budg
         rec["wide_batch"] = {"frames_per_launch": wide,
                              "value": sharding.aggregate_rate(wide * n * steps, world, elw) / 1e6,
                              "unit": "M points/s", "ms_per_launch": elw / steps * 1e3}
-        # the same frames as `wide // frames` batches of `frames`, `lanes` batches in flight (lanes 2 / 3 / 4 / 6:
-        # 451 / 510 / 584 / 430 M pts/s on 8 batches of 32 x 65 536 points)
+        # the same frames as `wide // frames` batches of `frames`, `lanes` batches in flight (round 6, lanes 3 / 4:
+        # 663-704 / 602-650 M pts/s on 8 batches of 32 x 65 536 points, profiles/r06/density_lanes_ab.txt: a process
+        # has 4 hardware queues, and a fourth lane's stream shares one)
         # (DensityStream.run_batches: a host thread + HIP stream + handle per lane)
         bl = [xw[i:i + frames] for i in range(0, wide, frames)]
         ref_b = ds.run_batches(bl, lanes=lanes)

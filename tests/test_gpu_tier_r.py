@@ -538,6 +538,12 @@ def test_density_run_batches_pipelined(cuda):
     bad = batches[:2] + [[T(names[0]), torch.zeros((0, 3), dtype=torch.float64, device=cuda)]]
     with pytest.raises(ValueError):
         ds.run_batches(bad, lanes=2)
+    # the default (three lanes) and more lanes than hardware queues give the same results
+    for ln in (None, 5):
+        got = ds.run_batches(batches) if ln is None else ds.run_batches(batches, lanes=ln)
+        for wb, gb in zip(want, got):
+            for name, a, b in zip(names * 2, wb, gb):
+                _same_analyze(name, a, b)
     ds.close()
 
 

@@ -555,7 +555,7 @@ def tier_r_leg(dev, rank, world, frames=32, n=65536, steps=3, cpu=True, cpu_budg
     return rec
 
 
-def host_frame_leg(rank, world, frames=16, n=65536, cpu=True):
+def host_frame_leg(rank, world, frames=16, n=65536, cpu=True, feed_frames=64, feed_batch=32):
     """host frames through the drop-in API — preprocess_lidar_data(numpy) ->
     CrowdDensityModel().analyze -> dict, PCIe included, one frame per call (what app.py does);
     and the same frames through frame_feed.HostFrameFeed (pinned staging, H2D on a copy stream
@@ -565,25 +565,28 @@ def host_frame_leg(rank, world, frames=16, n=65536, cpu=True):
     from lidar_ai_recommendation_software_amd.crowd_density_model import CrowdDensityModel
     from lidar_ai_recommendation_software_amd.frame_feed import HostFrameFeed
     from lidar_ai_recommendation_software_amd.synthetic import uniform_frame
-    xs = [uniform_frame(n, 7000 + 131 * rank + i) for i in range(frames)]
+    xs = [uniform_frame(n, 7000 + 131 * rank + i) for i in range(max(frames, feed_frames))]
     model = CrowdDensityModel()
     model.analyze(dp.preprocess_lidar_data(xs[0]))  # warm-up
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    want = [model.analyze(dp.preprocess_lidar_data(x)) for x in xs]
+    want = [model.analyze(dp.preprocess_lidar_data(x)) for x in xs[:frames]]
     dt = time.perf_counter() - t0
-    feed = HostFrameFeed(batch=8)
-    feed.run(xs[:8])  # warm-up: pinned buffers and workspaces sized
+    # the feed in 32-frame batches over 64 frames (batch 8 / 16 / 32: 133-135 / 235-236 / 290-329 M points/s,
+    # tools/micro/frame_feed_ab.py, profiles/r06/frame_feed_ab.txt)
+    feed = HostFrameFeed(batch=feed_batch)
+    feed.run(xs[:feed_batch])  # warm-up: pinned buffers and workspaces sized
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
-    got = feed.run(xs)
+    got = feed.run(xs[:feed_frames])
     dt2 = time.perf_counter() - t0
     assert all(a["total_people"] == b["total_people"] and np.array_equal(a["density_map"], b["density_map"])
                for a, b in zip(want, got)), "HostFrameFeed differs from the drop-in API"
     return {"metric": "M points/s, host numpy frames -> preprocess_lidar_data -> CrowdDensityModel.analyze "
                       "dicts (PCIe-inclusive)",
             "drop_in_per_frame": {"value": frames * n / dt / 1e6, "unit": "M points/s", "ms_per_frame": dt / frames * 1e3},
-            "host_frame_feed": {"value": frames * n / dt2 / 1e6, "unit": "M points/s",
-                                "ms_per_frame": dt2 / frames * 1e3, "batch": 8},
+            "host_frame_feed": {"value": feed_frames * n / dt2 / 1e6, "unit": "M points/s",
+                                "ms_per_frame": dt2 / feed_frames * 1e3, "batch": feed_batch, "frames": feed_frames},
             "frames": frames, "points_per_frame": n, "parity": "HostFrameFeed == the drop-in API, frame for frame"}
 
 

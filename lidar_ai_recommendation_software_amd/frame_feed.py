@@ -21,7 +21,9 @@ from .streams import side_streams
 
 
 class HostFrameFeed:
-    def __init__(self, device=None, batch=8, grid_size=1.0):
+    def __init__(self, device=None, batch=32, grid_size=1.0):
+        """batch: frames per density launch (32: the latency-bound per-frame phases then run 32 workgroups
+        at once; 8 / 16 / 32 measured 133-135 / 235-236 / 290-329 M points/s on 65 536-point frames)."""
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.batch = max(1, int(batch))
         self.ds = DensityStream(self.device, workers=1, grid_size=grid_size)

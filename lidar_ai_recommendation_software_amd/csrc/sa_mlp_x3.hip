@@ -137,9 +137,13 @@ __device__ __forceinline__ float max_row_groups(float v)
 #ifndef LIDAR_SA_E3_BOUND
 #define LIDAR_SA_E3_BOUND 1
 #endif
+// LIDAR_SA1_W: waves per SIMD the fused SA1 kernel (NS = 32, fp32 contract) is built for (A/B builds only)
+#ifndef LIDAR_SA1_W
+#define LIDAR_SA1_W 5
+#endif
 constexpr int kBqCap = LIDAR_BQ_CAP;  // candidates per window a fused wave ranks in LDS (more: index-order scan)
 template <int C1, int C2, int C3, int NS, int L1, int R, bool X1, bool BQ = false>
-__global__ __launch_bounds__(256, (BQ && !X1 && NS == 32) ? 5 : (R == 1 ? 3 : 2)) void sa_x3_kernel(const float *__restrict__ P, int64_t stride,
+__global__ __launch_bounds__(256, (BQ && !X1 && NS == 32) ? LIDAR_SA1_W : (R == 1 ? 3 : 2)) void sa_x3_kernel(const float *__restrict__ P, int64_t stride,
                                                      const float *__restrict__ Q, const int32_t *__restrict__ idx,
                                                      int n, int m, int64_t total, const uint4 *__restrict__ packed,
                                                      float *__restrict__ out, int64_t out_stride, int64_t out_offset,

@@ -934,7 +934,7 @@ def main():
                     "frames": f, "peak_basis": "bf16 MFMA dense peak" if dtype == "bf16" else "bf16 dense peak / 3 (h3)",
                     "stack_mfma_frac": sum(mw[k] * v[1] for k, v in mk.items()) / (sum(v[2] for v in mk.values()) / 1e3)
                                        / 1e12 / peak}
-                got = latest_profile("pmc_traffic_msg.json") if msg else None
+                got = latest_profile("pmc_traffic_msg.json" if msg else "pmc_traffic_cfg1.json")
                 if got and got[0]["config"].get("points_per_frame") == n2 and dk in got[0]["kernels"]:
                     tpf = got[0]["kernels"][dk]["traffic_per_frame"]  # memory-side bytes per frame (PMC)
                     r4 = extras[key]["roofline"]

@@ -9,8 +9,9 @@
 #     the SSG bench at the driver's shape (FETCH_SIZE; WRITE_SIZE; the SQ / GRBM VALU group)
 #   5 the voxel leg's kernels (tools/voxel_micro.py: 20 batched launches at the bench's shape): kernel
 #     trace, FETCH_SIZE and WRITE_SIZE passes (tools/pmc_voxel.py reduces them)
-#   6 (round 6) configs[4]'s MSG pipeline: kernel trace + FETCH_SIZE / WRITE_SIZE passes (tools/pmc_msg.py), and
-#     the SA1 FPS step phases inside the SSG pipeline (tools/micro/fps_pipe_phases.py, diagnostic library)
+#   6 (round 6) configs[4]'s MSG pipeline: kernel trace + FETCH_SIZE / WRITE_SIZE passes (tools/pmc_msg.py), the same
+#     passes over configs[1]'s pipeline (tools/pmc_msg.py --cfg1), and the SA1 FPS step phases inside the SSG
+#     pipeline (tools/micro/fps_pipe_phases.py, diagnostic library)
 # reduce afterwards (CPU): tools/pmc_traffic.py and tools/pmc_valu.py with the passes' bench lines
 # usage (on the box): bash tools/profile_round.sh TAG [tests|notests]
 set -o pipefail
@@ -57,6 +58,11 @@ timeout -s KILL 200 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format cs
     python3 $R/tools/msg_pipe.py 30 0 3,3,0 > $O/mpmc_fetch.log 2>&1 || exit 24
 timeout -s KILL 200 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $O/mpmc_write -o m -- \
     python3 $R/tools/msg_pipe.py 30 0 3,3,0 > $O/mpmc_write.log 2>&1 || exit 25
+# configs[1] (round 6): FETCH_SIZE / WRITE_SIZE passes over its pipeline at the bench's leg settings (tools/pmc_msg.py --cfg1)
+timeout -s KILL 200 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $O/cpmc_fetch -o c -- \
+    python3 $R/tools/msg_pipe.py --cfg1 40 > $O/cpmc_fetch.log 2>&1 || exit 27
+timeout -s KILL 200 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $O/cpmc_write -o c -- \
+    python3 $R/tools/msg_pipe.py --cfg1 40 > $O/cpmc_write.log 2>&1 || exit 28
 # the SA1 FPS step phases in the pipeline and alone (the diagnostic library)
 cd $R
 LIDAR_AMD_LIB=$R/lidar_ai_recommendation_software_amd/liblidar_amd_diag.so timeout -k 10 300 \

@@ -555,7 +555,7 @@ def tier_r_leg(dev, rank, world, frames=32, n=65536, steps=3, cpu=True, cpu_budg
     return rec
 
 
-def host_frame_leg(rank, world, frames=16, n=65536, cpu=True, feed_frames=64, feed_batch=32):
+def host_frame_leg(rank, world, frames=16, n=65536, cpu=True, feed_frames=192, feed_batch=32):
     """host frames through the drop-in API — preprocess_lidar_data(numpy) ->
     CrowdDensityModel().analyze -> dict, PCIe included, one frame per call (what app.py does);
     and the same frames through frame_feed.HostFrameFeed (pinned staging, H2D on a copy stream
@@ -572,10 +572,10 @@ def host_frame_leg(rank, world, frames=16, n=65536, cpu=True, feed_frames=64, fe
     t0 = time.perf_counter()
     want = [model.analyze(dp.preprocess_lidar_data(x)) for x in xs[:frames]]
     dt = time.perf_counter() - t0
-    # the feed in 32-frame batches over 64 frames (batch 8 / 16 / 32: 133-135 / 235-236 / 290-329 M points/s,
-    # tools/micro/frame_feed_ab.py, profiles/r06/frame_feed_ab.txt)
+    # the feed in 32-frame batches, three in flight, over 192 frames (two windows; tools/micro/frame_feed_ab.py,
+    # profiles/r06/frame_feed_ab.txt)
     feed = HostFrameFeed(batch=feed_batch)
-    feed.run(xs[:feed_batch])  # warm-up: pinned buffers and workspaces sized
+    feed.run(xs[:feed_batch * feed.lanes])  # warm-up: every lane's pinned buffers, handle and workspaces sized
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     got = feed.run(xs[:feed_frames])

@@ -4,10 +4,10 @@
 The drop-in API takes one host NumPy frame per call, uploads it, runs the kernels and reads the
 result back: each frame pays its parse, its copy and its kernels one after the other
 (``app.py:78-84`` -> ``utils/data_processing.py:8-229``).  ``HostFrameFeed`` pipelines a stream of
-frames in batches: a staging thread parses (``load_lidar_data``'s multithreaded C parser for
-PCD / PLY) or takes the frames, packs batch k+1 into a pinned host buffer and issues its H2D copy
-on a copy stream, while the GPU runs batch k through ``DensityStream.run_batch`` (one launch per
-phase over the CSR batch).  Results are the drop-in API's, frame for frame (same kernels); the
+frames in batches: staging threads parse (``load_lidar_data``'s multithreaded C parser for
+PCD / PLY) or take the frames, pack the next `lanes` batches into pinned host buffers and issue their
+H2D copies on a copy stream, while the GPU runs the current `lanes` batches through
+``DensityStream.run_batches`` (one launch per phase over each CSR batch, the batches in flight at once).  Results are the drop-in API's, frame for frame (same kernels); the
 reference's exceptions are raised for the first bad frame.
 """
 import concurrent.futures
@@ -21,16 +21,23 @@ from .streams import side_streams
 
 
 class HostFrameFeed:
-    def __init__(self, device=None, batch=32, grid_size=1.0):
+    def __init__(self, device=None, batch=32, grid_size=1.0, lanes=3):
         """batch: frames per density launch (32: the latency-bound per-frame phases then run 32 workgroups
-        at once; 8 / 16 / 32 measured 133-135 / 235-236 / 290-329 M points/s on 65 536-point frames)."""
+        at once; 8 / 16 / 32 measured 133-135 / 235-236 / 290-329 M points/s on 65 536-point frames).
+        lanes: batches run at once through DensityStream.run_batches (one host thread, HIP stream and
+        handle each; the next `lanes` batches are staged meanwhile, one staging thread per batch);
+        1: one batch at a time through run_batch."""
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.batch = max(1, int(batch))
+        self.lanes = max(1, int(lanes))
         self.ds = DensityStream(self.device, workers=1, grid_size=grid_size)
-        self.copy_stream = side_streams(self.device, 1)[0]
-        self._pinned = [None, None]  # host staging, double-buffered
-        self._dev = [None, None]
-        self._pool = concurrent.futures.ThreadPoolExecutor(max_workers=1)
+        # the copies on a stream of their own, past the lanes' (run_batches takes side streams 0 .. lanes - 1)
+        self.copy_stream = side_streams(self.device, 1, start=self.lanes)[0]
+        nslot = 2 * self.lanes  # host staging, double-buffered per lane
+        self._pinned = [None] * nslot
+        self._dev = [None] * nslot
+        self._pool = concurrent.futures.ThreadPoolExecutor(max_workers=self.lanes)  # one batch each
+        self._win = concurrent.futures.ThreadPoolExecutor(max_workers=1)  # stages a window of batches
 
     def _buffers(self, slot, rows):
         if self._pinned[slot] is None or self._pinned[slot].shape[0] < rows:
@@ -67,19 +74,43 @@ class HostFrameFeed:
             o += n
         return views, ev
 
+    def _stage_window(self, window, half, from_files):
+        """(window thread) the window's batches staged in parallel into half `half` of the slots; per batch
+        (views, event) or the exception its staging raised."""
+        futs = [self._pool.submit(self._stage, b, half * self.lanes + j, from_files) for j, b in enumerate(window)]
+        out = []
+        for f in futs:
+            try:
+                out.append(f.result())
+            except Exception as e:  # noqa: BLE001 — raised in batch order by _run
+                out.append(e)
+        return out
+
     def _run(self, items, from_files):
         batches = [items[i:i + self.batch] for i in range(0, len(items), self.batch)]
         out = []
         if not batches:
             return out
-        fut = self._pool.submit(self._stage, batches[0], 0, from_files)
-        for i in range(len(batches)):
-            views, ev = fut.result()
-            # batch i - 1 (slot (i + 1) % 2) is complete: run_batch ends with host read-backs
-            if i + 1 < len(batches):
-                fut = self._pool.submit(self._stage, batches[i + 1], (i + 1) % 2, from_files)
-            torch.cuda.current_stream(self.device).wait_event(ev)
-            out += self.ds.run_batch(views)
+        L = self.lanes
+        windows = [batches[i:i + L] for i in range(0, len(batches), L)]
+        fut = self._win.submit(self._stage_window, windows[0], 0, from_files)
+        for w in range(len(windows)):
+            staged = fut.result()
+            # window w - 1 (the other half of the slots) is complete: run_batch(es) end with host read-backs
+            if w + 1 < len(windows):
+                fut = self._win.submit(self._stage_window, windows[w + 1], (w + 1) % 2, from_files)
+            bad = next((j for j, st in enumerate(staged) if isinstance(st, Exception)), len(staged))
+            cur = torch.cuda.current_stream(self.device)
+            for views, ev in staged[:bad]:
+                cur.wait_event(ev)
+            ok = [views for views, _ in staged[:bad]]
+            if L == 1 or len(ok) == 1:
+                for views in ok:
+                    out += self.ds.run_batch(views)
+            elif ok:
+                out += [r for res in self.ds.run_batches(ok, lanes=L) for r in res]
+            if bad < len(staged):  # the batches before it ran (and raised first, if one of them fails)
+                raise staged[bad]
         return out
 
     def run(self, frames):

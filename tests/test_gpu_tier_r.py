@@ -1012,10 +1012,12 @@ def test_host_frame_feed_matches_drop_in(cuda, tmp_path):
     from lidar_ai_recommendation_software_amd.frame_feed import HostFrameFeed
     names = ["uniform_16384_s0", "small_12", "crowd_16384_s7", "int_4096", "lattice_8163_s4", "small_20", "dup_4096"]
     frames = [FRAMES[k]() for k in names]
+    for lanes in (1, 2, 3):  # one batch at a time (run_batch), and batches in flight (run_batches)
+        got = HostFrameFeed(batch=2 if lanes == 2 else 3, lanes=lanes).run(frames)
+        assert len(got) == len(frames)
+        for name, f, g in zip(names, frames, got):
+            _same_analyze(name, g, CrowdDensityModel().analyze(dp.preprocess_lidar_data(f)))
     feed = HostFrameFeed(batch=3)
-    got = feed.run(frames)
-    for name, f, g in zip(names, frames, got):
-        _same_analyze(name, g, CrowdDensityModel().analyze(dp.preprocess_lidar_data(f)))
     paths = []
     for i, f in enumerate(frames[:3]):
         p = tmp_path / f"f{i}.pcd"
@@ -1028,6 +1030,12 @@ def test_host_frame_feed_matches_drop_in(cuda, tmp_path):
             paths[names.index(name)]))))
     with pytest.raises(IndexError):
         feed.run([frames[0], ERROR_FRAMES["const_col"]()])
+    # the first bad frame's exception, in frame order, whichever stage finds it: a kernel-side IndexError in
+    # batch 0 beats a staging-side ValueError (an empty frame) in batch 1 of the same window
+    with pytest.raises(IndexError):
+        HostFrameFeed(batch=2, lanes=3).run([frames[0], ERROR_FRAMES["const_col"](), np.zeros((0, 3))])
+    with pytest.raises(ValueError):
+        HostFrameFeed(batch=2, lanes=3).run([frames[0], frames[1], np.zeros((0, 3))])
 
 
 @pytest.mark.parametrize("kind", STRESS_KINDS)
